@@ -1,0 +1,540 @@
+// livo_capi.cpp — the C ABI (include/livo.h): context, device map, resident
+// scans, and the host side of the batched IEKF loop.
+//
+// Host control is launch-only: every evaluation of the IEKF loop
+// (laser_mapping.cpp:178) is one k_hshare launch + one k_solve launch on the
+// context's stream, and the loop's branches (convergence, rematch, stop) are
+// taken on the device (IekfCtrl), so a scan update costs one host->device
+// upload of the states and one device->host read of the results, with no
+// round trip per iteration.  Evaluations past a scan's stop exit at the first
+// instruction.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "livo_internal.h"
+
+using namespace livo;
+
+namespace {
+
+struct ScanBuf {
+    bool used = false;
+    int64_t n = 0;
+    int32_t nblk = 0;
+    float* pts = nullptr;  // n x 4
+    float* nn_xyz = nullptr;
+    int32_t* nn_idx = nullptr;
+    float* nn_d = nullptr;
+    int32_t* nn_cnt = nullptr;
+    double* partial = nullptr;  // nblk x kRedCols
+    bool searched = false;      // a search has filled the neighbour cache
+};
+
+template <typename T>
+static int dev_alloc(T** p, size_t count) {
+    *p = nullptr;
+    if (count == 0) count = 1;
+    if (hipMalloc((void**)p, count * sizeof(T)) != hipSuccess) {
+        *p = nullptr;
+        return LIVO_E_OOM;
+    }
+    return LIVO_OK;
+}
+
+template <typename T>
+static void dev_free(T*& p) {
+    if (p) (void)hipFree((void*)p);
+    p = nullptr;
+}
+
+}  // namespace
+
+struct livo_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    livo_params params{};
+    // map
+    MapNode* nodes = nullptr;
+    int64_t map_points = 0;
+    int64_t map_slots = 0;
+    int32_t map_depth = 0;
+    bool has_map = false;
+    // scans
+    std::vector<ScanBuf> scans;
+    // batch resources
+    int32_t slot_cap = 0;
+    IekfSlot* d_slots = nullptr;
+    IekfSlot* h_slots = nullptr;  // pinned
+    HsJob* d_jobs = nullptr;
+    HsJob* h_jobs = nullptr;      // pinned
+    // scratch for livo_knn / debug outputs
+    void* scratch = nullptr;
+    size_t scratch_bytes = 0;
+    // profiling
+    int profiling = 0;
+    hipEvent_t ev[2 * LIVO_MAX_EVALS + 2] = {};
+    bool events_ready = false;
+    livo_timings last{};
+};
+
+#define HIP_TRY(x)                                  \
+    do {                                            \
+        if ((x) != hipSuccess) return LIVO_E_HIP;   \
+    } while (0)
+
+static int set_device(livo_ctx* c) {
+    return hipSetDevice(c->device) == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+
+static int ensure_scratch(livo_ctx* c, size_t bytes) {
+    if (bytes <= c->scratch_bytes) return LIVO_OK;
+    if (c->scratch) (void)hipFree(c->scratch);
+    c->scratch = nullptr;
+    c->scratch_bytes = 0;
+    if (hipMalloc(&c->scratch, bytes) != hipSuccess) return LIVO_E_OOM;
+    c->scratch_bytes = bytes;
+    return LIVO_OK;
+}
+
+static int ensure_slots(livo_ctx* c, int32_t n) {
+    if (n <= c->slot_cap) return LIVO_OK;
+    int32_t cap = std::max(n, 8);
+    dev_free(c->d_slots);
+    dev_free(c->d_jobs);
+    if (c->h_slots) (void)hipHostFree(c->h_slots);
+    if (c->h_jobs) (void)hipHostFree(c->h_jobs);
+    c->h_slots = nullptr;
+    c->h_jobs = nullptr;
+    c->slot_cap = 0;
+    if (dev_alloc(&c->d_slots, cap) || dev_alloc(&c->d_jobs, cap)) return LIVO_E_OOM;
+    if (hipHostMalloc((void**)&c->h_slots, sizeof(IekfSlot) * cap, 0) != hipSuccess) return LIVO_E_OOM;
+    if (hipHostMalloc((void**)&c->h_jobs, sizeof(HsJob) * cap, 0) != hipSuccess) return LIVO_E_OOM;
+    c->slot_cap = cap;
+    return LIVO_OK;
+}
+
+static bool params_valid(const livo_params* p) {
+    return p && p->laser_point_cov > 0.0 && p->max_iterations >= 0 && p->max_iterations + 1 <= LIVO_MAX_EVALS &&
+           p->flags == 0;
+}
+
+static HsParams make_hs_params(livo_ctx* c) {
+    HsParams hp{};
+    hp.nodes = c->nodes;
+    hp.jobs = c->d_jobs;
+    std::memcpy(hp.R_LI, c->params.R_LI, sizeof(hp.R_LI));
+    std::memcpy(hp.t_LI, c->params.t_LI, sizeof(hp.t_LI));
+    hp.inv_r = 1.0 / c->params.laser_point_cov;
+    hp.max_res = c->params.max_residual;
+    hp.plane_thr = c->params.plane_threshold;
+    hp.max_sqd = c->params.max_nn_sqdist;
+    hp.has_map = c->has_map && c->map_points > 0 ? 1 : 0;
+    hp.force = -1;
+    return hp;
+}
+
+static void fill_job(HsJob& j, ScanBuf& s, IekfSlot* slot) {
+    j.pts = s.pts;
+    j.nn_xyz = s.nn_xyz;
+    j.nn_idx = s.nn_idx;
+    j.nn_d = s.nn_d;
+    j.nn_cnt = s.nn_cnt;
+    j.partial = s.partial;
+    j.slot = slot;
+    j.n = (int32_t)s.n;
+    j.nblk = s.nblk;
+}
+
+static void init_slot(IekfSlot& s, const livo_state& st, const livo_state& prior, int max_iter) {
+    std::memset(&s, 0, sizeof(IekfSlot));
+    s.state = st;
+    s.prior = prior;
+    s.ctrl.stop = 0;
+    s.ctrl.search_en = 1;
+    s.ctrl.iter_count = -1;
+    s.ctrl.rematch_num = 0;
+    s.ctrl.max_iter = max_iter;
+}
+
+extern "C" {
+
+int livo_abi_version(void) { return LIVO_ABI_VERSION; }
+
+const char* livo_error_string(int code) {
+    switch (code) {
+        case LIVO_OK: return "ok";
+        case LIVO_E_INVALID: return "invalid argument";
+        case LIVO_E_HIP: return "HIP runtime error (no usable GPU or launch failure)";
+        case LIVO_E_NOMAP: return "map not built";
+        case LIVO_E_NOSCAN: return "unknown scan id";
+        case LIVO_E_OOM: return "device allocation failed";
+        case LIVO_E_RANGE: return "size out of supported range";
+        default: return "unknown error";
+    }
+}
+
+int livo_params_default(livo_params* p) {
+    if (!p) return LIVO_E_INVALID;
+    std::memset(p, 0, sizeof(*p));
+    p->laser_point_cov = 0.001;
+    p->R_LI[0] = p->R_LI[4] = p->R_LI[8] = 1.0;
+    p->max_residual = 2.0;
+    p->plane_threshold = 0.1f;
+    p->max_nn_sqdist = 5.0f;
+    p->max_iterations = 4;
+    p->flags = 0;
+    return LIVO_OK;
+}
+
+int livo_ctx_create(int device, const livo_params* p, livo_ctx** out) {
+    if (!out) return LIVO_E_INVALID;
+    *out = nullptr;
+    livo_params def;
+    livo_params_default(&def);
+    if (p && !params_valid(p)) return LIVO_E_INVALID;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return LIVO_E_HIP;
+    if (device < 0 || device >= ndev) return LIVO_E_INVALID;
+    livo_ctx* c = new (std::nothrow) livo_ctx();
+    if (!c) return LIVO_E_OOM;
+    c->device = device;
+    c->params = p ? *p : def;
+    if (set_device(c) || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return LIVO_E_HIP;
+    }
+    *out = c;
+    return LIVO_OK;
+}
+
+int livo_ctx_destroy(livo_ctx* c) {
+    if (!c) return LIVO_E_INVALID;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto& s : c->scans) {
+        dev_free(s.pts); dev_free(s.nn_xyz); dev_free(s.nn_idx); dev_free(s.nn_d); dev_free(s.nn_cnt);
+        dev_free(s.partial);
+    }
+    dev_free(c->nodes);
+    dev_free(c->d_slots);
+    dev_free(c->d_jobs);
+    if (c->h_slots) (void)hipHostFree(c->h_slots);
+    if (c->h_jobs) (void)hipHostFree(c->h_jobs);
+    if (c->scratch) (void)hipFree(c->scratch);
+    if (c->events_ready)
+        for (auto& e : c->ev) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return LIVO_OK;
+}
+
+int livo_ctx_set_params(livo_ctx* c, const livo_params* p) {
+    if (!c || !params_valid(p)) return LIVO_E_INVALID;
+    c->params = *p;
+    return LIVO_OK;
+}
+
+int livo_ctx_set_profiling(livo_ctx* c, int enable) {
+    if (!c) return LIVO_E_INVALID;
+    if (set_device(c)) return LIVO_E_HIP;
+    if (enable && !c->events_ready) {
+        for (auto& e : c->ev) HIP_TRY(hipEventCreate(&e));
+        c->events_ready = true;
+    }
+    c->profiling = enable ? 1 : 0;
+    return LIVO_OK;
+}
+
+int livo_last_timings(livo_ctx* c, livo_timings* out) {
+    if (!c || !out) return LIVO_E_INVALID;
+    *out = c->last;
+    return LIVO_OK;
+}
+
+int livo_map_build(livo_ctx* c, const float* xyz, int64_t M, int64_t stride_bytes) {
+    if (!c || M < 0 || (M > 0 && !xyz)) return LIVO_E_INVALID;
+    if (set_device(c)) return LIVO_E_HIP;
+    HostMap hm;
+    int rc = build_host_map(xyz, M, stride_bytes, &hm);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    dev_free(c->nodes);
+    c->has_map = false;
+    const size_t bytes = (size_t)(hm.num_slots + 1) * sizeof(MapNode);
+    if (hipMalloc((void**)&c->nodes, bytes) != hipSuccess) {
+        free_host_map(&hm);
+        c->nodes = nullptr;
+        return LIVO_E_OOM;
+    }
+    hipError_t e = hipMemcpy(c->nodes, hm.nodes, bytes, hipMemcpyHostToDevice);
+    free_host_map(&hm);
+    if (e != hipSuccess) return LIVO_E_HIP;
+    c->map_points = M;
+    c->map_slots = hm.num_slots;
+    c->map_depth = hm.depth;
+    c->has_map = true;
+    for (auto& s : c->scans) s.searched = false;  // cached neighbours refer to the old map
+    return LIVO_OK;
+}
+
+int livo_map_get_info(livo_ctx* c, livo_map_info* out) {
+    if (!c || !out) return LIVO_E_INVALID;
+    if (!c->has_map) return LIVO_E_NOMAP;
+    out->num_points = c->map_points;
+    out->depth = c->map_depth;
+    out->reserved = 0;
+    out->num_slots = c->map_slots;
+    out->device_bytes = (c->map_slots + 1) * (int64_t)sizeof(MapNode);
+    return LIVO_OK;
+}
+
+int livo_knn(livo_ctx* c, const float* q, int64_t n, int32_t k, int32_t* idx, float* d) {
+    if (!c || n < 0 || k < 1 || k > kNN || (n > 0 && (!q || !idx || !d))) return LIVO_E_INVALID;
+    if (!c->has_map) return LIVO_E_NOMAP;
+    if (n == 0) return LIVO_OK;
+    if (set_device(c)) return LIVO_E_HIP;
+    const size_t qb = (size_t)n * 3 * sizeof(float), ib = (size_t)n * k * sizeof(int32_t),
+                 db = (size_t)n * k * sizeof(float);
+    int rc = ensure_scratch(c, qb + ib + db + 64);
+    if (rc) return rc;
+    char* base = (char*)c->scratch;
+    float* dq = (float*)base;
+    int32_t* di = (int32_t*)(base + qb);
+    float* dd = (float*)(base + qb + ib);
+    HIP_TRY(hipMemcpyAsync(dq, q, qb, hipMemcpyHostToDevice, c->stream));
+    rc = launch_knn(c->nodes, c->map_points > 0, c->map_depth, dq, n, k, di, dd, c->stream);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(idx, di, ib, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(d, dd, db, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return LIVO_OK;
+}
+
+int livo_scan_upload(livo_ctx* c, const float* xyz, int64_t N, int64_t stride_bytes, int32_t* scan_id) {
+    if (!c || !scan_id || N < 0 || (N > 0 && !xyz)) return LIVO_E_INVALID;
+    if (N > (int64_t)0x7FFFFFFF - kBlock) return LIVO_E_RANGE;
+    if (stride_bytes == 0) stride_bytes = 3 * sizeof(float);
+    if (stride_bytes < (int64_t)(3 * sizeof(float))) return LIVO_E_INVALID;
+    if (set_device(c)) return LIVO_E_HIP;
+    ScanBuf s;
+    s.used = true;
+    s.n = N;
+    s.nblk = (int32_t)((N + kBlock - 1) / kBlock);
+    int rc = 0;
+    rc |= dev_alloc(&s.pts, (size_t)N * 4);
+    rc |= dev_alloc(&s.nn_xyz, (size_t)N * 15);
+    rc |= dev_alloc(&s.nn_idx, (size_t)N * 5);
+    rc |= dev_alloc(&s.nn_d, (size_t)N * 5);
+    rc |= dev_alloc(&s.nn_cnt, (size_t)N);
+    rc |= dev_alloc(&s.partial, (size_t)std::max(s.nblk, 1) * kRedCols);
+    if (rc) {
+        dev_free(s.pts); dev_free(s.nn_xyz); dev_free(s.nn_idx); dev_free(s.nn_d); dev_free(s.nn_cnt);
+        dev_free(s.partial);
+        return LIVO_E_OOM;
+    }
+    if (N > 0) {
+        std::vector<float> h((size_t)N * 4);
+        const char* base = (const char*)xyz;
+        for (int64_t i = 0; i < N; i++) {
+            const float* p = (const float*)(base + i * stride_bytes);
+            h[4 * i + 0] = p[0];
+            h[4 * i + 1] = p[1];
+            h[4 * i + 2] = p[2];
+            h[4 * i + 3] = 0.0f;
+        }
+        if (hipMemcpy(s.pts, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) return LIVO_E_HIP;
+        if (hipMemset(s.nn_cnt, 0, (size_t)N * sizeof(int32_t)) != hipSuccess) return LIVO_E_HIP;
+    }
+    int32_t id = -1;
+    for (size_t i = 0; i < c->scans.size(); i++)
+        if (!c->scans[i].used) { id = (int32_t)i; break; }
+    if (id < 0) {
+        id = (int32_t)c->scans.size();
+        c->scans.push_back(s);
+    } else {
+        c->scans[id] = s;
+    }
+    *scan_id = id;
+    return LIVO_OK;
+}
+
+int livo_scan_release(livo_ctx* c, int32_t id) {
+    if (!c) return LIVO_E_INVALID;
+    if (id < 0 || id >= (int32_t)c->scans.size() || !c->scans[id].used) return LIVO_E_NOSCAN;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    ScanBuf& s = c->scans[id];
+    dev_free(s.pts); dev_free(s.nn_xyz); dev_free(s.nn_idx); dev_free(s.nn_d); dev_free(s.nn_cnt);
+    dev_free(s.partial);
+    s = ScanBuf{};
+    return LIVO_OK;
+}
+
+static ScanBuf* get_scan(livo_ctx* c, int32_t id) {
+    if (id < 0 || id >= (int32_t)c->scans.size() || !c->scans[id].used) return nullptr;
+    return &c->scans[id];
+}
+
+int livo_h_share(livo_ctx* c, int32_t id, const livo_state* state, int search_en, double HTH[81], double HTL[9],
+                 int64_t* effct, const livo_point_out* out) {
+    if (!c || !state || !HTH || !HTL) return LIVO_E_INVALID;
+    ScanBuf* s = get_scan(c, id);
+    if (!s) return LIVO_E_NOSCAN;
+    if (!c->has_map) return LIVO_E_NOMAP;
+    if (set_device(c)) return LIVO_E_HIP;
+    int rc = ensure_slots(c, 1);
+    if (rc) return rc;
+    const int64_t N = s->n;
+    // debug scratch: normvec N*4, sel N, world N*3
+    const size_t nvb = (size_t)N * 16, wb = (size_t)N * 12, sb = (size_t)N;
+    rc = ensure_scratch(c, nvb + wb + sb + 64);
+    if (rc) return rc;
+    char* base = (char*)c->scratch;
+    init_slot(c->h_slots[0], *state, *state, c->params.max_iterations);
+    fill_job(c->h_jobs[0], *s, c->d_slots);
+    HIP_TRY(hipMemcpyAsync(c->d_slots, c->h_slots, sizeof(IekfSlot), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->d_jobs, c->h_jobs, sizeof(HsJob), hipMemcpyHostToDevice, c->stream));
+    HsParams hp = make_hs_params(c);
+    hp.force = search_en ? 1 : 0;
+    const bool want_nv = out && out->normvec, want_sel = out && out->selected, want_w = out && out->world_xyz;
+    hp.dbg.normvec = want_nv ? (float*)base : nullptr;
+    hp.dbg.world = want_w ? (float*)(base + nvb) : nullptr;
+    hp.dbg.sel = want_sel ? (uint8_t*)(base + nvb + wb) : nullptr;
+    if (!search_en && !s->searched) {
+        // no cached neighbours yet: nothing is matched (points_near.size() < 5, :525)
+        if (N > 0) HIP_TRY(hipMemsetAsync(s->nn_cnt, 0, (size_t)N * sizeof(int32_t), c->stream));
+    }
+    rc = launch_hshare(hp, 1, std::max(s->nblk, 1), c->map_depth, search_en != 0, c->stream);
+    if (rc) return rc;
+    SolveParams sp{c->d_slots, c->d_jobs, 1};
+    rc = launch_solve(sp, 1, c->stream);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(c->h_slots, c->d_slots, sizeof(IekfSlot), hipMemcpyDeviceToHost, c->stream));
+    if (N > 0 && out) {
+        if (want_nv) HIP_TRY(hipMemcpyAsync(out->normvec, hp.dbg.normvec, nvb, hipMemcpyDeviceToHost, c->stream));
+        if (want_w) HIP_TRY(hipMemcpyAsync(out->world_xyz, hp.dbg.world, wb, hipMemcpyDeviceToHost, c->stream));
+        if (want_sel) HIP_TRY(hipMemcpyAsync(out->selected, hp.dbg.sel, sb, hipMemcpyDeviceToHost, c->stream));
+    }
+    std::vector<int32_t> idx_t;
+    std::vector<float> d_t;
+    if (N > 0 && out && (out->nn_idx || out->nn_sqdist)) {
+        idx_t.resize((size_t)N * 5);
+        d_t.resize((size_t)N * 5);
+        HIP_TRY(hipMemcpyAsync(idx_t.data(), s->nn_idx, (size_t)N * 5 * 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(d_t.data(), s->nn_d, (size_t)N * 5 * 4, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (search_en) s->searched = true;
+    const IekfSlot& hs = c->h_slots[0];
+    const double* r = hs.red;
+    std::memset(HTH, 0, 81 * sizeof(double));
+    std::memset(HTL, 0, 9 * sizeof(double));
+    int q = 0;
+    for (int a = 0; a < 6; a++)
+        for (int b = a; b < 6; b++) {
+            HTH[a * 9 + b] = r[q];
+            HTH[b * 9 + a] = r[q];
+            q++;
+        }
+    for (int a = 0; a < 6; a++) HTL[a] = r[21 + a];
+    if (effct) *effct = (int64_t)r[28];
+    if (out && out->visits) *out->visits = (int64_t)hs.visits[0];
+    if (!idx_t.empty()) {
+        for (int64_t i = 0; i < N; i++)
+            for (int k = 0; k < 5; k++) {
+                if (out->nn_idx) out->nn_idx[i * 5 + k] = idx_t[(size_t)k * N + i];
+                if (out->nn_sqdist) out->nn_sqdist[i * 5 + k] = d_t[(size_t)k * N + i];
+            }
+    }
+    return LIVO_OK;
+}
+
+int livo_iekf_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_state* states, const livo_state* priors,
+                           livo_iter_stats* stats) {
+    if (!c || n < 0 || (n > 0 && (!ids || !states))) return LIVO_E_INVALID;
+    if (n == 0) return LIVO_OK;
+    if (!c->has_map) return LIVO_E_NOMAP;
+    for (int32_t b = 0; b < n; b++)
+        if (!get_scan(c, ids[b])) return LIVO_E_NOSCAN;
+    if (set_device(c)) return LIVO_E_HIP;
+    int rc = ensure_slots(c, n);
+    if (rc) return rc;
+    const int max_iter = c->params.max_iterations;
+    int max_nblk = 1;
+    int64_t queries = 0;
+    for (int32_t b = 0; b < n; b++) {
+        ScanBuf* s = get_scan(c, ids[b]);
+        init_slot(c->h_slots[b], states[b], priors ? priors[b] : states[b], max_iter);
+        fill_job(c->h_jobs[b], *s, c->d_slots + b);
+        max_nblk = std::max(max_nblk, s->nblk);
+        queries += s->n;
+    }
+    HIP_TRY(hipMemcpyAsync(c->d_slots, c->h_slots, sizeof(IekfSlot) * n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->d_jobs, c->h_jobs, sizeof(HsJob) * n, hipMemcpyHostToDevice, c->stream));
+    HsParams hp = make_hs_params(c);
+    SolveParams sp{c->d_slots, c->d_jobs, 0};
+    const bool prof = c->profiling && c->events_ready;
+    const int evals = max_iter + 1;
+    for (int e = 0; e < evals; e++) {
+        if (prof) HIP_TRY(hipEventRecord(c->ev[2 * e], c->stream));
+        rc = launch_hshare(hp, n, max_nblk, c->map_depth, e == 0, c->stream);
+        if (rc) return rc;
+        if (prof) HIP_TRY(hipEventRecord(c->ev[2 * e + 1], c->stream));
+        rc = launch_solve(sp, n, c->stream);
+        if (rc) return rc;
+    }
+    if (prof) HIP_TRY(hipEventRecord(c->ev[2 * LIVO_MAX_EVALS], c->stream));
+    HIP_TRY(hipMemcpyAsync(c->h_slots, c->d_slots, sizeof(IekfSlot) * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (int32_t b = 0; b < n; b++) {
+        const IekfSlot& s = c->h_slots[b];
+        states[b] = s.state;
+        if (stats) stats[b] = s.stats;
+        c->scans[ids[b]].searched = true;
+    }
+    if (prof) {
+        livo_timings t{};
+        for (int e = 0; e < evals; e++) {
+            float ms_h = 0.f, ms_s = 0.f;
+            (void)hipEventElapsedTime(&ms_h, c->ev[2 * e], c->ev[2 * e + 1]);
+            const hipEvent_t end = (e + 1 < evals) ? c->ev[2 * e + 2] : c->ev[2 * LIVO_MAX_EVALS];
+            (void)hipEventElapsedTime(&ms_s, c->ev[2 * e + 1], end);
+            if (e == 0) {
+                t.knn_ms += ms_h;
+                t.knn_launches++;
+            } else {
+                t.plane_ms += ms_h;
+            }
+            t.solve_ms += ms_s;
+        }
+        // the first evaluation (k_hshare<true>) searches for every point of every scan
+        for (int32_t b = 0; b < n; b++) {
+            t.knn_visits += (int64_t)c->h_slots[b].visits[0];
+            t.knn_queries += c->scans[ids[b]].n;
+            t.effct_points += c->h_slots[b].stats.effct_feat_num[0];
+        }
+        c->last = t;
+    }
+    (void)queries;
+    return LIVO_OK;
+}
+
+int livo_iekf_update(livo_ctx* c, int32_t id, livo_state* state, const livo_state* prior, livo_iter_stats* stats) {
+    if (!state) return LIVO_E_INVALID;
+    return livo_iekf_update_batch(c, 1, &id, state, prior, stats);
+}
+
+int livo_sync(livo_ctx* c) {
+    if (!c) return LIVO_E_INVALID;
+    if (set_device(c)) return LIVO_E_HIP;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return LIVO_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,126 @@
+// livo_internal.h — layouts shared by the host runtime (livo_capi.cpp,
+// map_build.cpp) and the CDNA4 kernels (livo_kernels.hip).  Not part of the ABI.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include "livo.h"
+
+namespace livo {
+
+constexpr int kNN = LIVO_NUM_MATCH_POINTS;  // 5
+constexpr int kDim = LIVO_DIM_STATE;        // 18
+constexpr int kBlock = 256;                 // threads per block of the per-point kernels
+constexpr int kRedCols = 32;                // doubles per block partial (29 used)
+constexpr int kRedUsed = 29;                // 21 HTH upper-tri + 6 HTL + residual sum + count
+
+// ---------------------------------------------------------------------------
+// Device map: the ikd-Tree built exactly as KD_TREE::Build (median of the
+// longest-extent axis, ikd_Tree.cpp:537-602) stored in heap order (root = 0,
+// children 2h+1 / 2h+2) as one 64-B record per node.  A record carries what
+// the traversal needs at that node and nothing else: the node point, and the
+// bounding boxes of its two children (KD_TREE_NODE::node_range_* of the
+// sons, read at ikd_Tree.cpp:867-868 through calc_box_dist).  Record h lives
+// at slot h+1 so the two children of a node (2h+1, 2h+2) share one 128-B line.
+//
+//   a = (x, y, z, meta)      meta = orig_index | left_exists<<30 | right_exists<<31
+//   b = (L.minx, L.maxx, L.miny, L.maxy)
+//   c = (L.minz, L.maxz, R.minx, R.maxx)
+//   d = (R.miny, R.maxy, R.minz, R.maxz)
+// ---------------------------------------------------------------------------
+struct alignas(16) MapNode {
+    float a[4];
+    float b[4];
+    float c[4];
+    float d[4];
+};
+static_assert(sizeof(MapNode) == 64, "MapNode must be 64 bytes");
+
+constexpr uint32_t kIdxMask = 0x3FFFFFFFu;
+constexpr uint32_t kLeftBit = 0x40000000u;
+constexpr uint32_t kRightBit = 0x80000000u;
+constexpr int64_t kMaxMapPoints = (int64_t)kIdxMask;  // 2^30 - 1
+constexpr int kMaxDepth = 31;
+
+// IEKF control block (the loop variables of laser_mapping.cpp:166-238).
+struct IekfCtrl {
+    int32_t stop;         // EKF_stop_flg reached: every later launch for this scan exits
+    int32_t search_en;    // nearest_search_en for the next evaluation
+    int32_t iter_count;   // iterCount of the next evaluation (starts at -1)
+    int32_t rematch_num;
+    int32_t converged;    // flg_EKF_converged of the last evaluation
+    int32_t n_evals;      // evaluations done
+    int32_t max_iter;     // NUM_MAX_ITERATIONS
+    int32_t last_search;  // nearest_search_en used by the last evaluation
+};
+
+// Everything one scan update needs on the device (one per batch entry).
+struct alignas(16) IekfSlot {
+    livo_state state;     // in/out
+    livo_state prior;     // state_propagat
+    double G[kDim * kDim];
+    double Pinv[kDim * kDim];   // state.cov^-1, constant over one update
+    double red[kRedCols];       // last reduced h_share sums (for livo_h_share)
+    livo_iter_stats stats;
+    IekfCtrl ctrl;
+    unsigned long long visits[LIVO_MAX_EVALS];  // k-NN nodes visited per evaluation
+    int32_t eval_search[LIVO_MAX_EVALS];
+};
+
+// One scan of a batched launch.
+struct HsJob {
+    const float* pts;     // N x 4 floats (x, y, z, 0), device
+    float* nn_xyz;        // 15 x N SoA neighbour coordinates (Nearest_Points cache)
+    int32_t* nn_idx;      // 5 x N map indices
+    float* nn_d;          // 5 x N squared distances
+    int32_t* nn_cnt;      // N neighbours found
+    double* partial;      // nblk x kRedCols block partial sums
+    IekfSlot* slot;
+    int32_t n;
+    int32_t nblk;
+};
+
+// Optional per-point debug outputs (single-scan livo_h_share only).
+struct HsDebug {
+    float* normvec;   // N x 4
+    uint8_t* sel;     // N
+    float* world;     // N x 3
+};
+
+struct HsParams {
+    const MapNode* nodes;   // slot 0 unused; root at slot 1
+    const HsJob* jobs;
+    HsDebug dbg;
+    double R_LI[9];
+    double t_LI[3];
+    double inv_r;           // 1.0 / LASER_POINT_COV
+    double max_res;         // 2.0
+    float plane_thr;        // 0.1f
+    float max_sqd;          // 5.0f
+    int32_t has_map;
+    int32_t force;          // -1: follow ctrl; 0: no search; 1: search
+};
+
+struct SolveParams {
+    IekfSlot* slots;
+    const HsJob* jobs;
+    int32_t mode;           // 0: reduce + solve + control; 1: reduce only (livo_h_share)
+};
+
+// Host-side map build (map_build.cpp).
+struct HostMap {
+    MapNode* nodes = nullptr;  // (num_slots + 1) records, slot 0 unused
+    int64_t num_points = 0;
+    int64_t num_slots = 0;
+    int32_t depth = 0;
+};
+int build_host_map(const float* xyz, int64_t M, int64_t stride_bytes, HostMap* out);
+void free_host_map(HostMap* m);
+
+// Kernel launchers (livo_kernels.hip).  All asynchronous on `stream`.
+int launch_hshare(const HsParams& p, int n_jobs, int max_nblk, int depth, bool first, void* stream);
+int launch_solve(const SolveParams& p, int n_jobs, void* stream);
+int launch_knn(const MapNode* nodes, int has_map, int depth, const float* q, int64_t n, int k, int32_t* idx,
+               float* d, void* stream);
+
+}  // namespace livo

@@ -1,0 +1,914 @@
+// livo_kernels.hip — CDNA4 (gfx950) kernels of the LIO scan-to-map IEKF path.
+//
+//   k_hshare<FIRST>  one thread per scan point, 256-thread blocks, grid
+//                    (blocks per scan, scans in the batch):
+//                      pointBodyToWorld            laser_mapping.cpp:662-671
+//                      exact k=5 NN (if searching) ikd_Tree.cpp:350-380, 843-986
+//                      sqdis[4] > 5 gate           laser_mapping.cpp:518
+//                      esti_plane (float QR)       common_lib.h:670-702
+//                      residual / s > 0.9 gate     laser_mapping.cpp:532-543
+//                      |pd2| <= 2 compaction gate  laser_mapping.cpp:552
+//                      H row + HᵀH / HᵀL partials  laser_mapping.cpp:564-593
+//                    FIRST = the first evaluation of an update (iterCount -1),
+//                    which always searches; !FIRST follows the device-side
+//                    nearest_search_en of each scan.  Two symbols so rocprof
+//                    separates the full k-NN pass from the re-fit passes.
+//   k_solve          one 256-thread block per scan: deterministic reduction of
+//                    the block partials, the 18x18 solve, boxplus, convergence
+//                    and rematch control, covariance update
+//                    (laser_mapping.cpp:171-238, common_lib.h:565-587).
+//   k_knn            standalone k-NN (livo_knn).
+//
+// Numerics: compiled with -ffp-contract=off and correctly rounded f32
+// division/sqrt, and every expression keeps the reference's operation order,
+// so the float plane fit and the float k-NN distances are bit-identical to
+// the CPU restatement (oracle/livo_oracle.cpp).  Doubles are summed in a
+// fixed order (wave shuffle tree -> LDS -> block order) so results are
+// reproducible run to run.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "livo_internal.h"
+
+namespace livo {
+
+// ============================================================== k-NN ======
+// PointType_CMP::operator< (ikd_Tree.h:57-60).
+__device__ __forceinline__ bool cand_less(float da, float xa, float db, float xb) {
+    if ((double)fabsf(da - db) < 1e-10) return xa < xb;
+    return da < db;
+}
+
+// MANUAL_HEAP (ikd_Tree.cpp:1345-1411) with capacity 2k and at most k = 5
+// live entries, held in registers: every slot index below is a compile-time
+// constant (the runtime heap size only selects a branch), so nothing spills
+// to scratch.  The same FloatUp / MoveDown steps as the reference keep even
+// the order of entries that compare equal (duplicate points) identical.
+struct KHeap {
+    float d[kNN];
+    float x[kNN];
+    uint32_t node[kNN];  // heap index of the map record
+    int size;
+};
+
+#define KH_CPY(h, i, j) do { (h).d[i] = (h).d[j]; (h).x[i] = (h).x[j]; (h).node[i] = (h).node[j]; } while (0)
+#define KH_SET(h, i, cd, cx, cn) do { (h).d[i] = (cd); (h).x[i] = (cx); (h).node[i] = (cn); } while (0)
+#define KH_LT(h, i, cd, cx) cand_less((h).d[i], (h).x[i], (cd), (cx))     /* heap[i] < c */
+#define KH_GT(h, i, cd, cx) cand_less((cd), (cx), (h).d[i], (h).x[i])     /* c < heap[i] */
+
+// push into a heap of size s < 5: FloatUp from slot s.
+__device__ __forceinline__ void kh_push(KHeap& h, float cd, float cx, uint32_t cn) {
+    const int s = h.size;
+    if (s == 0) {
+        KH_SET(h, 0, cd, cx, cn);
+    } else if (s == 1) {
+        if (KH_LT(h, 0, cd, cx)) { KH_CPY(h, 1, 0); KH_SET(h, 0, cd, cx, cn); } else KH_SET(h, 1, cd, cx, cn);
+    } else if (s == 2) {
+        if (KH_LT(h, 0, cd, cx)) { KH_CPY(h, 2, 0); KH_SET(h, 0, cd, cx, cn); } else KH_SET(h, 2, cd, cx, cn);
+    } else if (s == 3) {
+        if (KH_LT(h, 1, cd, cx)) {
+            KH_CPY(h, 3, 1);
+            if (KH_LT(h, 0, cd, cx)) { KH_CPY(h, 1, 0); KH_SET(h, 0, cd, cx, cn); } else KH_SET(h, 1, cd, cx, cn);
+        } else KH_SET(h, 3, cd, cx, cn);
+    } else {
+        if (KH_LT(h, 1, cd, cx)) {
+            KH_CPY(h, 4, 1);
+            if (KH_LT(h, 0, cd, cx)) { KH_CPY(h, 1, 0); KH_SET(h, 0, cd, cx, cn); } else KH_SET(h, 1, cd, cx, cn);
+        } else KH_SET(h, 4, cd, cx, cn);
+    }
+    h.size = s + 1;
+}
+
+// pop the top of a heap of size s >= 1: heap[0] = heap[s-1], MoveDown(0).
+__device__ __forceinline__ void kh_pop(KHeap& h) {
+    const int s = h.size;
+    if (s <= 1) { h.size = 0; return; }
+    float td, tx;
+    uint32_t tn;
+    if (s == 5) { td = h.d[4]; tx = h.x[4]; tn = h.node[4]; }
+    else if (s == 4) { td = h.d[3]; tx = h.x[3]; tn = h.node[3]; }
+    else if (s == 3) { td = h.d[2]; tx = h.x[2]; tn = h.node[2]; }
+    else { td = h.d[1]; tx = h.x[1]; tn = h.node[1]; }
+    const int ns = s - 1;  // heap_size after the pop (1..4)
+    if (ns == 1) {
+        KH_SET(h, 0, td, tx, tn);
+    } else if (ns == 2) {
+        if (KH_GT(h, 1, td, tx)) { KH_CPY(h, 0, 1); KH_SET(h, 1, td, tx, tn); } else KH_SET(h, 0, td, tx, tn);
+    } else {
+        // ns = 3 or 4: l = 1, or 2 if heap[1] < heap[2]
+        const bool right = cand_less(h.d[1], h.x[1], h.d[2], h.x[2]);
+        if (!right) {
+            if (KH_GT(h, 1, td, tx)) {
+                KH_CPY(h, 0, 1);
+                if (ns == 4 && KH_GT(h, 3, td, tx)) { KH_CPY(h, 1, 3); KH_SET(h, 3, td, tx, tn); }
+                else KH_SET(h, 1, td, tx, tn);
+            } else KH_SET(h, 0, td, tx, tn);
+        } else {
+            if (KH_GT(h, 2, td, tx)) { KH_CPY(h, 0, 2); KH_SET(h, 2, td, tx, tn); } else KH_SET(h, 0, td, tx, tn);
+        }
+    }
+    h.size = ns;
+}
+
+// The candidate list handed back by Nearest_Search (:374-378): the heap
+// popped top-first and inserted at the front, i.e. ascending.
+struct Cands {
+    float d[kNN];
+    uint32_t node[kNN];
+    int n;
+};
+
+__device__ __forceinline__ void kh_extract(KHeap& h, Cands& c) {
+    const int found = h.size;
+    float pd[kNN];
+    uint32_t pn[kNN];
+#pragma unroll
+    for (int i = 0; i < kNN; i++) {  // pd[i] = i-th pop (descending)
+        pd[i] = h.d[0];
+        pn[i] = h.node[0];
+        if (i < found) kh_pop(h);
+    }
+#pragma unroll
+    for (int j = 0; j < kNN; j++) {  // c[j] = pop number found-1-j
+        float dj = INFINITY;
+        uint32_t nj = 0u;
+#pragma unroll
+        for (int i = 0; i < kNN; i++)
+            if (i == found - 1 - j) { dj = pd[i]; nj = pn[i]; }
+        c.d[j] = dj;
+        c.node[j] = nj;
+    }
+    c.n = found;
+}
+
+// calc_box_dist (ikd_Tree.cpp:1297-1307), same add order.
+__device__ __forceinline__ float box_dist(float px, float py, float pz, float x0, float x1, float y0, float y1,
+                                          float z0, float z1) {
+    float m = 0.0f;
+    float t;
+    t = px - x0; if (px < x0) m = m + t * t;
+    t = px - x1; if (px > x1) m = m + t * t;
+    t = py - y0; if (py < y0) m = m + t * t;
+    t = py - y1; if (py > y1) m = m + t * t;
+    t = pz - z0; if (pz < z0) m = m + t * t;
+    t = pz - z1; if (pz > z1) m = m + t * t;
+    return m;
+}
+
+__device__ __forceinline__ const float4* rec_ptr(const MapNode* nodes, uint32_t h) {
+    return reinterpret_cast<const float4*>(nodes + (size_t)h + 1);
+}
+
+// Exact k-NN with the visiting order of KD_TREE::Search (ikd_Tree.cpp:843-986):
+// at each node the point is offered to the candidate list, then the sons are
+// taken near-first (left on a tie, :869), each only if the list is not full
+// or its box distance is below the current k-th distance at the moment it is
+// reached.  The far son waits on a per-lane stack in LDS (stack[e * stride]).
+// Same visits as the reference, so the candidate set and order are identical,
+// ties included.
+__device__ __forceinline__ void knn_search(const MapNode* __restrict__ nodes, int has_map, float qx, float qy,
+                                           float qz, uint2* stack, int stride, Cands& c, unsigned& visits) {
+    KHeap h;
+#pragma unroll
+    for (int j = 0; j < kNN; j++) {
+        h.d[j] = INFINITY;
+        h.x[j] = 0.0f;
+        h.node[j] = 0u;
+    }
+    h.size = 0;
+    if (!has_map) {
+        kh_extract(h, c);
+        return;
+    }
+    uint32_t node = 0;
+    bool has = true;
+    int sp = 0;
+    while (true) {
+        if (!has) {
+            while (sp > 0) {
+                sp--;
+                const uint2 e = stack[sp * stride];
+                const float de = __uint_as_float(e.y);
+                if (h.size < kNN || de < h.d[0]) {
+                    node = e.x;
+                    has = true;
+                    break;
+                }
+            }
+            if (!has) break;
+        }
+        const float4* rp = rec_ptr(nodes, node);
+        const float4 a = rp[0];
+        const float4 b = rp[1];
+        const float4 cc = rp[2];
+        const float4 dd = rp[3];
+        visits++;
+        const uint32_t meta = __float_as_uint(a.w);
+        {
+            // calc_dist (ikd_Tree.cpp:1291-1295), float, left to right
+            const float dx = qx - a.x, dy = qy - a.y, dz = qz - a.z;
+            const float dist = (dx * dx + dy * dy) + dz * dz;
+            if (dist <= INFINITY && (h.size < kNN || dist < h.d[0])) {
+                if (h.size >= kNN) kh_pop(h);  // q.pop(); q.push(current_point)  (:861-863)
+                kh_push(h, dist, a.x, node);
+            }
+        }
+        const bool hl = (meta & kLeftBit) != 0u;
+        const bool hr = (meta & kRightBit) != 0u;
+        const float dl = hl ? box_dist(qx, qy, qz, b.x, b.y, b.z, b.w, cc.x, cc.y) : INFINITY;
+        const float dr = hr ? box_dist(qx, qy, qz, cc.z, cc.w, dd.x, dd.y, dd.z, dd.w) : INFINITY;
+        const bool left_first = dl <= dr;
+        const uint32_t nnear = left_first ? 2u * node + 1u : 2u * node + 2u;
+        const uint32_t nfar = left_first ? 2u * node + 2u : 2u * node + 1u;
+        const float dnear = left_first ? dl : dr;
+        const float dfar = left_first ? dr : dl;
+        const bool enear = left_first ? hl : hr;
+        const bool efar = left_first ? hr : hl;
+        const bool full = h.size >= kNN;
+        const float top = h.d[0];
+        if (efar && (!full || dfar < top)) {
+            stack[sp * stride] = make_uint2(nfar, __float_as_uint(dfar));
+            sp++;
+        }
+        if (enear && (!full || dnear < top)) {
+            node = nnear;
+        } else {
+            has = false;
+        }
+    }
+    kh_extract(h, c);
+}
+
+// ======================================================== esti_plane ======
+// Eigen 3.3 ColPivHouseholderQR<Matrix<float,5,3>> + solve(-1), restated with
+// the SSE2 reduction orders documented in oracle/livo_oracle.cpp.  Columns of
+// A live in registers as q[col][row] with compile-time indices only.
+__device__ __forceinline__ float dot_tail(const float (&a)[5], const float (&b)[5], int k) {
+    // sum_{i=k+1..4} a[i]*b[i]; length 4 uses the Packet4f predux order
+    if (k == 0) return ((a[1] * b[1]) + (a[3] * b[3])) + ((a[2] * b[2]) + (a[4] * b[4]));
+    if (k == 1) return (a[2] * b[2] + a[3] * b[3]) + a[4] * b[4];
+    return a[3] * b[3] + a[4] * b[4];
+}
+__device__ __forceinline__ float sqn_tail(const float (&a)[5], int k) {
+    if (k == 0) return ((a[1] * a[1] + a[2] * a[2]) + a[3] * a[3]) + a[4] * a[4];
+    if (k == 1) return (a[2] * a[2] + a[3] * a[3]) + a[4] * a[4];
+    return a[3] * a[3] + a[4] * a[4];
+}
+
+__device__ __forceinline__ void swap_cols(float (&u)[5], float (&v)[5]) {
+#pragma unroll
+    for (int r = 0; r < 5; r++) {
+        float t = u[r]; u[r] = v[r]; v[r] = t;
+    }
+}
+
+__device__ __forceinline__ bool esti_plane(const float (&px)[5], const float (&py)[5], const float (&pz)[5],
+                                           float thr, float (&pabcd)[4]) {
+    float q0[5], q1[5], q2[5];
+#pragma unroll
+    for (int r = 0; r < 5; r++) { q0[r] = px[r]; q1[r] = py[r]; q2[r] = pz[r]; }
+    float nu[3], nd[3], hc[3];
+    int tr[3];
+    {
+        float s0 = ((q0[0] * q0[0] + q0[2] * q0[2]) + (q0[1] * q0[1] + q0[3] * q0[3])) + q0[4] * q0[4];
+        float s1 = ((q1[0] * q1[0] + q1[2] * q1[2]) + (q1[1] * q1[1] + q1[3] * q1[3])) + q1[4] * q1[4];
+        float s2 = ((q2[0] * q2[0] + q2[2] * q2[2]) + (q2[1] * q2[1] + q2[3] * q2[3])) + q2[4] * q2[4];
+        nd[0] = sqrtf(s0); nd[1] = sqrtf(s1); nd[2] = sqrtf(s2);
+        nu[0] = nd[0]; nu[1] = nd[1]; nu[2] = nd[2];
+    }
+    const float eps = 1.1920928955078125e-07f;  // FLT_EPSILON
+    float mxn = nu[0];
+    if (nu[1] > mxn) mxn = nu[1];
+    if (nu[2] > mxn) mxn = nu[2];
+    const float th_help = (mxn * eps) * (mxn * eps) / 5.0f;
+    const float ndt = sqrtf(eps);
+    int nonzero = 3;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        // pivot: first maximum of the updated norms over columns k..2
+        int big = k;
+        float bigv = nu[k];
+#pragma unroll
+        for (int j = k + 1; j < 3; j++)
+            if (nu[j] > bigv) { bigv = nu[j]; big = j; }
+        const float big_sq = bigv * bigv;
+        if (nonzero == 3 && big_sq < th_help * (float)(5 - k)) nonzero = k;
+        tr[k] = big;
+        if (big != k) {
+            if (k == 0) {
+                if (big == 1) { swap_cols(q0, q1); float t = nu[0]; nu[0] = nu[1]; nu[1] = t; t = nd[0]; nd[0] = nd[1]; nd[1] = t; }
+                else { swap_cols(q0, q2); float t = nu[0]; nu[0] = nu[2]; nu[2] = t; t = nd[0]; nd[0] = nd[2]; nd[2] = t; }
+            } else {
+                swap_cols(q1, q2); float t = nu[1]; nu[1] = nu[2]; nu[2] = t; t = nd[1]; nd[1] = nd[2]; nd[2] = t;
+            }
+        }
+        float (&col)[5] = (k == 0) ? q0 : (k == 1 ? q1 : q2);
+        // makeHouseholderInPlace
+        const float c0 = col[k];
+        const float tailSq = sqn_tail(col, k);
+        float tau, beta;
+        if (tailSq <= 1.17549435082228750797e-38f) {  // FLT_MIN
+            tau = 0.0f;
+            beta = c0;
+#pragma unroll
+            for (int i = k + 1; i < 5; i++) col[i] = 0.0f;
+        } else {
+            beta = sqrtf(c0 * c0 + tailSq);
+            if (c0 >= 0.0f) beta = -beta;
+            const float den = c0 - beta;
+#pragma unroll
+            for (int i = k + 1; i < 5; i++) col[i] = col[i] / den;
+            tau = (beta - c0) / beta;
+        }
+        hc[k] = tau;
+        col[k] = beta;
+        // applyHouseholderOnTheLeft on columns k+1..2
+        if (tau != 0.0f) {
+#pragma unroll
+            for (int j = k + 1; j < 3; j++) {
+                float (&cj)[5] = (j == 1) ? q1 : q2;
+                float tmp = dot_tail(col, cj, k);
+                tmp = tmp + cj[k];
+                cj[k] = cj[k] - tau * tmp;
+#pragma unroll
+                for (int i = k + 1; i < 5; i++) cj[i] = cj[i] - (tau * col[i]) * tmp;
+            }
+        }
+        // norm downdate
+#pragma unroll
+        for (int j = k + 1; j < 3; j++) {
+            const float (&cj)[5] = (j == 1) ? q1 : q2;
+            if (nu[j] != 0.0f) {
+                float temp = fabsf(cj[k]) / nu[j];
+                temp = (1.0f + temp) * (1.0f - temp);
+                temp = temp < 0.0f ? 0.0f : temp;
+                const float ratio = nu[j] / nd[j];
+                const float temp2 = temp * (ratio * ratio);
+                if (temp2 <= ndt) {
+                    nd[j] = sqrtf(sqn_tail(cj, k));
+                    nu[j] = nd[j];
+                } else {
+                    nu[j] = nu[j] * sqrtf(temp);
+                }
+            }
+        }
+    }
+    int perm[3] = {0, 1, 2};
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        // swap(perm[k], perm[tr[k]]) with compile-time indices
+        const int t = tr[k];
+        int pk = perm[k];
+        int pt = (t == 0) ? perm[0] : (t == 1 ? perm[1] : perm[2]);
+        if (t != k) {
+            if (t == 1) perm[1] = pk; else if (t == 2) perm[2] = pk; else perm[0] = pk;
+            perm[k] = pt;
+        }
+    }
+    float x0 = 0.0f, x1 = 0.0f, x2 = 0.0f;
+    if (nonzero > 0) {
+        float c[5] = {-1.0f, -1.0f, -1.0f, -1.0f, -1.0f};
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            if (k < nonzero) {
+                const float tau = hc[k];
+                if (tau != 0.0f) {
+                    const float (&ess)[5] = (k == 0) ? q0 : (k == 1 ? q1 : q2);
+                    float tmp = dot_tail(ess, c, k);
+                    tmp = tmp + c[k];
+                    c[k] = c[k] - tau * tmp;
+#pragma unroll
+                    for (int i = k + 1; i < 5; i++) c[i] = c[i] - (tau * ess[i]) * tmp;
+                }
+            }
+        }
+        // back substitution with R = upper triangle of q (R(s,i) = q_i[s])
+#pragma unroll
+        for (int i = 2; i >= 0; i--) {
+            if (i < nonzero && c[i] != 0.0f) {
+                const float (&qi)[5] = (i == 0) ? q0 : (i == 1 ? q1 : q2);
+                c[i] = c[i] / qi[i];
+#pragma unroll
+                for (int s = 0; s < i; s++) c[s] = c[s] - c[i] * qi[s];
+            }
+        }
+        float xs[3] = {0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            if (i < nonzero) {
+                const int pi = perm[i];
+                if (pi == 0) xs[0] = c[i]; else if (pi == 1) xs[1] = c[i]; else xs[2] = c[i];
+            }
+        }
+        x0 = xs[0]; x1 = xs[1]; x2 = xs[2];
+    }
+    const float n = sqrtf((x0 * x0 + x1 * x1) + x2 * x2);
+    pabcd[0] = x0 / n;
+    pabcd[1] = x1 / n;
+    pabcd[2] = x2 / n;
+    pabcd[3] = (float)(1.0 / (double)n);
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+        const float r = ((pabcd[0] * px[j] + pabcd[1] * py[j]) + pabcd[2] * pz[j]) + pabcd[3];
+        if (fabsf(r) > thr) ok = false;
+    }
+    return ok;
+}
+
+// ======================================================= reductions =======
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// ===================================================== per-point pass =====
+template <bool FIRST>
+__global__ __launch_bounds__(kBlock) void k_hshare(HsParams P) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const HsJob job = P.jobs[blockIdx.y];
+    if ((int)blockIdx.x >= job.nblk) return;
+    IekfSlot* slot = job.slot;
+    int search;
+    if (P.force >= 0) {
+        search = P.force;
+    } else {
+        if (slot->ctrl.stop) return;  // block-uniform
+        search = FIRST ? 1 : slot->ctrl.search_en;
+    }
+    const int tid = threadIdx.x;
+    const int i = blockIdx.x * kBlock + tid;
+    const bool valid = i < job.n;
+    double* red_lds = reinterpret_cast<double*>(smem);                       // 4 waves x 32
+    uint2* stack = reinterpret_cast<uint2*>(smem + 4 * kRedCols * sizeof(double));
+
+    const livo_state& S = slot->state;
+    double acc[kRedUsed];
+#pragma unroll
+    for (int j = 0; j < kRedUsed; j++) acc[j] = 0.0;
+    unsigned visits = 0;
+
+    if (valid) {
+        const float4 pb = reinterpret_cast<const float4*>(job.pts)[i];
+        // pointBodyToWorld (laser_mapping.cpp:662-671): double math, float storage
+        const double bx = pb.x, by = pb.y, bz = pb.z;
+        const double* RL = P.R_LI;
+        const double ix = ((RL[0] * bx + RL[1] * by) + RL[2] * bz) + P.t_LI[0];
+        const double iy = ((RL[3] * bx + RL[4] * by) + RL[5] * bz) + P.t_LI[1];
+        const double iz = ((RL[6] * bx + RL[7] * by) + RL[8] * bz) + P.t_LI[2];
+        const double* R = S.rot;
+        const float wx = (float)(((R[0] * ix + R[1] * iy) + R[2] * iz) + S.pos[0]);
+        const float wy = (float)(((R[3] * ix + R[4] * iy) + R[5] * iz) + S.pos[1]);
+        const float wz = (float)(((R[6] * ix + R[7] * iy) + R[8] * iz) + S.pos[2]);
+        if (P.dbg.world) {
+            P.dbg.world[3 * i + 0] = wx;
+            P.dbg.world[3 * i + 1] = wy;
+            P.dbg.world[3 * i + 2] = wz;
+        }
+        const int n = job.n;
+        float nx[kNN], ny[kNN], nz[kNN];
+        int cnt;
+        bool sel;
+        if (search) {
+            Cands c;
+            knn_search(P.nodes, P.has_map, wx, wy, wz, stack + tid, kBlock, c, visits);
+            cnt = c.n;
+#pragma unroll
+            for (int k = 0; k < kNN; k++) {
+                if (k < cnt) {
+                    const float4 a = rec_ptr(P.nodes, c.node[k])[0];
+                    nx[k] = a.x; ny[k] = a.y; nz[k] = a.z;
+                    job.nn_idx[k * n + i] = (int32_t)(__float_as_uint(a.w) & kIdxMask);
+                    job.nn_d[k * n + i] = c.d[k];
+                } else {
+                    nx[k] = ny[k] = nz[k] = 0.0f;
+                    job.nn_idx[k * n + i] = -1;
+                    job.nn_d[k * n + i] = INFINITY;
+                }
+                job.nn_xyz[(3 * k + 0) * n + i] = nx[k];
+                job.nn_xyz[(3 * k + 1) * n + i] = ny[k];
+                job.nn_xyz[(3 * k + 2) * n + i] = nz[k];
+            }
+            job.nn_cnt[i] = cnt;
+            // point_selected_surf[i] = sqdis[4] > 5 ? false : true  (laser_mapping.cpp:518)
+            sel = (cnt == kNN) && !(c.d[kNN - 1] > P.max_sqd);
+        } else {
+            cnt = job.nn_cnt[i];
+#pragma unroll
+            for (int k = 0; k < kNN; k++) {
+                nx[k] = job.nn_xyz[(3 * k + 0) * n + i];
+                ny[k] = job.nn_xyz[(3 * k + 1) * n + i];
+                nz[k] = job.nn_xyz[(3 * k + 2) * n + i];
+            }
+            sel = true;  // point_selected_surf re-initialised each call (:490)
+        }
+        bool accepted = false, keep = false;
+        float pa[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        float pd2 = 0.0f;
+        if (sel && cnt >= kNN) {
+            if (esti_plane(nx, ny, nz, P.plane_thr, pa)) {
+                pd2 = ((pa[0] * wx + pa[1] * wy) + pa[2] * wz) + pa[3];
+                const double bn = sqrt((bx * bx + by * by) + bz * bz);
+                const float s = (float)(1 - 0.9 * (double)fabsf(pd2) / sqrt(bn));
+                accepted = (double)s > 0.9;                          // :535-542
+                keep = accepted && (double)fabsf(pd2) <= P.max_res;  // :552
+            }
+        }
+        if (P.dbg.normvec)
+            reinterpret_cast<float4*>(P.dbg.normvec)[i] =
+                accepted ? make_float4(pa[0], pa[1], pa[2], pd2) : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (P.dbg.sel) P.dbg.sel[i] = keep ? 1 : 0;
+        if (keep) {
+            // Jacobian row (laser_mapping.cpp:564-593): p_I = R_LI p_b + t_LI;
+            // A = [p_I]x * rot^T * n;  Hsub = [A, n]
+            const double cr[9] = {0.0, -iz, iy, iz, 0.0, -ix, -iy, ix, 0.0};
+            double M[9];
+#pragma unroll
+            for (int r = 0; r < 3; r++)
+#pragma unroll
+                for (int cI = 0; cI < 3; cI++)
+                    M[r * 3 + cI] = (cr[r * 3 + 0] * R[cI * 3 + 0] + cr[r * 3 + 1] * R[cI * 3 + 1]) +
+                                    cr[r * 3 + 2] * R[cI * 3 + 2];
+            const double n0 = pa[0], n1 = pa[1], n2 = pa[2];
+            double H[6];
+            H[0] = (M[0] * n0 + M[1] * n1) + M[2] * n2;
+            H[1] = (M[3] * n0 + M[4] * n1) + M[5] * n2;
+            H[2] = (M[6] * n0 + M[7] * n1) + M[8] * n2;
+            H[3] = n0; H[4] = n1; H[5] = n2;
+            const double err = -(double)pd2;
+            int q = 0;
+#pragma unroll
+            for (int r = 0; r < 6; r++) {
+                const double hs = H[r] * P.inv_r;
+#pragma unroll
+                for (int cI = r; cI < 6; cI++) acc[q++] = hs * H[cI];
+            }
+#pragma unroll
+            for (int r = 0; r < 6; r++) acc[21 + r] = (H[r] * P.inv_r) * err;
+            acc[27] = (double)fabsf(pd2);
+            acc[28] = 1.0;
+        }
+    }
+    // block reduction: wave shuffle tree, then waves in order
+    const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+    for (int j = 0; j < kRedUsed; j++) {
+        const double v = wave_sum(acc[j]);
+        if (lane == 0) red_lds[wave * kRedCols + j] = v;
+    }
+    unsigned long long wv = visits;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) wv += __shfl_xor(wv, off, 64);
+    __syncthreads();
+    if (tid < kRedUsed) {
+        const double v = ((red_lds[0 * kRedCols + tid] + red_lds[1 * kRedCols + tid]) + red_lds[2 * kRedCols + tid]) +
+                         red_lds[3 * kRedCols + tid];
+        job.partial[(size_t)blockIdx.x * kRedCols + tid] = v;
+    }
+    if (search && lane == 0 && wv) {
+        int e = P.force >= 0 ? 0 : slot->ctrl.n_evals;
+        e = e < LIVO_MAX_EVALS ? e : LIVO_MAX_EVALS - 1;
+        atomicAdd(&slot->visits[e], wv);
+    }
+}
+
+// ========================================================== solve =========
+// 18x18 LU with partial pivoting in LDS (PartialPivLU semantics, as the
+// oracle) and inverse by forward/back substitution, one column per thread.
+__device__ void lds_inverse18(double* A /*18x18, destroyed*/, double* Inv, int* piv, int* pivsel) {
+    const int tid = threadIdx.x;
+    if (tid < kDim) piv[tid] = tid;
+    __syncthreads();
+    for (int k = 0; k < kDim; k++) {
+        if (tid == 0) {
+            int p = k;
+            double best = fabs(A[k * kDim + k]);
+            for (int i = k + 1; i < kDim; i++) {
+                const double v = fabs(A[i * kDim + k]);
+                if (v > best) { best = v; p = i; }
+            }
+            *pivsel = p;
+        }
+        __syncthreads();
+        const int p = *pivsel;
+        if (p != k) {
+            if (tid < kDim) {
+                const double t = A[k * kDim + tid];
+                A[k * kDim + tid] = A[p * kDim + tid];
+                A[p * kDim + tid] = t;
+            }
+            if (tid == 0) {
+                const int t = piv[k]; piv[k] = piv[p]; piv[p] = t;
+            }
+        }
+        __syncthreads();
+        const double d = A[k * kDim + k];
+        const int rows = kDim - 1 - k, cols = kDim - k;
+        double nv0 = 0.0, nv1 = 0.0;
+        int e0 = tid, e1 = tid + blockDim.x;
+        const int ne = rows * cols;
+        if (e0 < ne) {
+            const int i = k + 1 + e0 / cols, j = k + e0 % cols;
+            const double f = A[i * kDim + k] / d;
+            nv0 = (j == k) ? f : A[i * kDim + j] - f * A[k * kDim + j];
+        }
+        if (e1 < ne) {
+            const int i = k + 1 + e1 / cols, j = k + e1 % cols;
+            const double f = A[i * kDim + k] / d;
+            nv1 = (j == k) ? f : A[i * kDim + j] - f * A[k * kDim + j];
+        }
+        __syncthreads();
+        if (e0 < ne) A[(k + 1 + e0 / cols) * kDim + k + e0 % cols] = nv0;
+        if (e1 < ne) A[(k + 1 + e1 / cols) * kDim + k + e1 % cols] = nv1;
+        __syncthreads();
+    }
+    if (tid < kDim) {
+        const int c = tid;
+        double y[kDim];
+#pragma unroll
+        for (int i = 0; i < kDim; i++) {
+            double s = (piv[i] == c) ? 1.0 : 0.0;
+#pragma unroll
+            for (int j = 0; j < i; j++) s = s - A[i * kDim + j] * y[j];
+            y[i] = s;
+        }
+#pragma unroll
+        for (int i = kDim - 1; i >= 0; i--) {
+            double s = y[i];
+#pragma unroll
+            for (int j = i + 1; j < kDim; j++) s = s - A[i * kDim + j] * y[j];
+            y[i] = s / A[i * kDim + i];
+        }
+#pragma unroll
+        for (int i = 0; i < kDim; i++) Inv[i * kDim + c] = y[i];
+    }
+    __syncthreads();
+}
+
+__device__ void so3_exp(double v1, double v2, double v3, double* R) {
+    const double norm = sqrt(v1 * v1 + v2 * v2 + v3 * v3);
+    for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0) ? 1.0 : 0.0;
+    if (norm > 0.00001) {
+        const double r[3] = {v1 / norm, v2 / norm, v3 / norm};
+        const double K[9] = {0.0, -r[2], r[1], r[2], 0.0, -r[0], -r[1], r[0], 0.0};
+        const double s = sin(norm), c1 = 1.0 - cos(norm);
+        double cK[9];
+        for (int i = 0; i < 9; i++) cK[i] = c1 * K[i];
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) {
+                const double kk = (cK[i * 3 + 0] * K[0 * 3 + j] + cK[i * 3 + 1] * K[1 * 3 + j]) + cK[i * 3 + 2] * K[2 * 3 + j];
+                R[i * 3 + j] = (R[i * 3 + j] + s * K[i * 3 + j]) + kk;
+            }
+    }
+}
+
+__device__ void so3_log(const double* R, double* o) {
+    const double tr = (R[0] + R[4]) + R[8];
+    const double theta = (tr > 3.0 - 1e-6) ? 0.0 : acos(0.5 * (tr - 1));
+    const double K[3] = {R[7] - R[5], R[2] - R[6], R[3] - R[1]};
+    if (fabs(theta) < 0.001) {
+        for (int i = 0; i < 3; i++) o[i] = 0.5 * K[i];
+    } else {
+        const double f = 0.5 * theta / sin(theta);
+        for (int i = 0; i < 3; i++) o[i] = f * K[i];
+    }
+}
+
+__device__ void mat3_mul(const double* A, const double* B, double* C) {
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+            C[i * 3 + j] = (A[i * 3 + 0] * B[0 * 3 + j] + A[i * 3 + 1] * B[1 * 3 + j]) + A[i * 3 + 2] * B[2 * 3 + j];
+}
+
+__global__ __launch_bounds__(kBlock) void k_solve(SolveParams P) {
+    __shared__ double s_red[8][kRedCols];
+    __shared__ double s_sum[kRedCols];
+    __shared__ double s_A[kDim * kDim];
+    __shared__ double s_Pinv[kDim * kDim];
+    __shared__ double s_K1[kDim * kDim];
+    __shared__ double s_G[kDim * kDim];
+    __shared__ double s_HTH[81];
+    __shared__ double s_HTL[9];
+    __shared__ double s_vec[kDim];
+    __shared__ double s_sol[kDim];
+    __shared__ int s_piv[kDim];
+    __shared__ int s_pivsel;
+    __shared__ int s_stop;
+
+    const HsJob job = P.jobs[blockIdx.x];
+    IekfSlot* slot = job.slot;
+    const int tid = threadIdx.x;
+    if (P.mode == 0 && slot->ctrl.stop) return;
+
+    // 1. deterministic reduction of the block partials: 8 strided partial sums
+    //    per column, then the 8 in order.
+    {
+        const int col = tid & 31, part = tid >> 5;  // 8 parts x 32 columns
+        double s = 0.0;
+        if (col < kRedUsed)
+            for (int b = part; b < job.nblk; b += 8) s += job.partial[(size_t)b * kRedCols + col];
+        s_red[part][col] = s;
+        __syncthreads();
+        if (tid < kRedCols) {
+            double t = s_red[0][tid];
+            for (int p = 1; p < 8; p++) t += s_red[p][tid];
+            s_sum[tid] = t;
+            slot->red[tid] = t;
+        }
+        __syncthreads();
+    }
+    if (P.mode == 1) return;
+
+    // 2. HTH (9x9, GNSS rows/cols 6..8 zero: gnss_en = 0) and HTL
+    if (tid < 81) {
+        const int r = tid / 9, c = tid % 9;
+        double v = 0.0;
+        if (r < 6 && c < 6) {
+            const int a = r < c ? r : c, b = r < c ? c : r;
+            const int q = a * 6 - (a * (a - 1)) / 2 + (b - a);  // upper-tri packed index
+            v = s_sum[q];
+        }
+        s_HTH[tid] = v;
+    }
+    if (tid < 9) s_HTL[tid] = tid < 6 ? s_sum[21 + tid] : 0.0;
+    IekfCtrl ctrl = slot->ctrl;
+    const int e = ctrl.n_evals;
+
+    // 3. P^-1 once per update (state.cov does not change inside the loop)
+    if (e == 0) {
+        for (int t = tid; t < kDim * kDim; t += blockDim.x) s_A[t] = slot->state.cov[t];
+        __syncthreads();
+        lds_inverse18(s_A, s_Pinv, s_piv, &s_pivsel);
+        for (int t = tid; t < kDim * kDim; t += blockDim.x) slot->Pinv[t] = s_Pinv[t];
+    } else {
+        for (int t = tid; t < kDim * kDim; t += blockDim.x) s_Pinv[t] = slot->Pinv[t];
+    }
+    __syncthreads();
+    // 4. K1 = (H_T_H + P^-1)^-1
+    for (int t = tid; t < kDim * kDim; t += blockDim.x) {
+        const int r = t / kDim, c = t % kDim;
+        const double h = (r < 9 && c < 9) ? s_HTH[r * 9 + c] : 0.0;
+        s_A[t] = h + s_Pinv[t];
+    }
+    __syncthreads();
+    lds_inverse18(s_A, s_K1, s_piv, &s_pivsel);
+    // 5. G(:,0:9) = K1(:,0:9) * HTH ; columns 9..17 stay zero
+    for (int t = tid; t < kDim * kDim; t += blockDim.x) {
+        const int i = t / kDim, j = t % kDim;
+        double s = 0.0;
+        if (j < 9) {
+            s = s_K1[i * kDim + 0] * s_HTH[0 * 9 + j];
+            for (int l = 1; l < 9; l++) s = s + s_K1[i * kDim + l] * s_HTH[l * 9 + j];
+        }
+        s_G[t] = s;
+    }
+    // 6. vec = state_propagat - state
+    if (tid == 0) {
+        const livo_state& a = slot->prior;
+        const livo_state& b = slot->state;
+        double bt[9], rd[9];
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) bt[i * 3 + j] = b.rot[j * 3 + i];
+        mat3_mul(bt, a.rot, rd);
+        so3_log(rd, s_vec);
+        for (int i = 0; i < 3; i++) {
+            s_vec[3 + i] = a.pos[i] - b.pos[i];
+            s_vec[6 + i] = a.vel[i] - b.vel[i];
+            s_vec[9 + i] = a.bias_g[i] - b.bias_g[i];
+            s_vec[12 + i] = a.bias_a[i] - b.bias_a[i];
+            s_vec[15 + i] = a.gravity[i] - b.gravity[i];
+        }
+    }
+    __syncthreads();
+    // 7. solution = K1(:,0:9) HTL + vec - G(:,0:9) vec(0:9)
+    if (tid < kDim) {
+        const int i = tid;
+        double a = s_K1[i * kDim + 0] * s_HTL[0];
+        for (int l = 1; l < 9; l++) a = a + s_K1[i * kDim + l] * s_HTL[l];
+        double g = s_G[i * kDim + 0] * s_vec[0];
+        for (int l = 1; l < 9; l++) g = g + s_G[i * kDim + l] * s_vec[l];
+        s_sol[i] = (a + s_vec[i]) - g;
+    }
+    for (int t = tid; t < kDim * kDim; t += blockDim.x) slot->G[t] = s_G[t];
+    __syncthreads();
+    // 8. boxplus, convergence, rematch control (laser_mapping.cpp:204-237)
+    if (tid == 0) {
+        livo_state& st = slot->state;
+        double E[9], Rn[9];
+        so3_exp(s_sol[0], s_sol[1], s_sol[2], E);
+        mat3_mul(st.rot, E, Rn);
+        for (int k = 0; k < 9; k++) st.rot[k] = Rn[k];
+        for (int k = 0; k < 3; k++) {
+            st.pos[k] += s_sol[3 + k];
+            st.vel[k] += s_sol[6 + k];
+            st.bias_g[k] += s_sol[9 + k];
+            st.bias_a[k] += s_sol[12 + k];
+            st.gravity[k] += s_sol[15 + k];
+        }
+        const double rn = sqrt((s_sol[0] * s_sol[0] + s_sol[1] * s_sol[1]) + s_sol[2] * s_sol[2]);
+        const double tn = sqrt((s_sol[3] * s_sol[3] + s_sol[4] * s_sol[4]) + s_sol[5] * s_sol[5]);
+        const bool converged = (rn * 180 / (3.14159265358) < 0.01) && (tn * 100 < 0.015);
+        const int searched = ctrl.search_en;
+        bool next_search = false;
+        if (converged || ((ctrl.rematch_num == 0) && (ctrl.iter_count == (ctrl.max_iter - 2)))) {
+            next_search = true;
+            ctrl.rematch_num++;
+        }
+        const bool stop = (ctrl.rematch_num >= 2 || (ctrl.iter_count == ctrl.max_iter - 1));
+        livo_iter_stats& S = slot->stats;
+        if (e < LIVO_MAX_EVALS) {
+            S.effct_feat_num[e] = (int64_t)s_sum[28];
+            S.res_mean[e] = s_sum[27] / s_sum[28];
+            for (int k = 0; k < kDim; k++) S.solution[e][k] = s_sol[k];
+            slot->eval_search[e] = searched;
+        }
+        S.iterations = e + 1;
+        S.knn_passes += searched ? 1 : 0;
+        S.converged = converged ? 1 : 0;
+        S.rematch_num = ctrl.rematch_num;
+        ctrl.converged = converged ? 1 : 0;
+        ctrl.last_search = searched;
+        ctrl.search_en = next_search ? 1 : 0;
+        ctrl.iter_count++;
+        ctrl.n_evals = e + 1;
+        // the loop condition iterCount < NUM_MAX_ITERATIONS (:178) also ends it
+        ctrl.stop = (stop || ctrl.iter_count >= ctrl.max_iter || ctrl.n_evals >= LIVO_MAX_EVALS) ? 1 : 0;
+        s_stop = stop ? 1 : 0;
+        slot->ctrl = ctrl;
+    }
+    __syncthreads();
+    // 9. covariance update state.cov = (I - G) * state.cov (:224-227)
+    if (s_stop) {
+        for (int t = tid; t < kDim * kDim; t += blockDim.x) s_A[t] = slot->state.cov[t];
+        __syncthreads();
+        for (int t = tid; t < kDim * kDim; t += blockDim.x) {
+            const int i = t / kDim, j = t % kDim;
+            double s = (((i == 0) ? 1.0 : 0.0) - s_G[i * kDim + 0]) * s_A[0 * kDim + j];
+            for (int l = 1; l < kDim; l++) s = s + (((i == l) ? 1.0 : 0.0) - s_G[i * kDim + l]) * s_A[l * kDim + j];
+            slot->state.cov[t] = s;
+        }
+    }
+}
+
+// ====================================================== standalone kNN ====
+__global__ __launch_bounds__(kBlock) void k_knn(const MapNode* nodes, int has_map, const float* q, int64_t n, int k,
+                                                int32_t* idx, float* dout) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint2* stack = reinterpret_cast<uint2*>(smem);
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    Cands c;
+    unsigned v = 0;
+    knn_search(nodes, has_map, q[3 * i], q[3 * i + 1], q[3 * i + 2], stack + threadIdx.x, kBlock, c, v);
+    for (int j = 0; j < k; j++) {
+        float dj = INFINITY;
+        uint32_t nd = 0;
+#pragma unroll
+        for (int t = 0; t < kNN; t++)
+            if (t == j) { dj = c.d[t]; nd = c.node[t]; }
+        if (j < c.n) {
+            const float4 a = rec_ptr(nodes, nd)[0];
+            idx[i * k + j] = (int32_t)(__float_as_uint(a.w) & kIdxMask);
+            dout[i * k + j] = dj;
+        } else {
+            idx[i * k + j] = -1;
+            dout[i * k + j] = INFINITY;
+        }
+    }
+}
+
+// ======================================================== launchers =======
+static size_t hshare_lds(int depth) {
+    const int d = depth > 0 ? depth : 1;
+    return 4 * kRedCols * sizeof(double) + (size_t)d * kBlock * sizeof(uint2);
+}
+
+int launch_hshare(const HsParams& p, int n_jobs, int max_nblk, int depth, bool first, void* stream) {
+    if (n_jobs <= 0 || max_nblk <= 0) return LIVO_OK;
+    dim3 grid(max_nblk, n_jobs), block(kBlock);
+    const size_t lds = hshare_lds(depth);
+    if (first)
+        hipLaunchKernelGGL(k_hshare<true>, grid, block, lds, (hipStream_t)stream, p);
+    else
+        hipLaunchKernelGGL(k_hshare<false>, grid, block, lds, (hipStream_t)stream, p);
+    return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+
+int launch_solve(const SolveParams& p, int n_jobs, void* stream) {
+    if (n_jobs <= 0) return LIVO_OK;
+    hipLaunchKernelGGL(k_solve, dim3(n_jobs), dim3(kBlock), 0, (hipStream_t)stream, p);
+    return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+
+int launch_knn(const MapNode* nodes, int has_map, int depth, const float* q, int64_t n, int k, int32_t* idx,
+               float* d, void* stream) {
+    if (n <= 0) return LIVO_OK;
+    const int64_t nblk = (n + kBlock - 1) / kBlock;
+    const size_t lds = (size_t)(depth > 0 ? depth : 1) * kBlock * sizeof(uint2);
+    hipLaunchKernelGGL(k_knn, dim3((unsigned)nblk), dim3(kBlock), lds, (hipStream_t)stream, nodes, has_map, q, n, k,
+                       idx, d);
+    return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+
+}  // namespace livo

@@ -1,0 +1,158 @@
+// map_build.cpp — host construction of the device map (heap-ordered 64-B records).
+//
+// Same tree as KD_TREE::Build (include/ikd-Tree/ikd_Tree.cpp:337-348) on the
+// same input order: BuildTree (:537-602) picks the axis of largest extent over
+// Storage[l..r], nth_element-partitions at mid = (l+r)>>1 and recurses on
+// [l, mid-1] and [mid+1, r]; Update (:1110-1235) derives each node's bounding
+// box from its sons and its point.  We run the same std::nth_element on the
+// same element sequence, so the partition of points with equal coordinates
+// matches the reference as well.  Instead of 176-B pointer nodes the result is
+// written as heap-ordered MapNode records (livo_internal.h), each holding its
+// point and its two sons' boxes.  Disjoint subtrees are built on separate
+// threads (the result does not depend on the thread count).
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "livo_internal.h"
+
+namespace livo {
+namespace {
+
+struct BPoint {
+    float x, y, z;
+    uint32_t idx;
+};
+
+struct Box {
+    float mn[3], mx[3];
+    bool valid;
+};
+
+static bool cmp_x(const BPoint& a, const BPoint& b) { return a.x < b.x; }
+static bool cmp_y(const BPoint& a, const BPoint& b) { return a.y < b.y; }
+static bool cmp_z(const BPoint& a, const BPoint& b) { return a.z < b.z; }
+
+static int tree_depth(int64_t n) {
+    int d = 0;
+    while (n > 0) {  // larger half of [l, r] after removing mid has ceil((n-1)/2) points
+        d++;
+        n = n - 1 - ((n - 1) >> 1);
+    }
+    return d;
+}
+
+struct Builder {
+    std::vector<BPoint>& st;
+    MapNode* nodes;
+
+    Box build(int64_t l, int64_t r, int64_t h, int spawn_levels) {
+        Box out{};
+        if (l > r) {
+            out.valid = false;
+            return out;
+        }
+        int64_t mid = (l + r) >> 1;
+        float mn[3] = {INFINITY, INFINITY, INFINITY};
+        float mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int64_t i = l; i <= r; i++) {
+            mn[0] = std::min(mn[0], st[i].x); mn[1] = std::min(mn[1], st[i].y); mn[2] = std::min(mn[2], st[i].z);
+            mx[0] = std::max(mx[0], st[i].x); mx[1] = std::max(mx[1], st[i].y); mx[2] = std::max(mx[2], st[i].z);
+        }
+        float ext[3] = {mx[0] - mn[0], mx[1] - mn[1], mx[2] - mn[2]};
+        int axis = 0;
+        for (int i = 1; i < 3; i++)
+            if (ext[i] > ext[axis]) axis = i;
+        auto b = st.begin();
+        if (axis == 1) std::nth_element(b + l, b + mid, b + r + 1, cmp_y);
+        else if (axis == 2) std::nth_element(b + l, b + mid, b + r + 1, cmp_z);
+        else std::nth_element(b + l, b + mid, b + r + 1, cmp_x);
+        const BPoint p = st[mid];
+        Box bl, br;
+        if (spawn_levels > 0 && (r - l) > 65536) {
+            std::thread t([&] { bl = build(l, mid - 1, 2 * h + 1, spawn_levels - 1); });
+            br = build(mid + 1, r, 2 * h + 2, spawn_levels - 1);
+            t.join();
+        } else {
+            bl = build(l, mid - 1, 2 * h + 1, 0);
+            br = build(mid + 1, r, 2 * h + 2, 0);
+        }
+        MapNode& nd = nodes[h + 1];
+        uint32_t meta = p.idx | (bl.valid ? kLeftBit : 0u) | (br.valid ? kRightBit : 0u);
+        // An absent son gets an empty box; the kernel never reads it (meta bits).
+        Box el = bl.valid ? bl : Box{{INFINITY, INFINITY, INFINITY}, {-INFINITY, -INFINITY, -INFINITY}, false};
+        Box er = br.valid ? br : Box{{INFINITY, INFINITY, INFINITY}, {-INFINITY, -INFINITY, -INFINITY}, false};
+        float mw;
+        std::memcpy(&mw, &meta, 4);
+        nd.a[0] = p.x; nd.a[1] = p.y; nd.a[2] = p.z; nd.a[3] = mw;
+        nd.b[0] = el.mn[0]; nd.b[1] = el.mx[0]; nd.b[2] = el.mn[1]; nd.b[3] = el.mx[1];
+        nd.c[0] = el.mn[2]; nd.c[1] = el.mx[2]; nd.c[2] = er.mn[0]; nd.c[3] = er.mx[0];
+        nd.d[0] = er.mn[1]; nd.d[1] = er.mx[1]; nd.d[2] = er.mn[2]; nd.d[3] = er.mx[2];
+        // Update(): ikd_Tree.cpp:1110-1235 for a node without deletions.
+        Box o{};
+        o.valid = true;
+        const float pc[3] = {p.x, p.y, p.z};
+        if (bl.valid && br.valid) {
+            for (int k = 0; k < 3; k++) {
+                o.mn[k] = std::min(std::min(bl.mn[k], br.mn[k]), pc[k]);
+                o.mx[k] = std::max(std::max(bl.mx[k], br.mx[k]), pc[k]);
+            }
+        } else if (bl.valid || br.valid) {
+            const Box& s = bl.valid ? bl : br;
+            for (int k = 0; k < 3; k++) {
+                o.mn[k] = std::min(s.mn[k], pc[k]);
+                o.mx[k] = std::max(s.mx[k], pc[k]);
+            }
+        } else {
+            for (int k = 0; k < 3; k++) o.mn[k] = o.mx[k] = pc[k];
+        }
+        return o;
+    }
+};
+
+}  // namespace
+
+int build_host_map(const float* xyz, int64_t M, int64_t stride_bytes, HostMap* out) {
+    if (!out || M < 0 || (M > 0 && !xyz)) return LIVO_E_INVALID;
+    if (M > kMaxMapPoints) return LIVO_E_RANGE;
+    if (stride_bytes == 0) stride_bytes = 3 * sizeof(float);
+    if (stride_bytes < (int64_t)(3 * sizeof(float))) return LIVO_E_INVALID;
+    free_host_map(out);
+    int depth = tree_depth(M);
+    if (depth > kMaxDepth) return LIVO_E_RANGE;
+    int64_t slots = depth > 0 ? ((int64_t)1 << depth) - 1 : 0;
+    size_t bytes = (size_t)(slots + 1) * sizeof(MapNode);
+    MapNode* nodes = (MapNode*)std::calloc(slots + 1, sizeof(MapNode));
+    if (!nodes) return LIVO_E_OOM;
+    (void)bytes;
+    std::vector<BPoint> st((size_t)M);
+    const char* base = (const char*)xyz;
+    for (int64_t i = 0; i < M; i++) {
+        const float* p = (const float*)(base + i * stride_bytes);
+        st[i] = BPoint{p[0], p[1], p[2], (uint32_t)i};
+    }
+    if (M > 0) {
+        Builder b{st, nodes};
+        unsigned hw = std::thread::hardware_concurrency();
+        int spawn = 0;
+        while ((1u << spawn) < std::min(hw ? hw : 1u, 16u)) spawn++;
+        b.build(0, M - 1, 0, spawn);
+    }
+    out->nodes = nodes;
+    out->num_points = M;
+    out->num_slots = slots;
+    out->depth = depth;
+    return LIVO_OK;
+}
+
+void free_host_map(HostMap* m) {
+    if (m && m->nodes) {
+        std::free(m->nodes);
+        m->nodes = nullptr;
+    }
+}
+
+}  // namespace livo

@@ -1,0 +1,293 @@
+"""livo_amd — Python binding of the MI355X LIO scan-to-map C ABI (include/livo.h).
+
+A thin ctypes layer over fast-livo-noted_amd/lib/liblivo_hip.so used by the
+tests, smoke() and bench.py.  It mirrors the reference call surface for this
+path:
+
+    KD_TREE::Build / Nearest_Search      -> Context.map_build / Context.knn
+    LaserMapping::h_share_model          -> Context.h_share
+    IEKF loop of LaserMapping::Run       -> Context.iekf_update(_batch)
+
+There is no CPU fallback: loading fails loudly if the HIP library is missing,
+and every compute call raises LivoError when the GPU path fails.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "liblivo_hip.so")
+HEADER_PATH = os.path.join(os.path.dirname(PKG_ROOT), "include", "livo.h")
+
+DIM_STATE = 18
+NUM_MATCH_POINTS = 5
+MAX_EVALS = 16
+
+LIVO_OK = 0
+ERRORS = {-1: "LIVO_E_INVALID", -2: "LIVO_E_HIP", -3: "LIVO_E_NOMAP", -4: "LIVO_E_NOSCAN", -5: "LIVO_E_OOM",
+          -6: "LIVO_E_RANGE"}
+
+
+class LivoError(RuntimeError):
+    def __init__(self, fn, code):
+        self.code = code
+        super().__init__(f"{fn} failed: {ERRORS.get(code, code)} ({code})")
+
+
+class Params(C.Structure):
+    _fields_ = [("laser_point_cov", C.c_double), ("R_LI", C.c_double * 9), ("t_LI", C.c_double * 3),
+                ("max_residual", C.c_double), ("plane_threshold", C.c_float), ("max_nn_sqdist", C.c_float),
+                ("max_iterations", C.c_int32), ("flags", C.c_int32)]
+
+
+class State(C.Structure):
+    _fields_ = [("rot", C.c_double * 9), ("pos", C.c_double * 3), ("vel", C.c_double * 3),
+                ("bias_g", C.c_double * 3), ("bias_a", C.c_double * 3), ("gravity", C.c_double * 3),
+                ("cov", C.c_double * 324)]
+
+
+class IterStats(C.Structure):
+    _fields_ = [("iterations", C.c_int32), ("knn_passes", C.c_int32), ("converged", C.c_int32),
+                ("rematch_num", C.c_int32), ("effct_feat_num", C.c_int64 * MAX_EVALS),
+                ("solution", (C.c_double * 18) * MAX_EVALS), ("res_mean", C.c_double * MAX_EVALS)]
+
+
+class MapInfo(C.Structure):
+    _fields_ = [("num_points", C.c_int64), ("depth", C.c_int32), ("reserved", C.c_int32),
+                ("num_slots", C.c_int64), ("device_bytes", C.c_int64)]
+
+
+class PointOut(C.Structure):
+    _fields_ = [("normvec", C.c_void_p), ("selected", C.c_void_p), ("nn_idx", C.c_void_p),
+                ("nn_sqdist", C.c_void_p), ("world_xyz", C.c_void_p), ("visits", C.c_void_p)]
+
+
+class Timings(C.Structure):
+    _fields_ = [("knn_ms", C.c_double), ("plane_ms", C.c_double), ("solve_ms", C.c_double),
+                ("knn_launches", C.c_int64), ("knn_visits", C.c_int64), ("knn_queries", C.c_int64),
+                ("effct_points", C.c_int64)]
+
+
+# every entry point of include/livo.h, with its ctypes signature
+_P = C.c_void_p
+SIGNATURES = {
+    "livo_abi_version": (C.c_int, []),
+    "livo_error_string": (C.c_char_p, [C.c_int]),
+    "livo_params_default": (C.c_int, [C.POINTER(Params)]),
+    "livo_ctx_create": (C.c_int, [C.c_int, C.POINTER(Params), C.POINTER(_P)]),
+    "livo_ctx_destroy": (C.c_int, [_P]),
+    "livo_ctx_set_params": (C.c_int, [_P, C.POINTER(Params)]),
+    "livo_ctx_set_profiling": (C.c_int, [_P, C.c_int]),
+    "livo_last_timings": (C.c_int, [_P, C.POINTER(Timings)]),
+    "livo_map_build": (C.c_int, [_P, _P, C.c_int64, C.c_int64]),
+    "livo_map_get_info": (C.c_int, [_P, C.POINTER(MapInfo)]),
+    "livo_knn": (C.c_int, [_P, _P, C.c_int64, C.c_int32, _P, _P]),
+    "livo_scan_upload": (C.c_int, [_P, _P, C.c_int64, C.c_int64, C.POINTER(C.c_int32)]),
+    "livo_scan_release": (C.c_int, [_P, C.c_int32]),
+    "livo_h_share": (C.c_int, [_P, C.c_int32, C.POINTER(State), C.c_int, _P, _P, C.POINTER(C.c_int64),
+                               C.POINTER(PointOut)]),
+    "livo_iekf_update": (C.c_int, [_P, C.c_int32, C.POINTER(State), C.POINTER(State), C.POINTER(IterStats)]),
+    "livo_iekf_update_batch": (C.c_int, [_P, C.c_int32, _P, _P, _P, _P]),
+    "livo_sync": (C.c_int, [_P]),
+}
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load liblivo_hip.so (raises if it was not built: there is no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(path):
+            raise ImportError(f"HIP library not built: {path} (run __graft_entry__.build())")
+        L = C.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(fn, rc):
+    if rc != LIVO_OK:
+        raise LivoError(fn, rc)
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def default_params(**kw) -> Params:
+    p = Params()
+    _check("livo_params_default", load().livo_params_default(C.byref(p)))
+    for k, v in kw.items():
+        if k in ("R_LI",):
+            p.R_LI[:] = np.asarray(v, np.float64).reshape(9).tolist()
+        elif k == "t_LI":
+            p.t_LI[:] = np.asarray(v, np.float64).reshape(3).tolist()
+        else:
+            setattr(p, k, v)
+    return p
+
+
+def state_to_c(st: dict) -> State:
+    s = State()
+    s.rot[:] = np.asarray(st["rot"], np.float64).reshape(9).tolist()
+    for k in ("pos", "vel", "bias_g", "bias_a", "gravity"):
+        getattr(s, k)[:] = np.asarray(st[k], np.float64).reshape(3).tolist()
+    s.cov[:] = np.asarray(st["cov"], np.float64).reshape(324).tolist()
+    return s
+
+
+def state_from_c(s: State) -> dict:
+    return {"rot": np.array(s.rot[:]).reshape(3, 3), "pos": np.array(s.pos[:]), "vel": np.array(s.vel[:]),
+            "bias_g": np.array(s.bias_g[:]), "bias_a": np.array(s.bias_a[:]),
+            "gravity": np.array(s.gravity[:]), "cov": np.array(s.cov[:]).reshape(18, 18)}
+
+
+def stats_from_c(st: IterStats) -> dict:
+    ne = min(st.iterations, MAX_EVALS)
+    return {"iterations": st.iterations, "knn_passes": st.knn_passes, "converged": st.converged,
+            "rematch_num": st.rematch_num, "effct_feat_num": [st.effct_feat_num[i] for i in range(ne)],
+            "solution": np.array([list(st.solution[i]) for i in range(ne)]).reshape(ne, 18),
+            "res_mean": [st.res_mean[i] for i in range(ne)]}
+
+
+class Context:
+    """One livo_ctx: a HIP stream, the device map and resident scans on one GPU."""
+
+    def __init__(self, device: int = 0, params: Params | None = None, **kw):
+        L = load()
+        self._L = L
+        self.params = params if params is not None else default_params(**kw)
+        h = C.c_void_p()
+        _check("livo_ctx_create", L.livo_ctx_create(device, C.byref(self.params), C.byref(h)))
+        self.h = h
+        self.scans = {}
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.livo_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def set_params(self, **kw):
+        for k, v in kw.items():
+            if k == "R_LI":
+                self.params.R_LI[:] = np.asarray(v, np.float64).reshape(9).tolist()
+            elif k == "t_LI":
+                self.params.t_LI[:] = np.asarray(v, np.float64).reshape(3).tolist()
+            else:
+                setattr(self.params, k, v)
+        _check("livo_ctx_set_params", self._L.livo_ctx_set_params(self.h, C.byref(self.params)))
+
+    # ------------------------------------------------------------ map ----
+    def map_build(self, xyz: np.ndarray):
+        xyz = np.ascontiguousarray(xyz, np.float32)
+        assert xyz.ndim == 2 and xyz.shape[1] >= 3
+        _check("livo_map_build", self._L.livo_map_build(self.h, _ptr(xyz), xyz.shape[0], xyz.shape[1] * 4))
+
+    def map_info(self) -> dict:
+        mi = MapInfo()
+        _check("livo_map_get_info", self._L.livo_map_get_info(self.h, C.byref(mi)))
+        return {"num_points": mi.num_points, "depth": mi.depth, "num_slots": mi.num_slots,
+                "device_bytes": mi.device_bytes}
+
+    def knn(self, q: np.ndarray, k: int = 5):
+        q = np.ascontiguousarray(q, np.float32).reshape(-1, 3)
+        n = q.shape[0]
+        idx = np.empty((n, k), np.int32)
+        d = np.empty((n, k), np.float32)
+        _check("livo_knn", self._L.livo_knn(self.h, _ptr(q), n, k, _ptr(idx), _ptr(d)))
+        return idx, d
+
+    # ---------------------------------------------------------- scans ----
+    def scan_upload(self, xyz: np.ndarray) -> int:
+        xyz = np.ascontiguousarray(xyz, np.float32)
+        assert xyz.ndim == 2 and xyz.shape[1] >= 3
+        sid = C.c_int32()
+        _check("livo_scan_upload", self._L.livo_scan_upload(self.h, _ptr(xyz), xyz.shape[0], xyz.shape[1] * 4,
+                                                            C.byref(sid)))
+        self.scans[sid.value] = xyz.shape[0]
+        return sid.value
+
+    def scan_release(self, sid: int):
+        _check("livo_scan_release", self._L.livo_scan_release(self.h, sid))
+        self.scans.pop(sid, None)
+
+    # -------------------------------------------------------- hot path ----
+    def h_share(self, sid: int, state: dict, search_en: bool = True, outputs: bool = True):
+        n = self.scans[sid]
+        HTH = np.zeros(81)
+        HTL = np.zeros(9)
+        eff = C.c_int64()
+        po = None
+        res = {}
+        if outputs:
+            res = {"normvec": np.zeros((n, 4), np.float32), "sel": np.zeros(n, np.uint8),
+                   "nn_idx": np.zeros((n, 5), np.int32), "nn_d": np.zeros((n, 5), np.float32),
+                   "world": np.zeros((n, 3), np.float32), "visits": np.zeros(1, np.int64)}
+            po = PointOut(_ptr(res["normvec"]), _ptr(res["sel"]), _ptr(res["nn_idx"]), _ptr(res["nn_d"]),
+                          _ptr(res["world"]), _ptr(res["visits"]))
+        st = state_to_c(state)
+        _check("livo_h_share", self._L.livo_h_share(self.h, sid, C.byref(st), int(bool(search_en)), _ptr(HTH),
+                                                    _ptr(HTL), C.byref(eff), C.byref(po) if po else None))
+        res.update({"HTH": HTH.reshape(9, 9), "HTL": HTL, "effct": eff.value})
+        if outputs:
+            res["visits"] = int(res["visits"][0])
+        return res
+
+    def iekf_update(self, sid: int, state: dict, prior: dict | None = None):
+        st = state_to_c(state)
+        pr = state_to_c(prior) if prior is not None else None
+        stats = IterStats()
+        _check("livo_iekf_update", self._L.livo_iekf_update(self.h, sid, C.byref(st),
+                                                            C.byref(pr) if pr is not None else None,
+                                                            C.byref(stats)))
+        return state_from_c(st), stats_from_c(stats)
+
+    def iekf_update_batch(self, sids, states, priors=None, raw: bool = False):
+        n = len(sids)
+        ids = (C.c_int32 * n)(*sids)
+        if raw:  # states is already a ctypes State array (bench hot loop)
+            sts = states
+        else:
+            sts = (State * n)(*[state_to_c(s) for s in states])
+        prs = None
+        if priors is not None:
+            prs = priors if raw else (State * n)(*[state_to_c(s) for s in priors])
+        stats = (IterStats * n)()
+        _check("livo_iekf_update_batch",
+               self._L.livo_iekf_update_batch(self.h, n, C.cast(ids, C.c_void_p), C.cast(sts, C.c_void_p),
+                                              C.cast(prs, C.c_void_p) if prs is not None else None,
+                                              C.cast(stats, C.c_void_p)))
+        if raw:
+            return sts, stats
+        return [state_from_c(s) for s in sts], [stats_from_c(s) for s in stats]
+
+    def set_profiling(self, on: bool):
+        _check("livo_ctx_set_profiling", self._L.livo_ctx_set_profiling(self.h, int(bool(on))))
+
+    def last_timings(self) -> dict:
+        t = Timings()
+        _check("livo_last_timings", self._L.livo_last_timings(self.h, C.byref(t)))
+        return {f: getattr(t, f) for f, _ in Timings._fields_}
+
+    def sync(self):
+        _check("livo_sync", self._L.livo_sync(self.h))

@@ -1,0 +1,234 @@
+"""Deterministic synthetic inputs for the LIO scan-to-map path.
+
+The reference ships no bags, fixtures or golden vectors, so every
+workload here is generated from fixed seeds:
+
+* scene   — planar room (ground z=-1.6, ceiling z=2.4, four walls of a 60x40 m
+            box) plus 20 axis-aligned boxes, seed 0x5EED0001.  The world
+            origin is the sensor's start position, as in the reference (the
+            first scan defines the map frame), and no surface plane passes
+            within 0.5 m of it: esti_plane's A x = -1 formulation
+            (common_lib.h:670-702) cannot represent a plane through the origin;
+* map     — points sampled area-weighted on every surface with N(0, 0.01 m)
+            noise along the surface normal, exact duplicates removed,
+            seed 0x5EED0002;
+* scan    — a Livox-Avia-shaped rosette (70.4 x 77.2 deg FoV, 6 emitter
+            lines, `config/avia_resize.yaml:25`) ray-cast into the scene with
+            N(0, 0.02 m) range noise, kept when x^2+y^2 is in [blind, 900]
+            (`preprocess.cpp:322`), seed 0x5EED0003 + scan_id;
+* state   — true IMU pose perturbed by a rotation in a 1 deg ball and a
+            translation in a 0.1 m ball, seed 0x5EED0004 + scan_id;
+            P = INIT_COV * I18 (`common_lib.h:36,527`).
+
+Body frame = LiDAR frame; extrinsic R_LI = I, t_LI = [0.04165, 0.02326,
+-0.0284] (`config/avia_resize.yaml:31-34`).  Everything is numpy; nothing here
+runs on the GPU.
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+import os
+
+import numpy as np
+
+SEED_SCENE = 0x5EED0001
+SEED_MAP = 0x5EED0002
+SEED_SCAN = 0x5EED0003
+SEED_STATE = 0x5EED0004
+
+ROOM_MIN = np.array([-30.0, -20.0, -1.6])
+ROOM_MAX = np.array([30.0, 20.0, 2.4])
+T_LI = np.array([0.04165, 0.02326, -0.0284])
+R_LI = np.eye(3)
+INIT_COV = 0.001
+DIM_STATE = 18
+
+
+@dataclasses.dataclass
+class Scene:
+    boxes_min: np.ndarray  # (B, 3)
+    boxes_max: np.ndarray  # (B, 3)
+
+
+def make_scene(n_boxes: int = 20, seed: int = SEED_SCENE) -> Scene:
+    rng = np.random.default_rng(seed)
+    mins, maxs = [], []
+    while len(mins) < n_boxes:
+        c = rng.uniform([-26.0, -16.0], [26.0, 16.0])
+        sx, sy = rng.uniform(0.6, 4.0, size=2)
+        top = rng.choice([rng.uniform(-1.1, -0.5), rng.uniform(0.5, 2.0)])
+        lo = np.array([c[0] - sx / 2, c[1] - sy / 2])
+        hi = np.array([c[0] + sx / 2, c[1] + sy / 2])
+        # keep the sensor region clear and every face plane >= 1 m from the origin
+        if np.any((lo < 1.0) & (hi > -1.0)) or np.any(np.abs(np.concatenate([lo, hi])) < 1.0):
+            continue
+        if abs(c[0]) < 5.0 and abs(c[1]) < 5.0:
+            continue
+        mins.append([lo[0], lo[1], ROOM_MIN[2]])
+        maxs.append([hi[0], hi[1], top])
+    return Scene(np.array(mins), np.array(maxs))
+
+
+def _faces(scene: Scene):
+    """(origin, u, v, normal) for every sampled rectangle."""
+    faces = []
+    lo, hi = ROOM_MIN, ROOM_MAX
+    ext = hi - lo
+    e = np.eye(3)
+    # room: floor, ceiling, 4 walls
+    faces.append((lo.copy(), e[0] * ext[0], e[1] * ext[1], e[2]))
+    faces.append((np.array([lo[0], lo[1], hi[2]]), e[0] * ext[0], e[1] * ext[1], e[2]))
+    faces.append((lo.copy(), e[1] * ext[1], e[2] * ext[2], e[0]))
+    faces.append((np.array([hi[0], lo[1], lo[2]]), e[1] * ext[1], e[2] * ext[2], e[0]))
+    faces.append((lo.copy(), e[0] * ext[0], e[2] * ext[2], e[1]))
+    faces.append((np.array([lo[0], hi[1], lo[2]]), e[0] * ext[0], e[2] * ext[2], e[1]))
+    for bmin, bmax in zip(scene.boxes_min, scene.boxes_max):
+        d = bmax - bmin
+        faces.append((np.array([bmin[0], bmin[1], bmax[2]]), e[0] * d[0], e[1] * d[1], e[2]))
+        faces.append((bmin.copy(), e[1] * d[1], e[2] * d[2], e[0]))
+        faces.append((np.array([bmax[0], bmin[1], bmin[2]]), e[1] * d[1], e[2] * d[2], e[0]))
+        faces.append((bmin.copy(), e[0] * d[0], e[2] * d[2], e[1]))
+        faces.append((np.array([bmin[0], bmax[1], bmin[2]]), e[0] * d[0], e[2] * d[2], e[1]))
+    return faces
+
+
+def make_map(n_points: int, scene: Scene | None = None, seed: int = SEED_MAP,
+             noise: float = 0.01) -> np.ndarray:
+    """(M, 3) float32 map points, area-weighted on every scene surface."""
+    scene = scene or make_scene()
+    faces = _faces(scene)
+    areas = np.array([np.linalg.norm(np.cross(u, v)) for _, u, v, _ in faces])
+    rng = np.random.default_rng(seed)
+    out = np.empty((0, 3), np.float32)
+    need = n_points
+    while need > 0:
+        m = int(need * 1.02) + 16
+        fidx = rng.choice(len(faces), size=m, p=areas / areas.sum())
+        a = rng.random(m)
+        b = rng.random(m)
+        nz = rng.normal(0.0, noise, size=m)
+        O = np.stack([faces[i][0] for i in range(len(faces))])
+        U = np.stack([faces[i][1] for i in range(len(faces))])
+        V = np.stack([faces[i][2] for i in range(len(faces))])
+        Nn = np.stack([faces[i][3] for i in range(len(faces))])
+        pts = O[fidx] + a[:, None] * U[fidx] + b[:, None] * V[fidx] + nz[:, None] * Nn[fidx]
+        out = np.concatenate([out, pts.astype(np.float32)])
+        # remove exact duplicates, keep first occurrence order
+        _, first = np.unique(out, axis=0, return_index=True)
+        out = out[np.sort(first)]
+        need = n_points - len(out)
+    return np.ascontiguousarray(out[:n_points])
+
+
+def so3_exp(w: np.ndarray) -> np.ndarray:
+    th = float(np.linalg.norm(w))
+    if th < 1e-12:
+        return np.eye(3)
+    k = w / th
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + math.sin(th) * K + (1 - math.cos(th)) * K @ K
+
+
+def _ball(rng, radius):
+    v = rng.normal(size=3)
+    v /= np.linalg.norm(v)
+    return v * radius * rng.random() ** (1.0 / 3.0)
+
+
+def true_pose(scan_id: int):
+    rng = np.random.default_rng(SEED_SCAN + scan_id)
+    yaw = rng.uniform(0, 2 * math.pi)
+    roll, pitch = rng.uniform(-math.radians(5), math.radians(5), size=2)
+    R = so3_exp(np.array([0, 0, yaw])) @ so3_exp(np.array([0, pitch, 0])) @ so3_exp(np.array([roll, 0, 0]))
+    p = np.array([rng.uniform(-0.4, 0.4), rng.uniform(-0.4, 0.4), rng.uniform(-0.2, 0.2)])
+    return R, p, rng
+
+
+def _rosette_dirs(n, rng):
+    """Livox-Avia-like non-repetitive rosette directions in the LiDAR frame (+x forward)."""
+    half_h, half_v = math.radians(70.4) / 2, math.radians(77.2) / 2
+    line = np.arange(n) % 6
+    t = np.sort(rng.uniform(0, 0.1, size=n))  # 100 ms frame
+    w1, w2 = 2 * math.pi * 1300.0, 2 * math.pi * 1873.0  # incommensurate rates
+    phase = line * (math.pi / 3.0) + rng.normal(0, 0.002, size=n)
+    rho = np.abs(np.sin(w2 * t + line * 0.37))
+    phi = w1 * t + phase
+    az = half_h * rho * np.cos(phi)
+    el = half_v * rho * np.sin(phi)
+    d = np.stack([np.cos(el) * np.cos(az), np.cos(el) * np.sin(az), np.sin(el)], axis=1)
+    return d, t
+
+
+def _raycast(o, d, scene: Scene):
+    """Range along unit rays d from origin o to the first surface (room is a closed box)."""
+    with np.errstate(divide="ignore", invalid="ignore"):
+        inv = 1.0 / d
+        t1 = (ROOM_MIN - o) * inv
+        t2 = (ROOM_MAX - o) * inv
+        tmax = np.where(inv > 0, t2, t1)
+        t = np.nanmin(np.where(np.isfinite(tmax), tmax, np.inf), axis=1)
+        for bmin, bmax in zip(scene.boxes_min, scene.boxes_max):
+            a = (bmin - o) * inv
+            b = (bmax - o) * inv
+            tn = np.nanmax(np.where(np.isfinite(np.minimum(a, b)), np.minimum(a, b), -np.inf), axis=1)
+            tf = np.nanmin(np.where(np.isfinite(np.maximum(a, b)), np.maximum(a, b), np.inf), axis=1)
+            hit = (tn <= tf) & (tn > 1e-6)
+            t = np.where(hit & (tn < t), tn, t)
+    return t
+
+
+def make_scan(n_points: int, scan_id: int = 0, scene: Scene | None = None,
+              range_noise: float = 0.02, blind: float = 0.8):
+    """(N, 3) float32 body-frame (= LiDAR-frame) points + ground-truth IMU pose."""
+    scene = scene or make_scene()
+    R, p, rng = true_pose(scan_id)
+    R_wl = R @ R_LI
+    o_l = R @ T_LI + p
+    pts = np.empty((0, 3))
+    while len(pts) < n_points:
+        m = int((n_points - len(pts)) * 1.3) + 64
+        d_l, _ = _rosette_dirs(m, rng)
+        d_w = d_l @ R_wl.T
+        r = _raycast(o_l, d_w, scene) + rng.normal(0, range_noise, size=m)
+        q = r[:, None] * d_l
+        rr = q[:, 0] ** 2 + q[:, 1] ** 2
+        keep = np.isfinite(r) & (rr >= blind) & (rr <= 900.0)
+        pts = np.concatenate([pts, q[keep]])
+    return np.ascontiguousarray(pts[:n_points].astype(np.float32)), R, p
+
+
+def make_state(scan_id: int = 0, rot_deg: float = 1.0, trans_m: float = 0.1):
+    """Initial IEKF state (dict of float64 arrays) = truth perturbed, P = 0.001 I."""
+    R, p, _ = true_pose(scan_id)
+    rng = np.random.default_rng(SEED_STATE + scan_id)
+    dth = _ball(rng, math.radians(rot_deg))
+    dp = _ball(rng, trans_m)
+    return {
+        "rot": R @ so3_exp(dth),
+        "pos": p + dp,
+        "vel": np.zeros(3),
+        "bias_g": np.zeros(3),
+        "bias_a": np.zeros(3),
+        "gravity": np.array([0.0, 0.0, -9.81]),
+        "cov": np.eye(DIM_STATE) * INIT_COV,
+    }
+
+
+_CACHE_DIR = os.environ.get("LIVO_SYNTH_CACHE", "/tmp/livo_synth_cache")
+
+
+def cached_map(n_points: int) -> np.ndarray:
+    """make_map with an on-disk cache (maps of 1M-10M points take seconds to generate)."""
+    os.makedirs(_CACHE_DIR, exist_ok=True)
+    path = os.path.join(_CACHE_DIR, f"map_{n_points}_{SEED_MAP:x}.npy")
+    if os.path.exists(path):
+        try:
+            return np.load(path)
+        except Exception:
+            pass
+    m = make_map(n_points)
+    tmp = path + f".{os.getpid()}.tmp.npy"
+    np.save(tmp, m)
+    os.replace(tmp, path)
+    return m

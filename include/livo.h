@@ -1,0 +1,168 @@
+/*
+ * livo.h — C ABI of the MI355X-native LIO scan-to-map IEKF hot path.
+ *
+ * Drop-in boundary for FAST-LIVO's scan-to-map update.  The
+ * reference has no function boundary of its own for this path: the work lives
+ * in private members of LaserMapping with implicit state.  Each entry point
+ * below replaces one of them (reference paths under snowflakezzz/FAST-LIVO-noted):
+ *
+ *   livo_map_build      ← KD_TREE::Build            include/ikd-Tree/ikd_Tree.cpp:337-348
+ *                         (called at src/laser_mapping.cpp:134-142 for the first scan)
+ *   livo_knn            ← KD_TREE::Nearest_Search   include/ikd-Tree/ikd_Tree.cpp:350-380
+ *   livo_scan_upload    ← feats_down_body handed to h_share_model
+ *                                                   src/laser_mapping.cpp:129-131
+ *   livo_h_share        ← LaserMapping::h_share_model(MatrixXd&, VectorXd&)
+ *                                                   include/laser_mapping.h:83,
+ *                                                   src/laser_mapping.cpp:485-644
+ *   livo_iekf_update    ← the IEKF loop inlined in LaserMapping::Run
+ *                                                   src/laser_mapping.cpp:171-238
+ *   livo_iekf_update_batch ← the same for independent scans (scan farm, §8e)
+ *
+ * Conventions
+ *   - plain pointers and sizes only; no C++ or torch types cross the ABI;
+ *   - every function returns int: LIVO_OK (0) or a negative LIVO_E_* code;
+ *     nothing throws across the ABI (livo_error_string() explains a code);
+ *   - matrices are row-major doubles (the C++ facade in
+ *     fast-livo-noted_amd/host/ converts to/from Eigen-style column-major);
+ *   - host pointers are read/written synchronously before return;
+ *   - a livo_ctx owns one HIP stream, the device-resident map and scans, and
+ *     scratch; calls on one ctx are NOT thread-safe (use one ctx per host
+ *     thread / GPU, as the reference uses one LaserMapping per process).
+ *   - there is no CPU fallback: every compute entry point runs on the GPU and
+ *     fails with LIVO_E_HIP if no device is usable.
+ */
+#ifndef LIVO_H
+#define LIVO_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LIVO_ABI_VERSION 1
+#define LIVO_DIM_STATE 18        /* DIM_STATE, include/common_lib.h:32 */
+#define LIVO_NUM_MATCH_POINTS 5  /* NUM_MATCH_POINTS, include/common_lib.h:37 */
+#define LIVO_MAX_EVALS 16        /* max h_share/solve evaluations per scan update */
+
+enum {
+    LIVO_OK = 0,
+    LIVO_E_INVALID = -1,   /* bad argument (null pointer, negative size, ...) */
+    LIVO_E_HIP = -2,       /* HIP runtime error (no device, launch failure) */
+    LIVO_E_NOMAP = -3,     /* map not built */
+    LIVO_E_NOSCAN = -4,    /* unknown / released scan id */
+    LIVO_E_OOM = -5,       /* device allocation failed */
+    LIVO_E_RANGE = -6      /* size beyond the supported range */
+};
+
+typedef struct livo_ctx livo_ctx;
+
+/* Hot-path parameters (defaults = reference defaults, src/laser_mapping.cpp:945-1116). */
+typedef struct livo_params {
+    double laser_point_cov;  /* LASER_POINT_COV, laser_mapping.cpp:975 (0.001)          */
+    double R_LI[9];          /* Lidar_rot_to_IMU (row-major), default identity          */
+    double t_LI[3];          /* Lidar_offset_to_IMU, default 0                           */
+    double max_residual;     /* compaction gate |pd2| <= 2.0, laser_mapping.cpp:552      */
+    float plane_threshold;   /* esti_plane threshold 0.1f, laser_mapping.cpp:530         */
+    float max_nn_sqdist;     /* k-NN gate sqdis[4] > 5 => reject, laser_mapping.cpp:518  */
+    int32_t max_iterations;  /* NUM_MAX_ITERATIONS (max_iteration, default 4, :968)      */
+    int32_t flags;           /* reserved, must be 0                                      */
+} livo_params;
+
+/* StatesGroup (include/common_lib.h:518-603), row-major. */
+typedef struct livo_state {
+    double rot[9];      /* rot_end (IMU->world)  */
+    double pos[3];      /* pos_end               */
+    double vel[3];      /* vel_end               */
+    double bias_g[3];
+    double bias_a[3];
+    double gravity[3];
+    double cov[LIVO_DIM_STATE * LIVO_DIM_STATE];
+} livo_state;
+
+/* Per-scan-update statistics (the reference logs these ad hoc, laser_mapping.cpp:164-238). */
+typedef struct livo_iter_stats {
+    int32_t iterations;   /* h_share + solve evaluations performed            */
+    int32_t knn_passes;   /* evaluations with nearest_search_en               */
+    int32_t converged;    /* flg_EKF_converged at exit                        */
+    int32_t rematch_num;
+    int64_t effct_feat_num[LIVO_MAX_EVALS];
+    double solution[LIVO_MAX_EVALS][LIVO_DIM_STATE]; /* state delta per evaluation */
+    double res_mean[LIVO_MAX_EVALS];                 /* res_mean_last per evaluation */
+} livo_iter_stats;
+
+typedef struct livo_map_info {
+    int64_t num_points;   /* M                                                    */
+    int32_t depth;        /* tree levels                                          */
+    int32_t reserved;
+    int64_t num_slots;    /* heap-ordered node slots (2^depth - 1)                */
+    int64_t device_bytes; /* HBM bytes held by the map                            */
+} livo_map_info;
+
+/* Optional per-point outputs of livo_h_share (any pointer may be NULL). */
+typedef struct livo_point_out {
+    float* normvec;       /* N*4: plane n.x,n.y,n.z and pd2 (normvec->points[i], :537-541)      */
+    uint8_t* selected;    /* N:   point_selected_surf[i] && res_last[i] <= 2.0 (:552)            */
+    int32_t* nn_idx;      /* N*5: map indices (input order of livo_map_build), -1 pad           */
+    float* nn_sqdist;     /* N*5: squared distances (pointSearchSqDis), +inf pad                */
+    float* world_xyz;     /* N*3: feats_down_world (pointBodyToWorld, :508)                      */
+    int64_t* visits;      /* 1:   k-NN nodes visited over all points (the V_ref yardstick)       */
+} livo_point_out;
+
+/* Device time of the kernels of the last livo_iekf_update* call (profiling mode only).
+ * knn_* describe the first evaluation's k_hshare<true> launch, in which every
+ * point of every scan runs the k-NN (the dominant kernel). */
+typedef struct livo_timings {
+    double knn_ms;        /* first-evaluation launches (transform + k-NN + plane + H)   */
+    double plane_ms;      /* later evaluations (k-NN only where rematching)             */
+    double solve_ms;      /* reduction + 18x18 solve launches                           */
+    int64_t knn_launches; /* first-evaluation launches timed                            */
+    int64_t knn_visits;   /* tree nodes those launches visited                          */
+    int64_t knn_queries;  /* points those launches processed                            */
+    int64_t effct_points; /* effective points of those launches                         */
+} livo_timings;
+
+int livo_abi_version(void);
+const char* livo_error_string(int code);
+int livo_params_default(livo_params* p);
+
+int livo_ctx_create(int device, const livo_params* p, livo_ctx** out);
+int livo_ctx_destroy(livo_ctx* ctx);
+int livo_ctx_set_params(livo_ctx* ctx, const livo_params* p);
+int livo_ctx_set_profiling(livo_ctx* ctx, int enable);
+int livo_last_timings(livo_ctx* ctx, livo_timings* out);
+
+/* Build the device map from M host points (x,y,z floats at xyz + i*stride_bytes).
+ * Same tree as KD_TREE::Build on the same input order. Replaces any previous map. */
+int livo_map_build(livo_ctx* ctx, const float* xyz, int64_t M, int64_t stride_bytes);
+int livo_map_get_info(livo_ctx* ctx, livo_map_info* out);
+
+/* Exact k-NN (k <= 5) of n host queries; idx/sqdist are n*k, ascending. */
+int livo_knn(livo_ctx* ctx, const float* q_xyz, int64_t n, int32_t k, int32_t* idx, float* sqdist);
+
+/* Copy a body-frame scan (feats_down_body) to HBM; it stays resident until released. */
+int livo_scan_upload(livo_ctx* ctx, const float* xyz, int64_t N, int64_t stride_bytes, int32_t* scan_id);
+int livo_scan_release(livo_ctx* ctx, int32_t scan_id);
+
+/* One h_share_model evaluation on a resident scan at the given state.
+ * nearest_search_en != 0 runs the k-NN; otherwise the neighbours cached by the
+ * last search on this scan are reused (Nearest_Points, laser_mapping.h:165).
+ * HTH (9x9, row-major) and HTL (9) as HPH/HPL of the reference. */
+int livo_h_share(livo_ctx* ctx, int32_t scan_id, const livo_state* state, int nearest_search_en,
+                 double HTH[81], double HTL[9], int64_t* effct_feat_num, const livo_point_out* out);
+
+/* Full iterated update of one scan (laser_mapping.cpp:171-238): state in/out,
+ * prior = state_propagat (NULL: prior = input state). stats may be NULL. */
+int livo_iekf_update(livo_ctx* ctx, int32_t scan_id, livo_state* state, const livo_state* prior,
+                     livo_iter_stats* stats);
+
+/* n independent scan updates in one batched pass (states/priors/stats arrays of n). */
+int livo_iekf_update_batch(livo_ctx* ctx, int32_t n, const int32_t* scan_ids, livo_state* states,
+                           const livo_state* priors, livo_iter_stats* stats);
+
+int livo_sync(livo_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LIVO_H */

@@ -1,0 +1,174 @@
+"""ctypes wrapper around the CPU restatement (oracle/livo_oracle.cpp).
+
+TEST INFRASTRUCTURE ONLY — imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg as the checker.  Parity status: "parity unpinned"
+(see the header of livo_oracle.cpp and DESIGN.md §Oracle).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "build", "liblivo_oracle.so")
+
+DIM = 18
+MAX_EVALS = 16
+
+
+class OrcState(C.Structure):
+    _fields_ = [("rot", C.c_double * 9), ("pos", C.c_double * 3), ("vel", C.c_double * 3),
+                ("bias_g", C.c_double * 3), ("bias_a", C.c_double * 3), ("gravity", C.c_double * 3),
+                ("cov", C.c_double * 324)]
+
+
+class OrcIterStats(C.Structure):
+    _fields_ = [("iterations", C.c_int32), ("knn_passes", C.c_int32), ("converged", C.c_int32),
+                ("rematch_num", C.c_int32), ("effct_feat_num", C.c_int64 * MAX_EVALS),
+                ("solution", (C.c_double * 18) * MAX_EVALS), ("res_mean", C.c_double * MAX_EVALS)]
+
+
+def build(force: bool = False) -> str:
+    src = os.path.join(_HERE, "livo_oracle.cpp")
+    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", _HERE])
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(LIB_PATH)
+        P = C.c_void_p
+        fp = np.ctypeslib.ndpointer
+        L.orc_tree_build.restype = P
+        L.orc_tree_build.argtypes = [P, C.c_int64]
+        L.orc_tree_free.argtypes = [P]
+        L.orc_tree_size.restype = C.c_int64
+        L.orc_tree_size.argtypes = [P]
+        L.orc_knn.argtypes = [P, P, C.c_int64, C.c_int, P, P, P, C.c_int]
+        L.orc_knn_brute.argtypes = [P, C.c_int64, P, C.c_int64, C.c_int, P, P, C.c_int]
+        L.orc_esti_plane.argtypes = [P, C.c_float, P]
+        L.orc_h_share.argtypes = [P, P, C.c_int64, P, P, P, P, C.c_int, C.c_double, P, P, P, P, P, P, P, P,
+                                  P, P, C.c_int]
+        L.orc_iekf_update.argtypes = [P, P, C.c_int64, P, P, C.c_double, C.c_int, C.POINTER(OrcState),
+                                      C.POINTER(OrcState), C.POINTER(OrcIterStats), P, C.c_int]
+        del fp
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+def state_to_c(st: dict) -> OrcState:
+    s = OrcState()
+    s.rot[:] = np.asarray(st["rot"], np.float64).reshape(9).tolist()
+    for k in ("pos", "vel", "bias_g", "bias_a", "gravity"):
+        getattr(s, k)[:] = np.asarray(st[k], np.float64).reshape(3).tolist()
+    s.cov[:] = np.asarray(st["cov"], np.float64).reshape(324).tolist()
+    return s
+
+
+def state_from_c(s: OrcState) -> dict:
+    return {
+        "rot": np.array(s.rot[:]).reshape(3, 3),
+        "pos": np.array(s.pos[:]), "vel": np.array(s.vel[:]),
+        "bias_g": np.array(s.bias_g[:]), "bias_a": np.array(s.bias_a[:]),
+        "gravity": np.array(s.gravity[:]), "cov": np.array(s.cov[:]).reshape(18, 18),
+    }
+
+
+class Tree:
+    """kd-tree restating ikd-Tree Build (static map, no deletions)."""
+
+    def __init__(self, xyz: np.ndarray):
+        self.xyz = np.ascontiguousarray(xyz, np.float32)
+        assert self.xyz.ndim == 2 and self.xyz.shape[1] == 3
+        self.h = lib().orc_tree_build(_p(self.xyz), self.xyz.shape[0])
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.orc_tree_free(self.h)
+            self.h = None
+
+    def knn(self, q: np.ndarray, k: int = 5, threads: int = 1):
+        q = np.ascontiguousarray(q, np.float32)
+        n = q.shape[0]
+        idx = np.empty((n, k), np.int32)
+        d = np.empty((n, k), np.float32)
+        vis = np.empty(n, np.int64)
+        rc = lib().orc_knn(self.h, _p(q), n, k, _p(idx), _p(d), _p(vis), threads)
+        assert rc == 0
+        return idx, d, vis
+
+    def h_share(self, body, rot, pos, R_LI, t_LI, search_en, cache=None, lpc=0.001, threads=1):
+        body = np.ascontiguousarray(body, np.float32)
+        n = body.shape[0]
+        if cache is None:
+            cache = {"xyz": np.zeros((n, 15), np.float32), "cnt": np.zeros(n, np.int32),
+                     "idx": np.full((n, 5), -1, np.int32), "d": np.zeros((n, 5), np.float32)}
+        HTH = np.zeros(81)
+        HTL = np.zeros(9)
+        eff = np.zeros(1, np.int64)
+        vis = np.zeros(1, np.int64)
+        nv = np.zeros((n, 4), np.float32)
+        sel = np.zeros(n, np.uint8)
+        rot = np.ascontiguousarray(rot, np.float64)
+        pos = np.ascontiguousarray(pos, np.float64)
+        R_LI = np.ascontiguousarray(R_LI, np.float64)
+        t_LI = np.ascontiguousarray(t_LI, np.float64)
+        lib().orc_h_share(self.h, _p(body), n, _p(rot), _p(pos), _p(R_LI), _p(t_LI), int(bool(search_en)),
+                          lpc, _p(cache["xyz"]), _p(cache["cnt"]), _p(cache["idx"]), _p(cache["d"]),
+                          _p(HTH), _p(HTL), _p(eff), _p(nv), _p(sel), _p(vis), threads)
+        return {"HTH": HTH.reshape(9, 9), "HTL": HTL, "effct": int(eff[0]), "normvec": nv, "sel": sel,
+                "visits": int(vis[0]), "cache": cache}
+
+    def iekf_update(self, body, state: dict, prior: dict | None = None, R_LI=None, t_LI=None,
+                    max_iter: int = 4, lpc: float = 0.001, threads: int = 1):
+        from_state = state_to_c(state)
+        pr = state_to_c(prior if prior is not None else state)
+        st = OrcIterStats()
+        vt = np.zeros(1, np.int64)
+        body = np.ascontiguousarray(body, np.float32)
+        R_LI = np.ascontiguousarray(np.eye(3) if R_LI is None else R_LI, np.float64)
+        t_LI = np.ascontiguousarray(np.zeros(3) if t_LI is None else t_LI, np.float64)
+        rc = lib().orc_iekf_update(self.h, _p(body), body.shape[0], _p(R_LI), _p(t_LI), lpc, max_iter,
+                                   C.byref(from_state), C.byref(pr), C.byref(st), _p(vt), threads)
+        assert rc == 0
+        ne = st.iterations
+        stats = {
+            "iterations": ne, "knn_passes": st.knn_passes, "converged": st.converged,
+            "rematch_num": st.rematch_num,
+            "effct_feat_num": [st.effct_feat_num[i] for i in range(ne)],
+            "solution": np.array([list(st.solution[i]) for i in range(ne)]),
+            "res_mean": [st.res_mean[i] for i in range(ne)],
+            "visits": int(vt[0]),
+        }
+        return state_from_c(from_state), stats
+
+
+def knn_brute(xyz, q, k=5, threads=8):
+    xyz = np.ascontiguousarray(xyz, np.float32)
+    q = np.ascontiguousarray(q, np.float32)
+    n = q.shape[0]
+    idx = np.empty((n, k), np.int32)
+    d = np.empty((n, k), np.float32)
+    rc = lib().orc_knn_brute(_p(xyz), xyz.shape[0], _p(q), n, k, _p(idx), _p(d), threads)
+    assert rc == 0
+    return idx, d
+
+
+def esti_plane(pts5x3, threshold=0.1):
+    p = np.ascontiguousarray(pts5x3, np.float32).reshape(15)
+    out = np.zeros(4, np.float32)
+    ok = lib().orc_esti_plane(_p(p), C.c_float(threshold), _p(out))
+    return bool(ok), out

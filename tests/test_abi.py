@@ -1,0 +1,107 @@
+"""CPU checks of the drop-in boundary: the HIP library builds, loads and exports
+exactly the C ABI declared in include/livo.h; struct layouts agree between C
+and the Python binding; errors come back as codes (no GPU needed, no compute).
+"""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "livo.h")
+
+
+def _declared():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(livo_\w+)\s*\(", txt, flags=re.M)))
+
+
+def test_header_declares_abi():
+    names = _declared()
+    for n in ("livo_ctx_create", "livo_map_build", "livo_knn", "livo_scan_upload", "livo_h_share",
+              "livo_iekf_update", "livo_iekf_update_batch"):
+        assert n in names
+
+
+def test_library_exports_every_declared_symbol(built):
+    import livo_amd
+    lib = C.CDLL(livo_amd.LIB_PATH)
+    missing = [n for n in _declared() if not hasattr(lib, n)]
+    assert not missing, missing
+    # and the Python binding covers the whole ABI
+    assert set(_declared()) == set(livo_amd.SIGNATURES)
+    out = subprocess.run(["nm", "-D", "--defined-only", livo_amd.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (livo_\w+)", out))
+    assert exported == set(_declared())
+
+
+def test_hip_code_object_is_gfx950(built):
+    import livo_amd
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-S", livo_amd.LIB_PATH], capture_output=True,
+                         text=True).stdout
+    assert ".hip_fatbin" in out
+    blob = open(livo_amd.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_version_and_errors(built):
+    import livo_amd
+    L = livo_amd.load()
+    hdr = open(HEADER).read()
+    ver = int(re.search(r"#define LIVO_ABI_VERSION (\d+)", hdr).group(1))
+    assert L.livo_abi_version() == ver
+    for code in (0, -1, -2, -3, -4, -5, -6, -77):
+        assert isinstance(L.livo_error_string(code), bytes)
+    p = livo_amd.default_params()
+    # reference defaults (laser_mapping.cpp:968-983, :518, :530, :552)
+    assert p.laser_point_cov == 0.001 and p.max_iterations == 4
+    assert abs(p.plane_threshold - 0.1) < 1e-7 and p.max_nn_sqdist == 5.0 and p.max_residual == 2.0
+    assert list(p.R_LI) == [1, 0, 0, 0, 1, 0, 0, 0, 1] and list(p.t_LI) == [0, 0, 0]
+
+
+def test_invalid_arguments_return_codes(built):
+    import livo_amd
+    L = livo_amd.load()
+    assert L.livo_ctx_create(0, None, None) == -1  # LIVO_E_INVALID
+    assert L.livo_ctx_destroy(None) == -1
+    assert L.livo_params_default(None) == -1
+    bad = livo_amd.default_params()
+    bad.max_iterations = 99
+    h = C.c_void_p()
+    assert L.livo_ctx_create(0, C.byref(bad), C.byref(h)) == -1
+    assert L.livo_map_build(None, None, 0, 0) == -1
+    assert L.livo_sync(None) == -1
+
+
+def test_no_gpu_fails_loudly(built):
+    """Without a usable GPU every compute path reports LIVO_E_HIP: there is no CPU fallback."""
+    import livo_amd
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("GPU present")
+    except Exception:
+        pass
+    with pytest.raises(livo_amd.LivoError) as e:
+        livo_amd.Context(0)
+    assert e.value.code == -2
+
+
+def test_struct_layouts_match_c(tmp_path):
+    import livo_amd
+    src = tmp_path / "sz.c"
+    src.write_text('#include "livo.h"\n#include <stdio.h>\n#include <stddef.h>\nint main(void){printf("%zu %zu %zu %zu '
+                   '%zu %zu %zu %zu\\n", sizeof(livo_params), sizeof(livo_state), sizeof(livo_iter_stats), '
+                   'sizeof(livo_map_info), sizeof(livo_point_out), sizeof(livo_timings), '
+                   'offsetof(livo_params, max_iterations), offsetof(livo_iter_stats, solution));return 0;}\n')
+    exe = tmp_path / "sz"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(src)])
+    got = [int(x) for x in subprocess.check_output([str(exe)]).split()]
+    want = [C.sizeof(livo_amd.Params), C.sizeof(livo_amd.State), C.sizeof(livo_amd.IterStats),
+            C.sizeof(livo_amd.MapInfo), C.sizeof(livo_amd.PointOut), C.sizeof(livo_amd.Timings),
+            livo_amd.Params.max_iterations.offset, livo_amd.IterStats.solution.offset]
+    assert got == want
+    import oracle
+    assert C.sizeof(oracle.OrcState) == C.sizeof(livo_amd.State)

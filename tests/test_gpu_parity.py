@@ -1,0 +1,283 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Bar (BASELINE.json north_star):
+  * k-NN indices / squared distances, world points, plane normals, residuals
+    and selection flags: bit-exact (integer/index work, and float work done in
+    the reference's operation order on both sides);
+  * HTH / HTL (double, different summation order): 1e-9 relative;
+  * IEKF state delta per evaluation: 1e-5 relative (north_star tolerance);
+    iteration / k-NN-pass / effective-point counts: exact.
+Parity vs the reference itself is unpinned (see oracle/livo_oracle.cpp header).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REL_HTH = 1e-9
+REL_STATE = 1e-5
+
+
+def _synth():
+    from livo_amd import synth
+    return synth
+
+
+def _rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    den = max(np.linalg.norm(b), 1e-300)
+    return np.linalg.norm(a - b) / den
+
+
+@pytest.fixture(scope="module")
+def ctx100k(gpu_ctx, map100k):
+    gpu_ctx.map_build(map100k)
+    return gpu_ctx
+
+
+def test_map_info(ctx100k):
+    info = ctx100k.map_info()
+    assert info["num_points"] == 100_000
+    assert info["depth"] == 17  # floor(log2(1e5)) + 1
+    assert info["num_slots"] == 2 ** 17 - 1
+    assert info["device_bytes"] == (2 ** 17) * 64
+
+
+def test_knn_bit_exact(ctx100k, tree100k, map100k):
+    synth = _synth()
+    body, _, _ = synth.make_scan(10_000, 0)
+    st = synth.make_state(0)
+    q = ((body.astype(np.float64) + synth.T_LI) @ st["rot"].T + st["pos"]).astype(np.float32)
+    idx, d = ctx100k.knn(q, 5)
+    ridx, rd, _ = tree100k.knn(q, 5)
+    assert np.array_equal(idx, ridx)
+    assert np.array_equal(d.view(np.uint32), rd.view(np.uint32))
+    # ascending, and distances recomputed from the returned indices
+    assert np.all(np.diff(d, axis=1) >= 0)
+    p = map100k[idx]
+    dd = ((q[:, None, 0] - p[..., 0]) ** 2 + (q[:, None, 1] - p[..., 1]) ** 2) + (q[:, None, 2] - p[..., 2]) ** 2
+    assert np.array_equal(dd.astype(np.float32), d)
+
+
+@pytest.mark.parametrize("k", [1, 3, 5])
+def test_knn_k(ctx100k, tree100k, k):
+    rng = np.random.default_rng(7)
+    q = rng.uniform([-32, -22, -2], [32, 22, 3], size=(3000, 3)).astype(np.float32)
+    idx, d = ctx100k.knn(q, k)
+    ridx, rd, _ = tree100k.knn(q, k)
+    assert np.array_equal(idx, ridx) and np.array_equal(d, rd)
+
+
+def test_knn_edge_maps(built):
+    """Tiny maps (fewer points than k), duplicates / exact ties, far queries."""
+    import livo_amd
+    import oracle
+    rng = np.random.default_rng(3)
+    with livo_amd.Context(0) as ctx:
+        for M in (1, 2, 3, 4, 5, 6, 7, 31, 64, 65):
+            m = rng.normal(size=(M, 3)).astype(np.float32)
+            ctx.map_build(m)
+            q = np.concatenate([rng.normal(size=(200, 3)), [[1e4, 1e4, 1e4], [0, 0, 0]]]).astype(np.float32)
+            idx, d = ctx.knn(q, 5)
+            ridx, rd, _ = oracle.Tree(m).knn(q, 5)
+            assert np.array_equal(idx, ridx), M
+            assert np.array_equal(d, rd), M
+            assert np.all(idx[:, min(M, 5):] == -1)
+        # exact duplicates and equal-distance ties: a lattice
+        g = np.stack(np.meshgrid(np.arange(6), np.arange(6), np.arange(3)), -1).reshape(-1, 3).astype(np.float32)
+        m = np.concatenate([g, g[:20]])  # 20 exact duplicate points
+        ctx.map_build(m)
+        q = np.concatenate([g + 0.5, g, rng.uniform(0, 5, size=(300, 3))]).astype(np.float32)
+        idx, d = ctx.knn(q, 5)
+        ridx, rd, _ = oracle.Tree(m).knn(q, 5)
+        assert np.array_equal(idx, ridx)
+        assert np.array_equal(d, rd)
+
+
+def test_knn_empty_map(built):
+    import livo_amd
+    with livo_amd.Context(0) as ctx:
+        ctx.map_build(np.zeros((0, 3), np.float32))
+        idx, d = ctx.knn(np.zeros((4, 3), np.float32), 5)
+        assert np.all(idx == -1) and np.all(np.isinf(d))
+
+
+def _hshare_compare(g, r, n):
+    assert np.array_equal(g["nn_idx"], r["cache"]["idx"])
+    assert np.array_equal(g["nn_d"].view(np.uint32), r["cache"]["d"].view(np.uint32))
+    assert np.array_equal(g["normvec"].view(np.uint32), r["normvec"].view(np.uint32))
+    assert np.array_equal(g["sel"], r["sel"])
+    assert g["effct"] == r["effct"]
+    assert _rel(g["HTH"], r["HTH"]) < REL_HTH
+    assert _rel(g["HTL"], r["HTL"]) < REL_HTH
+
+
+def test_h_share_parity(ctx100k, tree100k):
+    synth = _synth()
+    body, _, _ = synth.make_scan(10_000, 1)
+    st = synth.make_state(1)
+    sid = ctx100k.scan_upload(body)
+    try:
+        g = ctx100k.h_share(sid, st, search_en=True)
+        r = tree100k.h_share(body, st["rot"], st["pos"], np.eye(3), synth.T_LI, True)
+        world = ((body.astype(np.float64) + synth.T_LI) @ st["rot"].T + st["pos"]).astype(np.float32)
+        assert np.abs(g["world"] - world).max() <= 1e-5
+        _hshare_compare(g, r, len(body))
+        assert g["visits"] == r["visits"]  # identical traversal => identical node visits
+        # re-fit at a moved state, reusing the cached neighbours (nearest_search_en = false)
+        st2 = dict(st)
+        st2["pos"] = st["pos"] + np.array([0.01, -0.02, 0.005])
+        g2 = ctx100k.h_share(sid, st2, search_en=False)
+        r2 = tree100k.h_share(body, st2["rot"], st2["pos"], np.eye(3), synth.T_LI, False, cache=r["cache"])
+        _hshare_compare(g2, r2, len(body))
+    finally:
+        ctx100k.scan_release(sid)
+
+
+def _iekf_compare(gpu_ctx, tree, body, st0, max_iter, t_LI):
+    gpu_ctx.set_params(max_iterations=max_iter)
+    sid = gpu_ctx.scan_upload(body)
+    try:
+        sg, stg = gpu_ctx.iekf_update(sid, st0)
+    finally:
+        gpu_ctx.scan_release(sid)
+    sr, str_ = tree.iekf_update(body, st0, R_LI=np.eye(3), t_LI=t_LI, max_iter=max_iter)
+    assert stg["iterations"] == str_["iterations"]
+    assert stg["knn_passes"] == str_["knn_passes"]
+    assert stg["converged"] == str_["converged"]
+    assert stg["effct_feat_num"] == str_["effct_feat_num"]
+    for e in range(stg["iterations"]):
+        assert _rel(stg["solution"][e], str_["solution"][e]) < REL_STATE, e
+    # final state: rotation / position change relative to the update
+    dth_g = np.linalg.norm(st0["rot"].T @ sg["rot"] - st0["rot"].T @ sr["rot"])
+    assert dth_g < REL_STATE * max(np.linalg.norm(str_["solution"][:, :3]), 1e-12)
+    assert _rel(sg["pos"] - st0["pos"], sr["pos"] - st0["pos"]) < REL_STATE
+    assert _rel(sg["cov"], sr["cov"]) < 1e-9
+    return stg
+
+
+@pytest.mark.parametrize("max_iter", [4, 2, 0, 1, 10])
+def test_iekf_parity_config1(ctx100k, tree100k, max_iter):
+    synth = _synth()
+    body, _, _ = synth.make_scan(10_000, 0)
+    st0 = synth.make_state(0)
+    _iekf_compare(ctx100k, tree100k, body, st0, max_iter, synth.T_LI)
+    ctx100k.set_params(max_iterations=4)
+
+
+def test_iekf_prior_differs(ctx100k, tree100k):
+    """state_propagat != state: the prior term vec = prior ⊟ state is exercised."""
+    synth = _synth()
+    body, _, _ = synth.make_scan(5_000, 2)
+    st0 = synth.make_state(2)
+    prior = dict(st0)
+    prior["pos"] = st0["pos"] + np.array([0.02, 0.0, -0.01])
+    prior["rot"] = st0["rot"] @ synth.so3_exp(np.array([0.002, -0.001, 0.003]))
+    prior["vel"] = np.array([0.5, 0.1, 0.0])
+    sid = ctx100k.scan_upload(body)
+    try:
+        sg, stg = ctx100k.iekf_update(sid, st0, prior)
+    finally:
+        ctx100k.scan_release(sid)
+    import oracle
+    sr, str_ = tree100k.iekf_update(body, st0, prior, R_LI=np.eye(3), t_LI=synth.T_LI, max_iter=4)
+    assert stg["iterations"] == str_["iterations"]
+    for e in range(stg["iterations"]):
+        assert _rel(stg["solution"][e], str_["solution"][e]) < REL_STATE
+    assert _rel(sg["vel"], sr["vel"]) < REL_STATE
+
+
+def test_batch_equals_single_and_deterministic(ctx100k):
+    synth = _synth()
+    sids, states = [], []
+    for s in range(4):
+        body, _, _ = synth.make_scan(3000 + 517 * s, s)
+        sids.append(ctx100k.scan_upload(body))
+        states.append(synth.make_state(s))
+    try:
+        b1, s1 = ctx100k.iekf_update_batch(sids, states)
+        b2, s2 = ctx100k.iekf_update_batch(sids, states)
+        for a, b in zip(b1, b2):  # run-to-run bitwise reproducible
+            assert all(np.array_equal(a[k], b[k]) for k in a)
+        for i, sid in enumerate(sids):
+            one, st1 = ctx100k.iekf_update(sid, states[i])
+            assert all(np.array_equal(one[k], b1[i][k]) for k in one)
+            assert st1["effct_feat_num"] == s1[i]["effct_feat_num"]
+    finally:
+        for sid in sids:
+            ctx100k.scan_release(sid)
+
+
+@pytest.mark.parametrize("n", [0, 1, 5, 255, 257])
+def test_ragged_scans(ctx100k, tree100k, n):
+    synth = _synth()
+    body, _, _ = synth.make_scan(max(n, 1), 3)
+    body = body[:n]
+    st0 = synth.make_state(3)
+    sid = ctx100k.scan_upload(body)
+    try:
+        g = ctx100k.h_share(sid, st0, True)
+        r = tree100k.h_share(body, st0["rot"], st0["pos"], np.eye(3), synth.T_LI, True)
+        _hshare_compare(g, r, n)
+        sg, stg = ctx100k.iekf_update(sid, st0)
+        assert stg["iterations"] >= 1
+    finally:
+        ctx100k.scan_release(sid)
+
+
+def test_bad_args(ctx100k):
+    import livo_amd
+    with pytest.raises(livo_amd.LivoError):
+        ctx100k.scan_release(12345)
+    with pytest.raises(livo_amd.LivoError):
+        ctx100k.iekf_update(9999, _synth().make_state(0))
+
+
+@pytest.mark.slow
+def test_config2_full_size_1M(built):
+    """100k-point scan vs 1M-point map (BASELINE configs[1]/[2]): full parity."""
+    import livo_amd
+    import oracle
+    synth = _synth()
+    m = synth.cached_map(1_000_000)
+    tree = oracle.Tree(m)
+    body, _, _ = synth.make_scan(100_000, 0)
+    st0 = synth.make_state(0)
+    with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=2) as ctx:
+        ctx.map_build(m)
+        assert ctx.map_info()["depth"] == 20
+        stg = _iekf_compare(ctx, tree, body, st0, 2, synth.T_LI)  # config 3: 3 IEKF iterations
+        assert stg["iterations"] == 3
+        stg = _iekf_compare(ctx, tree, body, st0, 4, synth.T_LI)  # config 2
+        sid = ctx.scan_upload(body)
+        g = ctx.h_share(sid, st0, True)
+        r = tree.h_share(body, st0["rot"], st0["pos"], np.eye(3), synth.T_LI, True)
+        _hshare_compare(g, r, len(body))
+        assert g["visits"] == r["visits"]
+
+
+@pytest.mark.slow
+def test_config5_10M_properties(built):
+    """10M-point map, 200k-point scan: size-independent properties + a sampled oracle check."""
+    import livo_amd
+    import oracle
+    synth = _synth()
+    m = synth.cached_map(10_000_000)
+    body, _, _ = synth.make_scan(200_000, 5)
+    st0 = synth.make_state(5)
+    with livo_amd.Context(0, t_LI=synth.T_LI) as ctx:
+        ctx.map_build(m)
+        q = ((body.astype(np.float64) + synth.T_LI) @ st0["rot"].T + st0["pos"]).astype(np.float32)
+        idx, d = ctx.knn(q, 5)
+        assert np.all(idx >= 0) and np.all(np.diff(d, axis=1) >= 0)
+        p = m[idx]
+        dd = ((q[:, None, 0] - p[..., 0]) ** 2 + (q[:, None, 1] - p[..., 1]) ** 2) + (q[:, None, 2] - p[..., 2]) ** 2
+        assert np.array_equal(dd.astype(np.float32), d)
+        tree = oracle.Tree(m)
+        sample = np.random.default_rng(0).choice(len(q), 4000, replace=False)
+        ridx, rd, _ = tree.knn(q[sample], 5, threads=8)
+        assert np.array_equal(idx[sample], ridx) and np.array_equal(d[sample], rd)
+        sid = ctx.scan_upload(body)
+        sg, stg = ctx.iekf_update(sid, st0)
+        assert stg["iterations"] >= 2 and stg["effct_feat_num"][0] > 150_000
