@@ -1,0 +1,226 @@
+#!/usr/bin/env python3
+"""bench.py — IEKF scan-to-map updates/s on MI355X (BASELINE.json metric, configs[1]).
+
+Workload: synthetic Livox-Avia-shaped
+100k-point scans against a 1M-point ikd-Tree map, the full IEKF scan update of
+laser_mapping.cpp:171-238 with max_iteration = 4 (k-NN + plane fit + Jacobian
++ HᵀH reduction + 18x18 solve per evaluation, rematch / convergence control on
+the device).  A step = one batched pass over --batch independent scans per GPU
+(scan farm, §8e); value = scan updates per second over the whole job, with
+scans and map already resident in HBM when the timed region starts.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+N > 1: launched by torch.distributed.run (one process per GPU, RCCL); every
+rank processes its own scans ("weak" scaling) and the ranks all-reduce only
+throughput counters.  Rank 0 prints one JSON line.
+
+Extra fields: roofline of the dominant kernel (k_hshare<true>: the first
+evaluation, transform + k-NN + plane fit + H for every point, timed with HIP
+events on the library's stream inside the timed region), cpu_baseline (the
+CPU restatement, oracle/, 1 thread on this host, bounded sample), parity of
+the first scan against that CPU run.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (os.path.join(ROOT, "fast-livo-noted_amd"), os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+# Algorithmic bytes: k-NN per query V(q)*64 + 12 (query) + 40 (5 idx + sqdist);
+# plane fit 77 B/point; transform 24 B/point; Jacobian/reduction 28 B per effective point.
+B_NODE = 64
+B_QUERY = 12 + 5 * 8
+B_PLANE = 77
+B_XFORM = 24
+B_JAC = 28
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=8, help="independent scans per step per GPU")
+    ap.add_argument("--scan-points", type=int, default=100_000)
+    ap.add_argument("--map-points", type=int, default=1_000_000)
+    ap.add_argument("--max-iter", type=int, default=4)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0: skip)")
+    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01_pmc_summary.json"))
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    import livo_amd
+    from livo_amd import farm, synth
+
+    rank, local_rank, world = farm.dist_env()
+    import torch
+    import torch.distributed as dist
+
+    torch_dev = None
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local_rank)
+        torch_dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl" if torch_dev is not None else "gloo")
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def sync():
+        if torch_dev is not None:
+            torch.cuda.synchronize()
+
+    # ---- inputs (identical generator on every rank; each rank its own scans)
+    m = synth.cached_map(a.map_points)
+    scan_ids = [rank * a.batch + j for j in range(a.batch)]
+    scans = [synth.make_scan(a.scan_points, s)[0] for s in scan_ids]
+    st0 = [synth.make_state(s) for s in scan_ids]
+
+    ctx = livo_amd.Context(local_rank, t_LI=synth.T_LI, max_iterations=a.max_iter)
+    t = time.time()
+    ctx.map_build(m)
+    map_build_s = time.time() - t
+    sids = [ctx.scan_upload(s) for s in scans]
+    init = (livo_amd.State * a.batch)(*[livo_amd.state_to_c(s) for s in st0])
+    work = (livo_amd.State * a.batch)()
+    nbytes = C.sizeof(init)
+
+    def step():
+        C.memmove(work, init, nbytes)  # every step restarts the same scans from their priors
+        _, stats = ctx.iekf_update_batch(sids, work, raw=True)
+        return stats
+
+    for _ in range(a.warmup):
+        step()
+    first_stats = [livo_amd.stats_from_c(s) for s in step()]
+    first_states = [livo_amd.state_from_c(s) for s in work]
+
+    counters = farm.Counters()
+    ctx.set_profiling(True)
+    knn_ms = 0.0
+    knn_launches = knn_visits = knn_queries = knn_effct = 0
+    sync()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        stats = step()
+        counters.add_stats(stats)
+        tm = ctx.last_timings()
+        knn_ms += tm["knn_ms"]
+        knn_launches += tm["knn_launches"]
+        knn_visits += tm["knn_visits"]
+        knn_queries += tm["knn_queries"]
+        knn_effct += tm["effct_points"]
+    sync()
+    barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    ctx.set_profiling(False)
+    counters.knn_visits, counters.knn_queries = knn_visits, knn_queries
+    elapsed_max = farm.allreduce_max(elapsed, torch_dev)
+    total = farm.allreduce_counters(counters, torch_dev)
+
+    # ---- roofline of the dominant kernel (rank-local, per launch)
+    launch_ms = knn_ms / max(knn_launches, 1)
+    bytes_per_launch = (knn_visits * B_NODE + knn_queries * (B_QUERY + B_PLANE + B_XFORM) + knn_effct * B_JAC) / max(
+        knn_launches, 1)
+    achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
+    traffic = None
+    try:
+        with open(a.pmc_summary) as f:
+            pmc = json.load(f)
+        if pmc.get("workload") == f"{a.scan_points}x{a.batch}@{a.map_points}":
+            traffic = pmc.get("hbm_bytes_per_launch")
+    except Exception:
+        pass
+
+    result = None
+    if rank == 0:
+        value = total.scans / elapsed_max
+        result = {
+            "metric": "IEKF scan-to-map updates/sec (100k-pt scan, 1M-pt map)",
+            "value": round(value, 3),
+            "unit": "scan updates/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed_max / a.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32+f64",
+            "data": "synthetic (seeded planar room map + Livox-Avia rosette scans; reference ships no bags)",
+            "config": {"workload": f"config2: {a.scan_points // 1000}k-pt scan vs {a.map_points // 1000000 or a.map_points}"
+                                   f"{'M' if a.map_points >= 1000000 else ''}-pt map, max_iteration={a.max_iter}, "
+                                   f"{a.batch} independent scans per GPU per step",
+                       "scan_points": a.scan_points, "map_points": a.map_points, "max_iteration": a.max_iter,
+                       "scans_per_step_per_gpu": a.batch, "parallelism": f"scan farm x{world}"},
+            "iekf_steps_per_s": round(total.evals / elapsed_max, 3),
+            "knn_queries_per_s": round((total.knn_passes * a.scan_points) / elapsed_max, 1),
+            "evals_per_scan": round(total.evals / max(total.scans, 1), 3),
+            "knn_passes_per_scan": round(total.knn_passes / max(total.scans, 1), 3),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "k_hshare<true> (transform + k-NN + plane + H, first evaluation)",
+                         "avg_launch_ms": round(launch_ms, 4),
+                         "alg_bytes_per_launch": int(bytes_per_launch),
+                         "visits_per_query": round(knn_visits / max(knn_queries, 1), 3)},
+            "map_build_s": round(map_build_s, 3),
+        }
+
+    # ---- CPU baseline: the oracle (CPU restatement), 1 thread, bounded sample; + parity of scan 0
+    if rank == 0 and a.cpu_seconds > 0:
+        import oracle
+        tree = oracle.Tree(m)
+        done = 0
+        t = time.perf_counter()
+        ref0 = None
+        while True:
+            j = done % a.batch
+            out, rs = tree.iekf_update(scans[j], st0[j], R_LI=np.eye(3), t_LI=synth.T_LI, max_iter=a.max_iter,
+                                       threads=1)
+            if done == 0:
+                ref0 = (out, rs)
+            done += 1
+            if time.perf_counter() - t >= a.cpu_seconds or done >= 64:
+                break
+        cpu_s = time.perf_counter() - t
+        result["cpu_baseline"] = {"value": round(done / cpu_s, 4), "unit": "scan updates/s", "cores": 1,
+                                  "kind": "port",
+                                  "sample": f"{done} full scan updates ({a.scan_points // 1000}k-pt scans vs "
+                                            f"{a.map_points}-pt map, max_iteration={a.max_iter}) by oracle/ "
+                                            f"(C++ restatement), 1 thread, {cpu_s:.1f} s"}
+        result["speedup_vs_cpu_1thread"] = round(result["value"] / result["cpu_baseline"]["value"], 1)
+        out, rs = ref0
+        gs = first_stats[0]
+        rel = max(np.linalg.norm(gs["solution"][e] - rs["solution"][e]) / np.linalg.norm(rs["solution"][e])
+                  for e in range(min(gs["iterations"], rs["iterations"])))
+        result["parity_scan0"] = {"iterations_equal": gs["iterations"] == rs["iterations"],
+                                  "effct_equal": gs["effct_feat_num"] == rs["effct_feat_num"],
+                                  "max_rel_state_delta": float(f"{rel:.3e}")}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
