@@ -15,9 +15,9 @@ N > 1: launched by torch.distributed.run (one process per GPU, RCCL); every
 rank processes its own scans ("weak" scaling) and the ranks all-reduce only
 throughput counters.  Rank 0 prints one JSON line.
 
-Extra fields: roofline of the dominant kernel (k_hshare<true>: the first
-evaluation, transform + k-NN + plane fit + H for every point, timed with HIP
-events on the library's stream inside the timed region), cpu_baseline (the
+Extra fields: roofline of the dominant kernel (k_knn_pass<true>: the first
+evaluation's transform + exact k-NN of every point, timed with HIP events on
+the library's stream inside the timed region), cpu_baseline (the
 CPU restatement, oracle/, 1 thread on this host, bounded sample), parity of
 the first scan against that CPU run.
 """
@@ -113,7 +113,8 @@ def main():
     counters = farm.Counters()
     ctx.set_profiling(True)
     knn_ms = 0.0
-    knn_launches = knn_visits = knn_queries = knn_effct = 0
+    knn_launches = knn_visits = knn_queries = knn_effct = replays = 0
+    t_rematch = t_plane = t_solve = 0.0
     sync()
     barrier()
     sync()
@@ -127,6 +128,10 @@ def main():
         knn_visits += tm["knn_visits"]
         knn_queries += tm["knn_queries"]
         knn_effct += tm["effct_points"]
+        replays += tm["knn_replays"]
+        t_rematch += tm["rematch_knn_ms"]
+        t_plane += tm["plane_ms"]
+        t_solve += tm["solve_ms"]
     sync()
     barrier()
     sync()
@@ -138,8 +143,7 @@ def main():
 
     # ---- roofline of the dominant kernel (rank-local, per launch)
     launch_ms = knn_ms / max(knn_launches, 1)
-    bytes_per_launch = (knn_visits * B_NODE + knn_queries * (B_QUERY + B_PLANE + B_XFORM) + knn_effct * B_JAC) / max(
-        knn_launches, 1)
+    bytes_per_launch = (knn_visits * B_NODE + knn_queries * B_QUERY) / max(knn_launches, 1)
     achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
     traffic = None
     try:
@@ -177,10 +181,13 @@ def main():
             "knn_passes_per_scan": round(total.knn_passes / max(total.scans, 1), 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "k_hshare<true> (transform + k-NN + plane + H, first evaluation)",
+                         "kernel": "k_knn_pass<true> (transform + exact k-NN of every point, first evaluation)",
                          "avg_launch_ms": round(launch_ms, 4),
                          "alg_bytes_per_launch": int(bytes_per_launch),
                          "visits_per_query": round(knn_visits / max(knn_queries, 1), 3)},
+            "device_ms_per_step": {"knn_first": round(knn_ms / a.steps, 4), "knn_rematch": round(t_rematch / a.steps, 4),
+                                   "plane_H": round(t_plane / a.steps, 4), "solve": round(t_solve / a.steps, 4)},
+            "knn_replays_per_step": round(replays / a.steps, 2),
             "map_build_s": round(map_build_s, 3),
         }
 

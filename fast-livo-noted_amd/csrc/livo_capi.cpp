@@ -28,10 +28,8 @@ struct ScanBuf {
     int64_t n = 0;
     int32_t nblk = 0;
     float* pts = nullptr;  // n x 4
-    float* nn_xyz = nullptr;
-    int32_t* nn_idx = nullptr;
-    float* nn_d = nullptr;
-    int32_t* nn_cnt = nullptr;
+    NNRec* nn = nullptr;   // neighbour records (Nearest_Points cache)
+    std::vector<int32_t> perm;  // stored (Morton) position -> caller's point index
     double* partial = nullptr;  // nblk x kRedCols
     bool searched = false;      // a search has filled the neighbour cache
 };
@@ -73,12 +71,17 @@ struct livo_ctx {
     IekfSlot* h_slots = nullptr;  // pinned
     HsJob* d_jobs = nullptr;
     HsJob* h_jobs = nullptr;      // pinned
+    // exact-replay list of the k-NN passes
+    unsigned* d_replay_count = nullptr;
+    unsigned long long* d_replay_total = nullptr;
+    unsigned long long* d_replay_list = nullptr;
+    int64_t replay_cap = 0;
     // scratch for livo_knn / debug outputs
     void* scratch = nullptr;
     size_t scratch_bytes = 0;
     // profiling
     int profiling = 0;
-    hipEvent_t ev[2 * LIVO_MAX_EVALS + 2] = {};
+    hipEvent_t ev[3 * LIVO_MAX_EVALS + 2] = {};
     bool events_ready = false;
     livo_timings last{};
 };
@@ -124,9 +127,71 @@ static bool params_valid(const livo_params* p) {
            p->flags == 0;
 }
 
+static int ensure_replay(livo_ctx* c, int64_t total) {
+    if (!c->d_replay_count && dev_alloc(&c->d_replay_count, 4)) return LIVO_E_OOM;
+    if (!c->d_replay_total) {
+        if (dev_alloc(&c->d_replay_total, 1)) return LIVO_E_OOM;
+        HIP_TRY(hipMemset(c->d_replay_total, 0, sizeof(unsigned long long)));
+    }
+    if (total <= c->replay_cap) return LIVO_OK;
+    dev_free(c->d_replay_list);
+    c->replay_cap = 0;
+    if (dev_alloc(&c->d_replay_list, (size_t)total)) return LIVO_E_OOM;
+    c->replay_cap = total;
+    return LIVO_OK;
+}
+
+static KnnParams make_knn_params(livo_ctx* c) {
+    KnnParams kp{};
+    kp.nodes = c->nodes;
+    kp.jobs = c->d_jobs;
+    kp.replay_count = c->d_replay_count;
+    kp.replay_list = c->d_replay_list;
+    kp.replay_total = c->d_replay_total;
+    std::memcpy(kp.R_LI, c->params.R_LI, sizeof(kp.R_LI));
+    std::memcpy(kp.t_LI, c->params.t_LI, sizeof(kp.t_LI));
+    kp.has_map = c->has_map && c->map_points > 0 ? 1 : 0;
+    kp.force = -1;
+    kp.depth = c->map_depth;
+    kp.identity = 0;
+    return kp;
+}
+
+// k-NN pass + exact replay of its flagged queries (one replay list per pass).
+static int knn_pass(livo_ctx* c, const KnnParams& kp, int n_jobs, int64_t max_n, bool seeded) {
+    HIP_TRY(hipMemsetAsync(c->d_replay_count, 0, sizeof(unsigned), c->stream));
+    return launch_knn_pass(kp, n_jobs, max_n, seeded, c->stream);
+}
+
+// Morton (Z-order) permutation of the body points: 0.25 m cells, 10 bits/axis.
+static std::vector<int32_t> morton_order(const std::vector<float>& p4, int64_t n) {
+    std::vector<std::pair<uint64_t, int32_t>> key((size_t)n);
+    float lo[3] = {INFINITY, INFINITY, INFINITY};
+    for (int64_t i = 0; i < n; i++)
+        for (int a = 0; a < 3; a++) lo[a] = std::min(lo[a], p4[4 * i + a]);
+    for (int64_t i = 0; i < n; i++) {
+        uint64_t code = 0;
+        uint32_t q[3];
+        for (int a = 0; a < 3; a++) {
+            float f = (p4[4 * i + a] - lo[a]) * 4.0f;
+            if (!(f >= 0.0f)) f = 0.0f;
+            q[a] = (uint32_t)std::min(f, 1048575.0f);
+        }
+        for (int b = 0; b < 20; b++)
+            for (int a = 0; a < 3; a++) code |= (uint64_t)((q[a] >> b) & 1u) << (3 * b + a);
+        key[i] = {code, (int32_t)i};
+    }
+    std::stable_sort(key.begin(), key.end(),
+                     [](const std::pair<uint64_t, int32_t>& x, const std::pair<uint64_t, int32_t>& y) {
+                         return x.first < y.first;
+                     });
+    std::vector<int32_t> perm((size_t)n);
+    for (int64_t i = 0; i < n; i++) perm[i] = key[i].second;
+    return perm;
+}
+
 static HsParams make_hs_params(livo_ctx* c) {
     HsParams hp{};
-    hp.nodes = c->nodes;
     hp.jobs = c->d_jobs;
     std::memcpy(hp.R_LI, c->params.R_LI, sizeof(hp.R_LI));
     std::memcpy(hp.t_LI, c->params.t_LI, sizeof(hp.t_LI));
@@ -134,17 +199,13 @@ static HsParams make_hs_params(livo_ctx* c) {
     hp.max_res = c->params.max_residual;
     hp.plane_thr = c->params.plane_threshold;
     hp.max_sqd = c->params.max_nn_sqdist;
-    hp.has_map = c->has_map && c->map_points > 0 ? 1 : 0;
     hp.force = -1;
     return hp;
 }
 
 static void fill_job(HsJob& j, ScanBuf& s, IekfSlot* slot) {
     j.pts = s.pts;
-    j.nn_xyz = s.nn_xyz;
-    j.nn_idx = s.nn_idx;
-    j.nn_d = s.nn_d;
-    j.nn_cnt = s.nn_cnt;
+    j.nn = s.nn;
     j.partial = s.partial;
     j.slot = slot;
     j.n = (int32_t)s.n;
@@ -218,10 +279,13 @@ int livo_ctx_destroy(livo_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto& s : c->scans) {
-        dev_free(s.pts); dev_free(s.nn_xyz); dev_free(s.nn_idx); dev_free(s.nn_d); dev_free(s.nn_cnt);
+        dev_free(s.pts); dev_free(s.nn);
         dev_free(s.partial);
     }
     dev_free(c->nodes);
+    dev_free(c->d_replay_count);
+    dev_free(c->d_replay_total);
+    dev_free(c->d_replay_list);
     dev_free(c->d_slots);
     dev_free(c->d_jobs);
     if (c->h_slots) (void)hipHostFree(c->h_slots);
@@ -298,21 +362,44 @@ int livo_knn(livo_ctx* c, const float* q, int64_t n, int32_t k, int32_t* idx, fl
     if (!c || n < 0 || k < 1 || k > kNN || (n > 0 && (!q || !idx || !d))) return LIVO_E_INVALID;
     if (!c->has_map) return LIVO_E_NOMAP;
     if (n == 0) return LIVO_OK;
+    if (n > (int64_t)0x7FFFFFFF - kBlock) return LIVO_E_RANGE;
     if (set_device(c)) return LIVO_E_HIP;
-    const size_t qb = (size_t)n * 3 * sizeof(float), ib = (size_t)n * k * sizeof(int32_t),
-                 db = (size_t)n * k * sizeof(float);
-    int rc = ensure_scratch(c, qb + ib + db + 64);
+    int rc = ensure_slots(c, 1);
+    if (rc) return rc;
+    const size_t qb = (size_t)n * 4 * sizeof(float), rb = (size_t)n * sizeof(NNRec);
+    rc = ensure_scratch(c, qb + rb + 256);
     if (rc) return rc;
     char* base = (char*)c->scratch;
     float* dq = (float*)base;
-    int32_t* di = (int32_t*)(base + qb);
-    float* dd = (float*)(base + qb + ib);
-    HIP_TRY(hipMemcpyAsync(dq, q, qb, hipMemcpyHostToDevice, c->stream));
-    rc = launch_knn(c->nodes, c->map_points > 0, c->map_depth, dq, n, k, di, dd, c->stream);
+    NNRec* dr = (NNRec*)(base + ((qb + 255) & ~(size_t)255));
+    std::vector<float> hq((size_t)n * 4);
+    for (int64_t i = 0; i < n; i++) {
+        hq[4 * i] = q[3 * i]; hq[4 * i + 1] = q[3 * i + 1]; hq[4 * i + 2] = q[3 * i + 2]; hq[4 * i + 3] = 0.f;
+    }
+    IekfSlot zero{};
+    std::memset(&zero, 0, sizeof(zero));
+    c->h_slots[0] = zero;
+    HsJob& j = c->h_jobs[0];
+    j = HsJob{};
+    j.pts = dq; j.nn = dr; j.slot = c->d_slots; j.n = (int32_t)n; j.nblk = 0;
+    HIP_TRY(hipMemcpyAsync(dq, hq.data(), qb, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->d_slots, c->h_slots, sizeof(IekfSlot), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->d_jobs, c->h_jobs, sizeof(HsJob), hipMemcpyHostToDevice, c->stream));
+    rc = ensure_replay(c, n);
     if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(idx, di, ib, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(d, dd, db, hipMemcpyDeviceToHost, c->stream));
+    KnnParams kp = make_knn_params(c);
+    kp.force = 1;
+    kp.identity = 1;
+    rc = knn_pass(c, kp, 1, n, false);
+    if (rc) return rc;
+    std::vector<NNRec> hr((size_t)n);
+    HIP_TRY(hipMemcpyAsync(hr.data(), dr, rb, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    for (int64_t i = 0; i < n; i++)
+        for (int t = 0; t < k; t++) {
+            idx[i * k + t] = hr[i].idx[t];
+            d[i * k + t] = hr[i].p[t][3];
+        }
     return LIVO_OK;
 }
 
@@ -328,18 +415,15 @@ int livo_scan_upload(livo_ctx* c, const float* xyz, int64_t N, int64_t stride_by
     s.nblk = (int32_t)((N + kBlock - 1) / kBlock);
     int rc = 0;
     rc |= dev_alloc(&s.pts, (size_t)N * 4);
-    rc |= dev_alloc(&s.nn_xyz, (size_t)N * 15);
-    rc |= dev_alloc(&s.nn_idx, (size_t)N * 5);
-    rc |= dev_alloc(&s.nn_d, (size_t)N * 5);
-    rc |= dev_alloc(&s.nn_cnt, (size_t)N);
+    rc |= dev_alloc(&s.nn, (size_t)N);
     rc |= dev_alloc(&s.partial, (size_t)std::max(s.nblk, 1) * kRedCols);
     if (rc) {
-        dev_free(s.pts); dev_free(s.nn_xyz); dev_free(s.nn_idx); dev_free(s.nn_d); dev_free(s.nn_cnt);
+        dev_free(s.pts); dev_free(s.nn);
         dev_free(s.partial);
         return LIVO_E_OOM;
     }
     if (N > 0) {
-        std::vector<float> h((size_t)N * 4);
+        std::vector<float> h((size_t)N * 4), hs((size_t)N * 4);
         const char* base = (const char*)xyz;
         for (int64_t i = 0; i < N; i++) {
             const float* p = (const float*)(base + i * stride_bytes);
@@ -348,8 +432,12 @@ int livo_scan_upload(livo_ctx* c, const float* xyz, int64_t N, int64_t stride_by
             h[4 * i + 2] = p[2];
             h[4 * i + 3] = 0.0f;
         }
-        if (hipMemcpy(s.pts, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) return LIVO_E_HIP;
-        if (hipMemset(s.nn_cnt, 0, (size_t)N * sizeof(int32_t)) != hipSuccess) return LIVO_E_HIP;
+        // stored in Morton order: neighbouring threads search neighbouring regions
+        s.perm = morton_order(h, N);
+        for (int64_t k = 0; k < N; k++)
+            for (int a = 0; a < 4; a++) hs[4 * k + a] = h[4 * (int64_t)s.perm[k] + a];
+        if (hipMemcpy(s.pts, hs.data(), hs.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) return LIVO_E_HIP;
+        if (hipMemset(s.nn, 0, (size_t)N * sizeof(NNRec)) != hipSuccess) return LIVO_E_HIP;
     }
     int32_t id = -1;
     for (size_t i = 0; i < c->scans.size(); i++)
@@ -370,7 +458,7 @@ int livo_scan_release(livo_ctx* c, int32_t id) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     ScanBuf& s = c->scans[id];
-    dev_free(s.pts); dev_free(s.nn_xyz); dev_free(s.nn_idx); dev_free(s.nn_d); dev_free(s.nn_cnt);
+    dev_free(s.pts); dev_free(s.nn);
     dev_free(s.partial);
     s = ScanBuf{};
     return LIVO_OK;
@@ -391,7 +479,7 @@ int livo_h_share(livo_ctx* c, int32_t id, const livo_state* state, int search_en
     int rc = ensure_slots(c, 1);
     if (rc) return rc;
     const int64_t N = s->n;
-    // debug scratch: normvec N*4, sel N, world N*3
+    // debug scratch: normvec N*4, world N*3, sel N
     const size_t nvb = (size_t)N * 16, wb = (size_t)N * 12, sb = (size_t)N;
     rc = ensure_scratch(c, nvb + wb + sb + 64);
     if (rc) return rc;
@@ -406,28 +494,43 @@ int livo_h_share(livo_ctx* c, int32_t id, const livo_state* state, int search_en
     hp.dbg.normvec = want_nv ? (float*)base : nullptr;
     hp.dbg.world = want_w ? (float*)(base + nvb) : nullptr;
     hp.dbg.sel = want_sel ? (uint8_t*)(base + nvb + wb) : nullptr;
-    if (!search_en && !s->searched) {
+    if (search_en) {
+        rc = ensure_replay(c, N);
+        if (rc) return rc;
+        KnnParams kp = make_knn_params(c);
+        kp.force = 1;
+        rc = knn_pass(c, kp, 1, N, false);
+        if (rc) return rc;
+    } else if (!s->searched && N > 0) {
         // no cached neighbours yet: nothing is matched (points_near.size() < 5, :525)
-        if (N > 0) HIP_TRY(hipMemsetAsync(s->nn_cnt, 0, (size_t)N * sizeof(int32_t), c->stream));
+        HIP_TRY(hipMemsetAsync(s->nn, 0, (size_t)N * sizeof(NNRec), c->stream));
     }
-    rc = launch_hshare(hp, 1, std::max(s->nblk, 1), c->map_depth, search_en != 0, c->stream);
+    rc = launch_hshare(hp, 1, std::max(s->nblk, 1), search_en != 0, c->stream);
     if (rc) return rc;
     SolveParams sp{c->d_slots, c->d_jobs, 1};
     rc = launch_solve(sp, 1, c->stream);
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(c->h_slots, c->d_slots, sizeof(IekfSlot), hipMemcpyDeviceToHost, c->stream));
+    std::vector<float> h_nv, h_w;
+    std::vector<uint8_t> h_sel;
     if (N > 0 && out) {
-        if (want_nv) HIP_TRY(hipMemcpyAsync(out->normvec, hp.dbg.normvec, nvb, hipMemcpyDeviceToHost, c->stream));
-        if (want_w) HIP_TRY(hipMemcpyAsync(out->world_xyz, hp.dbg.world, wb, hipMemcpyDeviceToHost, c->stream));
-        if (want_sel) HIP_TRY(hipMemcpyAsync(out->selected, hp.dbg.sel, sb, hipMemcpyDeviceToHost, c->stream));
+        if (want_nv) {
+            h_nv.resize((size_t)N * 4);
+            HIP_TRY(hipMemcpyAsync(h_nv.data(), hp.dbg.normvec, nvb, hipMemcpyDeviceToHost, c->stream));
+        }
+        if (want_w) {
+            h_w.resize((size_t)N * 3);
+            HIP_TRY(hipMemcpyAsync(h_w.data(), hp.dbg.world, wb, hipMemcpyDeviceToHost, c->stream));
+        }
+        if (want_sel) {
+            h_sel.resize((size_t)N);
+            HIP_TRY(hipMemcpyAsync(h_sel.data(), hp.dbg.sel, sb, hipMemcpyDeviceToHost, c->stream));
+        }
     }
-    std::vector<int32_t> idx_t;
-    std::vector<float> d_t;
+    std::vector<NNRec> recs;
     if (N > 0 && out && (out->nn_idx || out->nn_sqdist)) {
-        idx_t.resize((size_t)N * 5);
-        d_t.resize((size_t)N * 5);
-        HIP_TRY(hipMemcpyAsync(idx_t.data(), s->nn_idx, (size_t)N * 5 * 4, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipMemcpyAsync(d_t.data(), s->nn_d, (size_t)N * 5 * 4, hipMemcpyDeviceToHost, c->stream));
+        recs.resize((size_t)N);
+        HIP_TRY(hipMemcpyAsync(recs.data(), s->nn, (size_t)N * sizeof(NNRec), hipMemcpyDeviceToHost, c->stream));
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (search_en) s->searched = true;
@@ -445,11 +548,16 @@ int livo_h_share(livo_ctx* c, int32_t id, const livo_state* state, int search_en
     for (int a = 0; a < 6; a++) HTL[a] = r[21 + a];
     if (effct) *effct = (int64_t)r[28];
     if (out && out->visits) *out->visits = (int64_t)hs.visits[0];
-    if (!idx_t.empty()) {
-        for (int64_t i = 0; i < N; i++)
-            for (int k = 0; k < 5; k++) {
-                if (out->nn_idx) out->nn_idx[i * 5 + k] = idx_t[(size_t)k * N + i];
-                if (out->nn_sqdist) out->nn_sqdist[i * 5 + k] = d_t[(size_t)k * N + i];
+    // per-point outputs come back in the caller's point order (stored order is Morton)
+    for (int64_t k = 0; k < N; k++) {
+        const int64_t i = s->perm[k];
+        if (!h_nv.empty()) std::memcpy(out->normvec + 4 * i, &h_nv[4 * k], 16);
+        if (!h_w.empty()) std::memcpy(out->world_xyz + 3 * i, &h_w[3 * k], 12);
+        if (!h_sel.empty()) out->selected[i] = h_sel[k];
+        if (!recs.empty())
+            for (int j = 0; j < 5; j++) {
+                if (out->nn_idx) out->nn_idx[i * 5 + j] = recs[k].idx[j];
+                if (out->nn_sqdist) out->nn_sqdist[i * 5 + j] = recs[k].p[j][3];
             }
     }
     return LIVO_OK;
@@ -467,30 +575,42 @@ int livo_iekf_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_stat
     if (rc) return rc;
     const int max_iter = c->params.max_iterations;
     int max_nblk = 1;
-    int64_t queries = 0;
+    int64_t max_n = 1, total_n = 0;
     for (int32_t b = 0; b < n; b++) {
         ScanBuf* s = get_scan(c, ids[b]);
         init_slot(c->h_slots[b], states[b], priors ? priors[b] : states[b], max_iter);
         fill_job(c->h_jobs[b], *s, c->d_slots + b);
         max_nblk = std::max(max_nblk, s->nblk);
-        queries += s->n;
+        max_n = std::max<int64_t>(max_n, s->n);
+        total_n += s->n;
     }
     HIP_TRY(hipMemcpyAsync(c->d_slots, c->h_slots, sizeof(IekfSlot) * n, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->d_jobs, c->h_jobs, sizeof(HsJob) * n, hipMemcpyHostToDevice, c->stream));
+    rc = ensure_replay(c, total_n);
+    if (rc) return rc;
     HsParams hp = make_hs_params(c);
+    KnnParams kp = make_knn_params(c);
     SolveParams sp{c->d_slots, c->d_jobs, 0};
     const bool prof = c->profiling && c->events_ready;
     const int evals = max_iter + 1;
     for (int e = 0; e < evals; e++) {
-        if (prof) HIP_TRY(hipEventRecord(c->ev[2 * e], c->stream));
-        rc = launch_hshare(hp, n, max_nblk, c->map_depth, e == 0, c->stream);
+        if (prof) HIP_TRY(hipEventRecord(c->ev[3 * e], c->stream));
+        rc = knn_pass(c, kp, n, max_n, e > 0);  // rematch passes are seeded
         if (rc) return rc;
-        if (prof) HIP_TRY(hipEventRecord(c->ev[2 * e + 1], c->stream));
+        if (prof) HIP_TRY(hipEventRecord(c->ev[3 * e + 1], c->stream));
+        rc = launch_hshare(hp, n, max_nblk, e == 0, c->stream);
+        if (rc) return rc;
+        if (prof) HIP_TRY(hipEventRecord(c->ev[3 * e + 2], c->stream));
         rc = launch_solve(sp, n, c->stream);
         if (rc) return rc;
     }
-    if (prof) HIP_TRY(hipEventRecord(c->ev[2 * LIVO_MAX_EVALS], c->stream));
+    if (prof) HIP_TRY(hipEventRecord(c->ev[3 * LIVO_MAX_EVALS], c->stream));
     HIP_TRY(hipMemcpyAsync(c->h_slots, c->d_slots, sizeof(IekfSlot) * n, hipMemcpyDeviceToHost, c->stream));
+    unsigned long long replays = 0;
+    if (prof) {
+        HIP_TRY(hipMemcpyAsync(&replays, c->d_replay_total, 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemsetAsync(c->d_replay_total, 0, 8, c->stream));
+    }
     HIP_TRY(hipStreamSynchronize(c->stream));
     for (int32_t b = 0; b < n; b++) {
         const IekfSlot& s = c->h_slots[b];
@@ -501,27 +621,29 @@ int livo_iekf_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_stat
     if (prof) {
         livo_timings t{};
         for (int e = 0; e < evals; e++) {
-            float ms_h = 0.f, ms_s = 0.f;
-            (void)hipEventElapsedTime(&ms_h, c->ev[2 * e], c->ev[2 * e + 1]);
-            const hipEvent_t end = (e + 1 < evals) ? c->ev[2 * e + 2] : c->ev[2 * LIVO_MAX_EVALS];
-            (void)hipEventElapsedTime(&ms_s, c->ev[2 * e + 1], end);
+            float ms_k = 0.f, ms_h = 0.f, ms_s = 0.f;
+            (void)hipEventElapsedTime(&ms_k, c->ev[3 * e], c->ev[3 * e + 1]);
+            (void)hipEventElapsedTime(&ms_h, c->ev[3 * e + 1], c->ev[3 * e + 2]);
+            const hipEvent_t end = (e + 1 < evals) ? c->ev[3 * e + 3] : c->ev[3 * LIVO_MAX_EVALS];
+            (void)hipEventElapsedTime(&ms_s, c->ev[3 * e + 2], end);
             if (e == 0) {
-                t.knn_ms += ms_h;
+                t.knn_ms += ms_k;
                 t.knn_launches++;
             } else {
-                t.plane_ms += ms_h;
+                t.rematch_knn_ms += ms_k;
             }
+            t.plane_ms += ms_h;
             t.solve_ms += ms_s;
         }
-        // the first evaluation (k_hshare<true>) searches for every point of every scan
+        // the first evaluation's k_knn_pass<true> searches for every point of every scan
         for (int32_t b = 0; b < n; b++) {
             t.knn_visits += (int64_t)c->h_slots[b].visits[0];
             t.knn_queries += c->scans[ids[b]].n;
             t.effct_points += c->h_slots[b].stats.effct_feat_num[0];
         }
+        t.knn_replays = (int64_t)replays;
         c->last = t;
     }
-    (void)queries;
     return LIVO_OK;
 }
 

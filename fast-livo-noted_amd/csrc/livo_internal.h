@@ -11,6 +11,8 @@ namespace livo {
 constexpr int kNN = LIVO_NUM_MATCH_POINTS;  // 5
 constexpr int kDim = LIVO_DIM_STATE;        // 18
 constexpr int kBlock = 256;                 // threads per block of the per-point kernels
+constexpr int kKnnBlock = 128;              // threads per block of the k-NN pass (LDS stacks)
+constexpr int kSeedCap = 12;                // LDS stack entries of the seeded (rematch) k-NN pass
 constexpr int kRedCols = 32;                // doubles per block partial (29 used)
 constexpr int kRedUsed = 29;                // 21 HTH upper-tri + 6 HTL + residual sum + count
 
@@ -67,13 +69,21 @@ struct alignas(16) IekfSlot {
     int32_t eval_search[LIVO_MAX_EVALS];
 };
 
+// Nearest_Points[i] + pointSearchSqDis for one point: 128 B, written by the
+// k-NN pass, read by every plane-fit pass until the next search.
+struct alignas(16) NNRec {
+    float p[kNN][4];   // x, y, z, squared distance (ascending); +inf pad
+    int32_t idx[kNN];  // map indices (input order of livo_map_build), -1 pad
+    int32_t cnt;       // neighbours found (< 5 only for maps of < 5 points)
+    int32_t flag;      // why the exact replay recomputed it (bits, see k_knn_pass); 0x100: replayed
+    int32_t node[kNN]; // heap node ids of the neighbours (seeds of the next search)
+};
+static_assert(sizeof(NNRec) == 128, "NNRec must be 128 bytes");
+
 // One scan of a batched launch.
 struct HsJob {
     const float* pts;     // N x 4 floats (x, y, z, 0), device
-    float* nn_xyz;        // 15 x N SoA neighbour coordinates (Nearest_Points cache)
-    int32_t* nn_idx;      // 5 x N map indices
-    float* nn_d;          // 5 x N squared distances
-    int32_t* nn_cnt;      // N neighbours found
+    NNRec* nn;            // N neighbour records
     double* partial;      // nblk x kRedCols block partial sums
     IekfSlot* slot;
     int32_t n;
@@ -88,7 +98,6 @@ struct HsDebug {
 };
 
 struct HsParams {
-    const MapNode* nodes;   // slot 0 unused; root at slot 1
     const HsJob* jobs;
     HsDebug dbg;
     double R_LI[9];
@@ -97,8 +106,22 @@ struct HsParams {
     double max_res;         // 2.0
     float plane_thr;        // 0.1f
     float max_sqd;          // 5.0f
-    int32_t has_map;
     int32_t force;          // -1: follow ctrl; 0: no search; 1: search
+    int32_t pad;
+};
+
+struct KnnParams {
+    const MapNode* nodes;   // slot 0 unused; root at slot 1
+    const HsJob* jobs;
+    unsigned* replay_count;            // queries flagged for the exact replay (zeroed per pass)
+    unsigned long long* replay_list;   // (job << 32) | point
+    unsigned long long* replay_total;  // running count of replayed queries (diagnostics)
+    double R_LI[9];
+    double t_LI[3];
+    int32_t has_map;
+    int32_t force;          // -1: follow ctrl; 0: skip; 1: search
+    int32_t depth;          // tree levels (LDS stack entries of the full search)
+    int32_t identity;       // 1: pts are world points already (livo_knn)
 };
 
 struct SolveParams {
@@ -118,9 +141,9 @@ int build_host_map(const float* xyz, int64_t M, int64_t stride_bytes, HostMap* o
 void free_host_map(HostMap* m);
 
 // Kernel launchers (livo_kernels.hip).  All asynchronous on `stream`.
-int launch_hshare(const HsParams& p, int n_jobs, int max_nblk, int depth, bool first, void* stream);
+size_t knn_lds_bytes(int depth, bool seeded);
+int launch_knn_pass(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, void* stream);
+int launch_hshare(const HsParams& p, int n_jobs, int max_nblk, bool first, void* stream);
 int launch_solve(const SolveParams& p, int n_jobs, void* stream);
-int launch_knn(const MapNode* nodes, int has_map, int depth, const float* q, int64_t n, int k, int32_t* idx,
-               float* d, void* stream);
 
 }  // namespace livo

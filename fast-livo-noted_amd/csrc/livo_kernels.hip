@@ -1,23 +1,23 @@
 // livo_kernels.hip — CDNA4 (gfx950) kernels of the LIO scan-to-map IEKF path.
 //
-//   k_hshare<FIRST>  one thread per scan point, 256-thread blocks, grid
-//                    (blocks per scan, scans in the batch):
-//                      pointBodyToWorld            laser_mapping.cpp:662-671
-//                      exact k=5 NN (if searching) ikd_Tree.cpp:350-380, 843-986
-//                      sqdis[4] > 5 gate           laser_mapping.cpp:518
-//                      esti_plane (float QR)       common_lib.h:670-702
-//                      residual / s > 0.9 gate     laser_mapping.cpp:532-543
-//                      |pd2| <= 2 compaction gate  laser_mapping.cpp:552
-//                      H row + HᵀH / HᵀL partials  laser_mapping.cpp:564-593
-//                    FIRST = the first evaluation of an update (iterCount -1),
-//                    which always searches; !FIRST follows the device-side
-//                    nearest_search_en of each scan.  Two symbols so rocprof
-//                    separates the full k-NN pass from the re-fit passes.
-//   k_solve          one 256-thread block per scan: deterministic reduction of
-//                    the block partials, the 18x18 solve, boxplus, convergence
-//                    and rematch control, covariance update
-//                    (laser_mapping.cpp:171-238, common_lib.h:565-587).
-//   k_knn            standalone k-NN (livo_knn).
+//   k_knn_pass<SEEDED> exact k=5 NN of every scan point (ikd_Tree.cpp:350-380,
+//                      843-986) after pointBodyToWorld (laser_mapping.cpp:662-671),
+//                      one point per thread, writing one 128-B neighbour record per
+//                      point (the Nearest_Points cache, laser_mapping.h:165).
+//                      !SEEDED = the first evaluation of an update (every point);
+//                      SEEDED = rematch evaluations (where the device-side
+//                      nearest_search_en of a scan is set), bounded by the
+//                      previous neighbours.  k_knn_replay recomputes the rare
+//                      queries whose answer could depend on tie order with the
+//                      exact reference heap and visiting order.
+//   k_hshare<FIRST>    one thread per point, coalesced: plane fit (esti_plane,
+//                      common_lib.h:670-702), residual and gates
+//                      (laser_mapping.cpp:518,532-543,552), Jacobian row and the
+//                      HᵀH / HᵀL block partials (laser_mapping.cpp:564-593).
+//   k_solve            one 256-thread block per scan: deterministic reduction of
+//                      the block partials, the 18x18 solve, boxplus, convergence
+//                      and rematch control, covariance update
+//                      (laser_mapping.cpp:171-238, common_lib.h:565-587).
 //
 // Numerics: compiled with -ffp-contract=off and correctly rounded f32
 // division/sqrt, and every expression keeps the reference's operation order,
@@ -159,43 +159,259 @@ __device__ __forceinline__ const float4* rec_ptr(const MapNode* nodes, uint32_t 
     return reinterpret_cast<const float4*>(nodes + (size_t)h + 1);
 }
 
-// Exact k-NN with the visiting order of KD_TREE::Search (ikd_Tree.cpp:843-986):
-// at each node the point is offered to the candidate list, then the sons are
-// taken near-first (left on a tie, :869), each only if the list is not full
-// or its box distance is below the current k-th distance at the moment it is
-// reached.  The far son waits on a per-lane stack in LDS (stack[e * stride]).
-// Same visits as the reference, so the candidate set and order are identical,
-// ties included.
-__device__ __forceinline__ void knn_search(const MapNode* __restrict__ nodes, int has_map, float qx, float qy,
-                                           float qz, uint2* stack, int stride, Cands& c, unsigned& visits) {
+__device__ __forceinline__ int level_of(uint32_t h) { return 31 - __clz(h + 1); }
+
+// Reference k-NN: the visiting order of KD_TREE::Search (ikd_Tree.cpp:843-986)
+// with the exact MANUAL_HEAP (ikd_Tree.cpp:1345-1411), without a stack.  At
+// each node the point is offered to the heap; then the sons are taken
+// near-first (left on a tie, :869), each only if the heap is not full or its
+// box distance is below the current top at the moment it is reached.  With
+// heap-ordered records the pending far son of every level fits in one bit of
+// `trail`; when a subtree is finished the traversal jumps to the deepest
+// ancestor with a pending far son, re-reads that (already visited, cached)
+// record for the son's box distance and re-checks it, which is exactly the
+// check a stack pop makes.  Same visits, same candidates, same order, ties
+// included.  Used for the rare queries the fast pass flags (k_knn_replay).
+__device__ __noinline__ void knn_exact(const MapNode* __restrict__ nodes, int has_map, float qx, float qy, float qz,
+                                       Cands& c) {
     KHeap h;
 #pragma unroll
-    for (int j = 0; j < kNN; j++) {
-        h.d[j] = INFINITY;
-        h.x[j] = 0.0f;
-        h.node[j] = 0u;
-    }
+    for (int j = 0; j < kNN; j++) { h.d[j] = INFINITY; h.x[j] = 0.0f; h.node[j] = 0u; }
     h.size = 0;
-    if (!has_map) {
-        kh_extract(h, c);
-        return;
+    uint32_t cur = 0, trail = 0;
+    bool down = true;
+    while (has_map) {
+        const float4* rp = rec_ptr(nodes, cur);
+        const float4 a = rp[0], b = rp[1], cc = rp[2], dd = rp[3];
+        const uint32_t meta = __float_as_uint(a.w);
+        const bool hl = (meta & kLeftBit) != 0u, hr = (meta & kRightBit) != 0u;
+        const float dl = hl ? box_dist(qx, qy, qz, b.x, b.y, b.z, b.w, cc.x, cc.y) : INFINITY;
+        const float dr = hr ? box_dist(qx, qy, qz, cc.z, cc.w, dd.x, dd.y, dd.z, dd.w) : INFINITY;
+        const bool lf = dl <= dr;
+        const uint32_t nnear = 2u * cur + (lf ? 1u : 2u), nfar = 2u * cur + (lf ? 2u : 1u);
+        const float dnear = lf ? dl : dr, dfar = lf ? dr : dl;
+        const bool enear = lf ? hl : hr, efar = lf ? hr : hl;
+        const int lev = level_of(cur);
+        if (down) {
+            const float dx = qx - a.x, dy = qy - a.y, dz = qz - a.z;
+            const float dist = (dx * dx + dy * dy) + dz * dz;  // calc_dist (:1291-1295)
+            if (dist <= INFINITY && (h.size < kNN || dist < h.d[0])) {
+                if (h.size >= kNN) kh_pop(h);  // q.pop(); q.push(current_point)  (:861-863)
+                kh_push(h, dist, a.x, cur);
+            }
+            const bool full = h.size >= kNN;
+            const float top = h.d[0];
+            const bool far_ok = efar && (!full || dfar < top);
+            if (enear && (!full || dnear < top)) {
+                if (far_ok) trail |= (1u << lev);
+                cur = nnear;
+                continue;
+            }
+            if (far_ok) { cur = nfar; continue; }
+        } else {
+            const bool full = h.size >= kNN;
+            const float top = h.d[0];
+            trail &= ~(1u << lev);
+            if (efar && (!full || dfar < top)) { cur = nfar; down = true; continue; }
+        }
+        const uint32_t pend = trail & ((lev > 0) ? ((1u << lev) - 1u) : 0u);
+        if (pend == 0u) break;
+        const int al = 31 - __clz(pend);
+        cur = ((cur + 1u) >> (lev - al)) - 1u;
+        down = false;
     }
+    kh_extract(h, c);
+}
+
+// ------------------------------------------------------- fast candidates --
+// The hot loop keeps the 5 best candidates as a sorted list (compare-and-swap
+// insertion) and searches the same tree exactly, so it returns the exact 5
+// nearest points.  The reference's MANUAL_HEAP / PointType_CMP give the same
+// answer whenever it is unique, i.e. unless two candidates are CMP-equivalent
+// (|Δd| < 1e-10 and equal x: duplicate points), CMP stops being transitive
+// (chains of fuzz-close distances), or a 6th point ties exactly with the 5th.
+// The fast pass flags every query where that can happen: see sl_insert, and
+// a point rejected at exactly the current 5th distance (a tie the reference
+// resolves by visiting order); boxes at exactly that distance are searched
+// rather than pruned, so no tied point is missed.
+// Flagged queries are recomputed by knn_exact (k_knn_replay).
+constexpr float kFuzz = 0x1.b7cdfcp-34f;  // largest float < 1e-10: |d| < 1e-10 <=> |d| <= kFuzz
+
+struct SList {
+    float d[kNN];
+    float x[kNN];
+    uint32_t node[kNN];
+    bool fz[kNN];  // this entry has a fuzz-close partner
+    int n;
+    bool fuzz;     // the container may order differently from MANUAL_HEAP: replay
+};
+
+__device__ __forceinline__ bool cmp_less_f(float da, float xa, float db, float xb) {
+    return (fabsf(da - db) <= kFuzz) ? (xa < xb) : (da < db);
+}
+
+__device__ __forceinline__ void sl_init(SList& s) {
+#pragma unroll
+    for (int j = 0; j < kNN; j++) {
+        s.d[j] = INFINITY;
+        s.x[j] = 0.0f;
+        s.node[j] = 0u;
+        s.fz[j] = false;
+    }
+    s.n = 0;
+    s.fuzz = false;
+}
+
+// Insert keeping PointType_CMP order.  A pair within the fuzz but with
+// different x is still strictly ordered (by x) for both containers; the heap
+// and the list can only part ways on CMP-equivalent entries (fuzz-close and
+// equal x) or on chains of fuzz relations (CMP is then not transitive), and
+// those set `fuzz`.
+__device__ __forceinline__ void sl_insert(SList& s, float d, float x, uint32_t node) {
+    int nclose = 0;
+    bool bad = false;
+    bool close[kNN];
+#pragma unroll
+    for (int j = 0; j < kNN; j++) {
+        close[j] = (j < s.n) && (fabsf(d - s.d[j]) <= kFuzz);
+        nclose += close[j] ? 1 : 0;
+        bad |= close[j] && (x == s.x[j] || s.fz[j]);
+    }
+    s.fuzz |= bad || nclose > 1;
+#pragma unroll
+    for (int j = 0; j < kNN; j++) s.fz[j] = s.fz[j] || close[j];
+    s.d[kNN - 1] = d;
+    s.x[kNN - 1] = x;
+    s.node[kNN - 1] = node;
+    s.fz[kNN - 1] = nclose > 0;
+#pragma unroll
+    for (int j = kNN - 1; j > 0; j--) {
+        const bool sw = cmp_less_f(s.d[j], s.x[j], s.d[j - 1], s.x[j - 1]);
+        const float td = s.d[j], tx = s.x[j];
+        const uint32_t tn = s.node[j];
+        const bool tf = s.fz[j];
+        s.d[j] = sw ? s.d[j - 1] : td;
+        s.x[j] = sw ? s.x[j - 1] : tx;
+        s.node[j] = sw ? s.node[j - 1] : tn;
+        s.fz[j] = sw ? s.fz[j - 1] : tf;
+        s.d[j - 1] = sw ? td : s.d[j - 1];
+        s.x[j - 1] = sw ? tx : s.x[j - 1];
+        s.node[j - 1] = sw ? tn : s.node[j - 1];
+        s.fz[j - 1] = sw ? tf : s.fz[j - 1];
+    }
+    s.n = s.n < kNN ? s.n + 1 : kNN;
+}
+
+__device__ __forceinline__ void world_point(const double* R, const double* pos, const double* RL, const double* tL,
+                                            float bxf, float byf, float bzf, float& wx, float& wy, float& wz) {
+    // pointBodyToWorld (laser_mapping.cpp:662-671): double math, float storage
+    const double bx = bxf, by = byf, bz = bzf;
+    const double ix = ((RL[0] * bx + RL[1] * by) + RL[2] * bz) + tL[0];
+    const double iy = ((RL[3] * bx + RL[4] * by) + RL[5] * bz) + tL[1];
+    const double iz = ((RL[6] * bx + RL[7] * by) + RL[8] * bz) + tL[2];
+    wx = (float)(((R[0] * ix + R[1] * iy) + R[2] * iz) + pos[0]);
+    wy = (float)(((R[3] * ix + R[4] * iy) + R[5] * iz) + pos[1]);
+    wz = (float)(((R[6] * ix + R[7] * iy) + R[8] * iz) + pos[2]);
+}
+
+// One neighbour record per point (Nearest_Points[i] + pointSearchSqDis);
+// flag = 1 if the query goes to the exact replay; node[] = heap ids (seeds of the next search).
+__device__ __forceinline__ void write_nnrec(NNRec* __restrict__ out, const MapNode* __restrict__ nodes, int cnt,
+                                            const float (&d)[kNN], const uint32_t (&node)[kNN], int flag) {
+    float4* o4 = reinterpret_cast<float4*>(out);
+    int32_t idx[kNN];
+#pragma unroll
+    for (int k = 0; k < kNN; k++) {
+        float4 v = make_float4(0.f, 0.f, 0.f, INFINITY);
+        idx[k] = -1;
+        if (k < cnt) {
+            const float4 a = rec_ptr(nodes, node[k])[0];
+            v = make_float4(a.x, a.y, a.z, d[k]);
+            idx[k] = (int32_t)(__float_as_uint(a.w) & kIdxMask);
+        }
+        o4[k] = v;
+    }
+    int4* oi = reinterpret_cast<int4*>(out) + 5;
+    oi[0] = make_int4(idx[0], idx[1], idx[2], idx[3]);
+    oi[1] = make_int4(idx[4], cnt, flag, (int)node[0]);
+    oi[2] = make_int4((int)node[1], (int)node[2], (int)node[3], (int)node[4]);
+}
+
+__device__ __forceinline__ void query_point(const KnnParams& P, const IekfSlot* slot, const float4 b, float& qx,
+                                            float& qy, float& qz) {
+    if (P.identity) {
+        qx = b.x; qy = b.y; qz = b.z;
+    } else {
+        world_point(slot->state.rot, slot->state.pos, P.R_LI, P.t_LI, b.x, b.y, b.z, qx, qy, qz);
+    }
+}
+
+// ---------------------------------------------------------- k-NN pass ----
+// One query per thread, the near-first DFS of the reference with the far sons
+// on a per-lane LDS stack ([entry][lane], conflict-free), sorted-list
+// candidates.  SEEDED (rematch evaluations, !FIRST): the previous search's 5
+// neighbours of the point, re-measured from its new world position, give a
+// bound B >= the new 5th distance; boxes and points farther than B are
+// skipped (they cannot tie with the 5th), which keeps the search and its stack short
+// (kSeedCap entries; overflow is flagged too).  The points are stored in
+// Morton order at upload, so a wave walks one region of the tree.
+template <bool SEEDED>
+__global__ __launch_bounds__(kKnnBlock) void k_knn_pass(KnnParams P) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const HsJob job = P.jobs[blockIdx.y];
+    IekfSlot* slot = job.slot;
+    if (P.force >= 0) {
+        if (!P.force) return;
+    } else {
+        if (slot->ctrl.stop) return;
+        if (SEEDED && !slot->ctrl.search_en) return;
+    }
+    const int i = blockIdx.x * kKnnBlock + threadIdx.x;
+    if (i >= job.n) return;
+    const int cap = SEEDED ? kSeedCap : P.depth;
+    uint2* stack = reinterpret_cast<uint2*>(smem) + threadIdx.x;
+    const MapNode* __restrict__ nodes = P.nodes;
+    float qx, qy, qz;
+    query_point(P, slot, reinterpret_cast<const float4*>(job.pts)[i], qx, qy, qz);
+    SList s;
+    sl_init(s);
+    unsigned flag = 0;  // reason bits: 1 CMP fuzz / equivalence, 2 point tied with the 5th, 16 overflow
+    float B = INFINITY;
+    if (SEEDED) {
+        const int4* rec = reinterpret_cast<const int4*>(job.nn + i);
+        const int4 r6 = rec[6], r7 = rec[7];
+        if (r6.y == kNN) {
+            const uint32_t sn[kNN] = {(uint32_t)r6.w, (uint32_t)r7.x, (uint32_t)r7.y, (uint32_t)r7.z,
+                                      (uint32_t)r7.w};
+            float bmax = 0.0f;
+#pragma unroll
+            for (int k = 0; k < kNN; k++) {
+                const float4 a = rec_ptr(nodes, sn[k])[0];
+                const float dx = qx - a.x, dy = qy - a.y, dz = qz - a.z;
+                const float dist = (dx * dx + dy * dy) + dz * dz;
+                bmax = fmaxf(bmax, dist);
+            }
+            B = bmax;
+        }
+    }
+    unsigned visits = 0;
     uint32_t node = 0;
-    bool has = true;
+    bool has = P.has_map != 0;
     int sp = 0;
     while (true) {
         if (!has) {
-            while (sp > 0) {
-                sp--;
-                const uint2 e = stack[sp * stride];
-                const float de = __uint_as_float(e.y);
-                if (h.size < kNN || de < h.d[0]) {
-                    node = e.x;
-                    has = true;
-                    break;
-                }
+            if (sp == 0) break;
+            sp--;
+            const uint2 e = stack[sp * kKnnBlock];
+            const float de = __uint_as_float(e.y);
+            // boxes at exactly the current 5th distance are searched too (a point
+            // tied with the 5th may hide there): the answer is exact either way
+            if (s.n < kNN || de <= s.d[kNN - 1]) {
+                node = e.x;
+                has = true;
+            } else {
+                continue;
             }
-            if (!has) break;
         }
         const float4* rp = rec_ptr(nodes, node);
         const float4 a = rp[0];
@@ -205,38 +421,120 @@ __device__ __forceinline__ void knn_search(const MapNode* __restrict__ nodes, in
         visits++;
         const uint32_t meta = __float_as_uint(a.w);
         {
-            // calc_dist (ikd_Tree.cpp:1291-1295), float, left to right
             const float dx = qx - a.x, dy = qy - a.y, dz = qz - a.z;
-            const float dist = (dx * dx + dy * dy) + dz * dz;
-            if (dist <= INFINITY && (h.size < kNN || dist < h.d[0])) {
-                if (h.size >= kNN) kh_pop(h);  // q.pop(); q.push(current_point)  (:861-863)
-                kh_push(h, dist, a.x, node);
-            }
+            const float dist = (dx * dx + dy * dy) + dz * dz;  // calc_dist (:1291-1295)
+            const bool full = s.n >= kNN;
+            const float top = s.d[kNN - 1];
+            const bool pass_top = !full || dist < top;
+            // points beyond the seed bound B >= the final 5th distance cannot tie with it
+            if (pass_top && dist <= B) sl_insert(s, dist, a.x, node);  // (NaN fails dist <= B)
+            flag |= (full && dist == top) ? 2u : 0u;
         }
         const bool hl = (meta & kLeftBit) != 0u;
         const bool hr = (meta & kRightBit) != 0u;
         const float dl = hl ? box_dist(qx, qy, qz, b.x, b.y, b.z, b.w, cc.x, cc.y) : INFINITY;
         const float dr = hr ? box_dist(qx, qy, qz, cc.z, cc.w, dd.x, dd.y, dd.z, dd.w) : INFINITY;
         const bool left_first = dl <= dr;
-        const uint32_t nnear = left_first ? 2u * node + 1u : 2u * node + 2u;
-        const uint32_t nfar = left_first ? 2u * node + 2u : 2u * node + 1u;
         const float dnear = left_first ? dl : dr;
         const float dfar = left_first ? dr : dl;
         const bool enear = left_first ? hl : hr;
         const bool efar = left_first ? hr : hl;
-        const bool full = h.size >= kNN;
-        const float top = h.d[0];
-        if (efar && (!full || dfar < top)) {
-            stack[sp * stride] = make_uint2(nfar, __float_as_uint(dfar));
-            sp++;
+        const bool full = s.n >= kNN;
+        const float top = s.d[kNN - 1];
+        const bool far_ok = efar && (!full || dfar <= top) && dfar <= B;
+        if (far_ok) {
+            if (sp < cap) {
+                stack[sp * kKnnBlock] = make_uint2(2u * node + (left_first ? 2u : 1u), __float_as_uint(dfar));
+                sp++;
+            } else {
+                flag |= 16u;  // stack overflow (seeded cap): exact replay
+            }
         }
-        if (enear && (!full || dnear < top)) {
-            node = nnear;
-        } else {
-            has = false;
-        }
+        has = enear && (!full || dnear <= top) && dnear <= B;
+        node = 2u * node + (left_first ? 1u : 2u);
     }
-    kh_extract(h, c);
+    flag |= s.fuzz ? 1u : 0u;
+#ifdef LIVO_LAB_NOFLAGS
+    flag = 0;
+#endif
+    float od[kNN];
+    uint32_t on[kNN];
+#pragma unroll
+    for (int k = 0; k < kNN; k++) { od[k] = s.d[k]; on[k] = s.node[k]; }
+    write_nnrec(job.nn + i, nodes, s.n, od, on, (int)flag);
+    if (flag) {
+        const unsigned slot_i = atomicAdd(P.replay_count, 1u);
+        P.replay_list[slot_i] = ((unsigned long long)blockIdx.y << 32) | (unsigned)i;
+    }
+    unsigned long long wv = visits;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) wv += __shfl_xor(wv, off, 64);
+    if ((threadIdx.x & 63) == 0 && wv) {
+        int e = P.force >= 0 ? 0 : slot->ctrl.n_evals;
+        e = e < LIVO_MAX_EVALS ? e : LIVO_MAX_EVALS - 1;
+        atomicAdd(&slot->visits[e], wv);
+    }
+}
+
+// Exact reference-order recomputation of the queries the fast pass flagged:
+// KD_TREE::Search's visiting order with the far sons on an LDS stack and the
+// exact MANUAL_HEAP (rare: ties / duplicates; one query per thread).
+__global__ __launch_bounds__(64) void k_knn_replay(KnnParams P) {
+    __shared__ uint2 st_lds[kMaxDepth * 64];
+    const unsigned n = *P.replay_count;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && n) atomicAdd(P.replay_total, (unsigned long long)n);
+    uint2* stack = st_lds + threadIdx.x;
+    for (unsigned t = blockIdx.x * 64 + threadIdx.x; t < n; t += gridDim.x * 64) {
+        const unsigned long long e = P.replay_list[t];
+        const HsJob job = P.jobs[(unsigned)(e >> 32)];
+        const int i = (int)(unsigned)(e & 0xffffffffu);
+        float qx, qy, qz;
+        query_point(P, job.slot, reinterpret_cast<const float4*>(job.pts)[i], qx, qy, qz);
+        KHeap h;
+#pragma unroll
+        for (int j = 0; j < kNN; j++) { h.d[j] = INFINITY; h.x[j] = 0.0f; h.node[j] = 0u; }
+        h.size = 0;
+        uint32_t node = 0;
+        bool has = P.has_map != 0;
+        int sp = 0;
+        while (true) {
+            if (!has) {
+                if (sp == 0) break;
+                sp--;
+                const uint2 se = stack[sp * 64];
+                if (h.size < kNN || __uint_as_float(se.y) < h.d[0]) { node = se.x; has = true; }
+                else continue;
+            }
+            const float4* rp = rec_ptr(P.nodes, node);
+            const float4 a = rp[0], b = rp[1], cc = rp[2], dd = rp[3];
+            const uint32_t meta = __float_as_uint(a.w);
+            const float dx = qx - a.x, dy = qy - a.y, dz = qz - a.z;
+            const float dist = (dx * dx + dy * dy) + dz * dz;  // calc_dist (:1291-1295)
+            if (dist <= INFINITY && (h.size < kNN || dist < h.d[0])) {
+                if (h.size >= kNN) kh_pop(h);  // q.pop(); q.push(current_point)  (:861-863)
+                kh_push(h, dist, a.x, node);
+            }
+            const bool hl = (meta & kLeftBit) != 0u, hr = (meta & kRightBit) != 0u;
+            const float dl = hl ? box_dist(qx, qy, qz, b.x, b.y, b.z, b.w, cc.x, cc.y) : INFINITY;
+            const float dr = hr ? box_dist(qx, qy, qz, cc.z, cc.w, dd.x, dd.y, dd.z, dd.w) : INFINITY;
+            const bool lf = dl <= dr;
+            const bool full = h.size >= kNN;
+            const float top = h.d[0];
+            if ((lf ? hr : hl) && (!full || (lf ? dr : dl) < top)) {
+                stack[sp * 64] = make_uint2(2u * node + (lf ? 2u : 1u), __float_as_uint(lf ? dr : dl));
+                sp++;
+            }
+            has = (lf ? hl : hr) && (!full || (lf ? dl : dr) < top);
+            node = 2u * node + (lf ? 1u : 2u);
+        }
+        Cands c;
+        kh_extract(h, c);
+        float od[kNN];
+        uint32_t on[kNN];
+#pragma unroll
+        for (int k = 0; k < kNN; k++) { od[k] = c.d[k]; on[k] = c.node[k]; }
+        write_nnrec(job.nn + i, P.nodes, c.n, od, on, job.nn[i].flag | 0x100);
+    }
 }
 
 // ======================================================== esti_plane ======
@@ -426,7 +724,7 @@ __device__ __forceinline__ double wave_sum(double v) {
 // ===================================================== per-point pass =====
 template <bool FIRST>
 __global__ __launch_bounds__(kBlock) void k_hshare(HsParams P) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ double red_lds[4 * kRedCols];
     const HsJob job = P.jobs[blockIdx.y];
     if ((int)blockIdx.x >= job.nblk) return;
     IekfSlot* slot = job.slot;
@@ -440,75 +738,40 @@ __global__ __launch_bounds__(kBlock) void k_hshare(HsParams P) {
     const int tid = threadIdx.x;
     const int i = blockIdx.x * kBlock + tid;
     const bool valid = i < job.n;
-    double* red_lds = reinterpret_cast<double*>(smem);                       // 4 waves x 32
-    uint2* stack = reinterpret_cast<uint2*>(smem + 4 * kRedCols * sizeof(double));
-
     const livo_state& S = slot->state;
     double acc[kRedUsed];
 #pragma unroll
     for (int j = 0; j < kRedUsed; j++) acc[j] = 0.0;
-    unsigned visits = 0;
 
     if (valid) {
         const float4 pb = reinterpret_cast<const float4*>(job.pts)[i];
-        // pointBodyToWorld (laser_mapping.cpp:662-671): double math, float storage
-        const double bx = pb.x, by = pb.y, bz = pb.z;
-        const double* RL = P.R_LI;
-        const double ix = ((RL[0] * bx + RL[1] * by) + RL[2] * bz) + P.t_LI[0];
-        const double iy = ((RL[3] * bx + RL[4] * by) + RL[5] * bz) + P.t_LI[1];
-        const double iz = ((RL[6] * bx + RL[7] * by) + RL[8] * bz) + P.t_LI[2];
         const double* R = S.rot;
-        const float wx = (float)(((R[0] * ix + R[1] * iy) + R[2] * iz) + S.pos[0]);
-        const float wy = (float)(((R[3] * ix + R[4] * iy) + R[5] * iz) + S.pos[1]);
-        const float wz = (float)(((R[6] * ix + R[7] * iy) + R[8] * iz) + S.pos[2]);
+        float wx, wy, wz;
+        world_point(R, S.pos, P.R_LI, P.t_LI, pb.x, pb.y, pb.z, wx, wy, wz);
         if (P.dbg.world) {
             P.dbg.world[3 * i + 0] = wx;
             P.dbg.world[3 * i + 1] = wy;
             P.dbg.world[3 * i + 2] = wz;
         }
-        const int n = job.n;
+        const float4* rec = reinterpret_cast<const float4*>(job.nn + i);
         float nx[kNN], ny[kNN], nz[kNN];
-        int cnt;
-        bool sel;
-        if (search) {
-            Cands c;
-            knn_search(P.nodes, P.has_map, wx, wy, wz, stack + tid, kBlock, c, visits);
-            cnt = c.n;
+        float d4 = 0.0f;
 #pragma unroll
-            for (int k = 0; k < kNN; k++) {
-                if (k < cnt) {
-                    const float4 a = rec_ptr(P.nodes, c.node[k])[0];
-                    nx[k] = a.x; ny[k] = a.y; nz[k] = a.z;
-                    job.nn_idx[k * n + i] = (int32_t)(__float_as_uint(a.w) & kIdxMask);
-                    job.nn_d[k * n + i] = c.d[k];
-                } else {
-                    nx[k] = ny[k] = nz[k] = 0.0f;
-                    job.nn_idx[k * n + i] = -1;
-                    job.nn_d[k * n + i] = INFINITY;
-                }
-                job.nn_xyz[(3 * k + 0) * n + i] = nx[k];
-                job.nn_xyz[(3 * k + 1) * n + i] = ny[k];
-                job.nn_xyz[(3 * k + 2) * n + i] = nz[k];
-            }
-            job.nn_cnt[i] = cnt;
-            // point_selected_surf[i] = sqdis[4] > 5 ? false : true  (laser_mapping.cpp:518)
-            sel = (cnt == kNN) && !(c.d[kNN - 1] > P.max_sqd);
-        } else {
-            cnt = job.nn_cnt[i];
-#pragma unroll
-            for (int k = 0; k < kNN; k++) {
-                nx[k] = job.nn_xyz[(3 * k + 0) * n + i];
-                ny[k] = job.nn_xyz[(3 * k + 1) * n + i];
-                nz[k] = job.nn_xyz[(3 * k + 2) * n + i];
-            }
-            sel = true;  // point_selected_surf re-initialised each call (:490)
+        for (int k = 0; k < kNN; k++) {
+            const float4 v = rec[k];
+            nx[k] = v.x; ny[k] = v.y; nz[k] = v.z;
+            if (k == kNN - 1) d4 = v.w;
         }
+        const int cnt = reinterpret_cast<const int4*>(job.nn + i)[6].y;
+        // point_selected_surf: sqdis[4] > 5 => false after a search (:518); true otherwise (:490)
+        const bool sel = search ? ((cnt == kNN) && !(d4 > P.max_sqd)) : true;
         bool accepted = false, keep = false;
         float pa[4] = {0.0f, 0.0f, 0.0f, 0.0f};
         float pd2 = 0.0f;
         if (sel && cnt >= kNN) {
             if (esti_plane(nx, ny, nz, P.plane_thr, pa)) {
                 pd2 = ((pa[0] * wx + pa[1] * wy) + pa[2] * wz) + pa[3];
+                const double bx = pb.x, by = pb.y, bz = pb.z;
                 const double bn = sqrt((bx * bx + by * by) + bz * bz);
                 const float s = (float)(1 - 0.9 * (double)fabsf(pd2) / sqrt(bn));
                 accepted = (double)s > 0.9;                          // :535-542
@@ -522,6 +785,11 @@ __global__ __launch_bounds__(kBlock) void k_hshare(HsParams P) {
         if (keep) {
             // Jacobian row (laser_mapping.cpp:564-593): p_I = R_LI p_b + t_LI;
             // A = [p_I]x * rot^T * n;  Hsub = [A, n]
+            const double bx = pb.x, by = pb.y, bz = pb.z;
+            const double* RL = P.R_LI;
+            const double ix = ((RL[0] * bx + RL[1] * by) + RL[2] * bz) + P.t_LI[0];
+            const double iy = ((RL[3] * bx + RL[4] * by) + RL[5] * bz) + P.t_LI[1];
+            const double iz = ((RL[6] * bx + RL[7] * by) + RL[8] * bz) + P.t_LI[2];
             const double cr[9] = {0.0, -iz, iy, iz, 0.0, -ix, -iy, ix, 0.0};
             double M[9];
 #pragma unroll
@@ -557,19 +825,11 @@ __global__ __launch_bounds__(kBlock) void k_hshare(HsParams P) {
         const double v = wave_sum(acc[j]);
         if (lane == 0) red_lds[wave * kRedCols + j] = v;
     }
-    unsigned long long wv = visits;
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) wv += __shfl_xor(wv, off, 64);
     __syncthreads();
     if (tid < kRedUsed) {
         const double v = ((red_lds[0 * kRedCols + tid] + red_lds[1 * kRedCols + tid]) + red_lds[2 * kRedCols + tid]) +
                          red_lds[3 * kRedCols + tid];
         job.partial[(size_t)blockIdx.x * kRedCols + tid] = v;
-    }
-    if (search && lane == 0 && wv) {
-        int e = P.force >= 0 ? 0 : slot->ctrl.n_evals;
-        e = e < LIVO_MAX_EVALS ? e : LIVO_MAX_EVALS - 1;
-        atomicAdd(&slot->visits[e], wv);
     }
 }
 
@@ -851,63 +1111,38 @@ __global__ __launch_bounds__(kBlock) void k_solve(SolveParams P) {
     }
 }
 
-// ====================================================== standalone kNN ====
-__global__ __launch_bounds__(kBlock) void k_knn(const MapNode* nodes, int has_map, const float* q, int64_t n, int k,
-                                                int32_t* idx, float* dout) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint2* stack = reinterpret_cast<uint2*>(smem);
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    Cands c;
-    unsigned v = 0;
-    knn_search(nodes, has_map, q[3 * i], q[3 * i + 1], q[3 * i + 2], stack + threadIdx.x, kBlock, c, v);
-    for (int j = 0; j < k; j++) {
-        float dj = INFINITY;
-        uint32_t nd = 0;
-#pragma unroll
-        for (int t = 0; t < kNN; t++)
-            if (t == j) { dj = c.d[t]; nd = c.node[t]; }
-        if (j < c.n) {
-            const float4 a = rec_ptr(nodes, nd)[0];
-            idx[i * k + j] = (int32_t)(__float_as_uint(a.w) & kIdxMask);
-            dout[i * k + j] = dj;
-        } else {
-            idx[i * k + j] = -1;
-            dout[i * k + j] = INFINITY;
-        }
-    }
-}
-
 // ======================================================== launchers =======
-static size_t hshare_lds(int depth) {
-    const int d = depth > 0 ? depth : 1;
-    return 4 * kRedCols * sizeof(double) + (size_t)d * kBlock * sizeof(uint2);
+size_t knn_lds_bytes(int depth, bool seeded) {
+    const int entries = seeded ? kSeedCap : (depth > 0 ? depth : 1);
+    return (size_t)entries * kKnnBlock * sizeof(uint2);
 }
 
-int launch_hshare(const HsParams& p, int n_jobs, int max_nblk, int depth, bool first, void* stream) {
+int launch_knn_pass(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, void* stream) {
+    if (n_jobs <= 0 || max_n <= 0) return LIVO_OK;
+    dim3 grid((unsigned)((max_n + kKnnBlock - 1) / kKnnBlock), n_jobs), block(kKnnBlock);
+    const size_t lds = knn_lds_bytes(p.depth, seeded);
+    if (seeded)
+        hipLaunchKernelGGL(k_knn_pass<true>, grid, block, lds, (hipStream_t)stream, p);
+    else
+        hipLaunchKernelGGL(k_knn_pass<false>, grid, block, lds, (hipStream_t)stream, p);
+    if (hipGetLastError() != hipSuccess) return LIVO_E_HIP;
+    hipLaunchKernelGGL(k_knn_replay, dim3(64), dim3(64), 0, (hipStream_t)stream, p);
+    return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+
+int launch_hshare(const HsParams& p, int n_jobs, int max_nblk, bool first, void* stream) {
     if (n_jobs <= 0 || max_nblk <= 0) return LIVO_OK;
     dim3 grid(max_nblk, n_jobs), block(kBlock);
-    const size_t lds = hshare_lds(depth);
     if (first)
-        hipLaunchKernelGGL(k_hshare<true>, grid, block, lds, (hipStream_t)stream, p);
+        hipLaunchKernelGGL(k_hshare<true>, grid, block, 0, (hipStream_t)stream, p);
     else
-        hipLaunchKernelGGL(k_hshare<false>, grid, block, lds, (hipStream_t)stream, p);
+        hipLaunchKernelGGL(k_hshare<false>, grid, block, 0, (hipStream_t)stream, p);
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 
 int launch_solve(const SolveParams& p, int n_jobs, void* stream) {
     if (n_jobs <= 0) return LIVO_OK;
     hipLaunchKernelGGL(k_solve, dim3(n_jobs), dim3(kBlock), 0, (hipStream_t)stream, p);
-    return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
-}
-
-int launch_knn(const MapNode* nodes, int has_map, int depth, const float* q, int64_t n, int k, int32_t* idx,
-               float* d, void* stream) {
-    if (n <= 0) return LIVO_OK;
-    const int64_t nblk = (n + kBlock - 1) / kBlock;
-    const size_t lds = (size_t)(depth > 0 ? depth : 1) * kBlock * sizeof(uint2);
-    hipLaunchKernelGGL(k_knn, dim3((unsigned)nblk), dim3(kBlock), lds, (hipStream_t)stream, nodes, has_map, q, n, k,
-                       idx, d);
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 

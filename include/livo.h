@@ -110,16 +110,18 @@ typedef struct livo_point_out {
 } livo_point_out;
 
 /* Device time of the kernels of the last livo_iekf_update* call (profiling mode only).
- * knn_* describe the first evaluation's k_hshare<true> launch, in which every
+ * knn_* describe the first evaluation's k_knn_pass<true> launch, in which every
  * point of every scan runs the k-NN (the dominant kernel). */
 typedef struct livo_timings {
-    double knn_ms;        /* first-evaluation launches (transform + k-NN + plane + H)   */
-    double plane_ms;      /* later evaluations (k-NN only where rematching)             */
-    double solve_ms;      /* reduction + 18x18 solve launches                           */
-    int64_t knn_launches; /* first-evaluation launches timed                            */
-    int64_t knn_visits;   /* tree nodes those launches visited                          */
-    int64_t knn_queries;  /* points those launches processed                            */
-    int64_t effct_points; /* effective points of those launches                         */
+    double knn_ms;         /* first-evaluation k-NN launches                           */
+    double rematch_knn_ms; /* k-NN launches of later evaluations (rematch)             */
+    double plane_ms;       /* plane fit + Jacobian + partial-sum launches (all evals)  */
+    double solve_ms;       /* reduction + 18x18 solve launches                         */
+    int64_t knn_launches;  /* first-evaluation k-NN launches timed                     */
+    int64_t knn_visits;    /* tree nodes those launches visited                        */
+    int64_t knn_queries;   /* points those launches processed                          */
+    int64_t effct_points;  /* effective points of the first evaluation                 */
+    int64_t knn_replays;   /* queries recomputed by the exact tie-order replay (all passes) */
 } livo_timings;
 
 int livo_abi_version(void);

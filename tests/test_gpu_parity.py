@@ -281,3 +281,24 @@ def test_config5_10M_properties(built):
         sid = ctx.scan_upload(body)
         sg, stg = ctx.iekf_update(sid, st0)
         assert stg["iterations"] >= 2 and stg["effct_feat_num"][0] > 150_000
+
+
+def test_iekf_duplicate_map_replays(built):
+    """Every map point duplicated: every k-NN answer hinges on PointType_CMP ties, so the
+    fast pass flags the queries and the exact replay (reference heap + visiting order)
+    must reproduce the oracle bit for bit, in the full and in the seeded rematch passes."""
+    import livo_amd
+    import oracle
+    synth = _synth()
+    base = synth.make_map(30_000)
+    m = np.concatenate([base, base[::-1]])
+    body, _, _ = synth.make_scan(4_000, 8)
+    st0 = synth.make_state(8)
+    tree = oracle.Tree(m)
+    with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=4) as ctx:
+        ctx.map_build(m)
+        sid = ctx.scan_upload(body)
+        g = ctx.h_share(sid, st0, True)
+        r = tree.h_share(body, st0["rot"], st0["pos"], np.eye(3), synth.T_LI, True)
+        _hshare_compare(g, r, len(body))
+        _iekf_compare(ctx, tree, body, st0, 4, synth.T_LI)
