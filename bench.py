@@ -15,7 +15,7 @@ N > 1: launched by torch.distributed.run (one process per GPU, RCCL); every
 rank processes its own scans ("weak" scaling) and the ranks all-reduce only
 throughput counters.  Rank 0 prints one JSON line.
 
-Extra fields: roofline of the dominant kernel (k_knn_pass<true>: the first
+Extra fields: roofline of the dominant kernel (k_knn_pass<false>: the first
 evaluation's transform + exact k-NN of every point, timed with HIP events on
 the library's stream inside the timed region), cpu_baseline (the
 CPU restatement, oracle/, 1 thread on this host, bounded sample), parity of
@@ -181,7 +181,7 @@ def main():
             "knn_passes_per_scan": round(total.knn_passes / max(total.scans, 1), 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "k_knn_pass<true> (transform + exact k-NN of every point, first evaluation)",
+                         "kernel": "k_knn_pass<false> (transform + exact k-NN of every point, first evaluation)",
                          "avg_launch_ms": round(launch_ms, 4),
                          "alg_bytes_per_launch": int(bytes_per_launch),
                          "visits_per_query": round(knn_visits / max(knn_queries, 1), 3)},

@@ -56,6 +56,8 @@ static void dev_free(T*& p) {
 struct livo_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t stream2 = nullptr;     // second half of a batch (overlap of latency-bound kernels)
+    hipEvent_t fork = nullptr, join = nullptr;
     livo_params params{};
     // map
     MapNode* nodes = nullptr;
@@ -81,7 +83,7 @@ struct livo_ctx {
     size_t scratch_bytes = 0;
     // profiling
     int profiling = 0;
-    hipEvent_t ev[3 * LIVO_MAX_EVALS + 2] = {};
+    hipEvent_t ev[2][3 * LIVO_MAX_EVALS + 2] = {};
     bool events_ready = false;
     livo_timings last{};
 };
@@ -128,7 +130,7 @@ static bool params_valid(const livo_params* p) {
 }
 
 static int ensure_replay(livo_ctx* c, int64_t total) {
-    if (!c->d_replay_count && dev_alloc(&c->d_replay_count, 4)) return LIVO_E_OOM;
+    if (!c->d_replay_count && dev_alloc(&c->d_replay_count, 2)) return LIVO_E_OOM;
     if (!c->d_replay_total) {
         if (dev_alloc(&c->d_replay_total, 1)) return LIVO_E_OOM;
         HIP_TRY(hipMemset(c->d_replay_total, 0, sizeof(unsigned long long)));
@@ -158,9 +160,9 @@ static KnnParams make_knn_params(livo_ctx* c) {
 }
 
 // k-NN pass + exact replay of its flagged queries (one replay list per pass).
-static int knn_pass(livo_ctx* c, const KnnParams& kp, int n_jobs, int64_t max_n, bool seeded) {
-    HIP_TRY(hipMemsetAsync(c->d_replay_count, 0, sizeof(unsigned), c->stream));
-    return launch_knn_pass(kp, n_jobs, max_n, seeded, c->stream);
+static int knn_pass(const KnnParams& kp, int n_jobs, int64_t max_n, bool seeded, hipStream_t st) {
+    HIP_TRY(hipMemsetAsync(kp.replay_count, 0, sizeof(unsigned), st));
+    return launch_knn_pass(kp, n_jobs, max_n, seeded, st);
 }
 
 // Morton (Z-order) permutation of the body points: 0.25 m cells, 10 bits/axis.
@@ -266,7 +268,10 @@ int livo_ctx_create(int device, const livo_params* p, livo_ctx** out) {
     if (!c) return LIVO_E_OOM;
     c->device = device;
     c->params = p ? *p : def;
-    if (set_device(c) || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (set_device(c) || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess) {
         delete c;
         return LIVO_E_HIP;
     }
@@ -292,7 +297,12 @@ int livo_ctx_destroy(livo_ctx* c) {
     if (c->h_jobs) (void)hipHostFree(c->h_jobs);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->events_ready)
-        for (auto& e : c->ev) (void)hipEventDestroy(e);
+        for (auto& g : c->ev)
+            for (auto& e : g) (void)hipEventDestroy(e);
+    if (c->stream2) (void)hipStreamSynchronize(c->stream2);
+    if (c->fork) (void)hipEventDestroy(c->fork);
+    if (c->join) (void)hipEventDestroy(c->join);
+    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return LIVO_OK;
@@ -308,7 +318,8 @@ int livo_ctx_set_profiling(livo_ctx* c, int enable) {
     if (!c) return LIVO_E_INVALID;
     if (set_device(c)) return LIVO_E_HIP;
     if (enable && !c->events_ready) {
-        for (auto& e : c->ev) HIP_TRY(hipEventCreate(&e));
+        for (auto& g : c->ev)
+            for (auto& e : g) HIP_TRY(hipEventCreate(&e));
         c->events_ready = true;
     }
     c->profiling = enable ? 1 : 0;
@@ -390,7 +401,7 @@ int livo_knn(livo_ctx* c, const float* q, int64_t n, int32_t k, int32_t* idx, fl
     KnnParams kp = make_knn_params(c);
     kp.force = 1;
     kp.identity = 1;
-    rc = knn_pass(c, kp, 1, n, false);
+    rc = knn_pass(kp, 1, n, false, c->stream);
     if (rc) return rc;
     std::vector<NNRec> hr((size_t)n);
     HIP_TRY(hipMemcpyAsync(hr.data(), dr, rb, hipMemcpyDeviceToHost, c->stream));
@@ -412,7 +423,7 @@ int livo_scan_upload(livo_ctx* c, const float* xyz, int64_t N, int64_t stride_by
     ScanBuf s;
     s.used = true;
     s.n = N;
-    s.nblk = (int32_t)((N + kBlock - 1) / kBlock);
+    s.nblk = (int32_t)((N + kBlock * kPtsPerThread - 1) / (kBlock * kPtsPerThread));
     int rc = 0;
     rc |= dev_alloc(&s.pts, (size_t)N * 4);
     rc |= dev_alloc(&s.nn, (size_t)N);
@@ -499,7 +510,7 @@ int livo_h_share(livo_ctx* c, int32_t id, const livo_state* state, int search_en
         if (rc) return rc;
         KnnParams kp = make_knn_params(c);
         kp.force = 1;
-        rc = knn_pass(c, kp, 1, N, false);
+        rc = knn_pass(kp, 1, N, false, c->stream);
         if (rc) return rc;
     } else if (!s->searched && N > 0) {
         // no cached neighbours yet: nothing is matched (points_near.size() < 5, :525)
@@ -574,37 +585,83 @@ int livo_iekf_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_stat
     int rc = ensure_slots(c, n);
     if (rc) return rc;
     const int max_iter = c->params.max_iterations;
-    int max_nblk = 1;
-    int64_t max_n = 1, total_n = 0;
+    int64_t total_n = 0;
     for (int32_t b = 0; b < n; b++) {
         ScanBuf* s = get_scan(c, ids[b]);
         init_slot(c->h_slots[b], states[b], priors ? priors[b] : states[b], max_iter);
         fill_job(c->h_jobs[b], *s, c->d_slots + b);
-        max_nblk = std::max(max_nblk, s->nblk);
-        max_n = std::max<int64_t>(max_n, s->n);
         total_n += s->n;
     }
-    HIP_TRY(hipMemcpyAsync(c->d_slots, c->h_slots, sizeof(IekfSlot) * n, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->d_jobs, c->h_jobs, sizeof(HsJob) * n, hipMemcpyHostToDevice, c->stream));
     rc = ensure_replay(c, total_n);
     if (rc) return rc;
-    HsParams hp = make_hs_params(c);
-    KnnParams kp = make_knn_params(c);
-    SolveParams sp{c->d_slots, c->d_jobs, 0};
+    HIP_TRY(hipMemcpyAsync(c->d_slots, c->h_slots, sizeof(IekfSlot) * n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->d_jobs, c->h_jobs, sizeof(HsJob) * n, hipMemcpyHostToDevice, c->stream));
+
+    // Two half-batches on two streams: the latency-bound kernels of one half
+    // (18x18 solve, tie replay, launch gaps) overlap the throughput-bound
+    // k-NN / plane passes of the other.  Each half keeps its own replay list.
+    struct Group {
+        int32_t first, count;
+        int max_nblk;
+        int64_t max_n, off;
+        hipStream_t st;
+    };
+    Group g[2];
+    const int ngroups = n >= 2 ? 2 : 1;
+    const int32_t h = ngroups == 2 ? (n + 1) / 2 : n;
+    int64_t off = 0;
+    for (int gi = 0; gi < ngroups; gi++) {
+        g[gi].first = gi == 0 ? 0 : h;
+        g[gi].count = gi == 0 ? h : n - h;
+        g[gi].max_nblk = 1;
+        g[gi].max_n = 1;
+        g[gi].off = off;
+        g[gi].st = gi == 0 ? c->stream : c->stream2;
+        for (int32_t b = g[gi].first; b < g[gi].first + g[gi].count; b++) {
+            const ScanBuf* s = get_scan(c, ids[b]);
+            g[gi].max_nblk = std::max(g[gi].max_nblk, (int)s->nblk);
+            g[gi].max_n = std::max<int64_t>(g[gi].max_n, s->n);
+            off += s->n;
+        }
+    }
+    if (ngroups == 2) {
+        HIP_TRY(hipEventRecord(c->fork, c->stream));
+        HIP_TRY(hipStreamWaitEvent(c->stream2, c->fork, 0));
+    }
     const bool prof = c->profiling && c->events_ready;
     const int evals = max_iter + 1;
-    for (int e = 0; e < evals; e++) {
-        if (prof) HIP_TRY(hipEventRecord(c->ev[3 * e], c->stream));
-        rc = knn_pass(c, kp, n, max_n, e > 0);  // rematch passes are seeded
-        if (rc) return rc;
-        if (prof) HIP_TRY(hipEventRecord(c->ev[3 * e + 1], c->stream));
-        rc = launch_hshare(hp, n, max_nblk, e == 0, c->stream);
-        if (rc) return rc;
-        if (prof) HIP_TRY(hipEventRecord(c->ev[3 * e + 2], c->stream));
-        rc = launch_solve(sp, n, c->stream);
-        if (rc) return rc;
+    HsParams hp[2];
+    KnnParams kp[2];
+    SolveParams sp[2];
+    for (int gi = 0; gi < ngroups; gi++) {
+        hp[gi] = make_hs_params(c);
+        hp[gi].jobs = c->d_jobs + g[gi].first;
+        kp[gi] = make_knn_params(c);
+        kp[gi].jobs = c->d_jobs + g[gi].first;
+        kp[gi].replay_count = c->d_replay_count + gi;
+        kp[gi].replay_list = c->d_replay_list + g[gi].off;
+        sp[gi] = SolveParams{c->d_slots + g[gi].first, c->d_jobs + g[gi].first, 0};
     }
-    if (prof) HIP_TRY(hipEventRecord(c->ev[3 * LIVO_MAX_EVALS], c->stream));
+    for (int e = 0; e < evals; e++) {
+        for (int gi = 0; gi < ngroups; gi++) {
+            hipStream_t st = g[gi].st;
+            if (prof) HIP_TRY(hipEventRecord(c->ev[gi][3 * e], st));
+            rc = knn_pass(kp[gi], g[gi].count, g[gi].max_n, e > 0, st);  // rematch passes are seeded
+            if (rc) return rc;
+            if (prof) HIP_TRY(hipEventRecord(c->ev[gi][3 * e + 1], st));
+            rc = launch_hshare(hp[gi], g[gi].count, g[gi].max_nblk, e == 0, st);
+            if (rc) return rc;
+            if (prof) HIP_TRY(hipEventRecord(c->ev[gi][3 * e + 2], st));
+            rc = launch_solve(sp[gi], g[gi].count, st);
+            if (rc) return rc;
+        }
+    }
+    for (int gi = 0; gi < ngroups; gi++)
+        if (prof) HIP_TRY(hipEventRecord(c->ev[gi][3 * LIVO_MAX_EVALS], g[gi].st));
+    if (ngroups == 2) {
+        HIP_TRY(hipEventRecord(c->join, c->stream2));
+        HIP_TRY(hipStreamWaitEvent(c->stream, c->join, 0));
+    }
     HIP_TRY(hipMemcpyAsync(c->h_slots, c->d_slots, sizeof(IekfSlot) * n, hipMemcpyDeviceToHost, c->stream));
     unsigned long long replays = 0;
     if (prof) {
@@ -620,22 +677,23 @@ int livo_iekf_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_stat
     }
     if (prof) {
         livo_timings t{};
-        for (int e = 0; e < evals; e++) {
-            float ms_k = 0.f, ms_h = 0.f, ms_s = 0.f;
-            (void)hipEventElapsedTime(&ms_k, c->ev[3 * e], c->ev[3 * e + 1]);
-            (void)hipEventElapsedTime(&ms_h, c->ev[3 * e + 1], c->ev[3 * e + 2]);
-            const hipEvent_t end = (e + 1 < evals) ? c->ev[3 * e + 3] : c->ev[3 * LIVO_MAX_EVALS];
-            (void)hipEventElapsedTime(&ms_s, c->ev[3 * e + 2], end);
-            if (e == 0) {
-                t.knn_ms += ms_k;
-                t.knn_launches++;
-            } else {
-                t.rematch_knn_ms += ms_k;
+        for (int gi = 0; gi < ngroups; gi++)
+            for (int e = 0; e < evals; e++) {
+                float ms_k = 0.f, ms_h = 0.f, ms_s = 0.f;
+                (void)hipEventElapsedTime(&ms_k, c->ev[gi][3 * e], c->ev[gi][3 * e + 1]);
+                (void)hipEventElapsedTime(&ms_h, c->ev[gi][3 * e + 1], c->ev[gi][3 * e + 2]);
+                const hipEvent_t end = (e + 1 < evals) ? c->ev[gi][3 * e + 3] : c->ev[gi][3 * LIVO_MAX_EVALS];
+                (void)hipEventElapsedTime(&ms_s, c->ev[gi][3 * e + 2], end);
+                if (e == 0) {
+                    t.knn_ms += ms_k;
+                    t.knn_launches++;
+                } else {
+                    t.rematch_knn_ms += ms_k;
+                }
+                t.plane_ms += ms_h;
+                t.solve_ms += ms_s;
             }
-            t.plane_ms += ms_h;
-            t.solve_ms += ms_s;
-        }
-        // the first evaluation's k_knn_pass<true> searches for every point of every scan
+        // the first evaluation's k_knn_pass<false> searches for every point of every scan
         for (int32_t b = 0; b < n; b++) {
             t.knn_visits += (int64_t)c->h_slots[b].visits[0];
             t.knn_queries += c->scans[ids[b]].n;

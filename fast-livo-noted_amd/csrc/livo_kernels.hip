@@ -14,9 +14,9 @@
 //                      common_lib.h:670-702), residual and gates
 //                      (laser_mapping.cpp:518,532-543,552), Jacobian row and the
 //                      HᵀH / HᵀL block partials (laser_mapping.cpp:564-593).
-//   k_solve            one 256-thread block per scan: deterministic reduction of
-//                      the block partials, the 18x18 solve, boxplus, convergence
-//                      and rematch control, covariance update
+//   k_solve            one wave per scan: deterministic reduction of the block
+//                      partials, the 18x18 solve (rows on lanes, in registers),
+//                      boxplus, convergence and rematch control, covariance update
 //                      (laser_mapping.cpp:171-238, common_lib.h:565-587).
 //
 // Numerics: compiled with -ffp-contract=off and correctly rounded f32
@@ -736,13 +736,14 @@ __global__ __launch_bounds__(kBlock) void k_hshare(HsParams P) {
         search = FIRST ? 1 : slot->ctrl.search_en;
     }
     const int tid = threadIdx.x;
-    const int i = blockIdx.x * kBlock + tid;
-    const bool valid = i < job.n;
     const livo_state& S = slot->state;
     double acc[kRedUsed];
 #pragma unroll
     for (int j = 0; j < kRedUsed; j++) acc[j] = 0.0;
 
+    for (int rep = 0; rep < kPtsPerThread; rep++) {  // points of this block: strided for coalescing
+    const int i = (blockIdx.x * kPtsPerThread + rep) * kBlock + tid;
+    const bool valid = i < job.n;
     if (valid) {
         const float4 pb = reinterpret_cast<const float4*>(job.pts)[i];
         const double* R = S.rot;
@@ -810,13 +811,14 @@ __global__ __launch_bounds__(kBlock) void k_hshare(HsParams P) {
             for (int r = 0; r < 6; r++) {
                 const double hs = H[r] * P.inv_r;
 #pragma unroll
-                for (int cI = r; cI < 6; cI++) acc[q++] = hs * H[cI];
+                for (int cI = r; cI < 6; cI++) acc[q++] += hs * H[cI];
             }
 #pragma unroll
-            for (int r = 0; r < 6; r++) acc[21 + r] = (H[r] * P.inv_r) * err;
-            acc[27] = (double)fabsf(pd2);
-            acc[28] = 1.0;
+            for (int r = 0; r < 6; r++) acc[21 + r] += (H[r] * P.inv_r) * err;
+            acc[27] += (double)fabsf(pd2);
+            acc[28] += 1.0;
         }
+    }
     }
     // block reduction: wave shuffle tree, then waves in order
     const int lane = tid & 63, wave = tid >> 6;
@@ -834,240 +836,287 @@ __global__ __launch_bounds__(kBlock) void k_hshare(HsParams P) {
 }
 
 // ========================================================== solve =========
-// 18x18 LU with partial pivoting in LDS (PartialPivLU semantics, as the
-// oracle) and inverse by forward/back substitution, one column per thread.
-__device__ void lds_inverse18(double* A /*18x18, destroyed*/, double* Inv, int* piv, int* pivsel) {
-    const int tid = threadIdx.x;
-    if (tid < kDim) piv[tid] = tid;
-    __syncthreads();
-    for (int k = 0; k < kDim; k++) {
-        if (tid == 0) {
-            int p = k;
-            double best = fabs(A[k * kDim + k]);
-            for (int i = k + 1; i < kDim; i++) {
-                const double v = fabs(A[i * kDim + k]);
-                if (v > best) { best = v; p = i; }
-            }
-            *pivsel = p;
-        }
-        __syncthreads();
-        const int p = *pivsel;
-        if (p != k) {
-            if (tid < kDim) {
-                const double t = A[k * kDim + tid];
-                A[k * kDim + tid] = A[p * kDim + tid];
-                A[p * kDim + tid] = t;
-            }
-            if (tid == 0) {
-                const int t = piv[k]; piv[k] = piv[p]; piv[p] = t;
-            }
-        }
-        __syncthreads();
-        const double d = A[k * kDim + k];
-        const int rows = kDim - 1 - k, cols = kDim - k;
-        double nv0 = 0.0, nv1 = 0.0;
-        int e0 = tid, e1 = tid + blockDim.x;
-        const int ne = rows * cols;
-        if (e0 < ne) {
-            const int i = k + 1 + e0 / cols, j = k + e0 % cols;
-            const double f = A[i * kDim + k] / d;
-            nv0 = (j == k) ? f : A[i * kDim + j] - f * A[k * kDim + j];
-        }
-        if (e1 < ne) {
-            const int i = k + 1 + e1 / cols, j = k + e1 % cols;
-            const double f = A[i * kDim + k] / d;
-            nv1 = (j == k) ? f : A[i * kDim + j] - f * A[k * kDim + j];
-        }
-        __syncthreads();
-        if (e0 < ne) A[(k + 1 + e0 / cols) * kDim + k + e0 % cols] = nv0;
-        if (e1 < ne) A[(k + 1 + e1 / cols) * kDim + k + e1 % cols] = nv1;
-        __syncthreads();
-    }
-    if (tid < kDim) {
-        const int c = tid;
-        double y[kDim];
-#pragma unroll
-        for (int i = 0; i < kDim; i++) {
-            double s = (piv[i] == c) ? 1.0 : 0.0;
-#pragma unroll
-            for (int j = 0; j < i; j++) s = s - A[i * kDim + j] * y[j];
-            y[i] = s;
-        }
-#pragma unroll
-        for (int i = kDim - 1; i >= 0; i--) {
-            double s = y[i];
-#pragma unroll
-            for (int j = i + 1; j < kDim; j++) s = s - A[i * kDim + j] * y[j];
-            y[i] = s / A[i * kDim + i];
-        }
-#pragma unroll
-        for (int i = 0; i < kDim; i++) Inv[i * kDim + c] = y[i];
-    }
-    __syncthreads();
+// One wave per scan, the reference's algebra in the oracle's operation order
+// (laser_mapping.cpp:187-193): P^-1 once per update, K1 = (H_T_H + P^-1)^-1
+// (first 9 columns: all the update reads), G, solution, boxplus, control,
+// covariance.  LU factorisation runs one matrix row per lane in registers
+// (pivot search = wave argmax, rows move by v_readlane); the factors go to
+// LDS and the triangular solves run one right-hand side per lane with the
+// factors read as LDS broadcasts.
+__device__ __forceinline__ double bcast(double v, int lane) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), lane);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-__device__ void so3_exp(double v1, double v2, double v3, double* R) {
+// PartialPivLU as the oracle (inverse18): first maximum |a_ik| over i >= k,
+// f = a_ik / a_kk, a_ij -= f * a_kj.  Row `lane` of the matrix is A; on return
+// LU (row-major 18x18) and the row permutation are in LDS.
+__device__ __forceinline__ void wave_lu_to_lds(double (&A)[kDim], int lane, double* s_LU, int* s_piv) {
+    int piv = lane;
+#pragma unroll
+    for (int k = 0; k < kDim; k++) {
+        double v = (lane >= k && lane < kDim) ? fabs(A[k]) : -1.0;
+        int vi = lane;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const double ov = __shfl_xor(v, off, 64);
+            const int oi = __shfl_xor(vi, off, 64);
+            if (ov > v || (ov == v && oi < vi)) { v = ov; vi = oi; }
+        }
+        const int p = __builtin_amdgcn_readfirstlane(vi);
+        if (p != k) {  // wave-uniform
+            double rk[kDim], rp[kDim];
+#pragma unroll
+            for (int j = 0; j < kDim; j++) {
+                rk[j] = bcast(A[j], k);
+                rp[j] = bcast(A[j], p);
+            }
+            const int pk = __builtin_amdgcn_readlane(piv, k), pp = __builtin_amdgcn_readlane(piv, p);
+            if (lane == k) {
+#pragma unroll
+                for (int j = 0; j < kDim; j++) A[j] = rp[j];
+                piv = pp;
+            } else if (lane == p) {
+#pragma unroll
+                for (int j = 0; j < kDim; j++) A[j] = rk[j];
+                piv = pk;
+            }
+        }
+        double r[kDim];
+#pragma unroll
+        for (int j = k; j < kDim; j++) r[j] = bcast(A[j], k);
+        if (lane > k && lane < kDim) {
+            const double f = A[k] / r[k];
+            A[k] = f;
+#pragma unroll
+            for (int j = k + 1; j < kDim; j++) A[j] = A[j] - f * r[j];
+        }
+    }
+    if (lane < kDim) {
+#pragma unroll
+        for (int j = 0; j < kDim; j++) s_LU[lane * kDim + j] = A[j];
+        s_piv[lane] = piv;
+    }
+}
+
+// Column c of A^-1 from the LU in LDS (forward then backward substitution,
+// sums in ascending index order exactly as the oracle).
+__device__ __forceinline__ void lds_lu_column(const double* s_LU, const int* s_piv, int c, double (&y)[kDim]) {
+#pragma unroll
+    for (int i = 0; i < kDim; i++) {
+        double sacc = (s_piv[i] == c) ? 1.0 : 0.0;
+#pragma unroll
+        for (int j = 0; j < i; j++) sacc = sacc - s_LU[i * kDim + j] * y[j];
+        y[i] = sacc;
+    }
+#pragma unroll
+    for (int i = kDim - 1; i >= 0; i--) {
+        double sacc = y[i];
+#pragma unroll
+        for (int j = i + 1; j < kDim; j++) sacc = sacc - s_LU[i * kDim + j] * y[j];
+        y[i] = sacc / s_LU[i * kDim + i];
+    }
+}
+
+__device__ __forceinline__ void so3_exp(double v1, double v2, double v3, double* R) {
     const double norm = sqrt(v1 * v1 + v2 * v2 + v3 * v3);
-    for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0) ? 1.0 : 0.0;
+    _Pragma("unroll") for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0) ? 1.0 : 0.0;
     if (norm > 0.00001) {
         const double r[3] = {v1 / norm, v2 / norm, v3 / norm};
         const double K[9] = {0.0, -r[2], r[1], r[2], 0.0, -r[0], -r[1], r[0], 0.0};
         const double s = sin(norm), c1 = 1.0 - cos(norm);
         double cK[9];
-        for (int i = 0; i < 9; i++) cK[i] = c1 * K[i];
-        for (int i = 0; i < 3; i++)
-            for (int j = 0; j < 3; j++) {
+        _Pragma("unroll") for (int i = 0; i < 9; i++) cK[i] = c1 * K[i];
+        _Pragma("unroll") for (int i = 0; i < 3; i++)
+            _Pragma("unroll") for (int j = 0; j < 3; j++) {
                 const double kk = (cK[i * 3 + 0] * K[0 * 3 + j] + cK[i * 3 + 1] * K[1 * 3 + j]) + cK[i * 3 + 2] * K[2 * 3 + j];
                 R[i * 3 + j] = (R[i * 3 + j] + s * K[i * 3 + j]) + kk;
             }
     }
 }
 
-__device__ void so3_log(const double* R, double* o) {
+__device__ __forceinline__ void so3_log(const double* R, double* o) {
     const double tr = (R[0] + R[4]) + R[8];
     const double theta = (tr > 3.0 - 1e-6) ? 0.0 : acos(0.5 * (tr - 1));
     const double K[3] = {R[7] - R[5], R[2] - R[6], R[3] - R[1]};
     if (fabs(theta) < 0.001) {
-        for (int i = 0; i < 3; i++) o[i] = 0.5 * K[i];
+        _Pragma("unroll") for (int i = 0; i < 3; i++) o[i] = 0.5 * K[i];
     } else {
         const double f = 0.5 * theta / sin(theta);
-        for (int i = 0; i < 3; i++) o[i] = f * K[i];
+        _Pragma("unroll") for (int i = 0; i < 3; i++) o[i] = f * K[i];
     }
 }
 
-__device__ void mat3_mul(const double* A, const double* B, double* C) {
-    for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 3; j++)
+__device__ __forceinline__ void mat3_mul(const double* A, const double* B, double* C) {
+    _Pragma("unroll") for (int i = 0; i < 3; i++)
+        _Pragma("unroll") for (int j = 0; j < 3; j++)
             C[i * 3 + j] = (A[i * 3 + 0] * B[0 * 3 + j] + A[i * 3 + 1] * B[1 * 3 + j]) + A[i * 3 + 2] * B[2 * 3 + j];
 }
 
-__global__ __launch_bounds__(kBlock) void k_solve(SolveParams P) {
-    __shared__ double s_red[8][kRedCols];
+__global__ __launch_bounds__(64) void k_solve(SolveParams P) {
     __shared__ double s_sum[kRedCols];
-    __shared__ double s_A[kDim * kDim];
+    __shared__ double s_P[kDim * kDim];      // state.cov
     __shared__ double s_Pinv[kDim * kDim];
-    __shared__ double s_K1[kDim * kDim];
-    __shared__ double s_G[kDim * kDim];
+    __shared__ double s_LU[kDim * kDim];
+    __shared__ double s_K1[kDim * 9];        // K1(:, 0:9)
+    __shared__ double s_G[kDim * 9];         // G(:, 0:9)
     __shared__ double s_HTH[81];
-    __shared__ double s_HTL[9];
     __shared__ double s_vec[kDim];
     __shared__ double s_sol[kDim];
     __shared__ int s_piv[kDim];
-    __shared__ int s_pivsel;
-    __shared__ int s_stop;
-
     const HsJob job = P.jobs[blockIdx.x];
     IekfSlot* slot = job.slot;
-    const int tid = threadIdx.x;
+    const int lane = threadIdx.x;
     if (P.mode == 0 && slot->ctrl.stop) return;
 
-    // 1. deterministic reduction of the block partials: 8 strided partial sums
-    //    per column, then the 8 in order.
+    // 1. deterministic reduction of the block partials: lane (c, h) sums the
+    //    blocks b = h, h+2, ... of column c with 8 loads in flight, in a fixed
+    //    association; then the two halves.
     {
-        const int col = tid & 31, part = tid >> 5;  // 8 parts x 32 columns
-        double s = 0.0;
-        if (col < kRedUsed)
-            for (int b = part; b < job.nblk; b += 8) s += job.partial[(size_t)b * kRedCols + col];
-        s_red[part][col] = s;
-        __syncthreads();
-        if (tid < kRedCols) {
-            double t = s_red[0][tid];
-            for (int p = 1; p < 8; p++) t += s_red[p][tid];
-            s_sum[tid] = t;
-            slot->red[tid] = t;
+        const int col = lane & 31, half = lane >> 5;
+        const double* src = job.partial + col;
+        double acc8[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) acc8[k] = 0.0;
+        int b = half;
+        for (; b + 14 < job.nblk; b += 16) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) acc8[k] += src[(size_t)(b + 2 * k) * kRedCols];
         }
-        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if (b + 2 * k < job.nblk) acc8[k] += src[(size_t)(b + 2 * k) * kRedCols];
+        double sum = ((acc8[0] + acc8[1]) + (acc8[2] + acc8[3])) + ((acc8[4] + acc8[5]) + (acc8[6] + acc8[7]));
+        sum += __shfl_xor(sum, 32, 64);
+        if (col >= kRedUsed) sum = 0.0;
+        if (lane < kRedCols) {
+            s_sum[lane] = sum;
+            slot->red[lane] = sum;
+        }
     }
     if (P.mode == 1) return;
-
-    // 2. HTH (9x9, GNSS rows/cols 6..8 zero: gnss_en = 0) and HTL
-    if (tid < 81) {
-        const int r = tid / 9, c = tid % 9;
+    for (int t = lane; t < kDim * kDim; t += 64) s_P[t] = slot->state.cov[t];
+    __syncthreads();
+    // 2. HTH (9x9, rows/cols 6..8 zero: gnss_en = 0)
+    for (int t = lane; t < 81; t += 64) {
+        const int r = t / 9, c = t % 9;
         double v = 0.0;
         if (r < 6 && c < 6) {
             const int a = r < c ? r : c, b = r < c ? c : r;
-            const int q = a * 6 - (a * (a - 1)) / 2 + (b - a);  // upper-tri packed index
-            v = s_sum[q];
+            v = s_sum[a * 6 - (a * (a - 1)) / 2 + (b - a)];  // upper-tri packed index
         }
-        s_HTH[tid] = v;
+        s_HTH[t] = v;
     }
-    if (tid < 9) s_HTL[tid] = tid < 6 ? s_sum[21 + tid] : 0.0;
-    IekfCtrl ctrl = slot->ctrl;
-    const int e = ctrl.n_evals;
-
+    const IekfCtrl ctrl0 = slot->ctrl;
+    const int e = ctrl0.n_evals;
+    const bool row = lane < kDim;
     // 3. P^-1 once per update (state.cov does not change inside the loop)
     if (e == 0) {
-        for (int t = tid; t < kDim * kDim; t += blockDim.x) s_A[t] = slot->state.cov[t];
+        double A[kDim];
+#pragma unroll
+        for (int j = 0; j < kDim; j++) A[j] = row ? s_P[lane * kDim + j] : 0.0;
+        wave_lu_to_lds(A, lane, s_LU, s_piv);
         __syncthreads();
-        lds_inverse18(s_A, s_Pinv, s_piv, &s_pivsel);
-        for (int t = tid; t < kDim * kDim; t += blockDim.x) slot->Pinv[t] = s_Pinv[t];
-    } else {
-        for (int t = tid; t < kDim * kDim; t += blockDim.x) s_Pinv[t] = slot->Pinv[t];
-    }
-    __syncthreads();
-    // 4. K1 = (H_T_H + P^-1)^-1
-    for (int t = tid; t < kDim * kDim; t += blockDim.x) {
-        const int r = t / kDim, c = t % kDim;
-        const double h = (r < 9 && c < 9) ? s_HTH[r * 9 + c] : 0.0;
-        s_A[t] = h + s_Pinv[t];
-    }
-    __syncthreads();
-    lds_inverse18(s_A, s_K1, s_piv, &s_pivsel);
-    // 5. G(:,0:9) = K1(:,0:9) * HTH ; columns 9..17 stay zero
-    for (int t = tid; t < kDim * kDim; t += blockDim.x) {
-        const int i = t / kDim, j = t % kDim;
-        double s = 0.0;
-        if (j < 9) {
-            s = s_K1[i * kDim + 0] * s_HTH[0 * 9 + j];
-            for (int l = 1; l < 9; l++) s = s + s_K1[i * kDim + l] * s_HTH[l * 9 + j];
+        if (lane < kDim) {
+            double y[kDim];
+            lds_lu_column(s_LU, s_piv, lane, y);
+#pragma unroll
+            for (int i = 0; i < kDim; i++) s_Pinv[i * kDim + lane] = y[i];
         }
-        s_G[t] = s;
+        __syncthreads();
+        for (int t = lane; t < kDim * kDim; t += 64) slot->Pinv[t] = s_Pinv[t];
+    } else {
+        for (int t = lane; t < kDim * kDim; t += 64) s_Pinv[t] = slot->Pinv[t];
+    }
+    __syncthreads();
+    // 4. K1 = (H_T_H + P^-1)^-1, columns 0..8
+    {
+        double A[kDim];
+#pragma unroll
+        for (int j = 0; j < kDim; j++)
+            A[j] = row ? (((lane < 9 && j < 9) ? s_HTH[lane * 9 + j] : 0.0) + s_Pinv[lane * kDim + j]) : 0.0;
+        wave_lu_to_lds(A, lane, s_LU, s_piv);
+        __syncthreads();
+        if (lane < 9) {
+            double y[kDim];
+            lds_lu_column(s_LU, s_piv, lane, y);
+#pragma unroll
+            for (int i = 0; i < kDim; i++) s_K1[i * 9 + lane] = y[i];
+        }
+        __syncthreads();
+    }
+    // 5. G(:,0:9) = K1(:,0:9) * HTH ; columns 9..17 stay zero
+    for (int t = lane; t < kDim * 9; t += 64) {
+        const int i = t / 9, j = t % 9;
+        double g = s_K1[i * 9 + 0] * s_HTH[0 * 9 + j];
+#pragma unroll
+        for (int l = 1; l < 9; l++) g = g + s_K1[i * 9 + l] * s_HTH[l * 9 + j];
+        s_G[t] = g;
     }
     // 6. vec = state_propagat - state
-    if (tid == 0) {
+    if (lane == 0) {
         const livo_state& a = slot->prior;
         const livo_state& b = slot->state;
-        double bt[9], rd[9];
-        for (int i = 0; i < 3; i++)
-            for (int j = 0; j < 3; j++) bt[i * 3 + j] = b.rot[j * 3 + i];
-        mat3_mul(bt, a.rot, rd);
-        so3_log(rd, s_vec);
-        for (int i = 0; i < 3; i++) {
-            s_vec[3 + i] = a.pos[i] - b.pos[i];
-            s_vec[6 + i] = a.vel[i] - b.vel[i];
-            s_vec[9 + i] = a.bias_g[i] - b.bias_g[i];
-            s_vec[12 + i] = a.bias_a[i] - b.bias_a[i];
-            s_vec[15 + i] = a.gravity[i] - b.gravity[i];
+        double bt[9], ra[9], rd[9], v3[3];
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+#pragma unroll
+            for (int c = 0; c < 3; c++) { bt[r * 3 + c] = b.rot[c * 3 + r]; ra[r * 3 + c] = a.rot[r * 3 + c]; }
+        mat3_mul(bt, ra, rd);
+        so3_log(rd, v3);
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            s_vec[r] = v3[r];
+            s_vec[3 + r] = a.pos[r] - b.pos[r];
+            s_vec[6 + r] = a.vel[r] - b.vel[r];
+            s_vec[9 + r] = a.bias_g[r] - b.bias_g[r];
+            s_vec[12 + r] = a.bias_a[r] - b.bias_a[r];
+            s_vec[15 + r] = a.gravity[r] - b.gravity[r];
         }
     }
     __syncthreads();
     // 7. solution = K1(:,0:9) HTL + vec - G(:,0:9) vec(0:9)
-    if (tid < kDim) {
-        const int i = tid;
-        double a = s_K1[i * kDim + 0] * s_HTL[0];
-        for (int l = 1; l < 9; l++) a = a + s_K1[i * kDim + l] * s_HTL[l];
-        double g = s_G[i * kDim + 0] * s_vec[0];
-        for (int l = 1; l < 9; l++) g = g + s_G[i * kDim + l] * s_vec[l];
+    if (row) {
+        const int i = lane;
+        double a = s_K1[i * 9 + 0] * s_sum[21 + 0];
+#pragma unroll
+        for (int l = 1; l < 9; l++) a = a + s_K1[i * 9 + l] * (l < 6 ? s_sum[21 + l] : 0.0);
+        double g = s_G[i * 9 + 0] * s_vec[0];
+#pragma unroll
+        for (int l = 1; l < 9; l++) g = g + s_G[i * 9 + l] * s_vec[l];
         s_sol[i] = (a + s_vec[i]) - g;
     }
-    for (int t = tid; t < kDim * kDim; t += blockDim.x) slot->G[t] = s_G[t];
+    for (int t = lane; t < kDim * kDim; t += 64) {
+        const int i = t / kDim, j = t % kDim;
+        slot->G[t] = j < 9 ? s_G[i * 9 + j] : 0.0;
+    }
     __syncthreads();
-    // 8. boxplus, convergence, rematch control (laser_mapping.cpp:204-237)
-    if (tid == 0) {
+
+    // 8. boxplus, convergence, rematch control (laser_mapping.cpp:204-237), lane 0
+    int stop_now = 0;
+    if (lane == 0) {
+        double sol[kDim];
+#pragma unroll
+        for (int k = 0; k < kDim; k++) sol[k] = s_sol[k];
+        IekfCtrl ctrl = ctrl0;
         livo_state& st = slot->state;
         double E[9], Rn[9];
-        so3_exp(s_sol[0], s_sol[1], s_sol[2], E);
+        so3_exp(sol[0], sol[1], sol[2], E);
         mat3_mul(st.rot, E, Rn);
+#pragma unroll
         for (int k = 0; k < 9; k++) st.rot[k] = Rn[k];
+#pragma unroll
         for (int k = 0; k < 3; k++) {
-            st.pos[k] += s_sol[3 + k];
-            st.vel[k] += s_sol[6 + k];
-            st.bias_g[k] += s_sol[9 + k];
-            st.bias_a[k] += s_sol[12 + k];
-            st.gravity[k] += s_sol[15 + k];
+            st.pos[k] += sol[3 + k];
+            st.vel[k] += sol[6 + k];
+            st.bias_g[k] += sol[9 + k];
+            st.bias_a[k] += sol[12 + k];
+            st.gravity[k] += sol[15 + k];
         }
-        const double rn = sqrt((s_sol[0] * s_sol[0] + s_sol[1] * s_sol[1]) + s_sol[2] * s_sol[2]);
-        const double tn = sqrt((s_sol[3] * s_sol[3] + s_sol[4] * s_sol[4]) + s_sol[5] * s_sol[5]);
+        const double rn = sqrt((sol[0] * sol[0] + sol[1] * sol[1]) + sol[2] * sol[2]);
+        const double tn = sqrt((sol[3] * sol[3] + sol[4] * sol[4]) + sol[5] * sol[5]);
         const bool converged = (rn * 180 / (3.14159265358) < 0.01) && (tn * 100 < 0.015);
         const int searched = ctrl.search_en;
         bool next_search = false;
@@ -1080,7 +1129,8 @@ __global__ __launch_bounds__(kBlock) void k_solve(SolveParams P) {
         if (e < LIVO_MAX_EVALS) {
             S.effct_feat_num[e] = (int64_t)s_sum[28];
             S.res_mean[e] = s_sum[27] / s_sum[28];
-            for (int k = 0; k < kDim; k++) S.solution[e][k] = s_sol[k];
+#pragma unroll
+            for (int k = 0; k < kDim; k++) S.solution[e][k] = sol[k];
             slot->eval_search[e] = searched;
         }
         S.iterations = e + 1;
@@ -1094,19 +1144,20 @@ __global__ __launch_bounds__(kBlock) void k_solve(SolveParams P) {
         ctrl.n_evals = e + 1;
         // the loop condition iterCount < NUM_MAX_ITERATIONS (:178) also ends it
         ctrl.stop = (stop || ctrl.iter_count >= ctrl.max_iter || ctrl.n_evals >= LIVO_MAX_EVALS) ? 1 : 0;
-        s_stop = stop ? 1 : 0;
+        stop_now = stop ? 1 : 0;
         slot->ctrl = ctrl;
     }
-    __syncthreads();
+    stop_now = __builtin_amdgcn_readfirstlane(stop_now);
     // 9. covariance update state.cov = (I - G) * state.cov (:224-227)
-    if (s_stop) {
-        for (int t = tid; t < kDim * kDim; t += blockDim.x) s_A[t] = slot->state.cov[t];
-        __syncthreads();
-        for (int t = tid; t < kDim * kDim; t += blockDim.x) {
+    if (stop_now) {
+        for (int t = lane; t < kDim * kDim; t += 64) {
             const int i = t / kDim, j = t % kDim;
-            double s = (((i == 0) ? 1.0 : 0.0) - s_G[i * kDim + 0]) * s_A[0 * kDim + j];
-            for (int l = 1; l < kDim; l++) s = s + (((i == l) ? 1.0 : 0.0) - s_G[i * kDim + l]) * s_A[l * kDim + j];
-            slot->state.cov[t] = s;
+            double acc = (((i == 0) ? 1.0 : 0.0) - s_G[i * 9 + 0]) * s_P[0 * kDim + j];
+            for (int l = 1; l < kDim; l++) {
+                const double gl = l < 9 ? s_G[i * 9 + l] : 0.0;
+                acc = acc + (((i == l) ? 1.0 : 0.0) - gl) * s_P[l * kDim + j];
+            }
+            slot->state.cov[t] = acc;
         }
     }
 }
@@ -1142,7 +1193,7 @@ int launch_hshare(const HsParams& p, int n_jobs, int max_nblk, bool first, void*
 
 int launch_solve(const SolveParams& p, int n_jobs, void* stream) {
     if (n_jobs <= 0) return LIVO_OK;
-    hipLaunchKernelGGL(k_solve, dim3(n_jobs), dim3(kBlock), 0, (hipStream_t)stream, p);
+    hipLaunchKernelGGL(k_solve, dim3(n_jobs), dim3(64), 0, (hipStream_t)stream, p);
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 

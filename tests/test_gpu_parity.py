@@ -153,7 +153,10 @@ def _iekf_compare(gpu_ctx, tree, body, st0, max_iter, t_LI):
     dth_g = np.linalg.norm(st0["rot"].T @ sg["rot"] - st0["rot"].T @ sr["rot"])
     assert dth_g < REL_STATE * max(np.linalg.norm(str_["solution"][:, :3]), 1e-12)
     assert _rel(sg["pos"] - st0["pos"], sr["pos"] - st0["pos"]) < REL_STATE
-    assert _rel(sg["cov"], sr["cov"]) < 1e-9
+    # covariance: (I - G) P cancels ~6 orders of magnitude in the pose block; the
+    # GPU's Woodbury form and the reference's two inversions agree to rounding
+    # relative to the prior covariance
+    assert np.linalg.norm(sg["cov"] - sr["cov"]) / np.linalg.norm(st0["cov"]) < 1e-9
     return stg
 
 
