@@ -43,7 +43,8 @@ def _run(cmd):
 def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(LIB_DIR, exist_ok=True)
     os.makedirs(OBJ_DIR, exist_ok=True)
-    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(ROOT, "include", "livo.h")]
+    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(ROOT, "include", "livo.h")] + \
+        [os.path.join(HERE, "host", f) for f in os.listdir(os.path.join(HERE, "host"))]
     newest = max(os.path.getmtime(d) for d in deps)
     if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= newest:
         return LIB
@@ -61,7 +62,23 @@ def build(force: bool = False, verbose: bool = False) -> str:
     cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-pthread", "-o", LIB + ".tmp"] + objs
     _run(cmd)
     os.replace(LIB + ".tmp", LIB)
+    build_facade_demo(verbose)
     return LIB
+
+
+HOST = os.path.join(HERE, "host")
+FACADE_DEMO = os.path.join(LIB_DIR, "facade_demo")
+
+
+def build_facade_demo(verbose: bool = False) -> str:
+    """The C++ facade (host/laser_mapping_gpu.hpp) driven by host/facade_demo.cpp, linked to the C ABI."""
+    cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-I" + os.path.join(ROOT, "include"), "-I" + HOST,
+           os.path.join(HOST, "facade_demo.cpp"), "-L" + LIB_DIR, "-llivo_hip", "-Wl,-rpath,$ORIGIN",
+           "-o", FACADE_DEMO]
+    if verbose:
+        print(" ".join(cmd))
+    _run(cmd)
+    return FACADE_DEMO
 
 
 if __name__ == "__main__":

@@ -110,7 +110,7 @@ typedef struct livo_point_out {
 } livo_point_out;
 
 /* Device time of the kernels of the last livo_iekf_update* call (profiling mode only).
- * knn_* describe the first evaluation's k_knn_pass<true> launch, in which every
+ * knn_* describe the first evaluation's k_knn_pass<false> launch, in which every
  * point of every scan runs the k-NN (the dominant kernel). */
 typedef struct livo_timings {
     double knn_ms;         /* first-evaluation k-NN launches                           */

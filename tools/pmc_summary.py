@@ -27,7 +27,7 @@ def main(d, workload, out):
     res = {"workload": workload, "kernels": {}}
     for k, cs in per.items():
         res["kernels"][k] = {c: {"mean": sum(v) / len(v), "n": len(v)} for c, v in cs.items()}
-    dom = [k for k in res["kernels"] if "k_hshare<true>" in k]
+    dom = [k for k in res["kernels"] if "k_knn_pass<false>" in k]
     if dom:
         kc = res["kernels"][dom[0]]
         fetch = kc.get("FETCH_SIZE", {}).get("mean")
