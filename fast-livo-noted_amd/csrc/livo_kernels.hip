@@ -224,80 +224,51 @@ __device__ __noinline__ void knn_exact(const MapNode* __restrict__ nodes, int ha
 }
 
 // ------------------------------------------------------- fast candidates --
-// The hot loop keeps the 5 best candidates as a sorted list (compare-and-swap
-// insertion) and searches the same tree exactly, so it returns the exact 5
-// nearest points.  The reference's MANUAL_HEAP / PointType_CMP give the same
-// answer whenever it is unique, i.e. unless two candidates are CMP-equivalent
-// (|Δd| < 1e-10 and equal x: duplicate points), CMP stops being transitive
-// (chains of fuzz-close distances), or a 6th point ties exactly with the 5th.
-// The fast pass flags every query where that can happen: see sl_insert, and
-// a point rejected at exactly the current 5th distance (a tie the reference
-// resolves by visiting order); boxes at exactly that distance are searched
-// rather than pruned, so no tied point is missed.
-// Flagged queries are recomputed by knn_exact (k_knn_replay).
+// The hot loop keeps the 5 best candidates as a list sorted by distance
+// (compare-and-swap insertion) and searches the same tree exactly, so it
+// returns the exact 5 nearest points.  The reference's MANUAL_HEAP ordered by
+// PointType_CMP (distance, x within |Δd| < 1e-10) gives the same points in the
+// same order unless two inserted candidates are fuzz-close (CMP then looks at
+// x, and stops being transitive across chains) or a point ties exactly with
+// the 5th (the reference resolves that by visiting order).  Both are flagged
+// (fuzz-close pairs need |Δd| <= 1e-10, i.e. equal or near-duplicate
+// distances) and recomputed by the exact heap (k_knn_replay); boxes at exactly
+// the 5th distance are searched rather than pruned, so no tied point is missed.
 constexpr float kFuzz = 0x1.b7cdfcp-34f;  // largest float < 1e-10: |d| < 1e-10 <=> |d| <= kFuzz
 
 struct SList {
     float d[kNN];
-    float x[kNN];
     uint32_t node[kNN];
-    bool fz[kNN];  // this entry has a fuzz-close partner
     int n;
-    bool fuzz;     // the container may order differently from MANUAL_HEAP: replay
+    bool fuzz;  // two inserted candidates were fuzz-close: exact replay
 };
-
-__device__ __forceinline__ bool cmp_less_f(float da, float xa, float db, float xb) {
-    return (fabsf(da - db) <= kFuzz) ? (xa < xb) : (da < db);
-}
 
 __device__ __forceinline__ void sl_init(SList& s) {
 #pragma unroll
     for (int j = 0; j < kNN; j++) {
         s.d[j] = INFINITY;
-        s.x[j] = 0.0f;
         s.node[j] = 0u;
-        s.fz[j] = false;
     }
     s.n = 0;
     s.fuzz = false;
 }
 
-// Insert keeping PointType_CMP order.  A pair within the fuzz but with
-// different x is still strictly ordered (by x) for both containers; the heap
-// and the list can only part ways on CMP-equivalent entries (fuzz-close and
-// equal x) or on chains of fuzz relations (CMP is then not transitive), and
-// those set `fuzz`.
-__device__ __forceinline__ void sl_insert(SList& s, float d, float x, uint32_t node) {
-    int nclose = 0;
-    bool bad = false;
-    bool close[kNN];
+__device__ __forceinline__ void sl_insert(SList& s, float d, uint32_t node) {
+    bool close = false;
 #pragma unroll
-    for (int j = 0; j < kNN; j++) {
-        close[j] = (j < s.n) && (fabsf(d - s.d[j]) <= kFuzz);
-        nclose += close[j] ? 1 : 0;
-        bad |= close[j] && (x == s.x[j] || s.fz[j]);
-    }
-    s.fuzz |= bad || nclose > 1;
-#pragma unroll
-    for (int j = 0; j < kNN; j++) s.fz[j] = s.fz[j] || close[j];
+    for (int j = 0; j < kNN; j++) close |= fabsf(d - s.d[j]) <= kFuzz;  // empty slots are +inf
+    s.fuzz |= close;
     s.d[kNN - 1] = d;
-    s.x[kNN - 1] = x;
     s.node[kNN - 1] = node;
-    s.fz[kNN - 1] = nclose > 0;
 #pragma unroll
     for (int j = kNN - 1; j > 0; j--) {
-        const bool sw = cmp_less_f(s.d[j], s.x[j], s.d[j - 1], s.x[j - 1]);
-        const float td = s.d[j], tx = s.x[j];
+        const bool sw = s.d[j] < s.d[j - 1];
+        const float td = s.d[j];
         const uint32_t tn = s.node[j];
-        const bool tf = s.fz[j];
         s.d[j] = sw ? s.d[j - 1] : td;
-        s.x[j] = sw ? s.x[j - 1] : tx;
         s.node[j] = sw ? s.node[j - 1] : tn;
-        s.fz[j] = sw ? s.fz[j - 1] : tf;
         s.d[j - 1] = sw ? td : s.d[j - 1];
-        s.x[j - 1] = sw ? tx : s.x[j - 1];
         s.node[j - 1] = sw ? tn : s.node[j - 1];
-        s.fz[j - 1] = sw ? tf : s.fz[j - 1];
     }
     s.n = s.n < kNN ? s.n + 1 : kNN;
 }
@@ -347,16 +318,19 @@ __device__ __forceinline__ void query_point(const KnnParams& P, const IekfSlot* 
 }
 
 // ---------------------------------------------------------- k-NN pass ----
-// One query per thread, the near-first DFS of the reference with the far sons
-// on a per-lane LDS stack ([entry][lane], conflict-free), sorted-list
-// candidates.  SEEDED (rematch evaluations, !FIRST): the previous search's 5
-// neighbours of the point, re-measured from its new world position, give a
-// bound B >= the new 5th distance; boxes and points farther than B are
-// skipped (they cannot tie with the 5th), which keeps the search and its stack short
-// (kSeedCap entries; overflow is flagged too).  The points are stored in
-// Morton order at upload, so a wave walks one region of the tree.
+// One query per thread, the near-first DFS of the reference with sorted-list
+// candidates.  The pending far sons lie on the current root-to-node path, at
+// most one per level, so the "stack" is a trail bit mask plus one box
+// distance per level in LDS ([level][lane], conflict-free, 4 B per entry):
+// popping takes the deepest pending level and rebuilds the son's heap id from
+// the current node id.  4 B x (depth-1) per lane keeps 8 waves per SIMD
+// resident at 1M points.  SEEDED (rematch evaluations, !FIRST): the previous
+// search's 5 neighbours of the point, re-measured from its new world
+// position, give a bound B >= the new 5th distance; boxes and points farther
+// than B are skipped (they cannot tie with the 5th).  The points are stored
+// in Morton order at upload, so a wave walks one region of the tree.
 template <bool SEEDED>
-__global__ __launch_bounds__(kKnnBlock) void k_knn_pass(KnnParams P) {
+__global__ __launch_bounds__(kKnnBlock, 8) void k_knn_pass(KnnParams P) {  // 8 waves/SIMD: <= 64 VGPRs
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const HsJob job = P.jobs[blockIdx.y];
     IekfSlot* slot = job.slot;
@@ -368,14 +342,15 @@ __global__ __launch_bounds__(kKnnBlock) void k_knn_pass(KnnParams P) {
     }
     const int i = blockIdx.x * kKnnBlock + threadIdx.x;
     if (i >= job.n) return;
-    const int cap = SEEDED ? kSeedCap : P.depth;
-    uint2* stack = reinterpret_cast<uint2*>(smem) + threadIdx.x;
+    // far sons pending on the current path, one per level: the son's id follows
+    // from the path (cur), so only its box distance is kept, per level per lane
+    float* dstack = reinterpret_cast<float*>(smem) + threadIdx.x;
     const MapNode* __restrict__ nodes = P.nodes;
     float qx, qy, qz;
     query_point(P, slot, reinterpret_cast<const float4*>(job.pts)[i], qx, qy, qz);
     SList s;
     sl_init(s);
-    unsigned flag = 0;  // reason bits: 1 CMP fuzz / equivalence, 2 point tied with the 5th, 16 overflow
+    unsigned flag = 0;  // reason bits: 1 CMP fuzz / equivalence, 2 point tied with the 5th
     float B = INFINITY;
     if (SEEDED) {
         const int4* rec = reinterpret_cast<const int4*>(job.nn + i);
@@ -395,24 +370,23 @@ __global__ __launch_bounds__(kKnnBlock) void k_knn_pass(KnnParams P) {
         }
     }
     unsigned visits = 0;
-    uint32_t node = 0;
+    uint32_t node = 0, cur = 0;
+    uint32_t trail = 0;  // bit L: a far son at level L is pending (its box distance in dstack[L-1])
     bool has = P.has_map != 0;
-    int sp = 0;
     while (true) {
         if (!has) {
-            if (sp == 0) break;
-            sp--;
-            const uint2 e = stack[sp * kKnnBlock];
-            const float de = __uint_as_float(e.y);
+            if (trail == 0u) break;
+            const int L = 31 - __clz(trail);
+            trail &= ~(1u << L);
+            const float de = dstack[(L - 1) * kKnnBlock];
             // boxes at exactly the current 5th distance are searched too (a point
             // tied with the 5th may hide there): the answer is exact either way
-            if (s.n < kNN || de <= s.d[kNN - 1]) {
-                node = e.x;
-                has = true;
-            } else {
-                continue;
-            }
+            if (!(s.n < kNN || de <= s.d[kNN - 1])) continue;
+            // the pending son is the sibling of cur's ancestor at level L
+            const uint32_t a = ((cur + 1u) >> (level_of(cur) - L)) - 1u;
+            node = ((a - 1u) ^ 1u) + 1u;
         }
+        cur = node;
         const float4* rp = rec_ptr(nodes, node);
         const float4 a = rp[0];
         const float4 b = rp[1];
@@ -427,7 +401,7 @@ __global__ __launch_bounds__(kKnnBlock) void k_knn_pass(KnnParams P) {
             const float top = s.d[kNN - 1];
             const bool pass_top = !full || dist < top;
             // points beyond the seed bound B >= the final 5th distance cannot tie with it
-            if (pass_top && dist <= B) sl_insert(s, dist, a.x, node);  // (NaN fails dist <= B)
+            if (pass_top && dist <= B) sl_insert(s, dist, node);  // (NaN fails dist <= B)
             flag |= (full && dist == top) ? 2u : 0u;
         }
         const bool hl = (meta & kLeftBit) != 0u;
@@ -441,14 +415,10 @@ __global__ __launch_bounds__(kKnnBlock) void k_knn_pass(KnnParams P) {
         const bool efar = left_first ? hr : hl;
         const bool full = s.n >= kNN;
         const float top = s.d[kNN - 1];
-        const bool far_ok = efar && (!full || dfar <= top) && dfar <= B;
-        if (far_ok) {
-            if (sp < cap) {
-                stack[sp * kKnnBlock] = make_uint2(2u * node + (left_first ? 2u : 1u), __float_as_uint(dfar));
-                sp++;
-            } else {
-                flag |= 16u;  // stack overflow (seeded cap): exact replay
-            }
+        if (efar && (!full || dfar <= top) && dfar <= B) {
+            const int Lc = level_of(node) + 1;  // level of the sons
+            dstack[(Lc - 1) * kKnnBlock] = dfar;
+            trail |= 1u << Lc;
         }
         has = enear && (!full || dnear <= top) && dnear <= B;
         node = 2u * node + (left_first ? 1u : 2u);
@@ -1163,9 +1133,9 @@ __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
 }
 
 // ======================================================== launchers =======
-size_t knn_lds_bytes(int depth, bool seeded) {
-    const int entries = seeded ? kSeedCap : (depth > 0 ? depth : 1);
-    return (size_t)entries * kKnnBlock * sizeof(uint2);
+size_t knn_lds_bytes(int depth, bool /*seeded*/) {
+    const int entries = depth > 1 ? depth - 1 : 1;  // son levels 1 .. depth-1
+    return (size_t)entries * kKnnBlock * sizeof(float);
 }
 
 int launch_knn_pass(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, void* stream) {

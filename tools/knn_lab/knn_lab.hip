@@ -72,7 +72,7 @@ __device__ __forceinline__ void knn_trail(const MapNode* __restrict__ nodes, flo
 #pragma unroll
                 for (int j = 0; j < kNN; j++) dup |= (j < s.n) && (s.node[j] == cur);
             }
-            if (!dup && dist <= INFINITY && (s.n < kNN || dist < s.d[kNN - 1])) sl_insert(s, dist, a.x, cur);
+            if (!dup && dist <= INFINITY && (s.n < kNN || dist < s.d[kNN - 1])) sl_insert(s, dist, cur);
             const bool full = s.n >= kNN;
             const float top = s.d[kNN - 1];
             const bool far_ok = efar && (!full || dfar < top);
@@ -188,7 +188,7 @@ __device__ __forceinline__ bool trail_step(const MapNode* __restrict__ nodes, fl
         visits++;
         const float dx = qx - a.x, dy = qy - a.y, dz = qz - a.z;
         const float dist = (dx * dx + dy * dy) + dz * dz;
-        if (dist <= INFINITY && (s.n < kNN || dist < s.d[kNN - 1])) sl_insert(s, dist, a.x, t.cur);
+        if (dist <= INFINITY && (s.n < kNN || dist < s.d[kNN - 1])) sl_insert(s, dist, t.cur);
         const bool full = s.n >= kNN;
         const float top = s.d[kNN - 1];
         const bool far_ok = efar && (!full || dfar < top);
@@ -261,7 +261,7 @@ __global__ __launch_bounds__(kLabBlock) void k_lab(const MapNode* __restrict__ n
                         const uint32_t meta = __float_as_uint(a.w);
                         const float dx = p.x - a.x, dy = p.y - a.y, dz = p.z - a.z;
                         const float dist = (dx * dx + dy * dy) + dz * dz;
-                        if (dist <= INFINITY && (s.n < kNN || dist < s.d[kNN - 1])) sl_insert(s, dist, a.x, node);
+                        if (dist <= INFINITY && (s.n < kNN || dist < s.d[kNN - 1])) sl_insert(s, dist, node);
                         const bool hl = (meta & kLeftBit) != 0u, hr = (meta & kRightBit) != 0u;
                         const float dl = hl ? box_dist(p.x, p.y, p.z, b.x, b.y, b.z, b.w, cc.x, cc.y) : INFINITY;
                         const float dr = hr ? box_dist(p.x, p.y, p.z, cc.z, cc.w, dd.x, dd.y, dd.z, dd.w) : INFINITY;
@@ -371,7 +371,7 @@ __global__ __launch_bounds__(BLK) void k_lab_cap(const MapNode* __restrict__ nod
             const uint32_t meta = __float_as_uint(a.w);
             const float dx = p.x - a.x, dy = p.y - a.y, dz = p.z - a.z;
             const float dist = (dx * dx + dy * dy) + dz * dz;
-            if (dist <= INFINITY && (s.n < kNN || dist < s.d[kNN - 1])) sl_insert(s, dist, a.x, node);
+            if (dist <= INFINITY && (s.n < kNN || dist < s.d[kNN - 1])) sl_insert(s, dist, node);
             else flag |= fabsf(dist - s.d[kNN - 1]) <= kFuzz;
             const bool hl = (meta & kLeftBit) != 0u, hr = (meta & kRightBit) != 0u;
             const float dl = hl ? box_dist(p.x, p.y, p.z, b.x, b.y, b.z, b.w, cc.x, cc.y) : INFINITY;
@@ -439,7 +439,7 @@ __global__ __launch_bounds__(BLK) void k_lab_seed(const MapNode* __restrict__ no
                 const float4 a = rec_ptr(nodes, sn[k])[0];
                 const float dx = p.x - a.x, dy = p.y - a.y, dz = p.z - a.z;
                 const float dist = (dx * dx + dy * dy) + dz * dz;
-                sl_insert(s, dist, a.x, sn[k]);
+                sl_insert(s, dist, sn[k]);
             }
         }
         uint32_t node = 0;
@@ -465,7 +465,7 @@ __global__ __launch_bounds__(BLK) void k_lab_seed(const MapNode* __restrict__ no
 #pragma unroll
             for (int k = 0; k < kNN; k++) dup |= (k < s.n) && (s.node[k] == node);
             if (!dup) {
-                if (dist <= INFINITY && (s.n < kNN || dist < s.d[kNN - 1])) sl_insert(s, dist, a.x, node);
+                if (dist <= INFINITY && (s.n < kNN || dist < s.d[kNN - 1])) sl_insert(s, dist, node);
                 else flag |= fabsf(dist - s.d[kNN - 1]) <= kFuzz;
             }
             const bool hl = (meta & kLeftBit) != 0u, hr = (meta & kRightBit) != 0u;
