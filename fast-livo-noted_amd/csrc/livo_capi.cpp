@@ -56,14 +56,22 @@ static void dev_free(T*& p) {
 struct livo_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipStream_t stream2 = nullptr;     // second half of a batch (overlap of latency-bound kernels)
-    hipEvent_t fork = nullptr, join = nullptr;
+    // extra streams for the groups of a batch (overlap of latency-bound kernels)
+    hipStream_t xstream[kMaxGroups - 1] = {};
+    hipEvent_t xjoin[kMaxGroups - 1] = {};
+    int groups = 4;                    // stream groups per batch (LIVO_STREAM_GROUPS)
+    int leaf_size = kLeafSize;         // leaf-map points per leaf (LIVO_LEAF_SIZE)
+    hipEvent_t fork = nullptr;
     livo_params params{};
     // map
     MapNode* nodes = nullptr;
     int64_t map_points = 0;
     int64_t map_slots = 0;
     int32_t map_depth = 0;
+    LeafNode* lnodes = nullptr;        // leaf map (batched IEKF search)
+    float* lpts = nullptr;
+    int32_t leaf_depth = 0;
+    int64_t leaf_bytes = 0;
     bool has_map = false;
     // scans
     std::vector<ScanBuf> scans;
@@ -83,7 +91,7 @@ struct livo_ctx {
     size_t scratch_bytes = 0;
     // profiling
     int profiling = 0;
-    hipEvent_t ev[2][3 * LIVO_MAX_EVALS + 2] = {};
+    hipEvent_t ev[kMaxGroups][3 * LIVO_MAX_EVALS + 2] = {};
     bool events_ready = false;
     livo_timings last{};
 };
@@ -130,7 +138,7 @@ static bool params_valid(const livo_params* p) {
 }
 
 static int ensure_replay(livo_ctx* c, int64_t total) {
-    if (!c->d_replay_count && dev_alloc(&c->d_replay_count, 2)) return LIVO_E_OOM;
+    if (!c->d_replay_count && dev_alloc(&c->d_replay_count, kMaxGroups)) return LIVO_E_OOM;
     if (!c->d_replay_total) {
         if (dev_alloc(&c->d_replay_total, 1)) return LIVO_E_OOM;
         HIP_TRY(hipMemset(c->d_replay_total, 0, sizeof(unsigned long long)));
@@ -155,14 +163,18 @@ static KnnParams make_knn_params(livo_ctx* c) {
     kp.has_map = c->has_map && c->map_points > 0 ? 1 : 0;
     kp.force = -1;
     kp.depth = c->map_depth;
+    kp.lnodes = c->lnodes;
+    kp.lpts = c->lpts;
+    kp.ldepth = c->leaf_depth;
+    kp.lM = c->has_map ? c->map_points : 0;
     kp.identity = 0;
     return kp;
 }
 
 // k-NN pass + exact replay of its flagged queries (one replay list per pass).
-static int knn_pass(const KnnParams& kp, int n_jobs, int64_t max_n, bool seeded, hipStream_t st) {
+static int knn_pass(const KnnParams& kp, int n_jobs, int64_t max_n, hipStream_t st) {
     HIP_TRY(hipMemsetAsync(kp.replay_count, 0, sizeof(unsigned), st));
-    return launch_knn_pass(kp, n_jobs, max_n, seeded, st);
+    return launch_knn_pass(kp, n_jobs, max_n, st);
 }
 
 // Morton (Z-order) permutation of the body points: 0.25 m cells, 10 bits/axis.
@@ -225,6 +237,15 @@ static void init_slot(IekfSlot& s, const livo_state& st, const livo_state& prior
     s.ctrl.max_iter = max_iter;
 }
 
+static int create_group_streams(livo_ctx* c) {
+    for (int k = 0; k < kMaxGroups - 1; k++) {
+        if (hipStreamCreateWithFlags(&c->xstream[k], hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&c->xjoin[k], hipEventDisableTiming) != hipSuccess)
+            return 1;
+    }
+    return 0;
+}
+
 extern "C" {
 
 int livo_abi_version(void) { return LIVO_ABI_VERSION; }
@@ -268,10 +289,16 @@ int livo_ctx_create(int device, const livo_params* p, livo_ctx** out) {
     if (!c) return LIVO_E_OOM;
     c->device = device;
     c->params = p ? *p : def;
+    if (const char* env = std::getenv("LIVO_STREAM_GROUPS")) {  // tuning knob
+        const int v = std::atoi(env);
+        if (v >= 1 && v <= kMaxGroups) c->groups = v;
+    }
+    if (const char* env = std::getenv("LIVO_LEAF_SIZE")) {  // tuning knob
+        const int v = std::atoi(env);
+        if (v >= 2 && v <= 256) c->leaf_size = v;
+    }
     if (set_device(c) || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess || create_group_streams(c)) {
         delete c;
         return LIVO_E_HIP;
     }
@@ -288,6 +315,8 @@ int livo_ctx_destroy(livo_ctx* c) {
         dev_free(s.partial);
     }
     dev_free(c->nodes);
+    dev_free(c->lnodes);
+    dev_free(c->lpts);
     dev_free(c->d_replay_count);
     dev_free(c->d_replay_total);
     dev_free(c->d_replay_list);
@@ -299,10 +328,12 @@ int livo_ctx_destroy(livo_ctx* c) {
     if (c->events_ready)
         for (auto& g : c->ev)
             for (auto& e : g) (void)hipEventDestroy(e);
-    if (c->stream2) (void)hipStreamSynchronize(c->stream2);
+    for (int k = 0; k < kMaxGroups - 1; k++) {
+        if (c->xstream[k]) (void)hipStreamSynchronize(c->xstream[k]);
+        if (c->xjoin[k]) (void)hipEventDestroy(c->xjoin[k]);
+        if (c->xstream[k]) (void)hipStreamDestroy(c->xstream[k]);
+    }
     if (c->fork) (void)hipEventDestroy(c->fork);
-    if (c->join) (void)hipEventDestroy(c->join);
-    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return LIVO_OK;
@@ -338,18 +369,38 @@ int livo_map_build(livo_ctx* c, const float* xyz, int64_t M, int64_t stride_byte
     HostMap hm;
     int rc = build_host_map(xyz, M, stride_bytes, &hm);
     if (rc) return rc;
+    HostLeafMap lm;
+    rc = build_leaf_map(xyz, M, stride_bytes, c->leaf_size, &lm);
+    if (rc) {
+        free_host_map(&hm);
+        return rc;
+    }
     HIP_TRY(hipStreamSynchronize(c->stream));
+    for (int k = 0; k < kMaxGroups - 1; k++) HIP_TRY(hipStreamSynchronize(c->xstream[k]));
     dev_free(c->nodes);
+    dev_free(c->lnodes);
+    dev_free(c->lpts);
+    c->nodes = nullptr;
+    c->lnodes = nullptr;
+    c->lpts = nullptr;
     c->has_map = false;
     const size_t bytes = (size_t)(hm.num_slots + 1) * sizeof(MapNode);
-    if (hipMalloc((void**)&c->nodes, bytes) != hipSuccess) {
+    const size_t lnb = (size_t)std::max<int64_t>(((int64_t)1 << lm.depth) - 1, 1) * sizeof(LeafNode);
+    const size_t lpb = (size_t)(M + 3) * 4 * sizeof(float);  // chunk padding
+    if (hipMalloc((void**)&c->nodes, bytes) != hipSuccess || hipMalloc((void**)&c->lnodes, lnb) != hipSuccess ||
+        hipMalloc((void**)&c->lpts, lpb) != hipSuccess) {
         free_host_map(&hm);
-        c->nodes = nullptr;
+        free_leaf_map(&lm);
         return LIVO_E_OOM;
     }
     hipError_t e = hipMemcpy(c->nodes, hm.nodes, bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(c->lnodes, lm.nodes, lnb, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(c->lpts, lm.pts, lpb, hipMemcpyHostToDevice);
     free_host_map(&hm);
+    free_leaf_map(&lm);
     if (e != hipSuccess) return LIVO_E_HIP;
+    c->leaf_depth = lm.depth;
+    c->leaf_bytes = (int64_t)(lnb + lpb);
     c->map_points = M;
     c->map_slots = hm.num_slots;
     c->map_depth = hm.depth;
@@ -365,7 +416,7 @@ int livo_map_get_info(livo_ctx* c, livo_map_info* out) {
     out->depth = c->map_depth;
     out->reserved = 0;
     out->num_slots = c->map_slots;
-    out->device_bytes = (c->map_slots + 1) * (int64_t)sizeof(MapNode);
+    out->device_bytes = (c->map_slots + 1) * (int64_t)sizeof(MapNode) + c->leaf_bytes;
     return LIVO_OK;
 }
 
@@ -401,7 +452,7 @@ int livo_knn(livo_ctx* c, const float* q, int64_t n, int32_t k, int32_t* idx, fl
     KnnParams kp = make_knn_params(c);
     kp.force = 1;
     kp.identity = 1;
-    rc = knn_pass(kp, 1, n, false, c->stream);
+    rc = knn_pass(kp, 1, n, c->stream);
     if (rc) return rc;
     std::vector<NNRec> hr((size_t)n);
     HIP_TRY(hipMemcpyAsync(hr.data(), dr, rb, hipMemcpyDeviceToHost, c->stream));
@@ -510,7 +561,7 @@ int livo_h_share(livo_ctx* c, int32_t id, const livo_state* state, int search_en
         if (rc) return rc;
         KnnParams kp = make_knn_params(c);
         kp.force = 1;
-        rc = knn_pass(kp, 1, N, false, c->stream);
+        rc = knn_pass(kp, 1, N, c->stream);
         if (rc) return rc;
     } else if (!s->searched && N > 0) {
         // no cached neighbours yet: nothing is matched (points_near.size() < 5, :525)
@@ -518,7 +569,7 @@ int livo_h_share(livo_ctx* c, int32_t id, const livo_state* state, int search_en
     }
     rc = launch_hshare(hp, 1, std::max(s->nblk, 1), search_en != 0, c->stream);
     if (rc) return rc;
-    SolveParams sp{c->d_slots, c->d_jobs, 1};
+    SolveParams sp{c->d_slots, c->d_jobs, 1};  // mode 1: reduce the partials only
     rc = launch_solve(sp, 1, c->stream);
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(c->h_slots, c->d_slots, sizeof(IekfSlot), hipMemcpyDeviceToHost, c->stream));
@@ -597,26 +648,26 @@ int livo_iekf_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_stat
     HIP_TRY(hipMemcpyAsync(c->d_slots, c->h_slots, sizeof(IekfSlot) * n, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->d_jobs, c->h_jobs, sizeof(HsJob) * n, hipMemcpyHostToDevice, c->stream));
 
-    // Two half-batches on two streams: the latency-bound kernels of one half
-    // (18x18 solve, tie replay, launch gaps) overlap the throughput-bound
-    // k-NN / plane passes of the other.  Each half keeps its own replay list.
+    // The batch in groups on separate streams: the latency-bound kernels of
+    // one group (18x18 solve, tie replay, launch gaps) overlap the
+    // throughput-bound k-NN / plane passes of the others.  Each group keeps
+    // its own replay list.
     struct Group {
         int32_t first, count;
         int max_nblk;
         int64_t max_n, off;
         hipStream_t st;
     };
-    Group g[2];
-    const int ngroups = n >= 2 ? 2 : 1;
-    const int32_t h = ngroups == 2 ? (n + 1) / 2 : n;
+    Group g[kMaxGroups];
+    const int ngroups = std::max(1, std::min<int>(c->groups, n));
     int64_t off = 0;
     for (int gi = 0; gi < ngroups; gi++) {
-        g[gi].first = gi == 0 ? 0 : h;
-        g[gi].count = gi == 0 ? h : n - h;
+        g[gi].first = (int32_t)((int64_t)n * gi / ngroups);
+        g[gi].count = (int32_t)((int64_t)n * (gi + 1) / ngroups) - g[gi].first;
         g[gi].max_nblk = 1;
         g[gi].max_n = 1;
         g[gi].off = off;
-        g[gi].st = gi == 0 ? c->stream : c->stream2;
+        g[gi].st = gi == 0 ? c->stream : c->xstream[gi - 1];
         for (int32_t b = g[gi].first; b < g[gi].first + g[gi].count; b++) {
             const ScanBuf* s = get_scan(c, ids[b]);
             g[gi].max_nblk = std::max(g[gi].max_nblk, (int)s->nblk);
@@ -624,15 +675,17 @@ int livo_iekf_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_stat
             off += s->n;
         }
     }
-    if (ngroups == 2) {
-        HIP_TRY(hipEventRecord(c->fork, c->stream));
-        HIP_TRY(hipStreamWaitEvent(c->stream2, c->fork, 0));
-    }
     const bool prof = c->profiling && c->events_ready;
+    // profiling: the batch's first search starts at ev[0][0], before the fork
+    if (prof) HIP_TRY(hipEventRecord(c->ev[0][0], c->stream));
+    if (ngroups > 1) {
+        HIP_TRY(hipEventRecord(c->fork, c->stream));
+        for (int gi = 1; gi < ngroups; gi++) HIP_TRY(hipStreamWaitEvent(g[gi].st, c->fork, 0));
+    }
     const int evals = max_iter + 1;
-    HsParams hp[2];
-    KnnParams kp[2];
-    SolveParams sp[2];
+    HsParams hp[kMaxGroups];
+    KnnParams kp[kMaxGroups];
+    SolveParams sp[kMaxGroups];
     for (int gi = 0; gi < ngroups; gi++) {
         hp[gi] = make_hs_params(c);
         hp[gi].jobs = c->d_jobs + g[gi].first;
@@ -645,8 +698,10 @@ int livo_iekf_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_stat
     for (int e = 0; e < evals; e++) {
         for (int gi = 0; gi < ngroups; gi++) {
             hipStream_t st = g[gi].st;
-            if (prof) HIP_TRY(hipEventRecord(c->ev[gi][3 * e], st));
-            rc = knn_pass(kp[gi], g[gi].count, g[gi].max_n, e > 0, st);  // rematch passes are seeded
+            if (prof && (e > 0 || gi > 0)) HIP_TRY(hipEventRecord(c->ev[gi][3 * e], st));
+            // leaf-map search; rematch passes are bounded by the previous neighbours
+            HIP_TRY(hipMemsetAsync(kp[gi].replay_count, 0, sizeof(unsigned), st));
+            rc = launch_knn_leaf(kp[gi], g[gi].count, g[gi].max_n, e > 0, st);
             if (rc) return rc;
             if (prof) HIP_TRY(hipEventRecord(c->ev[gi][3 * e + 1], st));
             rc = launch_hshare(hp[gi], g[gi].count, g[gi].max_nblk, e == 0, st);
@@ -658,9 +713,9 @@ int livo_iekf_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_stat
     }
     for (int gi = 0; gi < ngroups; gi++)
         if (prof) HIP_TRY(hipEventRecord(c->ev[gi][3 * LIVO_MAX_EVALS], g[gi].st));
-    if (ngroups == 2) {
-        HIP_TRY(hipEventRecord(c->join, c->stream2));
-        HIP_TRY(hipStreamWaitEvent(c->stream, c->join, 0));
+    for (int gi = 1; gi < ngroups; gi++) {
+        HIP_TRY(hipEventRecord(c->xjoin[gi - 1], g[gi].st));
+        HIP_TRY(hipStreamWaitEvent(c->stream, c->xjoin[gi - 1], 0));
     }
     HIP_TRY(hipMemcpyAsync(c->h_slots, c->d_slots, sizeof(IekfSlot) * n, hipMemcpyDeviceToHost, c->stream));
     unsigned long long replays = 0;
@@ -677,23 +732,26 @@ int livo_iekf_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_stat
     }
     if (prof) {
         livo_timings t{};
+        // first search of the whole batch: wall time from its start on stream 0
+        // to the later of the two streams' ends (the halves run concurrently)
+        for (int gi = 0; gi < ngroups; gi++) {
+            float ms = 0.f;
+            (void)hipEventElapsedTime(&ms, c->ev[0][0], c->ev[gi][1]);
+            t.knn_ms = std::max(t.knn_ms, (double)ms);
+        }
+        t.knn_launches = 1;
         for (int gi = 0; gi < ngroups; gi++)
             for (int e = 0; e < evals; e++) {
                 float ms_k = 0.f, ms_h = 0.f, ms_s = 0.f;
-                (void)hipEventElapsedTime(&ms_k, c->ev[gi][3 * e], c->ev[gi][3 * e + 1]);
+                if (e > 0) (void)hipEventElapsedTime(&ms_k, c->ev[gi][3 * e], c->ev[gi][3 * e + 1]);
                 (void)hipEventElapsedTime(&ms_h, c->ev[gi][3 * e + 1], c->ev[gi][3 * e + 2]);
                 const hipEvent_t end = (e + 1 < evals) ? c->ev[gi][3 * e + 3] : c->ev[gi][3 * LIVO_MAX_EVALS];
                 (void)hipEventElapsedTime(&ms_s, c->ev[gi][3 * e + 2], end);
-                if (e == 0) {
-                    t.knn_ms += ms_k;
-                    t.knn_launches++;
-                } else {
-                    t.rematch_knn_ms += ms_k;
-                }
+                t.rematch_knn_ms += ms_k;
                 t.plane_ms += ms_h;
                 t.solve_ms += ms_s;
             }
-        // the first evaluation's k_knn_pass<false> searches for every point of every scan
+        // the first evaluation searches for every point of every scan
         for (int32_t b = 0; b < n; b++) {
             t.knn_visits += (int64_t)c->h_slots[b].visits[0];
             t.knn_queries += c->scans[ids[b]].n;

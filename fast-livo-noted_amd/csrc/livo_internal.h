@@ -15,6 +15,7 @@ constexpr int kKnnBlock = 128;              // threads per block of the k-NN pas
 constexpr int kPtsPerThread = 4;            // points per thread of the plane-fit pass
 constexpr int kRedCols = 32;                // doubles per block partial (29 used)
 constexpr int kRedUsed = 29;                // 21 HTH upper-tri + 6 HTL + residual sum + count
+constexpr int kMaxGroups = 4;               // stream groups of a batched IEKF update
 
 // ---------------------------------------------------------------------------
 // Device map: the ikd-Tree built exactly as KD_TREE::Build (median of the
@@ -43,6 +44,38 @@ constexpr uint32_t kLeftBit = 0x40000000u;
 constexpr uint32_t kRightBit = 0x80000000u;
 constexpr int64_t kMaxMapPoints = (int64_t)kIdxMask;  // 2^30 - 1
 constexpr int kMaxDepth = 31;
+
+// ---------------------------------------------------------------------------
+// Leaf map: the search structure of the batched IEKF k-NN passes.  A balanced
+// kd-tree over the same points, split by median on the longest extent down to
+// a fixed depth D so that every leaf holds ceil/floor(M / 2^D) <= leaf_size
+// points; leaf j owns points [j*M >> D, (j+1)*M >> D) of a permuted copy of
+// the map stored as float4 (x, y, z, original index bits).  Internal node h
+// (heap order, 0 .. 2^D-2) is one 64-B record holding its two sons' boxes in
+// the MapNode b/c/d layout.  The point array is padded by 3 points so that a
+// leaf chunk of 4 can always be loaded.  It finds the same exact 5 nearest points as the
+// ikd-Tree with fewer dependent steps (leaves are scanned with independent
+// loads); the answers the reference's heap could order or pick differently
+// (ties within PointType_CMP's 1e-10) are flagged and recomputed on the
+// reference tree (k_knn_replay), see k_knn_leaf.
+// ---------------------------------------------------------------------------
+struct alignas(16) LeafNode {
+    float b[4];
+    float c[4];
+    float d[4];
+    float pad[4];  // 64 B: one record = one leaf chunk of 4 points (uniform loads)
+};
+static_assert(sizeof(LeafNode) == 64, "LeafNode must be 64 bytes");
+constexpr int kLeafSize = 16;  // default maximum points per leaf
+
+struct HostLeafMap {
+    LeafNode* nodes = nullptr;  // 2^depth - 1 internal records
+    float* pts = nullptr;       // (M + 3) x 4 floats
+    int64_t num_points = 0;
+    int32_t depth = 0;          // D: leaves at level D
+};
+int build_leaf_map(const float* xyz, int64_t M, int64_t stride_bytes, int leaf_size, HostLeafMap* out);
+void free_leaf_map(HostLeafMap* m);
 
 // IEKF control block (the loop variables of laser_mapping.cpp:166-238).
 struct IekfCtrl {
@@ -122,6 +155,11 @@ struct KnnParams {
     int32_t force;          // -1: follow ctrl; 0: skip; 1: search
     int32_t depth;          // tree levels (LDS stack entries of the full search)
     int32_t identity;       // 1: pts are world points already (livo_knn)
+    int32_t nb;             // blocks per scan (set by the launcher)
+    int32_t ldepth;         // leaf map depth D
+    const LeafNode* lnodes; // leaf map internal records
+    const float* lpts;      // leaf map points, 4 floats each (x, y, z, index bits)
+    int64_t lM;             // leaf map points
 };
 
 struct SolveParams {
@@ -141,8 +179,13 @@ int build_host_map(const float* xyz, int64_t M, int64_t stride_bytes, HostMap* o
 void free_host_map(HostMap* m);
 
 // Kernel launchers (livo_kernels.hip).  All asynchronous on `stream`.
-size_t knn_lds_bytes(int depth, bool seeded);
-int launch_knn_pass(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, void* stream);
+size_t knn_lds_bytes(int depth);
+// Reference-order k-NN on the ikd-Tree records (livo_knn, livo_h_share): the
+// visiting order of KD_TREE::Search, so the node visits it counts are V_ref.
+int launch_knn_pass(const KnnParams& p, int n_jobs, int64_t max_n, void* stream);
+// Batched IEKF k-NN on the leaf map; seeded: rematch pass bounded by the
+// point's previous neighbours.  Both are followed by the exact tie replay.
+int launch_knn_leaf(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, void* stream);
 int launch_hshare(const HsParams& p, int n_jobs, int max_nblk, bool first, void* stream);
 int launch_solve(const SolveParams& p, int n_jobs, void* stream);
 

@@ -317,33 +317,54 @@ __device__ __forceinline__ void query_point(const KnnParams& P, const IekfSlot* 
     }
 }
 
-// ---------------------------------------------------------- k-NN pass ----
-// One query per thread, the near-first DFS of the reference with sorted-list
-// candidates.  The pending far sons lie on the current root-to-node path, at
-// most one per level, so the "stack" is a trail bit mask plus one box
-// distance per level in LDS ([level][lane], conflict-free, 4 B per entry):
-// popping takes the deepest pending level and rebuilds the son's heap id from
-// the current node id.  4 B x (depth-1) per lane keeps 8 waves per SIMD
-// resident at 1M points.  SEEDED (rematch evaluations, !FIRST): the previous
-// search's 5 neighbours of the point, re-measured from its new world
-// position, give a bound B >= the new 5th distance; boxes and points farther
-// than B are skipped (they cannot tie with the 5th).  The points are stored
-// in Morton order at upload, so a wave walks one region of the tree.
-template <bool SEEDED>
+// XCD-aware block order for a 1-D grid of nb blocks per scan: blocks are dealt
+// round-robin over the 8 XCDs, so give each XCD one contiguous run of (scan,
+// block) ids -- one region of Morton-ordered points -- and its L2 only the
+// part of the map around that region (bijective for any grid size).
+__device__ __forceinline__ void xcd_block(int nb, unsigned& job, unsigned& bx) {
+    const unsigned nwg = gridDim.x, orig = blockIdx.x, xcd = orig % 8u, q = nwg / 8u, r = nwg % 8u;
+    const unsigned wgid = (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q) + orig / 8u;
+    job = wgid / (unsigned)nb;
+    bx = wgid % (unsigned)nb;
+}
+
+__device__ __forceinline__ void count_visits(const KnnParams& P, IekfSlot* slot, unsigned visits) {
+    unsigned long long wv = visits;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) wv += __shfl_xor(wv, off, 64);
+    if ((threadIdx.x & 63) == 0 && wv) {
+        int e = P.force >= 0 ? 0 : slot->ctrl.n_evals;
+        e = e < LIVO_MAX_EVALS ? e : LIVO_MAX_EVALS - 1;
+        atomicAdd(&slot->visits[e], wv);
+    }
+}
+
+__device__ __forceinline__ void flag_for_replay(const KnnParams& P, unsigned job, int i) {
+    const unsigned slot_i = atomicAdd(P.replay_count, 1u);
+    P.replay_list[slot_i] = ((unsigned long long)job << 32) | (unsigned)i;
+}
+
+// ------------------------------------------------ reference-order k-NN ----
+// livo_knn / livo_h_share: one query per thread, the near-first DFS of
+// KD_TREE::Search on the ikd-Tree records, so the nodes it visits (counted)
+// are exactly the reference's V_ref.  Sorted-list candidates.  The pending
+// far sons lie on the current root-to-node path, at most one per level, so
+// the "stack" is a trail bit mask plus one box distance per level in LDS
+// ([level][lane], conflict-free, 4 B per entry): popping takes the deepest
+// pending level and rebuilds the son's heap id from the current node id.
 __global__ __launch_bounds__(kKnnBlock, 8) void k_knn_pass(KnnParams P) {  // 8 waves/SIMD: <= 64 VGPRs
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const HsJob job = P.jobs[blockIdx.y];
+    unsigned bjob, bx;
+    xcd_block(P.nb, bjob, bx);
+    const HsJob job = P.jobs[bjob];
     IekfSlot* slot = job.slot;
     if (P.force >= 0) {
         if (!P.force) return;
-    } else {
-        if (slot->ctrl.stop) return;
-        if (SEEDED && !slot->ctrl.search_en) return;
+    } else if (slot->ctrl.stop) {
+        return;
     }
-    const int i = blockIdx.x * kKnnBlock + threadIdx.x;
+    const int i = (int)bx * kKnnBlock + threadIdx.x;
     if (i >= job.n) return;
-    // far sons pending on the current path, one per level: the son's id follows
-    // from the path (cur), so only its box distance is kept, per level per lane
     float* dstack = reinterpret_cast<float*>(smem) + threadIdx.x;
     const MapNode* __restrict__ nodes = P.nodes;
     float qx, qy, qz;
@@ -351,24 +372,6 @@ __global__ __launch_bounds__(kKnnBlock, 8) void k_knn_pass(KnnParams P) {  // 8 
     SList s;
     sl_init(s);
     unsigned flag = 0;  // reason bits: 1 CMP fuzz / equivalence, 2 point tied with the 5th
-    float B = INFINITY;
-    if (SEEDED) {
-        const int4* rec = reinterpret_cast<const int4*>(job.nn + i);
-        const int4 r6 = rec[6], r7 = rec[7];
-        if (r6.y == kNN) {
-            const uint32_t sn[kNN] = {(uint32_t)r6.w, (uint32_t)r7.x, (uint32_t)r7.y, (uint32_t)r7.z,
-                                      (uint32_t)r7.w};
-            float bmax = 0.0f;
-#pragma unroll
-            for (int k = 0; k < kNN; k++) {
-                const float4 a = rec_ptr(nodes, sn[k])[0];
-                const float dx = qx - a.x, dy = qy - a.y, dz = qz - a.z;
-                const float dist = (dx * dx + dy * dy) + dz * dz;
-                bmax = fmaxf(bmax, dist);
-            }
-            B = bmax;
-        }
-    }
     unsigned visits = 0;
     uint32_t node = 0, cur = 0;
     uint32_t trail = 0;  // bit L: a far son at level L is pending (its box distance in dstack[L-1])
@@ -399,9 +402,7 @@ __global__ __launch_bounds__(kKnnBlock, 8) void k_knn_pass(KnnParams P) {  // 8 
             const float dist = (dx * dx + dy * dy) + dz * dz;  // calc_dist (:1291-1295)
             const bool full = s.n >= kNN;
             const float top = s.d[kNN - 1];
-            const bool pass_top = !full || dist < top;
-            // points beyond the seed bound B >= the final 5th distance cannot tie with it
-            if (pass_top && dist <= B) sl_insert(s, dist, node);  // (NaN fails dist <= B)
+            if (!full || dist < top) sl_insert(s, dist, node);
             flag |= (full && dist == top) ? 2u : 0u;
         }
         const bool hl = (meta & kLeftBit) != 0u;
@@ -415,12 +416,12 @@ __global__ __launch_bounds__(kKnnBlock, 8) void k_knn_pass(KnnParams P) {  // 8 
         const bool efar = left_first ? hr : hl;
         const bool full = s.n >= kNN;
         const float top = s.d[kNN - 1];
-        if (efar && (!full || dfar <= top) && dfar <= B) {
+        if (efar && (!full || dfar <= top)) {
             const int Lc = level_of(node) + 1;  // level of the sons
             dstack[(Lc - 1) * kKnnBlock] = dfar;
             trail |= 1u << Lc;
         }
-        has = enear && (!full || dnear <= top) && dnear <= B;
+        has = enear && (!full || dnear <= top);
         node = 2u * node + (left_first ? 1u : 2u);
     }
     flag |= s.fuzz ? 1u : 0u;
@@ -432,18 +433,169 @@ __global__ __launch_bounds__(kKnnBlock, 8) void k_knn_pass(KnnParams P) {  // 8 
 #pragma unroll
     for (int k = 0; k < kNN; k++) { od[k] = s.d[k]; on[k] = s.node[k]; }
     write_nnrec(job.nn + i, nodes, s.n, od, on, (int)flag);
-    if (flag) {
-        const unsigned slot_i = atomicAdd(P.replay_count, 1u);
-        P.replay_list[slot_i] = ((unsigned long long)blockIdx.y << 32) | (unsigned)i;
+    if (flag) flag_for_replay(P, bjob, i);
+    count_visits(P, slot, visits);
+}
+
+// ------------------------------------------------------- leaf-map k-NN ----
+// The batched IEKF search (k_knn_leaf<SEEDED>): one query per thread on the
+// leaf map (livo_internal.h), the same trail/LDS distance stack over the
+// internal levels, and a leaf scan with independent loads at the bottom.
+//
+// Equivalence with the reference (ikd_Tree.cpp:843-986, MANUAL_HEAP
+// :1345-1411, PointType_CMP ikd_Tree.h:50-61).  Let S5 be the 5 nearest map
+// points by squared distance, d5 the 5th distance and d6 the next one.  If
+//   (C1) d6 - d5 > 1e-10 (float subtraction, as PointType_CMP computes it), and
+//   (C2) no two members of S5 are within 1e-10 of each other,
+// then every S5 member compares below every other point under PointType_CMP,
+// so no heap operation can place an S5 member above a non-member, a full heap
+// always pops a non-member, every S5 member passes the push test when
+// visited, and Nearest_Search returns exactly S5 in ascending distance --
+// whatever the visiting order.  The search below finds S5 exactly, and also
+// every point within 1e-10 of d5: a box is skipped only if its distance
+// exceeds min(5th candidate, seed bound B) by more than 1e-10 (both are
+// >= d5 and float subtraction is monotone; box distances never exceed the
+// distance of a point inside, as in calc_box_dist).  It tracks e6, the
+// smallest distance rejected or evicted from the 5 candidates, and flags the
+// query (exact replay on the ikd-Tree) if C1 or C2 fails.
+template <bool SEEDED>
+__global__ __launch_bounds__(kKnnBlock, 8) void k_knn_leaf(KnnParams P) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned bjob, bx;
+    xcd_block(P.nb, bjob, bx);
+    const HsJob job = P.jobs[bjob];
+    IekfSlot* slot = job.slot;
+    if (P.force >= 0) {
+        if (!P.force) return;
+    } else {
+        if (slot->ctrl.stop) return;
+        if (SEEDED && !slot->ctrl.search_en) return;
     }
-    unsigned long long wv = visits;
+    const int i = (int)bx * kKnnBlock + threadIdx.x;
+    if (i >= job.n) return;
+    float* dstack = reinterpret_cast<float*>(smem) + threadIdx.x;
+    const float4* __restrict__ lnodes = reinterpret_cast<const float4*>(P.lnodes);
+    const float4* __restrict__ lpts = reinterpret_cast<const float4*>(P.lpts);
+    float qx, qy, qz;
+    query_point(P, slot, reinterpret_cast<const float4*>(job.pts)[i], qx, qy, qz);
+    float B = INFINITY;
+    if (SEEDED) {
+        // the point's 5 previous neighbours, re-measured: 5 distinct map points
+        // at distance <= B, so B >= d5
+        const NNRec* sr = job.nn + i;
+        if (sr->cnt == kNN) {
+            float bmax = 0.0f;
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) wv += __shfl_xor(wv, off, 64);
-    if ((threadIdx.x & 63) == 0 && wv) {
-        int e = P.force >= 0 ? 0 : slot->ctrl.n_evals;
-        e = e < LIVO_MAX_EVALS ? e : LIVO_MAX_EVALS - 1;
-        atomicAdd(&slot->visits[e], wv);
+            for (int k = 0; k < kNN; k++) {
+                const float4 a = reinterpret_cast<const float4*>(sr->p)[k];
+                const float dx = qx - a.x, dy = qy - a.y, dz = qz - a.z;
+                bmax = fmaxf(bmax, (dx * dx + dy * dy) + dz * dz);
+            }
+            B = bmax;
+        }
     }
+    float d[kNN];
+    uint32_t nd[kNN];
+#pragma unroll
+    for (int k = 0; k < kNN; k++) { d[k] = INFINITY; nd[k] = 0u; }
+    float e6 = INFINITY;
+    const int D = P.ldepth;
+    const uint32_t first_leaf = (1u << D) - 1u;
+    const int64_t M = P.lM;
+    unsigned visits = 0;
+    uint32_t node = 0, cur = 0, trail = 0;
+    bool has = M > 0;
+    while (true) {
+        if (!has) {
+            if (trail == 0u) break;
+            const int L = 31 - __clz(trail);
+            trail &= ~(1u << L);
+            const float de = dstack[(L - 1) * kKnnBlock];
+            if (de - fminf(d[kNN - 1], B) > kFuzz) continue;
+            const uint32_t a = ((cur + 1u) >> (level_of(cur) - L)) - 1u;
+            node = ((a - 1u) ^ 1u) + 1u;
+        }
+        cur = node;
+        visits++;
+        if (node >= first_leaf) {
+            // leaf: its points, 4 independent loads at a time
+            const int64_t j = node - first_leaf;
+            const int lo = (int)((j * M) >> D), hi = (int)(((j + 1) * M) >> D);
+            for (int k0 = lo; k0 < hi; k0 += 4) {
+                float4 v[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) v[u] = lpts[k0 + u];  // padded by 3 points
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    if (k0 + u < hi) {
+                        const float dx = qx - v[u].x, dy = qy - v[u].y, dz = qz - v[u].z;
+                        const float dist = (dx * dx + dy * dy) + dz * dz;  // calc_dist (:1291-1295)
+                        if (dist < d[kNN - 1]) {
+                            e6 = fminf(e6, d[kNN - 1]);  // evicted (+inf while not full)
+                            d[kNN - 1] = dist;
+                            nd[kNN - 1] = (uint32_t)(k0 + u);
+#pragma unroll
+                            for (int q = kNN - 1; q > 0; q--) {
+                                const bool sw = d[q] < d[q - 1];
+                                const float td = d[q];
+                                const uint32_t tn = nd[q];
+                                d[q] = sw ? d[q - 1] : td;
+                                nd[q] = sw ? nd[q - 1] : tn;
+                                d[q - 1] = sw ? td : d[q - 1];
+                                nd[q - 1] = sw ? tn : nd[q - 1];
+                            }
+                        } else {
+                            e6 = fminf(e6, dist);
+                        }
+                    }
+                }
+            }
+            has = false;
+            continue;
+        }
+        const float4* rp = lnodes + 4 * (size_t)node;
+        const float4 b = rp[0];
+        const float4 cc = rp[1];
+        const float4 dd = rp[2];
+        const float dl = box_dist(qx, qy, qz, b.x, b.y, b.z, b.w, cc.x, cc.y);
+        const float dr = box_dist(qx, qy, qz, cc.z, cc.w, dd.x, dd.y, dd.z, dd.w);
+        const bool left_first = dl <= dr;
+        const float dnear = left_first ? dl : dr;
+        const float dfar = left_first ? dr : dl;
+        const float thr = fminf(d[kNN - 1], B);
+        if (dfar - thr <= kFuzz) {
+            const int Lc = level_of(node) + 1;
+            dstack[(Lc - 1) * kKnnBlock] = dfar;
+            trail |= 1u << Lc;
+        }
+        has = dnear - thr <= kFuzz;
+        node = 2u * node + (left_first ? 1u : 2u);
+    }
+    const int cnt = (int)min<int64_t>(M, (int64_t)kNN);
+    bool amb = e6 - d[kNN - 1] <= kFuzz;  // C1 (false while e6 = +inf)
+#pragma unroll
+    for (int k = 0; k + 1 < kNN; k++) amb |= (k + 1 < cnt) && (d[k + 1] - d[k] <= kFuzz);  // C2
+    // neighbour record: points, distances, original indices; node[] = leaf-map slots
+    float4* o4 = reinterpret_cast<float4*>(job.nn + i);
+    int32_t idx[kNN];
+#pragma unroll
+    for (int k = 0; k < kNN; k++) {
+        float4 v = make_float4(0.f, 0.f, 0.f, INFINITY);
+        idx[k] = -1;
+        if (k < cnt) {
+            const float4 a = lpts[nd[k]];
+            v = make_float4(a.x, a.y, a.z, d[k]);
+            idx[k] = (int32_t)__float_as_uint(a.w);
+        }
+        o4[k] = v;
+    }
+    const int flag = amb ? 4 : 0;
+    int4* oi = reinterpret_cast<int4*>(job.nn + i) + 5;
+    oi[0] = make_int4(idx[0], idx[1], idx[2], idx[3]);
+    oi[1] = make_int4(idx[4], cnt, flag, (int)nd[0]);
+    oi[2] = make_int4((int)nd[1], (int)nd[2], (int)nd[3], (int)nd[4]);
+    if (amb) flag_for_replay(P, bjob, i);
+    count_visits(P, slot, visits);
 }
 
 // Exact reference-order recomputation of the queries the fast pass flagged:
@@ -1133,21 +1285,36 @@ __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
 }
 
 // ======================================================== launchers =======
-size_t knn_lds_bytes(int depth, bool /*seeded*/) {
+size_t knn_lds_bytes(int depth) {
     const int entries = depth > 1 ? depth - 1 : 1;  // son levels 1 .. depth-1
     return (size_t)entries * kKnnBlock * sizeof(float);
 }
 
-int launch_knn_pass(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, void* stream) {
+int launch_knn_pass(const KnnParams& p, int n_jobs, int64_t max_n, void* stream) {
     if (n_jobs <= 0 || max_n <= 0) return LIVO_OK;
-    dim3 grid((unsigned)((max_n + kKnnBlock - 1) / kKnnBlock), n_jobs), block(kKnnBlock);
-    const size_t lds = knn_lds_bytes(p.depth, seeded);
-    if (seeded)
-        hipLaunchKernelGGL(k_knn_pass<true>, grid, block, lds, (hipStream_t)stream, p);
-    else
-        hipLaunchKernelGGL(k_knn_pass<false>, grid, block, lds, (hipStream_t)stream, p);
+    KnnParams q = p;
+    q.nb = (int32_t)((max_n + kKnnBlock - 1) / kKnnBlock);
+    if ((int64_t)q.nb * n_jobs >= (1ll << 31)) return LIVO_E_RANGE;
+    hipLaunchKernelGGL(k_knn_pass, dim3((unsigned)(q.nb * n_jobs)), dim3(kKnnBlock), knn_lds_bytes(p.depth),
+                       (hipStream_t)stream, q);
     if (hipGetLastError() != hipSuccess) return LIVO_E_HIP;
-    hipLaunchKernelGGL(k_knn_replay, dim3(64), dim3(64), 0, (hipStream_t)stream, p);
+    hipLaunchKernelGGL(k_knn_replay, dim3(64), dim3(64), 0, (hipStream_t)stream, q);
+    return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+
+int launch_knn_leaf(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, void* stream) {
+    if (n_jobs <= 0 || max_n <= 0) return LIVO_OK;
+    KnnParams q = p;
+    q.nb = (int32_t)((max_n + kKnnBlock - 1) / kKnnBlock);
+    if ((int64_t)q.nb * n_jobs >= (1ll << 31)) return LIVO_E_RANGE;
+    const dim3 grid((unsigned)(q.nb * n_jobs)), block(kKnnBlock);
+    const size_t lds = knn_lds_bytes(p.ldepth + 1);
+    if (seeded)
+        hipLaunchKernelGGL(k_knn_leaf<true>, grid, block, lds, (hipStream_t)stream, q);
+    else
+        hipLaunchKernelGGL(k_knn_leaf<false>, grid, block, lds, (hipStream_t)stream, q);
+    if (hipGetLastError() != hipSuccess) return LIVO_E_HIP;
+    hipLaunchKernelGGL(k_knn_replay, dim3(64), dim3(64), 0, (hipStream_t)stream, q);
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 

@@ -156,3 +156,129 @@ void free_host_map(HostMap* m) {
 }
 
 }  // namespace livo
+
+// ---------------------------------------------------------------------------
+// Leaf map (livo_internal.h): balanced median kd-tree of fixed depth D with
+// leaves of <= leaf_size points.  Leaf j = points [j*M >> D, (j+1)*M >> D) of
+// the permuted array; node h at level L covers leaves [jl, jl + 2^(D-L)) and is
+// split at the first point of its middle leaf, on its longest extent.
+// ---------------------------------------------------------------------------
+namespace livo {
+namespace {
+
+struct LeafBuilder {
+    std::vector<BPoint>& st;
+    LeafNode* nodes;
+    int64_t M;
+    int D;
+
+    int64_t leaf_start(int64_t j) const { return (int64_t)(((unsigned __int128)j * (unsigned __int128)M) >> D); }
+
+    Box build(int64_t h, int level, int64_t jl, int spawn_levels) {
+        const int64_t nleaves = (int64_t)1 << (D - level);
+        const int64_t lo = leaf_start(jl), hi = leaf_start(jl + nleaves);
+        Box out{};
+        out.valid = true;
+        for (int k = 0; k < 3; k++) {
+            out.mn[k] = INFINITY;
+            out.mx[k] = -INFINITY;
+        }
+        if (level == D) {
+            for (int64_t i = lo; i < hi; i++) {
+                const float pc[3] = {st[i].x, st[i].y, st[i].z};
+                for (int k = 0; k < 3; k++) {
+                    out.mn[k] = std::min(out.mn[k], pc[k]);
+                    out.mx[k] = std::max(out.mx[k], pc[k]);
+                }
+            }
+            return out;
+        }
+        for (int64_t i = lo; i < hi; i++) {
+            const float pc[3] = {st[i].x, st[i].y, st[i].z};
+            for (int k = 0; k < 3; k++) {
+                out.mn[k] = std::min(out.mn[k], pc[k]);
+                out.mx[k] = std::max(out.mx[k], pc[k]);
+            }
+        }
+        int axis = 0;
+        for (int k = 1; k < 3; k++)
+            if (out.mx[k] - out.mn[k] > out.mx[axis] - out.mn[axis]) axis = k;
+        const int64_t jm = jl + nleaves / 2, mid = leaf_start(jm);
+        auto b = st.begin();
+        if (mid > lo && mid < hi) {
+            if (axis == 1) std::nth_element(b + lo, b + mid, b + hi, cmp_y);
+            else if (axis == 2) std::nth_element(b + lo, b + mid, b + hi, cmp_z);
+            else std::nth_element(b + lo, b + mid, b + hi, cmp_x);
+        }
+        Box bl, br;
+        if (spawn_levels > 0 && hi - lo > 65536) {
+            std::thread t([&] { bl = build(2 * h + 1, level + 1, jl, spawn_levels - 1); });
+            br = build(2 * h + 2, level + 1, jm, spawn_levels - 1);
+            t.join();
+        } else {
+            bl = build(2 * h + 1, level + 1, jl, 0);
+            br = build(2 * h + 2, level + 1, jm, 0);
+        }
+        LeafNode& nd = nodes[h];
+        nd.b[0] = bl.mn[0]; nd.b[1] = bl.mx[0]; nd.b[2] = bl.mn[1]; nd.b[3] = bl.mx[1];
+        nd.c[0] = bl.mn[2]; nd.c[1] = bl.mx[2]; nd.c[2] = br.mn[0]; nd.c[3] = br.mx[0];
+        nd.d[0] = br.mn[1]; nd.d[1] = br.mx[1]; nd.d[2] = br.mn[2]; nd.d[3] = br.mx[2];
+        return out;
+    }
+};
+
+}  // namespace
+
+int build_leaf_map(const float* xyz, int64_t M, int64_t stride_bytes, int leaf_size, HostLeafMap* out) {
+    if (!out || M < 0 || (M > 0 && !xyz) || leaf_size < 1) return LIVO_E_INVALID;
+    if (M > kMaxMapPoints) return LIVO_E_RANGE;
+    if (stride_bytes == 0) stride_bytes = 3 * sizeof(float);
+    if (stride_bytes < (int64_t)(3 * sizeof(float))) return LIVO_E_INVALID;
+    free_leaf_map(out);
+    int D = 0;
+    while (D < kMaxDepth - 1 && ((M + ((int64_t)1 << D) - 1) >> D) > leaf_size) D++;  // ceil(M / 2^D)
+    const int64_t n_int = ((int64_t)1 << D) - 1;
+    LeafNode* nodes = (LeafNode*)std::calloc((size_t)std::max<int64_t>(n_int, 1), sizeof(LeafNode));
+    float* pts = (float*)std::calloc((size_t)(M + 3), 4 * sizeof(float));  // +3: chunk padding
+    if (!nodes || !pts) {
+        std::free(nodes);
+        std::free(pts);
+        return LIVO_E_OOM;
+    }
+    std::vector<BPoint> st((size_t)M);
+    const char* base = (const char*)xyz;
+    for (int64_t i = 0; i < M; i++) {
+        const float* p = (const float*)(base + i * stride_bytes);
+        st[i] = BPoint{p[0], p[1], p[2], (uint32_t)i};
+    }
+    if (M > 0) {
+        LeafBuilder b{st, nodes, M, D};
+        unsigned hw = std::thread::hardware_concurrency();
+        int spawn = 0;
+        while ((1u << spawn) < std::min(hw ? hw : 1u, 16u)) spawn++;
+        b.build(0, 0, 0, spawn);
+    }
+    for (int64_t i = 0; i < M; i++) {
+        float w;
+        std::memcpy(&w, &st[i].idx, 4);
+        pts[4 * i + 0] = st[i].x;
+        pts[4 * i + 1] = st[i].y;
+        pts[4 * i + 2] = st[i].z;
+        pts[4 * i + 3] = w;
+    }
+    out->nodes = nodes;
+    out->pts = pts;
+    out->num_points = M;
+    out->depth = D;
+    return LIVO_OK;
+}
+
+void free_leaf_map(HostLeafMap* m) {
+    if (!m) return;
+    std::free(m->nodes);
+    std::free(m->pts);
+    m->nodes = nullptr;
+    m->pts = nullptr;
+}
+
+}  // namespace livo

@@ -110,15 +110,17 @@ typedef struct livo_point_out {
 } livo_point_out;
 
 /* Device time of the kernels of the last livo_iekf_update* call (profiling mode only).
- * knn_* describe the first evaluation's k_knn_pass<false> launch, in which every
- * point of every scan runs the k-NN (the dominant kernel). */
+ * knn_* describe the first evaluation's k-NN of the whole batch (pilot pass +
+ * pilot-seeded pass + their tie replays, both streams), in which every point of
+ * every scan is searched: the dominant kernels.  The other times are summed
+ * over the streams (they overlap). */
 typedef struct livo_timings {
-    double knn_ms;         /* first-evaluation k-NN launches                           */
+    double knn_ms;         /* first-evaluation k-NN of the batch, device wall time     */
     double rematch_knn_ms; /* k-NN launches of later evaluations (rematch)             */
     double plane_ms;       /* plane fit + Jacobian + partial-sum launches (all evals)  */
     double solve_ms;       /* reduction + 18x18 solve launches                         */
-    int64_t knn_launches;  /* first-evaluation k-NN launches timed                     */
-    int64_t knn_visits;    /* tree nodes those launches visited                        */
+    int64_t knn_launches;  /* first-evaluation k-NN phases timed (1 per call)          */
+    int64_t knn_visits;    /* tree nodes those searches visited (pilot-seeded: < V_ref) */
     int64_t knn_queries;   /* points those launches processed                          */
     int64_t effct_points;  /* effective points of the first evaluation                 */
     int64_t knn_replays;   /* queries recomputed by the exact tie-order replay (all passes) */

@@ -41,7 +41,8 @@ def test_map_info(ctx100k):
     assert info["num_points"] == 100_000
     assert info["depth"] == 17  # floor(log2(1e5)) + 1
     assert info["num_slots"] == 2 ** 17 - 1
-    assert info["device_bytes"] == (2 ** 17) * 64
+    # ikd-Tree records + leaf map (internal boxes + float4 points)
+    assert info["device_bytes"] >= (2 ** 17) * 64 + 100_000 * 16
 
 
 def test_knn_bit_exact(ctx100k, tree100k, map100k):
@@ -305,3 +306,61 @@ def test_iekf_duplicate_map_replays(built):
         r = tree.h_share(body, st0["rot"], st0["pos"], np.eye(3), synth.T_LI, True)
         _hshare_compare(g, r, len(body))
         _iekf_compare(ctx, tree, body, st0, 4, synth.T_LI)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("leaf_size", [2, 5, 16, 64])
+def test_iekf_leaf_size(built, map100k, tree100k, leaf_size, monkeypatch):
+    """The batched IEKF searches the leaf map (LIVO_LEAF_SIZE points per leaf) and
+    replays PointType_CMP-ambiguous queries on the ikd-Tree; any leaf size must give
+    the oracle's answer."""
+    import livo_amd
+    synth = _synth()
+    monkeypatch.setenv("LIVO_LEAF_SIZE", str(leaf_size))
+    with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=4) as ctx:
+        ctx.map_build(map100k)
+        for scan_id in (3, 4):
+            body, _, _ = synth.make_scan(7_777, scan_id)
+            st0 = synth.make_state(scan_id)
+            _iekf_compare(ctx, tree100k, body, st0, 4, synth.T_LI)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_map", [5, 17, 100, 1000])
+def test_iekf_small_maps(built, n_map):
+    """Leaf maps of depth 0..6 (a single leaf up to many), IEKF against the oracle."""
+    import livo_amd
+    import oracle
+    synth = _synth()
+    m = synth.make_map(100_000)[:: 100_000 // n_map][:n_map].copy()
+    body, _, _ = synth.make_scan(2_000, 6)
+    st0 = synth.make_state(6)
+    tree = oracle.Tree(m)
+    with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=4) as ctx:
+        ctx.map_build(m)
+        sid = ctx.scan_upload(body)
+        _, stg = ctx.iekf_update(sid, st0)
+    _, str_ = tree.iekf_update(body, st0, R_LI=np.eye(3), t_LI=synth.T_LI, max_iter=4)
+    assert stg["iterations"] == str_["iterations"]
+    assert stg["effct_feat_num"] == str_["effct_feat_num"]
+    for e in range(stg["iterations"]):
+        if np.linalg.norm(str_["solution"][e]) > 0:
+            assert _rel(stg["solution"][e], str_["solution"][e]) < REL_STATE, e
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("groups", [1, 3, 4])
+def test_batch_stream_groups(built, map100k, groups, monkeypatch):
+    """A batch split over 1..4 stream groups (LIVO_STREAM_GROUPS) gives the single-scan results."""
+    import livo_amd
+    synth = _synth()
+    monkeypatch.setenv("LIVO_STREAM_GROUPS", str(groups))
+    with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=4) as ctx:
+        ctx.map_build(map100k)
+        sids = [ctx.scan_upload(synth.make_scan(2500 + 301 * s, s)[0]) for s in range(5)]
+        states = [synth.make_state(s) for s in range(5)]
+        b, st = ctx.iekf_update_batch(sids, states)
+        for i, sid in enumerate(sids):
+            one, st1 = ctx.iekf_update(sid, states[i])
+            assert all(np.array_equal(one[k], b[i][k]) for k in one)
+            assert st1["iterations"] == st[i]["iterations"]

@@ -686,7 +686,7 @@ extern "C" int lab_product_pass(int seeded_from_last, int32_t* flags_out, double
     hipMemcpy(d_job, &j, sizeof(j), hipMemcpyHostToDevice);
     KnnParams kp{};
     kp.nodes = g_nodes; kp.jobs = d_job; kp.replay_count = d_cnt; kp.replay_list = d_list; kp.replay_total = d_tot;
-    kp.has_map = 1; kp.force = 1; kp.depth = g_depth; kp.identity = 1;
+    kp.has_map = 1; kp.force = 1; kp.depth = g_depth; kp.identity = 1; kp.nb = (int32_t)((g_n + kKnnBlock - 1) / kKnnBlock);
     hipEvent_t e0, e1, e2;
     hipEventCreate(&e0); hipEventCreate(&e1); hipEventCreate(&e2);
     const int reps = 10;
@@ -695,9 +695,9 @@ extern "C" int lab_product_pass(int seeded_from_last, int32_t* flags_out, double
         hipMemsetAsync(d_cnt, 0, 4, g_stream);
         hipEventRecord(e0, g_stream);
         dim3 grid((unsigned)((g_n + kKnnBlock - 1) / kKnnBlock), 1);
-        const size_t lds = knn_lds_bytes(kp.depth, seeded_from_last != 0);
-        if (seeded_from_last) hipLaunchKernelGGL(k_knn_pass<true>, grid, dim3(kKnnBlock), lds, g_stream, kp);
-        else hipLaunchKernelGGL(k_knn_pass<false>, grid, dim3(kKnnBlock), lds, g_stream, kp);
+        const size_t lds = knn_lds_bytes(kp.depth);
+        (void)seeded_from_last;
+        hipLaunchKernelGGL(k_knn_pass, grid, dim3(kKnnBlock), lds, g_stream, kp);
         hipEventRecord(e1, g_stream);
         hipLaunchKernelGGL(k_knn_replay, dim3(64), dim3(64), 0, g_stream, kp);
         hipEventRecord(e2, g_stream);
