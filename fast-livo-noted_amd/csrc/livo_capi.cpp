@@ -569,7 +569,7 @@ int livo_h_share(livo_ctx* c, int32_t id, const livo_state* state, int search_en
     }
     rc = launch_hshare(hp, 1, std::max(s->nblk, 1), search_en != 0, c->stream);
     if (rc) return rc;
-    SolveParams sp{c->d_slots, c->d_jobs, 1};  // mode 1: reduce the partials only
+    SolveParams sp{c->d_slots, c->d_jobs, nullptr, 1};  // mode 1: reduce the partials only
     rc = launch_solve(sp, 1, c->stream);
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(c->h_slots, c->d_slots, sizeof(IekfSlot), hipMemcpyDeviceToHost, c->stream));
@@ -675,6 +675,7 @@ int livo_iekf_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_stat
             off += s->n;
         }
     }
+    HIP_TRY(hipMemsetAsync(c->d_replay_count, 0, sizeof(unsigned) * kMaxGroups, c->stream));
     const bool prof = c->profiling && c->events_ready;
     // profiling: the batch's first search starts at ev[0][0], before the fork
     if (prof) HIP_TRY(hipEventRecord(c->ev[0][0], c->stream));
@@ -693,14 +694,14 @@ int livo_iekf_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_stat
         kp[gi].jobs = c->d_jobs + g[gi].first;
         kp[gi].replay_count = c->d_replay_count + gi;
         kp[gi].replay_list = c->d_replay_list + g[gi].off;
-        sp[gi] = SolveParams{c->d_slots + g[gi].first, c->d_jobs + g[gi].first, 0};
+        sp[gi] = SolveParams{c->d_slots + g[gi].first, c->d_jobs + g[gi].first, c->d_replay_count + gi, 0};
     }
     for (int e = 0; e < evals; e++) {
         for (int gi = 0; gi < ngroups; gi++) {
             hipStream_t st = g[gi].st;
             if (prof && (e > 0 || gi > 0)) HIP_TRY(hipEventRecord(c->ev[gi][3 * e], st));
             // leaf-map search; rematch passes are bounded by the previous neighbours
-            HIP_TRY(hipMemsetAsync(kp[gi].replay_count, 0, sizeof(unsigned), st));
+            // (the group's replay count was zeroed before the batch / by the last k_solve)
             rc = launch_knn_leaf(kp[gi], g[gi].count, g[gi].max_n, e > 0, st);
             if (rc) return rc;
             if (prof) HIP_TRY(hipEventRecord(c->ev[gi][3 * e + 1], st));

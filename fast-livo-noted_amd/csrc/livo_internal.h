@@ -165,6 +165,7 @@ struct KnnParams {
 struct SolveParams {
     IekfSlot* slots;
     const HsJob* jobs;
+    unsigned* replay_count;  // zeroed by block 0 for the next k-NN pass (may be null)
     int32_t mode;           // 0: reduce + solve + control; 1: reduce only (livo_h_share)
 };
 

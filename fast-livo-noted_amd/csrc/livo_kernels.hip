@@ -979,15 +979,18 @@ __device__ __forceinline__ void wave_lu_to_lds(double (&A)[kDim], int lane, doub
     int piv = lane;
 #pragma unroll
     for (int k = 0; k < kDim; k++) {
-        double v = (lane >= k && lane < kDim) ? fabs(A[k]) : -1.0;
-        int vi = lane;
+        // pivot: the first maximum of |a_ik| over i >= k, scanned in row order
+        // on wave-uniform copies of column k (v_readlane, no LDS round trips)
+        int p = k;
+        double best = fabs(bcast(A[k], k));
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            const double ov = __shfl_xor(v, off, 64);
-            const int oi = __shfl_xor(vi, off, 64);
-            if (ov > v || (ov == v && oi < vi)) { v = ov; vi = oi; }
+        for (int i = k + 1; i < kDim; i++) {
+            const double v = fabs(bcast(A[k], i));
+            if (v > best) {
+                best = v;
+                p = i;
+            }
         }
-        const int p = __builtin_amdgcn_readfirstlane(vi);
         if (p != k) {  // wave-uniform
             double rk[kDim], rp[kDim];
 #pragma unroll
@@ -1077,6 +1080,12 @@ __device__ __forceinline__ void mat3_mul(const double* A, const double* B, doubl
             C[i * 3 + j] = (A[i * 3 + 0] * B[0 * 3 + j] + A[i * 3 + 1] * B[1 * 3 + j]) + A[i * 3 + 2] * B[2 * 3 + j];
 }
 
+#ifdef LIVO_SOLVE_PROF  // phase timestamps for tools/solve_lab (compiled out of the product)
+__device__ unsigned long long g_solve_prof[256][16];
+#define SOLVE_MARK(k) do { if (threadIdx.x == 0) g_solve_prof[blockIdx.x][k] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define SOLVE_MARK(k) do { } while (0)
+#endif
 __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
     __shared__ double s_sum[kRedCols];
     __shared__ double s_P[kDim * kDim];      // state.cov
@@ -1091,7 +1100,10 @@ __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
     const HsJob job = P.jobs[blockIdx.x];
     IekfSlot* slot = job.slot;
     const int lane = threadIdx.x;
+    // the k-NN replay of this evaluation has run (stream order): reset its count
+    if (P.replay_count && blockIdx.x == 0 && lane == 0) *P.replay_count = 0u;
     if (P.mode == 0 && slot->ctrl.stop) return;
+    SOLVE_MARK(0);
 
     // 1. deterministic reduction of the block partials: lane (c, h) sums the
     //    blocks b = h, h+2, ... of column c with 8 loads in flight, in a fixed
@@ -1118,6 +1130,7 @@ __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
             slot->red[lane] = sum;
         }
     }
+    SOLVE_MARK(1);
     if (P.mode == 1) return;
     for (int t = lane; t < kDim * kDim; t += 64) s_P[t] = slot->state.cov[t];
     __syncthreads();
@@ -1132,6 +1145,7 @@ __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
         s_HTH[t] = v;
     }
     const IekfCtrl ctrl0 = slot->ctrl;
+    SOLVE_MARK(2);
     const int e = ctrl0.n_evals;
     const bool row = lane < kDim;
     // 3. P^-1 once per update (state.cov does not change inside the loop)
@@ -1153,6 +1167,7 @@ __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
         for (int t = lane; t < kDim * kDim; t += 64) s_Pinv[t] = slot->Pinv[t];
     }
     __syncthreads();
+    SOLVE_MARK(3);
     // 4. K1 = (H_T_H + P^-1)^-1, columns 0..8
     {
         double A[kDim];
@@ -1161,6 +1176,7 @@ __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
             A[j] = row ? (((lane < 9 && j < 9) ? s_HTH[lane * 9 + j] : 0.0) + s_Pinv[lane * kDim + j]) : 0.0;
         wave_lu_to_lds(A, lane, s_LU, s_piv);
         __syncthreads();
+        SOLVE_MARK(4);
         if (lane < 9) {
             double y[kDim];
             lds_lu_column(s_LU, s_piv, lane, y);
@@ -1169,6 +1185,7 @@ __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
         }
         __syncthreads();
     }
+    SOLVE_MARK(5);
     // 5. G(:,0:9) = K1(:,0:9) * HTH ; columns 9..17 stay zero
     for (int t = lane; t < kDim * 9; t += 64) {
         const int i = t / 9, j = t % 9;
@@ -1199,6 +1216,7 @@ __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
         }
     }
     __syncthreads();
+    SOLVE_MARK(6);
     // 7. solution = K1(:,0:9) HTL + vec - G(:,0:9) vec(0:9)
     if (row) {
         const int i = lane;
@@ -1216,6 +1234,7 @@ __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
     }
     __syncthreads();
 
+    SOLVE_MARK(7);
     // 8. boxplus, convergence, rematch control (laser_mapping.cpp:204-237), lane 0
     int stop_now = 0;
     if (lane == 0) {
@@ -1270,6 +1289,7 @@ __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
         slot->ctrl = ctrl;
     }
     stop_now = __builtin_amdgcn_readfirstlane(stop_now);
+    SOLVE_MARK(8);
     // 9. covariance update state.cov = (I - G) * state.cov (:224-227)
     if (stop_now) {
         for (int t = lane; t < kDim * kDim; t += 64) {
@@ -1282,6 +1302,7 @@ __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
             slot->state.cov[t] = acc;
         }
     }
+    SOLVE_MARK(9);
 }
 
 // ======================================================== launchers =======
