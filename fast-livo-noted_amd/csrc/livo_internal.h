@@ -6,13 +6,17 @@
 
 #include "livo.h"
 
+#ifndef LIVO_PTS_PER_THREAD
+#define LIVO_PTS_PER_THREAD 4
+#endif
+
 namespace livo {
 
 constexpr int kNN = LIVO_NUM_MATCH_POINTS;  // 5
 constexpr int kDim = LIVO_DIM_STATE;        // 18
 constexpr int kBlock = 256;                 // threads per block of the per-point kernels
 constexpr int kKnnBlock = 128;              // threads per block of the k-NN pass (LDS stacks)
-constexpr int kPtsPerThread = 4;            // points per thread of the plane-fit pass
+constexpr int kPtsPerThread = LIVO_PTS_PER_THREAD;  // points per thread of the plane-fit pass
 constexpr int kRedCols = 32;                // doubles per block partial (29 used)
 constexpr int kRedUsed = 29;                // 21 HTH upper-tri + 6 HTL + residual sum + count
 constexpr int kMaxGroups = 4;               // stream groups of a batched IEKF update

@@ -20,7 +20,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "liblivo_hip.so")
+LIB_PATH = os.environ.get("LIVO_LIB") or os.path.join(PKG_ROOT, "lib", "liblivo_hip.so")  # LIVO_LIB: A/B builds
 HEADER_PATH = os.path.join(os.path.dirname(PKG_ROOT), "include", "livo.h")
 
 DIM_STATE = 18
