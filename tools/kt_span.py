@@ -1,0 +1,42 @@
+"""Per-batch span of the first-evaluation k-NN from a rocprofv3 kernel trace.
+
+bench.py's roofline unit is the first-evaluation k-NN of one batch: one
+k_knn_leaf<false> dispatch per stream group (4 groups run concurrently) plus
+their tie replays, timed with HIP events as the wall time from the batch's
+start to the last group's end.  This groups the k_knn_leaf<false> dispatches
+of a rocprofv3 --kernel-trace run into batches of `groups` and reports the
+mean span (first start -> last end, extended to the replay dispatch that
+follows each one on its queue) so it can be compared with bench's
+roofline.avg_launch_ms.
+usage: python tools/kt_span.py <kernel_trace.csv> [groups=4] [skip_batches=4]
+"""
+import csv
+import sys
+
+
+def main(path, groups="4", skip="4"):
+    groups, skip = int(groups), int(skip)
+    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+    by_q = {}
+    for r in rows:
+        by_q.setdefault(r["Queue_Id"], []).append(r)
+    items = []  # (start, end incl. following replay) per k_knn_leaf<false> dispatch
+    for q, rs in by_q.items():
+        for i, r in enumerate(rs):
+            if "k_knn_leaf<false>" in r["Kernel_Name"]:
+                end = int(r["End_Timestamp"])
+                if i + 1 < len(rs) and "k_knn_replay" in rs[i + 1]["Kernel_Name"]:
+                    end = int(rs[i + 1]["End_Timestamp"])
+                items.append((int(r["Start_Timestamp"]), end, int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+    items.sort()
+    spans, durs = [], [d for _, _, d in items]
+    for b in range(skip, len(items) // groups):
+        chunk = items[b * groups:(b + 1) * groups]
+        spans.append(max(e for _, e, _ in chunk) - min(s for s, _, _ in chunk))
+    print(f"k_knn_leaf<false> dispatches: {len(items)}, mean dispatch {sum(durs) / len(durs) / 1e3:.1f} us")
+    print(f"batches of {groups}: {len(spans)} (first {skip} skipped), mean first-eval k-NN span "
+          f"{sum(spans) / len(spans) / 1e3:.1f} us (min {min(spans) / 1e3:.1f}, max {max(spans) / 1e3:.1f})")
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:4])
