@@ -353,7 +353,7 @@ int livo_ctx_set_profiling(livo_ctx* c, int enable) {
             for (auto& e : g) HIP_TRY(hipEventCreate(&e));
         c->events_ready = true;
     }
-    c->profiling = enable ? 1 : 0;
+    c->profiling = enable < 0 ? 0 : (enable > 2 ? 2 : enable);
     return LIVO_OK;
 }
 
@@ -676,7 +676,8 @@ int livo_iekf_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_stat
         }
     }
     HIP_TRY(hipMemsetAsync(c->d_replay_count, 0, sizeof(unsigned) * kMaxGroups, c->stream));
-    const bool prof = c->profiling && c->events_ready;
+    const bool prof = c->profiling && c->events_ready;  // 1: first-search events only
+    const bool full = prof && c->profiling >= 2;         // 2: every evaluation's stages too
     // profiling: the batch's first search starts at ev[0][0], before the fork
     if (prof) HIP_TRY(hipEventRecord(c->ev[0][0], c->stream));
     if (ngroups > 1) {
@@ -699,21 +700,21 @@ int livo_iekf_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_stat
     for (int e = 0; e < evals; e++) {
         for (int gi = 0; gi < ngroups; gi++) {
             hipStream_t st = g[gi].st;
-            if (prof && (e > 0 || gi > 0)) HIP_TRY(hipEventRecord(c->ev[gi][3 * e], st));
+            if (full && (e > 0 || gi > 0)) HIP_TRY(hipEventRecord(c->ev[gi][3 * e], st));
             // leaf-map search; rematch passes are bounded by the previous neighbours
             // (the group's replay count was zeroed before the batch / by the last k_solve)
             rc = launch_knn_leaf(kp[gi], g[gi].count, g[gi].max_n, e > 0, st);
             if (rc) return rc;
-            if (prof) HIP_TRY(hipEventRecord(c->ev[gi][3 * e + 1], st));
+            if ((prof && e == 0) || full) HIP_TRY(hipEventRecord(c->ev[gi][3 * e + 1], st));
             rc = launch_hshare(hp[gi], g[gi].count, g[gi].max_nblk, e == 0, st);
             if (rc) return rc;
-            if (prof) HIP_TRY(hipEventRecord(c->ev[gi][3 * e + 2], st));
+            if (full) HIP_TRY(hipEventRecord(c->ev[gi][3 * e + 2], st));
             rc = launch_solve(sp[gi], g[gi].count, st);
             if (rc) return rc;
         }
     }
     for (int gi = 0; gi < ngroups; gi++)
-        if (prof) HIP_TRY(hipEventRecord(c->ev[gi][3 * LIVO_MAX_EVALS], g[gi].st));
+        if (full) HIP_TRY(hipEventRecord(c->ev[gi][3 * LIVO_MAX_EVALS], g[gi].st));
     for (int gi = 1; gi < ngroups; gi++) {
         HIP_TRY(hipEventRecord(c->xjoin[gi - 1], g[gi].st));
         HIP_TRY(hipStreamWaitEvent(c->stream, c->xjoin[gi - 1], 0));
@@ -741,7 +742,7 @@ int livo_iekf_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_stat
             t.knn_ms = std::max(t.knn_ms, (double)ms);
         }
         t.knn_launches = 1;
-        for (int gi = 0; gi < ngroups; gi++)
+        for (int gi = 0; gi < ngroups && full; gi++)
             for (int e = 0; e < evals; e++) {
                 float ms_k = 0.f, ms_h = 0.f, ms_s = 0.f;
                 if (e > 0) (void)hipEventElapsedTime(&ms_k, c->ev[gi][3 * e], c->ev[gi][3 * e + 1]);

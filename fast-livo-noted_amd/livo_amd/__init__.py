@@ -282,8 +282,10 @@ class Context:
             return sts, stats
         return [state_from_c(s) for s in sts], [stats_from_c(s) for s in stats]
 
-    def set_profiling(self, on: bool):
-        _check("livo_ctx_set_profiling", self._L.livo_ctx_set_profiling(self.h, int(bool(on))))
+    def set_profiling(self, level):
+        """0/False off, 1 first-search timing only, 2/True every stage (livo_ctx_set_profiling)."""
+        level = 2 if level is True else int(level)
+        _check("livo_ctx_set_profiling", self._L.livo_ctx_set_profiling(self.h, level))
 
     def last_timings(self) -> dict:
         t = Timings()

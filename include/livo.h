@@ -133,7 +133,10 @@ int livo_params_default(livo_params* p);
 int livo_ctx_create(int device, const livo_params* p, livo_ctx** out);
 int livo_ctx_destroy(livo_ctx* ctx);
 int livo_ctx_set_params(livo_ctx* ctx, const livo_params* p);
-int livo_ctx_set_profiling(livo_ctx* ctx, int enable);
+/* Device timing of livo_iekf_update* (livo_last_timings): 0 off; 1 the first
+ * search of the batch only (two events per stream group); 2 also every
+ * evaluation's k-NN / plane / solve stages (costs ~10% of throughput). */
+int livo_ctx_set_profiling(livo_ctx* ctx, int level);
 int livo_last_timings(livo_ctx* ctx, livo_timings* out);
 
 /* Build the device map from M host points (x,y,z floats at xyz + i*stride_bytes).

@@ -364,3 +364,26 @@ def test_batch_stream_groups(built, map100k, groups, monkeypatch):
             one, st1 = ctx.iekf_update(sid, states[i])
             assert all(np.array_equal(one[k], b[i][k]) for k in one)
             assert st1["iterations"] == st[i]["iterations"]
+
+
+@pytest.mark.gpu
+def test_profiling_levels(ctx100k):
+    """Profiling level 1 times only the batch's first search, level 2 every stage; neither
+    changes the results."""
+    synth = _synth()
+    sids = [ctx100k.scan_upload(synth.make_scan(3000, s)[0]) for s in range(3)]
+    states = [synth.make_state(s) for s in range(3)]
+    try:
+        ref, _ = ctx100k.iekf_update_batch(sids, states)
+        for level in (1, 2):
+            ctx100k.set_profiling(level)
+            out, _ = ctx100k.iekf_update_batch(sids, states)
+            t = ctx100k.last_timings()
+            ctx100k.set_profiling(0)
+            assert t["knn_ms"] > 0 and t["knn_queries"] == 9000
+            assert (t["solve_ms"] > 0) == (level == 2) and (t["plane_ms"] > 0) == (level == 2)
+            for a, b in zip(out, ref):
+                assert all(np.array_equal(a[k], b[k]) for k in a)
+    finally:
+        for sid in sids:
+            ctx100k.scan_release(sid)
