@@ -371,12 +371,17 @@ __global__ __launch_bounds__(kKnnBlock, 8) void k_knn_pass(KnnParams P) {  // 8 
     query_point(P, slot, reinterpret_cast<const float4*>(job.pts)[i], qx, qy, qz);
     SList s;
     sl_init(s);
-    unsigned flag = 0;  // reason bits: 1 CMP fuzz / equivalence, 2 point tied with the 5th
+    unsigned flag = 0;  // reason bits: 1 CMP fuzz / equivalence, 2 point tied with the 5th, 8 overrun
     unsigned visits = 0;
+    const unsigned max_visits = (2u << P.depth) + 64u;  // exit every wave reaches (see k_knn_leaf)
     uint32_t node = 0, cur = 0;
     uint32_t trail = 0;  // bit L: a far son at level L is pending (its box distance in dstack[L-1])
     bool has = P.has_map != 0;
     while (true) {
+        if (visits > max_visits) {
+            flag |= 8u;
+            break;
+        }
         if (!has) {
             if (trail == 0u) break;
             const int L = 31 - __clz(trail);
@@ -458,8 +463,104 @@ __global__ __launch_bounds__(kKnnBlock, 8) void k_knn_pass(KnnParams P) {  // 8 
 // distance of a point inside, as in calc_box_dist).  It tracks e6, the
 // smallest distance rejected or evicted from the 5 candidates, and flags the
 // query (exact replay on the ikd-Tree) if C1 or C2 fails.
+// One query of the leaf-map search: its world point, seed bound, sorted
+// 5-candidate list and e6 (smallest distance rejected or evicted).
+struct LeafQuery {
+    float qx, qy, qz, B, e6;
+    float d[kNN];
+    uint32_t nd[kNN];
+};
+
 template <bool SEEDED>
-__global__ __launch_bounds__(kKnnBlock, 8) void k_knn_leaf(KnnParams P) {
+__device__ __forceinline__ void lq_init(LeafQuery& q, const KnnParams& P, const IekfSlot* slot, const HsJob& job, int i,
+                                        bool valid) {
+#pragma unroll
+    for (int k = 0; k < kNN; k++) { q.d[k] = INFINITY; q.nd[k] = 0u; }
+    q.e6 = INFINITY;
+    q.B = INFINITY;
+    q.qx = q.qy = q.qz = 0.0f;
+    if (!valid) {
+        q.B = -INFINITY;  // threshold -inf: never asks for a box
+        return;
+    }
+    query_point(P, slot, reinterpret_cast<const float4*>(job.pts)[i], q.qx, q.qy, q.qz);
+    if (SEEDED) {
+        // the point's 5 previous neighbours, re-measured: 5 distinct map points
+        // at distance <= B, so B >= d5
+        const NNRec* sr = job.nn + i;
+        if (sr->cnt == kNN) {
+            float bmax = 0.0f;
+#pragma unroll
+            for (int k = 0; k < kNN; k++) {
+                const float4 a = reinterpret_cast<const float4*>(sr->p)[k];
+                const float dx = q.qx - a.x, dy = q.qy - a.y, dz = q.qz - a.z;
+                bmax = fmaxf(bmax, (dx * dx + dy * dy) + dz * dz);
+            }
+            q.B = bmax;
+        }
+    }
+}
+
+__device__ __forceinline__ float lq_thr(const LeafQuery& q) { return fminf(q.d[kNN - 1], q.B); }
+
+__device__ __forceinline__ void lq_point(LeafQuery& q, const float4 v, uint32_t slot) {
+    const float dx = q.qx - v.x, dy = q.qy - v.y, dz = q.qz - v.z;
+    const float dist = (dx * dx + dy * dy) + dz * dz;  // calc_dist (:1291-1295)
+    if (dist < q.d[kNN - 1]) {
+        q.e6 = fminf(q.e6, q.d[kNN - 1]);  // evicted (+inf while not full)
+        q.d[kNN - 1] = dist;
+        q.nd[kNN - 1] = slot;
+#pragma unroll
+        for (int k = kNN - 1; k > 0; k--) {
+            const bool sw = q.d[k] < q.d[k - 1];
+            const float td = q.d[k];
+            const uint32_t tn = q.nd[k];
+            q.d[k] = sw ? q.d[k - 1] : td;
+            q.nd[k] = sw ? q.nd[k - 1] : tn;
+            q.d[k - 1] = sw ? td : q.d[k - 1];
+            q.nd[k - 1] = sw ? tn : q.nd[k - 1];
+        }
+    } else {
+        q.e6 = fminf(q.e6, dist);
+    }
+}
+
+// C1/C2 check, neighbour record, replay flag.
+__device__ __forceinline__ void lq_finish(const LeafQuery& q, const KnnParams& P, const HsJob& job, unsigned bjob,
+                                          int i, const float4* __restrict__ lpts, bool overrun) {
+    const int cnt = (int)min<int64_t>(P.lM, (int64_t)kNN);
+    bool amb = overrun || q.e6 - q.d[kNN - 1] <= kFuzz;  // C1 (false while e6 = +inf)
+#pragma unroll
+    for (int k = 0; k + 1 < kNN; k++) amb |= (k + 1 < cnt) && (q.d[k + 1] - q.d[k] <= kFuzz);  // C2
+    // neighbour record: points, distances, original indices; node[] = leaf-map slots
+    float4* o4 = reinterpret_cast<float4*>(job.nn + i);
+    int32_t idx[kNN];
+#pragma unroll
+    for (int k = 0; k < kNN; k++) {
+        float4 v = make_float4(0.f, 0.f, 0.f, INFINITY);
+        idx[k] = -1;
+        if (k < cnt) {
+            const float4 a = lpts[q.nd[k]];
+            v = make_float4(a.x, a.y, a.z, q.d[k]);
+            idx[k] = (int32_t)__float_as_uint(a.w);
+        }
+        o4[k] = v;
+    }
+    const int flag = amb ? 4 : 0;
+    int4* oi = reinterpret_cast<int4*>(job.nn + i) + 5;
+    oi[0] = make_int4(idx[0], idx[1], idx[2], idx[3]);
+    oi[1] = make_int4(idx[4], cnt, flag, (int)q.nd[0]);
+    oi[2] = make_int4((int)q.nd[1], (int)q.nd[2], (int)q.nd[3], (int)q.nd[4]);
+    if (amb) flag_for_replay(P, bjob, i);
+}
+
+// Q queries per thread walk the tree together (a box is entered if any of them
+// may need it; a pending far son keeps the smallest of their box distances and
+// is re-checked against the largest threshold, which may visit a box no query
+// needs, never skip one).  Only Q = 1 is launched: measured on MI355X, Q = 2
+// (Morton-adjacent pairs sharing each load) was 1.4x slower at 8 scans.
+template <bool SEEDED, int Q>
+__global__ __launch_bounds__(kKnnBlock, Q == 1 ? 8 : 6) void k_knn_leaf(KnnParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned bjob, bx;
     xcd_block(P.nb, bjob, bx);
@@ -471,47 +572,38 @@ __global__ __launch_bounds__(kKnnBlock, 8) void k_knn_leaf(KnnParams P) {
         if (slot->ctrl.stop) return;
         if (SEEDED && !slot->ctrl.search_en) return;
     }
-    const int i = (int)bx * kKnnBlock + threadIdx.x;
-    if (i >= job.n) return;
+    const int i0 = ((int)bx * kKnnBlock + threadIdx.x) * Q;
+    if (i0 >= job.n) return;
     float* dstack = reinterpret_cast<float*>(smem) + threadIdx.x;
     const float4* __restrict__ lnodes = reinterpret_cast<const float4*>(P.lnodes);
     const float4* __restrict__ lpts = reinterpret_cast<const float4*>(P.lpts);
-    float qx, qy, qz;
-    query_point(P, slot, reinterpret_cast<const float4*>(job.pts)[i], qx, qy, qz);
-    float B = INFINITY;
-    if (SEEDED) {
-        // the point's 5 previous neighbours, re-measured: 5 distinct map points
-        // at distance <= B, so B >= d5
-        const NNRec* sr = job.nn + i;
-        if (sr->cnt == kNN) {
-            float bmax = 0.0f;
+    LeafQuery q[Q];
 #pragma unroll
-            for (int k = 0; k < kNN; k++) {
-                const float4 a = reinterpret_cast<const float4*>(sr->p)[k];
-                const float dx = qx - a.x, dy = qy - a.y, dz = qz - a.z;
-                bmax = fmaxf(bmax, (dx * dx + dy * dy) + dz * dz);
-            }
-            B = bmax;
-        }
-    }
-    float d[kNN];
-    uint32_t nd[kNN];
-#pragma unroll
-    for (int k = 0; k < kNN; k++) { d[k] = INFINITY; nd[k] = 0u; }
-    float e6 = INFINITY;
+    for (int u = 0; u < Q; u++) lq_init<SEEDED>(q[u], P, slot, job, i0 + u, i0 + u < job.n);
     const int D = P.ldepth;
     const uint32_t first_leaf = (1u << D) - 1u;
     const int64_t M = P.lM;
     unsigned visits = 0;
+    // a correct search visits each node at most once: past that, stop and let
+    // the exact replay answer (every wave reaches an exit)
+    const unsigned max_visits = (2u << D) + 64u;
+    bool overrun = false;
     uint32_t node = 0, cur = 0, trail = 0;
     bool has = M > 0;
     while (true) {
+        if (visits > max_visits) {
+            overrun = true;
+            break;
+        }
         if (!has) {
             if (trail == 0u) break;
             const int L = 31 - __clz(trail);
             trail &= ~(1u << L);
             const float de = dstack[(L - 1) * kKnnBlock];
-            if (de - fminf(d[kNN - 1], B) > kFuzz) continue;
+            float thr = lq_thr(q[0]);
+#pragma unroll
+            for (int u = 1; u < Q; u++) thr = fmaxf(thr, lq_thr(q[u]));
+            if (de - thr > kFuzz) continue;
             const uint32_t a = ((cur + 1u) >> (level_of(cur) - L)) - 1u;
             node = ((a - 1u) ^ 1u) + 1u;
         }
@@ -524,31 +616,13 @@ __global__ __launch_bounds__(kKnnBlock, 8) void k_knn_leaf(KnnParams P) {
             for (int k0 = lo; k0 < hi; k0 += 4) {
                 float4 v[4];
 #pragma unroll
-                for (int u = 0; u < 4; u++) v[u] = lpts[k0 + u];  // padded by 3 points
+                for (int w = 0; w < 4; w++) v[w] = lpts[k0 + w];  // padded by 3 points
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    if (k0 + u < hi) {
-                        const float dx = qx - v[u].x, dy = qy - v[u].y, dz = qz - v[u].z;
-                        const float dist = (dx * dx + dy * dy) + dz * dz;  // calc_dist (:1291-1295)
-                        if (dist < d[kNN - 1]) {
-                            e6 = fminf(e6, d[kNN - 1]);  // evicted (+inf while not full)
-                            d[kNN - 1] = dist;
-                            nd[kNN - 1] = (uint32_t)(k0 + u);
+                for (int w = 0; w < 4; w++)
+                    if (k0 + w < hi) {
 #pragma unroll
-                            for (int q = kNN - 1; q > 0; q--) {
-                                const bool sw = d[q] < d[q - 1];
-                                const float td = d[q];
-                                const uint32_t tn = nd[q];
-                                d[q] = sw ? d[q - 1] : td;
-                                nd[q] = sw ? nd[q - 1] : tn;
-                                d[q - 1] = sw ? td : d[q - 1];
-                                nd[q - 1] = sw ? tn : nd[q - 1];
-                            }
-                        } else {
-                            e6 = fminf(e6, dist);
-                        }
+                        for (int u = 0; u < Q; u++) lq_point(q[u], v[w], (uint32_t)(k0 + w));
                     }
-                }
             }
             has = false;
             continue;
@@ -557,44 +631,34 @@ __global__ __launch_bounds__(kKnnBlock, 8) void k_knn_leaf(KnnParams P) {
         const float4 b = rp[0];
         const float4 cc = rp[1];
         const float4 dd = rp[2];
-        const float dl = box_dist(qx, qy, qz, b.x, b.y, b.z, b.w, cc.x, cc.y);
-        const float dr = box_dist(qx, qy, qz, cc.z, cc.w, dd.x, dd.y, dd.z, dd.w);
-        const bool left_first = dl <= dr;
-        const float dnear = left_first ? dl : dr;
-        const float dfar = left_first ? dr : dl;
-        const float thr = fminf(d[kNN - 1], B);
-        if (dfar - thr <= kFuzz) {
+        bool want_l = false, want_r = false;
+        float ml = INFINITY, mr = INFINITY;
+#pragma unroll
+        for (int u = 0; u < Q; u++) {
+            const float dl = box_dist(q[u].qx, q[u].qy, q[u].qz, b.x, b.y, b.z, b.w, cc.x, cc.y);
+            const float dr = box_dist(q[u].qx, q[u].qy, q[u].qz, cc.z, cc.w, dd.x, dd.y, dd.z, dd.w);
+            const float thr = lq_thr(q[u]);
+            want_l |= dl - thr <= kFuzz;
+            want_r |= dr - thr <= kFuzz;
+            ml = fminf(ml, dl);
+            mr = fminf(mr, dr);
+        }
+        const bool left_first = ml <= mr;
+        const bool want_near = left_first ? want_l : want_r, want_far = left_first ? want_r : want_l;
+        // the far son waits on the stack only while the near son is searched
+        // first (a pop must find cur at or below the pending level); if only
+        // the far son is wanted, go there directly
+        if (want_near && want_far) {
             const int Lc = level_of(node) + 1;
-            dstack[(Lc - 1) * kKnnBlock] = dfar;
+            dstack[(Lc - 1) * kKnnBlock] = left_first ? mr : ml;
             trail |= 1u << Lc;
         }
-        has = dnear - thr <= kFuzz;
-        node = 2u * node + (left_first ? 1u : 2u);
+        has = want_near || want_far;
+        node = 2u * node + ((left_first == want_near) ? 1u : 2u);
     }
-    const int cnt = (int)min<int64_t>(M, (int64_t)kNN);
-    bool amb = e6 - d[kNN - 1] <= kFuzz;  // C1 (false while e6 = +inf)
 #pragma unroll
-    for (int k = 0; k + 1 < kNN; k++) amb |= (k + 1 < cnt) && (d[k + 1] - d[k] <= kFuzz);  // C2
-    // neighbour record: points, distances, original indices; node[] = leaf-map slots
-    float4* o4 = reinterpret_cast<float4*>(job.nn + i);
-    int32_t idx[kNN];
-#pragma unroll
-    for (int k = 0; k < kNN; k++) {
-        float4 v = make_float4(0.f, 0.f, 0.f, INFINITY);
-        idx[k] = -1;
-        if (k < cnt) {
-            const float4 a = lpts[nd[k]];
-            v = make_float4(a.x, a.y, a.z, d[k]);
-            idx[k] = (int32_t)__float_as_uint(a.w);
-        }
-        o4[k] = v;
-    }
-    const int flag = amb ? 4 : 0;
-    int4* oi = reinterpret_cast<int4*>(job.nn + i) + 5;
-    oi[0] = make_int4(idx[0], idx[1], idx[2], idx[3]);
-    oi[1] = make_int4(idx[4], cnt, flag, (int)nd[0]);
-    oi[2] = make_int4((int)nd[1], (int)nd[2], (int)nd[3], (int)nd[4]);
-    if (amb) flag_for_replay(P, bjob, i);
+    for (int u = 0; u < Q; u++)
+        if (i0 + u < job.n) lq_finish(q[u], P, job, bjob, i0 + u, lpts, overrun);
     count_visits(P, slot, visits);
 }
 
@@ -1331,9 +1395,9 @@ int launch_knn_leaf(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, 
     const dim3 grid((unsigned)(q.nb * n_jobs)), block(kKnnBlock);
     const size_t lds = knn_lds_bytes(p.ldepth + 1);
     if (seeded)
-        hipLaunchKernelGGL(k_knn_leaf<true>, grid, block, lds, (hipStream_t)stream, q);
+        hipLaunchKernelGGL((k_knn_leaf<true, 1>), grid, block, lds, (hipStream_t)stream, q);
     else
-        hipLaunchKernelGGL(k_knn_leaf<false>, grid, block, lds, (hipStream_t)stream, q);
+        hipLaunchKernelGGL((k_knn_leaf<false, 1>), grid, block, lds, (hipStream_t)stream, q);
     if (hipGetLastError() != hipSuccess) return LIVO_E_HIP;
     hipLaunchKernelGGL(k_knn_replay, dim3(64), dim3(64), 0, (hipStream_t)stream, q);
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;

@@ -52,7 +52,7 @@ def test_facade_matches_oracle(built, tmp_path):
     import oracle
     from livo_amd import synth
     m, body, st, files = _inputs(tmp_path)
-    r = subprocess.run([DEMO, *files, "4"], capture_output=True, text=True, timeout=300)
+    r = subprocess.run([DEMO, *files, "4"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     lines = {ln.split()[0]: ln.split()[1:] for ln in r.stdout.splitlines()}
     hs = np.array(lines["hshare"], dtype=np.float64)
