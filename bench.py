@@ -209,7 +209,7 @@ def main():
                          "visits_per_query_ref": round(v_ref / max(queries_per_launch, 1), 3),
                          "visits_per_query_gpu": round(knn_visits / max(knn_queries, 1), 3)},
             "device_ms_per_step": {"knn_first": round(t_first / n_prof, 4), "knn_rematch": round(t_rematch / n_prof, 4),
-                                   "plane_H": round(t_plane / n_prof, 4), "solve": round(t_solve / n_prof, 4),
+                                   "plane_H_solve": round(t_plane / n_prof, 4),
                                    "note": f"{n_prof} extra untimed steps with per-stage events; stages other than "
                                            "knn_first summed over the concurrent stream groups"},
             "knn_replays_per_step": round(replays / a.steps, 2),

@@ -474,7 +474,8 @@ int livo_scan_upload(livo_ctx* c, const float* xyz, int64_t N, int64_t stride_by
     ScanBuf s;
     s.used = true;
     s.n = N;
-    s.nblk = (int32_t)((N + kBlock * kPtsPerThread - 1) / (kBlock * kPtsPerThread));
+    // at least one plane-pass block: its last block also runs the scan's solve
+    s.nblk = (int32_t)std::max<int64_t>(1, (N + kBlock * kPtsPerThread - 1) / (kBlock * kPtsPerThread));
     int rc = 0;
     rc |= dev_alloc(&s.pts, (size_t)N * 4);
     rc |= dev_alloc(&s.nn, (size_t)N);
@@ -569,9 +570,7 @@ int livo_h_share(livo_ctx* c, int32_t id, const livo_state* state, int search_en
     }
     rc = launch_hshare(hp, 1, std::max(s->nblk, 1), search_en != 0, c->stream);
     if (rc) return rc;
-    SolveParams sp{c->d_slots, c->d_jobs, nullptr, 1};  // mode 1: reduce the partials only
-    rc = launch_solve(sp, 1, c->stream);
-    if (rc) return rc;
+    // the last plane-pass block has reduced the sums into slot->red (hp.solve = 0)
     HIP_TRY(hipMemcpyAsync(c->h_slots, c->d_slots, sizeof(IekfSlot), hipMemcpyDeviceToHost, c->stream));
     std::vector<float> h_nv, h_w;
     std::vector<uint8_t> h_sel;
@@ -687,7 +686,6 @@ int livo_iekf_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_stat
     const int evals = max_iter + 1;
     HsParams hp[kMaxGroups];
     KnnParams kp[kMaxGroups];
-    SolveParams sp[kMaxGroups];
     for (int gi = 0; gi < ngroups; gi++) {
         hp[gi] = make_hs_params(c);
         hp[gi].jobs = c->d_jobs + g[gi].first;
@@ -695,7 +693,8 @@ int livo_iekf_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_stat
         kp[gi].jobs = c->d_jobs + g[gi].first;
         kp[gi].replay_count = c->d_replay_count + gi;
         kp[gi].replay_list = c->d_replay_list + g[gi].off;
-        sp[gi] = SolveParams{c->d_slots + g[gi].first, c->d_jobs + g[gi].first, c->d_replay_count + gi, 0};
+        hp[gi].solve = 1;  // the last plane-pass block of each scan runs its solve
+        hp[gi].replay_count = c->d_replay_count + gi;
     }
     for (int e = 0; e < evals; e++) {
         for (int gi = 0; gi < ngroups; gi++) {
@@ -707,9 +706,6 @@ int livo_iekf_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_stat
             if (rc) return rc;
             if ((prof && e == 0) || full) HIP_TRY(hipEventRecord(c->ev[gi][3 * e + 1], st));
             rc = launch_hshare(hp[gi], g[gi].count, g[gi].max_nblk, e == 0, st);
-            if (rc) return rc;
-            if (full) HIP_TRY(hipEventRecord(c->ev[gi][3 * e + 2], st));
-            rc = launch_solve(sp[gi], g[gi].count, st);
             if (rc) return rc;
         }
     }
@@ -744,14 +740,12 @@ int livo_iekf_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_stat
         t.knn_launches = 1;
         for (int gi = 0; gi < ngroups && full; gi++)
             for (int e = 0; e < evals; e++) {
-                float ms_k = 0.f, ms_h = 0.f, ms_s = 0.f;
+                float ms_k = 0.f, ms_h = 0.f;
                 if (e > 0) (void)hipEventElapsedTime(&ms_k, c->ev[gi][3 * e], c->ev[gi][3 * e + 1]);
-                (void)hipEventElapsedTime(&ms_h, c->ev[gi][3 * e + 1], c->ev[gi][3 * e + 2]);
                 const hipEvent_t end = (e + 1 < evals) ? c->ev[gi][3 * e + 3] : c->ev[gi][3 * LIVO_MAX_EVALS];
-                (void)hipEventElapsedTime(&ms_s, c->ev[gi][3 * e + 2], end);
+                (void)hipEventElapsedTime(&ms_h, c->ev[gi][3 * e + 1], end);
                 t.rematch_knn_ms += ms_k;
-                t.plane_ms += ms_h;
-                t.solve_ms += ms_s;
+                t.plane_ms += ms_h;  // plane pass + the solve run by its last block
             }
         // the first evaluation searches for every point of every scan
         for (int32_t b = 0; b < n; b++) {

@@ -104,6 +104,8 @@ struct alignas(16) IekfSlot {
     IekfCtrl ctrl;
     unsigned long long visits[LIVO_MAX_EVALS];  // k-NN nodes visited per evaluation
     int32_t eval_search[LIVO_MAX_EVALS];
+    unsigned hs_ticket;         // k_hshare blocks done in the current pass (the last one reduces)
+    unsigned pad_[3];
 };
 
 // Nearest_Points[i] + pointSearchSqDis for one point: 128 B, written by the
@@ -144,7 +146,8 @@ struct HsParams {
     float plane_thr;        // 0.1f
     float max_sqd;          // 5.0f
     int32_t force;          // -1: follow ctrl; 0: no search; 1: search
-    int32_t pad;
+    int32_t solve;          // 1: the last block of a scan also runs its solve (IEKF loop)
+    unsigned* replay_count; // zeroed once per launch (the group's k-NN replay count), may be null
 };
 
 struct KnnParams {

@@ -907,120 +907,6 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
-// ===================================================== per-point pass =====
-template <bool FIRST>
-__global__ __launch_bounds__(kBlock) void k_hshare(HsParams P) {
-    __shared__ double red_lds[4 * kRedCols];
-    const HsJob job = P.jobs[blockIdx.y];
-    if ((int)blockIdx.x >= job.nblk) return;
-    IekfSlot* slot = job.slot;
-    int search;
-    if (P.force >= 0) {
-        search = P.force;
-    } else {
-        if (slot->ctrl.stop) return;  // block-uniform
-        search = FIRST ? 1 : slot->ctrl.search_en;
-    }
-    const int tid = threadIdx.x;
-    const livo_state& S = slot->state;
-    double acc[kRedUsed];
-#pragma unroll
-    for (int j = 0; j < kRedUsed; j++) acc[j] = 0.0;
-
-    for (int rep = 0; rep < kPtsPerThread; rep++) {  // points of this block: strided for coalescing
-    const int i = (blockIdx.x * kPtsPerThread + rep) * kBlock + tid;
-    const bool valid = i < job.n;
-    if (valid) {
-        const float4 pb = reinterpret_cast<const float4*>(job.pts)[i];
-        const double* R = S.rot;
-        float wx, wy, wz;
-        world_point(R, S.pos, P.R_LI, P.t_LI, pb.x, pb.y, pb.z, wx, wy, wz);
-        if (P.dbg.world) {
-            P.dbg.world[3 * i + 0] = wx;
-            P.dbg.world[3 * i + 1] = wy;
-            P.dbg.world[3 * i + 2] = wz;
-        }
-        const float4* rec = reinterpret_cast<const float4*>(job.nn + i);
-        float nx[kNN], ny[kNN], nz[kNN];
-        float d4 = 0.0f;
-#pragma unroll
-        for (int k = 0; k < kNN; k++) {
-            const float4 v = rec[k];
-            nx[k] = v.x; ny[k] = v.y; nz[k] = v.z;
-            if (k == kNN - 1) d4 = v.w;
-        }
-        const int cnt = reinterpret_cast<const int4*>(job.nn + i)[6].y;
-        // point_selected_surf: sqdis[4] > 5 => false after a search (:518); true otherwise (:490)
-        const bool sel = search ? ((cnt == kNN) && !(d4 > P.max_sqd)) : true;
-        bool accepted = false, keep = false;
-        float pa[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        float pd2 = 0.0f;
-        if (sel && cnt >= kNN) {
-            if (esti_plane(nx, ny, nz, P.plane_thr, pa)) {
-                pd2 = ((pa[0] * wx + pa[1] * wy) + pa[2] * wz) + pa[3];
-                const double bx = pb.x, by = pb.y, bz = pb.z;
-                const double bn = sqrt((bx * bx + by * by) + bz * bz);
-                const float s = (float)(1 - 0.9 * (double)fabsf(pd2) / sqrt(bn));
-                accepted = (double)s > 0.9;                          // :535-542
-                keep = accepted && (double)fabsf(pd2) <= P.max_res;  // :552
-            }
-        }
-        if (P.dbg.normvec)
-            reinterpret_cast<float4*>(P.dbg.normvec)[i] =
-                accepted ? make_float4(pa[0], pa[1], pa[2], pd2) : make_float4(0.f, 0.f, 0.f, 0.f);
-        if (P.dbg.sel) P.dbg.sel[i] = keep ? 1 : 0;
-        if (keep) {
-            // Jacobian row (laser_mapping.cpp:564-593): p_I = R_LI p_b + t_LI;
-            // A = [p_I]x * rot^T * n;  Hsub = [A, n]
-            const double bx = pb.x, by = pb.y, bz = pb.z;
-            const double* RL = P.R_LI;
-            const double ix = ((RL[0] * bx + RL[1] * by) + RL[2] * bz) + P.t_LI[0];
-            const double iy = ((RL[3] * bx + RL[4] * by) + RL[5] * bz) + P.t_LI[1];
-            const double iz = ((RL[6] * bx + RL[7] * by) + RL[8] * bz) + P.t_LI[2];
-            const double cr[9] = {0.0, -iz, iy, iz, 0.0, -ix, -iy, ix, 0.0};
-            double M[9];
-#pragma unroll
-            for (int r = 0; r < 3; r++)
-#pragma unroll
-                for (int cI = 0; cI < 3; cI++)
-                    M[r * 3 + cI] = (cr[r * 3 + 0] * R[cI * 3 + 0] + cr[r * 3 + 1] * R[cI * 3 + 1]) +
-                                    cr[r * 3 + 2] * R[cI * 3 + 2];
-            const double n0 = pa[0], n1 = pa[1], n2 = pa[2];
-            double H[6];
-            H[0] = (M[0] * n0 + M[1] * n1) + M[2] * n2;
-            H[1] = (M[3] * n0 + M[4] * n1) + M[5] * n2;
-            H[2] = (M[6] * n0 + M[7] * n1) + M[8] * n2;
-            H[3] = n0; H[4] = n1; H[5] = n2;
-            const double err = -(double)pd2;
-            int q = 0;
-#pragma unroll
-            for (int r = 0; r < 6; r++) {
-                const double hs = H[r] * P.inv_r;
-#pragma unroll
-                for (int cI = r; cI < 6; cI++) acc[q++] += hs * H[cI];
-            }
-#pragma unroll
-            for (int r = 0; r < 6; r++) acc[21 + r] += (H[r] * P.inv_r) * err;
-            acc[27] += (double)fabsf(pd2);
-            acc[28] += 1.0;
-        }
-    }
-    }
-    // block reduction: wave shuffle tree, then waves in order
-    const int lane = tid & 63, wave = tid >> 6;
-#pragma unroll
-    for (int j = 0; j < kRedUsed; j++) {
-        const double v = wave_sum(acc[j]);
-        if (lane == 0) red_lds[wave * kRedCols + j] = v;
-    }
-    __syncthreads();
-    if (tid < kRedUsed) {
-        const double v = ((red_lds[0 * kRedCols + tid] + red_lds[1 * kRedCols + tid]) + red_lds[2 * kRedCols + tid]) +
-                         red_lds[3 * kRedCols + tid];
-        job.partial[(size_t)blockIdx.x * kRedCols + tid] = v;
-    }
-}
-
 // ========================================================== solve =========
 // One wave per scan, the reference's algebra in the oracle's operation order
 // (laser_mapping.cpp:187-193): P^-1 once per update, K1 = (H_T_H + P^-1)^-1
@@ -1150,54 +1036,38 @@ __device__ unsigned long long g_solve_prof[256][16];
 #else
 #define SOLVE_MARK(k) do { } while (0)
 #endif
-__global__ __launch_bounds__(64) void k_solve(SolveParams P) {
-    __shared__ double s_sum[kRedCols];
-    __shared__ double s_P[kDim * kDim];      // state.cov
-    __shared__ double s_Pinv[kDim * kDim];
-    __shared__ double s_LU[kDim * kDim];
-    __shared__ double s_K1[kDim * 9];        // K1(:, 0:9)
-    __shared__ double s_G[kDim * 9];         // G(:, 0:9)
-    __shared__ double s_HTH[81];
-    __shared__ double s_vec[kDim];
-    __shared__ double s_sol[kDim];
-    __shared__ int s_piv[kDim];
-    const HsJob job = P.jobs[blockIdx.x];
-    IekfSlot* slot = job.slot;
-    const int lane = threadIdx.x;
-    // the k-NN replay of this evaluation has run (stream order): reset its count
-    if (P.replay_count && blockIdx.x == 0 && lane == 0) *P.replay_count = 0u;
-    if (P.mode == 0 && slot->ctrl.stop) return;
-    SOLVE_MARK(0);
+// LDS of one scan's solve.
+struct SolveLds {
+    double sum[kRedCols];
+    double P[kDim * kDim];      // state.cov
+    double Pinv[kDim * kDim];
+    double LU[kDim * kDim];
+    double K1[kDim * 9];        // K1(:, 0:9)
+    double G[kDim * 9];         // G(:, 0:9)
+    double HTH[81];
+    double vec[kDim];
+    double sol[kDim];
+    int piv[kDim];
+};
 
-    // 1. deterministic reduction of the block partials: lane (c, h) sums the
-    //    blocks b = h, h+2, ... of column c with 8 loads in flight, in a fixed
-    //    association; then the two halves.
-    {
-        const int col = lane & 31, half = lane >> 5;
-        const double* src = job.partial + col;
-        double acc8[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) acc8[k] = 0.0;
-        int b = half;
-        for (; b + 14 < job.nblk; b += 16) {
-#pragma unroll
-            for (int k = 0; k < 8; k++) acc8[k] += src[(size_t)(b + 2 * k) * kRedCols];
-        }
-#pragma unroll
-        for (int k = 0; k < 8; k++)
-            if (b + 2 * k < job.nblk) acc8[k] += src[(size_t)(b + 2 * k) * kRedCols];
-        double sum = ((acc8[0] + acc8[1]) + (acc8[2] + acc8[3])) + ((acc8[4] + acc8[5]) + (acc8[6] + acc8[7]));
-        sum += __shfl_xor(sum, 32, 64);
-        if (col >= kRedUsed) sum = 0.0;
-        if (lane < kRedCols) {
-            s_sum[lane] = sum;
-            slot->red[lane] = sum;
-        }
-    }
-    SOLVE_MARK(1);
-    if (P.mode == 1) return;
+// One wave (lanes 0..63 of the calling block, the other waves idle): the
+// reference's algebra in the oracle's operation order (laser_mapping.cpp:187-238)
+// from the reduced h_share sums in L.sum.  Only this wave touches L, so LDS
+// hand-offs between lanes need a wave-level fence, not a block barrier.
+#define WAVE_SYNC() do { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); __builtin_amdgcn_wave_barrier(); } while (0)
+__device__ __forceinline__ void solve_scan(IekfSlot* slot, SolveLds& L, const int lane) {
+    double* const s_sum = L.sum;
+    double* const s_P = L.P;
+    double* const s_Pinv = L.Pinv;
+    double* const s_LU = L.LU;
+    double* const s_K1 = L.K1;
+    double* const s_G = L.G;
+    double* const s_HTH = L.HTH;
+    double* const s_vec = L.vec;
+    double* const s_sol = L.sol;
+    int* const s_piv = L.piv;
     for (int t = lane; t < kDim * kDim; t += 64) s_P[t] = slot->state.cov[t];
-    __syncthreads();
+    WAVE_SYNC();
     // 2. HTH (9x9, rows/cols 6..8 zero: gnss_en = 0)
     for (int t = lane; t < 81; t += 64) {
         const int r = t / 9, c = t % 9;
@@ -1218,19 +1088,19 @@ __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
 #pragma unroll
         for (int j = 0; j < kDim; j++) A[j] = row ? s_P[lane * kDim + j] : 0.0;
         wave_lu_to_lds(A, lane, s_LU, s_piv);
-        __syncthreads();
+        WAVE_SYNC();
         if (lane < kDim) {
             double y[kDim];
             lds_lu_column(s_LU, s_piv, lane, y);
 #pragma unroll
             for (int i = 0; i < kDim; i++) s_Pinv[i * kDim + lane] = y[i];
         }
-        __syncthreads();
+        WAVE_SYNC();
         for (int t = lane; t < kDim * kDim; t += 64) slot->Pinv[t] = s_Pinv[t];
     } else {
         for (int t = lane; t < kDim * kDim; t += 64) s_Pinv[t] = slot->Pinv[t];
     }
-    __syncthreads();
+    WAVE_SYNC();
     SOLVE_MARK(3);
     // 4. K1 = (H_T_H + P^-1)^-1, columns 0..8
     {
@@ -1239,7 +1109,7 @@ __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
         for (int j = 0; j < kDim; j++)
             A[j] = row ? (((lane < 9 && j < 9) ? s_HTH[lane * 9 + j] : 0.0) + s_Pinv[lane * kDim + j]) : 0.0;
         wave_lu_to_lds(A, lane, s_LU, s_piv);
-        __syncthreads();
+        WAVE_SYNC();
         SOLVE_MARK(4);
         if (lane < 9) {
             double y[kDim];
@@ -1247,7 +1117,7 @@ __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
 #pragma unroll
             for (int i = 0; i < kDim; i++) s_K1[i * 9 + lane] = y[i];
         }
-        __syncthreads();
+        WAVE_SYNC();
     }
     SOLVE_MARK(5);
     // 5. G(:,0:9) = K1(:,0:9) * HTH ; columns 9..17 stay zero
@@ -1279,7 +1149,7 @@ __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
             s_vec[15 + r] = a.gravity[r] - b.gravity[r];
         }
     }
-    __syncthreads();
+    WAVE_SYNC();
     SOLVE_MARK(6);
     // 7. solution = K1(:,0:9) HTL + vec - G(:,0:9) vec(0:9)
     if (row) {
@@ -1296,7 +1166,7 @@ __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
         const int i = t / kDim, j = t % kDim;
         slot->G[t] = j < 9 ? s_G[i * 9 + j] : 0.0;
     }
-    __syncthreads();
+    WAVE_SYNC();
 
     SOLVE_MARK(7);
     // 8. boxplus, convergence, rematch control (laser_mapping.cpp:204-237), lane 0
@@ -1367,6 +1237,217 @@ __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
         }
     }
     SOLVE_MARK(9);
+}
+
+// ===================================================== per-point pass =====
+template <bool FIRST>
+__global__ __launch_bounds__(kBlock) void k_hshare(HsParams P) {
+    __shared__ double red_lds[4 * kRedCols];
+    __shared__ double fin_lds[8 * kRedCols];
+    __shared__ SolveLds L;
+    __shared__ int last_lds;
+    const HsJob job = P.jobs[blockIdx.y];
+    // the k-NN replay of this evaluation has run (stream order): reset its count
+    if (P.replay_count && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *P.replay_count = 0u;
+    if ((int)blockIdx.x >= job.nblk) return;
+    IekfSlot* slot = job.slot;
+    int search;
+    if (P.force >= 0) {
+        search = P.force;
+    } else {
+        if (slot->ctrl.stop) return;  // block-uniform
+        search = FIRST ? 1 : slot->ctrl.search_en;
+    }
+    const int tid = threadIdx.x;
+    const livo_state& S = slot->state;
+    double acc[kRedUsed];
+#pragma unroll
+    for (int j = 0; j < kRedUsed; j++) acc[j] = 0.0;
+
+    for (int rep = 0; rep < kPtsPerThread; rep++) {  // points of this block: strided for coalescing
+    const int i = (blockIdx.x * kPtsPerThread + rep) * kBlock + tid;
+    const bool valid = i < job.n;
+    if (valid) {
+        const float4 pb = reinterpret_cast<const float4*>(job.pts)[i];
+        const double* R = S.rot;
+        float wx, wy, wz;
+        world_point(R, S.pos, P.R_LI, P.t_LI, pb.x, pb.y, pb.z, wx, wy, wz);
+        if (P.dbg.world) {
+            P.dbg.world[3 * i + 0] = wx;
+            P.dbg.world[3 * i + 1] = wy;
+            P.dbg.world[3 * i + 2] = wz;
+        }
+        const float4* rec = reinterpret_cast<const float4*>(job.nn + i);
+        float nx[kNN], ny[kNN], nz[kNN];
+        float d4 = 0.0f;
+#pragma unroll
+        for (int k = 0; k < kNN; k++) {
+            const float4 v = rec[k];
+            nx[k] = v.x; ny[k] = v.y; nz[k] = v.z;
+            if (k == kNN - 1) d4 = v.w;
+        }
+        const int cnt = reinterpret_cast<const int4*>(job.nn + i)[6].y;
+        // point_selected_surf: sqdis[4] > 5 => false after a search (:518); true otherwise (:490)
+        const bool sel = search ? ((cnt == kNN) && !(d4 > P.max_sqd)) : true;
+        bool accepted = false, keep = false;
+        float pa[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        float pd2 = 0.0f;
+        if (sel && cnt >= kNN) {
+            if (esti_plane(nx, ny, nz, P.plane_thr, pa)) {
+                pd2 = ((pa[0] * wx + pa[1] * wy) + pa[2] * wz) + pa[3];
+                const double bx = pb.x, by = pb.y, bz = pb.z;
+                const double bn = sqrt((bx * bx + by * by) + bz * bz);
+                const float s = (float)(1 - 0.9 * (double)fabsf(pd2) / sqrt(bn));
+                accepted = (double)s > 0.9;                          // :535-542
+                keep = accepted && (double)fabsf(pd2) <= P.max_res;  // :552
+            }
+        }
+        if (P.dbg.normvec)
+            reinterpret_cast<float4*>(P.dbg.normvec)[i] =
+                accepted ? make_float4(pa[0], pa[1], pa[2], pd2) : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (P.dbg.sel) P.dbg.sel[i] = keep ? 1 : 0;
+        if (keep) {
+            // Jacobian row (laser_mapping.cpp:564-593): p_I = R_LI p_b + t_LI;
+            // A = [p_I]x * rot^T * n;  Hsub = [A, n]
+            const double bx = pb.x, by = pb.y, bz = pb.z;
+            const double* RL = P.R_LI;
+            const double ix = ((RL[0] * bx + RL[1] * by) + RL[2] * bz) + P.t_LI[0];
+            const double iy = ((RL[3] * bx + RL[4] * by) + RL[5] * bz) + P.t_LI[1];
+            const double iz = ((RL[6] * bx + RL[7] * by) + RL[8] * bz) + P.t_LI[2];
+            const double cr[9] = {0.0, -iz, iy, iz, 0.0, -ix, -iy, ix, 0.0};
+            double M[9];
+#pragma unroll
+            for (int r = 0; r < 3; r++)
+#pragma unroll
+                for (int cI = 0; cI < 3; cI++)
+                    M[r * 3 + cI] = (cr[r * 3 + 0] * R[cI * 3 + 0] + cr[r * 3 + 1] * R[cI * 3 + 1]) +
+                                    cr[r * 3 + 2] * R[cI * 3 + 2];
+            const double n0 = pa[0], n1 = pa[1], n2 = pa[2];
+            double H[6];
+            H[0] = (M[0] * n0 + M[1] * n1) + M[2] * n2;
+            H[1] = (M[3] * n0 + M[4] * n1) + M[5] * n2;
+            H[2] = (M[6] * n0 + M[7] * n1) + M[8] * n2;
+            H[3] = n0; H[4] = n1; H[5] = n2;
+            const double err = -(double)pd2;
+            int q = 0;
+#pragma unroll
+            for (int r = 0; r < 6; r++) {
+                const double hs = H[r] * P.inv_r;
+#pragma unroll
+                for (int cI = r; cI < 6; cI++) acc[q++] += hs * H[cI];
+            }
+#pragma unroll
+            for (int r = 0; r < 6; r++) acc[21 + r] += (H[r] * P.inv_r) * err;
+            acc[27] += (double)fabsf(pd2);
+            acc[28] += 1.0;
+        }
+    }
+    }
+    // block reduction: wave shuffle tree, then waves in order
+    const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+    for (int j = 0; j < kRedUsed; j++) {
+        const double v = wave_sum(acc[j]);
+        if (lane == 0) red_lds[wave * kRedCols + j] = v;
+    }
+    __syncthreads();
+    // Wave 0 stores the block partial write-through (sc1) and, once the store
+    // has drained, takes the scan's ticket; the last block of the scan then
+    // reduces every partial with sc1 loads in a fixed order and its wave 0 runs
+    // the scan's solve (MI355X_MICROARCH.md §Workgroup dispatch: sc1 hand-off,
+    // no L2 write-back fence).  One launch less per evaluation than a separate
+    // solve kernel.
+    if (tid < 64) {
+        if (tid < kRedUsed) {
+            const double v = ((red_lds[0 * kRedCols + tid] + red_lds[1 * kRedCols + tid]) +
+                              red_lds[2 * kRedCols + tid]) + red_lds[3 * kRedCols + tid];
+            __hip_atomic_store(job.partial + (size_t)blockIdx.x * kRedCols + tid, v, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (tid == 0)
+            last_lds = __hip_atomic_fetch_add(&slot->hs_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                       (unsigned)job.nblk - 1u;
+    }
+    __syncthreads();
+    if (!last_lds) return;
+    {
+        // thread (g, c) sums blocks g, g+8, ... of column c, 16 loads in flight
+        const int c = tid & 31, g = tid >> 5;
+        double acc16 = 0.0;
+        if (c < kRedUsed) {
+            double* src = job.partial + c;
+            for (int b0 = g; b0 < job.nblk; b0 += 128) {
+                double v[16];
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    const int b = b0 + 8 * k;
+                    v[k] = b < job.nblk ? __hip_atomic_load(src + (size_t)b * kRedCols, __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT)
+                                        : 0.0;
+                }
+#pragma unroll
+                for (int k = 0; k < 16; k++) acc16 += v[k];
+            }
+        }
+        fin_lds[g * kRedCols + c] = acc16;
+    }
+    __syncthreads();
+    if (tid >= 64) return;  // the solve is one wave's work
+    if (tid < kRedCols) {
+        double v = 0.0;
+        if (tid < kRedUsed)
+            v = ((fin_lds[0 * kRedCols + tid] + fin_lds[1 * kRedCols + tid]) +
+                 (fin_lds[2 * kRedCols + tid] + fin_lds[3 * kRedCols + tid])) +
+                ((fin_lds[4 * kRedCols + tid] + fin_lds[5 * kRedCols + tid]) +
+                 (fin_lds[6 * kRedCols + tid] + fin_lds[7 * kRedCols + tid]));
+        L.sum[tid] = v;
+        slot->red[tid] = v;
+    }
+    if (tid == 0) slot->hs_ticket = 0u;  // ready for the next pass
+    if (!P.solve) return;  // livo_h_share: the sums only
+    WAVE_SYNC();
+    solve_scan(slot, L, tid);
+}
+
+__global__ __launch_bounds__(64) void k_solve(SolveParams P) {
+    __shared__ SolveLds L;
+    const HsJob job = P.jobs[blockIdx.x];
+    IekfSlot* slot = job.slot;
+    const int lane = threadIdx.x;
+    // the k-NN replay of this evaluation has run (stream order): reset its count
+    if (P.replay_count && blockIdx.x == 0 && lane == 0) *P.replay_count = 0u;
+    if (P.mode == 0 && slot->ctrl.stop) return;
+    SOLVE_MARK(0);
+    // deterministic reduction of the block partials: lane (c, h) sums the
+    // blocks b = h, h+2, ... of column c with 8 loads in flight, in a fixed
+    // association; then the two halves.
+    {
+        const int col = lane & 31, half = lane >> 5;
+        const double* src = job.partial + col;
+        double acc8[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) acc8[k] = 0.0;
+        int b = half;
+        for (; b + 14 < job.nblk; b += 16) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) acc8[k] += src[(size_t)(b + 2 * k) * kRedCols];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if (b + 2 * k < job.nblk) acc8[k] += src[(size_t)(b + 2 * k) * kRedCols];
+        double sum = ((acc8[0] + acc8[1]) + (acc8[2] + acc8[3])) + ((acc8[4] + acc8[5]) + (acc8[6] + acc8[7]));
+        sum += __shfl_xor(sum, 32, 64);
+        if (col >= kRedUsed) sum = 0.0;
+        if (lane < kRedCols) {
+            L.sum[lane] = sum;
+            slot->red[lane] = sum;
+        }
+    }
+    SOLVE_MARK(1);
+    if (P.mode == 1) return;
+    WAVE_SYNC();
+    solve_scan(slot, L, lane);
 }
 
 // ======================================================== launchers =======

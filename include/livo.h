@@ -117,8 +117,8 @@ typedef struct livo_point_out {
 typedef struct livo_timings {
     double knn_ms;         /* first-evaluation k-NN of the batch, device wall time     */
     double rematch_knn_ms; /* k-NN launches of later evaluations (rematch)             */
-    double plane_ms;       /* plane fit + Jacobian + partial-sum launches (all evals)  */
-    double solve_ms;       /* reduction + 18x18 solve launches                         */
+    double plane_ms;       /* plane fit + Jacobian + reduction + 18x18 solve (fused)   */
+    double solve_ms;       /* 0: the solve runs in the plane pass's last block         */
     int64_t knn_launches;  /* first-evaluation k-NN phases timed (1 per call)          */
     int64_t knn_visits;    /* tree nodes those searches visited (pilot-seeded: < V_ref) */
     int64_t knn_queries;   /* points those launches processed                          */

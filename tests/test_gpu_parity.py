@@ -381,7 +381,7 @@ def test_profiling_levels(ctx100k):
             t = ctx100k.last_timings()
             ctx100k.set_profiling(0)
             assert t["knn_ms"] > 0 and t["knn_queries"] == 9000
-            assert (t["solve_ms"] > 0) == (level == 2) and (t["plane_ms"] > 0) == (level == 2)
+            assert (t["plane_ms"] > 0) == (level == 2)  # plane pass + the solve of its last block
             for a, b in zip(out, ref):
                 assert all(np.array_equal(a[k], b[k]) for k in a)
     finally:
