@@ -77,11 +77,17 @@ def main():
     import torch.distributed as dist
 
     torch_dev = None
+    device = local_rank
     if torch.cuda.is_available():
-        torch.cuda.set_device(local_rank)
-        torch_dev = torch.device("cuda", local_rank)
+        # one process per GPU; more ranks than GPUs (a rehearsal on a 1-GPU box) share them
+        device = local_rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(device)
+        torch_dev = torch.device("cuda", device)
+    # RCCL (backend "nccl") over xGMI on the GPU node; LIVO_BENCH_BACKEND=gloo for rehearsals
+    backend = os.environ.get("LIVO_BENCH_BACKEND") or ("nccl" if torch_dev is not None else "gloo")
+    coll_dev = torch_dev if backend == "nccl" else None
     if world > 1:
-        dist.init_process_group("nccl" if torch_dev is not None else "gloo")
+        dist.init_process_group(backend)
 
     def barrier():
         if world > 1:
@@ -97,7 +103,7 @@ def main():
     scans = [synth.make_scan(a.scan_points, s)[0] for s in scan_ids]
     st0 = [synth.make_state(s) for s in scan_ids]
 
-    ctx = livo_amd.Context(local_rank, t_LI=synth.T_LI, max_iterations=a.max_iter)
+    ctx = livo_amd.Context(device, t_LI=synth.T_LI, max_iterations=a.max_iter)
     t = time.time()
     ctx.map_build(m)
     map_build_s = time.time() - t
@@ -158,8 +164,8 @@ def main():
         t_solve += tm["solve_ms"]
     ctx.set_profiling(0)
     counters.knn_visits, counters.knn_queries = knn_visits, knn_queries
-    elapsed_max = farm.allreduce_max(elapsed, torch_dev)
-    total = farm.allreduce_counters(counters, torch_dev)
+    elapsed_max = farm.allreduce_max(elapsed, coll_dev)
+    total = farm.allreduce_counters(counters, coll_dev)
 
     # ---- roofline of the dominant kernels (rank-local): the first-evaluation
     # k-NN of one batch (pilot + pilot-seeded passes + replays, both streams)
