@@ -215,6 +215,57 @@ def make_state(scan_id: int = 0, rot_deg: float = 1.0, trans_m: float = 0.1):
     }
 
 
+IKN = 23                   # state_ikfom DOF (use-ikfom.hpp:12-21)
+S2_LEN = 98090.0 / 10000.0  # MTK::S2<double, 98090, 10000, 1> length (use-ikfom.hpp:9)
+
+
+def rot_to_quat(R: np.ndarray) -> np.ndarray:
+    """Unit quaternion (w, x, y, z), w >= 0, of a rotation matrix (Shepperd's method)."""
+    R = np.asarray(R, np.float64)
+    t = np.trace(R)
+    if t > 0:
+        s = math.sqrt(t + 1.0) * 2
+        q = [0.25 * s, (R[2, 1] - R[1, 2]) / s, (R[0, 2] - R[2, 0]) / s, (R[1, 0] - R[0, 1]) / s]
+    else:
+        i = int(np.argmax(np.diag(R)))
+        j, k = (i + 1) % 3, (i + 2) % 3
+        s = math.sqrt(1.0 + R[i, i] - R[j, j] - R[k, k]) * 2
+        q = [0.0] * 4
+        q[0] = (R[k, j] - R[j, k]) / s
+        q[1 + i] = 0.25 * s
+        q[1 + j] = (R[j, i] + R[i, j]) / s
+        q[1 + k] = (R[k, i] + R[i, k]) / s
+    q = np.array(q)
+    q /= np.linalg.norm(q)
+    return q if q[0] >= 0 else -q
+
+
+def quat_to_rot(q) -> np.ndarray:
+    w, x, y, z = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                     [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                     [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+
+
+def ikfom_cov() -> np.ndarray:
+    """Initial P of the IKFoM state (FAST-LIO style diagonal: pose 1e-3, extrinsic 1e-5,
+    vel 1e-3, bg 1e-4, ba 1e-3, gravity 1e-5)."""
+    d = np.full(IKN, 1e-3)
+    d[6:12] = 1e-5
+    d[15:18] = 1e-4
+    d[21:23] = 1e-5
+    return np.diag(d)
+
+
+def make_ikfom_state(scan_id: int = 0, rot_deg: float = 1.0, trans_m: float = 0.1) -> dict:
+    """state_ikfom of the same perturbed pose as make_state (identity extrinsic rotation,
+    offset_T = T_LI, gravity on the S2 of length 9.809)."""
+    st = make_state(scan_id, rot_deg, trans_m)
+    return {"pos": st["pos"], "rot": rot_to_quat(st["rot"]), "offset_R": np.array([1.0, 0.0, 0.0, 0.0]),
+            "offset_T": T_LI.copy(), "vel": np.zeros(3), "bg": np.zeros(3), "ba": np.zeros(3),
+            "grav": np.array([0.0, 0.0, -S2_LEN]), "cov": ikfom_cov()}
+
+
 _CACHE_DIR = os.environ.get("LIVO_SYNTH_CACHE", "/tmp/livo_synth_cache")
 
 

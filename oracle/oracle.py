@@ -31,6 +31,40 @@ class OrcIterStats(C.Structure):
                 ("solution", (C.c_double * 18) * MAX_EVALS), ("res_mean", C.c_double * MAX_EVALS)]
 
 
+IKN = 23  # state_ikfom degrees of freedom (use-ikfom.hpp:12-21)
+
+
+class OrcIkfomState(C.Structure):
+    """state_ikfom: quaternions (w, x, y, z) for rot / offset_R, S2 gravity as a 3-vector."""
+    _fields_ = [("pos", C.c_double * 3), ("rot", C.c_double * 4), ("offset_R", C.c_double * 4),
+                ("offset_T", C.c_double * 3), ("vel", C.c_double * 3), ("bg", C.c_double * 3),
+                ("ba", C.c_double * 3), ("grav", C.c_double * 3), ("cov", C.c_double * (IKN * IKN))]
+
+
+class OrcIkfomStats(C.Structure):
+    _fields_ = [("iterations", C.c_int32), ("knn_passes", C.c_int32), ("converged", C.c_int32),
+                ("t", C.c_int32), ("effct_feat_num", C.c_int64 * MAX_EVALS),
+                ("dx", (C.c_double * IKN) * MAX_EVALS), ("res_mean", C.c_double * MAX_EVALS)]
+
+
+IK_FIELDS = (("pos", 3), ("rot", 4), ("offset_R", 4), ("offset_T", 3), ("vel", 3), ("bg", 3), ("ba", 3),
+             ("grav", 3))
+
+
+def ikfom_to_c(st: dict) -> OrcIkfomState:
+    s = OrcIkfomState()
+    for k, n in IK_FIELDS:
+        getattr(s, k)[:] = np.asarray(st[k], np.float64).reshape(n).tolist()
+    s.cov[:] = np.asarray(st["cov"], np.float64).reshape(IKN * IKN).tolist()
+    return s
+
+
+def ikfom_from_c(s) -> dict:
+    out = {k: np.array(getattr(s, k)[:]) for k, _ in IK_FIELDS}
+    out["cov"] = np.array(s.cov[:]).reshape(IKN, IKN)
+    return out
+
+
 def build(force: bool = False) -> str:
     src = os.path.join(_HERE, "livo_oracle.cpp")
     if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
@@ -60,6 +94,9 @@ def lib():
                                   P, P, C.c_int]
         L.orc_iekf_update.argtypes = [P, P, C.c_int64, P, P, C.c_double, C.c_int, C.POINTER(OrcState),
                                       C.POINTER(OrcState), C.POINTER(OrcIterStats), P, C.c_int]
+        L.orc_ikfom_update.argtypes = [P, P, C.c_int64, C.c_double, C.c_int, C.POINTER(OrcIkfomState),
+                                       C.POINTER(OrcIkfomStats), P, C.c_int]
+        L.orc_ikfom_mtk.argtypes = [C.c_int, P, P, P]
         del fp
         _lib = L
     return _lib
@@ -154,6 +191,41 @@ class Tree:
             "visits": int(vt[0]),
         }
         return state_from_c(from_state), stats
+
+
+def _ikfom_update(self, body, state: dict, max_iter: int = 4, lpc: float = 0.001, threads: int = 1):
+    """IKFoM scan update (esekfom.hpp:1619-1928 with origin_laserMapping.cpp:916-1048)."""
+    cs = ikfom_to_c(state)
+    st = OrcIkfomStats()
+    vt = np.zeros(1, np.int64)
+    body = np.ascontiguousarray(body, np.float32)
+    rc = lib().orc_ikfom_update(self.h, _p(body), body.shape[0], lpc, max_iter, C.byref(cs), C.byref(st), _p(vt),
+                                threads)
+    assert rc == 0
+    ne = st.iterations
+    stats = {"iterations": ne, "knn_passes": st.knn_passes, "converged": st.converged, "t": st.t,
+             "effct_feat_num": [st.effct_feat_num[i] for i in range(ne)],
+             "dx": np.array([list(st.dx[i]) for i in range(ne)]),
+             "res_mean": [st.res_mean[i] for i in range(ne)], "visits": int(vt[0])}
+    return ikfom_from_c(cs), stats
+
+
+Tree.ikfom_update = _ikfom_update
+
+
+def mtk(op: int, a, b):
+    """MTK pieces: 0 S2 boxplus (vec3, delta2), 1 S2 boxminus (a3, b3), 2 A_matrix (v3),
+    3 state boxplus/boxminus round trip (ikfom state dict, dx23)."""
+    if op == 3:
+        sa = ikfom_to_c(a)
+        a_buf = np.frombuffer(bytes(sa), np.float64).copy()
+        out = np.zeros(IKN)
+    else:
+        a_buf = np.ascontiguousarray(a, np.float64)
+        out = np.zeros({0: 3, 1: 2, 2: 9}[op])
+    b_buf = np.ascontiguousarray(b, np.float64)
+    assert lib().orc_ikfom_mtk(op, _p(a_buf), _p(b_buf), _p(out)) == 0
+    return out
 
 
 def knn_brute(xyz, q, k=5, threads=8):

@@ -8,6 +8,7 @@ the restatement is pinned against independent implementations instead:
   * numpy float64 for the Jacobian / normal equations and the IEKF algebra;
 and against its own committed golden fixtures (tests/golden/) for regressions.
 """
+import math
 import os
 
 import numpy as np
@@ -217,3 +218,127 @@ def test_oracle_matches_golden(built):
     assert stats["iterations"] == int(g["iterations"])
     assert np.array_equal(stats["solution"], g["solution"])
     assert np.array_equal(out["rot"], g["out_rot"]) and np.array_equal(out["pos"], g["out_pos"])
+
+
+# ---------------------------------------------------------------- IKFoM ----
+# The IKFoM formulation: MTK manifold pieces, then the
+# first update checked against an independent numpy restatement.
+
+def _hat(v):
+    return np.array([[0, -v[2], v[1]], [v[2], 0, -v[0]], [-v[1], v[0], 0]])
+
+
+def _so3_exp(v):
+    th = np.linalg.norm(v)
+    if th < 1e-15:
+        return np.eye(3)
+    K = _hat(v / th)
+    return np.eye(3) + math.sin(th) * K + (1 - math.cos(th)) * K @ K
+
+
+def test_mtk_A_matrix_is_left_jacobian():
+    import oracle
+    rng = np.random.default_rng(3)
+    for _ in range(5):
+        v = rng.normal(size=3) * 0.7
+        A = oracle.mtk(2, v, [0.0]).reshape(3, 3)
+        d = rng.normal(size=3) * 1e-6
+        lhs = _so3_exp(v + d) @ _so3_exp(v).T          # Exp(v + d) Exp(v)^-1 = Exp(A d)
+        w = np.array([lhs[2, 1] - lhs[1, 2], lhs[0, 2] - lhs[2, 0], lhs[1, 0] - lhs[0, 1]]) / 2
+        assert np.allclose(w, A @ d, rtol=0, atol=1e-11)
+    assert np.allclose(oracle.mtk(2, [0.0, 0.0, 0.0], [0.0]).reshape(3, 3), np.eye(3))
+
+
+def test_mtk_s2_roundtrip_and_length():
+    import oracle
+    from livo_amd import synth
+    rng = np.random.default_rng(4)
+    for _ in range(20):
+        g = rng.normal(size=3)
+        g = g / np.linalg.norm(g) * synth.S2_LEN
+        d = rng.normal(size=2) * 0.3
+        g2 = oracle.mtk(0, g, d)
+        assert abs(np.linalg.norm(g2) - synth.S2_LEN) < 1e-12
+        assert np.allclose(oracle.mtk(1, g2, g), d, rtol=0, atol=1e-12)
+
+
+def test_ikfom_state_boxplus_boxminus_roundtrip():
+    import oracle
+    from livo_amd import synth
+    st = synth.make_ikfom_state(2)
+    dx = np.random.default_rng(5).normal(size=23) * 0.05
+    assert np.allclose(oracle.mtk(3, st, dx), dx, rtol=0, atol=1e-12)
+
+
+def _ikfom_dx0_numpy(tree, map_xyz, body, st, lpc=0.001):
+    """First-evaluation dx of the IKFoM update in numpy (x = x_propagated: dx_new = 0,
+    dx = P_inv[:, :12] H^T h, information form), from the oracle's k-NN and plane fit."""
+    import oracle
+    from livo_amd import synth
+    R = synth.quat_to_rot(st["rot"])
+    pI = body.astype(np.float64) + st["offset_T"]
+    world = (pI @ R.T + st["pos"]).astype(np.float32)
+    idx, d, _ = tree.knn(world)
+    rows, hs = [], []
+    for i in range(len(body)):
+        if d[i, 4] > 5.0:
+            continue
+        ok, pa = oracle.esti_plane(map_xyz[idx[i]])
+        if not ok:
+            continue
+        pd2 = np.float32(pa[0] * world[i, 0] + pa[1] * world[i, 1] + pa[2] * world[i, 2] + pa[3])
+        s = 1 - 0.9 * abs(float(pd2)) / math.sqrt(np.linalg.norm(body[i].astype(np.float64)))
+        if not (np.float32(s) > 0.9 and abs(float(pd2)) <= 2.0):
+            continue
+        n = pa[:3].astype(np.float64)
+        C = R.T @ n
+        A = _hat(pI[i]) @ C
+        B = _hat(body[i].astype(np.float64)) @ C   # offset_R = identity
+        rows.append(np.concatenate([n, A, B, C]))
+        hs.append(-float(pd2))
+    H, h = np.array(rows).reshape(-1, 12), np.array(hs)
+    Pt = np.linalg.inv(st["cov"] / lpc)
+    Pt[:12, :12] += H.T @ H
+    Pinv = np.linalg.inv(Pt)
+    return Pinv[:, :12] @ (H.T @ h), len(rows)
+
+
+def test_ikfom_first_update_matches_numpy(tree100k, map100k):
+    from livo_amd import synth
+    body, _, _ = synth.make_scan(4000, 7)
+    st = synth.make_ikfom_state(7)
+    _, stats = tree100k.ikfom_update(body, st, max_iter=0)
+    dx, m = _ikfom_dx0_numpy(tree100k, map100k, body, st)
+    assert stats["effct_feat_num"][0] == m
+    assert np.linalg.norm(stats["dx"][0] - dx) <= 1e-8 * np.linalg.norm(dx)
+
+
+def test_ikfom_update_reduces_pose_error(tree100k):
+    from livo_amd import synth
+    body, _, _ = synth.make_scan(8000, 9)
+    st0 = synth.make_ikfom_state(9)
+    Rt, pt, _ = synth.true_pose(9)
+    st, stats = tree100k.ikfom_update(body, st0, max_iter=4)
+    assert 1 <= stats["iterations"] <= 5 and stats["knn_passes"] >= 1
+    err0 = np.linalg.norm(st0["pos"] - pt)
+    err1 = np.linalg.norm(st["pos"] - pt)
+    assert err1 < 0.2 * err0
+    Rerr = synth.quat_to_rot(st["rot"]).T @ Rt
+    assert math.degrees(math.acos(min(1.0, (np.trace(Rerr) - 1) / 2))) < 0.2
+    assert abs(np.linalg.norm(st["grav"]) - synth.S2_LEN) < 1e-9
+    assert np.all(np.linalg.eigvalsh((st["cov"] + st["cov"].T) / 2) > 0)
+    assert np.all(np.diag(st["cov"])[:6] < np.diag(st0["cov"])[:6])
+
+
+def test_ikfom_few_points_measurement_space_branch(tree100k, map100k):
+    """Fewer than 23 effective points: the reference switches to the
+    measurement-space gain (esekfom.hpp:1701-1736), the same update as the
+    information form up to rounding."""
+    from livo_amd import synth
+    body, _, _ = synth.make_scan(4000, 3)
+    st0 = synth.make_ikfom_state(3)
+    few = body[:12]
+    _, stats = tree100k.ikfom_update(few, st0, max_iter=0)
+    dx, m = _ikfom_dx0_numpy(tree100k, map100k, few, st0)
+    assert 0 < m < 23 and stats["effct_feat_num"][0] == m
+    assert np.linalg.norm(stats["dx"][0] - dx) <= 1e-8 * np.linalg.norm(dx)
