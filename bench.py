@@ -222,6 +222,35 @@ def main():
             "map_build_s": round(map_build_s, 3),
         }
 
+    # ---- the IKFoM formulation on the same scans: throughput
+    # of livo_ikfom_update_batch (extra steps, not part of `value`)
+    ik_init = (livo_amd.IkfomState * a.batch)(*[livo_amd.ikfom_to_c(synth.make_ikfom_state(s)) for s in scan_ids])
+    ik_work = (livo_amd.IkfomState * a.batch)()
+    ik_bytes = C.sizeof(ik_init)
+
+    def ik_step():
+        C.memmove(ik_work, ik_init, ik_bytes)
+        return ctx.ikfom_update_batch(sids, ik_work, raw=True)[1]
+
+    for _ in range(2):
+        ik_step()
+    ik_steps = max(5, a.steps // 2)
+    sync()
+    t = time.perf_counter()
+    ik_evals = 0
+    for _ in range(ik_steps):
+        ik_evals += sum(s.iterations for s in ik_step())
+    sync()
+    ik_elapsed = farm.allreduce_max(time.perf_counter() - t, coll_dev)
+    ik_total = farm.allreduce_counters(farm.Counters(scans=ik_steps * a.batch, evals=ik_evals), coll_dev)
+    ik_first = livo_amd.ikfom_stats_from_c(ik_step()[0])
+    if rank == 0:
+        result["ikfom"] = {"updates_per_s": round(ik_total.scans / ik_elapsed, 3),
+                           "ms_per_step": round(ik_elapsed / ik_steps * 1e3, 4),
+                           "evals_per_scan": round(ik_total.evals / max(ik_total.scans, 1), 3),
+                           "note": "livo_ikfom_update_batch (state_ikfom, esekfom.hpp:1619-1928) on the same "
+                                   f"{a.batch} scans per GPU, {ik_steps} steps after the headline run"}
+
     # ---- CPU baseline: the oracle (CPU restatement), 1 thread, bounded sample; + parity of scan 0
     if rank == 0 and a.cpu_seconds > 0:
         import oracle
@@ -252,6 +281,14 @@ def main():
         result["parity_scan0"] = {"iterations_equal": gs["iterations"] == rs["iterations"],
                                   "effct_equal": gs["effct_feat_num"] == rs["effct_feat_num"],
                                   "max_rel_state_delta": float(f"{rel:.3e}")}
+        # the IKFoM update of scan 0 against the oracle's
+        ir, irs = tree.ikfom_update(scans[0], synth.make_ikfom_state(scan_ids[0]), max_iter=a.max_iter, threads=8)
+        iscale = max(np.linalg.norm(d) for d in irs["dx"])  # relative to the scan's largest step
+        irel = max(np.linalg.norm(ik_first["dx"][e] - irs["dx"][e]) / iscale
+                   for e in range(min(ik_first["iterations"], irs["iterations"])))
+        result["ikfom"]["parity_scan0"] = {"iterations_equal": ik_first["iterations"] == irs["iterations"],
+                                           "effct_equal": ik_first["effct_feat_num"] == irs["effct_feat_num"],
+                                           "max_dx_error_rel_to_largest_step": float(f"{irel:.3e}")}
     if rank == 0:
         print(json.dumps(result), flush=True)
     ctx.close()

@@ -30,7 +30,7 @@ struct ScanBuf {
     float* pts = nullptr;  // n x 4
     NNRec* nn = nullptr;   // neighbour records (Nearest_Points cache)
     std::vector<int32_t> perm;  // stored (Morton) position -> caller's point index
-    double* partial = nullptr;  // nblk x kRedCols
+    double* partial = nullptr;  // nblk x kIkCols (the A-path uses kRedCols of each)
     bool searched = false;      // a search has filled the neighbour cache
 };
 
@@ -210,6 +210,7 @@ static HsParams make_hs_params(livo_ctx* c) {
     std::memcpy(hp.R_LI, c->params.R_LI, sizeof(hp.R_LI));
     std::memcpy(hp.t_LI, c->params.t_LI, sizeof(hp.t_LI));
     hp.inv_r = 1.0 / c->params.laser_point_cov;
+    hp.lpc = c->params.laser_point_cov;
     hp.max_res = c->params.max_residual;
     hp.plane_thr = c->params.plane_threshold;
     hp.max_sqd = c->params.max_nn_sqdist;
@@ -224,6 +225,18 @@ static void fill_job(HsJob& j, ScanBuf& s, IekfSlot* slot) {
     j.slot = slot;
     j.n = (int32_t)s.n;
     j.nblk = s.nblk;
+}
+
+// IKFoM: x_ = x_propagated = the input state (its cov is P_propagated); the
+// first h_dyn_share searches (dyn_share.converge = true, esekfom.hpp:1623).
+static void init_slot_ik(IekfSlot& s, const livo_ikfom_state& st, int max_iter) {
+    std::memset(&s, 0, sizeof(IekfSlot));
+    s.model = kModelIkfom;
+    s.ik.x = st;
+    s.ik.xp = st;
+    s.ctrl.search_en = 1;
+    s.ctrl.iter_count = -1;
+    s.ctrl.max_iter = max_iter;
 }
 
 static void init_slot(IekfSlot& s, const livo_state& st, const livo_state& prior, int max_iter) {
@@ -479,7 +492,7 @@ int livo_scan_upload(livo_ctx* c, const float* xyz, int64_t N, int64_t stride_by
     int rc = 0;
     rc |= dev_alloc(&s.pts, (size_t)N * 4);
     rc |= dev_alloc(&s.nn, (size_t)N);
-    rc |= dev_alloc(&s.partial, (size_t)std::max(s.nblk, 1) * kRedCols);
+    rc |= dev_alloc(&s.partial, (size_t)std::max(s.nblk, 1) * kIkCols);  // IKFoM partials are the wider
     if (rc) {
         dev_free(s.pts); dev_free(s.nn);
         dev_free(s.partial);
@@ -624,9 +637,12 @@ int livo_h_share(livo_ctx* c, int32_t id, const livo_state* state, int search_en
     return LIVO_OK;
 }
 
-int livo_iekf_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_state* states, const livo_state* priors,
-                           livo_iter_stats* stats) {
-    if (!c || n < 0 || (n > 0 && (!ids || !states))) return LIVO_E_INVALID;
+// The batched iterated update of both formulations: the LaserMapping IEKF
+// (states/priors/stats, model 0) or the IKFoM update (ik_states/ik_stats, model 1).
+static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, livo_state* states,
+                        const livo_state* priors, livo_iter_stats* stats, livo_ikfom_state* ik_states,
+                        livo_ikfom_stats* ik_stats) {
+    if (!c || n < 0 || (n > 0 && (!ids || (model == kModelIkfom ? !ik_states : !states)))) return LIVO_E_INVALID;
     if (n == 0) return LIVO_OK;
     if (!c->has_map) return LIVO_E_NOMAP;
     for (int32_t b = 0; b < n; b++)
@@ -638,7 +654,11 @@ int livo_iekf_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_stat
     int64_t total_n = 0;
     for (int32_t b = 0; b < n; b++) {
         ScanBuf* s = get_scan(c, ids[b]);
-        init_slot(c->h_slots[b], states[b], priors ? priors[b] : states[b], max_iter);
+        if (model == kModelIkfom) {
+            init_slot_ik(c->h_slots[b], ik_states[b], max_iter);
+        } else {
+            init_slot(c->h_slots[b], states[b], priors ? priors[b] : states[b], max_iter);
+        }
         fill_job(c->h_jobs[b], *s, c->d_slots + b);
         total_n += s->n;
     }
@@ -705,7 +725,8 @@ int livo_iekf_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_stat
             rc = launch_knn_leaf(kp[gi], g[gi].count, g[gi].max_n, e > 0, st);
             if (rc) return rc;
             if ((prof && e == 0) || full) HIP_TRY(hipEventRecord(c->ev[gi][3 * e + 1], st));
-            rc = launch_hshare(hp[gi], g[gi].count, g[gi].max_nblk, e == 0, st);
+            rc = model == kModelIkfom ? launch_hshare_ik(hp[gi], g[gi].count, g[gi].max_nblk, e == 0, st)
+                                      : launch_hshare(hp[gi], g[gi].count, g[gi].max_nblk, e == 0, st);
             if (rc) return rc;
         }
     }
@@ -724,8 +745,13 @@ int livo_iekf_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_stat
     HIP_TRY(hipStreamSynchronize(c->stream));
     for (int32_t b = 0; b < n; b++) {
         const IekfSlot& s = c->h_slots[b];
-        states[b] = s.state;
-        if (stats) stats[b] = s.stats;
+        if (model == kModelIkfom) {
+            ik_states[b] = s.ik.x;
+            if (ik_stats) ik_stats[b] = s.ik.stats;
+        } else {
+            states[b] = s.state;
+            if (stats) stats[b] = s.stats;
+        }
         c->scans[ids[b]].searched = true;
     }
     if (prof) {
@@ -751,7 +777,8 @@ int livo_iekf_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_stat
         for (int32_t b = 0; b < n; b++) {
             t.knn_visits += (int64_t)c->h_slots[b].visits[0];
             t.knn_queries += c->scans[ids[b]].n;
-            t.effct_points += c->h_slots[b].stats.effct_feat_num[0];
+            t.effct_points += model == kModelIkfom ? c->h_slots[b].ik.stats.effct_feat_num[0]
+                                                   : c->h_slots[b].stats.effct_feat_num[0];
         }
         t.knn_replays = (int64_t)replays;
         c->last = t;
@@ -759,9 +786,24 @@ int livo_iekf_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_stat
     return LIVO_OK;
 }
 
+int livo_iekf_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_state* states, const livo_state* priors,
+                           livo_iter_stats* stats) {
+    return batch_update(c, n, ids, kModelLaserMapping, states, priors, stats, nullptr, nullptr);
+}
+
 int livo_iekf_update(livo_ctx* c, int32_t id, livo_state* state, const livo_state* prior, livo_iter_stats* stats) {
     if (!state) return LIVO_E_INVALID;
     return livo_iekf_update_batch(c, 1, &id, state, prior, stats);
+}
+
+int livo_ikfom_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_ikfom_state* states,
+                            livo_ikfom_stats* stats) {
+    return batch_update(c, n, ids, kModelIkfom, nullptr, nullptr, nullptr, states, stats);
+}
+
+int livo_ikfom_update(livo_ctx* c, int32_t id, livo_ikfom_state* state, livo_ikfom_stats* stats) {
+    if (!state) return LIVO_E_INVALID;
+    return livo_ikfom_update_batch(c, 1, &id, state, stats);
 }
 
 int livo_sync(livo_ctx* c) {

@@ -93,6 +93,22 @@ struct IekfCtrl {
     int32_t last_search;  // nearest_search_en used by the last evaluation
 };
 
+constexpr int kIkDim = LIVO_IKFOM_DOF;  // 23
+constexpr int kIkCols = 96;             // doubles per IKFoM block partial (92 used)
+constexpr int kIkUsed = 92;             // 78 HTH upper-tri + 12 HTh + residual sum + count
+
+// IKFoM update state (esekfom.hpp:1619-1928): x_, x_propagated (its cov is
+// P_propagated), the converged counter t.
+struct alignas(16) IkBlock {
+    livo_ikfom_state x;
+    livo_ikfom_state xp;
+    livo_ikfom_stats stats;
+    int32_t t;
+    int32_t pad[3];
+};
+
+enum SlotModel { kModelLaserMapping = 0, kModelIkfom = 1 };
+
 // Everything one scan update needs on the device (one per batch entry).
 struct alignas(16) IekfSlot {
     livo_state state;     // in/out
@@ -105,7 +121,9 @@ struct alignas(16) IekfSlot {
     unsigned long long visits[LIVO_MAX_EVALS];  // k-NN nodes visited per evaluation
     int32_t eval_search[LIVO_MAX_EVALS];
     unsigned hs_ticket;         // k_hshare blocks done in the current pass (the last one reduces)
-    unsigned pad_[3];
+    int32_t model;              // SlotModel
+    unsigned pad_[2];
+    IkBlock ik;                 // model == kModelIkfom
 };
 
 // Nearest_Points[i] + pointSearchSqDis for one point: 128 B, written by the
@@ -146,6 +164,7 @@ struct HsParams {
     float plane_thr;        // 0.1f
     float max_sqd;          // 5.0f
     int32_t force;          // -1: follow ctrl; 0: no search; 1: search
+    double lpc;             // LASER_POINT_COV (the IKFoM gain divides P by it)
     int32_t solve;          // 1: the last block of a scan also runs its solve (IEKF loop)
     unsigned* replay_count; // zeroed once per launch (the group's k-NN replay count), may be null
 };
@@ -195,6 +214,8 @@ int launch_knn_pass(const KnnParams& p, int n_jobs, int64_t max_n, void* stream)
 // point's previous neighbours.  Both are followed by the exact tie replay.
 int launch_knn_leaf(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, void* stream);
 int launch_hshare(const HsParams& p, int n_jobs, int max_nblk, bool first, void* stream);
+// IKFoM plane pass (12-wide rows) with the manifold update in each scan's last block.
+int launch_hshare_ik(const HsParams& p, int n_jobs, int max_nblk, bool first, void* stream);
 int launch_solve(const SolveParams& p, int n_jobs, void* stream);
 
 }  // namespace livo

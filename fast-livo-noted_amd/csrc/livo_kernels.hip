@@ -32,6 +32,230 @@
 
 namespace livo {
 
+// ========================================================= IKFoM path =====
+// The IKFoM formulation: state_ikfom (use-ikfom.hpp:12-21),
+// the legacy h-model (origin_laserMapping.cpp:916-1048) and
+// esekf::update_iterated_dyn_share_modified (esekfom.hpp:1619-1928) with the
+// MTK pieces it uses.  Same operation order as oracle/livo_oracle.cpp.
+constexpr double kMtkTol = 1e-11;            // MTK::tolerance<double>() (mtkmath.hpp:122)
+constexpr double kS2Len = 98090.0 / 10000.0;  // S2<double, 98090, 10000, 1> (use-ikfom.hpp:9)
+
+struct Qd {
+    double w, x, y, z;
+};
+__device__ __forceinline__ Qd qd_mul(const Qd& a, const Qd& b) {  // Eigen generic quat_product
+    return Qd{a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z, a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y,
+              a.w * b.y + a.y * b.w + a.z * b.x - a.x * b.z, a.w * b.z + a.z * b.w + a.x * b.y - a.y * b.x};
+}
+__device__ __forceinline__ Qd qd_conj(const Qd& q) { return Qd{q.w, -q.x, -q.y, -q.z}; }
+__device__ __forceinline__ Qd qd_load(const double* a) { return Qd{a[0], a[1], a[2], a[3]}; }
+__device__ __forceinline__ void qd_store(const Qd& q, double* a) { a[0] = q.w; a[1] = q.x; a[2] = q.y; a[3] = q.z; }
+__device__ __forceinline__ void cross3d(const double* a, const double* b, double* o) {
+    o[0] = a[1] * b[2] - a[2] * b[1];
+    o[1] = a[2] * b[0] - a[0] * b[2];
+    o[2] = a[0] * b[1] - a[1] * b[0];
+}
+// Eigen::QuaternionBase::_transformVector
+__device__ __forceinline__ void qd_rot(const Qd& q, const double* v, double* o) {
+    const double qv[3] = {q.x, q.y, q.z};
+    double uv[3], c[3];
+    cross3d(qv, v, uv);
+    _Pragma("unroll") for (int i = 0; i < 3; i++) uv[i] = uv[i] + uv[i];
+    cross3d(qv, uv, c);
+    _Pragma("unroll") for (int i = 0; i < 3; i++) o[i] = (v[i] + q.w * uv[i]) + c[i];
+}
+__device__ __forceinline__ void qd_mat(const Qd& q, double* R) {  // toRotationMatrix
+    const double tx = 2 * q.x, ty = 2 * q.y, tz = 2 * q.z;
+    const double twx = tx * q.w, twy = ty * q.w, twz = tz * q.w;
+    const double txx = tx * q.x, txy = ty * q.x, txz = tz * q.x;
+    const double tyy = ty * q.y, tyz = tz * q.y, tzz = tz * q.z;
+    R[0] = 1 - (tyy + tzz); R[1] = txy - twz;       R[2] = txz + twy;
+    R[3] = txy + twz;       R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
+}
+__device__ __forceinline__ void hat3d(const double* v, double* H) {
+    H[0] = 0; H[1] = -v[2]; H[2] = v[1];
+    H[3] = v[2]; H[4] = 0; H[5] = -v[0];
+    H[6] = -v[1]; H[7] = v[0]; H[8] = 0;
+}
+__device__ __forceinline__ void mat3d_mul(const double* A, const double* B, double* C) {
+    _Pragma("unroll") for (int i = 0; i < 3; i++)
+        _Pragma("unroll") for (int j = 0; j < 3; j++)
+            C[i * 3 + j] = (A[i * 3 + 0] * B[0 * 3 + j] + A[i * 3 + 1] * B[1 * 3 + j]) + A[i * 3 + 2] * B[2 * 3 + j];
+}
+__device__ __forceinline__ void mat3d_vec(const double* M, const double* v, double* o) {
+    _Pragma("unroll") for (int r = 0; r < 3; r++) o[r] = (M[r * 3] * v[0] + M[r * 3 + 1] * v[1]) + M[r * 3 + 2] * v[2];
+}
+// MTK::cos_sinc_sqrt (mtkmath.hpp:142-171)
+__device__ __forceinline__ void cos_sinc_sqrt_d(double x2, double& c, double& sc) {
+    const double taylor_0 = 2.220446049250313e-16, taylor_2 = sqrt(taylor_0), taylor_n = sqrt(taylor_2);
+    if (x2 >= taylor_n) {
+        const double x = sqrt(x2);
+        c = cos(x);
+        sc = sin(x) / x;
+        return;
+    }
+    const double inv[7] = {1 / 3., 1 / 4., 1 / 5., 1 / 6., 1 / 7., 1 / 8., 1 / 9.};
+    double cosi = 1., sinc = 1;
+    double term = -1 / 2. * x2;
+    _Pragma("unroll") for (int i = 0; i < 3; ++i) {
+        cosi += term;
+        term *= inv[2 * i];
+        sinc += term;
+        term *= -inv[2 * i + 1] * x2;
+    }
+    c = cosi;
+    sc = sinc;
+}
+__device__ __forceinline__ Qd mtk_exp_d(const double* v, double scale) {  // MTK::exp -> quaternion
+    const double norm2 = (v[0] * v[0] + v[1] * v[1]) + v[2] * v[2];
+    double c, sc;
+    cos_sinc_sqrt_d(scale * scale * norm2, c, sc);
+    const double mult = sc * scale;
+    return Qd{c, mult * v[0], mult * v[1], mult * v[2]};
+}
+__device__ __forceinline__ void so3_log_qd(const Qd& q, double* o) {  // SO3::log (periodic)
+    double nv = sqrt((q.x * q.x + q.y * q.y) + q.z * q.z);
+    if (nv < kMtkTol) nv = kMtkTol;
+    const double s = 2.0 / nv * atan(nv / q.w);
+    o[0] = s * q.x;
+    o[1] = s * q.y;
+    o[2] = s * q.z;
+}
+__device__ __forceinline__ void A_matrix_d(const double* v, double* A) {  // MTK::A_matrix
+    const double sq = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+    const double norm = sqrt(sq);
+    _Pragma("unroll") for (int i = 0; i < 9; i++) A[i] = (i % 4 == 0) ? 1.0 : 0.0;
+    if (norm < kMtkTol) return;
+    double H[9], HH[9];
+    hat3d(v, H);
+    mat3d_mul(H, H, HH);
+    const double a = (1 - cos(norm)) / sq, b = (1 - sin(norm) / norm) / sq;
+    _Pragma("unroll") for (int i = 0; i < 9; i++) A[i] = (A[i] + a * H[i]) + b * HH[i];
+}
+__device__ __forceinline__ void s2_Bx_d(const double* vec, double* B) {  // S2_Bx, S2_typ = 1
+    const double L = kS2Len;
+    if (vec[0] + L > kMtkTol) {
+        B[0] = -vec[1];
+        B[1] = -vec[2];
+        B[2] = L - vec[1] * vec[1] / (L + vec[0]);
+        B[3] = -vec[2] * vec[1] / (L + vec[0]);
+        B[4] = -vec[2] * vec[1] / (L + vec[0]);
+        B[5] = L - vec[2] * vec[2] / (L + vec[0]);
+        _Pragma("unroll") for (int i = 0; i < 6; i++) B[i] /= L;
+    } else {
+        _Pragma("unroll") for (int i = 0; i < 6; i++) B[i] = 0.0;
+        B[3] = -1;
+        B[4] = 1;
+    }
+}
+__device__ __forceinline__ void s2_boxplus_d(double* vec, const double* delta) {
+    double B[6];
+    s2_Bx_d(vec, B);
+    const double Bu[3] = {B[0] * delta[0] + B[1] * delta[1], B[2] * delta[0] + B[3] * delta[1],
+                          B[4] * delta[0] + B[5] * delta[1]};
+    const Qd r = mtk_exp_d(Bu, 0.5);
+    double R[9], o[3];
+    qd_mat(r, R);
+    mat3d_vec(R, vec, o);
+    vec[0] = o[0];
+    vec[1] = o[1];
+    vec[2] = o[2];
+}
+__device__ __forceinline__ void s2_boxminus_d(const double* vec, const double* other, double* res) {
+    double H[9], hv[3];
+    hat3d(vec, H);
+    mat3d_vec(H, other, hv);
+    const double v_sin = sqrt((hv[0] * hv[0] + hv[1] * hv[1]) + hv[2] * hv[2]);
+    const double v_cos = (vec[0] * other[0] + vec[1] * other[1]) + vec[2] * other[2];
+    const double theta = atan2(v_sin, v_cos);
+    if (v_sin < kMtkTol) {
+        res[0] = fabs(theta) > kMtkTol ? 3.1415926 : 0.0;
+        res[1] = 0.0;
+        return;
+    }
+    double B[6], Ho[9], t[3];
+    s2_Bx_d(other, B);
+    hat3d(other, Ho);
+    mat3d_vec(Ho, vec, t);
+    const double f = theta / v_sin;
+    _Pragma("unroll") for (int r = 0; r < 2; r++) res[r] = f * ((B[0 * 2 + r] * t[0] + B[1 * 2 + r] * t[1]) + B[2 * 2 + r] * t[2]);
+}
+// J = S2_Nx_yy(x.grav) * S2_Mx(xp.grav, seg)  (2x2; exp_delta in S2_Mx is the identity)
+__device__ __forceinline__ void s2_J_d(const double* gx, const double* gp, const double* seg, double* J) {
+    double B[6], H[9], N[6], M[6];
+    s2_Bx_d(gx, B);
+    hat3d(gx, H);
+    const double f = 1 / kS2Len / kS2Len;
+    _Pragma("unroll") for (int r = 0; r < 2; r++)
+        _Pragma("unroll") for (int c = 0; c < 3; c++)
+            N[r * 3 + c] = f * ((B[0 * 2 + r] * H[0 * 3 + c] + B[1 * 2 + r] * H[1 * 3 + c]) + B[2 * 2 + r] * H[2 * 3 + c]);
+    s2_Bx_d(gp, B);
+    hat3d(gp, H);
+    const double dn = sqrt(seg[0] * seg[0] + seg[1] * seg[1]);
+    if (dn < kMtkTol) {
+        _Pragma("unroll") for (int r = 0; r < 3; r++)
+            _Pragma("unroll") for (int c = 0; c < 2; c++)
+                M[r * 2 + c] = -((H[r * 3 + 0] * B[0 * 2 + c] + H[r * 3 + 1] * B[1 * 2 + c]) + H[r * 3 + 2] * B[2 * 2 + c]);
+    } else {
+        const double Bu[3] = {B[0] * seg[0] + B[1] * seg[1], B[2] * seg[0] + B[3] * seg[1], B[4] * seg[0] + B[5] * seg[1]};
+        double A[9], AT[9], HA[9];
+        A_matrix_d(Bu, A);
+        _Pragma("unroll") for (int r = 0; r < 3; r++)
+            _Pragma("unroll") for (int c = 0; c < 3; c++) AT[r * 3 + c] = A[c * 3 + r];
+        mat3d_mul(H, AT, HA);
+        _Pragma("unroll") for (int r = 0; r < 3; r++)
+            _Pragma("unroll") for (int c = 0; c < 2; c++)
+                M[r * 2 + c] = -((HA[r * 3 + 0] * B[0 * 2 + c] + HA[r * 3 + 1] * B[1 * 2 + c]) + HA[r * 3 + 2] * B[2 * 2 + c]);
+    }
+    _Pragma("unroll") for (int r = 0; r < 2; r++)
+        _Pragma("unroll") for (int c = 0; c < 2; c++)
+            J[r * 2 + c] = (N[r * 3 + 0] * M[0 * 2 + c] + N[r * 3 + 1] * M[1 * 2 + c]) + N[r * 3 + 2] * M[2 * 2 + c];
+}
+__device__ __forceinline__ void so3_J_d(const double* seg, double* J) {  // A_matrix(seg)^T
+    double A[9];
+    A_matrix_d(seg, A);
+    _Pragma("unroll") for (int r = 0; r < 3; r++)
+        _Pragma("unroll") for (int c = 0; c < 3; c++) J[r * 3 + c] = A[c * 3 + r];
+}
+__device__ __forceinline__ void ik_boxplus_d(livo_ikfom_state& s, const double* dx) {
+    _Pragma("unroll") for (int i = 0; i < 3; i++) s.pos[i] += dx[i];
+    qd_store(qd_mul(qd_load(s.rot), mtk_exp_d(dx + 3, 0.5)), s.rot);
+    qd_store(qd_mul(qd_load(s.offset_R), mtk_exp_d(dx + 6, 0.5)), s.offset_R);
+    _Pragma("unroll") for (int i = 0; i < 3; i++) {
+        s.offset_T[i] += dx[9 + i];
+        s.vel[i] += dx[12 + i];
+        s.bg[i] += dx[15 + i];
+        s.ba[i] += dx[18 + i];
+    }
+    s2_boxplus_d(s.grav, dx + 21);
+}
+__device__ __forceinline__ void ik_boxminus_d(const livo_ikfom_state& a, const livo_ikfom_state& b, double* dx) {
+    _Pragma("unroll") for (int i = 0; i < 3; i++) dx[i] = a.pos[i] - b.pos[i];
+    so3_log_qd(qd_mul(qd_conj(qd_load(b.rot)), qd_load(a.rot)), dx + 3);
+    so3_log_qd(qd_mul(qd_conj(qd_load(b.offset_R)), qd_load(a.offset_R)), dx + 6);
+    _Pragma("unroll") for (int i = 0; i < 3; i++) {
+        dx[9 + i] = a.offset_T[i] - b.offset_T[i];
+        dx[12 + i] = a.vel[i] - b.vel[i];
+        dx[15 + i] = a.bg[i] - b.bg[i];
+        dx[18 + i] = a.ba[i] - b.ba[i];
+    }
+    s2_boxminus_d(a.grav, b.grav, dx + 21);
+}
+// p_global = rot * (offset_R * p_body + offset_T) + pos (origin_laserMapping.cpp:937), stored as float
+__device__ __forceinline__ void ik_world_point(const livo_ikfom_state& s, float bx, float by, float bz, float& wx,
+                                               float& wy, float& wz) {
+    const double b[3] = {(double)bx, (double)by, (double)bz};
+    double t0[3], t1[3], g[3];
+    qd_rot(qd_load(s.offset_R), b, t0);
+    _Pragma("unroll") for (int c = 0; c < 3; c++) t1[c] = t0[c] + s.offset_T[c];
+    qd_rot(qd_load(s.rot), t1, g);
+    wx = (float)(g[0] + s.pos[0]);
+    wy = (float)(g[1] + s.pos[1]);
+    wz = (float)(g[2] + s.pos[2]);
+}
+
+
 // ============================================================== k-NN ======
 // PointType_CMP::operator< (ikd_Tree.h:57-60).
 __device__ __forceinline__ bool cand_less(float da, float xa, float db, float xb) {
@@ -312,6 +536,8 @@ __device__ __forceinline__ void query_point(const KnnParams& P, const IekfSlot* 
                                             float& qy, float& qz) {
     if (P.identity) {
         qx = b.x; qy = b.y; qz = b.z;
+    } else if (slot->model == kModelIkfom) {
+        ik_world_point(slot->ik.x, b.x, b.y, b.z, qx, qy, qz);  // origin_laserMapping.cpp:937
     } else {
         world_point(slot->state.rot, slot->state.pos, P.R_LI, P.t_LI, b.x, b.y, b.z, qx, qy, qz);
     }
@@ -925,73 +1151,66 @@ __device__ __forceinline__ double bcast(double v, int lane) {
 // PartialPivLU as the oracle (inverse18): first maximum |a_ik| over i >= k,
 // f = a_ik / a_kk, a_ij -= f * a_kj.  Row `lane` of the matrix is A; on return
 // LU (row-major 18x18) and the row permutation are in LDS.
-__device__ __forceinline__ void wave_lu_to_lds(double (&A)[kDim], int lane, double* s_LU, int* s_piv) {
+template <int N>
+__device__ __forceinline__ void wave_lu_to_lds(double (&A)[N], int lane, double* s_LU, int* s_piv) {
     int piv = lane;
 #pragma unroll
-    for (int k = 0; k < kDim; k++) {
+    for (int k = 0; k < N; k++) {
         // pivot: the first maximum of |a_ik| over i >= k, scanned in row order
         // on wave-uniform copies of column k (v_readlane, no LDS round trips)
         int p = k;
         double best = fabs(bcast(A[k], k));
 #pragma unroll
-        for (int i = k + 1; i < kDim; i++) {
+        for (int i = k + 1; i < N; i++) {
             const double v = fabs(bcast(A[k], i));
             if (v > best) {
                 best = v;
                 p = i;
             }
         }
-        if (p != k) {  // wave-uniform
-            double rk[kDim], rp[kDim];
-#pragma unroll
-            for (int j = 0; j < kDim; j++) {
-                rk[j] = bcast(A[j], k);
-                rp[j] = bcast(A[j], p);
-            }
+        if (p != k) {  // wave-uniform: swap rows k and p, one element at a time
             const int pk = __builtin_amdgcn_readlane(piv, k), pp = __builtin_amdgcn_readlane(piv, p);
-            if (lane == k) {
 #pragma unroll
-                for (int j = 0; j < kDim; j++) A[j] = rp[j];
-                piv = pp;
-            } else if (lane == p) {
-#pragma unroll
-                for (int j = 0; j < kDim; j++) A[j] = rk[j];
-                piv = pk;
+            for (int j = 0; j < N; j++) {
+                const double ak = bcast(A[j], k), ap = bcast(A[j], p);
+                A[j] = lane == k ? ap : (lane == p ? ak : A[j]);
             }
+            piv = lane == k ? pp : (lane == p ? pk : piv);
         }
-        double r[kDim];
+        // f = a_ik / a_kk, a_ij -= f * a_kj (rows below k)
+        const double f = A[k] / bcast(A[k], k);
+        const bool below = lane > k && lane < N;
+        if (below) A[k] = f;
 #pragma unroll
-        for (int j = k; j < kDim; j++) r[j] = bcast(A[j], k);
-        if (lane > k && lane < kDim) {
-            const double f = A[k] / r[k];
-            A[k] = f;
-#pragma unroll
-            for (int j = k + 1; j < kDim; j++) A[j] = A[j] - f * r[j];
+        for (int j = k + 1; j < N; j++) {
+            const double rkj = bcast(A[j], k);
+            if (below) A[j] = A[j] - f * rkj;
         }
     }
-    if (lane < kDim) {
+    if (lane < N) {
 #pragma unroll
-        for (int j = 0; j < kDim; j++) s_LU[lane * kDim + j] = A[j];
+        for (int j = 0; j < N; j++) s_LU[lane * N + j] = A[j];
         s_piv[lane] = piv;
     }
 }
 
 // Column c of A^-1 from the LU in LDS (forward then backward substitution,
 // sums in ascending index order exactly as the oracle).
-__device__ __forceinline__ void lds_lu_column(const double* s_LU, const int* s_piv, int c, double (&y)[kDim]) {
+template <int N>
+__device__ __forceinline__ void lds_lu_column(const double* s_LU, const int* s_piv, int c, double (&y)[N]) {
 #pragma unroll
-    for (int i = 0; i < kDim; i++) {
+    for (int i = 0; i < N; i++) {
         double sacc = (s_piv[i] == c) ? 1.0 : 0.0;
 #pragma unroll
-        for (int j = 0; j < i; j++) sacc = sacc - s_LU[i * kDim + j] * y[j];
+        for (int j = 0; j < i; j++) sacc = sacc - s_LU[i * N + j] * y[j];
         y[i] = sacc;
     }
 #pragma unroll
-    for (int i = kDim - 1; i >= 0; i--) {
+    for (int i = N - 1; i >= 0; i--) {
         double sacc = y[i];
 #pragma unroll
-        for (int j = i + 1; j < kDim; j++) sacc = sacc - s_LU[i * kDim + j] * y[j];
-        y[i] = sacc / s_LU[i * kDim + i];
+        for (int j = i + 1; j < N; j++) sacc = sacc - s_LU[i * N + j] * y[j];
+        y[i] = sacc / s_LU[i * N + i];
     }
 }
 
@@ -1087,11 +1306,11 @@ __device__ __forceinline__ void solve_scan(IekfSlot* slot, SolveLds& L, const in
         double A[kDim];
 #pragma unroll
         for (int j = 0; j < kDim; j++) A[j] = row ? s_P[lane * kDim + j] : 0.0;
-        wave_lu_to_lds(A, lane, s_LU, s_piv);
+        wave_lu_to_lds<kDim>(A, lane, s_LU, s_piv);
         WAVE_SYNC();
         if (lane < kDim) {
             double y[kDim];
-            lds_lu_column(s_LU, s_piv, lane, y);
+            lds_lu_column<kDim>(s_LU, s_piv, lane, y);
 #pragma unroll
             for (int i = 0; i < kDim; i++) s_Pinv[i * kDim + lane] = y[i];
         }
@@ -1108,12 +1327,12 @@ __device__ __forceinline__ void solve_scan(IekfSlot* slot, SolveLds& L, const in
 #pragma unroll
         for (int j = 0; j < kDim; j++)
             A[j] = row ? (((lane < 9 && j < 9) ? s_HTH[lane * 9 + j] : 0.0) + s_Pinv[lane * kDim + j]) : 0.0;
-        wave_lu_to_lds(A, lane, s_LU, s_piv);
+        wave_lu_to_lds<kDim>(A, lane, s_LU, s_piv);
         WAVE_SYNC();
         SOLVE_MARK(4);
         if (lane < 9) {
             double y[kDim];
-            lds_lu_column(s_LU, s_piv, lane, y);
+            lds_lu_column<kDim>(s_LU, s_piv, lane, y);
 #pragma unroll
             for (int i = 0; i < kDim; i++) s_K1[i * 9 + lane] = y[i];
         }
@@ -1410,6 +1629,355 @@ __global__ __launch_bounds__(kBlock) void k_hshare(HsParams P) {
     solve_scan(slot, L, tid);
 }
 
+// Per-point persistent selection of the IKFoM h-model: point_selected_surf is a
+// global array there (origin_laserMapping.cpp:155), so a point dropped by the
+// plane test stays dropped until the next search.  NNRec.flag bit:
+constexpr int kIkDrop = 0x1000;
+
+// LDS of the IKFoM plane pass: per-rep point rows, then (last block) the solve.
+struct IkSolveLds {
+    double P[kIkDim * kIkDim];
+    double Pinv[kIkDim * kIkDim];
+    double LU[kIkDim * kIkDim];
+    double L[kIkDim * kIkDim];
+    double Kx[kIkDim * 12];
+    double sum[kIkCols];
+    double dx[kIkDim], dxn[kIkDim], dxu[kIkDim], Kh[kIkDim];
+    double J[9];
+    int piv[kIkDim];
+    int stop;
+};
+constexpr int kIkRow = 15;  // 12 row + h + |pd2| + keep
+
+// One wave: esekfom.hpp:1638-1921 from the reduced sums in S.sum.
+__device__ void ik_solve(IekfSlot* slot, IkSolveLds& S, const int lane, const double R) {
+    IkBlock& K = slot->ik;
+    const IekfCtrl ctrl0 = slot->ctrl;
+    const int e = ctrl0.n_evals;
+    const int it = ctrl0.iter_count;  // i of the reference loop (starts at -1)
+    constexpr int N = kIkDim;
+    if (lane == 0) {
+        double dx[N];
+        ik_boxminus_d(K.x, K.xp, dx);  // x_.boxminus(dx, x_propagated)
+        for (int k = 0; k < N; k++) S.dx[k] = S.dxn[k] = dx[k];
+    }
+    for (int t = lane; t < N * N; t += 64) S.P[t] = K.xp.cov[t];  // P_ = P_propagated
+    WAVE_SYNC();
+    // SO3 (idx 3, 6) and S2 (idx 21) corrections of dx_new and P_ (:1659-1697)
+    for (int b = 0; b < 3; b++) {
+        const int idx = b == 0 ? 3 : (b == 1 ? 6 : 21), d = b == 2 ? 2 : 3;
+        if (lane == 0) {
+            double J[9], o[3];
+            if (b < 2) so3_J_d(S.dx + idx, J);
+            else s2_J_d(K.x.grav, K.xp.grav, S.dx + 21, J);
+            for (int r = 0; r < d; r++) {
+                double acc = J[r * d] * S.dxn[idx];
+                for (int k = 1; k < d; k++) acc = acc + J[r * d + k] * S.dxn[idx + k];
+                o[r] = acc;
+            }
+            for (int r = 0; r < d; r++) S.dxn[idx + r] = o[r];
+            for (int k = 0; k < d * d; k++) S.J[k] = J[k];
+        }
+        WAVE_SYNC();
+        if (lane < N) {  // rows idx.. of column `lane`: J * P
+            double o[3];
+            for (int r = 0; r < d; r++) {
+                double acc = S.J[r * d] * S.P[idx * N + lane];
+                for (int k = 1; k < d; k++) acc = acc + S.J[r * d + k] * S.P[(idx + k) * N + lane];
+                o[r] = acc;
+            }
+            for (int r = 0; r < d; r++) S.P[(idx + r) * N + lane] = o[r];
+        }
+        WAVE_SYNC();
+        if (lane < N) {  // columns idx.. of row `lane`: P * J^T
+            double o[3];
+            for (int c = 0; c < d; c++) {
+                double acc = S.P[lane * N + idx] * S.J[c * d];
+                for (int k = 1; k < d; k++) acc = acc + S.P[lane * N + idx + k] * S.J[c * d + k];
+                o[c] = acc;
+            }
+            for (int c = 0; c < d; c++) S.P[lane * N + idx + c] = o[c];
+        }
+        WAVE_SYNC();
+    }
+    // gain, information form (:1775-1787): P_temp = (P_/R)^-1 + HTH, P_inv = P_temp^-1.
+    // (The reference takes the equivalent measurement-space form when fewer than
+    // 23 points are effective, :1701-1736; oracle and tests check both agree.)
+    double HT[12];  // the row's part of h_x^T h_x is read from S.sum below
+    {
+        double A[N];
+        for (int j = 0; j < N; j++) A[j] = lane < N ? S.P[lane * N + j] / R : 0.0;
+        wave_lu_to_lds<N>(A, lane, S.LU, S.piv);
+        WAVE_SYNC();
+        if (lane < N) {
+            double y[N];
+            lds_lu_column<N>(S.LU, S.piv, lane, y);
+            for (int i = 0; i < N; i++) S.Pinv[i * N + lane] = y[i];
+        }
+        WAVE_SYNC();
+        for (int t = lane; t < 144; t += 64) {
+            const int r = t / 12, c = t % 12;
+            const int a = r < c ? r : c, bb = r < c ? c : r;
+            S.Pinv[r * N + c] += S.sum[a * 12 - (a * (a - 1)) / 2 + (bb - a)];
+        }
+        WAVE_SYNC();
+        for (int j = 0; j < N; j++) A[j] = lane < N ? S.Pinv[lane * N + j] : 0.0;
+        wave_lu_to_lds<N>(A, lane, S.LU, S.piv);
+        WAVE_SYNC();
+        if (lane < N) {
+            double y[N];
+            lds_lu_column<N>(S.LU, S.piv, lane, y);
+            for (int i = 0; i < N; i++) S.Pinv[i * N + lane] = y[i];
+        }
+        WAVE_SYNC();
+    }
+    (void)HT;
+    auto hth = [&](int r, int c) {
+        const int a = r < c ? r : c, bb = r < c ? c : r;
+        return S.sum[a * 12 - (a * (a - 1)) / 2 + (bb - a)];
+    };
+    if (lane < N) {
+        const int r = lane;
+        double kh = S.Pinv[r * N] * S.sum[78];
+        for (int c = 1; c < 12; c++) kh = kh + S.Pinv[r * N + c] * S.sum[78 + c];
+        S.Kh[r] = kh;
+        for (int c = 0; c < 12; c++) {
+            double a2 = S.Pinv[r * N] * hth(0, c);
+            for (int k = 1; k < 12; k++) a2 = a2 + S.Pinv[r * N + k] * hth(k, c);
+            S.Kx[r * 12 + c] = a2;
+        }
+    }
+    WAVE_SYNC();
+    if (lane < N) {  // dx_ = K_h + (K_x - I) dx_new
+        const int r = lane;
+        double acc = 0.0;
+        for (int c = 0; c < N; c++) {
+            const double kxi = (c < 12 ? S.Kx[r * 12 + c] : 0.0) - (r == c ? 1.0 : 0.0);
+            acc = (c == 0) ? kxi * S.dxn[0] : acc + kxi * S.dxn[c];
+        }
+        S.dxu[r] = S.Kh[r] + acc;
+    }
+    WAVE_SYNC();
+    if (lane == 0) {
+        double dxu[N];
+        for (int k = 0; k < N; k++) dxu[k] = S.dxu[k];
+        ik_boxplus_d(K.x, dxu);
+        bool converge = true;
+        for (int k = 0; k < N; k++)
+            if (fabs(dxu[k]) > 0.001) {
+                converge = false;
+                break;
+            }
+        int t = K.t + (converge ? 1 : 0);
+        if (!t && it == ctrl0.max_iter - 2) converge = true;
+        const bool stop = t > 1 || it == ctrl0.max_iter - 1;
+        livo_ikfom_stats& st = K.stats;
+        if (e < LIVO_MAX_EVALS) {
+            st.effct_feat_num[e] = (int64_t)S.sum[91];
+            st.res_mean[e] = S.sum[90] / S.sum[91];
+            for (int k = 0; k < N; k++) st.dx[e][k] = dxu[k];
+        }
+        st.iterations = e + 1;
+        st.knn_passes += ctrl0.search_en ? 1 : 0;
+        st.converged = converge ? 1 : 0;
+        st.t = t;
+        K.t = t;
+        IekfCtrl ctrl = ctrl0;
+        ctrl.last_search = ctrl0.search_en;
+        ctrl.search_en = converge ? 1 : 0;  // dyn_share.converge: search at the next h_dyn_share
+        ctrl.converged = converge ? 1 : 0;
+        ctrl.iter_count = it + 1;
+        ctrl.n_evals = e + 1;
+        ctrl.stop = (stop || ctrl.iter_count >= ctrl.max_iter || ctrl.n_evals >= LIVO_MAX_EVALS) ? 1 : 0;
+        slot->ctrl = ctrl;
+        S.stop = stop ? 1 : 0;
+    }
+    WAVE_SYNC();
+    if (!S.stop) return;
+    // covariance (:1838-1921): L_ = P_ with the corrections at dx_, P_ = L_ - K_x(:,0:12) P_(0:12,:)
+    for (int t = lane; t < N * N; t += 64) S.L[t] = S.P[t];
+    WAVE_SYNC();
+    for (int b = 0; b < 3; b++) {
+        const int idx = b == 0 ? 3 : (b == 1 ? 6 : 21), d = b == 2 ? 2 : 3;
+        if (lane == 0) {
+            double J[9];
+            if (b < 2) so3_J_d(S.dxu + idx, J);
+            else s2_J_d(K.x.grav, K.xp.grav, S.dxu + 21, J);
+            for (int k = 0; k < d * d; k++) S.J[k] = J[k];
+        }
+        WAVE_SYNC();
+        if (lane < N) {  // L rows idx.. = J * P rows, column `lane`
+            for (int r = 0; r < d; r++) {
+                double acc = S.J[r * d] * S.P[idx * N + lane];
+                for (int k = 1; k < d; k++) acc = acc + S.J[r * d + k] * S.P[(idx + k) * N + lane];
+                S.L[(idx + r) * N + lane] = acc;
+            }
+        }
+        if (lane < 12) {  // K_x rows idx.. (first 12 columns), column `lane`
+            double o[3];
+            for (int r = 0; r < d; r++) {
+                double acc = S.J[r * d] * S.Kx[idx * 12 + lane];
+                for (int k = 1; k < d; k++) acc = acc + S.J[r * d + k] * S.Kx[(idx + k) * 12 + lane];
+                o[r] = acc;
+            }
+            for (int r = 0; r < d; r++) S.Kx[(idx + r) * 12 + lane] = o[r];
+        }
+        WAVE_SYNC();
+        if (lane < N) {  // L and P columns idx.. of row `lane`: * J^T
+            double lo[3], po[3];
+            for (int c = 0; c < d; c++) {
+                double al = S.L[lane * N + idx] * S.J[c * d], ap = S.P[lane * N + idx] * S.J[c * d];
+                for (int k = 1; k < d; k++) {
+                    al = al + S.L[lane * N + idx + k] * S.J[c * d + k];
+                    ap = ap + S.P[lane * N + idx + k] * S.J[c * d + k];
+                }
+                lo[c] = al;
+                po[c] = ap;
+            }
+            for (int c = 0; c < d; c++) {
+                S.L[lane * N + idx + c] = lo[c];
+                S.P[lane * N + idx + c] = po[c];
+            }
+        }
+        WAVE_SYNC();
+    }
+    for (int t = lane; t < N * N; t += 64) {
+        const int r = t / N, c = t % N;
+        double acc = S.Kx[r * 12] * S.P[c];
+        for (int k = 1; k < 12; k++) acc = acc + S.Kx[r * 12 + k] * S.P[k * N + c];
+        K.x.cov[t] = S.L[t] - acc;
+    }
+}
+
+// IKFoM plane pass (origin_laserMapping.cpp:916-1048): 4 points per thread as
+// k_hshare; each point's 12-wide row [n, A, B, C], h = -pd2 goes to LDS and the
+// block's 92 sums (h_x^T h_x upper triangle, h_x^T h, residual sum, count) are
+// formed by 92 threads over the rows in point order (k_solve_ik reduces them).
+template <bool FIRST>
+__global__ __launch_bounds__(kBlock) void k_hshare_ik(HsParams P) {
+    __shared__ double rows[kBlock * kIkRow];
+    const HsJob job = P.jobs[blockIdx.y];
+    if ((int)blockIdx.x >= job.nblk) return;
+    IekfSlot* slot = job.slot;
+    if (slot->ctrl.stop) return;  // block-uniform
+    const int search = FIRST ? 1 : slot->ctrl.search_en;
+    const int tid = threadIdx.x;
+    const livo_ikfom_state& X = slot->ik.x;
+    // this thread's output of the block sums (t < 92): (a, b) of the upper triangle, or HTh / res / count
+    int oa = 0, ob = 0;
+    if (tid < 78) {
+        int t = tid, a = 0;
+        while (t >= 12 - a) { t -= 12 - a; a++; }
+        oa = a;
+        ob = a + t;
+    }
+    double acc = 0.0;
+    for (int rep = 0; rep < kPtsPerThread; rep++) {
+        const int i = (blockIdx.x * kPtsPerThread + rep) * kBlock + tid;
+        double row[kIkRow];
+        for (int k = 0; k < kIkRow; k++) row[k] = 0.0;
+        if (i < job.n) {
+            const float4 pb = reinterpret_cast<const float4*>(job.pts)[i];
+            float wx, wy, wz;
+            ik_world_point(X, pb.x, pb.y, pb.z, wx, wy, wz);
+            const float4* rec = reinterpret_cast<const float4*>(job.nn + i);
+            float nx[kNN], ny[kNN], nz[kNN];
+            float d4 = 0.0f;
+#pragma unroll
+            for (int k = 0; k < kNN; k++) {
+                const float4 v = rec[k];
+                nx[k] = v.x; ny[k] = v.y; nz[k] = v.z;
+                if (k == kNN - 1) d4 = v.w;
+            }
+            int* flagp = reinterpret_cast<int*>(job.nn + i) + 26;  // NNRec::flag
+            const int cnt = reinterpret_cast<const int4*>(job.nn + i)[6].y;
+            const int flag = *flagp;
+            const bool sel = search ? ((cnt == kNN) && !(d4 > P.max_sqd)) : !(flag & kIkDrop);
+            bool fin = false;
+            float pa[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+            float pd2 = 0.0f;
+            if (sel && cnt >= kNN) {
+                if (esti_plane(nx, ny, nz, P.plane_thr, pa)) {
+                    pd2 = ((pa[0] * wx + pa[1] * wy) + pa[2] * wz) + pa[3];
+                    const double bx = pb.x, by = pb.y, bz = pb.z;
+                    const double bn = sqrt((bx * bx + by * by) + bz * bz);
+                    const float s = (float)(1 - 0.9 * (double)fabsf(pd2) / sqrt(bn));
+                    fin = (double)s > 0.9;
+                }
+            }
+            const int nflag = fin ? (flag & ~kIkDrop) : (flag | kIkDrop);
+            if (nflag != flag) *flagp = nflag;
+            if (P.dbg.sel) P.dbg.sel[i] = (fin && (double)fabsf(pd2) <= P.max_res) ? 1 : 0;
+            if (fin && (double)fabsf(pd2) <= P.max_res) {
+                const double be[3] = {(double)pb.x, (double)pb.y, (double)pb.z};
+                const Qd qo = qd_load(X.offset_R);
+                double t0[3], pt[3];
+                qd_rot(qo, be, t0);
+                for (int c = 0; c < 3; c++) pt[c] = t0[c] + X.offset_T[c];
+                const double n[3] = {(double)pa[0], (double)pa[1], (double)pa[2]};
+                double C[3], A[3], Bv[3], Hp[9], Hb[9], Rt[9], HbR[9];
+                qd_rot(qd_conj(qd_load(X.rot)), n, C);
+                hat3d(pt, Hp);
+                mat3d_vec(Hp, C, A);
+                hat3d(be, Hb);
+                qd_mat(qd_conj(qo), Rt);
+                mat3d_mul(Hb, Rt, HbR);
+                mat3d_vec(HbR, C, Bv);
+                row[0] = n[0]; row[1] = n[1]; row[2] = n[2];
+                row[3] = A[0]; row[4] = A[1]; row[5] = A[2];
+                row[6] = Bv[0]; row[7] = Bv[1]; row[8] = Bv[2];
+                row[9] = C[0]; row[10] = C[1]; row[11] = C[2];
+                row[12] = -(double)pd2;
+                row[13] = (double)fabsf(pd2);
+                row[14] = 1.0;
+            }
+        }
+        for (int k = 0; k < kIkRow; k++) rows[tid * kIkRow + k] = row[k];
+        __syncthreads();
+        if (tid < kIkUsed) {  // rows in point order
+            for (int r = 0; r < kBlock; r++) {
+                const double* q = rows + r * kIkRow;
+                double v;
+                if (tid < 78) v = q[oa] * q[ob];
+                else if (tid < 90) v = q[tid - 78] * q[12];
+                else v = q[tid == 90 ? 13 : 14];
+                acc += v;
+            }
+        }
+        __syncthreads();
+    }
+    if (tid < kIkUsed) job.partial[(size_t)blockIdx.x * kIkCols + tid] = acc;
+}
+
+// One 64-thread block per scan: fixed-order reduction of the IKFoM partials,
+// then ik_solve (kept out of the plane pass: the 23-wide solve needs far more
+// registers than the per-point work).
+__global__ __launch_bounds__(64) void k_solve_ik(HsParams P) {
+    __shared__ IkSolveLds S;
+    const HsJob job = P.jobs[blockIdx.x];
+    IekfSlot* slot = job.slot;
+    const int lane = threadIdx.x;
+    if (P.replay_count && blockIdx.x == 0 && lane == 0) *P.replay_count = 0u;
+    if (slot->ctrl.stop) return;
+    for (int c = lane; c < kIkCols; c += 64) {
+        double acc8[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) acc8[k] = 0.0;
+        if (c < kIkUsed) {
+            const double* src = job.partial + c;
+            int b = 0;
+            for (; b + 7 < job.nblk; b += 8) {
+#pragma unroll
+                for (int k = 0; k < 8; k++) acc8[k] += src[(size_t)(b + k) * kIkCols];
+            }
+            for (int k = 0; b + k < job.nblk; k++) acc8[k] += src[(size_t)(b + k) * kIkCols];
+        }
+        S.sum[c] = ((acc8[0] + acc8[1]) + (acc8[2] + acc8[3])) + ((acc8[4] + acc8[5]) + (acc8[6] + acc8[7]));
+    }
+    WAVE_SYNC();
+    ik_solve(slot, S, lane, P.lpc);
+}
+
 __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
     __shared__ SolveLds L;
     const HsJob job = P.jobs[blockIdx.x];
@@ -1491,6 +2059,19 @@ int launch_hshare(const HsParams& p, int n_jobs, int max_nblk, bool first, void*
         hipLaunchKernelGGL(k_hshare<true>, grid, block, 0, (hipStream_t)stream, p);
     else
         hipLaunchKernelGGL(k_hshare<false>, grid, block, 0, (hipStream_t)stream, p);
+    return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+
+int launch_hshare_ik(const HsParams& p, int n_jobs, int max_nblk, bool first, void* stream) {
+    if (n_jobs <= 0 || max_nblk <= 0) return LIVO_OK;
+    dim3 grid(max_nblk, n_jobs), block(kBlock);
+    if (first)
+        hipLaunchKernelGGL(k_hshare_ik<true>, grid, block, 0, (hipStream_t)stream, p);
+    else
+        hipLaunchKernelGGL(k_hshare_ik<false>, grid, block, 0, (hipStream_t)stream, p);
+    if (hipGetLastError() != hipSuccess) return LIVO_E_HIP;
+    if (!p.solve) return LIVO_OK;
+    hipLaunchKernelGGL(k_solve_ik, dim3(n_jobs), dim3(64), 0, (hipStream_t)stream, p);
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 

@@ -75,6 +75,48 @@ class Timings(C.Structure):
 
 # every entry point of include/livo.h, with its ctypes signature
 _P = C.c_void_p
+IKN = 23  # LIVO_IKFOM_DOF
+
+
+class IkfomState(C.Structure):
+    """livo_ikfom_state: state_ikfom with quaternions (w, x, y, z) and the S2 gravity vector."""
+    _fields_ = [("pos", C.c_double * 3), ("rot", C.c_double * 4), ("offset_R", C.c_double * 4),
+                ("offset_T", C.c_double * 3), ("vel", C.c_double * 3), ("bg", C.c_double * 3),
+                ("ba", C.c_double * 3), ("grav", C.c_double * 3), ("cov", C.c_double * (IKN * IKN))]
+
+
+class IkfomStats(C.Structure):
+    _fields_ = [("iterations", C.c_int32), ("knn_passes", C.c_int32), ("converged", C.c_int32),
+                ("t", C.c_int32), ("effct_feat_num", C.c_int64 * 16), ("dx", (C.c_double * IKN) * 16),
+                ("res_mean", C.c_double * 16)]
+
+
+_IK_FIELDS = (("pos", 3), ("rot", 4), ("offset_R", 4), ("offset_T", 3), ("vel", 3), ("bg", 3), ("ba", 3),
+              ("grav", 3))
+
+
+def ikfom_to_c(st: dict) -> IkfomState:
+    s = IkfomState()
+    for k, n in _IK_FIELDS:
+        getattr(s, k)[:] = np.asarray(st[k], np.float64).reshape(n).tolist()
+    s.cov[:] = np.asarray(st["cov"], np.float64).reshape(IKN * IKN).tolist()
+    return s
+
+
+def ikfom_from_c(s: IkfomState) -> dict:
+    out = {k: np.array(getattr(s, k)[:]) for k, _ in _IK_FIELDS}
+    out["cov"] = np.array(s.cov[:]).reshape(IKN, IKN)
+    return out
+
+
+def ikfom_stats_from_c(st: IkfomStats) -> dict:
+    ne = st.iterations
+    return {"iterations": ne, "knn_passes": st.knn_passes, "converged": st.converged, "t": st.t,
+            "effct_feat_num": [st.effct_feat_num[i] for i in range(min(ne, 16))],
+            "dx": np.array([list(st.dx[i]) for i in range(min(ne, 16))]),
+            "res_mean": [st.res_mean[i] for i in range(min(ne, 16))]}
+
+
 SIGNATURES = {
     "livo_abi_version": (C.c_int, []),
     "livo_error_string": (C.c_char_p, [C.c_int]),
@@ -93,6 +135,8 @@ SIGNATURES = {
                                C.POINTER(PointOut)]),
     "livo_iekf_update": (C.c_int, [_P, C.c_int32, C.POINTER(State), C.POINTER(State), C.POINTER(IterStats)]),
     "livo_iekf_update_batch": (C.c_int, [_P, C.c_int32, _P, _P, _P, _P]),
+    "livo_ikfom_update": (C.c_int, [_P, C.c_int32, C.POINTER(IkfomState), C.POINTER(IkfomStats)]),
+    "livo_ikfom_update_batch": (C.c_int, [_P, C.c_int32, _P, _P, _P]),
     "livo_sync": (C.c_int, [_P]),
 }
 
@@ -281,6 +325,26 @@ class Context:
         if raw:
             return sts, stats
         return [state_from_c(s) for s in sts], [stats_from_c(s) for s in stats]
+
+    # ------------------------------------------------------------ IKFoM ----
+    def ikfom_update(self, sid: int, state: dict):
+        """IKFoM iterated update (esekfom.hpp:1619-1928) of one resident scan."""
+        st = ikfom_to_c(state)
+        stats = IkfomStats()
+        _check("livo_ikfom_update", self._L.livo_ikfom_update(self.h, sid, C.byref(st), C.byref(stats)))
+        return ikfom_from_c(st), ikfom_stats_from_c(stats)
+
+    def ikfom_update_batch(self, sids, states, raw: bool = False):
+        n = len(sids)
+        ids = (C.c_int32 * n)(*sids)
+        sts = states if raw else (IkfomState * n)(*[ikfom_to_c(s) for s in states])
+        stats = (IkfomStats * n)()
+        _check("livo_ikfom_update_batch",
+               self._L.livo_ikfom_update_batch(self.h, n, C.cast(ids, C.c_void_p), C.cast(sts, C.c_void_p),
+                                               C.cast(stats, C.c_void_p)))
+        if raw:
+            return sts, stats
+        return [ikfom_from_c(s) for s in sts], [ikfom_stats_from_c(s) for s in stats]
 
     def set_profiling(self, level):
         """0/False off, 1 first-search timing only, 2/True every stage (livo_ctx_set_profiling)."""

@@ -167,6 +167,49 @@ int livo_iekf_update(livo_ctx* ctx, int32_t scan_id, livo_state* state, const li
 int livo_iekf_update_batch(livo_ctx* ctx, int32_t n, const int32_t* scan_ids, livo_state* states,
                            const livo_state* priors, livo_iter_stats* stats);
 
+/* ------------------------------------------------------------------------
+ * IKFoM formulation (the "solve in use-ikfom.hpp"):
+ *   state_ikfom                         include/use-ikfom.hpp:12-21 (23 DOF)
+ *   h_share_model (legacy h-model)      src/origin_laserMapping.cpp:916-1048
+ *   esekf::update_iterated_dyn_share_modified
+ *                                       include/IKFoM_toolkit/esekfom/esekfom.hpp:1619-1928
+ * The same map, scans and k-NN as above; 12-wide measurement rows [n, A, B, C]
+ * (extrinsic estimation on), the manifold (SO3 / S2) Jacobian corrections,
+ * per-DOF convergence |dx_i| <= 0.001 (origin_laserMapping.cpp:1231-1233),
+ * R = params.laser_point_cov, maximum_iter = params.max_iterations.
+ * ------------------------------------------------------------------------ */
+#define LIVO_IKFOM_DOF 23
+
+/* state_ikfom: quaternions (w, x, y, z) for rot and offset_R_L_I, the S2
+ * gravity as its 3-vector (length 98090/10000), cov = P_ (23x23 row-major). */
+typedef struct livo_ikfom_state {
+    double pos[3];
+    double rot[4];
+    double offset_R[4];
+    double offset_T[3];
+    double vel[3];
+    double bg[3];
+    double ba[3];
+    double grav[3];
+    double cov[LIVO_IKFOM_DOF * LIVO_IKFOM_DOF];
+} livo_ikfom_state;
+
+typedef struct livo_ikfom_stats {
+    int32_t iterations;   /* h_dyn_share + update evaluations                    */
+    int32_t knn_passes;   /* evaluations with dyn_share.converge (k-NN search)   */
+    int32_t converged;    /* dyn_share.converge at exit                          */
+    int32_t t;            /* converged-iteration counter t at exit               */
+    int64_t effct_feat_num[LIVO_MAX_EVALS];
+    double dx[LIVO_MAX_EVALS][LIVO_IKFOM_DOF];  /* dx_ applied per evaluation */
+    double res_mean[LIVO_MAX_EVALS];
+} livo_ikfom_stats;
+
+/* The IKFoM iterated update of n resident scans, each starting from its state
+ * (x_propagated = the input state, P_propagated = its cov).  stats may be NULL. */
+int livo_ikfom_update_batch(livo_ctx* ctx, int32_t n, const int32_t* scan_ids, livo_ikfom_state* states,
+                            livo_ikfom_stats* stats);
+int livo_ikfom_update(livo_ctx* ctx, int32_t scan_id, livo_ikfom_state* state, livo_ikfom_stats* stats);
+
 int livo_sync(livo_ctx* ctx);
 
 #ifdef __cplusplus

@@ -105,3 +105,20 @@ def test_struct_layouts_match_c(tmp_path):
     assert got == want
     import oracle
     assert C.sizeof(oracle.OrcState) == C.sizeof(livo_amd.State)
+
+
+def test_ikfom_struct_layouts_match_c(tmp_path):
+    import livo_amd
+    import oracle
+    src = tmp_path / "ik.c"
+    src.write_text('#include "livo.h"\n#include <stdio.h>\n#include <stddef.h>\nint main(void){printf("%zu %zu %zu '
+                   '%zu %zu\\n", sizeof(livo_ikfom_state), sizeof(livo_ikfom_stats), offsetof(livo_ikfom_state, cov), '
+                   'offsetof(livo_ikfom_stats, dx), offsetof(livo_ikfom_stats, res_mean));return 0;}\n')
+    exe = tmp_path / "ik"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(src)])
+    got = [int(x) for x in subprocess.check_output([str(exe)]).split()]
+    want = [C.sizeof(livo_amd.IkfomState), C.sizeof(livo_amd.IkfomStats), livo_amd.IkfomState.cov.offset,
+            livo_amd.IkfomStats.dx.offset, livo_amd.IkfomStats.res_mean.offset]
+    assert got == want
+    assert C.sizeof(oracle.OrcIkfomState) == C.sizeof(livo_amd.IkfomState)
+    assert C.sizeof(oracle.OrcIkfomStats) == C.sizeof(livo_amd.IkfomStats)
