@@ -72,6 +72,14 @@ struct livo_ctx {
     float* lpts = nullptr;
     int32_t leaf_depth = 0;
     int64_t leaf_bytes = 0;
+    int knn_kind = 1;                  // batched search structure: 0 leaf map, 1 cell grid (LIVO_KNN_KIND)
+    float grid_cell = 0.f;             // cell edge (LIVO_GRID_CELL; 0: from the map)
+    GridSlot* gslots = nullptr;        // cell grid
+    float* gpts = nullptr;
+    float gorg[3] = {0.f, 0.f, 0.f};
+    float gh = 1.f, geps = 0.f;
+    int32_t glog2 = 0;
+    int64_t grid_bytes = 0;
     bool has_map = false;
     // scans
     std::vector<ScanBuf> scans;
@@ -167,6 +175,12 @@ static KnnParams make_knn_params(livo_ctx* c) {
     kp.lpts = c->lpts;
     kp.ldepth = c->leaf_depth;
     kp.lM = c->has_map ? c->map_points : 0;
+    kp.gslots = c->gslots;
+    kp.gpts = c->gpts;
+    std::memcpy(kp.gorg, c->gorg, sizeof(kp.gorg));
+    kp.gh = c->gh;
+    kp.geps = c->geps;
+    kp.glog2 = c->glog2;
     kp.identity = 0;
     return kp;
 }
@@ -179,6 +193,11 @@ static int knn_pass(const KnnParams& kp, int n_jobs, int64_t max_n, hipStream_t 
 
 // Morton (Z-order) permutation of the body points: 0.25 m cells, 10 bits/axis.
 static std::vector<int32_t> morton_order(const std::vector<float>& p4, int64_t n) {
+    static const float scale = [] {  // cells per metre (LIVO_MORTON_SCALE tuning knob)
+        const char* e = std::getenv("LIVO_MORTON_SCALE");
+        const float v = e ? (float)std::atof(e) : 4.0f;
+        return v > 0.0f ? v : 4.0f;
+    }();
     std::vector<std::pair<uint64_t, int32_t>> key((size_t)n);
     float lo[3] = {INFINITY, INFINITY, INFINITY};
     for (int64_t i = 0; i < n; i++)
@@ -187,7 +206,7 @@ static std::vector<int32_t> morton_order(const std::vector<float>& p4, int64_t n
         uint64_t code = 0;
         uint32_t q[3];
         for (int a = 0; a < 3; a++) {
-            float f = (p4[4 * i + a] - lo[a]) * 4.0f;
+            float f = (p4[4 * i + a] - lo[a]) * scale;
             if (!(f >= 0.0f)) f = 0.0f;
             q[a] = (uint32_t)std::min(f, 1048575.0f);
         }
@@ -310,6 +329,11 @@ int livo_ctx_create(int device, const livo_params* p, livo_ctx** out) {
         const int v = std::atoi(env);
         if (v >= 2 && v <= 256) c->leaf_size = v;
     }
+    if (const char* env = std::getenv("LIVO_KNN_KIND")) c->knn_kind = std::strcmp(env, "leaf") == 0 ? 0 : 1;
+    if (const char* env = std::getenv("LIVO_GRID_CELL")) {
+        const float v = (float)std::atof(env);
+        if (v > 0.f) c->grid_cell = v;
+    }
     if (set_device(c) || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess || create_group_streams(c)) {
         delete c;
@@ -330,6 +354,8 @@ int livo_ctx_destroy(livo_ctx* c) {
     dev_free(c->nodes);
     dev_free(c->lnodes);
     dev_free(c->lpts);
+    dev_free(c->gslots);
+    dev_free(c->gpts);
     dev_free(c->d_replay_count);
     dev_free(c->d_replay_total);
     dev_free(c->d_replay_list);
@@ -383,7 +409,9 @@ int livo_map_build(livo_ctx* c, const float* xyz, int64_t M, int64_t stride_byte
     int rc = build_host_map(xyz, M, stride_bytes, &hm);
     if (rc) return rc;
     HostLeafMap lm;
-    rc = build_leaf_map(xyz, M, stride_bytes, c->leaf_size, &lm);
+    HostGridMap gm;
+    rc = c->knn_kind == 1 ? build_grid_map(xyz, M, stride_bytes, c->grid_cell, &gm)
+                          : build_leaf_map(xyz, M, stride_bytes, c->leaf_size, &lm);
     if (rc) {
         free_host_map(&hm);
         return rc;
@@ -393,27 +421,44 @@ int livo_map_build(livo_ctx* c, const float* xyz, int64_t M, int64_t stride_byte
     dev_free(c->nodes);
     dev_free(c->lnodes);
     dev_free(c->lpts);
+    dev_free(c->gslots);
+    dev_free(c->gpts);
     c->nodes = nullptr;
     c->lnodes = nullptr;
     c->lpts = nullptr;
+    c->gslots = nullptr;
+    c->gpts = nullptr;
+    c->leaf_bytes = c->grid_bytes = 0;
     c->has_map = false;
     const size_t bytes = (size_t)(hm.num_slots + 1) * sizeof(MapNode);
-    const size_t lnb = (size_t)std::max<int64_t>(((int64_t)1 << lm.depth) - 1, 1) * sizeof(LeafNode);
-    const size_t lpb = (size_t)(M + 3) * 4 * sizeof(float);  // chunk padding
-    if (hipMalloc((void**)&c->nodes, bytes) != hipSuccess || hipMalloc((void**)&c->lnodes, lnb) != hipSuccess ||
-        hipMalloc((void**)&c->lpts, lpb) != hipSuccess) {
-        free_host_map(&hm);
-        free_leaf_map(&lm);
-        return LIVO_E_OOM;
+    const size_t ppb = (size_t)(M + 3) * 4 * sizeof(float);  // chunk padding
+    hipError_t e = hipSuccess;
+    bool oom = hipMalloc((void**)&c->nodes, bytes) != hipSuccess;
+    if (c->knn_kind == 1) {
+        const size_t gsb = ((size_t)1 << gm.log2_slots) * sizeof(GridSlot);
+        oom = oom || hipMalloc((void**)&c->gslots, gsb) != hipSuccess || hipMalloc((void**)&c->gpts, ppb) != hipSuccess;
+        if (!oom) e = hipMemcpy(c->gslots, gm.slots, gsb, hipMemcpyHostToDevice);
+        if (!oom && e == hipSuccess) e = hipMemcpy(c->gpts, gm.pts, ppb, hipMemcpyHostToDevice);
+        c->grid_bytes = (int64_t)(gsb + ppb);
+        std::memcpy(c->gorg, gm.org, sizeof(c->gorg));
+        c->gh = gm.h;
+        c->glog2 = gm.log2_slots;
+        // slack for float rounding in the cell assignment (host) and cell bounds (device)
+        c->geps = (float)(32.0 * std::ldexp(1.0, -24) * (double)gm.cmax + 1e-7);
+    } else {
+        const size_t lnb = (size_t)std::max<int64_t>(((int64_t)1 << lm.depth) - 1, 1) * sizeof(LeafNode);
+        oom = oom || hipMalloc((void**)&c->lnodes, lnb) != hipSuccess || hipMalloc((void**)&c->lpts, ppb) != hipSuccess;
+        if (!oom) e = hipMemcpy(c->lnodes, lm.nodes, lnb, hipMemcpyHostToDevice);
+        if (!oom && e == hipSuccess) e = hipMemcpy(c->lpts, lm.pts, ppb, hipMemcpyHostToDevice);
+        c->leaf_depth = lm.depth;
+        c->leaf_bytes = (int64_t)(lnb + ppb);
     }
-    hipError_t e = hipMemcpy(c->nodes, hm.nodes, bytes, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(c->lnodes, lm.nodes, lnb, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(c->lpts, lm.pts, lpb, hipMemcpyHostToDevice);
+    if (!oom && e == hipSuccess) e = hipMemcpy(c->nodes, hm.nodes, bytes, hipMemcpyHostToDevice);
     free_host_map(&hm);
     free_leaf_map(&lm);
+    free_grid_map(&gm);
+    if (oom) return LIVO_E_OOM;
     if (e != hipSuccess) return LIVO_E_HIP;
-    c->leaf_depth = lm.depth;
-    c->leaf_bytes = (int64_t)(lnb + lpb);
     c->map_points = M;
     c->map_slots = hm.num_slots;
     c->map_depth = hm.depth;
@@ -429,7 +474,7 @@ int livo_map_get_info(livo_ctx* c, livo_map_info* out) {
     out->depth = c->map_depth;
     out->reserved = 0;
     out->num_slots = c->map_slots;
-    out->device_bytes = (c->map_slots + 1) * (int64_t)sizeof(MapNode) + c->leaf_bytes;
+    out->device_bytes = (c->map_slots + 1) * (int64_t)sizeof(MapNode) + c->leaf_bytes + c->grid_bytes;
     return LIVO_OK;
 }
 
@@ -543,6 +588,26 @@ int livo_scan_release(livo_ctx* c, int32_t id) {
 static ScanBuf* get_scan(livo_ctx* c, int32_t id) {
     if (id < 0 || id >= (int32_t)c->scans.size() || !c->scans[id].used) return nullptr;
     return &c->scans[id];
+}
+
+int livo_scan_neighbors(livo_ctx* c, int32_t id, int32_t* idx, float* sqdist) {
+    if (!c) return LIVO_E_INVALID;
+    ScanBuf* s = get_scan(c, id);
+    if (!s || !s->searched) return LIVO_E_NOSCAN;
+    if (set_device(c)) return LIVO_E_HIP;
+    std::vector<NNRec> rec((size_t)s->n);
+    if (s->n > 0) {
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        HIP_TRY(hipMemcpy(rec.data(), s->nn, (size_t)s->n * sizeof(NNRec), hipMemcpyDeviceToHost));
+    }
+    for (int64_t j = 0; j < s->n; j++) {
+        const int64_t o = s->perm.empty() ? j : (int64_t)s->perm[(size_t)j];  // caller's point index
+        for (int k = 0; k < kNN; k++) {
+            if (idx) idx[o * kNN + k] = rec[(size_t)j].idx[k];
+            if (sqdist) sqdist[o * kNN + k] = rec[(size_t)j].p[k][3];
+        }
+    }
+    return LIVO_OK;
 }
 
 int livo_h_share(livo_ctx* c, int32_t id, const livo_state* state, int search_en, double HTH[81], double HTL[9],
@@ -722,7 +787,8 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
             if (full && (e > 0 || gi > 0)) HIP_TRY(hipEventRecord(c->ev[gi][3 * e], st));
             // leaf-map search; rematch passes are bounded by the previous neighbours
             // (the group's replay count was zeroed before the batch / by the last k_solve)
-            rc = launch_knn_leaf(kp[gi], g[gi].count, g[gi].max_n, e > 0, st);
+            rc = c->knn_kind == 1 ? launch_knn_grid(kp[gi], g[gi].count, g[gi].max_n, e > 0, st)
+                                  : launch_knn_leaf(kp[gi], g[gi].count, g[gi].max_n, e > 0, st);
             if (rc) return rc;
             if ((prof && e == 0) || full) HIP_TRY(hipEventRecord(c->ev[gi][3 * e + 1], st));
             rc = model == kModelIkfom ? launch_hshare_ik(hp[gi], g[gi].count, g[gi].max_nblk, e == 0, st)

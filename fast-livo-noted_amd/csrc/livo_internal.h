@@ -15,7 +15,10 @@ namespace livo {
 constexpr int kNN = LIVO_NUM_MATCH_POINTS;  // 5
 constexpr int kDim = LIVO_DIM_STATE;        // 18
 constexpr int kBlock = 256;                 // threads per block of the per-point kernels
-constexpr int kKnnBlock = 128;              // threads per block of the k-NN pass (LDS stacks)
+#ifndef LIVO_KNN_BLOCK
+#define LIVO_KNN_BLOCK 128
+#endif
+constexpr int kKnnBlock = LIVO_KNN_BLOCK;   // threads per block of the k-NN pass (LDS stacks)
 constexpr int kPtsPerThread = LIVO_PTS_PER_THREAD;  // points per thread of the plane-fit pass
 constexpr int kRedCols = 32;                // doubles per block partial (29 used)
 constexpr int kRedUsed = 29;                // 21 HTH upper-tri + 6 HTL + residual sum + count
@@ -80,6 +83,40 @@ struct HostLeafMap {
 };
 int build_leaf_map(const float* xyz, int64_t M, int64_t stride_bytes, int leaf_size, HostLeafMap* out);
 void free_leaf_map(HostLeafMap* m);
+
+// ---------------------------------------------------------------------------
+// Cell grid: the other search structure of the batched IEKF (LIVO_KNN_KIND).
+// The map's points sorted by cubic cell (edge h, cell c = floor((p - org) / h)),
+// each cell a contiguous run, found through an open-addressing hash table of
+// 16-B slots {key, start, count}.  A query scans its cell, then whole rings of
+// cells around it, each pruned by box distance, until the ring boundary
+// certifies the 5 nearest (k_knn_grid) -- a few independent loads per query
+// instead of a chain of dependent tree visits.  Equivalence with the reference
+// as for the leaf map (C1 / C2, exact replay otherwise).
+// ---------------------------------------------------------------------------
+struct alignas(16) GridSlot {
+    unsigned long long key;  // kGridEmpty: free
+    uint32_t start;
+    uint32_t count;
+};
+constexpr unsigned long long kGridEmpty = ~0ull;
+constexpr int kGridBias = 1 << 20;  // cell index bias in the key (21 bits per axis)
+constexpr int kGridMaxRing = 3;     // cube radius searched for the first 5 points
+constexpr int kGridMaxCells = 729;  // stage-2 boxes beyond this: exact replay on the ikd-Tree
+
+struct HostGridMap {
+    GridSlot* slots = nullptr;  // 2^log2_slots
+    float* pts = nullptr;       // (M + 3) x 4 floats, sorted by cell
+    int64_t num_points = 0;
+    int32_t log2_slots = 0;
+    int64_t cells = 0;          // occupied cells
+    float org[3] = {0.f, 0.f, 0.f};
+    float h = 1.f;
+    float cmax = 0.f;           // largest |coordinate| (bounds the float rounding of cell bounds)
+};
+// cell_h <= 0: chosen from the map (about 20 points per occupied cell)
+int build_grid_map(const float* xyz, int64_t M, int64_t stride_bytes, float cell_h, HostGridMap* out);
+void free_grid_map(HostGridMap* m);
 
 // IEKF control block (the loop variables of laser_mapping.cpp:166-238).
 struct IekfCtrl {
@@ -186,6 +223,12 @@ struct KnnParams {
     const LeafNode* lnodes; // leaf map internal records
     const float* lpts;      // leaf map points, 4 floats each (x, y, z, index bits)
     int64_t lM;             // leaf map points
+    const GridSlot* gslots; // cell grid
+    const float* gpts;
+    float gorg[3];
+    float gh;               // cell edge
+    float geps;             // cell-bound slack for float rounding of the cell assignment
+    int32_t glog2;          // log2 of the hash table size
 };
 
 struct SolveParams {
@@ -213,6 +256,7 @@ int launch_knn_pass(const KnnParams& p, int n_jobs, int64_t max_n, void* stream)
 // Batched IEKF k-NN on the leaf map; seeded: rematch pass bounded by the
 // point's previous neighbours.  Both are followed by the exact tie replay.
 int launch_knn_leaf(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, void* stream);
+int launch_knn_grid(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, void* stream);
 int launch_hshare(const HsParams& p, int n_jobs, int max_nblk, bool first, void* stream);
 // IKFoM plane pass (12-wide rows) with the manifold update in each scan's last block.
 int launch_hshare_ik(const HsParams& p, int n_jobs, int max_nblk, bool first, void* stream);

@@ -752,12 +752,54 @@ __device__ __forceinline__ void lq_point(LeafQuery& q, const float4 v, uint32_t 
 }
 
 // C1/C2 check, neighbour record, replay flag.
-__device__ __forceinline__ void lq_finish(const LeafQuery& q, const KnnParams& P, const HsJob& job, unsigned bjob,
+//
+// Exact ties inside the list are resolved here rather than replayed.  The
+// reference inserts a point only when dist < top (ikd_Tree.cpp:860), so every
+// point nearer than the final 5th distance D is in its heap whatever the
+// visiting order; only a point AT D competing for the last place (C1:
+// e6 - d5 <= fuzz) depends on the order.  Its output order is the heap's pop
+// order under PointType_CMP (ikd_Tree.h:57-60): equal distances compare by x.
+// When every adjacent gap of the list is either 0 or > 1e-10 that comparison
+// is a strict total order on the 5 points, so sorting by (dist, x) gives the
+// reference's order.  A gap in (0, 1e-10] (CMP not transitive) or an exact tie
+// with equal x (neither point "less") still goes to the exact replay.
+__device__ __forceinline__ void lq_finish(LeafQuery& q, const KnnParams& P, const HsJob& job, unsigned bjob,
                                           int i, const float4* __restrict__ lpts, bool overrun) {
     const int cnt = (int)min<int64_t>(P.lM, (int64_t)kNN);
-    bool amb = overrun || q.e6 - q.d[kNN - 1] <= kFuzz;  // C1 (false while e6 = +inf)
+    float4 a[kNN];
 #pragma unroll
-    for (int k = 0; k + 1 < kNN; k++) amb |= (k + 1 < cnt) && (q.d[k + 1] - q.d[k] <= kFuzz);  // C2
+    for (int k = 0; k < kNN; k++) a[k] = k < cnt ? lpts[q.nd[k]] : make_float4(0.f, 0.f, 0.f, 0.f);
+    bool amb = overrun || q.e6 - q.d[kNN - 1] <= kFuzz;  // C1 (false while e6 = +inf)
+    bool tie = false;
+#pragma unroll
+    for (int k = 0; k + 1 < kNN; k++) {
+        if (k + 1 < cnt && q.d[k + 1] - q.d[k] <= kFuzz) {  // C2
+            if (q.d[k + 1] == q.d[k] && a[k + 1].x != a[k].x) tie = true;
+            else amb = true;
+        }
+    }
+    if (tie && !amb) {
+        // (dist, x) order; the list is already sorted by dist
+        float ax[kNN];
+#pragma unroll
+        for (int k = 0; k < kNN; k++) ax[k] = a[k].x;
+#pragma unroll
+        for (int pass = 0; pass + 1 < kNN; pass++) {
+#pragma unroll
+            for (int k = 0; k + 1 < kNN; k++) {
+                const bool sw = k + 1 < cnt && q.d[k + 1] == q.d[k] && ax[k + 1] < ax[k];
+                const float tx = ax[k];
+                const uint32_t tn = q.nd[k];
+                ax[k] = sw ? ax[k + 1] : tx;
+                q.nd[k] = sw ? q.nd[k + 1] : tn;
+                ax[k + 1] = sw ? tx : ax[k + 1];
+                q.nd[k + 1] = sw ? tn : q.nd[k + 1];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kNN; k++)
+            if (k < cnt) a[k] = lpts[q.nd[k]];
+    }
     // neighbour record: points, distances, original indices; node[] = leaf-map slots
     float4* o4 = reinterpret_cast<float4*>(job.nn + i);
     int32_t idx[kNN];
@@ -766,13 +808,12 @@ __device__ __forceinline__ void lq_finish(const LeafQuery& q, const KnnParams& P
         float4 v = make_float4(0.f, 0.f, 0.f, INFINITY);
         idx[k] = -1;
         if (k < cnt) {
-            const float4 a = lpts[q.nd[k]];
-            v = make_float4(a.x, a.y, a.z, q.d[k]);
-            idx[k] = (int32_t)__float_as_uint(a.w);
+            v = make_float4(a[k].x, a[k].y, a[k].z, q.d[k]);
+            idx[k] = (int32_t)__float_as_uint(a[k].w);
         }
         o4[k] = v;
     }
-    const int flag = amb ? 4 : 0;
+    const int flag = amb ? 4 : (tie ? 16 : 0);
     int4* oi = reinterpret_cast<int4*>(job.nn + i) + 5;
     oi[0] = make_int4(idx[0], idx[1], idx[2], idx[3]);
     oi[1] = make_int4(idx[4], cnt, flag, (int)q.nd[0]);
@@ -885,6 +926,160 @@ __global__ __launch_bounds__(kKnnBlock, Q == 1 ? 8 : 6) void k_knn_leaf(KnnParam
 #pragma unroll
     for (int u = 0; u < Q; u++)
         if (i0 + u < job.n) lq_finish(q[u], P, job, bjob, i0 + u, lpts, overrun);
+    count_visits(P, slot, visits);
+}
+
+// ------------------------------------------------------- cell-grid k-NN ----
+// The cell-grid search (LIVO_KNN_KIND=grid).  Stage 0 scans the 2x2x2 block of
+// cells around the query (its own cell first, then the neighbours on the side
+// of the cell the query lies in).  Stage 1 scans, within the 3x3x3 cube of
+// cells, those the current bound min(5th candidate, seed bound) still reaches
+// (the whole cube while fewer than 5 points are known), so the bound shrinks
+// before stage 2 scans every remaining cell overlapping the cube of half-edge
+// sqrt(bound) around the query: every point that can still enter the list lies
+// there, so the list is exact.  A query whose list is not full by then, or whose
+// stage-2 box exceeds kGridMaxCells cells, goes to the exact replay.  Cells are found by hashing (a 16-B slot holds the cell's
+// point range: one load, then the points), cells farther than
+// min(5th candidate, seed bound) + 1e-10 are skipped.  Same candidate list, e6
+// and C1/C2 flags as k_knn_leaf, so the same equivalence argument holds.
+__device__ __forceinline__ unsigned long long grid_key_d(int cx, int cy, int cz) {
+    return (unsigned long long)(cx + kGridBias) | ((unsigned long long)(cy + kGridBias) << 21) |
+           ((unsigned long long)(cz + kGridBias) << 42);
+}
+
+#ifndef LIVO_GRID_WAVES
+#define LIVO_GRID_WAVES 5  // waves per SIMD (VGPR budget 96: no spills)
+#endif
+template <bool SEEDED>
+__global__ __launch_bounds__(kKnnBlock, LIVO_GRID_WAVES) void k_knn_grid(KnnParams P) {
+    unsigned bjob, bx;
+    xcd_block(P.nb, bjob, bx);
+    const HsJob job = P.jobs[bjob];
+    IekfSlot* slot = job.slot;
+    if (P.force >= 0) {
+        if (!P.force) return;
+    } else {
+        if (slot->ctrl.stop) return;
+        if (SEEDED && !slot->ctrl.search_en) return;
+    }
+    const int i = (int)bx * kKnnBlock + threadIdx.x;
+    if (i >= job.n) return;
+    const float4* __restrict__ gpts = reinterpret_cast<const float4*>(P.gpts);
+    const GridSlot* __restrict__ slots = P.gslots;
+    LeafQuery q;
+    lq_init<SEEDED>(q, P, slot, job, i, true);
+    const float h = P.gh, inv = 1.0f / h, eps = P.geps;
+    const uint64_t mask = (1ull << P.glog2) - 1ull;
+    // query cell and the side of it the query lies in (dir = -1 / +1 per axis)
+    int c0, c1, c2, s0, s1, s2;
+    {
+        auto cell_of = [&](float v, float o, int& c, int& dir) {
+            const float t = (v - o) * inv;
+            float f = floorf(t);
+            f = fminf(fmaxf(f, (float)(8 - kGridBias)), (float)(kGridBias - 8));  // NaN -> 8 - bias
+            c = (int)f;
+            dir = (t - f < 0.5f) ? -1 : 1;
+        };
+        cell_of(q.qx, P.gorg[0], c0, s0);
+        cell_of(q.qy, P.gorg[1], c1, s1);
+        cell_of(q.qz, P.gorg[2], c2, s2);
+    }
+    unsigned visits = 0;
+    auto visit = [&](int cx, int cy, int cz) __attribute__((always_inline)) {
+        const float x0 = P.gorg[0] + (float)cx * h - eps, y0 = P.gorg[1] + (float)cy * h - eps;
+        const float z0 = P.gorg[2] + (float)cz * h - eps;
+        const float w = h + 2 * eps;
+        const float bd = box_dist(q.qx, q.qy, q.qz, x0, x0 + w, y0, y0 + w, z0, z0 + w);
+        if (bd - lq_thr(q) > kFuzz) return;
+        const unsigned long long key = grid_key_d(cx, cy, cz);
+        uint64_t sl = (uint64_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - P.glog2));
+        GridSlot gs = slots[sl];
+        visits++;
+        while (gs.key != key && gs.key != kGridEmpty) {  // linear probing (load factor <= 1/4)
+            sl = (sl + 1) & mask;
+            gs = slots[sl];
+        }
+        if (gs.key != key) return;
+        const int lo = (int)gs.start, hi = (int)(gs.start + gs.count);
+        for (int k0 = lo; k0 < hi; k0 += 4) {
+            float4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) v[u] = gpts[k0 + u];  // padded by 3 points
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (k0 + u < hi) lq_point(q, v[u], (uint32_t)(k0 + u));
+        }
+    };
+    // Cell boxes are int3 ranges [lo, hi]; a box with lo > hi is empty.
+    // scan_box visits the cells of `r` outside the skip box.
+    struct CBox { int l0, h0, l1, h1, l2, h2; };
+    auto inside = [](const CBox& b, int x, int y, int z) {
+        return x >= b.l0 && x <= b.h0 && y >= b.l1 && y <= b.h1 && z >= b.l2 && z <= b.h2;
+    };
+    auto scan_box = [&](const CBox& r, const CBox& skip) __attribute__((always_inline)) {
+#pragma unroll 1
+        for (int cz = r.l2; cz <= r.h2; cz++)
+#pragma unroll 1
+            for (int cy = r.l1; cy <= r.h1; cy++)
+#pragma unroll 1
+                for (int cx = r.l0; cx <= r.h0; cx++)
+                    if (!inside(skip, cx, cy, cz)) visit(cx, cy, cz);
+    };
+    // the cells that can hold a point within sqrt(t) (+ the fuzz, + the float
+    // slack of the cell assignment); false if that box is too large
+    auto range_of = [&](float t, CBox& r) {
+        const double rad = sqrt((double)t + 1e-9) * (1.0 + 1e-5) + (double)eps;
+        const double ih = 1.0 / (double)h;
+        const double lim = (double)(kGridBias - 8);
+        const double l0 = floor(((double)q.qx - rad - (double)P.gorg[0]) * ih), h0 = floor(((double)q.qx + rad - (double)P.gorg[0]) * ih);
+        const double l1 = floor(((double)q.qy - rad - (double)P.gorg[1]) * ih), h1 = floor(((double)q.qy + rad - (double)P.gorg[1]) * ih);
+        const double l2 = floor(((double)q.qz - rad - (double)P.gorg[2]) * ih), h2 = floor(((double)q.qz + rad - (double)P.gorg[2]) * ih);
+        if (!(fmax(fmax(fabs(l0), fabs(h0)), fmax(fmax(fabs(l1), fabs(h1)), fmax(fabs(l2), fabs(h2)))) < lim)) return false;
+        r = CBox{(int)l0, (int)h0, (int)l1, (int)h1, (int)l2, (int)h2};
+        return true;
+    };
+    bool certified = false;
+    if (P.lM > 0) {
+        // stage 0: the 2x2x2 block, own cell first
+#pragma unroll 1
+        for (int b = 0; b < 8; b++)
+            visit(c0 + ((b & 1) ? s0 : 0), c1 + ((b & 2) ? s1 : 0), c2 + ((b & 4) ? s2 : 0));
+        const CBox blk{c0 + min(s0, 0), c0 + max(s0, 0), c1 + min(s1, 0), c1 + max(s1, 0), c2 + min(s2, 0),
+                       c2 + max(s2, 0)};
+        const CBox cube{c0 - 1, c0 + 1, c1 - 1, c1 + 1, c2 - 1, c2 + 1};
+        // stage 1: within the 3x3x3 cube, the cells the current bound still
+        // reaches (all of them while fewer than 5 points are known)
+        CBox r1 = cube;
+        if (lq_thr(q) < INFINITY && range_of(lq_thr(q), r1)) {
+            r1.l0 = max(r1.l0, cube.l0); r1.h0 = min(r1.h0, cube.h0);
+            r1.l1 = max(r1.l1, cube.l1); r1.h1 = min(r1.h1, cube.h1);
+            r1.l2 = max(r1.l2, cube.l2); r1.h2 = min(r1.h2, cube.h2);
+        } else {
+            r1 = cube;
+        }
+        scan_box(r1, blk);
+        // still fewer than 5 points (sparse map): cubes of radius 2, 3, ...
+        CBox vis = cube;
+#pragma unroll 1
+        for (int rr = 2; rr <= kGridMaxRing && !(lq_thr(q) < INFINITY); rr++) {
+            const CBox nb{c0 - rr, c0 + rr, c1 - rr, c1 + rr, c2 - rr, c2 + rr};
+            scan_box(nb, vis);
+            vis = nb;
+        }
+        // stage 2: every cell the final bound reaches; the list is then exact.
+        // The bound only shrank, so the cells of `vis` it reaches are scanned
+        // (r1 / the block / the cubes; a cell skipped there was beyond the bound)
+        CBox r2;
+        const float t = lq_thr(q);
+        if (t < INFINITY && range_of(t, r2)) {
+            const double span = (double)(r2.h0 - r2.l0 + 1) * (double)(r2.h1 - r2.l1 + 1) * (double)(r2.h2 - r2.l2 + 1);
+            if (span <= (double)kGridMaxCells) {
+                scan_box(r2, vis);
+                certified = true;
+            }
+        }
+    }
+    lq_finish(q, P, job, bjob, i, gpts, !certified);
     count_visits(P, slot, visits);
 }
 
@@ -2047,6 +2242,21 @@ int launch_knn_leaf(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, 
         hipLaunchKernelGGL((k_knn_leaf<true, 1>), grid, block, lds, (hipStream_t)stream, q);
     else
         hipLaunchKernelGGL((k_knn_leaf<false, 1>), grid, block, lds, (hipStream_t)stream, q);
+    if (hipGetLastError() != hipSuccess) return LIVO_E_HIP;
+    hipLaunchKernelGGL(k_knn_replay, dim3(64), dim3(64), 0, (hipStream_t)stream, q);
+    return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+
+int launch_knn_grid(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, void* stream) {
+    if (n_jobs <= 0 || max_n <= 0) return LIVO_OK;
+    KnnParams q = p;
+    q.nb = (int32_t)((max_n + kKnnBlock - 1) / kKnnBlock);
+    if ((int64_t)q.nb * n_jobs >= (1ll << 31)) return LIVO_E_RANGE;
+    const dim3 grid((unsigned)(q.nb * n_jobs)), block(kKnnBlock);
+    if (seeded)
+        hipLaunchKernelGGL((k_knn_grid<true>), grid, block, 0, (hipStream_t)stream, q);
+    else
+        hipLaunchKernelGGL((k_knn_grid<false>), grid, block, 0, (hipStream_t)stream, q);
     if (hipGetLastError() != hipSuccess) return LIVO_E_HIP;
     hipLaunchKernelGGL(k_knn_replay, dim3(64), dim3(64), 0, (hipStream_t)stream, q);
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;

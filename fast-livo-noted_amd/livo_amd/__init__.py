@@ -131,6 +131,7 @@ SIGNATURES = {
     "livo_knn": (C.c_int, [_P, _P, C.c_int64, C.c_int32, _P, _P]),
     "livo_scan_upload": (C.c_int, [_P, _P, C.c_int64, C.c_int64, C.POINTER(C.c_int32)]),
     "livo_scan_release": (C.c_int, [_P, C.c_int32]),
+    "livo_scan_neighbors": (C.c_int, [_P, C.c_int32, _P, _P]),
     "livo_h_share": (C.c_int, [_P, C.c_int32, C.POINTER(State), C.c_int, _P, _P, C.POINTER(C.c_int64),
                                C.POINTER(PointOut)]),
     "livo_iekf_update": (C.c_int, [_P, C.c_int32, C.POINTER(State), C.POINTER(State), C.POINTER(IterStats)]),
@@ -275,6 +276,14 @@ class Context:
     def scan_release(self, sid: int):
         _check("livo_scan_release", self._L.livo_scan_release(self.h, sid))
         self.scans.pop(sid, None)
+
+    def scan_neighbors(self, sid: int):
+        """(idx (N, 5) int32, sqdist (N, 5) float32) of the scan's last search."""
+        n = self.scans[sid]
+        idx = np.empty((n, 5), np.int32)
+        d = np.empty((n, 5), np.float32)
+        _check("livo_scan_neighbors", self._L.livo_scan_neighbors(self.h, sid, _ptr(idx), _ptr(d)))
+        return idx, d
 
     # -------------------------------------------------------- hot path ----
     def h_share(self, sid: int, state: dict, search_en: bool = True, outputs: bool = True):

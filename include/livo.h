@@ -151,6 +151,13 @@ int livo_knn(livo_ctx* ctx, const float* q_xyz, int64_t n, int32_t k, int32_t* i
 int livo_scan_upload(livo_ctx* ctx, const float* xyz, int64_t N, int64_t stride_bytes, int32_t* scan_id);
 int livo_scan_release(livo_ctx* ctx, int32_t scan_id);
 
+/* The neighbour cache of a resident scan: the k = 5 nearest map points of each
+ * point from the last search on it (Nearest_Points, laser_mapping.h:165, in
+ * Nearest_Search's ascending PointType_CMP order, ikd_Tree.cpp:350-380).
+ * idx: N x 5 map indices (-1 pad); sqdist: N x 5 (+inf pad); either may be NULL.
+ * LIVO_E_NOSCAN if the scan was never searched. */
+int livo_scan_neighbors(livo_ctx* ctx, int32_t scan_id, int32_t* idx, float* sqdist);
+
 /* One h_share_model evaluation on a resident scan at the given state.
  * nearest_search_en != 0 runs the k-NN; otherwise the neighbours cached by the
  * last search on this scan are reused (Nearest_Points, laser_mapping.h:165).

@@ -316,6 +316,7 @@ def test_iekf_leaf_size(built, map100k, tree100k, leaf_size, monkeypatch):
     the oracle's answer."""
     import livo_amd
     synth = _synth()
+    monkeypatch.setenv("LIVO_KNN_KIND", "leaf")
     monkeypatch.setenv("LIVO_LEAF_SIZE", str(leaf_size))
     with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=4) as ctx:
         ctx.map_build(map100k)
@@ -327,11 +328,12 @@ def test_iekf_leaf_size(built, map100k, tree100k, leaf_size, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n_map", [5, 17, 100, 1000])
-def test_iekf_small_maps(built, n_map):
+def test_iekf_small_maps(built, n_map, monkeypatch):
     """Leaf maps of depth 0..6 (a single leaf up to many), IEKF against the oracle."""
     import livo_amd
     import oracle
     synth = _synth()
+    monkeypatch.setenv("LIVO_KNN_KIND", "leaf")
     m = synth.make_map(100_000)[:: 100_000 // n_map][:n_map].copy()
     body, _, _ = synth.make_scan(2_000, 6)
     st0 = synth.make_state(6)
@@ -387,3 +389,105 @@ def test_profiling_levels(ctx100k):
     finally:
         for sid in sids:
             ctx100k.scan_release(sid)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cell", [0.0, 0.05, 0.3, 2.0])
+def test_iekf_grid(built, map100k, tree100k, cell, monkeypatch):
+    """The cell-grid search (LIVO_KNN_KIND=grid; LIVO_GRID_CELL metres, 0: chosen
+    from the map) certifies the 5 nearest by ring distance and replays the rest
+    on the ikd-Tree; any cell size must give the oracle's answer."""
+    import livo_amd
+    synth = _synth()
+    monkeypatch.setenv("LIVO_KNN_KIND", "grid")
+    monkeypatch.setenv("LIVO_GRID_CELL", str(cell))
+    with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=4) as ctx:
+        ctx.map_build(map100k)
+        ctx.set_profiling(1)  # fills last_timings (replay count)
+        for scan_id in (3, 4):
+            body, _, _ = synth.make_scan(7_777, scan_id)
+            st0 = synth.make_state(scan_id)
+            _iekf_compare(ctx, tree100k, body, st0, 4, synth.T_LI)
+            t = ctx.last_timings()
+            if cell in (0.0, 0.3):  # the grid answers nearly every query itself
+                assert t["knn_replays"] <= 0.05 * t["knn_queries"], t
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_map", [5, 17, 1000])
+def test_iekf_grid_small_maps(built, n_map, monkeypatch):
+    """Cell grids of a handful of points: lists that never fill are replayed."""
+    import livo_amd
+    import oracle
+    synth = _synth()
+    monkeypatch.setenv("LIVO_KNN_KIND", "grid")
+    m = synth.make_map(100_000)[:: 100_000 // n_map][:n_map].copy()
+    body, _, _ = synth.make_scan(2_000, 6)
+    st0 = synth.make_state(6)
+    tree = oracle.Tree(m)
+    with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=4) as ctx:
+        ctx.map_build(m)
+        _iekf_compare(ctx, tree, body, st0, 4, synth.T_LI)
+
+
+@pytest.mark.gpu
+def test_grid_batch_equals_leaf(built, map100k, monkeypatch):
+    """Grid and leaf-map searches give bit-identical batched updates, including a
+    scan shifted 30 m off the map (queries beyond the ring limit: replayed)."""
+    import livo_amd
+    synth = _synth()
+    scans = [synth.make_scan(3000 + 211 * s, s)[0] for s in range(6)]
+    scans[5] = scans[5] + np.float32(30.0)
+    states = [synth.make_state(s) for s in range(6)]
+    out = {}
+    for kind in ("leaf", "grid"):
+        monkeypatch.setenv("LIVO_KNN_KIND", kind)
+        with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=4) as ctx:
+            ctx.map_build(map100k)
+            sids = [ctx.scan_upload(b) for b in scans]
+            out[kind] = ctx.iekf_update_batch(sids, states)
+    for i in range(6):
+        a, b = out["leaf"][0][i], out["grid"][0][i]
+        assert all(np.array_equal(a[k], b[k]) for k in a), i
+        assert out["leaf"][1][i]["iterations"] == out["grid"][1][i]["iterations"]
+
+
+def _tie_map(seed=7, n_base=20_000, n_q=2_000):
+    """Dyadic map + queries where each query has 2 or 4 map points at exactly the
+    same float distance (mirror pairs q +- v, q +- v' with v' = v with x, y swapped)."""
+    rng = np.random.default_rng(seed)
+    g = 2.0 ** -8
+    base = rng.integers(0, 16 * 256, size=(n_base, 3)) * g
+    q = rng.integers(256, 15 * 256, size=(n_q, 3)) * g
+    v = rng.integers(1, 4, size=(n_q, 3)) * rng.choice([-1, 1], size=(n_q, 3)) * g
+    v[:, 1] = np.sign(v[:, 1]) * ((np.abs(v[:, 0]) / g) % 3 + 1) * g  # |vx| != |vy|: distinct x
+    vp = v[:, [1, 0, 2]]
+    four = np.arange(n_q) % 2 == 0
+    extra = [q + v, q - v, (q + vp)[four], (q - vp)[four]]
+    m = np.concatenate([base] + extra).astype(np.float32)
+    return m, q.astype(np.float32)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["leaf", "grid"])
+def test_exact_ties_resolved_in_kernel(built, kind, monkeypatch):
+    """Exact distance ties inside the 5-NN list (distinct x) are ordered by
+    PointType_CMP's x rule in the batched search itself, without the replay; the
+    neighbour cache must equal the reference heap's Nearest_Search order."""
+    import livo_amd
+    import oracle
+    m, q = _tie_map()
+    monkeypatch.setenv("LIVO_KNN_KIND", kind)
+    st0 = {"rot": np.eye(3), "pos": np.zeros(3), "vel": np.zeros(3), "bias_g": np.zeros(3),
+           "bias_a": np.zeros(3), "gravity": np.array([0.0, 0.0, -9.81]), "cov": np.eye(18) * 1e-3}
+    with livo_amd.Context(0, t_LI=[0.0, 0.0, 0.0], max_iterations=0) as ctx:
+        ctx.map_build(m)
+        ctx.set_profiling(1)
+        sid = ctx.scan_upload(q)
+        ctx.iekf_update(sid, st0)  # one evaluation: the search at the identity pose
+        replays = ctx.last_timings()["knn_replays"]
+        idx_g, d_g = ctx.scan_neighbors(sid)
+    idx_r, d_r, _ = oracle.Tree(m).knn(q, 5)
+    np.testing.assert_array_equal(d_g, d_r)
+    np.testing.assert_array_equal(idx_g, idx_r)
+    assert replays <= 0.01 * len(q), replays
