@@ -63,7 +63,7 @@ def parse():
     ap.add_argument("--map-points", type=int, default=1_000_000)
     ap.add_argument("--max-iter", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0: skip)")
-    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01_pmc_summary.json"))
+    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01_pmc_summary_v4.json"))
     return ap.parse_args()
 
 

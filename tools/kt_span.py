@@ -23,7 +23,7 @@ def main(path, groups="4", skip="4"):
     items = []  # (start, end incl. following replay) per k_knn_leaf<false> dispatch
     for q, rs in by_q.items():
         for i, r in enumerate(rs):
-            if "k_knn_leaf<false>" in r["Kernel_Name"]:
+            if "k_knn_leaf<false>" in r["Kernel_Name"] or "k_knn_grid<false>" in r["Kernel_Name"]:
                 end = int(r["End_Timestamp"])
                 if i + 1 < len(rs) and "k_knn_replay" in rs[i + 1]["Kernel_Name"]:
                     end = int(rs[i + 1]["End_Timestamp"])
@@ -33,7 +33,7 @@ def main(path, groups="4", skip="4"):
     for b in range(skip, len(items) // groups):
         chunk = items[b * groups:(b + 1) * groups]
         spans.append(max(e for _, e, _ in chunk) - min(s for s, _, _ in chunk))
-    print(f"k_knn_leaf<false> dispatches: {len(items)}, mean dispatch {sum(durs) / len(durs) / 1e3:.1f} us")
+    print(f"first-search k-NN dispatches (leaf or grid): {len(items)}, mean dispatch {sum(durs) / len(durs) / 1e3:.1f} us")
     print(f"batches of {groups}: {len(spans)} (first {skip} skipped), mean first-eval k-NN span "
           f"{sum(spans) / len(spans) / 1e3:.1f} us (min {min(spans) / 1e3:.1f}, max {max(spans) / 1e3:.1f})")
 
