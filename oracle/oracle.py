@@ -97,6 +97,20 @@ def lib():
         L.orc_ikfom_update.argtypes = [P, P, C.c_int64, C.c_double, C.c_int, C.POINTER(OrcIkfomState),
                                        C.POINTER(OrcIkfomStats), P, C.c_int]
         L.orc_ikfom_mtk.argtypes = [C.c_int, P, P, P]
+        L.orc_ivox_create.restype = P
+        L.orc_ivox_create.argtypes = [C.c_float, C.c_int, C.c_int64]
+        L.orc_ivox_free.argtypes = [P]
+        L.orc_ivox_add_points.argtypes = [P, P, C.c_int64]
+        L.orc_ivox_info.argtypes = [P, P]
+        L.orc_ivox_knn.argtypes = [P, P, C.c_int64, C.c_int, C.c_double, P, P, P, P, C.c_int]
+        L.orc_ivox_dump.restype = C.c_int64
+        L.orc_ivox_dump.argtypes = [P, P, P, P, P]
+        L.orc_ivox_h_share.argtypes = [P, P, C.c_int64, P, P, P, P, C.c_int, C.c_double, P, P, P, P, P, P, P, P,
+                                       P, C.c_int]
+        L.orc_ivox_iekf_update.argtypes = [P, P, C.c_int64, P, P, C.c_double, C.c_int, C.POINTER(OrcState),
+                                           C.POINTER(OrcState), C.POINTER(OrcIterStats), P, P, P, P, C.c_int]
+        L.orc_ivox_map_incremental.argtypes = [P, P, C.c_int64, C.POINTER(OrcState), P, P, P, P, C.c_double,
+                                               C.c_int, P, P]
         del fp
         _lib = L
     return _lib
@@ -244,3 +258,116 @@ def esti_plane(pts5x3, threshold=0.1):
     out = np.zeros(4, np.float32)
     ok = lib().orc_esti_plane(_p(p), C.c_float(threshold), _p(out))
     return bool(ok), out
+
+
+def new_cache(n: int) -> dict:
+    """An empty neighbour cache (Nearest_Points, laser_mapping.h:165) for n points."""
+    return {"xyz": np.zeros((n, 15), np.float32), "cnt": np.zeros(n, np.int32),
+            "idx": np.full((n, 5), -1, np.int32), "d": np.zeros((n, 5), np.float32)}
+
+
+def resize_cache(cache: dict, n: int) -> dict:
+    """Nearest_Points.resize(n) (laser_mapping.cpp:165): entries below the old size are kept."""
+    out = new_cache(n)
+    m = min(n, cache["cnt"].shape[0])
+    for k in out:
+        out[k][:m] = cache[k][:m]
+    return out
+
+
+def _stats(st) -> dict:
+    ne = st.iterations
+    return {"iterations": ne, "knn_passes": st.knn_passes, "converged": st.converged,
+            "rematch_num": st.rematch_num, "effct_feat_num": [st.effct_feat_num[i] for i in range(ne)],
+            "solution": np.array([list(st.solution[i]) for i in range(ne)]),
+            "res_mean": [st.res_mean[i] for i in range(ne)]}
+
+
+class Ivox:
+    """faster_lio::IVox<3, DEFAULT, PointType> (ivox3d.h, ivox3d_node.hpp) restated with std containers."""
+
+    def __init__(self, resolution: float = 0.2, nearby_type: int = 18, capacity: int = 1_000_000):
+        self.h = lib().orc_ivox_create(C.c_float(resolution), nearby_type, capacity)
+        if not self.h:
+            raise ValueError("bad iVox options")
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.orc_ivox_free(self.h)
+            self.h = None
+
+    def add_points(self, xyz):
+        xyz = np.ascontiguousarray(xyz, np.float32).reshape(-1, 3)
+        lib().orc_ivox_add_points(self.h, _p(xyz), xyz.shape[0])
+
+    def info(self) -> dict:
+        c = np.zeros(3, np.int64)
+        lib().orc_ivox_info(self.h, _p(c))
+        return {"num_points": int(c[0]), "num_grids": int(c[1]), "ids_issued": int(c[2])}
+
+    def knn(self, q, max_num: int = 5, max_range: float = 5.0, threads: int = 8):
+        """idx, sqdist, xyz (n x max_num) and cnt (-1: nothing found, output untouched = pad)."""
+        q = np.ascontiguousarray(q, np.float32).reshape(-1, 3)
+        n = q.shape[0]
+        idx = np.full((n, max_num), -1, np.int32)
+        d = np.full((n, max_num), np.inf, np.float32)
+        xyz = np.zeros((n, max_num, 3), np.float32)
+        cnt = np.zeros(n, np.int32)
+        assert lib().orc_ivox_knn(self.h, _p(q), n, max_num, max_range, _p(idx), _p(d), _p(xyz), _p(cnt),
+                                  threads) == 0
+        return idx, d, xyz, cnt
+
+    def dump(self):
+        """Points grid by grid in LRU order (most recent first): xyz, id, grid ordinal; grid keys."""
+        n = lib().orc_ivox_dump(self.h, None, None, None, None)
+        g = self.info()["num_grids"]
+        xyz = np.zeros((n, 3), np.float32)
+        ids = np.zeros(n, np.int32)
+        keys = np.zeros((g, 3), np.int32)
+        gof = np.zeros(n, np.int32)
+        lib().orc_ivox_dump(self.h, _p(xyz), _p(ids), _p(keys), _p(gof))
+        return xyz, ids, gof, keys
+
+    def h_share(self, body, rot, pos, R_LI, t_LI, search_en, cache, lpc=0.001, threads=8):
+        body = np.ascontiguousarray(body, np.float32)
+        n = body.shape[0]
+        HTH = np.zeros(81)
+        HTL = np.zeros(9)
+        eff = np.zeros(1, np.int64)
+        nv = np.zeros((n, 4), np.float32)
+        sel = np.zeros(n, np.uint8)
+        args = [np.ascontiguousarray(a, np.float64) for a in (rot, pos, R_LI, t_LI)]
+        lib().orc_ivox_h_share(self.h, _p(body), n, *[_p(a) for a in args], int(bool(search_en)), lpc,
+                               _p(cache["xyz"]), _p(cache["cnt"]), _p(cache["idx"]), _p(cache["d"]), _p(HTH),
+                               _p(HTL), _p(eff), _p(nv), _p(sel), threads)
+        return {"HTH": HTH.reshape(9, 9), "HTL": HTL, "effct": int(eff[0]), "normvec": nv, "sel": sel,
+                "cache": cache}
+
+    def iekf_update(self, body, state: dict, cache: dict, prior: dict | None = None, R_LI=None, t_LI=None,
+                    max_iter: int = 4, lpc: float = 0.001, threads: int = 8):
+        cs = state_to_c(state)
+        pr = state_to_c(prior if prior is not None else state)
+        st = OrcIterStats()
+        body = np.ascontiguousarray(body, np.float32)
+        R_LI = np.ascontiguousarray(np.eye(3) if R_LI is None else R_LI, np.float64)
+        t_LI = np.ascontiguousarray(np.zeros(3) if t_LI is None else t_LI, np.float64)
+        rc = lib().orc_ivox_iekf_update(self.h, _p(body), body.shape[0], _p(R_LI), _p(t_LI), lpc, max_iter,
+                                        C.byref(cs), C.byref(pr), C.byref(st), _p(cache["xyz"]), _p(cache["cnt"]),
+                                        _p(cache["idx"]), _p(cache["d"]), threads)
+        assert rc == 0
+        return state_from_c(cs), _stats(st)
+
+    def map_incremental(self, body, state: dict, cache: dict, R_LI=None, t_LI=None,
+                        filter_size_map: float = 0.5, ekf_inited: bool = True):
+        """Returns the per-point category (0 skipped, 1 added, 2 added without downsampling) and counts."""
+        body = np.ascontiguousarray(body, np.float32)
+        n = body.shape[0]
+        cs = state_to_c(state)
+        R_LI = np.ascontiguousarray(np.eye(3) if R_LI is None else R_LI, np.float64)
+        t_LI = np.ascontiguousarray(np.zeros(3) if t_LI is None else t_LI, np.float64)
+        cat = np.zeros(n, np.uint8)
+        counts = np.zeros(2, np.int64)
+        lib().orc_ivox_map_incremental(self.h, _p(body), n, C.byref(cs), _p(R_LI), _p(t_LI), _p(cache["xyz"]),
+                                       _p(cache["cnt"]), filter_size_map, int(bool(ekf_inited)), _p(cat),
+                                       _p(counts))
+        return cat, {"added": int(counts[0]), "no_downsample": int(counts[1])}
