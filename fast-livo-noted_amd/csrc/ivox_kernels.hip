@@ -1,0 +1,421 @@
+// ivox_kernels.hip — CDNA4 (gfx950) kernels of the iVox backend and of
+// map_incremental.
+//
+//   k_ivox_knn<LATER, BIG>  IVox::GetClosestPoint(pt, closest, max_num,
+//                           max_range) (include/ivox3d/ivox3d.h:132-204) with
+//                           IVoxNode::KNNPointByCondition (ivox3d_node.hpp:
+//                           141-205) for every point of every scan: body->world
+//                           (laser_mapping.cpp:662-671), the nearby grids in
+//                           the reference's order, each grid's in-range points
+//                           in insertion order, libstdc++'s nth_element
+//                           restated (stl_select.h) so the survivors come out
+//                           in the reference's order, one 128-B NNRec per point.
+//                           One query per thread with a private candidate
+//                           array; a query that outgrows it (a grid with more
+//                           in-range points than kIvCap allows) is flagged and
+//                           recomputed by the BIG pass on a global-memory slice.
+//   k_iv_*                  IVox::AddPoints (ivox3d.h:256-281): grid keys
+//                           (Pos2Grid, :283-286) inserted into the hash, then
+//                           the CSR of grid runs rebuilt with the new points
+//                           appended to their grid in input order.
+//   k_map_incr              LaserMapping::map_incremental's per-point decision
+//                           (laser_mapping.cpp:343-380).
+//
+// Numerics as livo_kernels.hip: -ffp-contract=off, correctly rounded f32
+// division / sqrt, the reference's operation order (distance2 = Eigen's
+// unrolled squaredNorm of a Vector3f: d0^2 + (d1^2 + d2^2)).
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "device_common.h"
+#include "livo_internal.h"
+
+namespace livo {
+
+// NearbyType grids (ivox3d.h:211-235): NEARBY6 / 18 / 26 extend each other.
+__constant__ int c_nearby[kIvMaxNearby][3] = {
+    {0, 0, 0},   {-1, 0, 0}, {1, 0, 0},   {0, 1, 0},  {0, -1, 0},  {0, 0, -1}, {0, 0, 1},
+    {1, 1, 0},   {-1, 1, 0}, {1, -1, 0},  {-1, -1, 0}, {1, 0, 1},  {-1, 0, 1}, {1, 0, -1},
+    {-1, 0, -1}, {0, 1, 1},  {0, -1, 1},  {0, 1, -1}, {0, -1, -1}, {1, 1, 1},  {-1, 1, 1},
+    {1, -1, 1},  {1, 1, -1}, {-1, -1, 1}, {-1, 1, -1}, {1, -1, -1}, {-1, -1, -1}};
+
+__device__ __forceinline__ unsigned long long iv_key(int cx, int cy, int cz) {
+    return (unsigned long long)(cx + kIvBias) | ((unsigned long long)(cy + kIvBias) << 21) |
+           ((unsigned long long)(cz + kIvBias) << 42);
+}
+__device__ __forceinline__ uint64_t iv_hash(unsigned long long key, int log2) {
+    return (uint64_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - log2));
+}
+// Pos2Grid on one axis: round(v * inv_resolution) (float product, half away
+// from zero); false beyond `lim` cells (and for NaN).
+__device__ __forceinline__ bool iv_cell(float v, float inv, float lim, int& c) {
+    const float t = roundf(v * inv);
+    if (!(fabsf(t) <= lim)) return false;
+    c = (int)t;
+    return true;
+}
+// The grid's run {start, count} or count = 0.
+__device__ __forceinline__ uint2 iv_lookup(const GridSlot* __restrict__ slots, int log2, unsigned long long key) {
+    const uint64_t mask = (1ull << log2) - 1ull;
+    uint64_t sl = iv_hash(key, log2);
+    GridSlot gs = slots[sl];
+    while (gs.key != key && gs.key != kGridEmpty) {
+        sl = (sl + 1) & mask;
+        gs = slots[sl];
+    }
+    return gs.key == key ? make_uint2(gs.start, gs.count) : make_uint2(0u, 0u);
+}
+
+// ------------------------------------------------------------ search ----
+// GetClosestPoint into a[0..n): false with n = 0 when no candidate (the
+// caller's Nearest_Points entry then stays as it was, ivox3d.h:165-167);
+// overflow when a grid's in-range points do not fit in `cap`.
+template <class Arr>
+__device__ __forceinline__ int iv_query(const IvoxParams& V, float qx, float qy, float qz, Arr& a, int cap,
+                                        bool& overflow) {
+    overflow = false;
+    int kx, ky, kz;
+    const float qlim = (float)(kIvMaxKey + 8);  // beyond: no stored grid within one cell
+    if (!iv_cell(qx, V.inv_res, qlim, kx) || !iv_cell(qy, V.inv_res, qlim, ky) || !iv_cell(qz, V.inv_res, qlim, kz))
+        return 0;
+    const float4* __restrict__ pts = reinterpret_cast<const float4*>(V.pts);
+    const int K = V.max_num;
+    int n = 0;
+#pragma unroll 1
+    for (int t = 0; t < V.nearby; t++) {
+        const uint2 run = iv_lookup(V.slots, V.log2, iv_key(kx + c_nearby[t][0], ky + c_nearby[t][1], kz + c_nearby[t][2]));
+        const int old = n;
+#pragma unroll 1
+        for (uint32_t k = 0; k < run.y; k++) {
+            const float4 v = pts[run.x + k];
+            const float dx = v.x - qx, dy = v.y - qy, dz = v.z - qz;
+            const float d = dx * dx + (dy * dy + dz * dz);  // distance2, ivox3d_node.hpp:12-16
+            if ((double)d < V.range2) {
+                if (n >= cap) {
+                    overflow = true;
+                    return 0;
+                }
+                a[n] = SelElem{d, run.x + k};
+                n++;
+            }
+        }
+        // KNNPointByCondition (ivox3d_node.hpp:179-183)
+        if (!(old + K >= n)) {
+            sel_nth_element(a, old, old + K - 1, n);
+            n = old + K;
+        }
+    }
+    if (n == 0) return 0;
+    if (n > K) {  // ivox3d.h:173-177
+        sel_nth_element(a, 0, K - 1, n);
+        n = K;
+    }
+    sel_nth_element(a, 0, 0, n);  // ivox3d.h:178
+    return n;
+}
+
+template <class Arr>
+__device__ __forceinline__ void iv_write(NNRec* __restrict__ out, const float4* __restrict__ pts, const Arr& a,
+                                         int n) {
+    float4* o4 = reinterpret_cast<float4*>(out);
+    int32_t idx[kNN], node[kNN];
+#pragma unroll
+    for (int k = 0; k < kNN; k++) {
+        float4 v = make_float4(0.f, 0.f, 0.f, INFINITY);
+        idx[k] = -1;
+        node[k] = -1;
+        if (k < n) {
+            const float4 p = pts[a[k].id];
+            v = make_float4(p.x, p.y, p.z, a[k].d);
+            idx[k] = __float_as_int(p.w);
+            node[k] = (int32_t)a[k].id;
+        }
+        o4[k] = v;
+    }
+    int4* oi = reinterpret_cast<int4*>(out) + 5;
+    oi[0] = make_int4(idx[0], idx[1], idx[2], idx[3]);
+    oi[1] = make_int4(idx[4], n, 0, node[0]);
+    oi[2] = make_int4(node[1], node[2], node[3], node[4]);
+}
+
+__device__ __forceinline__ void iv_world(const KnnParams& P, const IekfSlot* slot, const float4 b, float& qx,
+                                         float& qy, float& qz) {
+    if (P.identity) {
+        qx = b.x; qy = b.y; qz = b.z;
+    } else {
+        world_point(slot->state.rot, slot->state.pos, P.R_LI, P.t_LI, b.x, b.y, b.z, qx, qy, qz);
+    }
+}
+
+// LATER: an evaluation after the first (searches only where the scan's
+// device-side nearest_search_en is set).  BIG: the overflow pass over the
+// flagged queries (grid-stride, one global-memory slice per thread).
+template <bool LATER>
+__global__ __launch_bounds__(kKnnBlock) void k_ivox_knn(KnnParams P) {
+    unsigned bjob, bx;
+    xcd_block(P.nb, bjob, bx);
+    const HsJob job = P.jobs[bjob];
+    const IekfSlot* slot = job.slot;
+    if (P.force >= 0) {
+        if (!P.force) return;
+    } else {
+        if (slot->ctrl.stop) return;
+        if (LATER && !slot->ctrl.search_en) return;
+    }
+    const int i = (int)bx * kKnnBlock + threadIdx.x;
+    if (i >= job.n) return;
+    const float4 b = reinterpret_cast<const float4*>(job.pts)[i];
+    float qx, qy, qz;
+    iv_world(P, slot, b, qx, qy, qz);
+    SelElem a[kIvCap];
+    bool overflow;
+    const int n = iv_query(P.iv, qx, qy, qz, a, kIvCap, overflow);
+    if (overflow) {
+        const unsigned r = atomicAdd(P.replay_count, 1u);
+        P.replay_list[r] = ((unsigned long long)bjob << 32) | (unsigned)i;
+        return;
+    }
+    if (n > 0) iv_write(job.nn + i, reinterpret_cast<const float4*>(P.iv.pts), a, n);
+}
+
+__global__ __launch_bounds__(64) void k_ivox_knn_big(KnnParams P) {
+    const unsigned cnt = *P.replay_count;
+    const unsigned tid = blockIdx.x * blockDim.x + threadIdx.x;
+    SelElem* a = P.iv.scratch + (int64_t)tid * P.iv.slice;
+    for (unsigned r = tid; r < cnt; r += gridDim.x * blockDim.x) {
+        const unsigned long long e = P.replay_list[r];
+        const unsigned bjob = (unsigned)(e >> 32);
+        const int i = (int)(e & 0xFFFFFFFFu);
+        const HsJob job = P.jobs[bjob];
+        const float4 b = reinterpret_cast<const float4*>(job.pts)[i];
+        float qx, qy, qz;
+        iv_world(P, job.slot, b, qx, qy, qz);
+        bool overflow;
+        const int n = iv_query(P.iv, qx, qy, qz, a, (int)P.iv.slice, overflow);
+        if (overflow) {  // cannot happen: slice >= nearby * max_num + the largest grid
+            atomicOr(P.iv.ctr, 2ull);
+            continue;
+        }
+        if (n > 0) iv_write(job.nn + i, reinterpret_cast<const float4*>(P.iv.pts), a, n);
+    }
+}
+
+int launch_ivox_knn(const KnnParams& p, int n_jobs, int64_t max_n, bool later, int64_t overflow_threads,
+                    void* stream) {
+    if (n_jobs <= 0 || max_n <= 0) return LIVO_OK;
+    KnnParams q = p;
+    q.nb = (int32_t)((max_n + kKnnBlock - 1) / kKnnBlock);
+    if ((int64_t)q.nb * n_jobs >= (1ll << 31)) return LIVO_E_RANGE;
+    const dim3 grid((unsigned)(q.nb * n_jobs)), block(kKnnBlock);
+    if (later)
+        hipLaunchKernelGGL((k_ivox_knn<true>), grid, block, 0, (hipStream_t)stream, q);
+    else
+        hipLaunchKernelGGL((k_ivox_knn<false>), grid, block, 0, (hipStream_t)stream, q);
+    if (hipGetLastError() != hipSuccess) return LIVO_E_HIP;
+    const unsigned blocks = (unsigned)std::max<int64_t>(1, overflow_threads / 64);
+    hipLaunchKernelGGL(k_ivox_knn_big, dim3(blocks), dim3(64), 0, (hipStream_t)stream, q);
+    return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+
+// --------------------------------------------------------- AddPoints ----
+__global__ void k_iv_clear(GridSlot* slots, int64_t table) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < table) slots[s] = GridSlot{kGridEmpty, 0u, 0u};
+}
+
+// Each point's grid key found or inserted (CAS on the key); new grids counted.
+__global__ void k_iv_insert(IvoxParams P) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n_src) return;
+    P.iota[i] = (uint32_t)i;
+    const float4 p = reinterpret_cast<const float4*>(P.src)[i];
+    int cx, cy, cz;
+    const float lim = (float)kIvMaxKey;
+    if (!iv_cell(p.x, P.inv_res, lim, cx) || !iv_cell(p.y, P.inv_res, lim, cy) || !iv_cell(p.z, P.inv_res, lim, cz)) {
+        P.slot_of[i] = (uint32_t)P.table;  // sorts last, never placed
+        atomicOr(P.ctr, 1ull);
+        return;
+    }
+    const unsigned long long key = iv_key(cx, cy, cz);
+    const uint64_t mask = (uint64_t)P.table - 1ull;
+    uint64_t sl = iv_hash(key, P.log2);
+    while (true) {
+        unsigned long long cur = __hip_atomic_load(&P.slots[sl].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == kGridEmpty) {
+            cur = atomicCAS(&P.slots[sl].key, kGridEmpty, key);
+            if (cur == kGridEmpty) {
+                atomicAdd(P.ctr + 1, 1ull);
+                break;
+            }
+        }
+        if (cur == key) break;
+        sl = (sl + 1) & mask;
+    }
+    P.slot_of[i] = (uint32_t)sl;
+    atomicAdd(P.addcnt + sl, 1u);
+}
+
+// The batch's new grids removed again (capacity reached): a new grid is a
+// used slot with no points yet; every slot it could shadow was filled before.
+__global__ void k_iv_rollback(IvoxParams P) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= P.table) return;
+    if (P.slots[s].key != kGridEmpty && P.slots[s].count == 0u) P.slots[s] = GridSlot{kGridEmpty, 0u, 0u};
+    P.addcnt[s] = 0u;
+}
+
+__global__ void k_iv_prepare(IvoxParams P) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= P.table) return;
+    P.tot[s] = (P.slots[s].key != kGridEmpty ? P.slots[s].count : 0u) + P.addcnt[s];
+}
+
+// Old runs moved to their new start (one thread per grid).
+__global__ void k_iv_move(IvoxParams P) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= P.table) return;
+    const GridSlot g = P.slots[s];
+    if (g.key == kGridEmpty || g.count == 0u) return;
+    const float4* __restrict__ src = reinterpret_cast<const float4*>(P.pts) + g.start;
+    float4* __restrict__ dst = reinterpret_cast<float4*>(P.npts) + P.newstart[s];
+    for (uint32_t k = 0; k < g.count; k++) dst[k] = src[k];
+}
+
+// New points appended to their grid's run in input order: the batch sorted by
+// slot (stable) gives each point its rank inside its grid.
+__global__ void k_iv_place(IvoxParams P) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= P.n_src) return;
+    const uint32_t sl = P.skeys[k];
+    if ((int64_t)sl >= P.table) return;
+    const uint32_t i = P.svals[k];
+    const uint32_t rank = (uint32_t)k - P.addstart[sl];
+    const float4 p = reinterpret_cast<const float4*>(P.src)[i];
+    const uint32_t id = (uint32_t)(P.base_id + (int64_t)i);
+    reinterpret_cast<float4*>(P.npts)[P.newstart[sl] + P.slots[sl].count + rank] =
+        make_float4(p.x, p.y, p.z, __uint_as_float(id));
+}
+
+__global__ void k_iv_fix(IvoxParams P) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= P.table) return;
+    GridSlot g = P.slots[s];
+    if (g.key == kGridEmpty) return;
+    g.start = P.newstart[s];
+    g.count += P.addcnt[s];
+    P.slots[s] = g;
+    P.addcnt[s] = 0u;
+    atomicMax(P.ctr + 2, (unsigned long long)g.count);
+}
+
+__global__ void k_iv_rehash(const GridSlot* __restrict__ old_slots, int64_t old_table, GridSlot* slots, int log2) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= old_table) return;
+    const GridSlot g = old_slots[s];
+    if (g.key == kGridEmpty) return;
+    const uint64_t mask = (1ull << log2) - 1ull;
+    uint64_t sl = iv_hash(g.key, log2);
+    while (atomicCAS(&slots[sl].key, kGridEmpty, g.key) != kGridEmpty) sl = (sl + 1) & mask;
+    slots[sl].start = g.start;
+    slots[sl].count = g.count;
+}
+
+static inline dim3 blocks_for(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }
+
+#define LAUNCH_CHECKED(kernel, n, ...)                                                         \
+    do {                                                                                       \
+        if ((n) <= 0) return LIVO_OK;                                                          \
+        hipLaunchKernelGGL(kernel, blocks_for(n), dim3(256), 0, (hipStream_t)stream, __VA_ARGS__); \
+        return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;                         \
+    } while (0)
+
+int launch_ivox_clear(GridSlot* slots, int64_t table, void* stream) { LAUNCH_CHECKED(k_iv_clear, table, slots, table); }
+int launch_ivox_insert(const IvoxParams& p, void* stream) { LAUNCH_CHECKED(k_iv_insert, p.n_src, p); }
+int launch_ivox_rollback(const IvoxParams& p, void* stream) { LAUNCH_CHECKED(k_iv_rollback, p.table, p); }
+int launch_ivox_prepare(const IvoxParams& p, void* stream) { LAUNCH_CHECKED(k_iv_prepare, p.table, p); }
+int launch_ivox_move(const IvoxParams& p, void* stream) { LAUNCH_CHECKED(k_iv_move, p.table, p); }
+int launch_ivox_place(const IvoxParams& p, void* stream) { LAUNCH_CHECKED(k_iv_place, p.n_src, p); }
+int launch_ivox_fix(const IvoxParams& p, void* stream) { LAUNCH_CHECKED(k_iv_fix, p.table, p); }
+int launch_ivox_rehash(const GridSlot* old_slots, int64_t old_table, GridSlot* slots, int log2, void* stream) {
+    LAUNCH_CHECKED(k_iv_rehash, old_table, old_slots, old_table, slots, log2);
+}
+
+// ---------------------------------------------------- map_incremental ----
+// laser_mapping.cpp:343-380 for one point (stored position j).
+__global__ void k_map_incr(MapIncrParams P) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= P.n) return;
+    const float4 b = reinterpret_cast<const float4*>(P.pts)[j];
+    float pw[3];
+    world_point(P.slot->state.rot, P.slot->state.pos, P.R_LI, P.t_LI, b.x, b.y, b.z, pw[0], pw[1], pw[2]);
+    const NNRec& r = P.nn[j];
+    const int cnt = r.cnt;
+    int cat = 1;
+    if (cnt > 0 && P.ekf_inited) {
+        const float fs = (float)P.fs;  // Eigen promotes the double scalar to float
+        float c[3];
+#pragma unroll
+        for (int a = 0; a < 3; a++) c[a] = (floorf(pw[a] / fs) + 0.5f) * fs;
+        const double half = 0.5 * P.fs;
+        if ((double)fabsf(r.p[0][0] - c[0]) > half && (double)fabsf(r.p[0][1] - c[1]) > half &&
+            (double)fabsf(r.p[0][2] - c[2]) > half) {
+            cat = 2;
+        } else {
+            // common::calc_dist(Vector3f, Vector3f) = (p1 - p2).norm() (common_lib.h:85)
+            auto norm3 = [&](float x, float y, float z) {
+                const float u = x - c[0], v = y - c[1], w = z - c[2];
+                return sqrtf(u * u + (v * v + w * w));
+            };
+            const float dist = norm3(pw[0], pw[1], pw[2]);
+            bool need_add = true;
+            if (cnt >= kNN)
+#pragma unroll
+                for (int k = 0; k < kNN; k++)
+                    if (need_add && (double)norm3(r.p[k][0], r.p[k][1], r.p[k][2]) < (double)dist + 1e-6)
+                        need_add = false;
+            cat = need_add ? 1 : 0;
+        }
+    }
+    if (P.cat) P.cat[j] = (uint8_t)cat;
+    if (cat) {
+        const int64_t pos = (cat == 1 ? 0 : (int64_t)P.n) + P.perm[j];
+        reinterpret_cast<float4*>(P.ordered)[pos] = make_float4(pw[0], pw[1], pw[2], 0.f);
+        P.flags[pos] = 1u;
+    }
+}
+
+int launch_map_incr(const MapIncrParams& p, void* stream) {
+    if (p.n <= 0) return LIVO_OK;
+    hipLaunchKernelGGL(k_map_incr, blocks_for(p.n), dim3(256), 0, (hipStream_t)stream, p);
+    return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+
+__global__ void k_compact(const float4* __restrict__ ordered, const uint32_t* __restrict__ flags,
+                          const uint32_t* __restrict__ pos, int64_t n, float4* __restrict__ dense) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n && flags[k]) dense[pos[k]] = ordered[k];
+}
+
+int launch_compact(const float* ordered, const uint32_t* flags, const uint32_t* pos, int64_t n, float* dense,
+                   void* stream) {
+    LAUNCH_CHECKED(k_compact, n, reinterpret_cast<const float4*>(ordered), flags, pos, n,
+                   reinterpret_cast<float4*>(dense));
+}
+
+__global__ void k_inherit_nn(NNRec* dst, const int32_t* dst_perm, int64_t n_dst, const NNRec* src,
+                             const int32_t* src_iperm, int64_t n_src) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_dst) return;
+    const int64_t o = dst_perm[j];
+    const int4* s = o < n_src ? reinterpret_cast<const int4*>(src + src_iperm[o]) : nullptr;
+    int4* d = reinterpret_cast<int4*>(dst + j);
+#pragma unroll
+    for (int k = 0; k < 8; k++) d[k] = s ? s[k] : make_int4(0, 0, 0, 0);
+}
+
+int launch_inherit_nn(NNRec* dst, const int32_t* dst_perm, int64_t n_dst, const NNRec* src,
+                      const int32_t* src_iperm, int64_t n_src, void* stream) {
+    LAUNCH_CHECKED(k_inherit_nn, n_dst, dst, dst_perm, n_dst, src, src_iperm, n_src);
+}
+
+}  // namespace livo

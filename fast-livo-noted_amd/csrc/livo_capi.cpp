@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -30,6 +31,8 @@ struct ScanBuf {
     float* pts = nullptr;  // n x 4
     NNRec* nn = nullptr;   // neighbour records (Nearest_Points cache)
     std::vector<int32_t> perm;  // stored (Morton) position -> caller's point index
+    int32_t* d_perm = nullptr;  // the same on the device
+    int32_t* d_iperm = nullptr; // caller's point index -> stored position
     double* partial = nullptr;  // nblk x kIkCols (the A-path uses kRedCols of each)
     bool searched = false;      // a search has filled the neighbour cache
 };
@@ -52,6 +55,32 @@ static void dev_free(T*& p) {
 }
 
 }  // namespace
+
+// The device iVox map and its AddPoints / overflow-pass scratch.
+struct IvoxDev {
+    bool ready = false;
+    livo_ivox_params prm{};
+    float inv_res = 5.0f;
+    int nearby = 19;
+    GridSlot* slots = nullptr;
+    int32_t log2 = 0;
+    int64_t table = 0;
+    uint32_t *addcnt = nullptr, *tot = nullptr, *newstart = nullptr, *addstart = nullptr;
+    float* pts[2] = {nullptr, nullptr};  // CSR double buffer (4 floats per point)
+    int64_t pts_cap[2] = {0, 0};
+    int cur = 0;
+    int64_t npts = 0, ngrids = 0, next_id = 0, max_grid = 0;
+    unsigned long long* ctr = nullptr;   // [0] error bits, [1] new grids, [2] max grid
+    // batch temporaries
+    float* src = nullptr;
+    uint32_t *slot_of = nullptr, *iota = nullptr, *skeys = nullptr, *svals = nullptr;
+    int64_t src_cap = 0;
+    void* prim_tmp = nullptr;
+    size_t prim_bytes = 0;
+    // overflow pass of the search
+    SelElem* big = nullptr;
+    int64_t big_threads = 0, big_slice = 0;
+};
 
 struct livo_ctx {
     int device = 0;
@@ -81,6 +110,8 @@ struct livo_ctx {
     int32_t glog2 = 0;
     int64_t grid_bytes = 0;
     bool has_map = false;
+    int backend = LIVO_BACKEND_IKDTREE;  // search structure of h_share / the IEKF loop
+    IvoxDev iv;                        // iVox map (LIVO_BACKEND_IVOX)
     // scans
     std::vector<ScanBuf> scans;
     // batch resources
@@ -159,6 +190,8 @@ static int ensure_replay(livo_ctx* c, int64_t total) {
     return LIVO_OK;
 }
 
+static IvoxParams ivox_params(livo_ctx* c);
+
 static KnnParams make_knn_params(livo_ctx* c) {
     KnnParams kp{};
     kp.nodes = c->nodes;
@@ -182,6 +215,7 @@ static KnnParams make_knn_params(livo_ctx* c) {
     kp.geps = c->geps;
     kp.glog2 = c->glog2;
     kp.identity = 0;
+    kp.iv = ivox_params(c);
     return kp;
 }
 
@@ -232,7 +266,8 @@ static HsParams make_hs_params(livo_ctx* c) {
     hp.lpc = c->params.laser_point_cov;
     hp.max_res = c->params.max_residual;
     hp.plane_thr = c->params.plane_threshold;
-    hp.max_sqd = c->params.max_nn_sqdist;
+    // the iVox branch has no sqdist gate (laser_mapping.cpp:519-525)
+    hp.max_sqd = c->backend == LIVO_BACKEND_IVOX ? INFINITY : c->params.max_nn_sqdist;
     hp.force = -1;
     return hp;
 }
@@ -278,6 +313,199 @@ static int create_group_streams(livo_ctx* c) {
     return 0;
 }
 
+
+// ------------------------------------------------------------------ iVox --
+static void ivox_free(IvoxDev& v) {
+    dev_free(v.slots);
+    dev_free(v.addcnt); dev_free(v.tot); dev_free(v.newstart); dev_free(v.addstart);
+    dev_free(v.pts[0]); dev_free(v.pts[1]);
+    dev_free(v.ctr);
+    dev_free(v.src); dev_free(v.slot_of); dev_free(v.iota); dev_free(v.skeys); dev_free(v.svals);
+    if (v.prim_tmp) (void)hipFree(v.prim_tmp);
+    dev_free(v.big);
+    v = IvoxDev{};
+}
+
+// Hash table with room for `grids` grids at load factor <= 1/2 (rehash on growth).
+static int ivox_ensure_table(livo_ctx* c, int64_t grids) {
+    IvoxDev& v = c->iv;
+    if (v.table >= 2 * grids && v.table > 0) return LIVO_OK;
+    int log2 = 10;
+    while (((int64_t)1 << log2) < 4 * grids) log2++;
+    if (log2 > 31) return LIVO_E_RANGE;
+    const int64_t table = (int64_t)1 << log2;
+    GridSlot* slots = nullptr;
+    if (dev_alloc(&slots, (size_t)table)) return LIVO_E_OOM;
+    int rc = launch_ivox_clear(slots, table, c->stream);
+    if (!rc && v.slots) rc = launch_ivox_rehash(v.slots, v.table, slots, log2, c->stream);
+    if (rc) {
+        dev_free(slots);
+        return rc;
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    dev_free(v.slots);
+    dev_free(v.addcnt); dev_free(v.tot); dev_free(v.newstart); dev_free(v.addstart);
+    v.slots = slots;
+    v.table = table;
+    v.log2 = log2;
+    if (dev_alloc(&v.addcnt, table) || dev_alloc(&v.tot, table) || dev_alloc(&v.newstart, table) ||
+        dev_alloc(&v.addstart, table))
+        return LIVO_E_OOM;
+    HIP_TRY(hipMemsetAsync(v.addcnt, 0, (size_t)table * sizeof(uint32_t), c->stream));
+    return LIVO_OK;
+}
+
+static int ivox_ensure_src(livo_ctx* c, int64_t n) {
+    IvoxDev& v = c->iv;
+    if (n <= v.src_cap) return LIVO_OK;
+    const int64_t cap = std::max<int64_t>(n, 4096);
+    dev_free(v.src); dev_free(v.slot_of); dev_free(v.iota); dev_free(v.skeys); dev_free(v.svals);
+    v.src_cap = 0;
+    if (dev_alloc(&v.src, (size_t)cap * 4) || dev_alloc(&v.slot_of, cap) || dev_alloc(&v.iota, cap) ||
+        dev_alloc(&v.skeys, cap) || dev_alloc(&v.svals, cap))
+        return LIVO_E_OOM;
+    v.src_cap = cap;
+    return LIVO_OK;
+}
+
+static int ivox_ensure_prim(livo_ctx* c, size_t bytes) {
+    IvoxDev& v = c->iv;
+    if (bytes <= v.prim_bytes) return LIVO_OK;
+    if (v.prim_tmp) (void)hipFree(v.prim_tmp);
+    v.prim_tmp = nullptr;
+    v.prim_bytes = 0;
+    if (hipMalloc(&v.prim_tmp, bytes) != hipSuccess) return LIVO_E_OOM;
+    v.prim_bytes = bytes;
+    return LIVO_OK;
+}
+
+// Exclusive scan of n u32 through rocPRIM (out != in).
+static int ivox_scan(livo_ctx* c, const uint32_t* in, uint32_t* out, int64_t n) {
+    size_t tb = 0;
+    int rc = prim_exclusive_scan_u32(nullptr, &tb, in, out, n, c->stream);
+    if (!rc) rc = ivox_ensure_prim(c, tb);
+    tb = c->iv.prim_bytes;
+    if (!rc) rc = prim_exclusive_scan_u32(c->iv.prim_tmp, &tb, in, out, n, c->stream);
+    return rc;
+}
+
+static IvoxParams ivox_params(livo_ctx* c) {
+    IvoxDev& v = c->iv;
+    IvoxParams P{};
+    P.slots = v.slots;
+    P.pts = v.pts[v.cur];
+    P.npts = v.pts[1 - v.cur];
+    P.src = v.src;
+    P.table = v.table;
+    P.addcnt = v.addcnt;
+    P.tot = v.tot;
+    P.newstart = v.newstart;
+    P.addstart = v.addstart;
+    P.slot_of = v.slot_of;
+    P.iota = v.iota;
+    P.skeys = v.skeys;
+    P.svals = v.svals;
+    P.ctr = v.ctr;
+    P.base_id = v.next_id;
+    P.inv_res = v.inv_res;
+    P.log2 = v.log2;
+    P.nearby = v.nearby;
+    P.max_num = kNN;
+    P.range2 = 5.0 * 5.0;  // GetClosestPoint's default max_range (ivox3d.h:79), laser_mapping.cpp:520
+    P.scratch = v.big;
+    P.slice = v.big_slice;
+    return P;
+}
+
+// Overflow-pass scratch: a slice holds every candidate one query can hold at once.
+static int ivox_ensure_big(livo_ctx* c) {
+    IvoxDev& v = c->iv;
+    const int64_t slice = (int64_t)v.nearby * kNN + v.max_grid + 8;
+    if (slice <= v.big_slice && v.big) return LIVO_OK;
+    const int64_t budget = (int64_t)1 << 30;  // 1 GiB
+    int64_t threads = budget / (slice * (int64_t)sizeof(SelElem));
+    threads = std::max<int64_t>(64, std::min<int64_t>(16384, threads)) / 64 * 64;
+    dev_free(v.big);
+    v.big_slice = 0;
+    v.big_threads = 0;
+    if (dev_alloc(&v.big, (size_t)(threads * slice))) return LIVO_E_OOM;
+    v.big_slice = slice;
+    v.big_threads = threads;
+    return LIVO_OK;
+}
+
+// IVox::AddPoints of the n points in v.src (insertion order), on the device.
+static int ivox_add_dev(livo_ctx* c, int64_t n) {
+    IvoxDev& v = c->iv;
+    if (n == 0) return LIVO_OK;
+    if (v.npts + n > (int64_t)0xFFFFFFFF || v.next_id + n > (int64_t)0x7FFFFFFF) return LIVO_E_RANGE;
+    int rc = ivox_ensure_table(c, v.ngrids + n);
+    if (rc) return rc;
+    HIP_TRY(hipMemsetAsync(v.ctr, 0, 3 * sizeof(unsigned long long), c->stream));
+    IvoxParams P = ivox_params(c);
+    P.n_src = n;
+    rc = launch_ivox_insert(P, c->stream);
+    if (rc) return rc;
+    unsigned long long ctr[3];
+    HIP_TRY(hipMemcpyAsync(ctr, v.ctr, sizeof(ctr), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    // the largest size the grid map reaches is ngrids + new grids: the LRU
+    // eviction (ivox3d.h:271-274) happens iff that reaches the capacity
+    const bool full = v.ngrids + (int64_t)ctr[1] >= v.prm.capacity;
+    if ((ctr[0] & 1ull) || full) {
+        rc = launch_ivox_rollback(P, c->stream);
+        if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = LIVO_E_HIP;
+        return rc ? rc : ((ctr[0] & 1ull) ? LIVO_E_RANGE : LIVO_E_CAPACITY);
+    }
+    // new CSR buffer
+    const int other = 1 - v.cur;
+    const int64_t need = v.npts + n + 3;
+    if (v.pts_cap[other] < need) {
+        dev_free(v.pts[other]);
+        v.pts_cap[other] = 0;
+        const int64_t cap = std::max<int64_t>(need + need / 2, 1 << 16);
+        if (dev_alloc(&v.pts[other], (size_t)cap * 4)) return LIVO_E_OOM;
+        v.pts_cap[other] = cap;
+        P.npts = v.pts[other];
+    }
+    rc = launch_ivox_prepare(P, c->stream);
+    if (!rc) rc = ivox_scan(c, v.tot, v.newstart, v.table);
+    if (!rc) rc = ivox_scan(c, v.addcnt, v.addstart, v.table);
+    if (!rc) {
+        int bits = 1;
+        while (((int64_t)1 << bits) <= v.table) bits++;  // the out-of-range key `table` included
+        size_t tb = 0;
+        rc = prim_sort_pairs_u32(nullptr, &tb, v.slot_of, v.skeys, v.iota, v.svals, n, bits, c->stream);
+        if (!rc) rc = ivox_ensure_prim(c, tb);
+        tb = v.prim_bytes;
+        if (!rc) rc = prim_sort_pairs_u32(v.prim_tmp, &tb, v.slot_of, v.skeys, v.iota, v.svals, n, bits, c->stream);
+    }
+    if (!rc) rc = launch_ivox_move(P, c->stream);
+    if (!rc) rc = launch_ivox_place(P, c->stream);
+    if (!rc) rc = launch_ivox_fix(P, c->stream);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(ctr, v.ctr, sizeof(ctr), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    v.cur = other;
+    v.npts += n;
+    v.ngrids += (int64_t)ctr[1];
+    v.next_id += n;
+    v.max_grid = (int64_t)ctr[2];
+    return ivox_ensure_big(c);
+}
+
+static bool map_ready(const livo_ctx* c) {
+    return c->backend == LIVO_BACKEND_IVOX ? c->iv.ready : c->has_map;
+}
+
+// The search of one evaluation with the context's backend (+ its exact /
+// overflow pass); `later`: an evaluation after the first (seeded / gated).
+static int backend_knn(livo_ctx* c, const KnnParams& kp, int n_jobs, int64_t max_n, bool later, hipStream_t st) {
+    if (c->backend == LIVO_BACKEND_IVOX) return launch_ivox_knn(kp, n_jobs, max_n, later, c->iv.big_threads, st);
+    return c->knn_kind == 1 ? launch_knn_grid(kp, n_jobs, max_n, later, st)
+                            : launch_knn_leaf(kp, n_jobs, max_n, later, st);
+}
+
 extern "C" {
 
 int livo_abi_version(void) { return LIVO_ABI_VERSION; }
@@ -291,6 +519,7 @@ const char* livo_error_string(int code) {
         case LIVO_E_NOSCAN: return "unknown scan id";
         case LIVO_E_OOM: return "device allocation failed";
         case LIVO_E_RANGE: return "size out of supported range";
+        case LIVO_E_CAPACITY: return "iVox grid capacity reached (LRU eviction is not done on the device)";
         default: return "unknown error";
     }
 }
@@ -350,7 +579,9 @@ int livo_ctx_destroy(livo_ctx* c) {
     for (auto& s : c->scans) {
         dev_free(s.pts); dev_free(s.nn);
         dev_free(s.partial);
+        dev_free(s.d_perm); dev_free(s.d_iperm);
     }
+    ivox_free(c->iv);
     dev_free(c->nodes);
     dev_free(c->lnodes);
     dev_free(c->lpts);
@@ -559,6 +790,15 @@ int livo_scan_upload(livo_ctx* c, const float* xyz, int64_t N, int64_t stride_by
             for (int a = 0; a < 4; a++) hs[4 * k + a] = h[4 * (int64_t)s.perm[k] + a];
         if (hipMemcpy(s.pts, hs.data(), hs.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) return LIVO_E_HIP;
         if (hipMemset(s.nn, 0, (size_t)N * sizeof(NNRec)) != hipSuccess) return LIVO_E_HIP;
+        std::vector<int32_t> iperm((size_t)N);
+        for (int64_t k = 0; k < N; k++) iperm[(size_t)s.perm[(size_t)k]] = (int32_t)k;
+        if (dev_alloc(&s.d_perm, (size_t)N) || dev_alloc(&s.d_iperm, (size_t)N)) {
+            dev_free(s.pts); dev_free(s.nn); dev_free(s.partial); dev_free(s.d_perm); dev_free(s.d_iperm);
+            return LIVO_E_OOM;
+        }
+        if (hipMemcpy(s.d_perm, s.perm.data(), (size_t)N * 4, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(s.d_iperm, iperm.data(), (size_t)N * 4, hipMemcpyHostToDevice) != hipSuccess)
+            return LIVO_E_HIP;
     }
     int32_t id = -1;
     for (size_t i = 0; i < c->scans.size(); i++)
@@ -581,6 +821,7 @@ int livo_scan_release(livo_ctx* c, int32_t id) {
     ScanBuf& s = c->scans[id];
     dev_free(s.pts); dev_free(s.nn);
     dev_free(s.partial);
+    dev_free(s.d_perm); dev_free(s.d_iperm);
     s = ScanBuf{};
     return LIVO_OK;
 }
@@ -615,7 +856,7 @@ int livo_h_share(livo_ctx* c, int32_t id, const livo_state* state, int search_en
     if (!c || !state || !HTH || !HTL) return LIVO_E_INVALID;
     ScanBuf* s = get_scan(c, id);
     if (!s) return LIVO_E_NOSCAN;
-    if (!c->has_map) return LIVO_E_NOMAP;
+    if (!map_ready(c)) return LIVO_E_NOMAP;
     if (set_device(c)) return LIVO_E_HIP;
     int rc = ensure_slots(c, 1);
     if (rc) return rc;
@@ -640,7 +881,12 @@ int livo_h_share(livo_ctx* c, int32_t id, const livo_state* state, int search_en
         if (rc) return rc;
         KnnParams kp = make_knn_params(c);
         kp.force = 1;
-        rc = knn_pass(kp, 1, N, c->stream);
+        if (c->backend == LIVO_BACKEND_IVOX) {
+            HIP_TRY(hipMemsetAsync(kp.replay_count, 0, sizeof(unsigned), c->stream));
+            rc = backend_knn(c, kp, 1, N, false, c->stream);
+        } else {
+            rc = knn_pass(kp, 1, N, c->stream);
+        }
         if (rc) return rc;
     } else if (!s->searched && N > 0) {
         // no cached neighbours yet: nothing is matched (points_near.size() < 5, :525)
@@ -709,7 +955,8 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
                         livo_ikfom_stats* ik_stats) {
     if (!c || n < 0 || (n > 0 && (!ids || (model == kModelIkfom ? !ik_states : !states)))) return LIVO_E_INVALID;
     if (n == 0) return LIVO_OK;
-    if (!c->has_map) return LIVO_E_NOMAP;
+    if (!map_ready(c)) return LIVO_E_NOMAP;
+    if (model == kModelIkfom && c->backend != LIVO_BACKEND_IKDTREE) return LIVO_E_INVALID;  // ikd-Tree h-model only
     for (int32_t b = 0; b < n; b++)
         if (!get_scan(c, ids[b])) return LIVO_E_NOSCAN;
     if (set_device(c)) return LIVO_E_HIP;
@@ -787,8 +1034,7 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
             if (full && (e > 0 || gi > 0)) HIP_TRY(hipEventRecord(c->ev[gi][3 * e], st));
             // leaf-map search; rematch passes are bounded by the previous neighbours
             // (the group's replay count was zeroed before the batch / by the last k_solve)
-            rc = c->knn_kind == 1 ? launch_knn_grid(kp[gi], g[gi].count, g[gi].max_n, e > 0, st)
-                                  : launch_knn_leaf(kp[gi], g[gi].count, g[gi].max_n, e > 0, st);
+            rc = backend_knn(c, kp[gi], g[gi].count, g[gi].max_n, e > 0, st);
             if (rc) return rc;
             if ((prof && e == 0) || full) HIP_TRY(hipEventRecord(c->ev[gi][3 * e + 1], st));
             rc = model == kModelIkfom ? launch_hshare_ik(hp[gi], g[gi].count, g[gi].max_nblk, e == 0, st)
@@ -870,6 +1116,244 @@ int livo_ikfom_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_ikf
 int livo_ikfom_update(livo_ctx* c, int32_t id, livo_ikfom_state* state, livo_ikfom_stats* stats) {
     if (!state) return LIVO_E_INVALID;
     return livo_ikfom_update_batch(c, 1, &id, state, stats);
+}
+
+int livo_ctx_set_backend(livo_ctx* c, int backend) {
+    if (!c || (backend != LIVO_BACKEND_IKDTREE && backend != LIVO_BACKEND_IVOX)) return LIVO_E_INVALID;
+    if (backend != c->backend)
+        for (auto& s : c->scans) s.searched = false;  // cached neighbours belong to the other map
+    c->backend = backend;
+    return LIVO_OK;
+}
+
+int livo_ivox_params_default(livo_ivox_params* p) {
+    if (!p) return LIVO_E_INVALID;
+    p->resolution = 0.2f;   // ivox_grid_resolution default (laser_mapping.cpp:1021)
+    p->nearby_type = 18;    // ivox_nearby_type default (laser_mapping.cpp:1022)
+    p->capacity = 1000000;  // Options::capacity_ (ivox3d.h:57)
+    return LIVO_OK;
+}
+
+int livo_ivox_init(livo_ctx* c, const livo_ivox_params* p) {
+    if (!c) return LIVO_E_INVALID;
+    livo_ivox_params prm;
+    livo_ivox_params_default(&prm);
+    if (p) prm = *p;
+    int nearby = 0;
+    switch (prm.nearby_type) {
+        case 0: nearby = 1; break;
+        case 6: nearby = 7; break;
+        case 18: nearby = 19; break;
+        case 26: nearby = 27; break;
+        default: return LIVO_E_INVALID;
+    }
+    if (!(prm.resolution > 0.f) || !std::isfinite(prm.resolution) || prm.capacity < 1) return LIVO_E_INVALID;
+    if (set_device(c)) return LIVO_E_HIP;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    ivox_free(c->iv);
+    IvoxDev& v = c->iv;
+    v.prm = prm;
+    v.inv_res = (float)(1.0 / (double)prm.resolution);  // options_.inv_resolution_ = 1.0 / resolution_
+    v.nearby = nearby;
+    if (dev_alloc(&v.ctr, 3)) return LIVO_E_OOM;
+    int rc = ivox_ensure_table(c, 1024);
+    if (!rc) rc = ivox_ensure_big(c);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    v.ready = true;
+    for (auto& s : c->scans) s.searched = false;
+    return LIVO_OK;
+}
+
+int livo_ivox_add_points(livo_ctx* c, const float* xyz, int64_t n, int64_t stride_bytes) {
+    if (!c || n < 0 || (n > 0 && !xyz)) return LIVO_E_INVALID;
+    if (stride_bytes == 0) stride_bytes = 3 * sizeof(float);
+    if (stride_bytes < (int64_t)(3 * sizeof(float))) return LIVO_E_INVALID;
+    if (!c->iv.ready) return LIVO_E_NOMAP;
+    if (n == 0) return LIVO_OK;
+    if (set_device(c)) return LIVO_E_HIP;
+    int rc = ivox_ensure_src(c, n);
+    if (rc) return rc;
+    std::vector<float> h((size_t)n * 4);
+    const char* base = (const char*)xyz;
+    for (int64_t i = 0; i < n; i++) {
+        const float* p = (const float*)(base + i * stride_bytes);
+        h[4 * i] = p[0]; h[4 * i + 1] = p[1]; h[4 * i + 2] = p[2]; h[4 * i + 3] = 0.f;
+    }
+    HIP_TRY(hipMemcpyAsync(c->iv.src, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    return ivox_add_dev(c, n);
+}
+
+int livo_ivox_knn(livo_ctx* c, const float* q, int64_t n, int32_t max_num, double max_range, int32_t* idx,
+                  float* d, int32_t* cnt) {
+    if (!c || n < 0 || max_num < 1 || max_num > kNN || !(max_range >= 0.0) ||
+        (n > 0 && (!q || !idx || !d || !cnt)))
+        return LIVO_E_INVALID;
+    if (!c->iv.ready) return LIVO_E_NOMAP;
+    if (n == 0) return LIVO_OK;
+    if (n > (int64_t)0x7FFFFFFF - kBlock) return LIVO_E_RANGE;
+    if (set_device(c)) return LIVO_E_HIP;
+    int rc = ensure_slots(c, 1);
+    if (rc) return rc;
+    const size_t qb = (size_t)n * 4 * sizeof(float), rb = (size_t)n * sizeof(NNRec);
+    rc = ensure_scratch(c, qb + rb + 256);
+    if (!rc) rc = ensure_replay(c, n);
+    if (rc) return rc;
+    char* base = (char*)c->scratch;
+    float* dq = (float*)base;
+    NNRec* dr = (NNRec*)(base + ((qb + 255) & ~(size_t)255));
+    std::vector<float> hq((size_t)n * 4);
+    for (int64_t i = 0; i < n; i++) {
+        hq[4 * i] = q[3 * i]; hq[4 * i + 1] = q[3 * i + 1]; hq[4 * i + 2] = q[3 * i + 2]; hq[4 * i + 3] = 0.f;
+    }
+    std::memset(&c->h_slots[0], 0, sizeof(IekfSlot));
+    HsJob& j = c->h_jobs[0];
+    j = HsJob{};
+    j.pts = dq; j.nn = dr; j.slot = c->d_slots; j.n = (int32_t)n; j.nblk = 0;
+    HIP_TRY(hipMemcpyAsync(dq, hq.data(), qb, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemsetAsync(dr, 0xFF, rb, c->stream));  // cnt = -1: left alone = nothing found
+    HIP_TRY(hipMemcpyAsync(c->d_slots, c->h_slots, sizeof(IekfSlot), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->d_jobs, c->h_jobs, sizeof(HsJob), hipMemcpyHostToDevice, c->stream));
+    KnnParams kp = make_knn_params(c);
+    kp.force = 1;
+    kp.identity = 1;
+    kp.iv.max_num = max_num;
+    kp.iv.range2 = max_range * max_range;
+    HIP_TRY(hipMemsetAsync(kp.replay_count, 0, sizeof(unsigned), c->stream));
+    rc = launch_ivox_knn(kp, 1, n, false, c->iv.big_threads, c->stream);
+    if (rc) return rc;
+    std::vector<NNRec> hr((size_t)n);
+    HIP_TRY(hipMemcpyAsync(hr.data(), dr, rb, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (int64_t i = 0; i < n; i++) {
+        cnt[i] = hr[i].cnt;
+        for (int t = 0; t < max_num; t++) {
+            const bool has = hr[i].cnt > t;
+            idx[i * max_num + t] = has ? hr[i].idx[t] : -1;
+            d[i * max_num + t] = has ? hr[i].p[t][3] : INFINITY;
+        }
+    }
+    return LIVO_OK;
+}
+
+int livo_ivox_get_info(livo_ctx* c, livo_ivox_info* out) {
+    if (!c || !out) return LIVO_E_INVALID;
+    if (!c->iv.ready) return LIVO_E_NOMAP;
+    const IvoxDev& v = c->iv;
+    out->num_points = v.npts;
+    out->num_grids = v.ngrids;
+    out->ids_issued = v.next_id;
+    out->max_grid_points = v.max_grid;
+    out->device_bytes = v.table * (int64_t)(sizeof(GridSlot) + 4 * sizeof(uint32_t)) +
+                        (v.pts_cap[0] + v.pts_cap[1]) * 16 + v.big_threads * v.big_slice * (int64_t)sizeof(SelElem);
+    return LIVO_OK;
+}
+
+int livo_ivox_dump(livo_ctx* c, float* xyz, int32_t* ids, int32_t* keys, int64_t cap, int64_t* n) {
+    if (!c || !n) return LIVO_E_INVALID;
+    if (!c->iv.ready) return LIVO_E_NOMAP;
+    const IvoxDev& v = c->iv;
+    *n = v.npts;
+    if (cap < v.npts) return LIVO_E_RANGE;
+    if (set_device(c)) return LIVO_E_HIP;
+    std::vector<GridSlot> slots((size_t)v.table);
+    std::vector<float> pts((size_t)v.npts * 4);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpy(slots.data(), v.slots, slots.size() * sizeof(GridSlot), hipMemcpyDeviceToHost));
+    if (v.npts) HIP_TRY(hipMemcpy(pts.data(), v.pts[v.cur], pts.size() * sizeof(float), hipMemcpyDeviceToHost));
+    int64_t k = 0;
+    for (const GridSlot& g : slots) {
+        if (g.key == kGridEmpty) continue;
+        const int kx = (int)(g.key & 0x1FFFFFull) - kIvBias, ky = (int)((g.key >> 21) & 0x1FFFFFull) - kIvBias,
+                  kz = (int)((g.key >> 42) & 0x1FFFFFull) - kIvBias;
+        for (uint32_t t = 0; t < g.count && k < v.npts; t++, k++) {
+            const float* p = &pts[4 * (size_t)(g.start + t)];
+            if (xyz) { xyz[3 * k] = p[0]; xyz[3 * k + 1] = p[1]; xyz[3 * k + 2] = p[2]; }
+            if (ids) std::memcpy(&ids[k], &p[3], 4);
+            if (keys) { keys[3 * k] = kx; keys[3 * k + 1] = ky; keys[3 * k + 2] = kz; }
+        }
+    }
+    return k == v.npts ? LIVO_OK : LIVO_E_HIP;
+}
+
+int livo_map_incremental(livo_ctx* c, int32_t id, const livo_state* state, double fs, int ekf_inited, uint8_t* cat,
+                         int64_t counts[2]) {
+    if (!c || !state || !(fs > 0.0)) return LIVO_E_INVALID;
+    if (c->backend != LIVO_BACKEND_IVOX) return LIVO_E_INVALID;  // ikd-Tree Add_Points: not on the device
+    if (!c->iv.ready) return LIVO_E_NOMAP;
+    ScanBuf* s = get_scan(c, id);
+    if (!s) return LIVO_E_NOSCAN;
+    if (set_device(c)) return LIVO_E_HIP;
+    const int64_t N = s->n;
+    if (counts) counts[0] = counts[1] = 0;
+    if (N == 0) return LIVO_OK;
+    int rc = ensure_slots(c, 1);
+    if (rc) return rc;
+    // scratch: ordered 2N x 16 B, flags 2N x 4, pos 2N x 4, cat N
+    const size_t ob = (size_t)N * 32, fb = (size_t)N * 8, cb = (size_t)N;
+    rc = ensure_scratch(c, ob + 2 * fb + cb + 1024);
+    if (!rc) rc = ivox_ensure_src(c, N);
+    if (rc) return rc;
+    char* base = (char*)c->scratch;
+    float* ordered = (float*)base;
+    uint32_t* flags = (uint32_t*)(base + ob);
+    uint32_t* pos = (uint32_t*)(base + ob + fb);
+    uint8_t* dcat = (uint8_t*)(base + ob + 2 * fb);
+    init_slot(c->h_slots[0], *state, *state, c->params.max_iterations);
+    HIP_TRY(hipMemcpyAsync(c->d_slots, c->h_slots, sizeof(IekfSlot), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemsetAsync(flags, 0, fb, c->stream));
+    MapIncrParams mp{};
+    mp.pts = s->pts;
+    mp.nn = s->nn;
+    mp.perm = s->d_perm;
+    mp.slot = c->d_slots;
+    std::memcpy(mp.R_LI, c->params.R_LI, sizeof(mp.R_LI));
+    std::memcpy(mp.t_LI, c->params.t_LI, sizeof(mp.t_LI));
+    mp.ordered = ordered;
+    mp.flags = flags;
+    mp.cat = cat ? dcat : nullptr;
+    mp.fs = fs;
+    mp.n = (int32_t)N;
+    mp.ekf_inited = ekf_inited ? 1 : 0;
+    rc = launch_map_incr(mp, c->stream);
+    if (!rc) rc = ivox_scan(c, flags, pos, 2 * N);
+    if (!rc) rc = launch_compact(ordered, flags, pos, 2 * N, c->iv.src, c->stream);
+    if (rc) return rc;
+    uint32_t tail[3];  // pos[N], pos[2N-1], flags[2N-1]
+    HIP_TRY(hipMemcpyAsync(&tail[0], pos + N, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(&tail[1], pos + 2 * N - 1, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(&tail[2], flags + 2 * N - 1, 4, hipMemcpyDeviceToHost, c->stream));
+    std::vector<uint8_t> hcat;
+    if (cat) {
+        hcat.resize((size_t)N);
+        HIP_TRY(hipMemcpyAsync(hcat.data(), dcat, cb, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const int64_t total = (int64_t)tail[1] + tail[2], n_add = tail[0];
+    if (cat)
+        for (int64_t k = 0; k < N; k++) cat[s->perm[(size_t)k]] = hcat[(size_t)k];
+    rc = ivox_add_dev(c, total);
+    if (rc) return rc;
+    if (counts) {
+        counts[0] = n_add;
+        counts[1] = total - n_add;
+    }
+    return LIVO_OK;
+}
+
+int livo_scan_inherit_neighbors(livo_ctx* c, int32_t dst, int32_t src) {
+    if (!c) return LIVO_E_INVALID;
+    ScanBuf* d = get_scan(c, dst);
+    ScanBuf* s = get_scan(c, src);
+    if (!d || !s) return LIVO_E_NOSCAN;
+    if (dst == src) return LIVO_OK;
+    if (set_device(c)) return LIVO_E_HIP;
+    if (d->n == 0) return LIVO_OK;
+    const int rc = launch_inherit_nn(d->nn, d->d_perm, d->n, s->nn, s->d_iperm, s->searched ? s->n : 0, c->stream);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    d->searched = true;  // the cache now holds the inherited entries
+    return LIVO_OK;
 }
 
 int livo_sync(livo_ctx* c) {

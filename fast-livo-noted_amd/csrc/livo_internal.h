@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "livo.h"
+#include "stl_select.h"
 
 #ifndef LIVO_PTS_PER_THREAD
 #define LIVO_PTS_PER_THREAD 4
@@ -118,6 +119,47 @@ struct HostGridMap {
 int build_grid_map(const float* xyz, int64_t M, int64_t stride_bytes, float cell_h, HostGridMap* out);
 void free_grid_map(HostGridMap* m);
 
+// ---------------------------------------------------------------------------
+// iVox map (faster_lio::IVox<3, DEFAULT>, include/ivox3d/ivox3d.h): the
+// compiled default k-NN backend of LaserMapping.  Grids (voxels of edge
+// `resolution`, key = round(p / resolution)) live in an open-addressing hash
+// of 16-B GridSlots {key, start, count}; the points of all grids are one CSR
+// array of float4 (x, y, z, id bits), each grid one run in insertion order
+// (IVoxNode::points_).  AddPoints rebuilds the CSR in one pass (old runs
+// moved, new points appended in input order): the search then reads each
+// grid as one contiguous run.  id = insertion sequence number of the point.
+// ---------------------------------------------------------------------------
+constexpr int kIvBias = 1 << 20;            // key bias (21 bits per axis)
+constexpr int kIvMaxKey = kIvBias - 64;     // |cell| limit of stored points
+constexpr int kIvCap = 64;                  // private candidates per query (k_ivox_knn); beyond: overflow pass
+constexpr int kIvMaxNearby = 27;
+
+struct IvoxParams {
+    GridSlot* slots;          // 2^log2 slots
+    const float* pts;         // CSR points, 4 floats each (search) / old points (AddPoints)
+    float* npts;              // AddPoints: new CSR
+    const float* src;         // AddPoints: points to add (4 floats each), in insertion order
+    int64_t n_src;
+    int64_t table;            // 2^log2
+    uint32_t* addcnt;         // per slot: points added by this batch
+    uint32_t* tot;            // per slot: count + addcnt (scan input)
+    uint32_t* newstart;       // per slot: start in the new CSR (scan of tot)
+    uint32_t* addstart;       // per slot: start of its run in the sorted batch (scan of addcnt)
+    uint32_t* slot_of;        // per src point: its slot (table: out of range)
+    uint32_t* iota;           // per src point: its index
+    const uint32_t* skeys;    // batch sorted by slot (stable)
+    const uint32_t* svals;
+    unsigned long long* ctr;  // [0] error bits, [1] new grids, [2] max points per grid
+    int64_t base_id;          // id of src[0]
+    float inv_res;            // Options::inv_resolution_ (float of 1.0 / resolution)
+    int32_t log2;
+    int32_t nearby;           // 1, 7, 19 or 27 nearby grids (NearbyType)
+    int32_t max_num;          // GetClosestPoint max_num (<= 5)
+    double range2;            // max_range * max_range
+    SelElem* scratch;         // overflow pass: one slice per thread
+    int64_t slice;            // elements per slice
+};
+
 // IEKF control block (the loop variables of laser_mapping.cpp:166-238).
 struct IekfCtrl {
     int32_t stop;         // EKF_stop_flg reached: every later launch for this scan exits
@@ -229,6 +271,7 @@ struct KnnParams {
     float gh;               // cell edge
     float geps;             // cell-bound slack for float rounding of the cell assignment
     int32_t glog2;          // log2 of the hash table size
+    IvoxParams iv;          // iVox backend (LIVO_BACKEND_IVOX)
 };
 
 struct SolveParams {
@@ -261,5 +304,49 @@ int launch_hshare(const HsParams& p, int n_jobs, int max_nblk, bool first, void*
 // IKFoM plane pass (12-wide rows) with the manifold update in each scan's last block.
 int launch_hshare_ik(const HsParams& p, int n_jobs, int max_nblk, bool first, void* stream);
 int launch_solve(const SolveParams& p, int n_jobs, void* stream);
+
+// iVox (ivox_kernels.hip).  AddPoints in stages, so the host can check the
+// new grid count against the LRU capacity before anything is moved:
+// insert (keys -> slots, counts) | rollback, or prepare -> scans + stable sort
+// by slot -> move (old runs) -> place (new points, input order) -> fix.
+int launch_ivox_clear(GridSlot* slots, int64_t table, void* stream);
+int launch_ivox_insert(const IvoxParams& p, void* stream);
+int launch_ivox_rollback(const IvoxParams& p, void* stream);
+int launch_ivox_prepare(const IvoxParams& p, void* stream);
+int launch_ivox_move(const IvoxParams& p, void* stream);
+int launch_ivox_place(const IvoxParams& p, void* stream);
+int launch_ivox_fix(const IvoxParams& p, void* stream);
+int launch_ivox_rehash(const GridSlot* old_slots, int64_t old_table, GridSlot* slots, int log2, void* stream);
+// GetClosestPoint of every point of every job (+ the overflow pass).
+int launch_ivox_knn(const KnnParams& p, int n_jobs, int64_t max_n, bool later, int64_t overflow_threads,
+                    void* stream);
+// rocPRIM wrappers (prims.hip); temp == nullptr queries the scratch size.
+int prim_sort_pairs_u32(void* temp, size_t* temp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
+                        const uint32_t* vals_in, uint32_t* vals_out, int64_t n, int bits, void* stream);
+int prim_exclusive_scan_u32(void* temp, size_t* temp_bytes, const uint32_t* in, uint32_t* out, int64_t n,
+                            void* stream);
+// map_incremental decision (laser_mapping.cpp:329-389): ordered[2N] holds the
+// points_to_add at their point index and point_no_need_downsample at N + index,
+// flags[2N] marks them; cat (stored order, may be null) 0 skip / 1 add / 2 no-downsample.
+struct MapIncrParams {
+    const float* pts;         // scan body points (stored order), N x 4
+    const NNRec* nn;
+    const int32_t* perm;      // stored position -> caller index
+    const IekfSlot* slot;     // its state = the updated state
+    double R_LI[9];
+    double t_LI[3];
+    float* ordered;           // 2N x 4 floats
+    uint32_t* flags;          // 2N
+    uint8_t* cat;             // N (stored order) or null
+    double fs;                // filter_size_map_min
+    int32_t n;
+    int32_t ekf_inited;
+};
+int launch_map_incr(const MapIncrParams& p, void* stream);
+int launch_compact(const float* ordered, const uint32_t* flags, const uint32_t* pos, int64_t n, float* dense,
+                   void* stream);
+// Nearest_Points carried over by point index (laser_mapping.cpp:165 resize keeps entries).
+int launch_inherit_nn(NNRec* dst, const int32_t* dst_perm, int64_t n_dst, const NNRec* src,
+                      const int32_t* src_iperm, int64_t n_src, void* stream);
 
 }  // namespace livo

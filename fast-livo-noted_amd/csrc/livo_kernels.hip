@@ -29,6 +29,7 @@
 #include <math.h>
 
 #include "livo_internal.h"
+#include "device_common.h"
 
 namespace livo {
 
@@ -497,18 +498,6 @@ __device__ __forceinline__ void sl_insert(SList& s, float d, uint32_t node) {
     s.n = s.n < kNN ? s.n + 1 : kNN;
 }
 
-__device__ __forceinline__ void world_point(const double* R, const double* pos, const double* RL, const double* tL,
-                                            float bxf, float byf, float bzf, float& wx, float& wy, float& wz) {
-    // pointBodyToWorld (laser_mapping.cpp:662-671): double math, float storage
-    const double bx = bxf, by = byf, bz = bzf;
-    const double ix = ((RL[0] * bx + RL[1] * by) + RL[2] * bz) + tL[0];
-    const double iy = ((RL[3] * bx + RL[4] * by) + RL[5] * bz) + tL[1];
-    const double iz = ((RL[6] * bx + RL[7] * by) + RL[8] * bz) + tL[2];
-    wx = (float)(((R[0] * ix + R[1] * iy) + R[2] * iz) + pos[0]);
-    wy = (float)(((R[3] * ix + R[4] * iy) + R[5] * iz) + pos[1]);
-    wz = (float)(((R[6] * ix + R[7] * iy) + R[8] * iz) + pos[2]);
-}
-
 // One neighbour record per point (Nearest_Points[i] + pointSearchSqDis);
 // flag = 1 if the query goes to the exact replay; node[] = heap ids (seeds of the next search).
 __device__ __forceinline__ void write_nnrec(NNRec* __restrict__ out, const MapNode* __restrict__ nodes, int cnt,
@@ -541,17 +530,6 @@ __device__ __forceinline__ void query_point(const KnnParams& P, const IekfSlot* 
     } else {
         world_point(slot->state.rot, slot->state.pos, P.R_LI, P.t_LI, b.x, b.y, b.z, qx, qy, qz);
     }
-}
-
-// XCD-aware block order for a 1-D grid of nb blocks per scan: blocks are dealt
-// round-robin over the 8 XCDs, so give each XCD one contiguous run of (scan,
-// block) ids -- one region of Morton-ordered points -- and its L2 only the
-// part of the map around that region (bijective for any grid size).
-__device__ __forceinline__ void xcd_block(int nb, unsigned& job, unsigned& bx) {
-    const unsigned nwg = gridDim.x, orig = blockIdx.x, xcd = orig % 8u, q = nwg / 8u, r = nwg % 8u;
-    const unsigned wgid = (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q) + orig / 8u;
-    job = wgid / (unsigned)nb;
-    bx = wgid % (unsigned)nb;
 }
 
 __device__ __forceinline__ void count_visits(const KnnParams& P, IekfSlot* slot, unsigned visits) {

@@ -19,7 +19,8 @@
 #pragma once
 #include <stdint.h>
 
-#if defined(__HIPCC__)
+#if defined(__HIP__)  // compiling HIP source (device + host)
+#include <hip/hip_runtime.h>
 #define SEL_HD __host__ __device__ __forceinline__
 #else
 #define SEL_HD inline

@@ -6,6 +6,8 @@ path:
 
     KD_TREE::Build / Nearest_Search      -> Context.map_build / Context.knn
     LaserMapping::h_share_model          -> Context.h_share
+    IVox (AddPoints / GetClosestPoint)   -> Context.ivox_init / ivox_add_points / ivox_knn
+    LaserMapping::map_incremental        -> Context.map_incremental
     IEKF loop of LaserMapping::Run       -> Context.iekf_update(_batch)
 
 There is no CPU fallback: loading fails loudly if the HIP library is missing,
@@ -29,7 +31,9 @@ MAX_EVALS = 16
 
 LIVO_OK = 0
 ERRORS = {-1: "LIVO_E_INVALID", -2: "LIVO_E_HIP", -3: "LIVO_E_NOMAP", -4: "LIVO_E_NOSCAN", -5: "LIVO_E_OOM",
-          -6: "LIVO_E_RANGE"}
+          -6: "LIVO_E_RANGE", -7: "LIVO_E_CAPACITY"}
+BACKEND_IKDTREE = 0  # -DUSE_ikdtree build (CMakeLists.txt:15)
+BACKEND_IVOX = 1     # the reference's default build: faster_lio::IVox
 
 
 class LivoError(RuntimeError):
@@ -117,6 +121,15 @@ def ikfom_stats_from_c(st: IkfomStats) -> dict:
             "res_mean": [st.res_mean[i] for i in range(min(ne, 16))]}
 
 
+class IvoxParams(C.Structure):
+    _fields_ = [("resolution", C.c_float), ("nearby_type", C.c_int32), ("capacity", C.c_int64)]
+
+
+class IvoxInfo(C.Structure):
+    _fields_ = [("num_points", C.c_int64), ("num_grids", C.c_int64), ("ids_issued", C.c_int64),
+                ("max_grid_points", C.c_int64), ("device_bytes", C.c_int64)]
+
+
 SIGNATURES = {
     "livo_abi_version": (C.c_int, []),
     "livo_error_string": (C.c_char_p, [C.c_int]),
@@ -138,6 +151,15 @@ SIGNATURES = {
     "livo_iekf_update_batch": (C.c_int, [_P, C.c_int32, _P, _P, _P, _P]),
     "livo_ikfom_update": (C.c_int, [_P, C.c_int32, C.POINTER(IkfomState), C.POINTER(IkfomStats)]),
     "livo_ikfom_update_batch": (C.c_int, [_P, C.c_int32, _P, _P, _P]),
+    "livo_ctx_set_backend": (C.c_int, [_P, C.c_int]),
+    "livo_ivox_params_default": (C.c_int, [C.POINTER(IvoxParams)]),
+    "livo_ivox_init": (C.c_int, [_P, C.POINTER(IvoxParams)]),
+    "livo_ivox_add_points": (C.c_int, [_P, _P, C.c_int64, C.c_int64]),
+    "livo_ivox_knn": (C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_double, _P, _P, _P]),
+    "livo_ivox_get_info": (C.c_int, [_P, C.POINTER(IvoxInfo)]),
+    "livo_ivox_dump": (C.c_int, [_P, _P, _P, _P, C.c_int64, C.POINTER(C.c_int64)]),
+    "livo_map_incremental": (C.c_int, [_P, C.c_int32, C.POINTER(State), C.c_double, C.c_int, _P, _P]),
+    "livo_scan_inherit_neighbors": (C.c_int, [_P, C.c_int32, C.c_int32]),
     "livo_sync": (C.c_int, [_P]),
 }
 
@@ -354,6 +376,60 @@ class Context:
         if raw:
             return sts, stats
         return [ikfom_from_c(s) for s in sts], [ikfom_stats_from_c(s) for s in stats]
+
+    # ----------------------------------------------------------- iVox ----
+    def set_backend(self, backend: int):
+        _check("livo_ctx_set_backend", self._L.livo_ctx_set_backend(self.h, backend))
+
+    def ivox_init(self, resolution: float = 0.2, nearby_type: int = 18, capacity: int = 1_000_000):
+        p = IvoxParams(resolution, nearby_type, capacity)
+        _check("livo_ivox_init", self._L.livo_ivox_init(self.h, C.byref(p)))
+
+    def ivox_add_points(self, xyz: np.ndarray):
+        xyz = np.ascontiguousarray(xyz, np.float32)
+        assert xyz.ndim == 2 and xyz.shape[1] >= 3
+        _check("livo_ivox_add_points", self._L.livo_ivox_add_points(self.h, _ptr(xyz), xyz.shape[0],
+                                                                    xyz.shape[1] * 4))
+
+    def ivox_knn(self, q: np.ndarray, max_num: int = 5, max_range: float = 5.0):
+        """GetClosestPoint: idx, sqdist (n, max_num) in the reference's order, cnt (-1: nothing found)."""
+        q = np.ascontiguousarray(q, np.float32).reshape(-1, 3)
+        n = q.shape[0]
+        idx = np.empty((n, max_num), np.int32)
+        d = np.empty((n, max_num), np.float32)
+        cnt = np.empty(n, np.int32)
+        _check("livo_ivox_knn", self._L.livo_ivox_knn(self.h, _ptr(q), n, max_num, max_range, _ptr(idx), _ptr(d),
+                                                      _ptr(cnt)))
+        return idx, d, cnt
+
+    def ivox_info(self) -> dict:
+        i = IvoxInfo()
+        _check("livo_ivox_get_info", self._L.livo_ivox_get_info(self.h, C.byref(i)))
+        return {k: getattr(i, k) for k, _ in IvoxInfo._fields_}
+
+    def ivox_dump(self):
+        """All points (xyz, ids, grid keys), grid by grid, insertion order inside a grid."""
+        n = self.ivox_info()["num_points"]
+        xyz = np.zeros((n, 3), np.float32)
+        ids = np.zeros(n, np.int32)
+        keys = np.zeros((n, 3), np.int32)
+        got = C.c_int64()
+        _check("livo_ivox_dump", self._L.livo_ivox_dump(self.h, _ptr(xyz), _ptr(ids), _ptr(keys), n, C.byref(got)))
+        return xyz, ids, keys
+
+    def map_incremental(self, sid: int, state: dict, filter_size_map: float = 0.5, ekf_inited: bool = True):
+        """Returns (cat per point: 0 skipped / 1 added / 2 added without downsampling, counts dict)."""
+        n = self.scans[sid]
+        cat = np.zeros(n, np.uint8)
+        counts = np.zeros(2, np.int64)
+        s = state_to_c(state)
+        _check("livo_map_incremental", self._L.livo_map_incremental(self.h, sid, C.byref(s), filter_size_map,
+                                                                    int(bool(ekf_inited)), _ptr(cat),
+                                                                    _ptr(counts)))
+        return cat, {"added": int(counts[0]), "no_downsample": int(counts[1])}
+
+    def scan_inherit_neighbors(self, dst: int, src: int):
+        _check("livo_scan_inherit_neighbors", self._L.livo_scan_inherit_neighbors(self.h, dst, src))
 
     def set_profiling(self, level):
         """0/False off, 1 first-search timing only, 2/True every stage (livo_ctx_set_profiling)."""

@@ -17,6 +17,10 @@
  *   livo_iekf_update    ← the IEKF loop inlined in LaserMapping::Run
  *                                                   src/laser_mapping.cpp:171-238
  *   livo_iekf_update_batch ← the same for independent scans (scan farm, §8e)
+ *   livo_ivox_*         ← faster_lio::IVox, the compiled default k-NN backend
+ *                                                   include/ivox3d/ivox3d.h:37-305
+ *   livo_map_incremental ← LaserMapping::map_incremental (iVox branch)
+ *                                                   src/laser_mapping.cpp:329-389
  *
  * Conventions
  *   - plain pointers and sizes only; no C++ or torch types cross the ABI;
@@ -52,7 +56,9 @@ enum {
     LIVO_E_NOMAP = -3,     /* map not built */
     LIVO_E_NOSCAN = -4,    /* unknown / released scan id */
     LIVO_E_OOM = -5,       /* device allocation failed */
-    LIVO_E_RANGE = -6      /* size beyond the supported range */
+    LIVO_E_RANGE = -6,     /* size beyond the supported range */
+    LIVO_E_CAPACITY = -7   /* iVox grid count would reach Options::capacity_ (LRU eviction
+                              is not done on the device; the map is left unchanged) */
 };
 
 typedef struct livo_ctx livo_ctx;
@@ -216,6 +222,68 @@ typedef struct livo_ikfom_stats {
 int livo_ikfom_update_batch(livo_ctx* ctx, int32_t n, const int32_t* scan_ids, livo_ikfom_state* states,
                             livo_ikfom_stats* stats);
 int livo_ikfom_update(livo_ctx* ctx, int32_t scan_id, livo_ikfom_state* state, livo_ikfom_stats* stats);
+
+/* ------------------------------------------------------------------------
+ * iVox backend: faster_lio::IVox<3, DEFAULT, PointType>
+ * (include/laser_mapping.h:65), the k-NN backend of the reference's default
+ * build (CMakeLists.txt:15 leaves USE_ikdtree undefined).  With
+ * livo_ctx_set_backend(ctx, LIVO_BACKEND_IVOX), livo_h_share and
+ * livo_iekf_update[_batch] search the iVox map with
+ * GetClosestPoint(point_world, points_near, 5) (laser_mapping.cpp:520): no
+ * sqdist gate, a point is matched iff 5 neighbours within 5 m were found
+ * (:525), the neighbours are in the order the reference's std::nth_element
+ * leaves them, and a point with no candidate keeps its previous
+ * Nearest_Points entry (ivox3d.h:165-167).
+ * ------------------------------------------------------------------------ */
+#define LIVO_BACKEND_IKDTREE 0  /* -DUSE_ikdtree build (CMakeLists.txt:15)            */
+#define LIVO_BACKEND_IVOX 1     /* the default build: IVox (laser_mapping.cpp:519-521) */
+
+typedef struct livo_ivox_params {
+    float resolution;     /* ivox_grid_resolution (0.2, laser_mapping.cpp:1021)          */
+    int32_t nearby_type;  /* ivox_nearby_type: 0 CENTER, 6, 18 (default, :1022-1035), 26 */
+    int64_t capacity;     /* Options::capacity_ (1000000, ivox3d.h:57)                   */
+} livo_ivox_params;
+
+typedef struct livo_ivox_info {
+    int64_t num_points;      /* points held (IVox::NumPoints)                       */
+    int64_t num_grids;       /* IVox::NumValidGrids (ivox3d.h:206-209)              */
+    int64_t ids_issued;      /* points ever added = the id of the next point        */
+    int64_t max_grid_points; /* largest grid                                        */
+    int64_t device_bytes;    /* HBM held by the iVox map                            */
+} livo_ivox_info;
+
+int livo_ctx_set_backend(livo_ctx* ctx, int backend);
+int livo_ivox_params_default(livo_ivox_params* p);
+/* IVox(Options) (ivox3d.h:64-67, laser_mapping.cpp:776): an empty map. */
+int livo_ivox_init(livo_ctx* ctx, const livo_ivox_params* p);
+/* IVox::AddPoints (ivox3d.h:256-281) of n host points, in order (the first
+ * scan's feats_down_body, laser_mapping.cpp:147).  Point ids continue from
+ * ids_issued.  LIVO_E_CAPACITY / LIVO_E_RANGE leave the map unchanged. */
+int livo_ivox_add_points(livo_ctx* ctx, const float* xyz, int64_t n, int64_t stride_bytes);
+/* IVox::GetClosestPoint(pt, closest_pt, max_num, max_range) (ivox3d.h:132-204)
+ * for n host queries: idx / sqdist n*max_num in the reference's order (the
+ * nearest first), cnt[i] = neighbours found, -1 when there was no candidate
+ * (the reference returns false and leaves its output vector alone). */
+int livo_ivox_knn(livo_ctx* ctx, const float* q_xyz, int64_t n, int32_t max_num, double max_range, int32_t* idx,
+                  float* sqdist, int32_t* cnt);
+int livo_ivox_get_info(livo_ctx* ctx, livo_ivox_info* out);
+/* Every point, grid by grid (grid order unspecified, insertion order inside a
+ * grid): xyz n*3, ids n, keys n*3 (the grid of each point); any may be NULL.
+ * *n = points; LIVO_E_RANGE if cap < *n (nothing written). */
+int livo_ivox_dump(livo_ctx* ctx, float* xyz, int32_t* ids, int32_t* keys, int64_t cap, int64_t* n);
+
+/* LaserMapping::map_incremental, iVox branch (laser_mapping.cpp:329-389): the
+ * scan's points at `state` (the updated state), the add / no-downsample / skip
+ * decision from the scan's neighbour cache, then AddPoints(points_to_add) and
+ * AddPoints(point_no_need_downsample) on the device.  cat (may be NULL): per
+ * point 0 skipped, 1 added, 2 added without downsampling; counts[2] = the two
+ * batch sizes.  ekf_inited = flg_EKF_inited.  iVox backend only. */
+int livo_map_incremental(livo_ctx* ctx, int32_t scan_id, const livo_state* state, double filter_size_map_min,
+                         int ekf_inited, uint8_t* cat, int64_t counts[2]);
+/* Nearest_Points.resize(N) between scans (laser_mapping.cpp:165) keeps the
+ * entries of the previous scan's points: dst's point i starts with src's
+ * point i's cache (empty for i >= src's size). */
+int livo_scan_inherit_neighbors(livo_ctx* ctx, int32_t dst_scan, int32_t src_scan);
 
 int livo_sync(livo_ctx* ctx);
 

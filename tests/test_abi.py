@@ -122,3 +122,28 @@ def test_ikfom_struct_layouts_match_c(tmp_path):
     assert got == want
     assert C.sizeof(oracle.OrcIkfomState) == C.sizeof(livo_amd.IkfomState)
     assert C.sizeof(oracle.OrcIkfomStats) == C.sizeof(livo_amd.IkfomStats)
+
+
+def test_ivox_abi_layouts_and_args(tmp_path, built):
+    import livo_amd
+    src = tmp_path / "iv.c"
+    src.write_text('#include "livo.h"\n#include <stdio.h>\n#include <stddef.h>\nint main(void){printf("%zu %zu %zu '
+                   '%d %d %d\\n", sizeof(livo_ivox_params), sizeof(livo_ivox_info), offsetof(livo_ivox_params, '
+                   'capacity), LIVO_BACKEND_IKDTREE, LIVO_BACKEND_IVOX, LIVO_E_CAPACITY);return 0;}\n')
+    exe = tmp_path / "iv"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(src)])
+    got = [int(x) for x in subprocess.check_output([str(exe)]).split()]
+    assert got == [C.sizeof(livo_amd.IvoxParams), C.sizeof(livo_amd.IvoxInfo), livo_amd.IvoxParams.capacity.offset,
+                   livo_amd.BACKEND_IKDTREE, livo_amd.BACKEND_IVOX, -7]
+    L = livo_amd.load()
+    p = livo_amd.IvoxParams()
+    assert L.livo_ivox_params_default(C.byref(p)) == 0
+    # reference defaults: ivox_grid_resolution 0.2, NEARBY18 (laser_mapping.cpp:1021-1035), capacity 1e6
+    assert abs(p.resolution - 0.2) < 1e-7 and p.nearby_type == 18 and p.capacity == 1_000_000
+    assert L.livo_ivox_params_default(None) == -1
+    assert L.livo_ivox_init(None, None) == -1
+    assert L.livo_ctx_set_backend(None, 1) == -1
+    assert L.livo_ivox_add_points(None, None, 0, 0) == -1
+    assert L.livo_map_incremental(None, 0, None, 0.5, 1, None, None) == -1
+    assert L.livo_scan_inherit_neighbors(None, 0, 0) == -1
+    assert b"capacity" in L.livo_error_string(-7)

@@ -1,0 +1,310 @@
+"""GPU parity of the iVox backend and map_incremental.
+
+The HIP path (through the C ABI) against the CPU oracle's IVox restatement
+(oracle/livo_oracle.cpp, iVox section; pinned in tests/test_ivox_oracle.py):
+  * GetClosestPoint: neighbour ids, squared distances AND their order (the
+    order libstdc++'s nth_element leaves, which esti_plane's row order
+    depends on), and the no-candidate case: bit-exact;
+  * AddPoints: every grid's points, in insertion order: exact;
+  * h_share / IEKF / map_incremental with the iVox backend: same bars as the
+    ikd-Tree path (tests/test_gpu_parity.py): normals, flags, categories
+    bit-exact, state delta 1e-5 relative, counts exact.
+"""
+import collections
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REL_HTH = 1e-9
+REL_STATE = 1e-5
+
+
+def _synth():
+    from livo_amd import synth
+    return synth
+
+
+def _rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
+
+
+@pytest.fixture(scope="module")
+def ivctx(built):
+    import livo_amd
+    from livo_amd import synth
+    ctx = livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=4)
+    ctx.set_backend(livo_amd.BACKEND_IVOX)
+    yield ctx
+    ctx.close()
+
+
+def _pair(ctx, m, **kw):
+    import oracle
+    ctx.ivox_init(**kw)
+    iv = oracle.Ivox(**kw)
+    if m is not None and len(m):
+        ctx.ivox_add_points(m)
+        iv.add_points(m)
+    return iv
+
+
+def _world(body, st):
+    synth = _synth()
+    return ((body.astype(np.float64) + synth.T_LI) @ st["rot"].T + st["pos"]).astype(np.float32)
+
+
+def _knn_equal(ctx, iv, q, max_num=5, max_range=5.0):
+    gi, gd, gc = ctx.ivox_knn(q, max_num, max_range)
+    ri, rd, _, rc = iv.knn(q, max_num, max_range)
+    assert np.array_equal(gc, rc)
+    assert np.array_equal(gi, ri)
+    assert np.array_equal(gd.view(np.uint32), rd.view(np.uint32))
+    return gc
+
+
+def test_ivox_knn_bit_exact_room(ivctx):
+    synth = _synth()
+    iv = _pair(ivctx, synth.make_map(300_000))
+    info = ivctx.ivox_info()
+    ri = iv.info()
+    assert info["num_points"] == ri["num_points"] == 300_000
+    assert info["num_grids"] == ri["num_grids"]
+    body, _, _ = synth.make_scan(20_000, 3)
+    q = _world(body, synth.make_state(3))
+    cnt = _knn_equal(ivctx, iv, q)
+    assert (cnt == 5).mean() > 0.5 and (cnt == -1).sum() >= 0
+    rng = np.random.default_rng(1)
+    far = rng.uniform(-100, 100, size=(2000, 3)).astype(np.float32)  # mostly nothing found
+    cnt = _knn_equal(ivctx, iv, far)
+    assert (cnt == -1).mean() > 0.5
+
+
+@pytest.mark.parametrize("nearby,res,max_num,rng_m", [(0, 0.2, 5, 5.0), (6, 0.5, 3, 5.0), (26, 0.2, 5, 0.15),
+                                                      (18, 1.0, 1, 5.0)])
+def test_ivox_knn_options(ivctx, nearby, res, max_num, rng_m):
+    rng = np.random.default_rng(nearby)
+    m = rng.uniform(-4, 4, size=(60_000, 3)).astype(np.float32)
+    iv = _pair(ivctx, m, resolution=res, nearby_type=nearby)
+    q = rng.uniform(-4.5, 4.5, size=(8000, 3)).astype(np.float32)
+    _knn_equal(ivctx, iv, q, max_num, rng_m)
+
+
+def test_ivox_ties_and_dense_grids(ivctx):
+    """Exact distance ties (duplicates, lattices) — the order is nth_element's —
+    and grids far beyond the private candidate array (the overflow pass)."""
+    rng = np.random.default_rng(4)
+    lattice = (np.stack(np.meshgrid(*[np.arange(-10, 11)] * 3), -1).reshape(-1, 3) * 0.05).astype(np.float32)
+    dense = np.repeat(rng.uniform(-0.05, 0.05, size=(300, 3)).astype(np.float32), 3, axis=0)  # one grid, dups
+    m = np.concatenate([lattice, lattice[::7], dense, rng.uniform(-1, 1, size=(5000, 3)).astype(np.float32)])
+    iv = _pair(ivctx, m)
+    assert ivctx.ivox_info()["max_grid_points"] > 64
+    q = np.concatenate([lattice[::5] + np.float32(0.025), lattice[::11], rng.uniform(-0.6, 0.6, size=(3000, 3))])
+    _knn_equal(ivctx, iv, q.astype(np.float32))
+
+
+def _dump_by_grid(xyz, ids, keys):
+    g = collections.defaultdict(list)
+    for p, i, k in zip(xyz, ids, map(tuple, keys)):
+        g[k].append((int(i), tuple(p.tolist())))
+    return g
+
+
+def _oracle_by_grid(iv):
+    xyz, ids, gof, keys = iv.dump()
+    g = collections.defaultdict(list)
+    for p, i, go in zip(xyz, ids, gof):
+        g[tuple(keys[go])].append((int(i), tuple(p.tolist())))
+    return g
+
+
+def test_ivox_add_points_batches_match_oracle(ivctx):
+    rng = np.random.default_rng(8)
+    import oracle
+    ivctx.ivox_init(resolution=0.3, nearby_type=18)
+    iv = oracle.Ivox(resolution=0.3, nearby_type=18)
+    for n in (1, 0, 777, 5000, 1, 20000, 3):
+        pts = rng.normal(0, 2, size=(n, 3)).astype(np.float32)
+        ivctx.ivox_add_points(pts)
+        iv.add_points(pts)
+    assert _dump_by_grid(*ivctx.ivox_dump()) == _oracle_by_grid(iv)
+    assert ivctx.ivox_info()["ids_issued"] == iv.info()["ids_issued"]
+
+
+def test_ivox_capacity_leaves_map_unchanged(ivctx):
+    import livo_amd
+    rng = np.random.default_rng(2)
+    ivctx.ivox_init(resolution=0.5, nearby_type=6, capacity=200)
+    a = rng.uniform(-1, 1, size=(50, 3)).astype(np.float32)
+    ivctx.ivox_add_points(a)
+    before = ivctx.ivox_dump()
+    with pytest.raises(livo_amd.LivoError) as e:
+        ivctx.ivox_add_points(rng.uniform(-50, 50, size=(5000, 3)).astype(np.float32))
+    assert e.value.code == -7
+    after = ivctx.ivox_dump()
+    assert all(np.array_equal(x, y) for x, y in zip(before, after))
+    assert ivctx.ivox_info()["ids_issued"] == 50
+
+
+def _hs_equal(g, r):
+    assert np.array_equal(g["nn_idx"], r["cache"]["idx"])
+    assert np.array_equal(g["nn_d"].view(np.uint32), r["cache"]["d"].view(np.uint32))
+    assert np.array_equal(g["normvec"].view(np.uint32), r["normvec"].view(np.uint32))
+    assert np.array_equal(g["sel"], r["sel"])
+    assert g["effct"] == r["effct"]
+    assert _rel(g["HTH"], r["HTH"]) < REL_HTH
+    assert _rel(g["HTL"], r["HTL"]) < REL_HTH
+
+
+def test_ivox_h_share_parity(ivctx):
+    import oracle
+    synth = _synth()
+    iv = _pair(ivctx, synth.make_map(1_000_000))
+    body, _, _ = synth.make_scan(20_000, 5)
+    st = synth.make_state(5)
+    sid = ivctx.scan_upload(body)
+    try:
+        cache = oracle.new_cache(len(body))
+        g = ivctx.h_share(sid, st, search_en=True)
+        r = iv.h_share(body, st["rot"], st["pos"], np.eye(3), synth.T_LI, True, cache)
+        _hs_equal(g, r)
+        assert g["effct"] > 5000
+        st2 = dict(st)
+        st2["pos"] = st["pos"] + np.array([0.02, 0.01, -0.01])
+        g2 = ivctx.h_share(sid, st2, search_en=False)
+        r2 = iv.h_share(body, st2["rot"], st2["pos"], np.eye(3), synth.T_LI, False, r["cache"])
+        _hs_equal(g2, r2)
+    finally:
+        ivctx.scan_release(sid)
+
+
+def _iekf_check(stg, sg, str_, sr, st0):
+    assert stg["iterations"] == str_["iterations"]
+    assert stg["knn_passes"] == str_["knn_passes"]
+    assert stg["converged"] == str_["converged"]
+    assert stg["effct_feat_num"] == str_["effct_feat_num"]
+    for e in range(stg["iterations"]):
+        assert _rel(stg["solution"][e], str_["solution"][e]) < REL_STATE, e
+    assert _rel(sg["pos"] - st0["pos"], sr["pos"] - st0["pos"]) < REL_STATE
+    assert np.linalg.norm(sg["cov"] - sr["cov"]) / np.linalg.norm(st0["cov"]) < 1e-9
+
+
+@pytest.mark.parametrize("max_iter", [4, 2, 0])
+def test_ivox_iekf_parity(ivctx, max_iter):
+    import oracle
+    synth = _synth()
+    iv = _pair(ivctx, synth.make_map(1_000_000))
+    ivctx.set_params(max_iterations=max_iter)
+    try:
+        for scan in (6, 7):
+            body, _, _ = synth.make_scan(30_000, scan)
+            st0 = synth.make_state(scan)
+            sid = ivctx.scan_upload(body)
+            try:
+                sg, stg = ivctx.iekf_update(sid, st0)
+            finally:
+                ivctx.scan_release(sid)
+            sr, str_ = iv.iekf_update(body, st0, oracle.new_cache(len(body)), t_LI=synth.T_LI, max_iter=max_iter)
+            _iekf_check(stg, sg, str_, sr, st0)
+    finally:
+        ivctx.set_params(max_iterations=4)
+
+
+def test_ivox_batch_equals_single(ivctx):
+    synth = _synth()
+    _pair(ivctx, synth.make_map(300_000))
+    bodies = [synth.make_scan(n, 10 + k)[0] for k, n in enumerate((9_000, 1, 0, 12_345, 700))]
+    sts = [synth.make_state(10 + k) for k in range(len(bodies))]
+    # fresh uploads for the batch: a point with no candidate keeps its cached
+    # neighbours (ivox3d.h:165-167), so a second update of the same scan differs
+    sids = [ivctx.scan_upload(b) for b in bodies]
+    sids2 = [ivctx.scan_upload(b) for b in bodies]
+    try:
+        singles = [ivctx.iekf_update(s, st) for s, st in zip(sids, sts)]
+        batch_states, batch_stats = ivctx.iekf_update_batch(sids2, sts)
+        for (s1, t1), s2, t2 in zip(singles, batch_states, batch_stats):
+            assert t1["iterations"] == t2["iterations"] and t1["effct_feat_num"] == t2["effct_feat_num"]
+            assert np.array_equal(s1["pos"], s2["pos"]) and np.array_equal(s1["rot"], s2["rot"])
+    finally:
+        for s in sids + sids2:
+            ivctx.scan_release(s)
+
+
+def test_map_incremental_and_odometry_sequence(ivctx):
+    """First scan -> AddPoints(body) (laser_mapping.cpp:145-150); every later scan:
+    Nearest_Points carried over by index, the IEKF update, map_incremental;
+    states, categories and the whole map compared after every scan."""
+    import oracle
+    synth = _synth()
+    ivctx.ivox_init()
+    iv = oracle.Ivox()
+    base = synth.make_map(200_000)
+    ivctx.ivox_add_points(base)
+    iv.add_points(base)
+    first, _, _ = synth.make_scan(8_000, 20)
+    ivctx.ivox_add_points(first)
+    iv.add_points(first)
+    prev_sid, cache = None, oracle.new_cache(0)
+    for k, n in enumerate((10_000, 7_000, 12_000, 12_000)):
+        body, _, _ = synth.make_scan(n, 21 + k)
+        st0 = synth.make_state(21 + k)
+        sid = ivctx.scan_upload(body)
+        if prev_sid is not None:
+            ivctx.scan_inherit_neighbors(sid, prev_sid)
+            ivctx.scan_release(prev_sid)
+        cache = oracle.resize_cache(cache, n)
+        sg, stg = ivctx.iekf_update(sid, st0)
+        sr, str_ = iv.iekf_update(body, st0, cache, t_LI=synth.T_LI)
+        _iekf_check(stg, sg, str_, sr, st0)
+        gi, _ = ivctx.scan_neighbors(sid)
+        assert np.array_equal(gi, cache["idx"])
+        # map_incremental at the (oracle's) updated state: identical inputs on both sides
+        cat_g, cnt_g = ivctx.map_incremental(sid, sr, filter_size_map=0.5)
+        cat_r, cnt_r = iv.map_incremental(body, sr, cache, t_LI=synth.T_LI, filter_size_map=0.5)
+        assert np.array_equal(cat_g, cat_r) and cnt_g == cnt_r
+        assert cnt_g["added"] > 0
+        prev_sid = sid
+    ivctx.scan_release(prev_sid)
+    assert ivctx.ivox_info()["num_points"] == iv.info()["num_points"]
+    assert _dump_by_grid(*ivctx.ivox_dump()) == _oracle_by_grid(iv)
+
+
+def test_map_incremental_not_inited_adds_all(ivctx):
+    import oracle
+    synth = _synth()
+    iv = _pair(ivctx, synth.make_map(100_000))
+    body, _, _ = synth.make_scan(3_000, 30)
+    st = synth.make_state(30)
+    sid = ivctx.scan_upload(body)
+    try:
+        ivctx.h_share(sid, st, search_en=True)
+        cat, cnt = ivctx.map_incremental(sid, st, ekf_inited=False)
+        assert np.all(cat == 1) and cnt == {"added": 3000, "no_downsample": 0}
+        cache = oracle.new_cache(len(body))
+        iv.h_share(body, st["rot"], st["pos"], np.eye(3), synth.T_LI, True, cache)
+        iv.map_incremental(body, st, cache, t_LI=synth.T_LI, ekf_inited=False)
+        assert _dump_by_grid(*ivctx.ivox_dump()) == _oracle_by_grid(iv)
+    finally:
+        ivctx.scan_release(sid)
+
+
+def test_ivox_backend_args(ivctx):
+    import livo_amd
+    with pytest.raises(livo_amd.LivoError):
+        ivctx.ivox_init(nearby_type=5)
+    with pytest.raises(livo_amd.LivoError):
+        ivctx.set_backend(7)
+    ivctx.ivox_init()
+    with pytest.raises(livo_amd.LivoError):
+        ivctx.ivox_knn(np.zeros((1, 3), np.float32), max_num=6)
+    # IKFoM runs on the ikd-Tree h-model only
+    synth = _synth()
+    sid = ivctx.scan_upload(synth.make_scan(100, 0)[0])
+    try:
+        with pytest.raises(livo_amd.LivoError):
+            ivctx.ikfom_update(sid, synth.make_ikfom_state(0))
+    finally:
+        ivctx.scan_release(sid)
