@@ -49,8 +49,11 @@ B_JAC = 28
 
 
 def knn_kernel_desc():
-    return ("first-evaluation k-NN of the batch (both streams): k_knn_leaf<false> (transform + exact 5-NN of "
-            "every point on the leaf map) + k_knn_replay (PointType_CMP-ambiguous queries on the ikd-Tree)")
+    if os.environ.get("LIVO_KNN_KIND") == "leaf":
+        return ("first-evaluation k-NN of the batch (4 stream groups): k_knn_leaf<false> (transform + exact 5-NN "
+                "of every point on the leaf map) + k_knn_replay (PointType_CMP-ambiguous queries on the ikd-Tree)")
+    return ("first-evaluation k-NN of the batch (4 stream groups): k_knn_grid<false> (transform + exact 5-NN of "
+            "every point on the cell grid) + k_knn_replay (PointType_CMP-ambiguous queries on the ikd-Tree)")
 
 
 def parse():
@@ -251,6 +254,68 @@ def main():
                            "note": "livo_ikfom_update_batch (state_ikfom, esekfom.hpp:1619-1928) on the same "
                                    f"{a.batch} scans per GPU, {ik_steps} steps after the headline run"}
 
+    # ---- the iVox backend (the reference's default build):
+    # the same scans against the same 1M points inserted with IVox::AddPoints,
+    # then a sequential odometry loop (scan update + map_incremental per scan)
+    ctx.set_backend(livo_amd.BACKEND_IVOX)
+    t = time.perf_counter()
+    ctx.ivox_init()
+    ctx.ivox_add_points(m)
+    iv_build_s = time.perf_counter() - t
+    iv_info = ctx.ivox_info()
+    # fresh scan buffers: a point without iVox candidates keeps its cached
+    # neighbours (ivox3d.h:165-167), so the first update starts from empty caches
+    iv_sids = [ctx.scan_upload(sc) for sc in scans]
+
+    def iv_step():
+        C.memmove(work, init, nbytes)
+        return ctx.iekf_update_batch(iv_sids, work, raw=True)[1]
+
+    iv_first = [livo_amd.stats_from_c(s) for s in iv_step()]
+    for _ in range(2):
+        iv_step()
+    iv_steps = max(5, a.steps // 2)
+    sync()
+    t = time.perf_counter()
+    iv_evals = 0
+    for _ in range(iv_steps):
+        iv_evals += sum(s.iterations for s in iv_step())
+    sync()
+    iv_elapsed = farm.allreduce_max(time.perf_counter() - t, coll_dev)
+    iv_total = farm.allreduce_counters(farm.Counters(scans=iv_steps * a.batch, evals=iv_evals), coll_dev)
+    # odometry: one scan after the other, each updated then merged into the map
+    odo_sids = [ctx.scan_upload(sc) for sc in scans]
+    sync()
+    t = time.perf_counter()
+    t_incr = 0.0
+    added = 0
+    for sid, s in zip(odo_sids, st0):
+        st, _ = ctx.iekf_update(sid, s)
+        t1 = time.perf_counter()
+        _, cnt = ctx.map_incremental(sid, st, filter_size_map=0.5)
+        t_incr += time.perf_counter() - t1
+        added += cnt["added"] + cnt["no_downsample"]
+    sync()
+    odo_elapsed = time.perf_counter() - t
+    for sid in odo_sids + iv_sids:
+        ctx.scan_release(sid)
+    ctx.set_backend(livo_amd.BACKEND_IKDTREE)
+    if rank == 0:
+        result["ivox"] = {
+            "updates_per_s": round(iv_total.scans / iv_elapsed, 3),
+            "ms_per_step": round(iv_elapsed / iv_steps * 1e3, 4),
+            "evals_per_scan": round(iv_total.evals / max(iv_total.scans, 1), 3),
+            "effct_first_eval_scan0": iv_first[0]["effct_feat_num"][0],
+            "map": {"points": iv_info["num_points"], "grids": iv_info["num_grids"],
+                    "max_grid_points": iv_info["max_grid_points"], "add_points_s": round(iv_build_s, 3)},
+            "odometry": {"scans_per_s": round(len(odo_sids) / odo_elapsed, 3),
+                         "ms_per_scan": round(odo_elapsed / len(odo_sids) * 1e3, 3),
+                         "map_incremental_ms_per_scan": round(t_incr / len(odo_sids) * 1e3, 3),
+                         "points_added_per_scan": round(added / len(odo_sids), 1),
+                         "note": "sequential: livo_iekf_update + livo_map_incremental per scan (map grows)"},
+            "note": "LIVO_BACKEND_IVOX: IVox GetClosestPoint (NEARBY18, 0.2 m grids, 5 m range) on the same "
+                    f"{a.batch} scans per GPU, {iv_steps} steps after the IKFoM run; not part of `value`"}
+
     # ---- CPU baseline: the oracle (CPU restatement), 1 thread, bounded sample; + parity of scan 0
     if rank == 0 and a.cpu_seconds > 0:
         import oracle
@@ -286,6 +351,22 @@ def main():
         iscale = max(np.linalg.norm(d) for d in irs["dx"])  # relative to the scan's largest step
         irel = max(np.linalg.norm(ik_first["dx"][e] - irs["dx"][e]) / iscale
                    for e in range(min(ik_first["iterations"], irs["iterations"])))
+        # the iVox backend: one CPU scan update (1 thread) and parity of scan 0
+        ivo = oracle.Ivox()
+        ivo.add_points(m)
+        t = time.perf_counter()
+        ivs, ivst = ivo.iekf_update(scans[0], st0[0], oracle.new_cache(len(scans[0])), t_LI=synth.T_LI,
+                                    max_iter=a.max_iter, threads=1)
+        iv_cpu_s = time.perf_counter() - t
+        ig = iv_first[0]
+        ivrel = max(np.linalg.norm(ig["solution"][e] - ivst["solution"][e]) / np.linalg.norm(ivst["solution"][e])
+                    for e in range(min(ig["iterations"], ivst["iterations"])))
+        result["ivox"]["cpu_baseline"] = {"value": round(1.0 / iv_cpu_s, 4), "unit": "scan updates/s", "cores": 1,
+                                          "kind": "port", "sample": "1 full scan update of scan 0 by oracle/ (IVox "
+                                                                    f"restatement), 1 thread, {iv_cpu_s:.2f} s"}
+        result["ivox"]["parity_scan0"] = {"iterations_equal": ig["iterations"] == ivst["iterations"],
+                                          "effct_equal": ig["effct_feat_num"] == ivst["effct_feat_num"],
+                                          "max_rel_state_delta": float(f"{ivrel:.3e}")}
         result["ikfom"]["parity_scan0"] = {"iterations_equal": ik_first["iterations"] == irs["iterations"],
                                            "effct_equal": ik_first["effct_feat_num"] == irs["effct_feat_num"],
                                            "max_dx_error_rel_to_largest_step": float(f"{irel:.3e}")}

@@ -80,10 +80,32 @@ __device__ __forceinline__ int iv_query(const IvoxParams& V, float qx, float qy,
         return 0;
     const float4* __restrict__ pts = reinterpret_cast<const float4*>(V.pts);
     const int K = V.max_num;
+    // the next grid's first hash slot is loaded while the current grid is
+    // processed (probe chains are short: load factor <= 1/2)
+    const uint64_t mask = (1ull << V.log2) - 1ull;
+    auto key_of = [&](int t) {
+        return iv_key(kx + c_nearby[t][0], ky + c_nearby[t][1], kz + c_nearby[t][2]);
+    };
+    unsigned long long nkey = key_of(0);
+    uint64_t nsl = iv_hash(nkey, V.log2);
+    GridSlot ngs = V.slots[nsl];
     int n = 0;
 #pragma unroll 1
     for (int t = 0; t < V.nearby; t++) {
-        const uint2 run = iv_lookup(V.slots, V.log2, iv_key(kx + c_nearby[t][0], ky + c_nearby[t][1], kz + c_nearby[t][2]));
+        const unsigned long long key = nkey;
+        uint64_t sl = nsl;
+        GridSlot gs = ngs;
+        if (t + 1 < V.nearby) {
+            nkey = key_of(t + 1);
+            nsl = iv_hash(nkey, V.log2);
+            ngs = V.slots[nsl];
+        }
+        while (gs.key != key && gs.key != kGridEmpty) {
+            sl = (sl + 1) & mask;
+            gs = V.slots[sl];
+        }
+        if (gs.key != key) continue;
+        const uint2 run = make_uint2(gs.start, gs.count);
         const int old = n;
 #pragma unroll 1
         for (uint32_t k = 0; k < run.y; k++) {

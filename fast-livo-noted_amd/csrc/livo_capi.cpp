@@ -422,13 +422,13 @@ static int ivox_ensure_big(livo_ctx* c) {
     IvoxDev& v = c->iv;
     const int64_t slice = (int64_t)v.nearby * kNN + v.max_grid + 8;
     if (slice <= v.big_slice && v.big) return LIVO_OK;
-    const int64_t budget = (int64_t)1 << 30;  // 1 GiB
+    const int64_t budget = (int64_t)1 << 28;  // 256 MiB per stream group
     int64_t threads = budget / (slice * (int64_t)sizeof(SelElem));
     threads = std::max<int64_t>(64, std::min<int64_t>(16384, threads)) / 64 * 64;
     dev_free(v.big);
     v.big_slice = 0;
     v.big_threads = 0;
-    if (dev_alloc(&v.big, (size_t)(threads * slice))) return LIVO_E_OOM;
+    if (dev_alloc(&v.big, (size_t)(kMaxGroups * threads * slice))) return LIVO_E_OOM;  // one set per stream group
     v.big_slice = slice;
     v.big_threads = threads;
     return LIVO_OK;
@@ -1025,6 +1025,8 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
         kp[gi].jobs = c->d_jobs + g[gi].first;
         kp[gi].replay_count = c->d_replay_count + gi;
         kp[gi].replay_list = c->d_replay_list + g[gi].off;
+        // the iVox overflow pass of each group has its own scratch slices (groups run concurrently)
+        if (kp[gi].iv.scratch) kp[gi].iv.scratch += (int64_t)gi * c->iv.big_threads * c->iv.big_slice;
         hp[gi].solve = 1;  // the last plane-pass block of each scan runs its solve
         hp[gi].replay_count = c->d_replay_count + gi;
     }
@@ -1245,7 +1247,8 @@ int livo_ivox_get_info(livo_ctx* c, livo_ivox_info* out) {
     out->ids_issued = v.next_id;
     out->max_grid_points = v.max_grid;
     out->device_bytes = v.table * (int64_t)(sizeof(GridSlot) + 4 * sizeof(uint32_t)) +
-                        (v.pts_cap[0] + v.pts_cap[1]) * 16 + v.big_threads * v.big_slice * (int64_t)sizeof(SelElem);
+                        (v.pts_cap[0] + v.pts_cap[1]) * 16 +
+                        kMaxGroups * v.big_threads * v.big_slice * (int64_t)sizeof(SelElem);
     return LIVO_OK;
 }
 

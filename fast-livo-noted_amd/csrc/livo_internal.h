@@ -131,7 +131,7 @@ void free_grid_map(HostGridMap* m);
 // ---------------------------------------------------------------------------
 constexpr int kIvBias = 1 << 20;            // key bias (21 bits per axis)
 constexpr int kIvMaxKey = kIvBias - 64;     // |cell| limit of stored points
-constexpr int kIvCap = 64;                  // private candidates per query (k_ivox_knn); beyond: overflow pass
+constexpr int kIvCap = 128;                 // private candidates per query (k_ivox_knn); beyond: overflow pass
 constexpr int kIvMaxNearby = 27;
 
 struct IvoxParams {

@@ -308,3 +308,28 @@ def test_ivox_backend_args(ivctx):
             ivctx.ikfom_update(sid, synth.make_ikfom_state(0))
     finally:
         ivctx.scan_release(sid)
+
+
+def test_ivox_batch_overflow_groups(ivctx):
+    """Coarse grids (1 m: every query outgrows the private candidate array), a
+    batch split over concurrent stream groups: each group's overflow pass has
+    its own scratch; the batch equals single updates and the oracle."""
+    import oracle
+    synth = _synth()
+    iv = _pair(ivctx, synth.make_map(300_000), resolution=1.0)
+    assert ivctx.ivox_info()["max_grid_points"] > 128
+    bodies = [synth.make_scan(4_000, 40 + k)[0] for k in range(6)]
+    sts = [synth.make_state(40 + k) for k in range(6)]
+    sids = [ivctx.scan_upload(b) for b in bodies]
+    sids2 = [ivctx.scan_upload(b) for b in bodies]
+    try:
+        bs, bst = ivctx.iekf_update_batch(sids, sts)
+        for k in (0, 5):
+            s1, t1 = ivctx.iekf_update(sids2[k], sts[k])
+            assert t1["effct_feat_num"] == bst[k]["effct_feat_num"]
+            assert np.array_equal(s1["pos"], bs[k]["pos"])
+            sr, tr = iv.iekf_update(bodies[k], sts[k], oracle.new_cache(len(bodies[k])), t_LI=synth.T_LI)
+            _iekf_check(t1, s1, tr, sr, sts[k])
+    finally:
+        for s in sids + sids2:
+            ivctx.scan_release(s)
