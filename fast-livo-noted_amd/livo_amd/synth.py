@@ -283,3 +283,35 @@ def cached_map(n_points: int) -> np.ndarray:
     np.save(tmp, m)
     os.replace(tmp, path)
     return m
+
+
+def make_raw_scan(n_points: int, scan_id: int = 0, n_imu: int = 21, scene: Scene | None = None):
+    """A raw (not yet de-skewed) scan and the IMU poses of its frame.
+
+    Points (n, 5) float32: x, y, z, intensity, curvature = offset time in ms
+    (preprocess.cpp:346), sorted by time as the Livox handler delivers them.
+    poses (n_imu, 22) float64: Pose6D rows (offset_time s, acc, gyr, vel, pos,
+    rot), offset 0 first, one per 5 ms, a smooth synthetic motion.  Returns
+    (raw, poses, rot_end, pos_end).
+    """
+    body, R, p = make_scan(n_points, scan_id, scene)
+    rng = np.random.default_rng(SEED_SCAN + 7919 * (scan_id + 1))
+    t_ms = np.sort(rng.uniform(0.0, 100.0, size=n_points)).astype(np.float32)
+    inten = rng.uniform(0, 255, size=n_points).astype(np.float32)
+    raw = np.concatenate([body, inten[:, None], t_ms[:, None]], axis=1).astype(np.float32)
+    w = rng.normal(0, 0.3, size=3)          # rad/s
+    v = rng.normal(0, 1.0, size=3)          # m/s
+    acc = rng.normal(0, 0.2, size=3)
+    poses = np.zeros((n_imu, 22))
+    for k in range(n_imu):
+        t = 0.005 * k
+        poses[k, 0] = t
+        poses[k, 1:4] = acc
+        poses[k, 4:7] = w + rng.normal(0, 0.01, size=3)
+        poses[k, 7:10] = v + acc * t
+        poses[k, 10:13] = p + v * t + 0.5 * acc * t * t
+        poses[k, 13:22] = (R @ so3_exp(w * t)).reshape(9)
+    t_end = 0.1
+    rot_end = R @ so3_exp(w * t_end)
+    pos_end = p + v * t_end + 0.5 * acc * t_end * t_end
+    return np.ascontiguousarray(raw), poses, rot_end, pos_end

@@ -371,3 +371,36 @@ class Ivox:
                                        _p(cache["cnt"]), filter_size_map, int(bool(ekf_inited)), _p(cat),
                                        _p(counts))
         return cat, {"added": int(counts[0]), "no_downsample": int(counts[1])}
+
+
+def _front_lib():
+    L = lib()
+    if not getattr(L, "_front", False):
+        L.orc_undistort.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                    C.c_void_p]
+        L.orc_voxel_grid.restype = C.c_int64
+        L.orc_voxel_grid.argtypes = [C.c_void_p, C.c_int64, C.c_float, C.c_void_p]
+        L._front = True
+    return L
+
+
+def undistort(raw, poses, rot_end, pos_end, R_LI=None, t_LI=None):
+    """UndistortPcl's backward propagation (IMU_Processing.cpp:340-378).
+    raw: (n, 5) float32 x, y, z, intensity, curvature(ms); poses: (m, 22) float64 Pose6D rows
+    (offset_time, acc3, gyr3, vel3, pos3, rot9).  Returns the compensated copy."""
+    out = np.ascontiguousarray(raw, np.float32).copy()
+    poses = np.ascontiguousarray(poses, np.float64).reshape(-1, 22)
+    R_LI = np.ascontiguousarray(np.eye(3) if R_LI is None else R_LI, np.float64)
+    t_LI = np.ascontiguousarray(np.zeros(3) if t_LI is None else t_LI, np.float64)
+    _front_lib().orc_undistort(_p(out), out.shape[0], _p(poses), poses.shape[0],
+                               _p(np.ascontiguousarray(rot_end, np.float64)),
+                               _p(np.ascontiguousarray(pos_end, np.float64)), _p(R_LI), _p(t_LI))
+    return out
+
+
+def voxel_grid(raw, leaf):
+    """PCL VoxelGrid (downsample_all_data_) of (n, 5) raw points -> (k, 5) centroids, ascending leaf index."""
+    raw = np.ascontiguousarray(raw, np.float32)
+    out = np.zeros_like(raw)
+    k = _front_lib().orc_voxel_grid(_p(raw), raw.shape[0], C.c_float(leaf), _p(out))
+    return out[:k].copy()
