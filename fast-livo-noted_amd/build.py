@@ -28,6 +28,7 @@ DEVICE = ["--offload-arch=" + ARCH, "-fhip-fp32-correctly-rounded-divide-sqrt", 
 SOURCES = [
     ("livo_kernels.hip", True),
     ("ivox_kernels.hip", True),
+    ("frontend_kernels.hip", True),
     ("prims.hip", True),
     ("livo_capi.cpp", False),
     ("map_build.cpp", False),

@@ -1,0 +1,262 @@
+// frontend_kernels.hip — CDNA4 (gfx950) kernels of the scan front-end
+// (SURVEY.md §8f row 3): the per-point work between the raw LiDAR frame and
+// the resident scan the IEKF reads (feats_down_body).
+//
+//   k_fe_segment / k_fe_undistort   ImuProcess::UndistortPcl's backward
+//       propagation (IMU_Processing.cpp:340-378).  The reference walks points
+//       and IMU segments backwards together; with non-decreasing segment
+//       times a point's segment is the suffix minimum over later points of
+//       "last segment starting before me" (k_fe_segment + a min-scan), so
+//       every point is moved independently.  The first point is moved once
+//       per remaining segment, as the reference's walk does (its inner loop
+//       breaks at begin() without stepping): one thread chains those moves.
+//   k_fe_minmax / k_fe_leaf / k_fe_runs / k_fe_centroid   PCL VoxelGrid::
+//       applyFilter (downSizeFilterSurf, laser_mapping.cpp:129-130): bounds,
+//       32-bit leaf index per point, a stable radix sort by leaf, one centroid
+//       per run in ascending leaf order.  (PCL sums a voxel in std::sort's
+//       unstable order; here in input order: centroids agree to float
+//       rounding, voxels and counts exactly.)
+//   k_fe_morton / k_fe_gather        the resident scan's Morton order, the
+//       same keys and stable order as livo_scan_upload's host sort.
+//
+// Numerics: -ffp-contract=off; doubles in the reference's expression order.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "device_common.h"
+#include "livo_internal.h"
+
+namespace livo {
+
+// Pose6D (msg/Pose6D.msg): offset_time, acc[3], gyr[3], vel[3], pos[3], rot[9]
+constexpr int kPoseD = 22;
+
+__global__ void k_fe_segment(const float* __restrict__ raw, int64_t n, const double* __restrict__ poses, int np,
+                             int32_t* __restrict__ seg_rev) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double t = (double)raw[5 * i + 4] / double(1000);
+    // last head h in [0, np-2] with offset(h) < t, else -1 (offsets non-decreasing)
+    int lo = 0, hi = np - 1;  // answer in [lo - 1, hi - 1]
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (poses[(int64_t)mid * kPoseD] < t)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    seg_rev[n - 1 - i] = lo - 1;  // reversed: a prefix min-scan gives the suffix minimum
+}
+
+// Exp(ang_vel, dt) (so3_math.h:31-52)
+__device__ __forceinline__ void so3_exp_dt(const double* g, double dt, double* R) {
+    const double nrm = sqrt((g[0] * g[0] + g[1] * g[1]) + g[2] * g[2]);
+#pragma unroll
+    for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0) ? 1.0 : 0.0;
+    if (nrm > 0.0000001) {
+        const double r[3] = {g[0] / nrm, g[1] / nrm, g[2] / nrm};
+        const double K[9] = {0.0, -r[2], r[1], r[2], 0.0, -r[0], -r[1], r[0], 0.0};
+        const double ang = nrm * dt;
+        const double s = sin(ang), c1 = 1.0 - cos(ang);
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                const double kk = ((c1 * K[i * 3 + 0]) * K[0 * 3 + j] + (c1 * K[i * 3 + 1]) * K[1 * 3 + j]) +
+                                  (c1 * K[i * 3 + 2]) * K[2 * 3 + j];
+                R[i * 3 + j] = (R[i * 3 + j] + s * K[i * 3 + j]) + kk;
+            }
+    }
+}
+
+__device__ __forceinline__ void m3v(const double* M, const double* v, double* o) {
+#pragma unroll
+    for (int i = 0; i < 3; i++) o[i] = (M[i * 3 + 0] * v[0] + M[i * 3 + 1] * v[1]) + M[i * 3 + 2] * v[2];
+}
+
+// P_compensate = extR_Ri * (R_i * (R_LI * P_i + t_LI) + T_ei) - exrR_extT (IMU_Processing.cpp:356-370)
+__device__ void fe_compensate(float* p, const double* __restrict__ head, const FrontParams& F) {
+    const double dt = (double)p[4] / double(1000) - head[0];
+    double Re[9], Ri[9];
+    so3_exp_dt(head + 4, dt, Re);
+    const double* Rh = head + 13;
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+            Ri[i * 3 + j] = (Rh[i * 3 + 0] * Re[0 * 3 + j] + Rh[i * 3 + 1] * Re[1 * 3 + j]) + Rh[i * 3 + 2] * Re[2 * 3 + j];
+    double T[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+        T[k] = ((head[10 + k] + head[7 + k] * dt) + ((0.5 * head[1 + k]) * dt) * dt) - F.pos_end[k];
+    const double Pi[3] = {(double)p[0], (double)p[1], (double)p[2]};
+    double a[3], b[3], c[3];
+    m3v(F.R_LI, Pi, a);
+#pragma unroll
+    for (int k = 0; k < 3; k++) a[k] = a[k] + F.t_LI[k];
+    m3v(Ri, a, b);
+#pragma unroll
+    for (int k = 0; k < 3; k++) b[k] = b[k] + T[k];
+    m3v(F.extR_Ri, b, c);
+    p[0] = (float)(c[0] - F.exrR_extT[0]);
+    p[1] = (float)(c[1] - F.exrR_extT[1]);
+    p[2] = (float)(c[2] - F.exrR_extT[2]);
+}
+
+// seg_rev holds the prefix minimum of the reversed segments: point i's
+// segment is seg_rev[n-1-i] (-1: untouched).
+__global__ void k_fe_undistort(FrontParams F) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= F.n) return;
+    const int h = F.seg_rev[F.n - 1 - i];
+    if (h < 0) return;
+    float p[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) p[k] = F.raw[5 * i + k];
+    if (i == 0) {
+        // the walk's inner loop breaks at begin() without stepping, so every
+        // earlier segment moves the first point again
+        for (int hh = h; hh >= 0; hh--) fe_compensate(p, F.poses + (int64_t)hh * kPoseD, F);
+    } else {
+        fe_compensate(p, F.poses + (int64_t)h * kPoseD, F);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; k++) F.raw[5 * i + k] = p[k];
+}
+
+// Order-preserving float <-> uint mapping for atomic min / max.
+__device__ __forceinline__ unsigned f2o(float f) {
+    const unsigned u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// minmax[0..2] = ordered min of x, y, z; [3..5] = ordered max (initialised to
+// 0xFFFFFFFF / 0 by the caller).  stride: floats per point.
+__global__ void k_fe_minmax(const float* __restrict__ pts, int64_t n, int stride, unsigned* minmax) {
+    unsigned mn[3] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu}, mx[3] = {0u, 0u, 0u};
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const unsigned o = f2o(pts[stride * i + k]);
+            mn[k] = min(mn[k], o);
+            mx[k] = max(mx[k], o);
+        }
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            mn[k] = min(mn[k], (unsigned)__shfl_xor((int)mn[k], off, 64));
+            mx[k] = max(mx[k], (unsigned)__shfl_xor((int)mx[k], off, 64));
+        }
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            atomicMin(minmax + k, mn[k]);
+            atomicMax(minmax + 3 + k, mx[k]);
+        }
+}
+
+// PCL leaf index (voxel_grid.hpp): ijk = int(floor(p * inv) - float(min_b)), idx = ijk . divb_mul
+__global__ void k_fe_leaf(FrontParams F) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= F.n) return;
+    const float inv = F.inv_leaf;
+    const int ijk0 = (int)(floorf(F.raw[5 * i + 0] * inv) - (float)F.min_b[0]);
+    const int ijk1 = (int)(floorf(F.raw[5 * i + 1] * inv) - (float)F.min_b[1]);
+    const int ijk2 = (int)(floorf(F.raw[5 * i + 2] * inv) - (float)F.min_b[2]);
+    F.keys[i] = (uint32_t)(ijk0 * F.divb_mul[0] + ijk1 * F.divb_mul[1] + ijk2 * F.divb_mul[2]);
+    F.iota[i] = (uint32_t)i;
+}
+
+// flags[k] = 1 where a new leaf starts in the sorted order
+__global__ void k_fe_runs(FrontParams F) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= F.n) return;
+    F.flags[k] = (k == 0 || F.skeys[k] != F.skeys[k - 1]) ? 1u : 0u;
+}
+
+__global__ void k_fe_starts(FrontParams F) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= F.n) return;
+    if (F.flags[k]) F.starts[F.vid[k]] = (uint32_t)k;
+    if (k == F.n - 1) F.starts[F.vid[k] + F.flags[k]] = (uint32_t)F.n;
+}
+
+// CentroidPoint of one leaf (AccumulatorXYZ / Intensity / Curvature: float sums / n)
+__global__ void k_fe_centroid(FrontParams F, int64_t n_vox) {
+    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n_vox) return;
+    const uint32_t a = F.starts[v], b = F.starts[v + 1];
+    float s[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    for (uint32_t k = a; k < b; k++) {
+        const float* p = F.raw + 5 * (int64_t)F.svals[k];
+#pragma unroll
+        for (int c = 0; c < 5; c++) s[c] += p[c];
+    }
+    const float cnt = (float)(b - a);
+#pragma unroll
+    for (int c = 0; c < 5; c++) F.down[5 * v + c] = s[c] / cnt;
+}
+
+// livo_scan_upload's Morton key (0.25 m cells by default, 20 bits per axis)
+__global__ void k_fe_morton(const float* __restrict__ pts, int64_t n, int stride, const unsigned* minmax,
+                            float scale, unsigned long long* codes, uint32_t* iota) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    unsigned long long code = 0;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const unsigned o = minmax[a];
+        const float lo = __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
+        float f = (pts[stride * i + a] - lo) * scale;
+        if (!(f >= 0.0f)) f = 0.0f;
+        const uint32_t q = (uint32_t)fminf(f, 1048575.0f);
+#pragma unroll
+        for (int b = 0; b < 20; b++) code |= (unsigned long long)((q >> b) & 1u) << (3 * b + a);
+    }
+    codes[i] = code;
+    iota[i] = (uint32_t)i;
+}
+
+// the scan in stored order: pts4[k] = point perm[k]; iperm[perm[k]] = k
+__global__ void k_fe_gather(const float* __restrict__ pts, int64_t n, int stride, const uint32_t* __restrict__ perm,
+                            float* __restrict__ pts4, int32_t* __restrict__ iperm) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint32_t j = perm[k];
+    reinterpret_cast<float4*>(pts4)[k] =
+        make_float4(pts[stride * (int64_t)j], pts[stride * (int64_t)j + 1], pts[stride * (int64_t)j + 2], 0.f);
+    iperm[j] = (int32_t)k;
+}
+
+static inline dim3 fe_blocks(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }
+#define FE_LAUNCH(kernel, n, ...)                                                                   \
+    do {                                                                                            \
+        if ((n) <= 0) return LIVO_OK;                                                               \
+        hipLaunchKernelGGL(kernel, fe_blocks(n), dim3(256), 0, (hipStream_t)stream, __VA_ARGS__); \
+        return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;                              \
+    } while (0)
+
+int launch_fe_segment(const FrontParams& F, void* stream) {
+    FE_LAUNCH(k_fe_segment, F.n, F.raw, F.n, F.poses, F.np, F.seg);
+}
+int launch_fe_undistort(const FrontParams& F, void* stream) { FE_LAUNCH(k_fe_undistort, F.n, F); }
+int launch_fe_minmax(const float* pts, int64_t n, int stride, unsigned* minmax, void* stream) {
+    if (n <= 0) return LIVO_OK;
+    const unsigned blocks = (unsigned)std::min<int64_t>(1024, (n + 255) / 256);
+    hipLaunchKernelGGL(k_fe_minmax, dim3(blocks), dim3(256), 0, (hipStream_t)stream, pts, n, stride, minmax);
+    return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+int launch_fe_leaf(const FrontParams& F, void* stream) { FE_LAUNCH(k_fe_leaf, F.n, F); }
+int launch_fe_runs(const FrontParams& F, void* stream) { FE_LAUNCH(k_fe_runs, F.n, F); }
+int launch_fe_starts(const FrontParams& F, void* stream) { FE_LAUNCH(k_fe_starts, F.n, F); }
+int launch_fe_centroid(const FrontParams& F, int64_t n_vox, void* stream) { FE_LAUNCH(k_fe_centroid, n_vox, F, n_vox); }
+int launch_fe_morton(const float* pts, int64_t n, int stride, const unsigned* minmax, float scale,
+                     unsigned long long* codes, uint32_t* iota, void* stream) {
+    FE_LAUNCH(k_fe_morton, n, pts, n, stride, minmax, scale, codes, iota);
+}
+int launch_fe_gather(const float* pts, int64_t n, int stride, const uint32_t* perm, float* pts4, int32_t* iperm,
+                     void* stream) {
+    FE_LAUNCH(k_fe_gather, n, pts, n, stride, perm, pts4, iperm);
+}
+}  // namespace livo

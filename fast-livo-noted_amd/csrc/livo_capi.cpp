@@ -75,8 +75,6 @@ struct IvoxDev {
     float* src = nullptr;
     uint32_t *slot_of = nullptr, *iota = nullptr, *skeys = nullptr, *svals = nullptr;
     int64_t src_cap = 0;
-    void* prim_tmp = nullptr;
-    size_t prim_bytes = 0;
     // overflow pass of the search
     SelElem* big = nullptr;
     int64_t big_threads = 0, big_slice = 0;
@@ -112,6 +110,10 @@ struct livo_ctx {
     bool has_map = false;
     int backend = LIVO_BACKEND_IKDTREE;  // search structure of h_share / the IEKF loop
     IvoxDev iv;                        // iVox map (LIVO_BACKEND_IVOX)
+    void* fe_buf = nullptr;            // scan front-end scratch (livo_scan_preprocess)
+    size_t fe_bytes = 0;
+    void* prim_tmp = nullptr;          // rocPRIM scratch (sorts, scans)
+    size_t prim_bytes = 0;
     // scans
     std::vector<ScanBuf> scans;
     // batch resources
@@ -225,13 +227,19 @@ static int knn_pass(const KnnParams& kp, int n_jobs, int64_t max_n, hipStream_t 
     return launch_knn_pass(kp, n_jobs, max_n, st);
 }
 
-// Morton (Z-order) permutation of the body points: 0.25 m cells, 10 bits/axis.
-static std::vector<int32_t> morton_order(const std::vector<float>& p4, int64_t n) {
+static float morton_scale() {
     static const float scale = [] {  // cells per metre (LIVO_MORTON_SCALE tuning knob)
         const char* e = std::getenv("LIVO_MORTON_SCALE");
         const float v = e ? (float)std::atof(e) : 4.0f;
         return v > 0.0f ? v : 4.0f;
     }();
+    return scale;
+}
+
+// Morton (Z-order) permutation of the body points: 0.25 m cells, 20 bits/axis.
+// (k_fe_morton computes the same keys on the device for livo_scan_preprocess.)
+static std::vector<int32_t> morton_order(const std::vector<float>& p4, int64_t n) {
+    const float scale = morton_scale();
     std::vector<std::pair<uint64_t, int32_t>> key((size_t)n);
     float lo[3] = {INFINITY, INFINITY, INFINITY};
     for (int64_t i = 0; i < n; i++)
@@ -321,7 +329,6 @@ static void ivox_free(IvoxDev& v) {
     dev_free(v.pts[0]); dev_free(v.pts[1]);
     dev_free(v.ctr);
     dev_free(v.src); dev_free(v.slot_of); dev_free(v.iota); dev_free(v.skeys); dev_free(v.svals);
-    if (v.prim_tmp) (void)hipFree(v.prim_tmp);
     dev_free(v.big);
     v = IvoxDev{};
 }
@@ -368,14 +375,13 @@ static int ivox_ensure_src(livo_ctx* c, int64_t n) {
     return LIVO_OK;
 }
 
-static int ivox_ensure_prim(livo_ctx* c, size_t bytes) {
-    IvoxDev& v = c->iv;
-    if (bytes <= v.prim_bytes) return LIVO_OK;
-    if (v.prim_tmp) (void)hipFree(v.prim_tmp);
-    v.prim_tmp = nullptr;
-    v.prim_bytes = 0;
-    if (hipMalloc(&v.prim_tmp, bytes) != hipSuccess) return LIVO_E_OOM;
-    v.prim_bytes = bytes;
+static int ensure_prim(livo_ctx* c, size_t bytes) {
+    if (bytes <= c->prim_bytes) return LIVO_OK;
+    if (c->prim_tmp) (void)hipFree(c->prim_tmp);
+    c->prim_tmp = nullptr;
+    c->prim_bytes = 0;
+    if (hipMalloc(&c->prim_tmp, bytes) != hipSuccess) return LIVO_E_OOM;
+    c->prim_bytes = bytes;
     return LIVO_OK;
 }
 
@@ -383,9 +389,9 @@ static int ivox_ensure_prim(livo_ctx* c, size_t bytes) {
 static int ivox_scan(livo_ctx* c, const uint32_t* in, uint32_t* out, int64_t n) {
     size_t tb = 0;
     int rc = prim_exclusive_scan_u32(nullptr, &tb, in, out, n, c->stream);
-    if (!rc) rc = ivox_ensure_prim(c, tb);
-    tb = c->iv.prim_bytes;
-    if (!rc) rc = prim_exclusive_scan_u32(c->iv.prim_tmp, &tb, in, out, n, c->stream);
+    if (!rc) rc = ensure_prim(c, tb);
+    tb = c->prim_bytes;
+    if (!rc) rc = prim_exclusive_scan_u32(c->prim_tmp, &tb, in, out, n, c->stream);
     return rc;
 }
 
@@ -476,9 +482,9 @@ static int ivox_add_dev(livo_ctx* c, int64_t n) {
         while (((int64_t)1 << bits) <= v.table) bits++;  // the out-of-range key `table` included
         size_t tb = 0;
         rc = prim_sort_pairs_u32(nullptr, &tb, v.slot_of, v.skeys, v.iota, v.svals, n, bits, c->stream);
-        if (!rc) rc = ivox_ensure_prim(c, tb);
-        tb = v.prim_bytes;
-        if (!rc) rc = prim_sort_pairs_u32(v.prim_tmp, &tb, v.slot_of, v.skeys, v.iota, v.svals, n, bits, c->stream);
+        if (!rc) rc = ensure_prim(c, tb);
+        tb = c->prim_bytes;
+        if (!rc) rc = prim_sort_pairs_u32(c->prim_tmp, &tb, v.slot_of, v.skeys, v.iota, v.svals, n, bits, c->stream);
     }
     if (!rc) rc = launch_ivox_move(P, c->stream);
     if (!rc) rc = launch_ivox_place(P, c->stream);
@@ -582,6 +588,8 @@ int livo_ctx_destroy(livo_ctx* c) {
         dev_free(s.d_perm); dev_free(s.d_iperm);
     }
     ivox_free(c->iv);
+    if (c->fe_buf) (void)hipFree(c->fe_buf);
+    if (c->prim_tmp) (void)hipFree(c->prim_tmp);
     dev_free(c->nodes);
     dev_free(c->lnodes);
     dev_free(c->lpts);
@@ -754,6 +762,74 @@ int livo_knn(livo_ctx* c, const float* q, int64_t n, int32_t k, int32_t* idx, fl
     return LIVO_OK;
 }
 
+static int32_t register_scan(livo_ctx* c, const ScanBuf& s) {
+    int32_t id = -1;
+    for (size_t i = 0; i < c->scans.size(); i++)
+        if (!c->scans[i].used) { id = (int32_t)i; break; }
+    if (id < 0) {
+        id = (int32_t)c->scans.size();
+        c->scans.push_back(s);
+    } else {
+        c->scans[id] = s;
+    }
+    return id;
+}
+
+static void free_scan_buf(ScanBuf& s) {
+    dev_free(s.pts); dev_free(s.nn); dev_free(s.partial); dev_free(s.d_perm); dev_free(s.d_iperm);
+}
+
+// A resident scan from N device points (x, y, z at d_src + stride * i floats):
+// the same Morton order as livo_scan_upload's host sort, computed on the device.
+static int scan_create_device(livo_ctx* c, const float* d_src, int stride, int64_t N, int32_t* scan_id) {
+    ScanBuf s;
+    s.used = true;
+    s.n = N;
+    s.nblk = (int32_t)std::max<int64_t>(1, (N + kBlock * kPtsPerThread - 1) / (kBlock * kPtsPerThread));
+    int rc = 0;
+    rc |= dev_alloc(&s.pts, (size_t)N * 4);
+    rc |= dev_alloc(&s.nn, (size_t)N);
+    rc |= dev_alloc(&s.partial, (size_t)std::max(s.nblk, 1) * kIkCols);
+    rc |= dev_alloc(&s.d_perm, (size_t)N);
+    rc |= dev_alloc(&s.d_iperm, (size_t)N);
+    if (rc) {
+        free_scan_buf(s);
+        return LIVO_E_OOM;
+    }
+    if (N > 0) {
+        unsigned long long *codes = nullptr, *scodes = nullptr;
+        uint32_t *iota = nullptr, *perm = nullptr;
+        unsigned* mm = nullptr;
+        rc = dev_alloc(&codes, (size_t)N) | dev_alloc(&scodes, (size_t)N) | dev_alloc(&iota, (size_t)N) |
+             dev_alloc(&perm, (size_t)N) | dev_alloc(&mm, 6);
+        const unsigned init[6] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u};
+        if (!rc && hipMemcpyAsync(mm, init, sizeof(init), hipMemcpyHostToDevice, c->stream) != hipSuccess) rc = LIVO_E_HIP;
+        if (!rc) rc = launch_fe_minmax(d_src, N, stride, mm, c->stream);
+        if (!rc) rc = launch_fe_morton(d_src, N, stride, mm, morton_scale(), codes, iota, c->stream);
+        if (!rc) {
+            size_t tb = 0;
+            rc = prim_sort_pairs_u64(nullptr, &tb, codes, scodes, iota, perm, N, 60, c->stream);
+            if (!rc) rc = ensure_prim(c, tb);
+            tb = c->prim_bytes;
+            if (!rc) rc = prim_sort_pairs_u64(c->prim_tmp, &tb, codes, scodes, iota, perm, N, 60, c->stream);
+        }
+        if (!rc) rc = launch_fe_gather(d_src, N, stride, perm, s.pts, s.d_iperm, c->stream);
+        s.perm.resize((size_t)N);
+        if (!rc && (hipMemcpyAsync(s.d_perm, perm, (size_t)N * 4, hipMemcpyDeviceToDevice, c->stream) != hipSuccess ||
+                    hipMemcpyAsync(s.perm.data(), perm, (size_t)N * 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+                    hipMemsetAsync(s.nn, 0, (size_t)N * sizeof(NNRec), c->stream) != hipSuccess ||
+                    hipStreamSynchronize(c->stream) != hipSuccess))
+            rc = LIVO_E_HIP;
+        dev_free(codes); dev_free(scodes); dev_free(iota); dev_free(perm); dev_free(mm);
+        if (rc) {
+            free_scan_buf(s);
+            return rc;
+        }
+    }
+    *scan_id = register_scan(c, s);
+    return LIVO_OK;
+}
+
 int livo_scan_upload(livo_ctx* c, const float* xyz, int64_t N, int64_t stride_bytes, int32_t* scan_id) {
     if (!c || !scan_id || N < 0 || (N > 0 && !xyz)) return LIVO_E_INVALID;
     if (N > (int64_t)0x7FFFFFFF - kBlock) return LIVO_E_RANGE;
@@ -800,16 +876,7 @@ int livo_scan_upload(livo_ctx* c, const float* xyz, int64_t N, int64_t stride_by
             hipMemcpy(s.d_iperm, iperm.data(), (size_t)N * 4, hipMemcpyHostToDevice) != hipSuccess)
             return LIVO_E_HIP;
     }
-    int32_t id = -1;
-    for (size_t i = 0; i < c->scans.size(); i++)
-        if (!c->scans[i].used) { id = (int32_t)i; break; }
-    if (id < 0) {
-        id = (int32_t)c->scans.size();
-        c->scans.push_back(s);
-    } else {
-        c->scans[id] = s;
-    }
-    *scan_id = id;
+    *scan_id = register_scan(c, s);
     return LIVO_OK;
 }
 
@@ -1357,6 +1424,157 @@ int livo_scan_inherit_neighbors(livo_ctx* c, int32_t dst, int32_t src) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     d->searched = true;  // the cache now holds the inherited entries
     return LIVO_OK;
+}
+
+int livo_scan_preprocess(livo_ctx* c, const livo_raw_point* raw, int64_t n, const livo_imu_pose* poses,
+                         int32_t n_poses, const double rot_end[9], const double pos_end[3], float leaf_size,
+                         int32_t* scan_id, livo_raw_point* undistorted, livo_raw_point* down, int64_t down_cap,
+                         int64_t* n_down) {
+    if (!c || !scan_id || n < 0 || (n > 0 && !raw) || n_poses < 0 || (n_poses > 0 && !poses) ||
+        !std::isfinite(leaf_size))
+        return LIVO_E_INVALID;
+    const bool deskew = n_poses >= 2 && n > 0;
+    if (deskew && (!rot_end || !pos_end)) return LIVO_E_INVALID;
+    for (int32_t k = 1; k < n_poses; k++)
+        if (!(poses[k].offset_time >= poses[k - 1].offset_time)) return LIVO_E_INVALID;  // the walk needs sorted segments
+    if (n > (int64_t)0x7FFFFFFF - kBlock) return LIVO_E_RANGE;
+    if (set_device(c)) return LIVO_E_HIP;
+    // scratch: raw 20n, poses, seg 2x4n, keys/iota/skeys/svals 4x4n, flags/vid 2x4n, starts 4(n+1), down 20n
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t nb = (size_t)std::max<int64_t>(n, 1);
+    const size_t b_raw = al(nb * 20), b_pose = al((size_t)std::max(n_poses, 1) * 22 * 8), b4 = al(nb * 4),
+                 b_st = al((nb + 1) * 4);
+    const size_t total = b_raw + b_pose + 8 * b4 + b_st + b_raw + 256;
+    if (total > c->fe_bytes) {
+        if (c->fe_buf) (void)hipFree(c->fe_buf);
+        c->fe_buf = nullptr;
+        c->fe_bytes = 0;
+        if (hipMalloc(&c->fe_buf, total) != hipSuccess) return LIVO_E_OOM;
+        c->fe_bytes = total;
+    }
+    char* p = (char*)c->fe_buf;
+    FrontParams F{};
+    F.raw = (float*)p; p += b_raw;
+    double* d_poses = (double*)p; p += b_pose;
+    int32_t* seg = (int32_t*)p; p += b4;
+    F.seg = seg;
+    F.seg_rev = (int32_t*)p; p += b4;
+    F.keys = (uint32_t*)p; p += b4;
+    F.iota = (uint32_t*)p; p += b4;
+    uint32_t* skeys = (uint32_t*)p; p += b4;
+    uint32_t* svals = (uint32_t*)p; p += b4;
+    F.flags = (uint32_t*)p; p += b4;
+    F.vid = (uint32_t*)p; p += b4;
+    F.starts = (uint32_t*)p; p += b_st;
+    F.down = (float*)p; p += b_raw;
+    unsigned* mm = (unsigned*)p;
+    F.skeys = skeys;
+    F.svals = svals;
+    F.n = n;
+    F.poses = d_poses;
+    F.np = n_poses;
+    std::memcpy(F.R_LI, c->params.R_LI, sizeof(F.R_LI));
+    std::memcpy(F.t_LI, c->params.t_LI, sizeof(F.t_LI));
+    if (n > 0) HIP_TRY(hipMemcpyAsync(F.raw, raw, (size_t)n * 20, hipMemcpyHostToDevice, c->stream));
+    int rc = LIVO_OK;
+    if (deskew) {
+        // extR_Ri = R_LI^T rot_end^T, exrR_extT = R_LI^T t_LI (IMU_Processing.cpp:337-338)
+        const double* RL = c->params.R_LI;
+        for (int i = 0; i < 3; i++) {
+            for (int j = 0; j < 3; j++) {
+                double acc = RL[0 * 3 + i] * rot_end[j * 3 + 0];
+                for (int l = 1; l < 3; l++) acc = acc + RL[l * 3 + i] * rot_end[j * 3 + l];
+                F.extR_Ri[i * 3 + j] = acc;
+            }
+            F.exrR_extT[i] = (RL[0 * 3 + i] * c->params.t_LI[0] + RL[1 * 3 + i] * c->params.t_LI[1]) +
+                             RL[2 * 3 + i] * c->params.t_LI[2];
+            F.pos_end[i] = pos_end[i];
+        }
+        static_assert(sizeof(livo_imu_pose) == 22 * sizeof(double), "Pose6D row");
+        HIP_TRY(hipMemcpyAsync(d_poses, poses, (size_t)n_poses * sizeof(livo_imu_pose), hipMemcpyHostToDevice,
+                               c->stream));
+        rc = launch_fe_segment(F, c->stream);
+        if (!rc) {
+            size_t tb = 0;
+            rc = prim_inclusive_min_scan_i32(nullptr, &tb, seg, F.seg_rev, n, c->stream);
+            if (!rc) rc = ensure_prim(c, tb);
+            tb = c->prim_bytes;
+            if (!rc) rc = prim_inclusive_min_scan_i32(c->prim_tmp, &tb, seg, F.seg_rev, n, c->stream);
+        }
+        if (!rc) rc = launch_fe_undistort(F, c->stream);
+        if (rc) return rc;
+    }
+    if (undistorted && n > 0)
+        HIP_TRY(hipMemcpyAsync(undistorted, F.raw, (size_t)n * 20, hipMemcpyDeviceToHost, c->stream));
+    // downSizeFilterSurf: PCL VoxelGrid::applyFilter
+    const float* kept = F.raw;
+    int64_t n_kept = n;
+    if (leaf_size > 0.f && n > 0) {
+        const unsigned init[6] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u};
+        HIP_TRY(hipMemcpyAsync(mm, init, sizeof(init), hipMemcpyHostToDevice, c->stream));
+        rc = launch_fe_minmax(F.raw, n, 5, mm, c->stream);
+        if (rc) return rc;
+        unsigned hm[6];
+        HIP_TRY(hipMemcpyAsync(hm, mm, sizeof(hm), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        float mn[3], mx[3];
+        auto dec = [](unsigned o) {
+            const unsigned u = (o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o;
+            float f;
+            std::memcpy(&f, &u, 4);
+            return f;
+        };
+        for (int k = 0; k < 3; k++) {
+            mn[k] = dec(hm[k]);
+            mx[k] = dec(hm[3 + k]);
+        }
+        const float inv = 1.0f / leaf_size;  // inverse_leaf_size_
+        const int64_t dx = static_cast<int64_t>((mx[0] - mn[0]) * inv) + 1;
+        const int64_t dy = static_cast<int64_t>((mx[1] - mn[1]) * inv) + 1;
+        const int64_t dz = static_cast<int64_t>((mx[2] - mn[2]) * inv) + 1;
+        if ((dx * dy * dz) <= static_cast<int64_t>(0x7FFFFFFF)) {  // else PCL returns the input
+            int max_b[3], div_b[3];
+            for (int k = 0; k < 3; k++) {
+                F.min_b[k] = static_cast<int>(std::floor(mn[k] * inv));
+                max_b[k] = static_cast<int>(std::floor(mx[k] * inv));
+                div_b[k] = max_b[k] - F.min_b[k] + 1;
+            }
+            F.divb_mul[0] = 1;
+            F.divb_mul[1] = div_b[0];
+            F.divb_mul[2] = div_b[0] * div_b[1];
+            F.inv_leaf = inv;
+            const int64_t cells = (int64_t)div_b[0] * div_b[1] * div_b[2];
+            int bits = 1;
+            while (bits < 32 && ((int64_t)1 << bits) < cells) bits++;
+            rc = launch_fe_leaf(F, c->stream);
+            if (!rc) {
+                size_t tb = 0;
+                rc = prim_sort_pairs_u32(nullptr, &tb, F.keys, skeys, F.iota, svals, n, bits, c->stream);
+                if (!rc) rc = ensure_prim(c, tb);
+                tb = c->prim_bytes;
+                if (!rc) rc = prim_sort_pairs_u32(c->prim_tmp, &tb, F.keys, skeys, F.iota, svals, n, bits, c->stream);
+            }
+            if (!rc) rc = launch_fe_runs(F, c->stream);
+            if (!rc) rc = ivox_scan(c, F.flags, F.vid, n);
+            if (rc) return rc;
+            uint32_t tail[2];
+            HIP_TRY(hipMemcpyAsync(&tail[0], F.vid + n - 1, 4, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipMemcpyAsync(&tail[1], F.flags + n - 1, 4, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            const int64_t n_vox = (int64_t)tail[0] + tail[1];
+            rc = launch_fe_starts(F, c->stream);
+            if (!rc) rc = launch_fe_centroid(F, n_vox, c->stream);
+            if (rc) return rc;
+            kept = F.down;
+            n_kept = n_vox;
+        }
+    }
+    if (n_down) *n_down = n_kept;
+    if (down) {
+        if (down_cap < n_kept) return LIVO_E_RANGE;
+        if (n_kept > 0) HIP_TRY(hipMemcpyAsync(down, kept, (size_t)n_kept * 20, hipMemcpyDeviceToHost, c->stream));
+    }
+    return scan_create_device(c, kept, 5, n_kept, scan_id);
 }
 
 int livo_sync(livo_ctx* c) {

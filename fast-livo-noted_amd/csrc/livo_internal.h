@@ -345,6 +345,48 @@ struct MapIncrParams {
 int launch_map_incr(const MapIncrParams& p, void* stream);
 int launch_compact(const float* ordered, const uint32_t* flags, const uint32_t* pos, int64_t n, float* dense,
                    void* stream);
+// Scan front-end (frontend_kernels.hip).
+struct FrontParams {
+    float* raw;               // n x 5 floats: x, y, z, intensity, curvature (ms); xyz de-skewed in place
+    int64_t n;
+    const double* poses;      // np x 22 (Pose6D rows)
+    int32_t np;
+    int32_t* seg;             // n: last segment starting before point n-1-k (reversed)
+    int32_t* seg_rev;         // n: its prefix minimum = the segment of point n-1-k
+    double R_LI[9], t_LI[3];
+    double extR_Ri[9];        // R_LI^T rot_end^T
+    double exrR_extT[3];      // R_LI^T t_LI
+    double pos_end[3];
+    // VoxelGrid
+    float inv_leaf;
+    int32_t min_b[3];
+    int32_t divb_mul[3];
+    uint32_t* keys;           // leaf index per point
+    uint32_t* iota;
+    const uint32_t* skeys;    // sorted by leaf (stable)
+    const uint32_t* svals;
+    uint32_t* flags;          // run heads in sorted order
+    uint32_t* vid;            // scan of flags
+    uint32_t* starts;         // n_vox + 1 run starts
+    float* down;              // n_vox x 5 centroids
+};
+int launch_fe_segment(const FrontParams& F, void* stream);
+int launch_fe_undistort(const FrontParams& F, void* stream);
+int launch_fe_minmax(const float* pts, int64_t n, int stride, unsigned* minmax, void* stream);
+int launch_fe_leaf(const FrontParams& F, void* stream);
+int launch_fe_runs(const FrontParams& F, void* stream);
+int launch_fe_starts(const FrontParams& F, void* stream);
+int launch_fe_centroid(const FrontParams& F, int64_t n_vox, void* stream);
+int launch_fe_morton(const float* pts, int64_t n, int stride, const unsigned* minmax, float scale,
+                     unsigned long long* codes, uint32_t* iota, void* stream);
+int launch_fe_gather(const float* pts, int64_t n, int stride, const uint32_t* perm, float* pts4, int32_t* iperm,
+                     void* stream);
+int prim_inclusive_min_scan_i32(void* temp, size_t* temp_bytes, const int32_t* in, int32_t* out, int64_t n,
+                                void* stream);
+int prim_sort_pairs_u64(void* temp, size_t* temp_bytes, const unsigned long long* keys_in,
+                        unsigned long long* keys_out, const uint32_t* vals_in, uint32_t* vals_out, int64_t n,
+                        int bits, void* stream);
+
 // Nearest_Points carried over by point index (laser_mapping.cpp:165 resize keeps entries).
 int launch_inherit_nn(NNRec* dst, const int32_t* dst_perm, int64_t n_dst, const NNRec* src,
                       const int32_t* src_iperm, int64_t n_src, void* stream);

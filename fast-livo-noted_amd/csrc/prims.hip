@@ -31,4 +31,25 @@ int prim_exclusive_scan_u32(void* temp, size_t* temp_bytes, const uint32_t* in, 
     return e == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 
+// Inclusive prefix minimum of n int32 (the front-end's suffix minimum on reversed data).
+int prim_inclusive_min_scan_i32(void* temp, size_t* temp_bytes, const int32_t* in, int32_t* out, int64_t n,
+                                void* stream) {
+    size_t tb = *temp_bytes;
+    const hipError_t e = rocprim::inclusive_scan(temp, tb, in, out, (size_t)n, rocprim::minimum<int32_t>(),
+                                                 (hipStream_t)stream);
+    *temp_bytes = tb;
+    return e == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+
+// Stable LSD radix sort of (u64 key, u32 value) pairs on bits [0, bits).
+int prim_sort_pairs_u64(void* temp, size_t* temp_bytes, const unsigned long long* keys_in,
+                        unsigned long long* keys_out, const uint32_t* vals_in, uint32_t* vals_out, int64_t n,
+                        int bits, void* stream) {
+    size_t tb = *temp_bytes;
+    const hipError_t e = rocprim::radix_sort_pairs(temp, tb, keys_in, keys_out, vals_in, vals_out, (size_t)n, 0,
+                                                   bits, (hipStream_t)stream);
+    *temp_bytes = tb;
+    return e == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+
 }  // namespace livo

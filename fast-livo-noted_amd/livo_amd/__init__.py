@@ -160,6 +160,8 @@ SIGNATURES = {
     "livo_ivox_dump": (C.c_int, [_P, _P, _P, _P, C.c_int64, C.POINTER(C.c_int64)]),
     "livo_map_incremental": (C.c_int, [_P, C.c_int32, C.POINTER(State), C.c_double, C.c_int, _P, _P]),
     "livo_scan_inherit_neighbors": (C.c_int, [_P, C.c_int32, C.c_int32]),
+    "livo_scan_preprocess": (C.c_int, [_P, _P, C.c_int64, _P, C.c_int32, _P, _P, C.c_float, C.POINTER(C.c_int32),
+                                       _P, _P, C.c_int64, C.POINTER(C.c_int64)]),
     "livo_sync": (C.c_int, [_P]),
 }
 
@@ -427,6 +429,26 @@ class Context:
                                                                     int(bool(ekf_inited)), _ptr(cat),
                                                                     _ptr(counts)))
         return cat, {"added": int(counts[0]), "no_downsample": int(counts[1])}
+
+    def scan_preprocess(self, raw: np.ndarray, poses=None, rot_end=None, pos_end=None, leaf_size: float = 0.5):
+        """Raw frame (n, 5: x, y, z, intensity, curvature ms) -> resident scan id, with the de-skewed
+        points (n, 5) and the downsampled cloud (k, 5) (livo_scan_preprocess)."""
+        raw = np.ascontiguousarray(raw, np.float32).reshape(-1, 5)
+        n = raw.shape[0]
+        und = np.zeros_like(raw)
+        down = np.zeros_like(raw)
+        nd = C.c_int64()
+        sid = C.c_int32()
+        if poses is not None:
+            poses = np.ascontiguousarray(poses, np.float64).reshape(-1, 22)
+            rot_end = np.ascontiguousarray(rot_end, np.float64).reshape(9)
+            pos_end = np.ascontiguousarray(pos_end, np.float64).reshape(3)
+        npo = 0 if poses is None else poses.shape[0]
+        _check("livo_scan_preprocess", self._L.livo_scan_preprocess(
+            self.h, _ptr(raw), n, _ptr(poses), npo, _ptr(rot_end), _ptr(pos_end), leaf_size, C.byref(sid),
+            _ptr(und), _ptr(down), n, C.byref(nd)))
+        self.scans[sid.value] = int(nd.value)
+        return sid.value, und, down[:nd.value].copy()
 
     def scan_inherit_neighbors(self, dst: int, src: int):
         _check("livo_scan_inherit_neighbors", self._L.livo_scan_inherit_neighbors(self.h, dst, src))

@@ -21,6 +21,9 @@
  *                                                   include/ivox3d/ivox3d.h:37-305
  *   livo_map_incremental ← LaserMapping::map_incremental (iVox branch)
  *                                                   src/laser_mapping.cpp:329-389
+ *   livo_scan_preprocess ← ImuProcess::UndistortPcl (per point) + downSizeFilterSurf
+ *                                                   src/IMU_Processing.cpp:340-378,
+ *                                                   src/laser_mapping.cpp:129-130
  *
  * Conventions
  *   - plain pointers and sizes only; no C++ or torch types cross the ABI;
@@ -284,6 +287,45 @@ int livo_map_incremental(livo_ctx* ctx, int32_t scan_id, const livo_state* state
  * entries of the previous scan's points: dst's point i starts with src's
  * point i's cache (empty for i >= src's size). */
 int livo_scan_inherit_neighbors(livo_ctx* ctx, int32_t dst_scan, int32_t src_scan);
+
+/* ------------------------------------------------------------------------
+ * Scan front-end: from the raw frame to the resident
+ * feats_down_body on the device.
+ *   ImuProcess::UndistortPcl, per-point backward propagation
+ *                                       src/IMU_Processing.cpp:340-378
+ *   downSizeFilterSurf.filter (PCL VoxelGrid)  src/laser_mapping.cpp:129-130
+ * ------------------------------------------------------------------------ */
+/* The PointXYZINormal fields the front-end reads; curvature = the point's
+ * offset time in ms (preprocess.cpp:346). */
+typedef struct livo_raw_point {
+    float x, y, z, intensity, curvature;
+} livo_raw_point;
+
+/* Pose6D (msg/Pose6D.msg, set_pose6d common_lib.h:618-633): one IMU sample of
+ * the frame's forward propagation, offset_time in seconds from the frame start. */
+typedef struct livo_imu_pose {
+    double offset_time;
+    double acc[3];
+    double gyr[3];
+    double vel[3];
+    double pos[3];
+    double rot[9];  /* row-major */
+} livo_imu_pose;
+
+/* Raw frame -> resident scan.  With n_poses >= 2 every point is first moved to
+ * the frame-end pose (rot_end, pos_end = state after propagation) through the
+ * IMU segment it falls in, exactly as UndistortPcl's backward walk (poses must
+ * have non-decreasing offset_time; the first point is re-compensated by every
+ * remaining segment, as in the reference); then, for leaf_size > 0, PCL
+ * VoxelGrid downsampling (voxel centroids of x, y, z, intensity, curvature in
+ * ascending leaf order; a leaf too small for 32-bit indices keeps the input,
+ * as PCL does).  The result becomes a resident scan (*scan_id), as
+ * livo_scan_upload would.  undistorted (n) and down (down_cap; *n_down = its
+ * size) are optional host copies. */
+int livo_scan_preprocess(livo_ctx* ctx, const livo_raw_point* raw, int64_t n, const livo_imu_pose* poses,
+                         int32_t n_poses, const double rot_end[9], const double pos_end[3], float leaf_size,
+                         int32_t* scan_id, livo_raw_point* undistorted, livo_raw_point* down, int64_t down_cap,
+                         int64_t* n_down);
 
 int livo_sync(livo_ctx* ctx);
 
