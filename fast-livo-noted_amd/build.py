@@ -66,6 +66,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     _run(cmd)
     os.replace(LIB + ".tmp", LIB)
     build_facade_demo(verbose)
+    build_checks(verbose)
     return LIB
 
 
@@ -86,3 +87,16 @@ def build_facade_demo(verbose: bool = False) -> str:
 
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+
+
+WAVE_CHECK = os.path.join(LIB_DIR, "wave_nth_check")
+
+
+def build_checks(verbose: bool = False) -> str:
+    """Device unit checks run by the -m gpu tests (built here, on the CPU, like the library)."""
+    cmd = [HIPCC, "-O3", "-std=c++17", "--offload-arch=" + ARCH, "-ffp-contract=off", "-I" + os.path.join(ROOT, "include"),
+           "-I" + CSRC, os.path.join(ROOT, "tests", "native", "wave_nth_check.hip"), "-o", WAVE_CHECK]
+    if verbose:
+        print(" ".join(cmd))
+    _run(cmd)
+    return WAVE_CHECK

@@ -13,9 +13,9 @@
 //   k_fe_minmax / k_fe_leaf / k_fe_runs / k_fe_centroid   PCL VoxelGrid::
 //       applyFilter (downSizeFilterSurf, laser_mapping.cpp:129-130): bounds,
 //       32-bit leaf index per point, a stable radix sort by leaf, one centroid
-//       per run in ascending leaf order.  (PCL sums a voxel in std::sort's
-//       unstable order; here in input order: centroids agree to float
-//       rounding, voxels and counts exactly.)
+//       per run (one wave each) in ascending leaf order.  (PCL sums a voxel in
+//       std::sort's unstable order; here a fixed lane-strided tree: centroids
+//       agree to float rounding, voxels and counts exactly.)
 //   k_fe_morton / k_fe_gather        the resident scan's Morton order, the
 //       same keys and stable order as livo_scan_upload's host sort.
 //
@@ -182,20 +182,31 @@ __global__ void k_fe_starts(FrontParams F) {
     if (k == F.n - 1) F.starts[F.vid[k] + F.flags[k]] = (uint32_t)F.n;
 }
 
-// CentroidPoint of one leaf (AccumulatorXYZ / Intensity / Curvature: float sums / n)
+// CentroidPoint of one leaf (AccumulatorXYZ / Intensity / Curvature: float
+// sums / n), one wave per leaf: lanes sum strided members in input order, a
+// fixed xor-tree combines them (PCL's own order is std::sort's, unspecified).
 __global__ void k_fe_centroid(FrontParams F, int64_t n_vox) {
-    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t v = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    const int lane = threadIdx.x & 63;
     if (v >= n_vox) return;
     const uint32_t a = F.starts[v], b = F.starts[v + 1];
     float s[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-    for (uint32_t k = a; k < b; k++) {
+    for (uint32_t k = a + lane; k < b; k += 64) {
         const float* p = F.raw + 5 * (int64_t)F.svals[k];
 #pragma unroll
         for (int c = 0; c < 5; c++) s[c] += p[c];
     }
-    const float cnt = (float)(b - a);
 #pragma unroll
-    for (int c = 0; c < 5; c++) F.down[5 * v + c] = s[c] / cnt;
+    for (int c = 0; c < 5; c++)
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) s[c] += __shfl_xor(s[c], off, 64);
+    if (lane < 5) {
+        const float cnt = (float)(b - a);
+        float val = s[0];
+#pragma unroll
+        for (int c = 1; c < 5; c++) val = lane == c ? s[c] : val;
+        F.down[5 * v + lane] = val / cnt;
+    }
 }
 
 // livo_scan_upload's Morton key (0.25 m cells by default, 20 bits per axis)
@@ -250,7 +261,11 @@ int launch_fe_minmax(const float* pts, int64_t n, int stride, unsigned* minmax, 
 int launch_fe_leaf(const FrontParams& F, void* stream) { FE_LAUNCH(k_fe_leaf, F.n, F); }
 int launch_fe_runs(const FrontParams& F, void* stream) { FE_LAUNCH(k_fe_runs, F.n, F); }
 int launch_fe_starts(const FrontParams& F, void* stream) { FE_LAUNCH(k_fe_starts, F.n, F); }
-int launch_fe_centroid(const FrontParams& F, int64_t n_vox, void* stream) { FE_LAUNCH(k_fe_centroid, n_vox, F, n_vox); }
+int launch_fe_centroid(const FrontParams& F, int64_t n_vox, void* stream) {
+    if (n_vox <= 0) return LIVO_OK;
+    hipLaunchKernelGGL(k_fe_centroid, dim3((unsigned)((n_vox + 3) / 4)), dim3(256), 0, (hipStream_t)stream, F, n_vox);
+    return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
 int launch_fe_morton(const float* pts, int64_t n, int stride, const unsigned* minmax, float scale,
                      unsigned long long* codes, uint32_t* iota, void* stream) {
     FE_LAUNCH(k_fe_morton, n, pts, n, stride, minmax, scale, codes, iota);

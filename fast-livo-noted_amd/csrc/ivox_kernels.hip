@@ -27,8 +27,12 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <cstdlib>
+#include <cstring>
+
 #include "device_common.h"
 #include "livo_internal.h"
+#include "wave_select.h"
 
 namespace livo {
 
@@ -222,17 +226,260 @@ __global__ __launch_bounds__(64) void k_ivox_knn_big(KnnParams P) {
     }
 }
 
+
+// ------------------------------------------------- wave-cooperative search --
+// One query per wave.  The nearby grids are probed by one lane each, their
+// points loaded at once (<= kWRaw per query, 4 per lane), the in-range ones
+// staged in LDS in the reference's push order (grid by grid, insertion order),
+// and every std::nth_element of GetClosestPoint is run by the whole wave:
+// libstdc++'s unguarded Hoare partition computed in parallel.  With pv the
+// pivot value and, over the original values of [lo, last), Lo = the positions
+// with !(a < pv) ascending and Ro = those with !(pv < a) descending, the
+// sequential partition swaps Lo[k] <-> Ro[k] for every k < k* (the pairs with
+// Lo[k] < Ro[k]) and returns cut = min(Lo[k*], Ro[k*-1]).  Ranks come from
+// ballots, partners from two LDS tables.  The median-of-3 step and the final
+// insertion sort of <= 3 elements are done by lane 0 as written.  Queries with
+// more than kWRaw raw points, or an introselect whose depth limit runs out
+// (libstdc++ then switches to a heap select), go to the global-memory pass.
+template <bool LATER>
+__global__ __launch_bounds__(64 * kWaves) void k_ivox_knn_wave(KnnParams P) {
+    __shared__ WaveLds lds[kWaves];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    WaveLds& L = lds[w];
+    unsigned bjob, bx;
+    xcd_block(P.nb, bjob, bx);
+    const HsJob job = P.jobs[bjob];
+    const IekfSlot* slot = job.slot;
+    if (P.force >= 0) {
+        if (!P.force) return;
+    } else {
+        if (slot->ctrl.stop) return;
+        if (LATER && !slot->ctrl.search_en) return;
+    }
+    const int i = (int)bx * kWaves + w;
+    if (i >= job.n) return;
+    const IvoxParams& V = P.iv;
+    const float4 b = reinterpret_cast<const float4*>(job.pts)[i];
+    float qx, qy, qz;
+    iv_world(P, slot, b, qx, qy, qz);
+    int kx, ky, kz;
+    const float qlim = (float)(kIvMaxKey + 8);
+    if (!iv_cell(qx, V.inv_res, qlim, kx) || !iv_cell(qy, V.inv_res, qlim, ky) || !iv_cell(qz, V.inv_res, qlim, kz))
+        return;  // no grid within reach: nothing found, the cache stays
+    // one nearby grid per lane
+    uint2 run = make_uint2(0u, 0u);
+    if (lane < V.nearby)
+        run = iv_lookup(V.slots, V.log2, iv_key(kx + c_nearby[lane][0], ky + c_nearby[lane][1], kz + c_nearby[lane][2]));
+    uint32_t incl = run.y;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t v = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += v;
+    }
+    const uint32_t R = __shfl(incl, 63, 64);
+    const uint32_t excl = incl - run.y;
+    if (R > (uint32_t)kWRaw) {
+        if (lane == 0) {
+            const unsigned r = atomicAdd(P.replay_count, 1u);
+            P.replay_list[r] = ((unsigned long long)bjob << 32) | (unsigned)i;
+        }
+        return;
+    }
+    if (lane <= kIvMaxNearby) L.m[lane] = 0u;
+    // every raw point at once (raw index g = 64 r + lane, in grid order)
+    const float4* __restrict__ pts = reinterpret_cast<const float4*>(V.pts);
+    float dist[4];
+    uint32_t pid[4];
+    int gnode[4];
+    bool inr[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const uint32_t g = 64u * r + lane;
+        int t = 0;
+#pragma unroll 1
+        for (int tt = 0; tt < V.nearby; tt++) {
+            const uint32_t e = __shfl(excl, tt, 64), c = __shfl(run.y, tt, 64);
+            if (g >= e && g < e + c) t = tt;
+        }
+        const uint32_t st = __shfl(run.x, t, 64), e = __shfl(excl, t, 64);
+        gnode[r] = t;
+        pid[r] = st + (g - e);
+        inr[r] = false;
+        dist[r] = 0.f;
+        if (g < R) {
+            const float4 v = pts[pid[r]];
+            const float dx = v.x - qx, dy = v.y - qy, dz = v.z - qz;
+            dist[r] = dx * dx + (dy * dy + dz * dz);  // distance2, ivox3d_node.hpp:12-16
+            inr[r] = (double)dist[r] < V.range2;
+        }
+    }
+    wave_sync();
+    // stage the in-range points in push order (ivox3d_node.hpp:154-164)
+    int base = 0;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const unsigned long long m = __ballot(inr[r]);
+        if (inr[r]) {
+            const int pos = base + lanes_below(m, lane);
+            L.d[pos] = dist[r];
+            L.id[pos] = pid[r];
+            L.node[pos] = (uint8_t)gnode[r];
+            atomicAdd(&L.m[gnode[r]], 1u);
+        }
+        base += __popcll(m);
+    }
+    wave_sync();
+#ifdef LIVO_IV_DEBUG_Q
+#define IVDBG(tag, cnt)                                                                        \
+    if (i == LIVO_IV_DEBUG_Q && lane == 0) {                                                   \
+        printf("%s n=%d:", tag, (int)(cnt));                                                   \
+        for (int z = 0; z < (int)(cnt); z++) printf(" (%.8f,%u,%d)", L.d[z], L.id[z], (int)L.node[z]); \
+        printf("\n");                                                                           \
+    }
+#else
+#define IVDBG(tag, cnt)
+#endif
+    IVDBG("staged", base);
+    if (base == 0) return;  // no candidate: the reference returns false, the cache stays
+    // per grid: KNNPointByCondition's nth_element on its own run (ivox3d_node.hpp:179-183)
+    const int K = V.max_num;
+    const uint32_t mt = lane < V.nearby ? L.m[lane] : 0u;
+    uint32_t s_incl = mt;
+    uint32_t k_incl = min(mt, (uint32_t)K);
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t v = __shfl_up(s_incl, off, 64), u = __shfl_up(k_incl, off, 64);
+        if (lane >= off) {
+            s_incl += v;
+            k_incl += u;
+        }
+    }
+    const uint32_t S = s_incl - mt;                      // the grid's staged segment start
+    const uint32_t O = k_incl - min(mt, (uint32_t)K);    // its survivors' start in the final list
+    const int n_final = (int)__shfl(k_incl, 63, 64);
+    bool ok = true;
+#pragma unroll 1
+    for (int tt = 0; tt < V.nearby && ok; tt++) {
+        const int m = (int)__shfl(mt, tt, 64);
+        if (m > K) {
+            const int s0 = (int)__shfl(S, tt, 64);
+            ok = wave_nth(L, s0, s0 + K - 1, s0 + m, lane);
+            IVDBG("pernode", base);
+        }
+    }
+    if (ok) {
+        // survivors: the first min(m, K) of each grid's segment, in grid order
+        float cd[4];
+        uint32_t cid[4];
+        int dst[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int p = 64 * r + lane;
+            // shuffles outside the branch: ds_bpermute reads 0 from inactive lanes
+            const int t = p < base ? L.node[p] : 0;
+            const int s0 = (int)__shfl(S, t, 64), o0 = (int)__shfl(O, t, 64);
+            dst[r] = -1;
+            if (p < base) {
+                cd[r] = L.d[p];
+                cid[r] = L.id[p];
+                if (p - s0 < K) dst[r] = o0 + (p - s0);
+            }
+        }
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+            if (dst[r] >= 0) {
+                L.d[dst[r]] = cd[r];
+                L.id[dst[r]] = cid[r];
+            }
+        wave_sync();
+        IVDBG("compact", n_final);
+        int n = n_final;
+        if (n > K) {  // ivox3d.h:173-177
+            ok = wave_nth(L, 0, K - 1, n, lane);
+            n = K;
+        }
+        IVDBG("nth4", n);
+        if (ok) ok = wave_nth(L, 0, 0, n, lane);  // ivox3d.h:178
+        IVDBG("final", n);
+        if (ok) {
+            // NNRec: lanes 0..4 the points, lane 0 the indices
+            NNRec* out = job.nn + i;
+            float4* o4 = reinterpret_cast<float4*>(out);
+            const uint32_t myid = lane < n ? L.id[lane] : 0u;
+            const float myd = lane < n ? L.d[lane] : INFINITY;
+            int32_t pidx = -1;
+            if (lane < kNN) {
+                float4 v = make_float4(0.f, 0.f, 0.f, INFINITY);
+                if (lane < n) {
+                    const float4 pp = pts[myid];
+                    v = make_float4(pp.x, pp.y, pp.z, myd);
+                    pidx = __float_as_int(pp.w);
+                }
+                o4[lane] = v;
+            }
+            const int32_t i0 = __shfl(pidx, 0, 64), i1 = __shfl(pidx, 1, 64), i2 = __shfl(pidx, 2, 64),
+                          i3 = __shfl(pidx, 3, 64), i4 = __shfl(pidx, 4, 64);
+            const int32_t nd0 = __shfl(lane < n ? (int)myid : -1, 0, 64), nd1 = __shfl(lane < n ? (int)myid : -1, 1, 64),
+                          nd2 = __shfl(lane < n ? (int)myid : -1, 2, 64), nd3 = __shfl(lane < n ? (int)myid : -1, 3, 64),
+                          nd4 = __shfl(lane < n ? (int)myid : -1, 4, 64);
+            if (lane == 0) {
+                int4* oi = reinterpret_cast<int4*>(out) + 5;
+                oi[0] = make_int4(i0, i1, i2, i3);
+                oi[1] = make_int4(i4, n, 0, nd0);
+                oi[2] = make_int4(nd1, nd2, nd3, nd4);
+            }
+            return;
+        }
+    }
+    // the depth limit ran out (libstdc++ would heap-select): the exact global-memory pass
+    if (lane == 0) {
+        const unsigned r = atomicAdd(P.replay_count, 1u);
+        P.replay_list[r] = ((unsigned long long)bjob << 32) | (unsigned)i;
+    }
+}
+
+// Kernel choice per launch: the wave-cooperative search has ~20x less latency
+// per query (small scans: the IEKF of one downsampled frame), the
+// one-query-per-thread search (private candidate array) more throughput when
+// hundreds of thousands of queries are in flight (scan farms).
+// LIVO_IVOX_KIND=thread|wave forces one; LIVO_IVOX_WAVE_MAX sets the switch
+// point (queries per launch, default 131072).
+static int ivox_kind(int64_t queries) {
+    static const int forced = [] {
+        const char* e = std::getenv("LIVO_IVOX_KIND");
+        if (!e) return -1;
+        return std::strcmp(e, "thread") == 0 ? 0 : (std::strcmp(e, "wave") == 0 ? 1 : -1);
+    }();
+    static const int64_t wave_max = [] {
+        const char* e = std::getenv("LIVO_IVOX_WAVE_MAX");
+        return e ? (int64_t)std::atoll(e) : (int64_t)131072;
+    }();
+    if (forced >= 0) return forced;
+    return queries <= wave_max ? 1 : 0;
+}
+
 int launch_ivox_knn(const KnnParams& p, int n_jobs, int64_t max_n, bool later, int64_t overflow_threads,
                     void* stream) {
     if (n_jobs <= 0 || max_n <= 0) return LIVO_OK;
     KnnParams q = p;
-    q.nb = (int32_t)((max_n + kKnnBlock - 1) / kKnnBlock);
-    if ((int64_t)q.nb * n_jobs >= (1ll << 31)) return LIVO_E_RANGE;
-    const dim3 grid((unsigned)(q.nb * n_jobs)), block(kKnnBlock);
-    if (later)
-        hipLaunchKernelGGL((k_ivox_knn<true>), grid, block, 0, (hipStream_t)stream, q);
-    else
-        hipLaunchKernelGGL((k_ivox_knn<false>), grid, block, 0, (hipStream_t)stream, q);
+    if (ivox_kind((int64_t)n_jobs * max_n) == 0) {
+        q.nb = (int32_t)((max_n + kKnnBlock - 1) / kKnnBlock);
+        if ((int64_t)q.nb * n_jobs >= (1ll << 31)) return LIVO_E_RANGE;
+        const dim3 grid((unsigned)(q.nb * n_jobs)), block(kKnnBlock);
+        if (later)
+            hipLaunchKernelGGL((k_ivox_knn<true>), grid, block, 0, (hipStream_t)stream, q);
+        else
+            hipLaunchKernelGGL((k_ivox_knn<false>), grid, block, 0, (hipStream_t)stream, q);
+    } else {
+        q.nb = (int32_t)((max_n + kWaves - 1) / kWaves);
+        if ((int64_t)q.nb * n_jobs >= (1ll << 31)) return LIVO_E_RANGE;
+        const dim3 grid((unsigned)(q.nb * n_jobs)), block(64 * kWaves);
+        if (later)
+            hipLaunchKernelGGL((k_ivox_knn_wave<true>), grid, block, 0, (hipStream_t)stream, q);
+        else
+            hipLaunchKernelGGL((k_ivox_knn_wave<false>), grid, block, 0, (hipStream_t)stream, q);
+    }
     if (hipGetLastError() != hipSuccess) return LIVO_E_HIP;
     const unsigned blocks = (unsigned)std::max<int64_t>(1, overflow_threads / 64);
     hipLaunchKernelGGL(k_ivox_knn_big, dim3(blocks), dim3(64), 0, (hipStream_t)stream, q);
@@ -320,14 +567,21 @@ __global__ void k_iv_place(IvoxParams P) {
 
 __global__ void k_iv_fix(IvoxParams P) {
     const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= P.table) return;
-    GridSlot g = P.slots[s];
-    if (g.key == kGridEmpty) return;
-    g.start = P.newstart[s];
-    g.count += P.addcnt[s];
-    P.slots[s] = g;
-    P.addcnt[s] = 0u;
-    atomicMax(P.ctr + 2, (unsigned long long)g.count);
+    unsigned cnt = 0;
+    if (s < P.table) {
+        GridSlot g = P.slots[s];
+        if (g.key != kGridEmpty) {
+            g.start = P.newstart[s];
+            g.count += P.addcnt[s];
+            P.slots[s] = g;
+            P.addcnt[s] = 0u;
+            cnt = g.count;
+        }
+    }
+    // the largest grid: one atomic per wave
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) cnt = max(cnt, (unsigned)__shfl_xor((int)cnt, off, 64));
+    if ((threadIdx.x & 63) == 0 && cnt) atomicMax(P.ctr + 2, (unsigned long long)cnt);
 }
 
 __global__ void k_iv_rehash(const GridSlot* __restrict__ old_slots, int64_t old_table, GridSlot* slots, int log2) {

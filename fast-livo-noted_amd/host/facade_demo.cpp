@@ -2,14 +2,18 @@
 // its members (laser_mapping.cpp:129-238), with minimal Eigen-shaped types,
 // and prints the results for tests/test_facade.py to compare with the oracle.
 //
-// usage: facade_demo <map.f32> <scan.f32> <state.f64> <max_iter>
+// usage: facade_demo <map.f32> <scan.f32> <state.f64> <max_iter> [ivox]
 //   map.f32 / scan.f32: raw float xyz triples; state.f64: 3x3 rot (row-major),
 //   pos, vel, bias_g, bias_a, gravity, 18x18 cov (row-major) = 348 doubles.
 // Output (text): "hshare <effct> <81 HPH> <9 HPL>" for the first
 // h_share_model(), then "iekf <iterations> <converged> <rot 9> <pos 3> <cov 324>".
+// With "ivox": the map goes in through ivox_->AddPoints (the reference's
+// default backend) and a final "incr <added> <no_downsample>" line reports
+// map_incremental() at the updated state.
 // Exit status: 0 ok, 2 usage/IO, 3 livo::Error (code printed on stderr).
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "laser_mapping_gpu.hpp"
@@ -55,10 +59,11 @@ std::vector<char> slurp(const char* path) {
 }  // namespace
 
 int main(int argc, char** argv) {
-    if (argc != 5) {
-        std::fprintf(stderr, "usage: %s map.f32 scan.f32 state.f64 max_iter\n", argv[0]);
+    if (argc != 5 && !(argc == 6 && std::string(argv[5]) == "ivox")) {
+        std::fprintf(stderr, "usage: %s map.f32 scan.f32 state.f64 max_iter [ivox]\n", argv[0]);
         return 2;
     }
+    const bool ivox = argc == 6;
     const std::vector<char> map = slurp(argv[1]), scan = slurp(argv[2]), st = slurp(argv[3]);
     if (map.empty() || scan.empty() || st.size() != 348 * sizeof(double)) {
         std::fprintf(stderr, "bad input files\n");
@@ -84,7 +89,12 @@ int main(int argc, char** argv) {
         p.t_LI[2] = -0.0284;
         p.max_iterations = std::atoi(argv[4]);
         livo::LaserMappingGpu lm(0, &p);
-        lm.build_map(reinterpret_cast<const float*>(map.data()), (int64_t)(map.size() / 12));
+        if (ivox) {
+            lm.use_ivox();  // reference defaults: 0.2 m grids, NEARBY18, capacity 1e6
+            lm.ivox_add_points(reinterpret_cast<const float*>(map.data()), (int64_t)(map.size() / 12));
+        } else {
+            lm.build_map(reinterpret_cast<const float*>(map.data()), (int64_t)(map.size() / 12));
+        }
         lm.set_scan(reinterpret_cast<const float*>(scan.data()), (int64_t)(scan.size() / 12));
         lm.set_state(s0);
         lm.set_state_propagat(s0);
@@ -108,6 +118,10 @@ int main(int argc, char** argv) {
         for (int i = 0; i < 18; i++)
             for (int j = 0; j < 18; j++) std::printf(" %.17g", s1.cov(i, j));
         std::printf("\n");
+        if (ivox) {
+            lm.map_incremental(0.5);  // filter_size_map default (laser_mapping.cpp:983)
+            std::printf("incr %lld %lld\n", (long long)lm.points_added, (long long)lm.points_no_downsample);
+        }
     } catch (const livo::Error& e) {
         std::fprintf(stderr, "livo::Error %d %s\n", e.code(), e.what());
         return 3;

@@ -107,15 +107,50 @@ public:
         check(livo_map_build(ctx_, xyz, M, stride_bytes), "livo_map_build");
     }
 
-    // feats_down_body for the next update; Nearest_Points is reset (laser_mapping.cpp:164).
+    // The compiled default backend: ivox_ = make_shared<IVoxType>(ivox_options_)
+    // (laser_mapping.cpp:776, options :1021-1035); h_share_model / iterate then
+    // search the iVox map (laser_mapping.cpp:519-521).
+    void use_ivox(const livo_ivox_params* options = nullptr) {
+        check(livo_ivox_init(ctx_, options), "livo_ivox_init");
+        check(livo_ctx_set_backend(ctx_, LIVO_BACKEND_IVOX), "livo_ctx_set_backend");
+        ivox_ = true;
+    }
+    // ivox_->AddPoints(points) (the first scan, laser_mapping.cpp:145-150).
+    void ivox_add_points(const float* xyz, int64_t n, int64_t stride_bytes = 3 * sizeof(float)) {
+        check(livo_ivox_add_points(ctx_, xyz, n, stride_bytes), "livo_ivox_add_points");
+    }
+
+    // feats_down_body for the next update (laser_mapping.cpp:129-131, 164-166).
+    // Nearest_Points.resize keeps the previous scan's entries, which only the
+    // iVox search can leave in place (ivox3d.h:165-167): carried over then.
     void set_scan(const float* body_xyz, int64_t N, int64_t stride_bytes = 3 * sizeof(float)) {
-        if (scan_id_ >= 0) {
-            check(livo_scan_release(ctx_, scan_id_), "livo_scan_release");
-            scan_id_ = -1;
-        }
-        check(livo_scan_upload(ctx_, body_xyz, N, stride_bytes, &scan_id_), "livo_scan_upload");
-        feats_down_size = N;
-        nearest_search_en = true;
+        int32_t id = -1;
+        check(livo_scan_upload(ctx_, body_xyz, N, stride_bytes, &id), "livo_scan_upload");
+        adopt_scan(id, N);
+    }
+
+    // The raw frame instead: UndistortPcl's per-point de-skew with the frame's
+    // IMU poses (IMU_Processing.cpp:340-378) and downSizeFilterSurf
+    // (laser_mapping.cpp:129-130) on the device; `down` (optional, cap
+    // down_cap) receives feats_down_body.
+    void set_scan_raw(const livo_raw_point* raw, int64_t n, const livo_imu_pose* poses, int32_t n_poses,
+                      float filter_size_surf, livo_raw_point* down = nullptr, int64_t down_cap = 0) {
+        int32_t id = -1;
+        int64_t nd = 0;
+        check(livo_scan_preprocess(ctx_, raw, n, poses, n_poses, state.rot, state.pos, filter_size_surf, &id,
+                                   nullptr, down, down_cap, &nd),
+              "livo_scan_preprocess");
+        adopt_scan(id, nd);
+    }
+
+    // map_incremental() (laser_mapping.cpp:329-389), iVox branch, at the updated state.
+    void map_incremental(double filter_size_map_min, bool flg_EKF_inited = true) {
+        int64_t counts[2] = {0, 0};
+        check(livo_map_incremental(ctx_, scan_id_, &state, filter_size_map_min, flg_EKF_inited ? 1 : 0, nullptr,
+                                   counts),
+              "livo_map_incremental");
+        points_added = counts[0];
+        points_no_downsample = counts[1];
     }
 
     template <class S>
@@ -164,11 +199,23 @@ public:
     bool flg_EKF_converged = false;
     int64_t effct_feat_num = 0;
     int64_t feats_down_size = 0;
+    int64_t points_added = 0, points_no_downsample = 0;  // last map_incremental
 
 private:
+    void adopt_scan(int32_t id, int64_t N) {
+        if (scan_id_ >= 0) {
+            if (ivox_) check(livo_scan_inherit_neighbors(ctx_, id, scan_id_), "livo_scan_inherit_neighbors");
+            check(livo_scan_release(ctx_, scan_id_), "livo_scan_release");
+        }
+        scan_id_ = id;
+        feats_down_size = N;
+        nearest_search_en = true;
+    }
+
     livo_ctx* ctx_ = nullptr;
     livo_params params_{};
     int32_t scan_id_ = -1;
+    bool ivox_ = false;
 };
 
 }  // namespace livo

@@ -1,0 +1,102 @@
+// GPU unit check (tests/test_gpu_ivox.py): wave_nth (fast-livo-noted_amd/csrc/
+// wave_select.h), the wave-parallel std::nth_element of the iVox search,
+// against libstdc++'s std::nth_element on the host, element for element.
+// One wave per case; cases of 1..256 elements with many ties.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <random>
+#include <vector>
+
+#include "wave_select.h"
+
+using namespace livo;
+
+struct Case {
+    int n, first, nth;
+};
+
+__global__ void k_check(const Case* cases, const float* d_in, float* d_out, uint32_t* id_out, int* status, int ncase) {
+    __shared__ WaveLds lds[1];
+    const int c = blockIdx.x, lane = threadIdx.x;
+    if (c >= ncase) return;
+    WaveLds& L = lds[0];
+    const Case k = cases[c];
+    for (int p = lane; p < k.n; p += 64) {
+        L.d[p] = d_in[c * kWRaw + p];
+        L.id[p] = (uint32_t)p;
+    }
+    wave_sync();
+    const bool ok = wave_nth(L, k.first, k.nth, k.n, lane);
+    for (int p = lane; p < k.n; p += 64) {
+        d_out[c * kWRaw + p] = L.d[p];
+        id_out[c * kWRaw + p] = L.id[p];
+    }
+    if (lane == 0) status[c] = ok ? 1 : 0;
+}
+
+struct DP {
+    float d;
+    uint32_t id;
+    bool operator<(const DP& o) const { return d < o.d; }
+};
+
+int main(int argc, char** argv) {
+    const int ncase = argc > 1 ? std::atoi(argv[1]) : 20000;
+    std::mt19937 rng(99);
+    std::vector<Case> cases(ncase);
+    std::vector<float> din((size_t)ncase * kWRaw, 0.f);
+    for (int c = 0; c < ncase; c++) {
+        const int n = 1 + (int)(rng() % (c % 5 == 0 ? 256u : 140u));
+        const int levels = 1 + (int)(rng() % 30u);
+        for (int p = 0; p < n; p++)
+            din[(size_t)c * kWRaw + p] = (c % 2) ? (float)(rng() % (unsigned)levels) * 0.25f
+                                                 : std::ldexp((float)(rng() & 0xFFFFF), -20);
+        const int first = (c % 4 == 0 && n > 1) ? (int)(rng() % (unsigned)n) : 0;
+        const int nth = first + (int)(rng() % (unsigned)(n - first));
+        cases[c] = Case{n, first, nth};
+    }
+    Case* dc;
+    float *di, *dd;
+    uint32_t* dids;
+    int* dst;
+    hipMalloc(&dc, sizeof(Case) * ncase);
+    hipMalloc(&di, din.size() * 4);
+    hipMalloc(&dd, din.size() * 4);
+    hipMalloc(&dids, din.size() * 4);
+    hipMalloc(&dst, 4 * ncase);
+    hipMemcpy(dc, cases.data(), sizeof(Case) * ncase, hipMemcpyHostToDevice);
+    hipMemcpy(di, din.data(), din.size() * 4, hipMemcpyHostToDevice);
+    hipLaunchKernelGGL(k_check, dim3(ncase), dim3(64), 0, 0, dc, di, dd, dids, dst, ncase);
+    if (hipDeviceSynchronize() != hipSuccess) {
+        std::printf("kernel failed\n");
+        return 2;
+    }
+    std::vector<float> dout(din.size());
+    std::vector<uint32_t> idout(din.size());
+    std::vector<int> st(ncase);
+    hipMemcpy(dout.data(), dd, din.size() * 4, hipMemcpyDeviceToHost);
+    hipMemcpy(idout.data(), dids, din.size() * 4, hipMemcpyDeviceToHost);
+    hipMemcpy(st.data(), dst, 4 * ncase, hipMemcpyDeviceToHost);
+    long bad = 0, fallback = 0;
+    for (int c = 0; c < ncase; c++) {
+        const Case k = cases[c];
+        std::vector<DP> ref(k.n);
+        for (int p = 0; p < k.n; p++) ref[p] = DP{din[(size_t)c * kWRaw + p], (uint32_t)p};
+        std::nth_element(ref.begin() + k.first, ref.begin() + k.nth, ref.begin() + k.n);
+        if (!st[c]) {
+            fallback++;
+            continue;
+        }
+        for (int p = 0; p < k.n; p++)
+            if (idout[(size_t)c * kWRaw + p] != ref[p].id) {
+                if (bad < 3) std::printf("case %d n %d first %d nth %d: pos %d got %u want %u\n", c, k.n, k.first,
+                                         k.nth, p, idout[(size_t)c * kWRaw + p], ref[p].id);
+                bad++;
+                break;
+            }
+    }
+    std::printf("%d cases, %ld mismatches, %ld depth-limit fallbacks\n", ncase, bad, fallback);
+    return bad == 0 ? 0 : 1;
+}

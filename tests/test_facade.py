@@ -71,3 +71,30 @@ def test_facade_matches_oracle(built, tmp_path):
     assert np.linalg.norm(pos - sr["pos"]) <= 1e-5 * upd
     assert np.linalg.norm(rot - sr["rot"]) <= 1e-5 * max(np.linalg.norm(rs["solution"][:, :3]), 1e-12)
     assert np.linalg.norm(cov - sr["cov"]) <= 1e-9 * np.linalg.norm(st["cov"])
+
+
+@pytest.mark.gpu
+def test_facade_ivox_matches_oracle(built, tmp_path):
+    """The default-build flow through the facade: use_ivox + AddPoints, h_share_model,
+    the IEKF loop, map_incremental — against the oracle's IVox restatement."""
+    import oracle
+    from livo_amd import synth
+    m, body, st, files = _inputs(tmp_path, n_map=300_000)
+    r = subprocess.run([DEMO, *files, "4", "ivox"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    lines = {ln.split()[0]: ln.split()[1:] for ln in r.stdout.splitlines()}
+    iv = oracle.Ivox()
+    iv.add_points(m)
+    hs = np.array(lines["hshare"], dtype=np.float64)
+    ref = iv.h_share(body, st["rot"], st["pos"], np.eye(3), synth.T_LI, True, oracle.new_cache(len(body)))
+    assert int(hs[0]) == ref["effct"]
+    assert np.linalg.norm(hs[1:82].reshape(9, 9) - ref["HTH"]) <= 1e-9 * np.linalg.norm(ref["HTH"])
+    cache = oracle.new_cache(len(body))
+    sr, rs = iv.iekf_update(body, st, cache, t_LI=synth.T_LI, max_iter=4)
+    it = np.array(lines["iekf"], dtype=np.float64)
+    assert int(it[0]) == rs["iterations"] and int(it[1]) == rs["converged"]
+    assert np.linalg.norm(it[11:14] - sr["pos"]) <= 1e-5 * np.linalg.norm(sr["pos"] - st["pos"])
+    # map_incremental ran at the GPU's updated state: same categories up to that state's rounding
+    _, cnt = iv.map_incremental(body, sr, cache, t_LI=synth.T_LI, filter_size_map=0.5)
+    got = [int(x) for x in lines["incr"]]
+    assert abs(got[0] - cnt["added"]) <= 2 and abs(got[1] - cnt["no_downsample"]) <= 2

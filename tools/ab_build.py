@@ -1,9 +1,9 @@
 """Build variant libraries for on-GPU A/B runs (LIVO_LIB selects one).
 
 usage: python tools/ab_build.py NAME [-DMACRO=VALUE ...] [ENV=VALUE ...]
-Writes fast-livo-noted_amd/lib/variants/NAME.so: livo_kernels.hip compiled with
-the extra -D flags (the tuning macros of livo_internal.h / livo_kernels.hip),
-linked with the host objects of the regular build.  Run A/B on one box, e.g.
+Writes fast-livo-noted_amd/lib/variants/NAME.so: every device source compiled
+with the extra -D flags (the tuning macros of livo_internal.h and the kernel
+files), linked with the host objects of the regular build.  Run A/B on one box, e.g.
   LIVO_LIB=fast-livo-noted_amd/lib/variants/NAME.so python bench.py
 """
 import os
@@ -19,14 +19,19 @@ def main(name, *flags):
     B.build()
     vdir = os.path.join(B.LIB_DIR, "variants")
     os.makedirs(vdir, exist_ok=True)
-    obj = os.path.join(vdir, name + ".o")
-    cmd = [B.HIPCC] + B.COMMON + B.DEVICE + ["-x", "hip"] + list(flags) + \
-        ["-c", "-o", obj, os.path.join(B.CSRC, "livo_kernels.hip")]
-    B._run(cmd)
-    host = [os.path.join(B.OBJ_DIR, s + ".o") for s, dev in B.SOURCES if not dev]
+    objs = []
+    for src, dev in B.SOURCES:
+        if not dev:
+            objs.append(os.path.join(B.OBJ_DIR, src + ".o"))
+            continue
+        obj = os.path.join(vdir, name + "." + src + ".o")
+        B._run([B.HIPCC] + B.COMMON + B.DEVICE + ["-x", "hip"] + list(flags) + ["-c", "-o", obj, os.path.join(B.CSRC, src)])
+        objs.append(obj)
     out = os.path.join(vdir, name + ".so")
-    B._run([B.HIPCC, "-shared", "-fPIC", "--offload-arch=" + B.ARCH, "-pthread", "-o", out, obj] + host)
-    os.remove(obj)
+    B._run([B.HIPCC, "-shared", "-fPIC", "--offload-arch=" + B.ARCH, "-pthread", "-o", out] + objs)
+    for o in objs:
+        if o.startswith(vdir):
+            os.remove(o)
     print(out)
 
 
