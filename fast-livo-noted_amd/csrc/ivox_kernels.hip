@@ -446,11 +446,8 @@ __global__ __launch_bounds__(64 * kWaves) void k_ivox_knn_wave(KnnParams P) {
 // LIVO_IVOX_KIND=thread|wave forces one; LIVO_IVOX_WAVE_MAX sets the switch
 // point (queries per launch, default 131072).
 static int ivox_kind(int64_t queries) {
-    static const int forced = [] {
-        const char* e = std::getenv("LIVO_IVOX_KIND");
-        if (!e) return -1;
-        return std::strcmp(e, "thread") == 0 ? 0 : (std::strcmp(e, "wave") == 0 ? 1 : -1);
-    }();
+    const char* e = std::getenv("LIVO_IVOX_KIND");  // read per launch (tests switch it)
+    const int forced = !e ? -1 : (std::strcmp(e, "thread") == 0 ? 0 : (std::strcmp(e, "wave") == 0 ? 1 : -1));
     static const int64_t wave_max = [] {
         const char* e = std::getenv("LIVO_IVOX_WAVE_MAX");
         return e ? (int64_t)std::atoll(e) : (int64_t)131072;

@@ -333,3 +333,39 @@ def test_ivox_batch_overflow_groups(ivctx):
     finally:
         for s in sids + sids2:
             ivctx.scan_release(s)
+
+
+def test_wave_nth_matches_libstdcxx(built):
+    """The wave-parallel std::nth_element of the wave-cooperative iVox search
+    (csrc/wave_select.h) against libstdc++ on the host, element for element:
+    20000 cases of 1..256 elements, many ties, nonzero first."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "fast-livo-noted_amd", "lib",
+                       "wave_nth_check")
+    r = subprocess.run([exe, "20000"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert " 0 mismatches" in r.stdout
+
+
+@pytest.mark.parametrize("kind", ["wave", "thread"])
+def test_ivox_kernel_kinds_agree(ivctx, kind, monkeypatch):
+    """Both search kernels (chosen per launch by size; LIVO_IVOX_KIND forces
+    one) give the oracle's answer, in batch IEKF updates too."""
+    import oracle
+    synth = _synth()
+    monkeypatch.setenv("LIVO_IVOX_KIND", kind)
+    m = synth.make_map(200_000)
+    iv = _pair(ivctx, m)
+    rng = np.random.default_rng(3)
+    q = (m[rng.choice(len(m), 30_000)] + rng.normal(0, 0.1, (30_000, 3))).astype(np.float32)
+    _knn_equal(ivctx, iv, q)
+    body, _, _ = synth.make_scan(20_000, 50)
+    st0 = synth.make_state(50)
+    sid = ivctx.scan_upload(body)
+    try:
+        sg, stg = ivctx.iekf_update(sid, st0)
+    finally:
+        ivctx.scan_release(sid)
+    sr, str_ = iv.iekf_update(body, st0, oracle.new_cache(len(body)), t_LI=synth.T_LI)
+    _iekf_check(stg, sg, str_, sr, st0)
