@@ -229,7 +229,7 @@ __global__ __launch_bounds__(64) void k_ivox_knn_big(KnnParams P) {
 
 // ------------------------------------------------- wave-cooperative search --
 // One query per wave.  The nearby grids are probed by one lane each, their
-// points loaded at once (<= kWRaw per query, 4 per lane), the in-range ones
+// points loaded at once (<= kWRaw per query, 8 per lane), the in-range ones
 // staged in LDS in the reference's push order (grid by grid, insertion order),
 // and every std::nth_element of GetClosestPoint is run by the whole wave:
 // libstdc++'s unguarded Hoare partition computed in parallel.  With pv the
@@ -238,9 +238,40 @@ __global__ __launch_bounds__(64) void k_ivox_knn_big(KnnParams P) {
 // sequential partition swaps Lo[k] <-> Ro[k] for every k < k* (the pairs with
 // Lo[k] < Ro[k]) and returns cut = min(Lo[k*], Ro[k*-1]).  Ranks come from
 // ballots, partners from two LDS tables.  The median-of-3 step and the final
-// insertion sort of <= 3 elements are done by lane 0 as written.  Queries with
-// more than kWRaw raw points, or an introselect whose depth limit runs out
-// (libstdc++ then switches to a heap select), go to the global-memory pass.
+// insertion sort of <= 3 elements are done by lane 0 as written.  A query with
+// more than kWRaw raw points streams grid by grid instead (each grid truncated
+// right away, as the reference does); one whose grids are too large even for
+// that, or whose introselect exhausts its depth limit (libstdc++ then switches
+// to a heap select), goes to the global-memory pass.
+// NNRec from the wave's first n (<= 5) list entries: lanes 0..4 the points, lane 0 the indices.
+__device__ __forceinline__ void wave_write(NNRec* __restrict__ out, const float4* __restrict__ pts, const WaveLds& L,
+                                           int n, int lane) {
+    float4* o4 = reinterpret_cast<float4*>(out);
+    const uint32_t myid = lane < n ? L.id[lane] : 0u;
+    const float myd = lane < n ? L.d[lane] : INFINITY;
+    int32_t pidx = -1;
+    if (lane < kNN) {
+        float4 v = make_float4(0.f, 0.f, 0.f, INFINITY);
+        if (lane < n) {
+            const float4 pp = pts[myid];
+            v = make_float4(pp.x, pp.y, pp.z, myd);
+            pidx = __float_as_int(pp.w);
+        }
+        o4[lane] = v;
+    }
+    const int32_t node = lane < n ? (int32_t)myid : -1;
+    const int32_t i0 = __shfl(pidx, 0, 64), i1 = __shfl(pidx, 1, 64), i2 = __shfl(pidx, 2, 64),
+                  i3 = __shfl(pidx, 3, 64), i4 = __shfl(pidx, 4, 64);
+    const int32_t n0 = __shfl(node, 0, 64), n1 = __shfl(node, 1, 64), n2 = __shfl(node, 2, 64),
+                  n3 = __shfl(node, 3, 64), n4 = __shfl(node, 4, 64);
+    if (lane == 0) {
+        int4* oi = reinterpret_cast<int4*>(out) + 5;
+        oi[0] = make_int4(i0, i1, i2, i3);
+        oi[1] = make_int4(i4, n, 0, n0);
+        oi[2] = make_int4(n1, n2, n3, n4);
+    }
+}
+
 template <bool LATER>
 __global__ __launch_bounds__(64 * kWaves) void k_ivox_knn_wave(KnnParams P) {
     __shared__ WaveLds lds[kWaves];
@@ -278,8 +309,57 @@ __global__ __launch_bounds__(64 * kWaves) void k_ivox_knn_wave(KnnParams P) {
     }
     const uint32_t R = __shfl(incl, 63, 64);
     const uint32_t excl = incl - run.y;
+    const int K = V.max_num;
+    const float4* __restrict__ pts = reinterpret_cast<const float4*>(V.pts);
     if (R > (uint32_t)kWRaw) {
-        if (lane == 0) {
+        // streaming: grid by grid, each truncated to K right away as the
+        // reference does, so only 5 per grid + one grid's points are staged
+        int n = 0;
+        bool ok = true;
+#pragma unroll 1
+        for (int tt = 0; tt < V.nearby && ok; tt++) {
+            const uint32_t c = __shfl(run.y, tt, 64), st = __shfl(run.x, tt, 64);
+            const int old = n;
+#pragma unroll 1
+            for (uint32_t k0 = 0; k0 < c && ok; k0 += 64) {
+                const uint32_t k = k0 + lane;
+                bool in = false;
+                float d = 0.f;
+                if (k < c) {
+                    const float4 v = pts[st + k];
+                    const float dx = v.x - qx, dy = v.y - qy, dz = v.z - qz;
+                    d = dx * dx + (dy * dy + dz * dz);
+                    in = (double)d < V.range2;
+                }
+                const unsigned long long m = __ballot(in);
+                if (n + __popcll(m) > kWRaw) {
+                    ok = false;
+                } else {
+                    if (in) {
+                        const int pos = n + lanes_below(m, lane);
+                        L.d[pos] = d;
+                        L.id[pos] = st + k;
+                    }
+                    n += __popcll(m);
+                }
+            }
+            wave_sync();
+            if (ok && n - old > K) {
+                ok = wave_nth(L, old, old + K - 1, n, lane);
+                n = old + K;
+            }
+        }
+        if (ok && n == 0) return;  // no candidate: the cache stays
+        if (ok && n > K) {
+            ok = wave_nth(L, 0, K - 1, n, lane);
+            n = K;
+        }
+        if (ok) ok = wave_nth(L, 0, 0, n, lane);
+        if (ok) {
+            wave_write(job.nn + i, pts, L, n, lane);
+            return;
+        }
+        if (lane == 0) {  // a grid too large even for streaming, or a heap select
             const unsigned r = atomicAdd(P.replay_count, 1u);
             P.replay_list[r] = ((unsigned long long)bjob << 32) | (unsigned)i;
         }
@@ -287,13 +367,12 @@ __global__ __launch_bounds__(64 * kWaves) void k_ivox_knn_wave(KnnParams P) {
     }
     if (lane <= kIvMaxNearby) L.m[lane] = 0u;
     // every raw point at once (raw index g = 64 r + lane, in grid order)
-    const float4* __restrict__ pts = reinterpret_cast<const float4*>(V.pts);
-    float dist[4];
-    uint32_t pid[4];
-    int gnode[4];
-    bool inr[4];
+    float dist[kWRounds];
+    uint32_t pid[kWRounds];
+    int gnode[kWRounds];
+    bool inr[kWRounds];
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
+    for (int r = 0; r < kWRounds; r++) {
         const uint32_t g = 64u * r + lane;
         int t = 0;
 #pragma unroll 1
@@ -317,7 +396,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_ivox_knn_wave(KnnParams P) {
     // stage the in-range points in push order (ivox3d_node.hpp:154-164)
     int base = 0;
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
+    for (int r = 0; r < kWRounds; r++) {
         const unsigned long long m = __ballot(inr[r]);
         if (inr[r]) {
             const int pos = base + lanes_below(m, lane);
@@ -342,7 +421,6 @@ __global__ __launch_bounds__(64 * kWaves) void k_ivox_knn_wave(KnnParams P) {
     IVDBG("staged", base);
     if (base == 0) return;  // no candidate: the reference returns false, the cache stays
     // per grid: KNNPointByCondition's nth_element on its own run (ivox3d_node.hpp:179-183)
-    const int K = V.max_num;
     const uint32_t mt = lane < V.nearby ? L.m[lane] : 0u;
     uint32_t s_incl = mt;
     uint32_t k_incl = min(mt, (uint32_t)K);
@@ -369,11 +447,11 @@ __global__ __launch_bounds__(64 * kWaves) void k_ivox_knn_wave(KnnParams P) {
     }
     if (ok) {
         // survivors: the first min(m, K) of each grid's segment, in grid order
-        float cd[4];
-        uint32_t cid[4];
-        int dst[4];
+        float cd[kWRounds];
+        uint32_t cid[kWRounds];
+        int dst[kWRounds];
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
+        for (int r = 0; r < kWRounds; r++) {
             const int p = 64 * r + lane;
             // shuffles outside the branch: ds_bpermute reads 0 from inactive lanes
             const int t = p < base ? L.node[p] : 0;
@@ -387,7 +465,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_ivox_knn_wave(KnnParams P) {
         }
         wave_sync();
 #pragma unroll
-        for (int r = 0; r < 4; r++)
+        for (int r = 0; r < kWRounds; r++)
             if (dst[r] >= 0) {
                 L.d[dst[r]] = cd[r];
                 L.id[dst[r]] = cid[r];
@@ -403,32 +481,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_ivox_knn_wave(KnnParams P) {
         if (ok) ok = wave_nth(L, 0, 0, n, lane);  // ivox3d.h:178
         IVDBG("final", n);
         if (ok) {
-            // NNRec: lanes 0..4 the points, lane 0 the indices
-            NNRec* out = job.nn + i;
-            float4* o4 = reinterpret_cast<float4*>(out);
-            const uint32_t myid = lane < n ? L.id[lane] : 0u;
-            const float myd = lane < n ? L.d[lane] : INFINITY;
-            int32_t pidx = -1;
-            if (lane < kNN) {
-                float4 v = make_float4(0.f, 0.f, 0.f, INFINITY);
-                if (lane < n) {
-                    const float4 pp = pts[myid];
-                    v = make_float4(pp.x, pp.y, pp.z, myd);
-                    pidx = __float_as_int(pp.w);
-                }
-                o4[lane] = v;
-            }
-            const int32_t i0 = __shfl(pidx, 0, 64), i1 = __shfl(pidx, 1, 64), i2 = __shfl(pidx, 2, 64),
-                          i3 = __shfl(pidx, 3, 64), i4 = __shfl(pidx, 4, 64);
-            const int32_t nd0 = __shfl(lane < n ? (int)myid : -1, 0, 64), nd1 = __shfl(lane < n ? (int)myid : -1, 1, 64),
-                          nd2 = __shfl(lane < n ? (int)myid : -1, 2, 64), nd3 = __shfl(lane < n ? (int)myid : -1, 3, 64),
-                          nd4 = __shfl(lane < n ? (int)myid : -1, 4, 64);
-            if (lane == 0) {
-                int4* oi = reinterpret_cast<int4*>(out) + 5;
-                oi[0] = make_int4(i0, i1, i2, i3);
-                oi[1] = make_int4(i4, n, 0, nd0);
-                oi[2] = make_int4(nd1, nd2, nd3, nd4);
-            }
+            wave_write(job.nn + i, pts, L, n, lane);
             return;
         }
     }
@@ -578,7 +631,9 @@ __global__ void k_iv_fix(IvoxParams P) {
     // the largest grid: one atomic per wave
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) cnt = max(cnt, (unsigned)__shfl_xor((int)cnt, off, 64));
-    if ((threadIdx.x & 63) == 0 && cnt) atomicMax(P.ctr + 2, (unsigned long long)cnt);
+    if ((threadIdx.x & 63) == 0 && cnt &&
+        (unsigned long long)cnt > __hip_atomic_load(P.ctr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicMax(P.ctr + 2, (unsigned long long)cnt);
 }
 
 __global__ void k_iv_rehash(const GridSlot* __restrict__ old_slots, int64_t old_table, GridSlot* slots, int log2) {

@@ -333,12 +333,9 @@ static void ivox_free(IvoxDev& v) {
     v = IvoxDev{};
 }
 
-// Hash table with room for `grids` grids at load factor <= 1/2 (rehash on growth).
-static int ivox_ensure_table(livo_ctx* c, int64_t grids) {
+// Rehash into a table of 2^log2 slots (and per-slot arrays to match).
+static int ivox_rehash_to(livo_ctx* c, int log2) {
     IvoxDev& v = c->iv;
-    if (v.table >= 2 * grids && v.table > 0) return LIVO_OK;
-    int log2 = 10;
-    while (((int64_t)1 << log2) < 4 * grids) log2++;
     if (log2 > 31) return LIVO_E_RANGE;
     const int64_t table = (int64_t)1 << log2;
     GridSlot* slots = nullptr;
@@ -360,6 +357,27 @@ static int ivox_ensure_table(livo_ctx* c, int64_t grids) {
         return LIVO_E_OOM;
     HIP_TRY(hipMemsetAsync(v.addcnt, 0, (size_t)table * sizeof(uint32_t), c->stream));
     return LIVO_OK;
+}
+
+static int table_log2_for(int64_t grids) {
+    int log2 = 10;
+    while (((int64_t)1 << log2) < 4 * grids) log2++;
+    return log2;
+}
+
+// Hash table with room for `grids` grids at load factor <= 1/2 (rehash on growth).
+static int ivox_ensure_table(livo_ctx* c, int64_t grids) {
+    IvoxDev& v = c->iv;
+    if (v.table >= 2 * grids && v.table > 0) return LIVO_OK;
+    return ivox_rehash_to(c, table_log2_for(grids));
+}
+
+// After an insert sized for its worst case (every point a new grid): shrink a
+// table left below 1/16 full, so the per-slot passes of later inserts stay short.
+static int ivox_trim_table(livo_ctx* c) {
+    IvoxDev& v = c->iv;
+    const int log2 = table_log2_for(std::max<int64_t>(v.ngrids, 256));
+    return log2 + 2 <= v.log2 ? ivox_rehash_to(c, log2) : LIVO_OK;
 }
 
 static int ivox_ensure_src(livo_ctx* c, int64_t n) {
@@ -497,7 +515,8 @@ static int ivox_add_dev(livo_ctx* c, int64_t n) {
     v.ngrids += (int64_t)ctr[1];
     v.next_id += n;
     v.max_grid = (int64_t)ctr[2];
-    return ivox_ensure_big(c);
+    rc = ivox_trim_table(c);
+    return rc ? rc : ivox_ensure_big(c);
 }
 
 static bool map_ready(const livo_ctx* c) {

@@ -10,11 +10,12 @@
 
 namespace livo {
 
-constexpr int kWRaw = 256;
+constexpr int kWRaw = 512;
 #ifndef LIVO_IV_WAVES
 #define LIVO_IV_WAVES 4
 #endif
 constexpr int kWaves = LIVO_IV_WAVES;  // queries (waves) per block
+constexpr int kWRounds = kWRaw / 64;  // positions per lane
 
 struct WaveLds {
     float d[kWRaw];
@@ -69,11 +70,11 @@ __device__ __forceinline__ bool wave_nth(WaveLds& L, int first, int nth, int las
         const float pv = L.d[first];
         const int lo = first + 1;
         const int nr = (last - lo + 63) >> 6;  // rounds of 64 positions actually in range (uniform)
-        bool lf[4], rf[4];
-        unsigned long long lm[4], rm[4];
+        bool lf[kWRounds], rf[kWRounds];
+        unsigned long long lm[kWRounds], rm[kWRounds];
         int nL = 0, nR = 0;
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
+        for (int r = 0; r < kWRounds; r++) {
             lf[r] = rf[r] = false;
             lm[r] = rm[r] = 0ull;
             if (r < nr) {
@@ -88,11 +89,11 @@ __device__ __forceinline__ bool wave_nth(WaveLds& L, int first, int nth, int las
                 nR += __popcll(rm[r]);
             }
         }
-        int lrank[4], rrank[4];
-        bool ok[4];
+        int lrank[kWRounds], rrank[kWRounds];
+        bool ok[kWRounds];
         int kstar = 0, lb = 0, rb = 0;
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
+        for (int r = 0; r < kWRounds; r++) {
             lrank[r] = lb + lanes_below(lm[r], lane);
             const int rle = rb + lanes_below(rm[r], lane) + (rf[r] ? 1 : 0);  // rf positions <= p
             rrank[r] = nR - rle;  // rf positions > p: the rank in Ro
@@ -102,17 +103,17 @@ __device__ __forceinline__ bool wave_nth(WaveLds& L, int first, int nth, int las
             rb += __popcll(rm[r]);
         }
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
+        for (int r = 0; r < kWRounds; r++) {
             const int p = lo + 64 * r + lane;
             if (lf[r]) L.lt[lrank[r]] = (uint16_t)p;
             if (rf[r]) L.rt[rrank[r]] = (uint16_t)p;
         }
         wave_sync();
-        float nd[4];
-        uint32_t nid[4];
-        bool sw[4];
+        float nd[kWRounds];
+        uint32_t nid[kWRounds];
+        bool sw[kWRounds];
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
+        for (int r = 0; r < kWRounds; r++) {
             sw[r] = (lf[r] && lrank[r] < kstar) || (rf[r] && rrank[r] < kstar);
             int partner = 0;
             if (lf[r] && lrank[r] < kstar) partner = L.rt[lrank[r]];
@@ -124,7 +125,7 @@ __device__ __forceinline__ bool wave_nth(WaveLds& L, int first, int nth, int las
                                      : (int)L.rt[kstar - 1];
         wave_sync();
 #pragma unroll
-        for (int r = 0; r < 4; r++)
+        for (int r = 0; r < kWRounds; r++)
             if (sw[r]) {
                 const int p = lo + 64 * r + lane;
                 L.d[p] = nd[r];

@@ -1,7 +1,7 @@
 // GPU unit check (tests/test_gpu_ivox.py): wave_nth (fast-livo-noted_amd/csrc/
 // wave_select.h), the wave-parallel std::nth_element of the iVox search,
 // against libstdc++'s std::nth_element on the host, element for element.
-// One wave per case; cases of 1..256 elements with many ties.
+// One wave per case; cases of 1..kWRaw elements with many ties.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -48,7 +48,7 @@ int main(int argc, char** argv) {
     std::vector<Case> cases(ncase);
     std::vector<float> din((size_t)ncase * kWRaw, 0.f);
     for (int c = 0; c < ncase; c++) {
-        const int n = 1 + (int)(rng() % (c % 5 == 0 ? 256u : 140u));
+        const int n = 1 + (int)(rng() % (c % 5 == 0 ? (unsigned)kWRaw : 140u));
         const int levels = 1 + (int)(rng() % 30u);
         for (int p = 0; p < n; p++)
             din[(size_t)c * kWRaw + p] = (c % 2) ? (float)(rng() % (unsigned)levels) * 0.25f

@@ -38,9 +38,12 @@ def test_facade_usage_error(built):
 
 
 def test_facade_fails_loudly_without_gpu(built, tmp_path):
-    import torch
-    if torch.cuda.is_available():
+    import livo_amd
+    try:
+        livo_amd.Context(0).close()
         pytest.skip("a GPU is present")
+    except livo_amd.LivoError:
+        pass
     _, _, _, files = _inputs(tmp_path, n_map=2000, n_scan=500)
     r = subprocess.run([DEMO, *files, "4"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 3, r.stdout + r.stderr
