@@ -315,3 +315,96 @@ def make_raw_scan(n_points: int, scan_id: int = 0, n_imu: int = 21, scene: Scene
     rot_end = R @ so3_exp(w * t_end)
     pos_end = p + v * t_end + 0.5 * acc * t_end * t_end
     return np.ascontiguousarray(raw), poses, rot_end, pos_end
+
+
+# ---------------------------------------------------------------- VIO ----
+# camera_pinhole_resize.yaml (640x512 pinhole, radial-tangential d0..d3)
+PINHOLE = {"width": 640, "height": 512, "fx": 431.795259219, "fy": 431.550090267, "cx": 310.833037316,
+           "cy": 266.985989326, "d": [-0.0944205499243979, 0.0946727677776504, -0.00807970960613932,
+                                      8.07461209775283e-05, 0.0]}
+# IMU (x forward, z up) -> camera (z forward, y down)
+R_CI = np.array([[0.0, -1.0, 0.0], [0.0, 0.0, -1.0], [1.0, 0.0, 0.0]])
+P_CI = np.array([0.02, -0.05, 0.03])
+
+
+def _texture(w: int, h: int, rng) -> np.ndarray:
+    """A smooth, textured 8-bit image (sums of oriented sinusoids and blobs)."""
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float64)
+    img = np.full((h, w), 128.0)
+    for _ in range(24):
+        k = rng.uniform(0.02, 0.12)
+        th = rng.uniform(0, np.pi)
+        ph = rng.uniform(0, 2 * np.pi)
+        img += rng.uniform(6, 14) * np.sin(k * (np.cos(th) * xx + np.sin(th) * yy) + ph)
+    for _ in range(60):
+        cx, cy, r = rng.uniform(0, w), rng.uniform(0, h), rng.uniform(4, 25)
+        img += rng.uniform(-40, 40) * np.exp(-((xx - cx) ** 2 + (yy - cy) ** 2) / (2 * r * r))
+    return np.clip(img, 0, 255).astype(np.uint8)
+
+
+def _world2cam(cam, pc):
+    u, v = pc[..., 0] / pc[..., 2], pc[..., 1] / pc[..., 2]
+    d = cam["d"]
+    r2 = u * u + v * v
+    cd = 1 + d[0] * r2 + d[1] * r2 * r2 + d[4] * r2 * r2 * r2
+    xd = u * cd + d[2] * 2 * u * v + d[3] * (r2 + 2 * u * u)
+    yd = v * cd + d[2] * (r2 + 2 * v * v) + d[3] * 2 * u * v
+    return np.stack([xd * cam["fx"] + cam["cx"], yd * cam["fy"] + cam["cy"]], axis=-1)
+
+
+def _patch(img, px, level, ps=4):
+    """The reference patch of one point at one level: the same bilinear sample
+    the update uses (lidar_selection.cpp:818-842), at the true projection."""
+    scale = 1 << level
+    h, w = img.shape
+    ui = int(np.floor(np.float32(px[0] / scale)) * scale)
+    vi = int(np.floor(np.float32(px[1] / scale)) * scale)
+    su = np.float32((np.float32(px[0]) - ui) / scale)
+    sv = np.float32((np.float32(px[1]) - vi) / scale)
+    wtl, wtr = np.float32((1 - su) * (1 - sv)), np.float32(su * (1 - sv))
+    wbl, wbr = np.float32((1 - su) * sv), np.float32(su * sv)
+    out = np.zeros(ps * ps, np.float32)
+    half = ps // 2
+    for x in range(ps):
+        for y in range(ps):
+            r = vi + x * scale - half * scale
+            c = ui - half * scale + y * scale
+            out[x * ps + y] = wtl * img[r, c] + wtr * img[r, c + scale] + wbl * img[r + scale, c] + \
+                wbr * img[r + scale, c + scale]
+    return out
+
+
+def make_vio_frame(n_points: int, frame_id: int = 0, patch_size: int = 4, rot_deg: float = 0.3,
+                   trans_m: float = 0.02):
+    """A synthetic VIO frame for the photometric update:
+    a textured 640x512 image, n visual points (world positions) seen in it,
+    their reference patches at levels 0..2 (sampled at the true pose), search
+    levels 0..2, and an initial state = truth perturbed.  Returns (frame, state0, truth)."""
+    rng = np.random.default_rng(SEED_SCAN + 104729 * (frame_id + 1))
+    cam = dict(PINHOLE)
+    img = _texture(cam["width"], cam["height"], rng)
+    R, p, _ = true_pose(frame_id)
+    margin = 80
+    px = np.stack([rng.uniform(margin, cam["width"] - margin, n_points),
+                   rng.uniform(margin, cam["height"] - margin, n_points)], axis=1)
+    depth = rng.uniform(2.0, 12.0, n_points)
+    # back-project (distortion ignored: the point is then wherever world2cam puts it)
+    xc = np.stack([(px[:, 0] - cam["cx"]) / cam["fx"], (px[:, 1] - cam["cy"]) / cam["fy"], np.ones(n_points)], 1)
+    pcam = xc * depth[:, None]
+    pos = ((pcam - P_CI) @ R_CI) @ R.T + p     # p_w = R (R_ci^T (p_c - P_ci)) + p
+    pc_true = ((pos - p) @ R) @ R_CI.T + P_CI
+    pix = _world2cam(cam, pc_true)
+    ok = (pix[:, 0] > 64) & (pix[:, 0] < cam["width"] - 64) & (pix[:, 1] > 64) & (pix[:, 1] < cam["height"] - 64)
+    pos, pix = pos[ok], pix[ok]
+    levels = rng.integers(0, 3, size=len(pos)).astype(np.int32)
+    pst = patch_size * patch_size
+    patches = np.zeros((len(pos), 3 * pst), np.float32)
+    for i in range(len(pos)):
+        for lv in range(3):
+            patches[i, lv * pst:(lv + 1) * pst] = _patch(img, pix[i], lv + levels[i], patch_size)
+    frame = {"image": img, "cam": cam, "pos": pos, "levels": levels, "patches": patches, "patch_size": patch_size,
+             "Rci": R_CI, "Pci": P_CI}
+    st = make_state(frame_id, rot_deg=rot_deg, trans_m=trans_m)
+    truth = dict(st)
+    truth["rot"], truth["pos"] = R, p
+    return frame, st, truth

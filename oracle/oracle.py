@@ -404,3 +404,51 @@ def voxel_grid(raw, leaf):
     out = np.zeros_like(raw)
     k = _front_lib().orc_voxel_grid(_p(raw), raw.shape[0], C.c_float(leaf), _p(out))
     return out[:k].copy()
+
+
+class OrcCam(C.Structure):
+    _fields_ = [("fx", C.c_double), ("fy", C.c_double), ("cx", C.c_double), ("cy", C.c_double),
+                ("d", C.c_double * 5), ("width", C.c_int32), ("height", C.c_int32)]
+
+
+class OrcVioStats(C.Structure):
+    _fields_ = [("iterations", C.c_int32 * 3), ("updates", C.c_int32 * 3), ("last_error", C.c_float * 3),
+                ("cov_updated", C.c_int32), ("n_meas", C.c_int64), ("out_of_frame", C.c_int64)]
+
+
+def cam_to_c(cam: dict) -> OrcCam:
+    c = OrcCam()
+    c.fx, c.fy, c.cx, c.cy = cam["fx"], cam["fy"], cam["cx"], cam["cy"]
+    c.d[:] = list(cam["d"]) + [0.0] * (5 - len(cam["d"]))
+    c.width, c.height = cam["width"], cam["height"]
+    return c
+
+
+def vio_stats_from(st) -> dict:
+    return {"iterations": list(st.iterations), "updates": list(st.updates), "last_error": list(st.last_error),
+            "cov_updated": st.cov_updated, "n_meas": st.n_meas, "out_of_frame": st.out_of_frame}
+
+
+def vio_update(frame: dict, state: dict, prior: dict | None = None, max_iter: int = 4, img_point_cov: float = 10.0):
+    """ComputeJ + UpdateState (lidar_selection.cpp:748-978) on a frame dict from synth.make_vio_frame."""
+    L = lib()
+    if not getattr(L, "_vio", False):
+        L.orc_vio_update.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(OrcCam), C.c_void_p, C.c_void_p,
+                                     C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_void_p, C.c_double, C.c_int,
+                                     C.POINTER(OrcState), C.POINTER(OrcState), C.c_void_p, C.POINTER(OrcVioStats)]
+        L._vio = True
+    img = np.ascontiguousarray(frame["image"], np.uint8)
+    pos = np.ascontiguousarray(frame["pos"], np.float64)
+    lev = np.ascontiguousarray(frame["levels"], np.int32)
+    pat = np.ascontiguousarray(frame["patches"], np.float32)
+    n = pos.shape[0]
+    cs = state_to_c(state)
+    pr = state_to_c(prior if prior is not None else state)
+    err = np.zeros(n, np.float32)
+    st = OrcVioStats()
+    cam = cam_to_c(frame["cam"])
+    L.orc_vio_update(_p(img), img.shape[1], img.shape[0], C.byref(cam), _p(pos), _p(lev), _p(pat), n,
+                     frame["patch_size"], _p(np.ascontiguousarray(frame["Rci"], np.float64)),
+                     _p(np.ascontiguousarray(frame["Pci"], np.float64)), img_point_cov, max_iter, C.byref(cs),
+                     C.byref(pr), _p(err), C.byref(st))
+    return state_from_c(cs), vio_stats_from(st), err
