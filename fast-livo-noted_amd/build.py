@@ -29,6 +29,7 @@ SOURCES = [
     ("livo_kernels.hip", True),
     ("ivox_kernels.hip", True),
     ("frontend_kernels.hip", True),
+    ("vio_kernels.hip", True),
     ("prims.hip", True),
     ("livo_capi.cpp", False),
     ("map_build.cpp", False),

@@ -3,6 +3,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "livo.h"
+
 namespace livo {
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -85,6 +87,82 @@ __device__ __forceinline__ void lds_lu_column(const double* s_LU, const int* s_p
 #pragma unroll
         for (int j = i + 1; j < N; j++) sacc = sacc - s_LU[i * N + j] * y[j];
         y[i] = sacc / s_LU[i * N + i];
+    }
+}
+
+#define WAVE_SYNC() do { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); __builtin_amdgcn_wave_barrier(); } while (0)
+
+// SO3 Exp / Log (so3_math.h:55-81) and 3x3 products, sums in index order.
+__device__ __forceinline__ void so3_exp(double v1, double v2, double v3, double* R) {
+    const double norm = sqrt(v1 * v1 + v2 * v2 + v3 * v3);
+    _Pragma("unroll") for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0) ? 1.0 : 0.0;
+    if (norm > 0.00001) {
+        const double r[3] = {v1 / norm, v2 / norm, v3 / norm};
+        const double K[9] = {0.0, -r[2], r[1], r[2], 0.0, -r[0], -r[1], r[0], 0.0};
+        const double s = sin(norm), c1 = 1.0 - cos(norm);
+        double cK[9];
+        _Pragma("unroll") for (int i = 0; i < 9; i++) cK[i] = c1 * K[i];
+        _Pragma("unroll") for (int i = 0; i < 3; i++)
+            _Pragma("unroll") for (int j = 0; j < 3; j++) {
+                const double kk = (cK[i * 3 + 0] * K[0 * 3 + j] + cK[i * 3 + 1] * K[1 * 3 + j]) + cK[i * 3 + 2] * K[2 * 3 + j];
+                R[i * 3 + j] = (R[i * 3 + j] + s * K[i * 3 + j]) + kk;
+            }
+    }
+}
+__device__ __forceinline__ void so3_log(const double* R, double* o) {
+    const double tr = (R[0] + R[4]) + R[8];
+    const double theta = (tr > 3.0 - 1e-6) ? 0.0 : acos(0.5 * (tr - 1));
+    const double K[3] = {R[7] - R[5], R[2] - R[6], R[3] - R[1]};
+    if (fabs(theta) < 0.001) {
+        _Pragma("unroll") for (int i = 0; i < 3; i++) o[i] = 0.5 * K[i];
+    } else {
+        const double f = 0.5 * theta / sin(theta);
+        _Pragma("unroll") for (int i = 0; i < 3; i++) o[i] = f * K[i];
+    }
+}
+__device__ __forceinline__ void mat3_mul(const double* A, const double* B, double* C) {
+    _Pragma("unroll") for (int i = 0; i < 3; i++)
+        _Pragma("unroll") for (int j = 0; j < 3; j++)
+            C[i * 3 + j] = (A[i * 3 + 0] * B[0 * 3 + j] + A[i * 3 + 1] * B[1 * 3 + j]) + A[i * 3 + 2] * B[2 * 3 + j];
+}
+
+// StatesGroup a - b (common_lib.h:576-587): Log(b.rot^T a.rot), then differences.
+__device__ __forceinline__ void state_minus_d(const livo_state& a, const livo_state& b, double* v) {
+    double bt[9], ra[9], rd[9], v3[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            bt[r * 3 + c] = b.rot[c * 3 + r];
+            ra[r * 3 + c] = a.rot[r * 3 + c];
+        }
+    mat3_mul(bt, ra, rd);
+    so3_log(rd, v3);
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        v[r] = v3[r];
+        v[3 + r] = a.pos[r] - b.pos[r];
+        v[6 + r] = a.vel[r] - b.vel[r];
+        v[9 + r] = a.bias_g[r] - b.bias_g[r];
+        v[12 + r] = a.bias_a[r] - b.bias_a[r];
+        v[15 + r] = a.gravity[r] - b.gravity[r];
+    }
+}
+
+// StatesGroup += (common_lib.h:565-574): rot * Exp(d0..2), the rest added.
+__device__ __forceinline__ void state_boxplus_d(livo_state& st, const double* sol) {
+    double E[9], Rn[9];
+    so3_exp(sol[0], sol[1], sol[2], E);
+    mat3_mul(st.rot, E, Rn);
+#pragma unroll
+    for (int k = 0; k < 9; k++) st.rot[k] = Rn[k];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        st.pos[k] += sol[3 + k];
+        st.vel[k] += sol[6 + k];
+        st.bias_g[k] += sol[9 + k];
+        st.bias_a[k] += sol[12 + k];
+        st.gravity[k] += sol[15 + k];
     }
 }
 

@@ -112,6 +112,8 @@ struct livo_ctx {
     IvoxDev iv;                        // iVox map (LIVO_BACKEND_IVOX)
     void* fe_buf = nullptr;            // scan front-end scratch (livo_scan_preprocess)
     size_t fe_bytes = 0;
+    void* vio_buf = nullptr;           // VIO frame (image, points, partials, slot)
+    size_t vio_bytes = 0;
     void* prim_tmp = nullptr;          // rocPRIM scratch (sorts, scans)
     size_t prim_bytes = 0;
     // scans
@@ -609,6 +611,7 @@ int livo_ctx_destroy(livo_ctx* c) {
     ivox_free(c->iv);
     if (c->fe_buf) (void)hipFree(c->fe_buf);
     if (c->prim_tmp) (void)hipFree(c->prim_tmp);
+    if (c->vio_buf) (void)hipFree(c->vio_buf);
     dev_free(c->nodes);
     dev_free(c->lnodes);
     dev_free(c->lpts);
@@ -1594,6 +1597,130 @@ int livo_scan_preprocess(livo_ctx* c, const livo_raw_point* raw, int64_t n, cons
         if (n_kept > 0) HIP_TRY(hipMemcpyAsync(down, kept, (size_t)n_kept * 20, hipMemcpyDeviceToHost, c->stream));
     }
     return scan_create_device(c, kept, 5, n_kept, scan_id);
+}
+
+int livo_vio_params_default(livo_vio_params* p) {
+    if (!p) return LIVO_E_INVALID;
+    std::memset(p, 0, sizeof(*p));
+    // camera_pinhole_resize.yaml
+    p->cam.width = 640;
+    p->cam.height = 512;
+    p->cam.fx = 431.795259219;
+    p->cam.fy = 431.550090267;
+    p->cam.cx = 310.833037316;
+    p->cam.cy = 266.985989326;
+    p->cam.d[0] = -0.0944205499243979;
+    p->cam.d[1] = 0.0946727677776504;
+    p->cam.d[2] = -0.00807970960613932;
+    p->cam.d[3] = 8.07461209775283e-05;
+    p->R_ci[0] = p->R_ci[4] = p->R_ci[8] = 1.0;
+    p->img_point_cov = 10.0;  // laser_mapping.cpp:976
+    p->patch_size = 4;        // laser_mapping.cpp:1015
+    p->max_iterations = 4;    // origin_laserMapping.cpp:1208 (NUM_MAX_ITERATIONS)
+    return LIVO_OK;
+}
+
+int livo_vio_update(livo_ctx* c, const livo_vio_params* p, const uint8_t* image, int32_t width, int32_t height,
+                    const double* pos, const int32_t* levels, const float* patches, int64_t n, livo_state* state,
+                    const livo_state* prior, float* errors, livo_vio_stats* stats) {
+    if (!c || !p || !state || n < 0 || width <= 0 || height <= 0 || !image ||
+        (n > 0 && (!pos || !levels || !patches)) || p->patch_size < 1 || p->patch_size > 8 ||
+        p->max_iterations < 0 || !(p->img_point_cov > 0.0))
+        return LIVO_E_INVALID;
+    for (int64_t i = 0; i < n; i++)
+        if (levels[i] < 0 || levels[i] > 8) return LIVO_E_INVALID;
+    if (n > (int64_t)0x7FFFFFFF - 256) return LIVO_E_RANGE;
+    if (set_device(c)) return LIVO_E_HIP;
+    const int pst = p->patch_size * p->patch_size;
+    const int nblk = (int)std::max<int64_t>(1, (n + 255) / 256);
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t b_img = al((size_t)width * height), b_pos = al((size_t)std::max<int64_t>(n, 1) * 24),
+                 b_lev = al((size_t)std::max<int64_t>(n, 1) * 4),
+                 b_pat = al((size_t)std::max<int64_t>(n, 1) * 3 * pst * 4),
+                 b_par = al((size_t)nblk * kVioCols * 8), b_err = al((size_t)std::max<int64_t>(n, 1) * 4),
+                 b_slot = al(sizeof(VioSlot));
+    const size_t total = b_img + b_pos + b_lev + b_pat + b_par + b_err + b_slot;
+    if (total > c->vio_bytes) {
+        if (c->vio_buf) (void)hipFree(c->vio_buf);
+        c->vio_buf = nullptr;
+        c->vio_bytes = 0;
+        if (hipMalloc(&c->vio_buf, total) != hipSuccess) return LIVO_E_OOM;
+        c->vio_bytes = total;
+    }
+    char* q = (char*)c->vio_buf;
+    uint8_t* d_img = (uint8_t*)q; q += b_img;
+    double* d_pos = (double*)q; q += b_pos;
+    int32_t* d_lev = (int32_t*)q; q += b_lev;
+    float* d_pat = (float*)q; q += b_pat;
+    double* d_par = (double*)q; q += b_par;
+    float* d_err = (float*)q; q += b_err;
+    VioSlot* d_slot = (VioSlot*)q;
+    VioSlot hs;
+    std::memset(&hs, 0, sizeof(hs));
+    hs.state = *state;
+    hs.prior = prior ? *prior : *state;
+    HIP_TRY(hipMemcpyAsync(d_img, image, (size_t)width * height, hipMemcpyHostToDevice, c->stream));
+    if (n > 0) {
+        HIP_TRY(hipMemcpyAsync(d_pos, pos, (size_t)n * 24, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(d_lev, levels, (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(d_pat, patches, (size_t)n * 3 * pst * 4, hipMemcpyHostToDevice, c->stream));
+    }
+    HIP_TRY(hipMemcpyAsync(d_slot, &hs, sizeof(hs), hipMemcpyHostToDevice, c->stream));
+    if (n > 0) HIP_TRY(hipMemsetAsync(d_err, 0, (size_t)n * 4, c->stream));  // errors: 0 until an iteration runs
+    VioParams P{};
+    P.img = d_img;
+    P.w = width;
+    P.h = height;
+    P.fx = p->cam.fx; P.fy = p->cam.fy; P.cx = p->cam.cx; P.cy = p->cam.cy;
+    std::memcpy(P.d, p->cam.d, sizeof(P.d));
+    P.distortion = std::fabs(p->cam.d[0]) > 0.0000001 ? 1 : 0;  // vikit: distortion_ = |d0| > 1e-7
+    P.n = (int32_t)n;
+    P.ps = p->patch_size;
+    P.pos = d_pos;
+    P.levels = d_lev;
+    P.patches = d_pat;
+    std::memcpy(P.Rci, p->R_ci, sizeof(P.Rci));
+    std::memcpy(P.Pci, p->P_ci, sizeof(P.Pci));
+    // init() (lidar_selection.cpp:44-55): Jdphi_dR = Rci, Jdp_dR = -Rci [Pic]x, Pic = -Rci^T Pci
+    std::memcpy(P.Jdphi_dR, p->R_ci, sizeof(P.Jdphi_dR));
+    double Pic[3];
+    for (int a = 0; a < 3; a++)
+        Pic[a] = -((p->R_ci[0 * 3 + a] * p->P_ci[0] + p->R_ci[1 * 3 + a] * p->P_ci[1]) + p->R_ci[2 * 3 + a] * p->P_ci[2]);
+    const double tmp[9] = {0.0, -Pic[2], Pic[1], Pic[2], 0.0, -Pic[0], -Pic[1], Pic[0], 0.0};
+    for (int a = 0; a < 3; a++)
+        for (int b = 0; b < 3; b++)
+            P.Jdp_dR[a * 3 + b] = ((-p->R_ci[a * 3 + 0]) * tmp[0 * 3 + b] + (-p->R_ci[a * 3 + 1]) * tmp[1 * 3 + b]) +
+                                  (-p->R_ci[a * 3 + 2]) * tmp[2 * 3 + b];
+    P.img_cov = p->img_point_cov;
+    P.max_iter = p->max_iterations;
+    P.nblk = nblk;
+    P.partial = d_par;
+    P.perr = d_err;
+    P.slot = d_slot;
+    int rc = LIVO_OK;
+    for (int level = 2; level >= 0 && !rc; level--) {  // ComputeJ (:970-974)
+        P.level = level;
+        rc = launch_vio_begin(P, level, c->stream);
+        for (int it = 0; it < p->max_iterations && !rc; it++) rc = launch_vio_iter(P, c->stream);
+    }
+    if (!rc) rc = launch_vio_end(P, c->stream);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(&hs, d_slot, sizeof(hs), hipMemcpyDeviceToHost, c->stream));
+    if (errors && n > 0) HIP_TRY(hipMemcpyAsync(errors, d_err, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (n > 0) *state = hs.state;
+    if (stats) {
+        std::memset(stats, 0, sizeof(*stats));
+        for (int k = 0; k < 3; k++) {
+            stats->iterations[k] = hs.ctrl.iters[k];
+            stats->updates[k] = hs.ctrl.updates[k];
+            stats->last_error[k] = hs.ctrl.level_error[k];
+        }
+        stats->cov_updated = hs.ctrl.cov_updated;
+        stats->n_meas = hs.ctrl.n_meas;
+        stats->out_of_frame = (int64_t)hs.ctrl.oof;
+    }
+    return LIVO_OK;
 }
 
 int livo_sync(livo_ctx* c) {

@@ -387,6 +387,51 @@ int prim_sort_pairs_u64(void* temp, size_t* temp_bytes, const unsigned long long
                         unsigned long long* keys_out, const uint32_t* vals_in, uint32_t* vals_out, int64_t n,
                         int bits, void* stream);
 
+// VIO photometric update (vio_kernels.hip).
+struct VioCtrl {
+    int32_t level;          // pyramid level of the current UpdateState (2, 1, 0)
+    int32_t end;            // EKF_end of the current level
+    int32_t iteration;      // iterations run in the current level
+    int32_t pinv_ready;     // Pinv holds (cov / img_point_cov)^-1
+    float last_error;       // UpdateState's last_error
+    float pad_;
+    int32_t iters[3], updates[3];
+    float level_error[3];   // UpdateState's return value per level (2, 1, 0)
+    int32_t cov_updated;
+    int64_t n_meas;
+    unsigned long long oof; // patch samples outside the image
+};
+struct alignas(16) VioSlot {
+    livo_state state;
+    livo_state old_state;
+    livo_state prior;       // state_propagat
+    double G6[kDim * 6];    // G(:, 0:6) of the last update
+    double Pinv[kDim * kDim];
+    VioCtrl ctrl;
+    unsigned ticket;        // blocks done in the current pass (the last one solves)
+    unsigned pad_[3];
+};
+constexpr int kVioCols = 28;  // per-block partial: 21 HTH upper-tri + 6 HTz (+ 1 spare)
+struct VioParams {
+    const uint8_t* img;
+    int32_t w, h;
+    double fx, fy, cx, cy, d[5];
+    int32_t distortion;     // vikit distortion_ = |d0| > 1e-7
+    int32_t n, ps;
+    const double* pos;      // n x 3
+    const int32_t* levels;  // n
+    const float* patches;   // n x 3 ps^2
+    double Rci[9], Pci[3], Jdphi_dR[9], Jdp_dR[9];
+    double img_cov;
+    int32_t max_iter, level, nblk, pad_;
+    double* partial;        // nblk x kVioCols
+    float* perr;            // n patch errors (sub_sparse_map->errors)
+    VioSlot* slot;
+};
+int launch_vio_begin(const VioParams& p, int level, void* stream);
+int launch_vio_iter(const VioParams& p, void* stream);
+int launch_vio_end(const VioParams& p, void* stream);
+
 // Nearest_Points carried over by point index (laser_mapping.cpp:165 resize keeps entries).
 int launch_inherit_nn(NNRec* dst, const int32_t* dst_perm, int64_t n_dst, const NNRec* src,
                       const int32_t* src_iperm, int64_t n_src, void* stream);

@@ -1302,40 +1302,8 @@ __device__ __forceinline__ bool esti_plane(const float (&px)[5], const float (&p
 
 // ======================================================= reductions =======
 
-__device__ __forceinline__ void so3_exp(double v1, double v2, double v3, double* R) {
-    const double norm = sqrt(v1 * v1 + v2 * v2 + v3 * v3);
-    _Pragma("unroll") for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0) ? 1.0 : 0.0;
-    if (norm > 0.00001) {
-        const double r[3] = {v1 / norm, v2 / norm, v3 / norm};
-        const double K[9] = {0.0, -r[2], r[1], r[2], 0.0, -r[0], -r[1], r[0], 0.0};
-        const double s = sin(norm), c1 = 1.0 - cos(norm);
-        double cK[9];
-        _Pragma("unroll") for (int i = 0; i < 9; i++) cK[i] = c1 * K[i];
-        _Pragma("unroll") for (int i = 0; i < 3; i++)
-            _Pragma("unroll") for (int j = 0; j < 3; j++) {
-                const double kk = (cK[i * 3 + 0] * K[0 * 3 + j] + cK[i * 3 + 1] * K[1 * 3 + j]) + cK[i * 3 + 2] * K[2 * 3 + j];
-                R[i * 3 + j] = (R[i * 3 + j] + s * K[i * 3 + j]) + kk;
-            }
-    }
-}
 
-__device__ __forceinline__ void so3_log(const double* R, double* o) {
-    const double tr = (R[0] + R[4]) + R[8];
-    const double theta = (tr > 3.0 - 1e-6) ? 0.0 : acos(0.5 * (tr - 1));
-    const double K[3] = {R[7] - R[5], R[2] - R[6], R[3] - R[1]};
-    if (fabs(theta) < 0.001) {
-        _Pragma("unroll") for (int i = 0; i < 3; i++) o[i] = 0.5 * K[i];
-    } else {
-        const double f = 0.5 * theta / sin(theta);
-        _Pragma("unroll") for (int i = 0; i < 3; i++) o[i] = f * K[i];
-    }
-}
 
-__device__ __forceinline__ void mat3_mul(const double* A, const double* B, double* C) {
-    _Pragma("unroll") for (int i = 0; i < 3; i++)
-        _Pragma("unroll") for (int j = 0; j < 3; j++)
-            C[i * 3 + j] = (A[i * 3 + 0] * B[0 * 3 + j] + A[i * 3 + 1] * B[1 * 3 + j]) + A[i * 3 + 2] * B[2 * 3 + j];
-}
 
 // ========================================================== solve =========
 // One wave per scan, the reference's algebra in the oracle's operation order
@@ -1366,7 +1334,6 @@ struct SolveLds {
 // reference's algebra in the oracle's operation order (laser_mapping.cpp:187-238)
 // from the reduced h_share sums in L.sum.  Only this wave touches L, so LDS
 // hand-offs between lanes need a wave-level fence, not a block barrier.
-#define WAVE_SYNC() do { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); __builtin_amdgcn_wave_barrier(); } while (0)
 __device__ __forceinline__ void solve_scan(IekfSlot* slot, SolveLds& L, const int lane) {
     double* const s_sum = L.sum;
     double* const s_P = L.P;
@@ -1441,26 +1408,7 @@ __device__ __forceinline__ void solve_scan(IekfSlot* slot, SolveLds& L, const in
         s_G[t] = g;
     }
     // 6. vec = state_propagat - state
-    if (lane == 0) {
-        const livo_state& a = slot->prior;
-        const livo_state& b = slot->state;
-        double bt[9], ra[9], rd[9], v3[3];
-#pragma unroll
-        for (int r = 0; r < 3; r++)
-#pragma unroll
-            for (int c = 0; c < 3; c++) { bt[r * 3 + c] = b.rot[c * 3 + r]; ra[r * 3 + c] = a.rot[r * 3 + c]; }
-        mat3_mul(bt, ra, rd);
-        so3_log(rd, v3);
-#pragma unroll
-        for (int r = 0; r < 3; r++) {
-            s_vec[r] = v3[r];
-            s_vec[3 + r] = a.pos[r] - b.pos[r];
-            s_vec[6 + r] = a.vel[r] - b.vel[r];
-            s_vec[9 + r] = a.bias_g[r] - b.bias_g[r];
-            s_vec[12 + r] = a.bias_a[r] - b.bias_a[r];
-            s_vec[15 + r] = a.gravity[r] - b.gravity[r];
-        }
-    }
+    if (lane == 0) state_minus_d(slot->prior, slot->state, s_vec);
     WAVE_SYNC();
     SOLVE_MARK(6);
     // 7. solution = K1(:,0:9) HTL + vec - G(:,0:9) vec(0:9)
@@ -1488,20 +1436,7 @@ __device__ __forceinline__ void solve_scan(IekfSlot* slot, SolveLds& L, const in
 #pragma unroll
         for (int k = 0; k < kDim; k++) sol[k] = s_sol[k];
         IekfCtrl ctrl = ctrl0;
-        livo_state& st = slot->state;
-        double E[9], Rn[9];
-        so3_exp(sol[0], sol[1], sol[2], E);
-        mat3_mul(st.rot, E, Rn);
-#pragma unroll
-        for (int k = 0; k < 9; k++) st.rot[k] = Rn[k];
-#pragma unroll
-        for (int k = 0; k < 3; k++) {
-            st.pos[k] += sol[3 + k];
-            st.vel[k] += sol[6 + k];
-            st.bias_g[k] += sol[9 + k];
-            st.bias_a[k] += sol[12 + k];
-            st.gravity[k] += sol[15 + k];
-        }
+        state_boxplus_d(slot->state, sol);
         const double rn = sqrt((sol[0] * sol[0] + sol[1] * sol[1]) + sol[2] * sol[2]);
         const double tn = sqrt((sol[3] * sol[3] + sol[4] * sol[4]) + sol[5] * sol[5]);
         const bool converged = (rn * 180 / (3.14159265358) < 0.01) && (tn * 100 < 0.015);

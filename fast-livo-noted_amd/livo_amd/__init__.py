@@ -130,6 +130,21 @@ class IvoxInfo(C.Structure):
                 ("max_grid_points", C.c_int64), ("device_bytes", C.c_int64)]
 
 
+class Cam(C.Structure):
+    _fields_ = [("fx", C.c_double), ("fy", C.c_double), ("cx", C.c_double), ("cy", C.c_double),
+                ("d", C.c_double * 5), ("width", C.c_int32), ("height", C.c_int32)]
+
+
+class VioParams(C.Structure):
+    _fields_ = [("cam", Cam), ("R_ci", C.c_double * 9), ("P_ci", C.c_double * 3), ("img_point_cov", C.c_double),
+                ("patch_size", C.c_int32), ("max_iterations", C.c_int32)]
+
+
+class VioStats(C.Structure):
+    _fields_ = [("iterations", C.c_int32 * 3), ("updates", C.c_int32 * 3), ("last_error", C.c_float * 3),
+                ("cov_updated", C.c_int32), ("n_meas", C.c_int64), ("out_of_frame", C.c_int64)]
+
+
 SIGNATURES = {
     "livo_abi_version": (C.c_int, []),
     "livo_error_string": (C.c_char_p, [C.c_int]),
@@ -162,6 +177,9 @@ SIGNATURES = {
     "livo_scan_inherit_neighbors": (C.c_int, [_P, C.c_int32, C.c_int32]),
     "livo_scan_preprocess": (C.c_int, [_P, _P, C.c_int64, _P, C.c_int32, _P, _P, C.c_float, C.POINTER(C.c_int32),
                                        _P, _P, C.c_int64, C.POINTER(C.c_int64)]),
+    "livo_vio_params_default": (C.c_int, [C.POINTER(VioParams)]),
+    "livo_vio_update": (C.c_int, [_P, C.POINTER(VioParams), _P, C.c_int32, C.c_int32, _P, _P, _P, C.c_int64,
+                                  C.POINTER(State), C.POINTER(State), _P, C.POINTER(VioStats)]),
     "livo_sync": (C.c_int, [_P]),
 }
 
@@ -449,6 +467,38 @@ class Context:
             _ptr(und), _ptr(down), n, C.byref(nd)))
         self.scans[sid.value] = int(nd.value)
         return sid.value, und, down[:nd.value].copy()
+
+    # ------------------------------------------------------------ VIO ----
+    def vio_update(self, frame: dict, state: dict, prior: dict | None = None, max_iter: int = 4,
+                   img_point_cov: float = 10.0):
+        """LidarSelector::ComputeJ / UpdateState on a frame dict (livo_amd.synth.make_vio_frame layout):
+        image, cam, pos, levels, patches, patch_size, Rci, Pci.  Returns (state, stats, errors)."""
+        p = VioParams()
+        _check("livo_vio_params_default", self._L.livo_vio_params_default(C.byref(p)))
+        cam = frame["cam"]
+        p.cam.fx, p.cam.fy, p.cam.cx, p.cam.cy = cam["fx"], cam["fy"], cam["cx"], cam["cy"]
+        p.cam.d[:] = list(cam["d"]) + [0.0] * (5 - len(cam["d"]))
+        p.cam.width, p.cam.height = cam["width"], cam["height"]
+        p.R_ci[:] = np.asarray(frame["Rci"], np.float64).reshape(9).tolist()
+        p.P_ci[:] = np.asarray(frame["Pci"], np.float64).reshape(3).tolist()
+        p.img_point_cov = img_point_cov
+        p.patch_size = frame["patch_size"]
+        p.max_iterations = max_iter
+        img = np.ascontiguousarray(frame["image"], np.uint8)
+        pos = np.ascontiguousarray(frame["pos"], np.float64).reshape(-1, 3)
+        lev = np.ascontiguousarray(frame["levels"], np.int32)
+        pat = np.ascontiguousarray(frame["patches"], np.float32)
+        n = pos.shape[0]
+        s = state_to_c(state)
+        pr = state_to_c(prior) if prior is not None else None
+        err = np.zeros(max(n, 1), np.float32)
+        st = VioStats()
+        _check("livo_vio_update", self._L.livo_vio_update(
+            self.h, C.byref(p), _ptr(img), img.shape[1], img.shape[0], _ptr(pos), _ptr(lev), _ptr(pat), n,
+            C.byref(s), C.byref(pr) if pr is not None else None, _ptr(err), C.byref(st)))
+        stats = {"iterations": list(st.iterations), "updates": list(st.updates), "last_error": list(st.last_error),
+                 "cov_updated": st.cov_updated, "n_meas": st.n_meas, "out_of_frame": st.out_of_frame}
+        return state_from_c(s), stats, err[:n]
 
     def scan_inherit_neighbors(self, dst: int, src: int):
         _check("livo_scan_inherit_neighbors", self._L.livo_scan_inherit_neighbors(self.h, dst, src))

@@ -21,6 +21,8 @@
  *                                                   include/ivox3d/ivox3d.h:37-305
  *   livo_map_incremental ← LaserMapping::map_incremental (iVox branch)
  *                                                   src/laser_mapping.cpp:329-389
+ *   livo_vio_update     ← LidarSelector::ComputeJ / UpdateState (VIO photometric update)
+ *                                                   src/lidar_selection.cpp:748-978
  *   livo_scan_preprocess ← ImuProcess::UndistortPcl (per point) + downSizeFilterSurf
  *                                                   src/IMU_Processing.cpp:340-378,
  *                                                   src/laser_mapping.cpp:129-130
@@ -326,6 +328,51 @@ int livo_scan_preprocess(livo_ctx* ctx, const livo_raw_point* raw, int64_t n, co
                          int32_t n_poses, const double rot_end[9], const double pos_end[3], float leaf_size,
                          int32_t* scan_id, livo_raw_point* undistorted, livo_raw_point* down, int64_t down_cap,
                          int64_t* n_down);
+
+/* ------------------------------------------------------------------------
+ * VIO photometric update: LidarSelector::ComputeJ and
+ * UpdateState (src/lidar_selection.cpp:748-978) for the visual points of
+ * sub_sparse_map: per point, patch_size^2 bilinear residuals against its
+ * reference patch at pyramid levels 2, 1, 0, the 6-wide Jacobian rows, and
+ * the 18-dim iterated update (K1 = (HᵀH + (P / img_point_cov)^-1)^-1), then
+ * cov -= G cov.  max_iterations is explicit: the compiled build never
+ * assigns LidarSelector::NUM_MAX_ITERATIONS (the legacy pipeline sets it to
+ * the LiDAR value, origin_laserMapping.cpp:1208).
+ * ------------------------------------------------------------------------ */
+/* vikit PinholeCamera (camera yaml: cam_fx ... cam_d0..d3; d[4] = k3). */
+typedef struct livo_cam {
+    double fx, fy, cx, cy;
+    double d[5];
+    int32_t width, height;
+} livo_cam;
+
+typedef struct livo_vio_params {
+    livo_cam cam;
+    double R_ci[9];          /* Rci = Rcl * Rli (lidar_selection.cpp:44), row-major */
+    double P_ci[3];          /* Pci = Rcl * Pli + Pcl                                */
+    double img_point_cov;    /* img_point_cov (10, laser_mapping.cpp:976)             */
+    int32_t patch_size;      /* patch_size (4, laser_mapping.cpp:1015), <= 8          */
+    int32_t max_iterations;  /* UpdateState iterations per level                      */
+} livo_vio_params;
+
+typedef struct livo_vio_stats {
+    int32_t iterations[3];   /* per level 2, 1, 0 */
+    int32_t updates[3];      /* iterations that updated the state (error did not grow) */
+    float last_error[3];     /* UpdateState's return value per level */
+    int32_t cov_updated;
+    int64_t n_meas;
+    int64_t out_of_frame;    /* patch samples outside the image (clamped; the reference reads out of bounds) */
+} livo_vio_stats;
+
+int livo_vio_params_default(livo_vio_params* p);
+/* image: 8-bit gray, width x height, row stride = width.  pos: n x 3 world
+ * positions; search_levels: n; patches: n x 3 x patch_size^2 reference
+ * patches (levels 0, 1, 2, Feature::patch_).  state in/out, prior =
+ * state_propagat (NULL: the input state).  errors (n, may be NULL) =
+ * sub_sparse_map->errors after the last iteration. */
+int livo_vio_update(livo_ctx* ctx, const livo_vio_params* p, const uint8_t* image, int32_t width, int32_t height,
+                    const double* pos, const int32_t* search_levels, const float* patches, int64_t n,
+                    livo_state* state, const livo_state* prior, float* errors, livo_vio_stats* stats);
 
 int livo_sync(livo_ctx* ctx);
 
