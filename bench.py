@@ -355,6 +355,29 @@ def main():
             "note": "LIVO_BACKEND_IVOX: IVox GetClosestPoint (NEARBY18, 0.2 m grids, 5 m range) on the same "
                     f"{a.batch} scans per GPU, {iv_steps} steps after the IKFoM run; not part of `value`"}
 
+    # ---- the VIO photometric update: frames per second
+    # at the reference's size (a 40-px grid on 640x512: <= 192 visual points)
+    # and at 20k points; not part of `value`
+    vio = {}
+    vio_frames = {}
+    for nv in (192, 20000):
+        fr, vst, _ = synth.make_vio_frame(nv, 100 + rank)
+        vio_frames[nv] = (fr, vst)
+        ctx.vio_update(fr, vst)  # warm-up
+        reps = 20 if nv < 1000 else 10
+        sync()
+        t = time.perf_counter()
+        for _ in range(reps):
+            _, vstats, _ = ctx.vio_update(fr, vst)
+        sync()
+        dt = (time.perf_counter() - t) / reps
+        vio[str(len(fr["pos"]))] = {"frames_per_s": round(1.0 / dt, 2), "ms_per_frame": round(dt * 1e3, 4),
+                                    "iterations_per_level": vstats["iterations"]}
+    if rank == 0:
+        result["vio"] = {"by_points": vio,
+                         "note": "livo_vio_update (LidarSelector::ComputeJ/UpdateState, patch 4x4, 3 levels, "
+                                 "max_iteration 4) on synthetic 640x512 frames, host-timed incl. the frame upload"}
+
     # ---- CPU baseline: the oracle (CPU restatement), 1 thread, bounded sample; + parity of scan 0
     if rank == 0 and a.cpu_seconds > 0:
         import oracle
@@ -413,6 +436,15 @@ def main():
         result["ivox"]["parity_scan0"] = {"iterations_equal": ig["iterations"] == ivst["iterations"],
                                           "effct_equal": ig["effct_feat_num"] == ivst["effct_feat_num"],
                                           "max_rel_state_delta": float(f"{ivrel:.3e}")}
+        # VIO: the oracle on the same frames (1 thread) and parity of the large one
+        for nv, (fr, vst) in vio_frames.items():
+            t = time.perf_counter()
+            vr, vrs, _ = oracle.vio_update(fr, vst)
+            key = str(len(fr["pos"]))
+            result["vio"]["by_points"][key]["cpu_ms_per_frame"] = round((time.perf_counter() - t) * 1e3, 3)
+        vg, vgs, _ = ctx.vio_update(*vio_frames[20000])
+        result["vio"]["parity_20k"] = {"iterations_equal": vgs["iterations"] == vrs["iterations"],
+                                       "max_abs_pos_delta": float(f"{np.abs(vg['pos'] - vr['pos']).max():.3e}")}
         result["ikfom"]["parity_scan0"] = {"iterations_equal": ik_first["iterations"] == irs["iterations"],
                                            "effct_equal": ik_first["effct_feat_num"] == irs["effct_feat_num"],
                                            "max_dx_error_rel_to_largest_step": float(f"{irel:.3e}")}
