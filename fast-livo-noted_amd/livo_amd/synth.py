@@ -408,3 +408,36 @@ def make_vio_frame(n_points: int, frame_id: int = 0, patch_size: int = 4, rot_de
     truth = dict(st)
     truth["rot"], truth["pos"] = R, p
     return frame, st, truth
+
+
+def boundary_points(rng, ds: float, n: int, span: int = 40) -> np.ndarray:
+    """(n, 3) float32 points within a few ulps of ikd-Tree downsample box faces j * ds
+    (ikd_Tree.cpp:392-397), where float rounding makes neighbouring boxes overlap or
+    leave gaps; about half the coordinates are on a face, the rest inside a box."""
+    f32 = np.float32
+    j = rng.integers(-span, span, size=(n, 3)).astype(f32)
+    face = (j * f32(ds)).astype(f32)
+    steps = rng.integers(-3, 4, size=(n, 3))
+    for k in range(3):
+        up = steps > k
+        dn = steps < -k
+        face = np.where(up, np.nextafter(face, f32(np.inf)), face)
+        face = np.where(dn, np.nextafter(face, f32(-np.inf)), face)
+    inner = (j * f32(ds) + rng.uniform(0, ds, size=(n, 3))).astype(f32)
+    return np.where(rng.random((n, 3)) < 0.5, face, inner).astype(f32)
+
+
+def centre_tie_points(ds: float, boxes: int = 8) -> tuple[np.ndarray, np.ndarray]:
+    """Map points in pairs at exactly the same distance from their box centre (different
+    coordinates) and one farther query point per box: Add_Points then keeps a stored point
+    picked by Search_by_range's order (ikd_Tree.cpp:405-411)."""
+    f32 = np.float32
+    pairs, far = [], []
+    for b in range(boxes):
+        lo = (np.floor(np.array([b * 1.7 + 0.2, 0.3 * b, -0.4 * b], f32) / f32(ds)) * f32(ds)).astype(f32)
+        hi = (lo + f32(ds)).astype(f32)
+        mid = (lo.astype(np.float64) + (hi - lo).astype(np.float64) / 2.0).astype(f32)
+        e = f32(ds / 8.0)
+        pairs += [mid + np.array([e, 0, 0], f32), mid - np.array([e, 0, 0], f32)]
+        far.append((lo + f32(ds) * f32(0.01)).astype(f32))
+    return np.array(pairs, f32), np.array(far, f32)

@@ -452,3 +452,92 @@ def vio_update(frame: dict, state: dict, prior: dict | None = None, max_iter: in
                      _p(np.ascontiguousarray(frame["Pci"], np.float64)), img_point_cov, max_iter, C.byref(cs),
                      C.byref(pr), _p(err), C.byref(st))
     return state_from_c(cs), vio_stats_from(st), err
+
+
+def _dyn_lib():
+    L = lib()
+    if not getattr(L, "_dyn", False):
+        P = C.c_void_p
+        L.orc_dyn_create.restype = P
+        L.orc_dyn_create.argtypes = [P, C.c_int64]
+        L.orc_dyn_free.argtypes = [P]
+        L.orc_dyn_add_points.argtypes = [P, P, C.c_int64, C.c_float, C.c_int, P]
+        L.orc_dyn_delete_boxes.restype = C.c_int64
+        L.orc_dyn_delete_boxes.argtypes = [P, P, C.c_int64]
+        L.orc_dyn_dump.restype = C.c_int64
+        L.orc_dyn_dump.argtypes = [P, P, P]
+        L.orc_dyn_knn.argtypes = [P, P, C.c_int64, C.c_int, P, P, C.c_int]
+        L.orc_dyn_iekf_update.argtypes = [P, P, C.c_int64, P, P, C.c_double, C.c_int, C.POINTER(OrcState),
+                                          C.POINTER(OrcState), C.POINTER(OrcIterStats), C.c_int]
+        L.orc_dyn_map_incremental.argtypes = [P, P, C.c_int64, C.POINTER(OrcState), P, P, C.c_double, P]
+        L._dyn = True
+    return L
+
+
+def _add_stats(st) -> dict:
+    return {"events": int(st[0]), "added": int(st[1]), "deleted": int(st[2]), "ambiguous": int(st[3])}
+
+
+class DynMap:
+    """The ikd-Tree map under KD_TREE::Add_Points / Delete_Point_Boxes (ikd_Tree.cpp:382-521) as a
+    point set with ids (initial map = its indices, kept points of a call = the next ids in input order)."""
+
+    def __init__(self, xyz: np.ndarray):
+        xyz = np.ascontiguousarray(xyz, np.float32).reshape(-1, 3)
+        self.h = _dyn_lib().orc_dyn_create(_p(xyz), xyz.shape[0])
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.orc_dyn_free(self.h)
+            self.h = None
+
+    def add_points(self, xyz, downsample_size: float = 0.5, downsample: bool = True) -> dict:
+        xyz = np.ascontiguousarray(xyz, np.float32).reshape(-1, 3)
+        st = np.zeros(4, np.int64)
+        assert _dyn_lib().orc_dyn_add_points(self.h, _p(xyz), xyz.shape[0], C.c_float(downsample_size),
+                                             int(bool(downsample)), _p(st)) == 0
+        return _add_stats(st)
+
+    def delete_boxes(self, boxes) -> int:
+        """boxes (n, 6): vertex_min xyz, vertex_max xyz (BoxPointType)."""
+        b = np.ascontiguousarray(boxes, np.float32).reshape(-1, 6)
+        return int(_dyn_lib().orc_dyn_delete_boxes(self.h, _p(b), b.shape[0]))
+
+    def dump(self):
+        """(xyz (n, 3), ids (n,)) of the alive points in id order."""
+        n = _dyn_lib().orc_dyn_dump(self.h, None, None)
+        xyz = np.zeros((n, 3), np.float32)
+        ids = np.zeros(n, np.int32)
+        _dyn_lib().orc_dyn_dump(self.h, _p(xyz), _p(ids))
+        return xyz, ids
+
+    def knn(self, q, k: int = 5, threads: int = 8):
+        q = np.ascontiguousarray(q, np.float32).reshape(-1, 3)
+        n = q.shape[0]
+        idx = np.empty((n, k), np.int32)
+        d = np.empty((n, k), np.float32)
+        assert _dyn_lib().orc_dyn_knn(self.h, _p(q), n, k, _p(idx), _p(d), threads) == 0
+        return idx, d
+
+    def iekf_update(self, body, state: dict, prior: dict | None = None, R_LI=None, t_LI=None,
+                    max_iter: int = 4, lpc: float = 0.001, threads: int = 8):
+        cs = state_to_c(state)
+        pr = state_to_c(prior if prior is not None else state)
+        st = OrcIterStats()
+        body = np.ascontiguousarray(body, np.float32)
+        R_LI = np.ascontiguousarray(np.eye(3) if R_LI is None else R_LI, np.float64)
+        t_LI = np.ascontiguousarray(np.zeros(3) if t_LI is None else t_LI, np.float64)
+        assert _dyn_lib().orc_dyn_iekf_update(self.h, _p(body), body.shape[0], _p(R_LI), _p(t_LI), lpc, max_iter,
+                                              C.byref(cs), C.byref(pr), C.byref(st), threads) == 0
+        return state_from_c(cs), _stats(st)
+
+    def map_incremental(self, body, state: dict, R_LI=None, t_LI=None, filter_size_map: float = 0.5) -> dict:
+        """map_incremental with USE_ikdtree (laser_mapping.cpp:383-384)."""
+        body = np.ascontiguousarray(body, np.float32)
+        cs = state_to_c(state)
+        R_LI = np.ascontiguousarray(np.eye(3) if R_LI is None else R_LI, np.float64)
+        t_LI = np.ascontiguousarray(np.zeros(3) if t_LI is None else t_LI, np.float64)
+        st = np.zeros(4, np.int64)
+        assert _dyn_lib().orc_dyn_map_incremental(self.h, _p(body), body.shape[0], C.byref(cs), _p(R_LI), _p(t_LI),
+                                                  filter_size_map, _p(st)) == 0
+        return _add_stats(st)
