@@ -30,6 +30,7 @@ SOURCES = [
     ("ivox_kernels.hip", True),
     ("frontend_kernels.hip", True),
     ("vio_kernels.hip", True),
+    ("ikd_incr_kernels.hip", True),
     ("prims.hip", True),
     ("livo_capi.cpp", False),
     ("map_build.cpp", False),
@@ -86,8 +87,6 @@ def build_facade_demo(verbose: bool = False) -> str:
     return FACADE_DEMO
 
 
-if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
 
 
 WAVE_CHECK = os.path.join(LIB_DIR, "wave_nth_check")
@@ -101,3 +100,7 @@ def build_checks(verbose: bool = False) -> str:
         print(" ".join(cmd))
     _run(cmd)
     return WAVE_CHECK
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

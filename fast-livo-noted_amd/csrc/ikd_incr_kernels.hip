@@ -1,0 +1,518 @@
+// ikd_incr_kernels.hip — CDNA4 (gfx950) kernels of the ikd-Tree incremental
+// map (the USE_ikdtree branch of
+// LaserMapping::map_incremental, src/laser_mapping.cpp:383-384).
+//
+//   KD_TREE::Add_Points(points, downsample_on) (include/ikd-Tree/ikd_Tree.cpp:
+//   382-457) with downsample_size = filter_size_map_min (laser_mapping.cpp:138):
+//   per point, in order, the box floor(p / ds) * ds .. + ds and its centre
+//   (:392-400); the box's stored points (Search_by_range, :988-1016, half open
+//   vmin <= p < vmax); the nearest of them replaces the new point only if
+//   strictly nearer the centre (:403-411); if the box held more than one point
+//   or the new point won (same_point, :1287-1289), the box is emptied
+//   (Delete_by_range, :626-688) and the winner added (:413-416).
+//
+//   k_add_prep    box key per point; a point within a rounding step of a box
+//                 face (neighbouring float boxes overlap or leave a gap) marks
+//                 the boxes it touches dirty
+//   (stable radix sort by box key: a box's points in input order)
+//   k_add_group   one thread per box: its stored points from the cell grid,
+//                 then the box's whole sequence of new points.  Boxes are
+//                 independent, except dirty boxes and boxes holding a stored
+//                 point that lies in two boxes: those are deferred
+//   k_add_seq     one thread: the deferred points in input order, with the
+//                 reference's sequential rule
+//   k_add_append  kept points appended with the next ids (input order)
+//   k_dyn_*       the cell grid of k_knn_grid rebuilt from the surviving
+//                 points (keys -> radix sort -> runs -> hash), and
+//                 Delete_Point_Boxes (:501-521)
+//
+// Stored points at exactly the same distance from the centre are taken in id
+// (insertion) order where the reference takes Search_by_range's tree order
+// (its tree shape depends on Rebuild and the background rebuild thread); the
+// boxes where that decides are counted (`ambiguous`).  Numerics as
+// livo_kernels.hip: -ffp-contract=off, the reference's float expressions.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "device_common.h"
+#include "livo_internal.h"
+
+namespace livo {
+
+__device__ __forceinline__ unsigned long long pack_key(int x, int y, int z) {  // = grid_key_d (livo_kernels.hip)
+    return (unsigned long long)(x + kGridBias) | ((unsigned long long)(y + kGridBias) << 21) |
+           ((unsigned long long)(z + kGridBias) << 42);
+}
+__device__ __forceinline__ int key_axis(unsigned long long k, int a) {
+    return (int)((k >> (21 * a)) & 0x1FFFFFull) - kGridBias;
+}
+// One axis of Box_of_Point (:392-397): [j * ds, j * ds + ds) in floats.
+__device__ __forceinline__ bool ax_in(float v, int j, float ds) {
+    const float lo = (float)j * ds, hi = lo + ds;
+    return lo <= v && hi > v;
+}
+struct DBox {
+    float lo[3], hi[3], mid[3];
+};
+__device__ __forceinline__ DBox dbox(unsigned long long k, float ds) {
+    DBox b;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        b.lo[a] = (float)key_axis(k, a) * ds;
+        b.hi[a] = b.lo[a] + ds;
+        b.mid[a] = (float)((double)b.lo[a] + (double)(b.hi[a] - b.lo[a]) / 2.0);  // mid_point (:398-400)
+    }
+    return b;
+}
+__device__ __forceinline__ bool in_dbox(const DBox& b, float x, float y, float z) {
+    return b.lo[0] <= x && b.hi[0] > x && b.lo[1] <= y && b.hi[1] > y && b.lo[2] <= z && b.hi[2] > z;
+}
+__device__ __forceinline__ float mid_dist(const DBox& b, float x, float y, float z) {  // calc_dist (:1291-1295)
+    const float dx = x - b.mid[0], dy = y - b.mid[1], dz = z - b.mid[2];
+    return (dx * dx + dy * dy) + dz * dz;
+}
+__device__ __forceinline__ bool same_pt(float ax, float ay, float az, float bx, float by, float bz) {  // :1287-1289
+    return (double)fabsf(ax - bx) < 1e-6 && (double)fabsf(ay - by) < 1e-6 && (double)fabsf(az - bz) < 1e-6;
+}
+// A point of box k that also lies in a neighbouring box (within a rounding step of a face).
+__device__ __forceinline__ bool in_two(unsigned long long k, float ds, float x, float y, float z) {
+    const float v[3] = {x, y, z};
+    bool m = false;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const int j = key_axis(k, a);
+        m = m || ax_in(v[a], j - 1, ds) || ax_in(v[a], j + 1, ds);
+    }
+    return m;
+}
+// Run {start, count} of grid cell (x, y, z); count 0 if empty.
+__device__ __forceinline__ uint2 cell_run(const GridSlot* __restrict__ slots, int log2, int x, int y, int z) {
+    const unsigned long long key = pack_key(x, y, z);
+    const uint64_t mask = (1ull << log2) - 1ull;
+    uint64_t sl = (uint64_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - log2));
+    GridSlot g = slots[sl];
+    while (g.key != key && g.key != kGridEmpty) {
+        sl = (sl + 1) & mask;
+        g = slots[sl];
+    }
+    return g.key == key ? make_uint2(g.start, g.count) : make_uint2(0u, 0u);
+}
+// Grid cells that can hold a point of the box (with the grid's rounding slack).
+__device__ __forceinline__ bool box_cells(const DynAddParams& P, const DBox& b, int (&l)[3], int (&h)[3]) {
+    const double ih = 1.0 / (double)P.gh;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const double lo = floor(((double)b.lo[a] - (double)P.geps - (double)P.gorg[a]) * ih);
+        const double hi = floor(((double)b.hi[a] + (double)P.geps - (double)P.gorg[a]) * ih);
+        if (!(fabs(lo) < (double)(kGridBias - 8) && fabs(hi) < (double)(kGridBias - 8))) return false;
+        l[a] = (int)lo;
+        h[a] = (int)hi;
+    }
+    return true;
+}
+
+// ------------------------------------------------------------ Add_Points ----
+__global__ void k_add_prep(DynAddParams P) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n) return;
+    const float4 p = reinterpret_cast<const float4*>(P.W)[i];
+    const float v[3] = {p.x, p.y, p.z};
+    const float am = fmaxf(fmaxf(fabsf(p.x), fabsf(p.y)), fabsf(p.z));
+    bool ok = am <= 1e30f;  // false for NaN / inf
+    // the point's cell of the map grid must be addressable (k_knn_grid's key range)
+#pragma unroll
+    for (int a = 0; a < 3; a++) ok = ok && fabsf(floorf((v[a] - P.gorg[a]) * P.ginv)) < (float)(kGridBias - 8);
+    P.iota[i] = (uint32_t)i;
+    P.keep[i] = P.downsample ? 0u : 1u;  // without downsampling every point is added (:438-454)
+    P.defer[i] = 0u;
+    if (ok) atomicMax(P.ctr + kDynAbsMax, (unsigned long long)__float_as_uint(am));
+    P.keys[i] = 0ull;
+    if (!P.downsample) {
+        if (!ok) atomicOr(P.ctr + kDynError, 1ull);
+        return;
+    }
+    int j[3] = {0, 0, 0};
+    bool mem[3][3];
+    bool clean = true;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const float f = floorf(v[a] / P.ds);
+        ok = ok && fabsf(f) < (float)(kGridBias - 8);
+        j[a] = ok ? (int)f : 0;
+#pragma unroll
+        for (int o = 0; o < 3; o++) mem[a][o] = ax_in(v[a], j[a] + o - 1, P.ds);
+        clean = clean && mem[a][1] && !mem[a][0] && !mem[a][2];
+    }
+    if (!ok) {
+        atomicOr(P.ctr + kDynError, 1ull);
+        return;
+    }
+    const unsigned long long k = pack_key(j[0], j[1], j[2]);
+    P.keys[i] = k;
+    if (clean) return;
+    // processed in box k, lying inside the boxes of `mem`: all of them go to the sequential pass
+    auto mark = [&](unsigned long long key) {
+        const unsigned long long s = atomicAdd(P.ctr + kDynDirty, 1ull);
+        if (s < (unsigned long long)P.dirty_cap) P.dirty[s] = key;
+    };
+    mark(k);
+    for (int o0 = 0; o0 < 3; o0++)
+        for (int o1 = 0; o1 < 3; o1++)
+            for (int o2 = 0; o2 < 3; o2++)
+                if (mem[0][o0] && mem[1][o1] && mem[2][o2] && !(o0 == 1 && o1 == 1 && o2 == 1))
+                    mark(pack_key(j[0] + o0 - 1, j[1] + o1 - 1, j[2] + o2 - 1));
+}
+
+__global__ void k_add_heads(DynAddParams P) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= P.n) return;
+    P.heads[k] = (k == 0 || P.skeys[k] != P.skeys[k - 1]) ? 1u : 0u;
+}
+
+__global__ void k_add_starts(DynAddParams P) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= P.n) return;
+    if (P.heads[k]) P.starts[P.runid[k]] = (uint32_t)k;
+    if (k == P.n - 1) {
+        const uint32_t runs = P.runid[k] + P.heads[k];
+        P.starts[runs] = (uint32_t)P.n;
+        P.ctr[kDynRuns] = runs;
+    }
+}
+
+// One box per thread: its stored points, then its new points in input order.
+__global__ __launch_bounds__(256) void k_add_group(DynAddParams P) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= (int64_t)P.ctr[kDynRuns]) return;
+    const uint32_t s0 = P.starts[g], s1 = P.starts[g + 1];
+    const unsigned long long key = P.skeys[s0];
+    const unsigned long long nd = P.ctr[kDynDirty];
+    bool defer = nd > (unsigned long long)P.dirty_cap;
+    for (unsigned long long d = 0; d < nd && d < (unsigned long long)P.dirty_cap && !defer; d++)
+        defer = P.dirty[d] == key;
+    const DBox b = dbox(key, P.ds);
+    int l[3] = {0, 0, 0}, h[3] = {-1, -1, -1};
+    if (!defer && !box_cells(P, b, l, h)) defer = true;
+    const float4* __restrict__ gp = reinterpret_cast<const float4*>(P.gpts);
+    const float4* __restrict__ W = reinterpret_cast<const float4*>(P.W);
+    // pass 1: Search_by_range -- count, the first nearest in id order, ties at that distance
+    int cnt = 0;
+    float bd = INFINITY, bx = 0.f, by = 0.f, bz = 0.f;
+    uint32_t bid = 0xFFFFFFFFu;
+    bool tie = false;
+    for (int z = l[2]; z <= h[2] && !defer; z++)
+        for (int y = l[1]; y <= h[1] && !defer; y++)
+            for (int x = l[0]; x <= h[0] && !defer; x++) {
+                const uint2 r = cell_run(P.gslots, P.glog2, x, y, z);
+                for (uint32_t k = r.x; k < r.x + r.y; k++) {
+                    const float4 q = gp[k];
+                    if (!in_dbox(b, q.x, q.y, q.z)) continue;
+                    if (in_two(key, P.ds, q.x, q.y, q.z)) {
+                        defer = true;
+                        break;
+                    }
+                    cnt++;
+                    const float d = mid_dist(b, q.x, q.y, q.z);
+                    const uint32_t id = __float_as_uint(q.w);
+                    if (d < bd) {
+                        bd = d; bid = id; bx = q.x; by = q.y; bz = q.z;
+                        tie = false;
+                    } else if (d == bd) {
+                        if (q.x != bx || q.y != by || q.z != bz) tie = true;
+                        if (id < bid) { bid = id; bx = q.x; by = q.y; bz = q.z; }
+                    }
+                }
+            }
+    if (defer) {
+        for (uint32_t k = s0; k < s1; k++) P.defer[P.svals[k]] = 1u;
+        return;
+    }
+    // the box's new points in input order (:390-437); after the first, the box holds one point
+    uint32_t win = P.svals[s0];
+    float4 p = W[win];
+    float dc = mid_dist(b, p.x, p.y, p.z);
+    bool newer = !(cnt > 0 && bd < dc);
+    float wx = p.x, wy = p.y, wz = p.z;
+    if (!newer) { dc = bd; wx = bx; wy = by; wz = bz; }
+    unsigned long long events = 0, amb = 0, deleted = 0;
+    if (cnt > 1 && !newer && tie) amb = 1;
+    if (cnt > 1 || newer || same_pt(p.x, p.y, p.z, wx, wy, wz)) events++;
+    for (uint32_t k = s0 + 1; k < s1; k++) {
+        const uint32_t i = P.svals[k];
+        p = W[i];
+        const float d = mid_dist(b, p.x, p.y, p.z);
+        if (d <= dc) {  // the stored point replaces it only if strictly nearer
+            newer = true; win = i; dc = d; wx = p.x; wy = p.y; wz = p.z;
+            events++;
+        } else if (same_pt(p.x, p.y, p.z, wx, wy, wz)) {
+            events++;
+        }
+    }
+    if (newer) P.keep[win] = 1u;
+    if (cnt > 0 && (newer || cnt > 1)) {
+        // pass 2: Delete_by_range of the box; a stored winner is deleted and added again (it stays)
+        for (int z = l[2]; z <= h[2]; z++)
+            for (int y = l[1]; y <= h[1]; y++)
+                for (int x = l[0]; x <= h[0]; x++) {
+                    const uint2 r = cell_run(P.gslots, P.glog2, x, y, z);
+                    for (uint32_t k = r.x; k < r.x + r.y; k++) {
+                        const float4 q = gp[k];
+                        if (!in_dbox(b, q.x, q.y, q.z)) continue;
+                        const uint32_t id = __float_as_uint(q.w);
+                        if (!newer && id == bid) continue;
+                        P.alive[id] = 0;
+                        deleted++;
+                    }
+                }
+    }
+    if (events) atomicAdd(P.ctr + kDynEvents, events);
+    if (deleted) atomicAdd(P.ctr + kDynDeleted, deleted);
+    if (amb) atomicAdd(P.ctr + kDynAmbig, amb);
+}
+
+__global__ void k_add_dlist(DynAddParams P) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n) return;
+    if (P.defer[i]) P.dlist[P.dpos[i]] = (uint32_t)i;
+    if (i == P.n - 1) P.ctr[kDynDeferred] = P.dpos[i] + P.defer[i];
+}
+
+// The deferred points in input order on one thread: exactly Add_Points' loop.
+__global__ void k_add_seq(DynAddParams P) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    const uint32_t D = (uint32_t)P.ctr[kDynDeferred];
+    const float4* __restrict__ gp = reinterpret_cast<const float4*>(P.gpts);
+    const float4* __restrict__ W = reinterpret_cast<const float4*>(P.W);
+    float4* seq = reinterpret_cast<float4*>(P.seq);  // this pass's kept points (x, y, z, input index)
+    uint32_t ns = 0;
+    unsigned long long events = 0, deleted = 0, amb = 0;
+    for (uint32_t t = 0; t < D; t++) {
+        const uint32_t i = P.dlist[t];
+        const float4 p = W[i];
+        const DBox b = dbox(P.keys[i], P.ds);
+        int l[3] = {0, 0, 0}, h[3] = {-1, -1, -1};
+        if (!box_cells(P, b, l, h)) {
+            atomicOr(P.ctr + kDynError, 2ull);
+            continue;
+        }
+        // Search_by_range: alive stored points (ord = id), this pass's kept points (ord = base + index)
+        int cnt = 0;
+        float bd = INFINITY, bx = 0.f, by = 0.f, bz = 0.f;
+        unsigned long long bo = ~0ull;
+        bool tie = false;
+        auto consider = [&](float qx, float qy, float qz, unsigned long long ord) {
+            cnt++;
+            const float d = mid_dist(b, qx, qy, qz);
+            if (d < bd) {
+                bd = d; bo = ord; bx = qx; by = qy; bz = qz;
+                tie = false;
+            } else if (d == bd) {
+                if (qx != bx || qy != by || qz != bz) tie = true;
+                if (ord < bo) { bo = ord; bx = qx; by = qy; bz = qz; }
+            }
+        };
+        for (int z = l[2]; z <= h[2]; z++)
+            for (int y = l[1]; y <= h[1]; y++)
+                for (int x = l[0]; x <= h[0]; x++) {
+                    const uint2 r = cell_run(P.gslots, P.glog2, x, y, z);
+                    for (uint32_t k = r.x; k < r.x + r.y; k++) {
+                        const float4 q = gp[k];
+                        const uint32_t id = __float_as_uint(q.w);
+                        if (P.alive[id] && in_dbox(b, q.x, q.y, q.z)) consider(q.x, q.y, q.z, id);
+                    }
+                }
+        for (uint32_t s = 0; s < ns; s++) {
+            const float4 q = seq[s];
+            const uint32_t qi = __float_as_uint(q.w);
+            if (qi != 0xFFFFFFFFu && in_dbox(b, q.x, q.y, q.z)) consider(q.x, q.y, q.z, (unsigned long long)P.base + qi);
+        }
+        const bool newer = !(cnt > 0 && bd < mid_dist(b, p.x, p.y, p.z));
+        if (cnt > 1 && !newer && tie) amb++;
+        if (!(cnt > 1 || newer || same_pt(p.x, p.y, p.z, bx, by, bz))) continue;
+        events++;
+        for (int z = l[2]; z <= h[2]; z++)
+            for (int y = l[1]; y <= h[1]; y++)
+                for (int x = l[0]; x <= h[0]; x++) {
+                    const uint2 r = cell_run(P.gslots, P.glog2, x, y, z);
+                    for (uint32_t k = r.x; k < r.x + r.y; k++) {
+                        const float4 q = gp[k];
+                        const uint32_t id = __float_as_uint(q.w);
+                        if (!P.alive[id] || !in_dbox(b, q.x, q.y, q.z) || (!newer && id == bo)) continue;
+                        P.alive[id] = 0;
+                        deleted++;
+                    }
+                }
+        for (uint32_t s = 0; s < ns; s++) {
+            const float4 q = seq[s];
+            const uint32_t qi = __float_as_uint(q.w);
+            if (qi == 0xFFFFFFFFu || !in_dbox(b, q.x, q.y, q.z) || (!newer && (unsigned long long)P.base + qi == bo))
+                continue;
+            P.keep[qi] = 0u;
+            seq[s].w = __uint_as_float(0xFFFFFFFFu);
+        }
+        if (newer) {
+            P.keep[i] = 1u;
+            seq[ns++] = make_float4(p.x, p.y, p.z, __uint_as_float(i));
+        }
+    }
+    if (events) atomicAdd(P.ctr + kDynEvents, events);
+    if (deleted) atomicAdd(P.ctr + kDynDeleted, deleted);
+    if (amb) atomicAdd(P.ctr + kDynAmbig, amb);
+}
+
+__global__ void k_add_append(const float4* __restrict__ W, const uint32_t* __restrict__ keep,
+                             const uint32_t* __restrict__ apos, int64_t n, int64_t base, float4* all, uint8_t* alive) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !keep[i]) return;
+    const float4 p = W[i];
+    const uint32_t id = (uint32_t)(base + (int64_t)apos[i]);
+    all[id] = make_float4(p.x, p.y, p.z, __uint_as_float(id));
+    alive[id] = 1;
+}
+
+// ------------------------------------------------------ grid rebuild ------
+__global__ void k_dyn_seed(const float4* __restrict__ gpts, int64_t M, float4* all, uint8_t* alive) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= M) return;
+    const float4 q = gpts[k];
+    const uint32_t id = __float_as_uint(q.w);
+    all[id] = q;
+    alive[id] = 1;
+}
+
+__global__ void k_dyn_world(DynWorldParams P) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= P.n) return;
+    const float4 b = reinterpret_cast<const float4*>(P.pts)[k];
+    float wx, wy, wz;
+    world_point(P.slot->state.rot, P.slot->state.pos, P.R_LI, P.t_LI, b.x, b.y, b.z, wx, wy, wz);
+    reinterpret_cast<float4*>(P.W)[P.perm[k]] = make_float4(wx, wy, wz, 0.f);
+}
+
+// Cell key of every alive point (k_knn_grid's cell_of: floor((p - org) * inv) in float).
+__global__ void k_dyn_cellkeys(const float4* __restrict__ all, const uint8_t* __restrict__ alive, int64_t n_ids,
+                               float ox, float oy, float oz, float inv, unsigned long long* keys, uint32_t* vals,
+                               unsigned long long* ctr) {
+    const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= n_ids) return;
+    vals[id] = (uint32_t)id;
+    if (!alive[id]) {
+        keys[id] = ~0ull;
+        return;
+    }
+    const float4 p = all[id];
+    const float lim = (float)(kGridBias - 8);
+    float c[3] = {floorf((p.x - ox) * inv), floorf((p.y - oy) * inv), floorf((p.z - oz) * inv)};
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        if (!(fabsf(c[a]) < lim)) atomicOr(ctr + kDynError, 4ull);
+        c[a] = fminf(fmaxf(c[a], -lim), lim);
+    }
+    keys[id] = pack_key((int)c[0], (int)c[1], (int)c[2]);
+}
+
+__global__ void k_dyn_gather(const unsigned long long* __restrict__ skeys, const uint32_t* __restrict__ sids,
+                             int64_t na, const float4* __restrict__ all, float4* gpts, uint32_t* heads) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= na + 3) return;
+    if (k >= na) {  // chunk padding of k_knn_grid
+        gpts[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        return;
+    }
+    gpts[k] = all[sids[k]];
+    heads[k] = (k == 0 || skeys[k] != skeys[k - 1]) ? 1u : 0u;
+}
+
+__global__ void k_dyn_runs(const uint32_t* __restrict__ heads, const uint32_t* __restrict__ runid, int64_t na,
+                           uint32_t* starts, unsigned long long* nruns) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= na) return;
+    if (heads[k]) starts[runid[k]] = (uint32_t)k;
+    if (k == na - 1) {
+        const uint32_t r = runid[k] + heads[k];
+        starts[r] = (uint32_t)na;
+        *nruns = r;
+    }
+}
+
+__global__ void k_dyn_slots(const unsigned long long* __restrict__ skeys, const uint32_t* __restrict__ starts,
+                            int64_t cells, GridSlot* slots, int log2) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= cells) return;
+    const uint32_t s0 = starts[g], s1 = starts[g + 1];
+    const unsigned long long key = skeys[s0];
+    const uint64_t mask = (1ull << log2) - 1ull;
+    uint64_t sl = (uint64_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - log2));
+    while (atomicCAS(&slots[sl].key, kGridEmpty, key) != kGridEmpty) sl = (sl + 1) & mask;
+    slots[sl].start = s0;
+    slots[sl].count = s1 - s0;
+}
+
+// Delete_Point_Boxes (:501-521): boxes as BoxPointType {vertex_min[3], vertex_max[3]}, half open.
+__global__ void k_dyn_delete_boxes(const float4* __restrict__ all, uint8_t* alive, int64_t n_ids,
+                                   const float* __restrict__ boxes, int64_t nb, unsigned long long* cnt) {
+    const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= n_ids || !alive[id]) return;
+    const float4 p = all[id];
+    for (int64_t b = 0; b < nb; b++) {
+        const float* B = boxes + 6 * b;
+        if (B[0] <= p.x && B[3] > p.x && B[1] <= p.y && B[4] > p.y && B[2] <= p.z && B[5] > p.z) {
+            alive[id] = 0;
+            atomicAdd(cnt, 1ull);
+            return;
+        }
+    }
+}
+
+// ------------------------------------------------------------ launchers ----
+static inline dim3 grid_for(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }
+
+#define DYN_LAUNCH(kernel, n, ...)                                                              \
+    do {                                                                                        \
+        if ((n) <= 0) return LIVO_OK;                                                           \
+        hipLaunchKernelGGL(kernel, grid_for(n), dim3(256), 0, (hipStream_t)stream, __VA_ARGS__); \
+        return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;                          \
+    } while (0)
+
+int launch_add_prep(const DynAddParams& p, void* stream) { DYN_LAUNCH(k_add_prep, p.n, p); }
+int launch_add_heads(const DynAddParams& p, void* stream) { DYN_LAUNCH(k_add_heads, p.n, p); }
+int launch_add_starts(const DynAddParams& p, void* stream) { DYN_LAUNCH(k_add_starts, p.n, p); }
+int launch_add_group(const DynAddParams& p, void* stream) { DYN_LAUNCH(k_add_group, p.n, p); }
+int launch_add_dlist(const DynAddParams& p, void* stream) { DYN_LAUNCH(k_add_dlist, p.n, p); }
+int launch_add_seq(const DynAddParams& p, void* stream) {
+    hipLaunchKernelGGL(k_add_seq, dim3(1), dim3(64), 0, (hipStream_t)stream, p);
+    return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+int launch_add_append(const float* W, const uint32_t* keep, const uint32_t* apos, int64_t n, int64_t base, float* all,
+                      uint8_t* alive, void* stream) {
+    DYN_LAUNCH(k_add_append, n, reinterpret_cast<const float4*>(W), keep, apos, n, base, reinterpret_cast<float4*>(all),
+               alive);
+}
+int launch_dyn_seed(const float* gpts, int64_t M, float* all, uint8_t* alive, void* stream) {
+    DYN_LAUNCH(k_dyn_seed, M, reinterpret_cast<const float4*>(gpts), M, reinterpret_cast<float4*>(all), alive);
+}
+int launch_dyn_world(const DynWorldParams& p, void* stream) { DYN_LAUNCH(k_dyn_world, p.n, p); }
+int launch_dyn_cellkeys(const float* all, const uint8_t* alive, int64_t n_ids, const float* org, float inv,
+                        unsigned long long* keys, uint32_t* vals, unsigned long long* ctr, void* stream) {
+    DYN_LAUNCH(k_dyn_cellkeys, n_ids, reinterpret_cast<const float4*>(all), alive, n_ids, org[0], org[1], org[2], inv,
+               keys, vals, ctr);
+}
+int launch_dyn_gather(const unsigned long long* skeys, const uint32_t* sids, int64_t na, const float* all, float* gpts,
+                      uint32_t* heads, void* stream) {
+    DYN_LAUNCH(k_dyn_gather, na + 3, skeys, sids, na, reinterpret_cast<const float4*>(all),
+               reinterpret_cast<float4*>(gpts), heads);
+}
+int launch_dyn_runs(const uint32_t* heads, const uint32_t* runid, int64_t na, uint32_t* starts,
+                    unsigned long long* nruns, void* stream) {
+    DYN_LAUNCH(k_dyn_runs, na, heads, runid, na, starts, nruns);
+}
+int launch_dyn_slots(const unsigned long long* skeys, const uint32_t* starts, int64_t cells, GridSlot* slots, int log2,
+                     void* stream) {
+    DYN_LAUNCH(k_dyn_slots, cells, skeys, starts, cells, slots, log2);
+}
+int launch_dyn_delete_boxes(const float* all, uint8_t* alive, int64_t n_ids, const float* boxes, int64_t nb,
+                            unsigned long long* cnt, void* stream) {
+    DYN_LAUNCH(k_dyn_delete_boxes, n_ids, reinterpret_cast<const float4*>(all), alive, n_ids, boxes, nb, cnt);
+}
+
+}  // namespace livo

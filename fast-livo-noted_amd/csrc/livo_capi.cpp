@@ -80,6 +80,27 @@ struct IvoxDev {
     int64_t big_threads = 0, big_slice = 0;
 };
 
+// The ikd-Tree incremental map (ikd_incr_kernels.hip): the point set by id
+// and the scratch of Add_Points / the grid rebuild.
+struct DynDev {
+    bool active = false;
+    float* all = nullptr;        // per id: x, y, z, id bits
+    uint8_t* alive = nullptr;
+    int64_t cap = 0, n_ids = 0, n_alive = 0;
+    float cmax = 0.f;            // largest |coordinate| (the grid's rounding slack)
+    unsigned long long *keys = nullptr, *skeys = nullptr;
+    uint32_t *iota = nullptr, *svals = nullptr, *heads = nullptr, *runid = nullptr, *starts = nullptr;
+    int64_t sort_cap = 0;
+    float *W = nullptr, *seq = nullptr;
+    uint32_t *defer = nullptr, *dpos = nullptr, *dlist = nullptr, *keep = nullptr, *apos = nullptr;
+    int64_t add_cap = 0;
+    float* boxes = nullptr;
+    int64_t box_cap = 0;
+    unsigned long long *dirty = nullptr, *ctr = nullptr;
+    int64_t gslot_cap = 0, gpts_cap = 0;  // capacities of ctx->gslots / ctx->gpts
+    livo_map_add_stats last{};
+};
+
 struct livo_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -104,7 +125,8 @@ struct livo_ctx {
     GridSlot* gslots = nullptr;        // cell grid
     float* gpts = nullptr;
     float gorg[3] = {0.f, 0.f, 0.f};
-    float gh = 1.f, geps = 0.f;
+    float gh = 1.f, geps = 0.f, gcmax = 0.f;
+    DynDev dyn;                        // the incremental map (livo_map_add_points, ...)
     int32_t glog2 = 0;
     int64_t grid_bytes = 0;
     bool has_map = false;
@@ -220,12 +242,15 @@ static KnnParams make_knn_params(livo_ctx* c) {
     kp.glog2 = c->glog2;
     kp.identity = 0;
     kp.iv = ivox_params(c);
+    kp.canon = c->dyn.active ? 1 : 0;
     return kp;
 }
 
 // k-NN pass + exact replay of its flagged queries (one replay list per pass).
 static int knn_pass(const KnnParams& kp, int n_jobs, int64_t max_n, hipStream_t st) {
     HIP_TRY(hipMemsetAsync(kp.replay_count, 0, sizeof(unsigned), st));
+    // the incremental map has no reference-order tree: the grid search + canonical replay
+    if (kp.canon) return launch_knn_grid(kp, n_jobs, max_n, false, st);
     return launch_knn_pass(kp, n_jobs, max_n, st);
 }
 
@@ -533,6 +558,260 @@ static int backend_knn(livo_ctx* c, const KnnParams& kp, int n_jobs, int64_t max
                             : launch_knn_leaf(kp, n_jobs, max_n, later, st);
 }
 
+// ---------------------------------------------- ikd-Tree incremental map --
+extern "C" {
+static ScanBuf* get_scan(livo_ctx* c, int32_t id);
+}
+static void dyn_free(DynDev& d) {
+    dev_free(d.all); dev_free(d.alive);
+    dev_free(d.keys); dev_free(d.skeys); dev_free(d.iota); dev_free(d.svals);
+    dev_free(d.heads); dev_free(d.runid); dev_free(d.starts);
+    dev_free(d.W); dev_free(d.seq);
+    dev_free(d.defer); dev_free(d.dpos); dev_free(d.dlist); dev_free(d.keep); dev_free(d.apos);
+    dev_free(d.boxes); dev_free(d.dirty); dev_free(d.ctr);
+    d = DynDev{};
+}
+
+static int dyn_grow(livo_ctx* c, int64_t need) {  // id capacity
+    DynDev& d = c->dyn;
+    if (need <= d.cap) return LIVO_OK;
+    if (need > kMaxMapPoints) return LIVO_E_RANGE;
+    const int64_t cap = std::min<int64_t>(std::max<int64_t>(need + (need >> 1), 1 << 16), kMaxMapPoints);
+    float* a = nullptr;
+    uint8_t* l = nullptr;
+    if (dev_alloc(&a, (size_t)cap * 4) || dev_alloc(&l, (size_t)cap)) {
+        dev_free(a);
+        dev_free(l);
+        return LIVO_E_OOM;
+    }
+    HIP_TRY(hipMemsetAsync(l, 0, (size_t)cap, c->stream));
+    if (d.n_ids > 0) {
+        HIP_TRY(hipMemcpyAsync(a, d.all, (size_t)d.n_ids * 16, hipMemcpyDeviceToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(l, d.alive, (size_t)d.n_ids, hipMemcpyDeviceToDevice, c->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    dev_free(d.all);
+    dev_free(d.alive);
+    d.all = a;
+    d.alive = l;
+    d.cap = cap;
+    return LIVO_OK;
+}
+
+static int dyn_sort_scratch(livo_ctx* c, int64_t n) {
+    DynDev& d = c->dyn;
+    if (n <= d.sort_cap) return LIVO_OK;
+    const int64_t cap = std::max<int64_t>(n + (n >> 2), 4096);
+    dev_free(d.keys); dev_free(d.skeys); dev_free(d.iota); dev_free(d.svals);
+    dev_free(d.heads); dev_free(d.runid); dev_free(d.starts);
+    d.sort_cap = 0;
+    if (dev_alloc(&d.keys, cap) || dev_alloc(&d.skeys, cap) || dev_alloc(&d.iota, cap) || dev_alloc(&d.svals, cap) ||
+        dev_alloc(&d.heads, cap) || dev_alloc(&d.runid, cap) || dev_alloc(&d.starts, cap + 1))
+        return LIVO_E_OOM;
+    d.sort_cap = cap;
+    return LIVO_OK;
+}
+
+static int dyn_add_scratch(livo_ctx* c, int64_t n) {
+    DynDev& d = c->dyn;
+    if (n <= d.add_cap) return LIVO_OK;
+    const int64_t cap = std::max<int64_t>(n + (n >> 2), 4096);
+    dev_free(d.W); dev_free(d.seq);
+    dev_free(d.defer); dev_free(d.dpos); dev_free(d.dlist); dev_free(d.keep); dev_free(d.apos);
+    d.add_cap = 0;
+    if (dev_alloc(&d.W, (size_t)cap * 4) || dev_alloc(&d.seq, (size_t)cap * 4) || dev_alloc(&d.defer, cap) ||
+        dev_alloc(&d.dpos, cap) || dev_alloc(&d.dlist, cap) || dev_alloc(&d.keep, cap) || dev_alloc(&d.apos, cap))
+        return LIVO_E_OOM;
+    d.add_cap = cap;
+    return LIVO_OK;
+}
+
+static int sort_u64(livo_ctx* c, const unsigned long long* kin, unsigned long long* kout, const uint32_t* vin,
+                    uint32_t* vout, int64_t n) {
+    size_t tb = 0;
+    int rc = prim_sort_pairs_u64(nullptr, &tb, kin, kout, vin, vout, n, 64, c->stream);
+    if (!rc) rc = ensure_prim(c, tb);
+    tb = c->prim_bytes;
+    if (!rc) rc = prim_sort_pairs_u64(c->prim_tmp, &tb, kin, kout, vin, vout, n, 64, c->stream);
+    return rc;
+}
+
+// The built map becomes the incremental point set (ids = build indices).
+static int dyn_activate(livo_ctx* c) {
+    DynDev& d = c->dyn;
+    if (d.active) return LIVO_OK;
+    if (!c->has_map) return LIVO_E_NOMAP;
+    if (c->knn_kind != 1) return LIVO_E_INVALID;  // kept on the cell grid (not LIVO_KNN_KIND=leaf)
+    if (!d.ctr && (dev_alloc(&d.ctr, kDynCtrN) || dev_alloc(&d.dirty, kDynDirtyCap))) return LIVO_E_OOM;
+    const int64_t M = c->map_points;
+    d.n_ids = d.n_alive = 0;
+    int rc = dyn_grow(c, M + 1);
+    if (rc) return rc;
+    if (M == 0) {  // an empty build chose its cell from nothing: use 0.4 m cells at the origin
+        c->gh = 0.4f;
+        c->gorg[0] = c->gorg[1] = c->gorg[2] = 0.f;
+    }
+    rc = launch_dyn_seed(c->gpts, M, d.all, d.alive, c->stream);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    d.n_ids = d.n_alive = M;
+    d.cmax = c->gcmax;
+    d.gslot_cap = (int64_t)1 << c->glog2;
+    d.gpts_cap = M + 3;
+    d.active = true;
+    return LIVO_OK;
+}
+
+// The cell grid of k_knn_grid rebuilt from the alive points (same layout as
+// build_grid_map: cells in key order, a cell's points in id order).
+static int dyn_rebuild(livo_ctx* c) {
+    DynDev& d = c->dyn;
+    int rc = dyn_sort_scratch(c, std::max<int64_t>(d.n_ids, 1));
+    if (rc) return rc;
+    const int64_t na = d.n_alive;
+    if (d.gpts_cap < na + 3) {
+        const int64_t cap = (na + 3) + ((na + 3) >> 2);
+        dev_free(c->gpts);
+        if (dev_alloc(&c->gpts, (size_t)cap * 4)) return LIVO_E_OOM;
+        d.gpts_cap = cap;
+    }
+    HIP_TRY(hipMemsetAsync(d.ctr, 0, kDynCtrN * sizeof(unsigned long long), c->stream));
+    if (d.n_ids > 0) {
+        rc = launch_dyn_cellkeys(d.all, d.alive, d.n_ids, c->gorg, 1.0f / c->gh, d.keys, d.iota, d.ctr, c->stream);
+        if (!rc) rc = sort_u64(c, d.keys, d.skeys, d.iota, d.svals, d.n_ids);
+    }
+    if (!rc) rc = launch_dyn_gather(d.skeys, d.svals, na, d.all, c->gpts, d.heads, c->stream);
+    if (!rc && na > 0) rc = ivox_scan(c, d.heads, d.runid, na);
+    if (!rc && na > 0) rc = launch_dyn_runs(d.heads, d.runid, na, d.starts, d.ctr + kDynRuns, c->stream);
+    if (rc) return rc;
+    unsigned long long h[kDynCtrN];
+    HIP_TRY(hipMemcpyAsync(h, d.ctr, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (h[kDynError]) return LIVO_E_RANGE;
+    const int64_t cells = (int64_t)h[kDynRuns];
+    int log2 = 4;
+    while (((int64_t)1 << log2) < 4 * cells) log2++;  // load factor <= 1/4, as build_grid_map
+    const int64_t table = (int64_t)1 << log2;
+    if (d.gslot_cap < table) {
+        dev_free(c->gslots);
+        if (dev_alloc(&c->gslots, (size_t)table)) return LIVO_E_OOM;
+        d.gslot_cap = table;
+    }
+    rc = launch_ivox_clear(c->gslots, table, c->stream);
+    if (!rc) rc = launch_dyn_slots(d.skeys, d.starts, cells, c->gslots, log2, c->stream);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->glog2 = log2;
+    c->map_points = na;
+    c->geps = (float)(32.0 * std::ldexp(1.0, -24) * (double)d.cmax + 1e-7);
+    c->grid_bytes = table * (int64_t)sizeof(GridSlot) + d.gpts_cap * 16;
+    for (auto& s : c->scans) s.searched = false;  // cached neighbours refer to the old map
+    return LIVO_OK;
+}
+
+// Add_Points of the n points in d.W (filled by the caller).
+static int dyn_add(livo_ctx* c, int64_t n, float ds, bool downsample, livo_map_add_stats* out) {
+    DynDev& d = c->dyn;
+    livo_map_add_stats st{};
+    if (n > 0) {
+        if (d.n_ids + n > kMaxMapPoints || n > (int64_t)0x7FFFFFFF) return LIVO_E_RANGE;
+        int rc = dyn_grow(c, d.n_ids + n);
+        if (!rc) rc = dyn_sort_scratch(c, n + 1);
+        if (rc) return rc;
+        HIP_TRY(hipMemsetAsync(d.ctr, 0, kDynCtrN * sizeof(unsigned long long), c->stream));
+        DynAddParams P{};
+        P.W = d.W; P.n = n; P.ds = ds; P.downsample = downsample ? 1 : 0;
+        P.gslots = c->gslots; P.gpts = c->gpts; P.glog2 = c->glog2;
+        std::memcpy(P.gorg, c->gorg, sizeof(P.gorg));
+        P.gh = c->gh; P.ginv = 1.0f / c->gh; P.geps = c->geps;
+        P.base = d.n_ids; P.alive = d.alive;
+        P.keys = d.keys; P.iota = d.iota; P.skeys = d.skeys; P.svals = d.svals;
+        P.heads = d.heads; P.runid = d.runid; P.starts = d.starts;
+        P.defer = d.defer; P.dpos = d.dpos; P.dlist = d.dlist; P.keep = d.keep; P.seq = d.seq;
+        P.dirty = d.dirty; P.dirty_cap = kDynDirtyCap; P.ctr = d.ctr;
+        rc = launch_add_prep(P, c->stream);
+        if (rc) return rc;
+        unsigned long long h[kDynCtrN];
+        HIP_TRY(hipMemcpyAsync(h, d.ctr, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (h[kDynError]) return LIVO_E_RANGE;  // nothing changed
+        if (downsample) {
+            rc = sort_u64(c, d.keys, d.skeys, d.iota, d.svals, n);
+            if (!rc) rc = launch_add_heads(P, c->stream);
+            if (!rc) rc = ivox_scan(c, d.heads, d.runid, n);
+            if (!rc) rc = launch_add_starts(P, c->stream);
+            if (!rc) rc = launch_add_group(P, c->stream);
+            if (!rc) rc = ivox_scan(c, d.defer, d.dpos, n);
+            if (!rc) rc = launch_add_dlist(P, c->stream);
+            if (!rc) rc = launch_add_seq(P, c->stream);
+        }
+        if (!rc) rc = ivox_scan(c, d.keep, d.apos, n);
+        if (rc) return rc;
+        uint32_t tail[2];
+        HIP_TRY(hipMemcpyAsync(&tail[0], d.apos + n - 1, 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(&tail[1], d.keep + n - 1, 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(h, d.ctr, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (h[kDynError]) return LIVO_E_RANGE;
+        const int64_t added = (int64_t)tail[0] + tail[1];
+        rc = launch_add_append(d.W, d.keep, d.apos, n, d.n_ids, d.all, d.alive, c->stream);
+        if (rc) return rc;
+        st.events = (int64_t)h[kDynEvents];
+        st.deleted = (int64_t)h[kDynDeleted];
+        st.ambiguous = (int64_t)h[kDynAmbig];
+        st.deferred = downsample ? (int64_t)h[kDynDeferred] : 0;
+        st.added = added;
+        d.n_ids += added;
+        d.n_alive += added - st.deleted;
+        const uint32_t am = (uint32_t)h[kDynAbsMax];
+        float amf;
+        std::memcpy(&amf, &am, 4);
+        d.cmax = std::max(d.cmax, amf);
+        rc = dyn_rebuild(c);
+        if (rc) return rc;
+    }
+    st.map_points = d.n_alive;
+    d.last = st;
+    if (out) *out = st;
+    return LIVO_OK;
+}
+
+// map_incremental with USE_ikdtree (laser_mapping.cpp:343-345, 383-384): every
+// point to the world frame at the state, then Add_Points(feats_down_world, true)
+// with downsample_size = filter_size_map_min (set_downsample_param, :138).
+static int map_incremental_ikd(livo_ctx* c, int32_t id, const livo_state* state, double fs, uint8_t* cat,
+                               int64_t counts[2]) {
+    if (!c->has_map) return LIVO_E_NOMAP;
+    ScanBuf* s = get_scan(c, id);
+    if (!s) return LIVO_E_NOSCAN;
+    if (set_device(c)) return LIVO_E_HIP;
+    const int64_t N = s->n;
+    if (counts) counts[0] = counts[1] = 0;
+    int rc = dyn_activate(c);
+    if (!rc) rc = dyn_add_scratch(c, std::max<int64_t>(N, 1));
+    if (!rc) rc = ensure_slots(c, 1);
+    if (rc) return rc;
+    if (N > 0) {
+        init_slot(c->h_slots[0], *state, *state, c->params.max_iterations);
+        HIP_TRY(hipMemcpyAsync(c->d_slots, c->h_slots, sizeof(IekfSlot), hipMemcpyHostToDevice, c->stream));
+        DynWorldParams wp{};
+        wp.pts = s->pts; wp.perm = s->d_perm; wp.n = N; wp.slot = c->d_slots; wp.W = c->dyn.W;
+        std::memcpy(wp.R_LI, c->params.R_LI, sizeof(wp.R_LI));
+        std::memcpy(wp.t_LI, c->params.t_LI, sizeof(wp.t_LI));
+        rc = launch_dyn_world(wp, c->stream);
+        if (rc) return rc;
+    }
+    livo_map_add_stats st{};
+    rc = dyn_add(c, N, (float)fs, true, &st);
+    if (rc) return rc;
+    if (cat && N > 0) std::memset(cat, 1, (size_t)N);  // every point is handed to Add_Points
+    if (counts) {
+        counts[0] = st.events;
+        counts[1] = st.deleted;
+    }
+    return LIVO_OK;
+}
+
 extern "C" {
 
 int livo_abi_version(void) { return LIVO_ABI_VERSION; }
@@ -609,6 +888,7 @@ int livo_ctx_destroy(livo_ctx* c) {
         dev_free(s.d_perm); dev_free(s.d_iperm);
     }
     ivox_free(c->iv);
+    dyn_free(c->dyn);
     if (c->fe_buf) (void)hipFree(c->fe_buf);
     if (c->prim_tmp) (void)hipFree(c->prim_tmp);
     if (c->vio_buf) (void)hipFree(c->vio_buf);
@@ -691,6 +971,9 @@ int livo_map_build(livo_ctx* c, const float* xyz, int64_t M, int64_t stride_byte
     c->gpts = nullptr;
     c->leaf_bytes = c->grid_bytes = 0;
     c->has_map = false;
+    c->dyn.active = false;  // a new static map (the incremental buffers are kept for reuse)
+    c->dyn.n_ids = c->dyn.n_alive = 0;
+    c->dyn.last = livo_map_add_stats{};
     const size_t bytes = (size_t)(hm.num_slots + 1) * sizeof(MapNode);
     const size_t ppb = (size_t)(M + 3) * 4 * sizeof(float);  // chunk padding
     hipError_t e = hipSuccess;
@@ -706,6 +989,7 @@ int livo_map_build(livo_ctx* c, const float* xyz, int64_t M, int64_t stride_byte
         c->glog2 = gm.log2_slots;
         // slack for float rounding in the cell assignment (host) and cell bounds (device)
         c->geps = (float)(32.0 * std::ldexp(1.0, -24) * (double)gm.cmax + 1e-7);
+        c->gcmax = gm.cmax;
     } else {
         const size_t lnb = (size_t)std::max<int64_t>(((int64_t)1 << lm.depth) - 1, 1) * sizeof(LeafNode);
         oom = oom || hipMalloc((void**)&c->lnodes, lnb) != hipSuccess || hipMalloc((void**)&c->lpts, ppb) != hipSuccess;
@@ -735,7 +1019,8 @@ int livo_map_get_info(livo_ctx* c, livo_map_info* out) {
     out->depth = c->map_depth;
     out->reserved = 0;
     out->num_slots = c->map_slots;
-    out->device_bytes = (c->map_slots + 1) * (int64_t)sizeof(MapNode) + c->leaf_bytes + c->grid_bytes;
+    out->device_bytes = (c->map_slots + 1) * (int64_t)sizeof(MapNode) + c->leaf_bytes + c->grid_bytes +
+                        c->dyn.cap * 17;
     return LIVO_OK;
 }
 
@@ -1371,7 +1656,7 @@ int livo_ivox_dump(livo_ctx* c, float* xyz, int32_t* ids, int32_t* keys, int64_t
 int livo_map_incremental(livo_ctx* c, int32_t id, const livo_state* state, double fs, int ekf_inited, uint8_t* cat,
                          int64_t counts[2]) {
     if (!c || !state || !(fs > 0.0)) return LIVO_E_INVALID;
-    if (c->backend != LIVO_BACKEND_IVOX) return LIVO_E_INVALID;  // ikd-Tree Add_Points: not on the device
+    if (c->backend != LIVO_BACKEND_IVOX) return map_incremental_ikd(c, id, state, fs, cat, counts);
     if (!c->iv.ready) return LIVO_E_NOMAP;
     ScanBuf* s = get_scan(c, id);
     if (!s) return LIVO_E_NOSCAN;
@@ -1720,6 +2005,107 @@ int livo_vio_update(livo_ctx* c, const livo_vio_params* p, const uint8_t* image,
         stats->n_meas = hs.ctrl.n_meas;
         stats->out_of_frame = (int64_t)hs.ctrl.oof;
     }
+    return LIVO_OK;
+}
+
+int livo_map_add_points(livo_ctx* c, const float* xyz, int64_t n, int64_t stride_bytes, float ds, int downsample_on,
+                        livo_map_add_stats* stats) {
+    if (!c || n < 0 || (n > 0 && !xyz)) return LIVO_E_INVALID;
+    if (downsample_on && !(ds > 0.f && std::isfinite(ds))) return LIVO_E_INVALID;
+    if (stride_bytes == 0) stride_bytes = 3 * sizeof(float);
+    if (stride_bytes < (int64_t)(3 * sizeof(float))) return LIVO_E_INVALID;
+    if (!c->has_map) return LIVO_E_NOMAP;
+    if (set_device(c)) return LIVO_E_HIP;
+    int rc = dyn_activate(c);
+    if (!rc) rc = dyn_add_scratch(c, std::max<int64_t>(n, 1));
+    if (rc) return rc;
+    if (n > 0) {
+        std::vector<float> h((size_t)n * 4);
+        const char* base = (const char*)xyz;
+        for (int64_t i = 0; i < n; i++) {
+            const float* p = (const float*)(base + i * stride_bytes);
+            h[4 * i] = p[0]; h[4 * i + 1] = p[1]; h[4 * i + 2] = p[2]; h[4 * i + 3] = 0.f;
+        }
+        HIP_TRY(hipMemcpy(c->dyn.W, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice));
+    }
+    return dyn_add(c, n, ds, downsample_on != 0, stats);
+}
+
+int livo_map_delete_boxes(livo_ctx* c, const float* boxes, int64_t nb, int64_t* deleted) {
+    if (!c || nb < 0 || (nb > 0 && !boxes)) return LIVO_E_INVALID;
+    if (!c->has_map) return LIVO_E_NOMAP;
+    if (set_device(c)) return LIVO_E_HIP;
+    if (deleted) *deleted = 0;
+    int rc = dyn_activate(c);
+    if (rc || nb == 0) return rc;
+    DynDev& d = c->dyn;
+    if (nb > d.box_cap) {
+        dev_free(d.boxes);
+        d.box_cap = 0;
+        if (dev_alloc(&d.boxes, (size_t)nb * 6)) return LIVO_E_OOM;
+        d.box_cap = nb;
+    }
+    HIP_TRY(hipMemcpyAsync(d.boxes, boxes, (size_t)nb * 6 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemsetAsync(d.ctr, 0, kDynCtrN * sizeof(unsigned long long), c->stream));
+    rc = launch_dyn_delete_boxes(d.all, d.alive, d.n_ids, d.boxes, nb, d.ctr + kDynDeleted, c->stream);
+    if (rc) return rc;
+    unsigned long long cnt = 0;
+    HIP_TRY(hipMemcpyAsync(&cnt, d.ctr + kDynDeleted, 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    d.n_alive -= (int64_t)cnt;
+    rc = dyn_rebuild(c);
+    if (rc) return rc;
+    if (deleted) *deleted = (int64_t)cnt;
+    return LIVO_OK;
+}
+
+int livo_map_dump(livo_ctx* c, float* xyz, int32_t* ids, int64_t cap, int64_t* n) {
+    if (!c || !n || cap < 0) return LIVO_E_INVALID;
+    if (!c->has_map) return LIVO_E_NOMAP;
+    if (set_device(c)) return LIVO_E_HIP;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    std::vector<float> p;
+    std::vector<int32_t> id;
+    if (c->dyn.active) {
+        const DynDev& d = c->dyn;
+        std::vector<float> all((size_t)d.n_ids * 4);
+        std::vector<uint8_t> alive((size_t)d.n_ids);
+        if (d.n_ids > 0) {
+            HIP_TRY(hipMemcpy(all.data(), d.all, all.size() * sizeof(float), hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpy(alive.data(), d.alive, alive.size(), hipMemcpyDeviceToHost));
+        }
+        for (int64_t k = 0; k < d.n_ids; k++)
+            if (alive[(size_t)k]) {
+                p.insert(p.end(), &all[(size_t)k * 4], &all[(size_t)k * 4] + 3);
+                id.push_back((int32_t)k);
+            }
+    } else {  // the static map: its search structure's points (x, y, z, index) by index
+        const int64_t M = c->map_points;
+        const float* src = c->knn_kind == 1 ? c->gpts : c->lpts;
+        std::vector<float> pts((size_t)M * 4);
+        if (M > 0) HIP_TRY(hipMemcpy(pts.data(), src, pts.size() * sizeof(float), hipMemcpyDeviceToHost));
+        p.resize((size_t)M * 3);
+        id.resize((size_t)M);
+        for (int64_t k = 0; k < M; k++) {
+            uint32_t ix;
+            std::memcpy(&ix, &pts[(size_t)k * 4 + 3], 4);
+            ix &= kIdxMask;
+            if ((int64_t)ix >= M) return LIVO_E_HIP;
+            std::memcpy(&p[(size_t)ix * 3], &pts[(size_t)k * 4], 12);
+            id[ix] = (int32_t)ix;
+        }
+    }
+    *n = (int64_t)id.size();
+    if (!xyz && !ids) return LIVO_OK;
+    if (cap < *n) return LIVO_E_RANGE;
+    if (xyz && !p.empty()) std::memcpy(xyz, p.data(), p.size() * sizeof(float));
+    if (ids && !id.empty()) std::memcpy(ids, id.data(), id.size() * sizeof(int32_t));
+    return LIVO_OK;
+}
+
+int livo_map_last_add_stats(livo_ctx* c, livo_map_add_stats* out) {
+    if (!c || !out) return LIVO_E_INVALID;
+    *out = c->dyn.last;
     return LIVO_OK;
 }
 

@@ -272,6 +272,7 @@ struct KnnParams {
     float geps;             // cell-bound slack for float rounding of the cell assignment
     int32_t glog2;          // log2 of the hash table size
     IvoxParams iv;          // iVox backend (LIVO_BACKEND_IVOX)
+    int32_t canon;          // incremental map: flagged queries -> k_knn_canon instead of the ikd-Tree replay
 };
 
 struct SolveParams {
@@ -431,6 +432,70 @@ struct VioParams {
 int launch_vio_begin(const VioParams& p, int level, void* stream);
 int launch_vio_iter(const VioParams& p, void* stream);
 int launch_vio_end(const VioParams& p, void* stream);
+
+// ikd-Tree incremental map (ikd_incr_kernels.hip):
+// KD_TREE::Add_Points / Delete_Point_Boxes on the map's point set, then the
+// cell grid rebuilt from the surviving points.  Counters in DynAddParams::ctr:
+enum { kDynEvents = 0, kDynDeleted = 1, kDynAmbig = 2, kDynDeferred = 3, kDynError = 4, kDynDirty = 5,
+       kDynAbsMax = 6, kDynRuns = 7, kDynCtrN = 8 };
+constexpr uint32_t kDynDirtyCap = 4096;  // dirty boxes listed; beyond, every point takes the sequential pass
+struct DynAddParams {
+    const float* W;             // n points to add (x, y, z, -), PointToAdd order
+    int64_t n;
+    float ds;                   // downsample_size
+    int32_t downsample;
+    const GridSlot* gslots;     // the map's cell grid before this call
+    const float* gpts;
+    int32_t glog2;
+    float gorg[3];
+    float gh, ginv, geps;
+    int64_t base;               // ids issued before this call
+    uint8_t* alive;             // per id
+    unsigned long long* keys;   // n: box key per point
+    uint32_t* iota;
+    const unsigned long long* skeys;  // sorted by box key (stable)
+    const uint32_t* svals;
+    uint32_t* heads;            // n
+    uint32_t* runid;            // n: exclusive scan of heads
+    uint32_t* starts;           // runs + 1
+    uint32_t* defer;            // n, by point: processed by the sequential pass
+    uint32_t* dpos;             // exclusive scan of defer
+    uint32_t* dlist;            // deferred points, input order
+    uint32_t* keep;             // n, by point: left in the map by this call
+    float* seq;                 // sequential pass: its kept points (4 floats each)
+    unsigned long long* dirty;  // dirty box keys
+    uint32_t dirty_cap;
+    unsigned long long* ctr;    // kDynCtrN counters
+};
+struct DynWorldParams {
+    const float* pts;           // scan body points (stored order, 4 floats each)
+    const int32_t* perm;        // stored position -> caller index
+    int64_t n;
+    const IekfSlot* slot;       // its state
+    double R_LI[9];
+    double t_LI[3];
+    float* W;                   // n world points in caller order (feats_down_world)
+};
+int launch_add_prep(const DynAddParams& p, void* stream);
+int launch_add_heads(const DynAddParams& p, void* stream);
+int launch_add_starts(const DynAddParams& p, void* stream);
+int launch_add_group(const DynAddParams& p, void* stream);
+int launch_add_dlist(const DynAddParams& p, void* stream);
+int launch_add_seq(const DynAddParams& p, void* stream);
+int launch_add_append(const float* W, const uint32_t* keep, const uint32_t* apos, int64_t n, int64_t base, float* all,
+                      uint8_t* alive, void* stream);
+int launch_dyn_seed(const float* gpts, int64_t M, float* all, uint8_t* alive, void* stream);
+int launch_dyn_world(const DynWorldParams& p, void* stream);
+int launch_dyn_cellkeys(const float* all, const uint8_t* alive, int64_t n_ids, const float* org, float inv,
+                        unsigned long long* keys, uint32_t* vals, unsigned long long* ctr, void* stream);
+int launch_dyn_gather(const unsigned long long* skeys, const uint32_t* sids, int64_t na, const float* all, float* gpts,
+                      uint32_t* heads, void* stream);
+int launch_dyn_runs(const uint32_t* heads, const uint32_t* runid, int64_t na, uint32_t* starts,
+                    unsigned long long* nruns, void* stream);
+int launch_dyn_slots(const unsigned long long* skeys, const uint32_t* starts, int64_t cells, GridSlot* slots, int log2,
+                     void* stream);
+int launch_dyn_delete_boxes(const float* all, uint8_t* alive, int64_t n_ids, const float* boxes, int64_t nb,
+                            unsigned long long* cnt, void* stream);
 
 // Nearest_Points carried over by point index (laser_mapping.cpp:165 resize keeps entries).
 int launch_inherit_nn(NNRec* dst, const int32_t* dst_perm, int64_t n_dst, const NNRec* src,

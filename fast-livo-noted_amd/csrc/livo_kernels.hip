@@ -1123,6 +1123,116 @@ __global__ __launch_bounds__(64) void k_knn_replay(KnnParams P) {
     }
 }
 
+// Canonical recomputation on the incremental map (livo_map_add_points, the
+// ikd-Tree map_incremental, livo_map_delete_boxes).  After those the map is a
+// point set whose ikd-Tree shape (Add_by_point, Rebuild and the background
+// rebuild thread, ikd_Tree.cpp:158-300, 604-624) has no deterministic
+// restatement, so the queries k_knn_grid flags (C1/C2) take the 5 nearest
+// alive points in (distance, x, id) order -- PointType_CMP's order
+// (ikd_Tree.h:50-61) wherever that is a strict order.  One query per thread:
+// every cell within the grid's 5th distance, or every point if that bound is
+// infinite or spans too many cells.
+constexpr int kCanonMaxCells = 1 << 15;
+__device__ __forceinline__ bool canon_less(float d1, float x1, uint32_t i1, float d2, float x2, uint32_t i2) {
+    return d1 < d2 || (d1 == d2 && (x1 < x2 || (x1 == x2 && i1 < i2)));
+}
+__global__ __launch_bounds__(64) void k_knn_canon(KnnParams P) {
+    const unsigned n = *P.replay_count;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && n) atomicAdd(P.replay_total, (unsigned long long)n);
+    const float4* __restrict__ gpts = reinterpret_cast<const float4*>(P.gpts);
+    const uint64_t mask = (1ull << P.glog2) - 1ull;
+    for (unsigned t = blockIdx.x * 64 + threadIdx.x; t < n; t += gridDim.x * 64) {
+        const unsigned long long e = P.replay_list[t];
+        const HsJob job = P.jobs[(unsigned)(e >> 32)];
+        const int i = (int)(unsigned)(e & 0xffffffffu);
+        float qx, qy, qz;
+        query_point(P, job.slot, reinterpret_cast<const float4*>(job.pts)[i], qx, qy, qz);
+        NNRec* rec = job.nn + i;
+        const float T = rec->cnt == kNN ? rec->p[kNN - 1][3] : INFINITY;
+        const int flag = rec->flag | 0x100;
+        float bd[kNN], bx[kNN];
+        uint32_t bi[kNN], bs[kNN];
+#pragma unroll
+        for (int k = 0; k < kNN; k++) { bd[k] = INFINITY; bx[k] = 0.f; bi[k] = 0xFFFFFFFFu; bs[k] = 0u; }
+        auto offer = [&](uint32_t s) {
+            const float4 v = gpts[s];
+            const float dx = qx - v.x, dy = qy - v.y, dz = qz - v.z;
+            const float d = (dx * dx + dy * dy) + dz * dz;  // calc_dist (:1291-1295)
+            const uint32_t id = __float_as_uint(v.w);
+            if (!canon_less(d, v.x, id, bd[kNN - 1], bx[kNN - 1], bi[kNN - 1])) return;
+            bd[kNN - 1] = d; bx[kNN - 1] = v.x; bi[kNN - 1] = id; bs[kNN - 1] = s;
+#pragma unroll
+            for (int k = kNN - 1; k > 0; k--) {
+                const bool sw = canon_less(bd[k], bx[k], bi[k], bd[k - 1], bx[k - 1], bi[k - 1]);
+                const float td = bd[k], tx = bx[k];
+                const uint32_t ti = bi[k], ts = bs[k];
+                bd[k] = sw ? bd[k - 1] : td; bx[k] = sw ? bx[k - 1] : tx;
+                bi[k] = sw ? bi[k - 1] : ti; bs[k] = sw ? bs[k - 1] : ts;
+                bd[k - 1] = sw ? td : bd[k - 1]; bx[k - 1] = sw ? tx : bx[k - 1];
+                bi[k - 1] = sw ? ti : bi[k - 1]; bs[k - 1] = sw ? ts : bs[k - 1];
+            }
+        };
+        bool scanned = false;
+        if (T < INFINITY && P.lM > 0) {
+            const double rad = sqrt((double)T + 1e-9) * (1.0 + 1e-5) + (double)P.geps;
+            const double ih = 1.0 / (double)P.gh, lim = (double)(kGridBias - 8);
+            const double q3[3] = {qx, qy, qz};
+            int l[3], h[3];
+            bool ok = true;
+            double span = 1.0;
+#pragma unroll
+            for (int a = 0; a < 3; a++) {
+                const double lo = floor((q3[a] - rad - (double)P.gorg[a]) * ih);
+                const double hi = floor((q3[a] + rad - (double)P.gorg[a]) * ih);
+                ok = ok && fabs(lo) < lim && fabs(hi) < lim;
+                l[a] = ok ? (int)lo : 0;
+                h[a] = ok ? (int)hi : -1;
+                span *= hi - lo + 1.0;
+            }
+            if (ok && span <= (double)kCanonMaxCells) {
+                const float eps = P.geps, w = P.gh + 2 * eps;
+                for (int cz = l[2]; cz <= h[2]; cz++)
+                    for (int cy = l[1]; cy <= h[1]; cy++)
+                        for (int cx = l[0]; cx <= h[0]; cx++) {
+                            const float x0 = P.gorg[0] + (float)cx * P.gh - eps, y0 = P.gorg[1] + (float)cy * P.gh - eps;
+                            const float z0 = P.gorg[2] + (float)cz * P.gh - eps;
+                            if (box_dist(qx, qy, qz, x0, x0 + w, y0, y0 + w, z0, z0 + w) - T > kFuzz) continue;
+                            const unsigned long long key = grid_key_d(cx, cy, cz);
+                            uint64_t sl = (uint64_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - P.glog2));
+                            GridSlot gs = P.gslots[sl];
+                            while (gs.key != key && gs.key != kGridEmpty) {
+                                sl = (sl + 1) & mask;
+                                gs = P.gslots[sl];
+                            }
+                            if (gs.key != key) continue;
+                            for (uint32_t s = gs.start; s < gs.start + gs.count; s++) offer(s);
+                        }
+                scanned = true;
+            }
+        }
+        if (!scanned)
+            for (int64_t s = 0; s < P.lM; s++) offer((uint32_t)s);
+        const int cnt = (int)min<int64_t>(P.lM, (int64_t)kNN);
+        float4* o4 = reinterpret_cast<float4*>(rec);
+        int32_t idx[kNN];
+#pragma unroll
+        for (int k = 0; k < kNN; k++) {
+            float4 v = make_float4(0.f, 0.f, 0.f, INFINITY);
+            idx[k] = -1;
+            if (k < cnt) {
+                const float4 a = gpts[bs[k]];
+                v = make_float4(a.x, a.y, a.z, bd[k]);
+                idx[k] = (int32_t)bi[k];
+            }
+            o4[k] = v;
+        }
+        int4* oi = reinterpret_cast<int4*>(rec) + 5;
+        oi[0] = make_int4(idx[0], idx[1], idx[2], idx[3]);
+        oi[1] = make_int4(idx[4], cnt, flag, (int)bs[0]);
+        oi[2] = make_int4((int)bs[1], (int)bs[2], (int)bs[3], (int)bs[4]);
+    }
+}
+
 // ======================================================== esti_plane ======
 // Eigen 3.3 ColPivHouseholderQR<Matrix<float,5,3>> + solve(-1), restated with
 // the SSE2 reduction orders documented in oracle/livo_oracle.cpp.  Columns of
@@ -2091,7 +2201,10 @@ int launch_knn_grid(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, 
     else
         hipLaunchKernelGGL((k_knn_grid<false>), grid, block, 0, (hipStream_t)stream, q);
     if (hipGetLastError() != hipSuccess) return LIVO_E_HIP;
-    hipLaunchKernelGGL(k_knn_replay, dim3(64), dim3(64), 0, (hipStream_t)stream, q);
+    if (q.canon)
+        hipLaunchKernelGGL(k_knn_canon, dim3(64), dim3(64), 0, (hipStream_t)stream, q);
+    else
+        hipLaunchKernelGGL(k_knn_replay, dim3(64), dim3(64), 0, (hipStream_t)stream, q);
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 

@@ -145,6 +145,11 @@ class VioStats(C.Structure):
                 ("cov_updated", C.c_int32), ("n_meas", C.c_int64), ("out_of_frame", C.c_int64)]
 
 
+class MapAddStats(C.Structure):
+    _fields_ = [("events", C.c_int64), ("added", C.c_int64), ("deleted", C.c_int64), ("ambiguous", C.c_int64),
+                ("deferred", C.c_int64), ("map_points", C.c_int64)]
+
+
 SIGNATURES = {
     "livo_abi_version": (C.c_int, []),
     "livo_error_string": (C.c_char_p, [C.c_int]),
@@ -180,6 +185,10 @@ SIGNATURES = {
     "livo_vio_params_default": (C.c_int, [C.POINTER(VioParams)]),
     "livo_vio_update": (C.c_int, [_P, C.POINTER(VioParams), _P, C.c_int32, C.c_int32, _P, _P, _P, C.c_int64,
                                   C.POINTER(State), C.POINTER(State), _P, C.POINTER(VioStats)]),
+    "livo_map_add_points": (C.c_int, [_P, _P, C.c_int64, C.c_int64, C.c_float, C.c_int, C.POINTER(MapAddStats)]),
+    "livo_map_delete_boxes": (C.c_int, [_P, _P, C.c_int64, C.POINTER(C.c_int64)]),
+    "livo_map_dump": (C.c_int, [_P, _P, _P, C.c_int64, C.POINTER(C.c_int64)]),
+    "livo_map_last_add_stats": (C.c_int, [_P, C.POINTER(MapAddStats)]),
     "livo_sync": (C.c_int, [_P]),
 }
 
@@ -400,6 +409,39 @@ class Context:
     # ----------------------------------------------------------- iVox ----
     def set_backend(self, backend: int):
         _check("livo_ctx_set_backend", self._L.livo_ctx_set_backend(self.h, backend))
+        self.backend = backend
+
+    # ------------------------------------------- ikd-Tree incremental map ----
+    def map_add_points(self, xyz: np.ndarray, downsample_size: float = 0.5, downsample: bool = True) -> dict:
+        """KD_TREE::Add_Points (ikd_Tree.cpp:382-457) on the device map."""
+        xyz = np.ascontiguousarray(xyz, np.float32)
+        assert xyz.ndim == 2 and xyz.shape[1] >= 3
+        st = MapAddStats()
+        _check("livo_map_add_points", self._L.livo_map_add_points(self.h, _ptr(xyz), xyz.shape[0], xyz.shape[1] * 4,
+                                                                  downsample_size, int(bool(downsample)),
+                                                                  C.byref(st)))
+        return {k: getattr(st, k) for k, _ in MapAddStats._fields_}
+
+    def map_delete_boxes(self, boxes) -> int:
+        """KD_TREE::Delete_Point_Boxes (ikd_Tree.cpp:501-521); boxes (n, 6) = vertex_min, vertex_max."""
+        b = np.ascontiguousarray(boxes, np.float32).reshape(-1, 6)
+        n = C.c_int64()
+        _check("livo_map_delete_boxes", self._L.livo_map_delete_boxes(self.h, _ptr(b), b.shape[0], C.byref(n)))
+        return n.value
+
+    def map_dump(self):
+        """(xyz (n, 3), ids (n,)) of the map's points in id order."""
+        n = C.c_int64()
+        _check("livo_map_dump", self._L.livo_map_dump(self.h, None, None, 0, C.byref(n)))
+        xyz = np.zeros((n.value, 3), np.float32)
+        ids = np.zeros(n.value, np.int32)
+        _check("livo_map_dump", self._L.livo_map_dump(self.h, _ptr(xyz), _ptr(ids), n.value, C.byref(n)))
+        return xyz, ids
+
+    def map_last_add_stats(self) -> dict:
+        st = MapAddStats()
+        _check("livo_map_last_add_stats", self._L.livo_map_last_add_stats(self.h, C.byref(st)))
+        return {k: getattr(st, k) for k, _ in MapAddStats._fields_}
 
     def ivox_init(self, resolution: float = 0.2, nearby_type: int = 18, capacity: int = 1_000_000):
         p = IvoxParams(resolution, nearby_type, capacity)
@@ -438,7 +480,8 @@ class Context:
         return xyz, ids, keys
 
     def map_incremental(self, sid: int, state: dict, filter_size_map: float = 0.5, ekf_inited: bool = True):
-        """Returns (cat per point: 0 skipped / 1 added / 2 added without downsampling, counts dict)."""
+        """Returns (cat per point: 0 skipped / 1 added / 2 added without downsampling, counts dict).
+        With the ikd-Tree backend: Add_Points of every point (cat 1), counts = the add statistics."""
         n = self.scans[sid]
         cat = np.zeros(n, np.uint8)
         counts = np.zeros(2, np.int64)
@@ -446,6 +489,8 @@ class Context:
         _check("livo_map_incremental", self._L.livo_map_incremental(self.h, sid, C.byref(s), filter_size_map,
                                                                     int(bool(ekf_inited)), _ptr(cat),
                                                                     _ptr(counts)))
+        if getattr(self, "backend", BACKEND_IKDTREE) == BACKEND_IKDTREE:
+            return cat, self.map_last_add_stats()
         return cat, {"added": int(counts[0]), "no_downsample": int(counts[1])}
 
     def scan_preprocess(self, raw: np.ndarray, poses=None, rot_end=None, pos_end=None, leaf_size: float = 0.5):

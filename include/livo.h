@@ -19,8 +19,10 @@
  *   livo_iekf_update_batch ← the same for independent scans (scan farm, §8e)
  *   livo_ivox_*         ← faster_lio::IVox, the compiled default k-NN backend
  *                                                   include/ivox3d/ivox3d.h:37-305
- *   livo_map_incremental ← LaserMapping::map_incremental (iVox branch)
+ *   livo_map_incremental ← LaserMapping::map_incremental (iVox and ikd-Tree branches)
  *                                                   src/laser_mapping.cpp:329-389
+ *   livo_map_add_points / livo_map_delete_boxes ← KD_TREE::Add_Points / Delete_Point_Boxes
+ *                                                   include/ikd-Tree/ikd_Tree.cpp:382-457, 501-521
  *   livo_vio_update     ← LidarSelector::ComputeJ / UpdateState (VIO photometric update)
  *                                                   src/lidar_selection.cpp:748-978
  *   livo_scan_preprocess ← ImuProcess::UndistortPcl (per point) + downSizeFilterSurf
@@ -373,6 +375,41 @@ int livo_vio_params_default(livo_vio_params* p);
 int livo_vio_update(livo_ctx* ctx, const livo_vio_params* p, const uint8_t* image, int32_t width, int32_t height,
                     const double* pos, const int32_t* search_levels, const float* patches, int64_t n,
                     livo_state* state, const livo_state* prior, float* errors, livo_vio_stats* stats);
+
+/* ------------------------------------------------------------------------
+ * ikd-Tree incremental map (the USE_ikdtree branch of
+ * map_incremental, src/laser_mapping.cpp:383-384, and the ikd-Tree's
+ * Delete_Point_Boxes).  The first call turns the built map (cell-grid search
+ * structure, the default) into an incremental point set: ids = the build's
+ * indices, then the next ids in input order for the points a call leaves in
+ * the map.  Later k-NN (livo_knn, livo_h_share, the IEKF loops) search the
+ * updated map; queries whose order the reference's tree shape would decide
+ * (PointType_CMP ties) come in (distance, x, id) order.
+ * livo_map_incremental with LIVO_BACKEND_IKDTREE runs Add_Points(world, true)
+ * on the scan at the given state: counts[0] = its return value, counts[1] =
+ * points deleted; cat = 1 for every point.
+ * ------------------------------------------------------------------------ */
+typedef struct livo_map_add_stats {
+    int64_t events;     /* Add_Points' return value (tmp_counter, include/ikd-Tree/ikd_Tree.cpp:416,428) */
+    int64_t added;      /* points of the call left in the map (new ids, input order)            */
+    int64_t deleted;    /* map points removed (Delete_by_range of a downsample box, :414)        */
+    int64_t ambiguous;  /* boxes whose kept stored point Search_by_range's order picks (ties)    */
+    int64_t deferred;   /* points handled by the in-order pass (box-face rounding cases)         */
+    int64_t map_points; /* points in the map after the call                                      */
+} livo_map_add_stats;
+
+/* KD_TREE::Add_Points(points, downsample_on) (ikd_Tree.cpp:382-457) with
+ * downsample_size (set_downsample_param, :35-40); xyz at xyz + i*stride_bytes. */
+int livo_map_add_points(livo_ctx* ctx, const float* xyz, int64_t n, int64_t stride_bytes, float downsample_size,
+                        int downsample_on, livo_map_add_stats* stats);
+/* KD_TREE::Delete_Point_Boxes (ikd_Tree.cpp:501-521): boxes n_boxes x 6 floats
+ * {vertex_min[3], vertex_max[3]} (BoxPointType), half open; *deleted = points removed. */
+int livo_map_delete_boxes(livo_ctx* ctx, const float* boxes, int64_t n_boxes, int64_t* deleted);
+/* The map's points in id order: *n = count; xyz (cap x 3) and ids (cap) may be
+ * NULL, else cap must be >= the count (LIVO_E_RANGE otherwise, *n still set). */
+int livo_map_dump(livo_ctx* ctx, float* xyz, int32_t* ids, int64_t cap, int64_t* n);
+/* Statistics of the last livo_map_add_points / ikd-Tree livo_map_incremental. */
+int livo_map_last_add_stats(livo_ctx* ctx, livo_map_add_stats* out);
 
 int livo_sync(livo_ctx* ctx);
 

@@ -1,0 +1,171 @@
+"""GPU parity of the ikd-Tree incremental map (the
+USE_ikdtree branch of map_incremental, laser_mapping.cpp:383-384, i.e.
+KD_TREE::Add_Points with downsampling, ikd_Tree.cpp:382-457, and
+Delete_Point_Boxes, :501-521): livo_map_add_points / livo_map_incremental /
+livo_map_delete_boxes against the oracle's restatement (pinned in
+tests/test_ikd_incr_oracle.py).
+
+Bars: the map after every call (ids and coordinates, bit for bit) and the
+call's counts (Add_Points' return value, points kept, points deleted, centre
+ties) exact; k-NN of the updated map (indices, squared distances and order)
+bit-exact; IEKF updates on the updated map: counts exact, state delta 1e-5
+relative (north_star tolerance).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+f32 = np.float32
+REL_STATE = 1e-5
+KEYS = ("events", "added", "deleted", "ambiguous")
+
+
+@pytest.fixture(scope="module")
+def ictx(built):
+    import livo_amd
+    from livo_amd import synth
+    ctx = livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=4)
+    yield ctx
+    ctx.close()
+
+
+def _world(body, st):
+    from livo_amd import synth
+    return ((body.astype(np.float64) + synth.T_LI) @ st["rot"].T + st["pos"]).astype(f32)
+
+
+def _pair(ctx, m):
+    import oracle
+    ctx.map_build(m)
+    return oracle.DynMap(m)
+
+
+def _same_map(ctx, dm):
+    gx, gi = ctx.map_dump()
+    rx, ri = dm.dump()
+    assert np.array_equal(gi, ri)
+    assert np.array_equal(gx.view(np.uint32), rx.view(np.uint32))
+
+
+def _same_add(g, r):
+    assert {k: g[k] for k in KEYS} == r, (g, r)
+
+
+@pytest.mark.parametrize("ds", [0.5, 0.3])
+def test_add_points_room(ictx, ds):
+    from livo_amd import synth
+    m = synth.make_map(200_000)
+    dm = _pair(ictx, m)
+    for sid in (0, 1):
+        body, _, _ = synth.make_scan(20_000, sid)
+        W = _world(body, synth.make_state(sid))
+        g = ictx.map_add_points(W, ds)
+        _same_add(g, dm.add_points(W, ds))
+        assert g["map_points"] == len(dm.dump()[1]) == ictx.map_info()["num_points"]
+        _same_map(ictx, dm)
+
+
+def test_add_points_box_faces_duplicates_and_ties(ictx):
+    """Points within ulps of box faces (the in-order pass), duplicates, centre ties, no-downsample adds."""
+    from livo_amd import synth
+    rng = np.random.default_rng(31)
+    deferred = amb = 0
+    for ds in (0.5, 0.3):
+        pairs, far = synth.centre_tie_points(ds)
+        m = np.concatenate([rng.uniform(-6, 6, (3000, 3)), synth.boundary_points(rng, ds, 600, span=12), pairs])
+        m = np.concatenate([m, m[:20]]).astype(f32)
+        dm = _pair(ictx, m)
+        for rep in range(4):
+            W = np.concatenate([rng.uniform(-6, 6, (800, 3)), synth.boundary_points(rng, ds, 400, span=12),
+                                m[rng.choice(len(m), 40)], far]).astype(f32)
+            W = W[rng.permutation(len(W))]
+            down = rep != 2
+            g = ictx.map_add_points(W, ds, downsample=down)
+            _same_add(g, dm.add_points(W, ds, downsample=down))
+            deferred += g["deferred"]
+            amb += g["ambiguous"]
+            _same_map(ictx, dm)
+    assert deferred > 0 and amb > 0  # both special paths ran
+
+
+def test_add_points_empty_and_tiny_maps(ictx):
+    rng = np.random.default_rng(5)
+    for M in (0, 1, 4):
+        m = rng.uniform(-1, 1, (M, 3)).astype(f32)
+        dm = _pair(ictx, m)
+        for _ in range(3):
+            W = rng.uniform(-2, 2, (50, 3)).astype(f32)
+            _same_add(ictx.map_add_points(W, 0.5), dm.add_points(W, 0.5))
+            _same_map(ictx, dm)
+        q = rng.uniform(-3, 3, (100, 3)).astype(f32)
+        gi, gd = ictx.knn(q)
+        ri, rd = dm.knn(q)
+        assert np.array_equal(gi, ri) and np.array_equal(gd, rd)
+
+
+def test_knn_after_add_and_delete(ictx):
+    from livo_amd import synth
+    rng = np.random.default_rng(9)
+    m = synth.make_map(100_000)
+    dm = _pair(ictx, m)
+    body, _, _ = synth.make_scan(20_000, 3)
+    W = _world(body, synth.make_state(3))
+    ictx.map_add_points(W, 0.3)
+    dm.add_points(W, 0.3)
+    boxes = np.array([[-5, -5, -2, 0, 0, 3], [10, 10, -2, 12, 12, 3]], f32)
+    assert ictx.map_delete_boxes(boxes) == dm.delete_boxes(boxes)
+    _same_map(ictx, dm)
+    P, _ = dm.dump()
+    q = np.concatenate([W[:5000], P[:2000], rng.uniform([-32, -22, -2], [32, 22, 3], (3000, 3))]).astype(f32)
+    gi, gd = ictx.knn(q)
+    ri, rd = dm.knn(q)
+    assert np.array_equal(gi, ri)
+    assert np.array_equal(gd.view(np.uint32), rd.view(np.uint32))
+
+
+def test_iekf_on_updated_map(ictx):
+    from livo_amd import synth
+    m = synth.make_map(100_000)
+    dm = _pair(ictx, m)
+    body0, _, _ = synth.make_scan(20_000, 0)
+    W = _world(body0, synth.make_state(0))
+    ictx.map_add_points(W, 0.5)
+    dm.add_points(W, 0.5)
+    body, _, _ = synth.make_scan(10_000, 1)
+    st = synth.make_state(1)
+    sid = ictx.scan_upload(body)
+    gs, gst = ictx.iekf_update(sid, st)
+    rs, rst = dm.iekf_update(body, st, t_LI=synth.T_LI, max_iter=4)
+    assert gst["iterations"] == rst["iterations"] and gst["effct_feat_num"] == rst["effct_feat_num"]
+    for e in range(gst["iterations"]):
+        rel = np.linalg.norm(gst["solution"][e] - rst["solution"][e]) / np.linalg.norm(rst["solution"][e])
+        assert rel < REL_STATE, (e, rel)
+    # the batched loop (4 stream groups) on the same map gives the same updates
+    sids = [sid] + [ictx.scan_upload(synth.make_scan(10_000, k)[0]) for k in (2, 3, 4)]
+    sts = [st] + [synth.make_state(k) for k in (2, 3, 4)]
+    _, bst = ictx.iekf_update_batch(sids, sts)
+    assert bst[0]["iterations"] == gst["iterations"] and np.array_equal(bst[0]["solution"], gst["solution"])
+    for s in sids:
+        ictx.scan_release(s)
+
+
+def test_odometry_with_ikd_map_incremental(ictx):
+    """LaserMapping::Run with USE_ikdtree: per scan the IEKF update, then map_incremental
+    (Add_Points of feats_down_world at the updated state)."""
+    from livo_amd import synth
+    m = synth.make_map(100_000)
+    dm = _pair(ictx, m)
+    for k in range(4):
+        body, _, _ = synth.make_scan(20_000, 10 + k)
+        st0 = synth.make_state(10 + k)
+        sid = ictx.scan_upload(body)
+        gs, gst = ictx.iekf_update(sid, st0)
+        rs, rst = dm.iekf_update(body, st0, t_LI=synth.T_LI, max_iter=4)
+        assert gst["iterations"] == rst["iterations"] and gst["effct_feat_num"] == rst["effct_feat_num"]
+        assert np.linalg.norm(gs["pos"] - rs["pos"]) <= REL_STATE * max(np.linalg.norm(rs["pos"] - st0["pos"]), 1e-9)
+        # both maps take the points at the GPU's updated state
+        cat, g = ictx.map_incremental(sid, gs, filter_size_map=0.3)
+        assert np.all(cat == 1)
+        _same_add(g, dm.map_incremental(body, gs, t_LI=synth.T_LI, filter_size_map=0.3))
+        _same_map(ictx, dm)
+        ictx.scan_release(sid)
