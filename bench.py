@@ -355,6 +355,51 @@ def main():
             "note": "LIVO_BACKEND_IVOX: IVox GetClosestPoint (NEARBY18, 0.2 m grids, 5 m range) on the same "
                     f"{a.batch} scans per GPU, {iv_steps} steps after the IKFoM run; not part of `value`"}
 
+    # ---- the ikd-Tree incremental map (the USE_ikdtree
+    # branch of map_incremental): sequential odometry on a second context --
+    # per scan the IEKF update, then Add_Points(feats_down_world, true) at the
+    # updated state (filter_size_map 0.5) into the 1M-point map, which grows
+    ik_ctx = livo_amd.Context(device, t_LI=synth.T_LI, max_iterations=a.max_iter)
+    ik_ctx.map_build(m)
+    ikd_rows = []
+    for rep in range(2):  # the first pass warms the allocations and activates the incremental map
+        ik_sids = [ik_ctx.scan_upload(sc) for sc in scans]
+        t_upd = t_add = 0.0
+        events = added = deleted = 0
+        sync()
+        t = time.perf_counter()
+        for sid, s in zip(ik_sids, st0):
+            t1 = time.perf_counter()
+            stn, _ = ik_ctx.iekf_update(sid, s)
+            t2 = time.perf_counter()
+            _, ast = ik_ctx.map_incremental(sid, stn, filter_size_map=0.5)
+            t3 = time.perf_counter()
+            t_upd += t2 - t1
+            t_add += t3 - t2
+            events += ast["events"]
+            added += ast["added"]
+            deleted += ast["deleted"]
+        sync()
+        ikd_elapsed = time.perf_counter() - t
+        for sid in ik_sids:
+            ik_ctx.scan_release(sid)
+        ikd_rows.append((ikd_elapsed, t_upd, t_add, events, added, deleted))
+    ikd_elapsed, t_upd, t_add, events, added, deleted = ikd_rows[-1]
+    if rank == 0:
+        nsc = len(scans)
+        result["ikd_incremental"] = {
+            "scans_per_s": round(nsc / ikd_elapsed, 3),
+            "iekf_ms_per_scan": round(t_upd / nsc * 1e3, 3),
+            "add_points_ms_per_scan": round(t_add / nsc * 1e3, 3),
+            "add_points_events_per_scan": round(events / nsc, 1),
+            "points_added_per_scan": round(added / nsc, 1),
+            "points_deleted_per_scan": round(deleted / nsc, 1),
+            "map_points_after": ik_ctx.map_info()["num_points"],
+            "note": f"sequential odometry on the {a.map_points}-pt map: livo_iekf_update + livo_map_incremental "
+                    "(ikd-Tree backend: KD_TREE::Add_Points of all scan points, downsample 0.5 m) per scan, "
+                    "second pass over the scans (the map has grown), host-timed; not part of `value`"}
+    ik_ctx.close()
+
     # ---- the VIO photometric update: frames per second
     # at the reference's size (a 40-px grid on 640x512: <= 192 visual points)
     # and at 20k points; not part of `value`
@@ -436,6 +481,25 @@ def main():
         result["ivox"]["parity_scan0"] = {"iterations_equal": ig["iterations"] == ivst["iterations"],
                                           "effct_equal": ig["effct_feat_num"] == ivst["effct_feat_num"],
                                           "max_rel_state_delta": float(f"{ivrel:.3e}")}
+        # the ikd-Tree incremental map: Add_Points of scan 0 by the oracle, 1 thread
+        dyn = oracle.DynMap(m)
+        t = time.perf_counter()
+        dyn.map_incremental(scans[0], first_states[0], t_LI=synth.T_LI, filter_size_map=0.5)
+        result["ikd_incremental"]["cpu_add_points_ms"] = round((time.perf_counter() - t) * 1e3, 3)
+        del dyn
+        # the reference's thread counts (MP_PROC_NUM = 4, CMakeLists.txt:30-33) and 16 host threads
+        by_threads = {}
+        for nt in (4, 16):
+            t = time.perf_counter()
+            k = 0
+            while k < 64:
+                tree.iekf_update(scans[k % a.batch], st0[k % a.batch], R_LI=np.eye(3), t_LI=synth.T_LI,
+                                 max_iter=a.max_iter, threads=nt)
+                k += 1
+                if time.perf_counter() - t >= a.cpu_seconds / 2:
+                    break
+            by_threads[str(nt)] = round(k / (time.perf_counter() - t), 4)
+        result["cpu_baseline"]["by_threads"] = by_threads
         # VIO: the oracle on the same frames (1 thread) and parity of the large one
         for nv, (fr, vst) in vio_frames.items():
             t = time.perf_counter()
