@@ -8,14 +8,15 @@ of a rocprofv3 --kernel-trace run into batches of `groups` and reports the
 mean span (first start -> last end, extended to the replay dispatch that
 follows each one on its queue) so it can be compared with bench's
 roofline.avg_launch_ms.
-usage: python tools/kt_span.py <kernel_trace.csv> [groups=4] [skip_batches=4]
+usage: python tools/kt_span.py <kernel_trace.csv> [groups=4] [skip_batches=4] [max_batches=all]
+(max_batches: only the headline run's batches, before the later legs of bench.py)
 """
 import csv
 import sys
 
 
-def main(path, groups="4", skip="4"):
-    groups, skip = int(groups), int(skip)
+def main(path, groups="4", skip="4", max_batches="0"):
+    groups, skip, mb = int(groups), int(skip), int(max_batches)
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     by_q = {}
     for r in rows:
@@ -29,6 +30,8 @@ def main(path, groups="4", skip="4"):
                     end = int(rs[i + 1]["End_Timestamp"])
                 items.append((int(r["Start_Timestamp"]), end, int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
     items.sort()
+    if mb > 0:
+        items = items[:mb * groups]
     spans, durs = [], [d for _, _, d in items]
     for b in range(skip, len(items) // groups):
         chunk = items[b * groups:(b + 1) * groups]
@@ -39,4 +42,4 @@ def main(path, groups="4", skip="4"):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:5])
