@@ -143,7 +143,9 @@ public:
         adopt_scan(id, nd);
     }
 
-    // map_incremental() (laser_mapping.cpp:329-389), iVox branch, at the updated state.
+    // map_incremental() (laser_mapping.cpp:329-389) at the updated state: the iVox branch
+    // (counts = added, added without downsampling) or, on the ikd-Tree backend, Add_Points
+    // of every point (:383-384; counts = Add_Points' return value, points deleted).
     void map_incremental(double filter_size_map_min, bool flg_EKF_inited = true) {
         int64_t counts[2] = {0, 0};
         check(livo_map_incremental(ctx_, scan_id_, &state, filter_size_map_min, flg_EKF_inited ? 1 : 0, nullptr,
