@@ -167,6 +167,10 @@ __global__ void k_add_heads(DynAddParams P) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= P.n) return;
     P.heads[k] = (k == 0 || P.skeys[k] != P.skeys[k - 1]) ? 1u : 0u;
+    // the points in box order: k_add_group then walks a box's sequence with contiguous loads
+    const uint32_t i = P.svals[k];
+    const float4 p = reinterpret_cast<const float4*>(P.W)[i];
+    reinterpret_cast<float4*>(P.Ws)[k] = make_float4(p.x, p.y, p.z, __uint_as_float(i));
 }
 
 __global__ void k_add_starts(DynAddParams P) {
@@ -194,7 +198,7 @@ __global__ __launch_bounds__(256) void k_add_group(DynAddParams P) {
     int l[3] = {0, 0, 0}, h[3] = {-1, -1, -1};
     if (!defer && !box_cells(P, b, l, h)) defer = true;
     const float4* __restrict__ gp = reinterpret_cast<const float4*>(P.gpts);
-    const float4* __restrict__ W = reinterpret_cast<const float4*>(P.W);
+    const float4* __restrict__ Ws = reinterpret_cast<const float4*>(P.Ws);
     // pass 1: Search_by_range -- count, the first nearest in id order, ties at that distance
     int cnt = 0;
     float bd = INFINITY, bx = 0.f, by = 0.f, bz = 0.f;
@@ -228,8 +232,8 @@ __global__ __launch_bounds__(256) void k_add_group(DynAddParams P) {
         return;
     }
     // the box's new points in input order (:390-437); after the first, the box holds one point
-    uint32_t win = P.svals[s0];
-    float4 p = W[win];
+    float4 p = Ws[s0];
+    uint32_t win = __float_as_uint(p.w);
     float dc = mid_dist(b, p.x, p.y, p.z);
     bool newer = !(cnt > 0 && bd < dc);
     float wx = p.x, wy = p.y, wz = p.z;
@@ -238,8 +242,8 @@ __global__ __launch_bounds__(256) void k_add_group(DynAddParams P) {
     if (cnt > 1 && !newer && tie) amb = 1;
     if (cnt > 1 || newer || same_pt(p.x, p.y, p.z, wx, wy, wz)) events++;
     for (uint32_t k = s0 + 1; k < s1; k++) {
-        const uint32_t i = P.svals[k];
-        p = W[i];
+        p = Ws[k];
+        const uint32_t i = __float_as_uint(p.w);
         const float d = mid_dist(b, p.x, p.y, p.z);
         if (d <= dc) {  // the stored point replaces it only if strictly nearer
             newer = true; win = i; dc = d; wx = p.x; wy = p.y; wz = p.z;

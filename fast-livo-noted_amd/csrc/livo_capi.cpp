@@ -91,7 +91,7 @@ struct DynDev {
     unsigned long long *keys = nullptr, *skeys = nullptr;
     uint32_t *iota = nullptr, *svals = nullptr, *heads = nullptr, *runid = nullptr, *starts = nullptr;
     int64_t sort_cap = 0;
-    float *W = nullptr, *seq = nullptr;
+    float *W = nullptr, *seq = nullptr, *Ws = nullptr;
     uint32_t *defer = nullptr, *dpos = nullptr, *dlist = nullptr, *keep = nullptr, *apos = nullptr;
     int64_t add_cap = 0;
     float* boxes = nullptr;
@@ -566,7 +566,7 @@ static void dyn_free(DynDev& d) {
     dev_free(d.all); dev_free(d.alive);
     dev_free(d.keys); dev_free(d.skeys); dev_free(d.iota); dev_free(d.svals);
     dev_free(d.heads); dev_free(d.runid); dev_free(d.starts);
-    dev_free(d.W); dev_free(d.seq);
+    dev_free(d.W); dev_free(d.seq); dev_free(d.Ws);
     dev_free(d.defer); dev_free(d.dpos); dev_free(d.dlist); dev_free(d.keep); dev_free(d.apos);
     dev_free(d.boxes); dev_free(d.dirty); dev_free(d.ctr);
     d = DynDev{};
@@ -616,10 +616,11 @@ static int dyn_add_scratch(livo_ctx* c, int64_t n) {
     DynDev& d = c->dyn;
     if (n <= d.add_cap) return LIVO_OK;
     const int64_t cap = std::max<int64_t>(n + (n >> 2), 4096);
-    dev_free(d.W); dev_free(d.seq);
+    dev_free(d.W); dev_free(d.seq); dev_free(d.Ws);
     dev_free(d.defer); dev_free(d.dpos); dev_free(d.dlist); dev_free(d.keep); dev_free(d.apos);
     d.add_cap = 0;
-    if (dev_alloc(&d.W, (size_t)cap * 4) || dev_alloc(&d.seq, (size_t)cap * 4) || dev_alloc(&d.defer, cap) ||
+    if (dev_alloc(&d.W, (size_t)cap * 4) || dev_alloc(&d.seq, (size_t)cap * 4) || dev_alloc(&d.Ws, (size_t)cap * 4) ||
+        dev_alloc(&d.defer, cap) ||
         dev_alloc(&d.dpos, cap) || dev_alloc(&d.dlist, cap) || dev_alloc(&d.keep, cap) || dev_alloc(&d.apos, cap))
         return LIVO_E_OOM;
     d.add_cap = cap;
@@ -725,7 +726,7 @@ static int dyn_add(livo_ctx* c, int64_t n, float ds, bool downsample, livo_map_a
         std::memcpy(P.gorg, c->gorg, sizeof(P.gorg));
         P.gh = c->gh; P.ginv = 1.0f / c->gh; P.geps = c->geps;
         P.base = d.n_ids; P.alive = d.alive;
-        P.keys = d.keys; P.iota = d.iota; P.skeys = d.skeys; P.svals = d.svals;
+        P.keys = d.keys; P.iota = d.iota; P.skeys = d.skeys; P.svals = d.svals; P.Ws = d.Ws;
         P.heads = d.heads; P.runid = d.runid; P.starts = d.starts;
         P.defer = d.defer; P.dpos = d.dpos; P.dlist = d.dlist; P.keep = d.keep; P.seq = d.seq;
         P.dirty = d.dirty; P.dirty_cap = kDynDirtyCap; P.ctr = d.ctr;

@@ -455,6 +455,7 @@ struct DynAddParams {
     uint32_t* iota;
     const unsigned long long* skeys;  // sorted by box key (stable)
     const uint32_t* svals;
+    float* Ws;                  // n x 4: the points in sorted order (x, y, z, input index bits)
     uint32_t* heads;            // n
     uint32_t* runid;            // n: exclusive scan of heads
     uint32_t* starts;           // runs + 1
