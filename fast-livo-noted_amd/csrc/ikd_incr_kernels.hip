@@ -184,29 +184,28 @@ __global__ void k_add_starts(DynAddParams P) {
     }
 }
 
-// One box per thread: its stored points, then its new points in input order.
-__global__ __launch_bounds__(256) void k_add_group(DynAddParams P) {
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= (int64_t)P.ctr[kDynRuns]) return;
-    const uint32_t s0 = P.starts[g], s1 = P.starts[g + 1];
-    const unsigned long long key = P.skeys[s0];
+// A box's stored points (Search_by_range): count, the first nearest in id
+// order, whether another one ties with it at a different position; `defer`
+// if the box is dirty or holds a point that also lies in a neighbouring box.
+struct BoxStore {
+    int cnt;
+    float bd, bx, by, bz;
+    uint32_t bid;
+    bool tie, defer;
+    int l[3], h[3];
+};
+__device__ __forceinline__ void box_store(const DynAddParams& P, unsigned long long key, const DBox& b, BoxStore& S) {
+    S.cnt = 0; S.bd = INFINITY; S.bx = S.by = S.bz = 0.f; S.bid = 0xFFFFFFFFu; S.tie = false;
+    S.l[0] = S.l[1] = S.l[2] = 0; S.h[0] = S.h[1] = S.h[2] = -1;
     const unsigned long long nd = P.ctr[kDynDirty];
     bool defer = nd > (unsigned long long)P.dirty_cap;
     for (unsigned long long d = 0; d < nd && d < (unsigned long long)P.dirty_cap && !defer; d++)
         defer = P.dirty[d] == key;
-    const DBox b = dbox(key, P.ds);
-    int l[3] = {0, 0, 0}, h[3] = {-1, -1, -1};
-    if (!defer && !box_cells(P, b, l, h)) defer = true;
+    if (!defer && !box_cells(P, b, S.l, S.h)) defer = true;
     const float4* __restrict__ gp = reinterpret_cast<const float4*>(P.gpts);
-    const float4* __restrict__ Ws = reinterpret_cast<const float4*>(P.Ws);
-    // pass 1: Search_by_range -- count, the first nearest in id order, ties at that distance
-    int cnt = 0;
-    float bd = INFINITY, bx = 0.f, by = 0.f, bz = 0.f;
-    uint32_t bid = 0xFFFFFFFFu;
-    bool tie = false;
-    for (int z = l[2]; z <= h[2] && !defer; z++)
-        for (int y = l[1]; y <= h[1] && !defer; y++)
-            for (int x = l[0]; x <= h[0] && !defer; x++) {
+    for (int z = S.l[2]; z <= S.h[2] && !defer; z++)
+        for (int y = S.l[1]; y <= S.h[1] && !defer; y++)
+            for (int x = S.l[0]; x <= S.h[0] && !defer; x++) {
                 const uint2 r = cell_run(P.gslots, P.glog2, x, y, z);
                 for (uint32_t k = r.x; k < r.x + r.y; k++) {
                     const float4 q = gp[k];
@@ -215,32 +214,68 @@ __global__ __launch_bounds__(256) void k_add_group(DynAddParams P) {
                         defer = true;
                         break;
                     }
-                    cnt++;
+                    S.cnt++;
                     const float d = mid_dist(b, q.x, q.y, q.z);
                     const uint32_t id = __float_as_uint(q.w);
-                    if (d < bd) {
-                        bd = d; bid = id; bx = q.x; by = q.y; bz = q.z;
-                        tie = false;
-                    } else if (d == bd) {
-                        if (q.x != bx || q.y != by || q.z != bz) tie = true;
-                        if (id < bid) { bid = id; bx = q.x; by = q.y; bz = q.z; }
+                    if (d < S.bd) {
+                        S.bd = d; S.bid = id; S.bx = q.x; S.by = q.y; S.bz = q.z;
+                        S.tie = false;
+                    } else if (d == S.bd) {
+                        if (q.x != S.bx || q.y != S.by || q.z != S.bz) S.tie = true;
+                        if (id < S.bid) { S.bid = id; S.bx = q.x; S.by = q.y; S.bz = q.z; }
                     }
                 }
             }
-    if (defer) {
+    S.defer = defer;
+}
+// Delete_by_range of the box; a stored winner is deleted and added again (it stays).
+__device__ __forceinline__ unsigned long long box_delete(const DynAddParams& P, const DBox& b, const BoxStore& S,
+                                                         bool newer) {
+    unsigned long long deleted = 0;
+    if (!(S.cnt > 0 && (newer || S.cnt > 1))) return 0;
+    const float4* __restrict__ gp = reinterpret_cast<const float4*>(P.gpts);
+    for (int z = S.l[2]; z <= S.h[2]; z++)
+        for (int y = S.l[1]; y <= S.h[1]; y++)
+            for (int x = S.l[0]; x <= S.h[0]; x++) {
+                const uint2 r = cell_run(P.gslots, P.glog2, x, y, z);
+                for (uint32_t k = r.x; k < r.x + r.y; k++) {
+                    const float4 q = gp[k];
+                    if (!in_dbox(b, q.x, q.y, q.z)) continue;
+                    const uint32_t id = __float_as_uint(q.w);
+                    if (!newer && id == S.bid) continue;
+                    P.alive[id] = 0;
+                    deleted++;
+                }
+            }
+    return deleted;
+}
+constexpr uint32_t kBigRun = 96;  // boxes with more new points: one wave each (k_add_group_big)
+
+// One box per thread: its stored points, then its new points in input order.
+__global__ __launch_bounds__(256) void k_add_group(DynAddParams P) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= (int64_t)P.ctr[kDynRuns]) return;
+    const uint32_t s0 = P.starts[g], s1 = P.starts[g + 1];
+    if (s1 - s0 > kBigRun) return;
+    const unsigned long long key = P.skeys[s0];
+    const DBox b = dbox(key, P.ds);
+    BoxStore S;
+    box_store(P, key, b, S);
+    if (S.defer) {
         for (uint32_t k = s0; k < s1; k++) P.defer[P.svals[k]] = 1u;
         return;
     }
+    const float4* __restrict__ Ws = reinterpret_cast<const float4*>(P.Ws);
     // the box's new points in input order (:390-437); after the first, the box holds one point
     float4 p = Ws[s0];
     uint32_t win = __float_as_uint(p.w);
     float dc = mid_dist(b, p.x, p.y, p.z);
-    bool newer = !(cnt > 0 && bd < dc);
+    bool newer = !(S.cnt > 0 && S.bd < dc);
     float wx = p.x, wy = p.y, wz = p.z;
-    if (!newer) { dc = bd; wx = bx; wy = by; wz = bz; }
-    unsigned long long events = 0, amb = 0, deleted = 0;
-    if (cnt > 1 && !newer && tie) amb = 1;
-    if (cnt > 1 || newer || same_pt(p.x, p.y, p.z, wx, wy, wz)) events++;
+    if (!newer) { dc = S.bd; wx = S.bx; wy = S.by; wz = S.bz; }
+    unsigned long long events = 0, amb = 0;
+    if (S.cnt > 1 && !newer && S.tie) amb = 1;
+    if (S.cnt > 1 || newer || same_pt(p.x, p.y, p.z, wx, wy, wz)) events++;
     for (uint32_t k = s0 + 1; k < s1; k++) {
         p = Ws[k];
         const uint32_t i = __float_as_uint(p.w);
@@ -253,25 +288,111 @@ __global__ __launch_bounds__(256) void k_add_group(DynAddParams P) {
         }
     }
     if (newer) P.keep[win] = 1u;
-    if (cnt > 0 && (newer || cnt > 1)) {
-        // pass 2: Delete_by_range of the box; a stored winner is deleted and added again (it stays)
-        for (int z = l[2]; z <= h[2]; z++)
-            for (int y = l[1]; y <= h[1]; y++)
-                for (int x = l[0]; x <= h[0]; x++) {
-                    const uint2 r = cell_run(P.gslots, P.glog2, x, y, z);
-                    for (uint32_t k = r.x; k < r.x + r.y; k++) {
-                        const float4 q = gp[k];
-                        if (!in_dbox(b, q.x, q.y, q.z)) continue;
-                        const uint32_t id = __float_as_uint(q.w);
-                        if (!newer && id == bid) continue;
-                        P.alive[id] = 0;
-                        deleted++;
-                    }
-                }
-    }
+    const unsigned long long deleted = box_delete(P, b, S, newer);
     if (events) atomicAdd(P.ctr + kDynEvents, events);
     if (deleted) atomicAdd(P.ctr + kDynDeleted, deleted);
     if (amb) atomicAdd(P.ctr + kDynAmbig, amb);
+}
+
+// The running winner as a scan: (distance, position) with the smaller distance,
+// the later position on ties ("d <= dc" lets the later point win).
+__device__ __forceinline__ void win_combine(float& d, int& k, float d2, int k2) {
+    if (d2 < d || (d2 == d && k2 > k)) { d = d2; k = k2; }
+}
+
+// One wave per box with more than kBigRun new points (boxes near the sensor):
+// lane 0 takes the stored points, then the sequence of new points is a
+// prefix scan of the running winner, 64 points per step.
+__global__ __launch_bounds__(64) void k_add_group_big(DynAddParams P) {
+    const int lane = threadIdx.x;
+    const int64_t runs = (int64_t)P.ctr[kDynRuns];
+    const float4* __restrict__ Ws = reinterpret_cast<const float4*>(P.Ws);
+    for (int64_t g = blockIdx.x; g < runs; g += gridDim.x) {
+        const uint32_t s0 = P.starts[g], s1 = P.starts[g + 1];
+        if (s1 - s0 <= kBigRun) continue;  // wave-uniform
+        const unsigned long long key = P.skeys[s0];
+        const DBox b = dbox(key, P.ds);
+        BoxStore S;
+        if (lane == 0) box_store(P, key, b, S);
+        const int defer = __shfl(lane == 0 ? (int)S.defer : 0, 0, 64);
+        if (defer) {
+            for (uint32_t k = s0 + lane; k < s1; k += 64) P.defer[P.svals[k]] = 1u;
+            continue;
+        }
+        // the first new point against the stored ones (lane 0), broadcast as the carry
+        float cd = 0.f;   // running winner: distance, position (-1: the stored point), coordinates
+        int ck = 0;
+        float cx = 0.f, cy = 0.f, cz = 0.f;
+        unsigned long long events = 0, amb = 0;
+        if (lane == 0) {
+            const float4 p = Ws[s0];
+            cd = mid_dist(b, p.x, p.y, p.z);
+            ck = (int)s0;
+            cx = p.x; cy = p.y; cz = p.z;
+            if (S.cnt > 0 && S.bd < cd) { cd = S.bd; ck = -1; cx = S.bx; cy = S.by; cz = S.bz; }
+            if (S.cnt > 1 && ck < 0 && S.tie) amb = 1;
+            if (S.cnt > 1 || ck >= 0 || same_pt(p.x, p.y, p.z, cx, cy, cz)) events = 1;
+        }
+        cd = __shfl(cd, 0, 64); ck = __shfl(ck, 0, 64);
+        cx = __shfl(cx, 0, 64); cy = __shfl(cy, 0, 64); cz = __shfl(cz, 0, 64);
+        for (uint32_t k0 = s0 + 1; k0 < s1; k0 += 64) {
+            const uint32_t k = k0 + lane;
+            const bool valid = k < s1;
+            float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+            float d = INFINITY;
+            int pk = -2;  // loses every comparison
+            if (valid) {
+                p = Ws[k];
+                d = mid_dist(b, p.x, p.y, p.z);
+                pk = (int)k;
+            }
+            // inclusive scan of the running winner over lanes 0..lane
+            float sd = d;
+            int sk = pk;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const float od = __shfl_up(sd, off, 64);
+                const int okk = __shfl_up(sk, off, 64);
+                if (lane >= off) win_combine(sd, sk, od, okk);
+            }
+            // the winner before this point: the carry (every earlier point), then the
+            // chunk's exclusive prefix -- later on equal distance, so the chunk wins ties
+            float pd = cd;
+            int pkk = ck;
+            const float xd = __shfl_up(sd, 1, 64);
+            const int xk = __shfl_up(sk, 1, 64);
+            if (lane > 0) win_combine(pd, pkk, xd, xk);
+            // the previous winner's coordinates
+            float qx = cx, qy = cy, qz = cz;
+            if (pkk >= 0 && pkk != ck) {
+                const float4 w = Ws[pkk];
+                qx = w.x; qy = w.y; qz = w.z;
+            }
+            unsigned long long ev = 0;
+            if (valid) ev = (d <= pd || same_pt(p.x, p.y, p.z, qx, qy, qz)) ? 1ull : 0ull;
+            events += ev;
+            // new carry: the inclusive winner of the last valid lane against the carry
+            const int last = (int)min<uint32_t>(63u, s1 - 1 - k0);
+            const float ld = __shfl(sd, last, 64);
+            const int lk = __shfl(sk, last, 64);
+            if (ld < cd || (ld == cd && lk > ck)) {
+                cd = ld; ck = lk;
+                const float4 w = Ws[lk];
+                cx = w.x; cy = w.y; cz = w.z;
+            }
+        }
+        // wave sums
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) events += __shfl_xor(events, off, 64);
+        if (lane == 0) {
+            const bool newer = ck >= 0;
+            if (newer) P.keep[__float_as_uint(Ws[ck].w)] = 1u;
+            const unsigned long long deleted = box_delete(P, b, S, newer);
+            if (events) atomicAdd(P.ctr + kDynEvents, events);
+            if (deleted) atomicAdd(P.ctr + kDynDeleted, deleted);
+            if (amb) atomicAdd(P.ctr + kDynAmbig, amb);
+        }
+    }
 }
 
 __global__ void k_add_dlist(DynAddParams P) {
@@ -481,7 +602,15 @@ static inline dim3 grid_for(int64_t n) { return dim3((unsigned)((n + 255) / 256)
 int launch_add_prep(const DynAddParams& p, void* stream) { DYN_LAUNCH(k_add_prep, p.n, p); }
 int launch_add_heads(const DynAddParams& p, void* stream) { DYN_LAUNCH(k_add_heads, p.n, p); }
 int launch_add_starts(const DynAddParams& p, void* stream) { DYN_LAUNCH(k_add_starts, p.n, p); }
-int launch_add_group(const DynAddParams& p, void* stream) { DYN_LAUNCH(k_add_group, p.n, p); }
+int launch_add_group(const DynAddParams& p, void* stream) {
+    if (p.n <= 0) return LIVO_OK;
+    hipLaunchKernelGGL(k_add_group, grid_for(p.n), dim3(256), 0, (hipStream_t)stream, p);
+    if (hipGetLastError() != hipSuccess) return LIVO_E_HIP;
+    const int64_t w = p.n / (kBigRun + 1) + 1;
+    const unsigned waves = (unsigned)(w < 4096 ? w : 4096);
+    hipLaunchKernelGGL(k_add_group_big, dim3(waves), dim3(64), 0, (hipStream_t)stream, p);
+    return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
 int launch_add_dlist(const DynAddParams& p, void* stream) { DYN_LAUNCH(k_add_dlist, p.n, p); }
 int launch_add_seq(const DynAddParams& p, void* stream) {
     hipLaunchKernelGGL(k_add_seq, dim3(1), dim3(64), 0, (hipStream_t)stream, p);

@@ -169,3 +169,17 @@ def test_odometry_with_ikd_map_incremental(ictx):
         _same_add(g, dm.map_incremental(body, gs, t_LI=synth.T_LI, filter_size_map=0.3))
         _same_map(ictx, dm)
         ictx.scan_release(sid)
+
+
+def test_add_points_crowded_boxes(ictx):
+    """Boxes with hundreds of new points (the wave-per-box pass), exact duplicates among them
+    (equal distances: the later point wins, ikd_Tree.cpp:405-411) and stored points inside."""
+    rng = np.random.default_rng(77)
+    m = rng.uniform(0, 1, (50, 3)).astype(f32)
+    dm = _pair(ictx, m)
+    for rep in range(3):
+        W = rng.uniform(0, 1, (3000, 3)).astype(f32)
+        W = np.concatenate([W, W[rng.choice(3000, 500)], np.full((40, 3), 0.25, f32)])
+        W = W[rng.permutation(len(W))]
+        _same_add(ictx.map_add_points(W, 0.5), dm.add_points(W, 0.5))
+        _same_map(ictx, dm)
