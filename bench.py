@@ -4,23 +4,27 @@
 Workload: synthetic Livox-Avia-shaped
 100k-point scans against a 1M-point ikd-Tree map, the full IEKF scan update of
 laser_mapping.cpp:171-238 with max_iteration = 4 (k-NN + plane fit + Jacobian
-+ HᵀH reduction + 18x18 solve per evaluation, rematch / convergence control on
-the device).  A step = one batched pass over --batch independent scans per GPU
-(scan farm, §8e); value = scan updates per second over the whole job, with
-scans and map already resident in HBM when the timed region starts.
++ HᵀH reduction + solve per evaluation, rematch / convergence control on the
+device).  A step = one batched pass over --batch independent scans per GPU
+(the scan farm of config 4, §8e: 64 scans over 8 GPUs = 8 per GPU); value =
+scan updates per second over the whole job, with scans and map already
+resident in HBM when the timed region starts.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
-N > 1: launched by torch.distributed.run (one process per GPU, RCCL); every
-rank processes its own scans ("weak" scaling) and the ranks all-reduce only
-throughput counters.  Rank 0 prints one JSON line.
+N > 1: one process per GPU.  Under torch.distributed.run (RANK set) this
+process is one rank; otherwise it starts N rank processes itself (before any
+GPU call), relays rank 0's JSON line and fails if any rank fails.  Every rank
+processes its own scans ("weak" scaling); the ranks all-reduce only
+throughput counters (RCCL; gloo when ranks share a GPU in a rehearsal).
 
-Extra fields: roofline of the dominant kernels (the first evaluation's
-transform + exact k-NN of every point: pilot pass + pilot-seeded pass, timed
-with HIP events on the library's streams inside the timed region, priced at
-the reference traversal's node visits V_ref), cpu_baseline (the
-CPU restatement, oracle/, 1 thread on this host, bounded sample), parity of
-the first scan against that CPU run.
+Extra fields: `roofline` of the dominant kernel (the batch's first-evaluation
+k-NN: HIP events on the library's streams, bytes the cell-grid search reads
+and writes, counted by the kernel; `traffic` from rocprofv3 PMC passes run by
+this bench in child processes), the drop-in regime (one scan at a time,
+with and without the upload), config 5 (10M-pt map, 200k-pt scans), the
+§8(f) legs, and `cpu_baseline` (oracle/, the C++ restatement, timed on this
+host: 1 thread, the reference's 4, and every core available to the job).
 """
 from __future__ import annotations
 
@@ -28,6 +32,9 @@ import argparse
 import ctypes as C
 import json
 import os
+import shutil
+import socket
+import subprocess
 import sys
 import time
 
@@ -39,21 +46,16 @@ for p in (os.path.join(ROOT, "fast-livo-noted_amd"), os.path.join(ROOT, "oracle"
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
-# Algorithmic bytes: k-NN per query V(q)*64 + 12 (query) + 40 (5 idx + sqdist);
-# plane fit 77 B/point; transform 24 B/point; Jacobian/reduction 28 B per effective point.
+# Bytes of the grid k-NN that the algorithm moves: per query the
+# body point in (16 B) and the 5 indices + squared distances out (40 B); per
+# hash slot read 16 B; per map point read 16 B (both counted by the kernel).
+B_QUERY_IO = 16 + 5 * 8
+B_SLOT = 16
+B_POINT = 16
+# SURVEY.md §8d's reference-equivalent pricing (the reference tree's traversal):
+# V_ref * 64 B per query + 12 B query + 40 B out.
 B_NODE = 64
-B_QUERY = 12 + 5 * 8
-B_PLANE = 77
-B_XFORM = 24
-B_JAC = 28
-
-
-def knn_kernel_desc():
-    if os.environ.get("LIVO_KNN_KIND") == "leaf":
-        return ("first-evaluation k-NN of the batch (4 stream groups): k_knn_leaf<false> (transform + exact 5-NN "
-                "of every point on the leaf map) + k_knn_replay (PointType_CMP-ambiguous queries on the ikd-Tree)")
-    return ("first-evaluation k-NN of the batch (4 stream groups): k_knn_grid<false> (transform + exact 5-NN of "
-            "every point on the cell grid) + k_knn_replay (PointType_CMP-ambiguous queries on the ikd-Tree)")
+B_QUERY_REF = 12 + 5 * 8
 
 
 def parse():
@@ -66,28 +68,148 @@ def parse():
     ap.add_argument("--map-points", type=int, default=1_000_000)
     ap.add_argument("--max-iter", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0: skip)")
-    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01_pmc_summary_v4.json"))
+    ap.add_argument("--legs", default="all", help="comma list: headline,latency,config5,ikfom,ivox,ikd,vio (all)")
+    ap.add_argument("--pmc", default="auto", choices=("auto", "off"),
+                    help="rocprofv3 PMC passes for roofline.traffic (rank 0, N = 1 only)")
     return ap.parse_args()
 
 
+# ----------------------------------------------------------------- ranks ----
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(a) -> int:
+    """--gpus N without a launcher: start N rank processes (no GPU call here)."""
+    n = a.gpus
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        # rank 0's stdout is this process's (the JSON line); the others' go to stderr
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else sys.stderr))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            c = p.poll()
+            if c is None:
+                continue
+            procs.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for q in procs:  # a failed rank leaves the others at a barrier
+                    q.kill()
+        time.sleep(0.05)
+    return rc
+
+
+def host_threads() -> int:
+    """Cores this job may use: the affinity set, capped by the cgroup CPU quota."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except Exception:
+        pass
+    return n
+
+
+# ------------------------------------------------------------------- PMC ----
+PMC_PASSES = (("FETCH_SIZE",), ("WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"),
+              ("SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_BUSY_CYCLES"))
+
+
+def pmc_traffic(a, kernel_key: str):
+    """rocprofv3 --pmc passes over tools/knn_probe.py (same map, scans and batch
+    as the headline), one child process per pass (MI355X_MICROARCH.md §rocprofv3
+    PMC slots): HBM bytes per first-evaluation k-NN of a batch = the unit
+    kernel's dispatches x (2 x FETCH_SIZE + WRITE_SIZE) (FETCH_SIZE doubled on
+    gfx950, §HBM), plus its L2 hit rate and wait share.  None if unavailable."""
+    prof = shutil.which("rocprofv3")
+    if a.pmc == "off" or not prof:
+        return None
+    import collections
+    import csv
+    import glob
+    import tempfile
+    out = tempfile.mkdtemp(prefix="livo_pmc_")
+    per = collections.defaultdict(list)
+    for k, counters in enumerate(PMC_PASSES):
+        d = os.path.join(out, f"pass{k}")
+        cmd = ["timeout", "-s", "KILL", "120", prof, "--pmc", *counters, "-d", d, "-o", "pmc", "--output-format",
+               "csv", "--", sys.executable, os.path.join(ROOT, "tools", "knn_probe.py"), "--scan-points",
+               str(a.scan_points), "--map-points", str(a.map_points), "--batch", str(a.batch)]
+        r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+        if r.returncode != 0:
+            sys.stderr.write(f"pmc pass {counters} failed ({r.returncode}): {r.stderr[-400:]}\n")
+            return None
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            acc = collections.defaultdict(float)
+            for row in csv.DictReader(open(f)):
+                if kernel_key in row["Kernel_Name"]:
+                    acc[(row["Dispatch_Id"], row["Counter_Name"])] += float(row["Counter_Value"])
+            for (_, cname), v in acc.items():
+                per[cname].append(v)
+    shutil.rmtree(out, ignore_errors=True)
+    mean = {k: sum(v) / len(v) for k, v in per.items() if v}
+    if "FETCH_SIZE" not in mean or "WRITE_SIZE" not in mean:
+        return None
+    disp = len(per["FETCH_SIZE"])
+    groups = min(4, a.batch)  # one first-search dispatch per stream group and batch
+    res = {"hbm_bytes_per_launch": groups * (2 * mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024,
+           "fetch_kib_per_dispatch": round(mean["FETCH_SIZE"], 1), "write_kib_per_dispatch": round(mean["WRITE_SIZE"], 1),
+           "dispatches_sampled": disp}
+    if mean.get("TCC_HIT_sum") is not None and mean.get("TCC_MISS_sum"):
+        res["l2_hit_rate"] = round(mean["TCC_HIT_sum"] / (mean["TCC_HIT_sum"] + mean["TCC_MISS_sum"]), 4)
+    if mean.get("SQ_WAVE_CYCLES"):
+        res["wait_any_share"] = round(mean.get("SQ_WAIT_ANY", 0.0) / mean["SQ_WAVE_CYCLES"], 4)
+    return res
+
+
+# ------------------------------------------------------------------ main ----
 def main():
     a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(launch_ranks(a))
+    if world > 1 and a.gpus != world:
+        sys.stderr.write(f"note: --gpus {a.gpus} but WORLD_SIZE {world}; {world} ranks run\n")
+    legs = set(a.legs.split(",")) if a.legs != "all" else {"headline", "latency", "config5", "ikfom", "ivox", "ikd",
+                                                           "vio"}
     import livo_amd
     from livo_amd import farm, synth
 
-    rank, local_rank, world = farm.dist_env()
+    # inputs (identical generator on every rank; each rank its own scans), made
+    # before any GPU call so that the PMC children find the map in the cache
+    m = synth.cached_map(a.map_points)
+    scan_ids = [rank * a.batch + j for j in range(a.batch)]
+    scans = [synth.make_scan(a.scan_points, s)[0] for s in scan_ids]
+    st0 = [synth.make_state(s) for s in scan_ids]
+    kind = os.environ.get("LIVO_KNN_KIND", "grid")
+    unit_kernel = {"leaf": "k_knn_leaf<false>", "grid": "k_knn_grid<false>"}.get(kind, "k_knn_grid<false>")
+    pmc = pmc_traffic(a, unit_kernel) if (rank == 0 and world == 1) else None
+
     import torch
     import torch.distributed as dist
 
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     torch_dev = None
     device = local_rank
+    ndev = torch.cuda.device_count()
     if torch.cuda.is_available():
         # one process per GPU; more ranks than GPUs (a rehearsal on a 1-GPU box) share them
-        device = local_rank % max(1, torch.cuda.device_count())
+        device = local_rank % max(1, ndev)
         torch.cuda.set_device(device)
         torch_dev = torch.device("cuda", device)
-    # RCCL (backend "nccl") over xGMI on the GPU node; LIVO_BENCH_BACKEND=gloo for rehearsals
-    backend = os.environ.get("LIVO_BENCH_BACKEND") or ("nccl" if torch_dev is not None else "gloo")
+    # RCCL (backend "nccl") over xGMI; gloo when ranks share a GPU (RCCL refuses that) or on request
+    backend = os.environ.get("LIVO_BENCH_BACKEND") or ("nccl" if torch_dev is not None and ndev >= world else "gloo")
     coll_dev = torch_dev if backend == "nccl" else None
     if world > 1:
         dist.init_process_group(backend)
@@ -100,20 +222,14 @@ def main():
         if torch_dev is not None:
             torch.cuda.synchronize()
 
-    # ---- inputs (identical generator on every rank; each rank its own scans)
-    m = synth.cached_map(a.map_points)
-    scan_ids = [rank * a.batch + j for j in range(a.batch)]
-    scans = [synth.make_scan(a.scan_points, s)[0] for s in scan_ids]
-    st0 = [synth.make_state(s) for s in scan_ids]
-
     ctx = livo_amd.Context(device, t_LI=synth.T_LI, max_iterations=a.max_iter)
     t = time.time()
     ctx.map_build(m)
     map_build_s = time.time() - t
     sids = [ctx.scan_upload(s) for s in scans]
     # V_ref: nodes the reference traversal visits for the first search of these
-    # scans (an unseeded full pass, identical to KD_TREE::Search's order, outside
-    # the timed region); the algorithmic bytes of the roofline are priced on it
+    # scans (the reference-order pass k_knn_pass, outside the timed region):
+    # the reference-equivalent pricing of SURVEY.md §8d
     v_ref = sum(ctx.h_share(sid, s, search_en=True)["visits"] for sid, s in zip(sids, st0))
     init = (livo_amd.State * a.batch)(*[livo_amd.state_to_c(s) for s in st0])
     work = (livo_amd.State * a.batch)()
@@ -135,7 +251,7 @@ def main():
     # from extra untimed steps below
     ctx.set_profiling(1)
     knn_ms = 0.0
-    knn_launches = knn_visits = knn_queries = knn_effct = replays = 0
+    knn_launches = knn_visits = knn_points = knn_queries = replays = 0
     sync()
     barrier()
     sync()
@@ -147,8 +263,8 @@ def main():
         knn_ms += tm["knn_ms"]
         knn_launches += tm["knn_launches"]
         knn_visits += tm["knn_visits"]
+        knn_points += tm["knn_points"]
         knn_queries += tm["knn_queries"]
-        knn_effct += tm["effct_points"]
         replays += tm["knn_replays"]
     sync()
     barrier()
@@ -157,37 +273,45 @@ def main():
     # per-stage device time (summed over the concurrent stream groups), untimed
     ctx.set_profiling(2)
     n_prof = 10
-    t_first = t_rematch = t_plane = t_solve = 0.0
+    t_first = t_rematch = t_plane = 0.0
     for _ in range(n_prof):
         step()
         tm = ctx.last_timings()
         t_first += tm["knn_ms"]
         t_rematch += tm["rematch_knn_ms"]
         t_plane += tm["plane_ms"]
-        t_solve += tm["solve_ms"]
     ctx.set_profiling(0)
     counters.knn_visits, counters.knn_queries = knn_visits, knn_queries
     elapsed_max = farm.allreduce_max(elapsed, coll_dev)
     total = farm.allreduce_counters(counters, coll_dev)
 
-    # ---- roofline of the dominant kernels (rank-local): the first-evaluation
-    # k-NN of one batch (pilot + pilot-seeded passes + replays, both streams)
-    launch_ms = knn_ms / max(knn_launches, 1)
-    queries_per_launch = knn_queries / max(knn_launches, 1)
-    bytes_per_launch = v_ref * B_NODE + queries_per_launch * B_QUERY
-    achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
-    traffic = None
-    try:
-        with open(a.pmc_summary) as f:
-            pmc = json.load(f)
-        if pmc.get("workload") == f"{a.scan_points}x{a.batch}@{a.map_points}":
-            traffic = pmc.get("hbm_bytes_per_launch")
-    except Exception:
-        pass
+    # roofline of the dominant kernel (rank-local): the first-evaluation k-NN of
+    # one batch (4 concurrent stream-group dispatches + their replays)
+    L = max(knn_launches, 1)
+    launch_ms = knn_ms / L
+    q_launch = knn_queries / L
+    alg_bytes = (knn_visits / L) * B_SLOT + (knn_points / L) * B_POINT + q_launch * B_QUERY_IO
+    achieved = alg_bytes / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
+    ref_equiv = (v_ref * B_NODE + q_launch * B_QUERY_REF) / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
 
     result = None
     if rank == 0:
         value = total.scans / elapsed_max
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": round(pmc["hbm_bytes_per_launch"]) if pmc else None,
+                "kernel": f"first-evaluation k-NN of the batch: {min(4, a.batch)} concurrent {unit_kernel} dispatches "
+                          "(one per stream group: transform + exact 5-NN of every point) + their tie replays",
+                "avg_launch_ms": round(launch_ms, 4),
+                "alg_bytes_per_launch": int(alg_bytes),
+                "alg_bytes_terms": {"slots_per_query": round(knn_visits / max(knn_queries, 1), 3),
+                                    "points_per_query": round(knn_points / max(knn_queries, 1), 2),
+                                    "bytes_per_query": round(alg_bytes / max(q_launch, 1), 1)},
+                "limiter": "dependent-load latency (map and grid L2/MALL-resident)",
+                "reference_equivalent_GBps": round(ref_equiv, 1),
+                "visits_per_query_ref": round(v_ref / max(q_launch, 1), 3)}
+        if pmc:
+            roof["pmc"] = {k: v for k, v in pmc.items() if k != "hbm_bytes_per_launch"}
         result = {
             "metric": "IEKF scan-to-map updates/sec (100k-pt scan, 1M-pt map)",
             "value": round(value, 3),
@@ -205,18 +329,14 @@ def main():
                                    f"{'M' if a.map_points >= 1000000 else ''}-pt map, max_iteration={a.max_iter}, "
                                    f"{a.batch} independent scans per GPU per step",
                        "scan_points": a.scan_points, "map_points": a.map_points, "max_iteration": a.max_iter,
-                       "scans_per_step_per_gpu": a.batch, "parallelism": f"scan farm x{world}"},
+                       "scans_per_step_per_gpu": a.batch, "parallelism": f"scan farm x{world}",
+                       "collective": backend if world > 1 else None},
+            "total_scans": total.scans,
             "iekf_steps_per_s": round(total.evals / elapsed_max, 3),
             "knn_queries_per_s": round((total.knn_passes * a.scan_points) / elapsed_max, 1),
             "evals_per_scan": round(total.evals / max(total.scans, 1), 3),
             "knn_passes_per_scan": round(total.knn_passes / max(total.scans, 1), 3),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": knn_kernel_desc(),
-                         "avg_launch_ms": round(launch_ms, 4),
-                         "alg_bytes_per_launch": int(bytes_per_launch),
-                         "visits_per_query_ref": round(v_ref / max(queries_per_launch, 1), 3),
-                         "visits_per_query_gpu": round(knn_visits / max(knn_queries, 1), 3)},
+            "roofline": roof,
             "device_ms_per_step": {"knn_first": round(t_first / n_prof, 4), "knn_rematch": round(t_rematch / n_prof, 4),
                                    "plane_H_solve": round(t_plane / n_prof, 4),
                                    "note": f"{n_prof} extra untimed steps with per-stage events; stages other than "
@@ -225,205 +345,281 @@ def main():
             "map_build_s": round(map_build_s, 3),
         }
 
-    # ---- the IKFoM formulation on the same scans: throughput
-    # of livo_ikfom_update_batch (extra steps, not part of `value`)
-    ik_init = (livo_amd.IkfomState * a.batch)(*[livo_amd.ikfom_to_c(synth.make_ikfom_state(s)) for s in scan_ids])
-    ik_work = (livo_amd.IkfomState * a.batch)()
-    ik_bytes = C.sizeof(ik_init)
-
-    def ik_step():
-        C.memmove(ik_work, ik_init, ik_bytes)
-        return ctx.ikfom_update_batch(sids, ik_work, raw=True)[1]
-
-    for _ in range(2):
-        ik_step()
-    ik_steps = max(5, a.steps // 2)
-    sync()
-    t = time.perf_counter()
-    ik_evals = 0
-    for _ in range(ik_steps):
-        ik_evals += sum(s.iterations for s in ik_step())
-    sync()
-    ik_elapsed = farm.allreduce_max(time.perf_counter() - t, coll_dev)
-    ik_total = farm.allreduce_counters(farm.Counters(scans=ik_steps * a.batch, evals=ik_evals), coll_dev)
-    ik_first = livo_amd.ikfom_stats_from_c(ik_step()[0])
-    if rank == 0:
-        result["ikfom"] = {"updates_per_s": round(ik_total.scans / ik_elapsed, 3),
-                           "ms_per_step": round(ik_elapsed / ik_steps * 1e3, 4),
-                           "evals_per_scan": round(ik_total.evals / max(ik_total.scans, 1), 3),
-                           "note": "livo_ikfom_update_batch (state_ikfom, esekfom.hpp:1619-1928) on the same "
-                                   f"{a.batch} scans per GPU, {ik_steps} steps after the headline run"}
-
-    # ---- the iVox backend (the reference's default build):
-    # the same scans against the same 1M points inserted with IVox::AddPoints,
-    # then a sequential odometry loop (scan update + map_incremental per scan)
-    ctx.set_backend(livo_amd.BACKEND_IVOX)
-    t = time.perf_counter()
-    ctx.ivox_init()
-    ctx.ivox_add_points(m)
-    iv_build_s = time.perf_counter() - t
-    iv_info = ctx.ivox_info()
-    # fresh scan buffers: a point without iVox candidates keeps its cached
-    # neighbours (ivox3d.h:165-167), so the first update starts from empty caches
-    iv_sids = [ctx.scan_upload(sc) for sc in scans]
-
-    def iv_step():
-        C.memmove(work, init, nbytes)
-        return ctx.iekf_update_batch(iv_sids, work, raw=True)[1]
-
-    iv_first = [livo_amd.stats_from_c(s) for s in iv_step()]
-    for _ in range(2):
-        iv_step()
-    iv_steps = max(5, a.steps // 2)
-    sync()
-    t = time.perf_counter()
-    iv_evals = 0
-    for _ in range(iv_steps):
-        iv_evals += sum(s.iterations for s in iv_step())
-    sync()
-    iv_elapsed = farm.allreduce_max(time.perf_counter() - t, coll_dev)
-    iv_total = farm.allreduce_counters(farm.Counters(scans=iv_steps * a.batch, evals=iv_evals), coll_dev)
-    # odometry: one scan after the other, each updated then merged into the map
-    odo_sids = [ctx.scan_upload(sc) for sc in scans]
-    sync()
-    t = time.perf_counter()
-    t_incr = 0.0
-    added = 0
-    for sid, s in zip(odo_sids, st0):
-        st, _ = ctx.iekf_update(sid, s)
-        t1 = time.perf_counter()
-        _, cnt = ctx.map_incremental(sid, st, filter_size_map=0.5)
-        t_incr += time.perf_counter() - t1
-        added += cnt["added"] + cnt["no_downsample"]
-    sync()
-    odo_elapsed = time.perf_counter() - t
-    for sid in odo_sids + iv_sids:
-        ctx.scan_release(sid)
-    # the whole per-frame pipeline on the device: raw
-    # 100k-point frame -> UndistortPcl de-skew + VoxelGrid (filter_size_surf
-    # 0.5, livo_scan_preprocess) -> IEKF update (iVox) -> map_incremental
-    raws = [synth.make_raw_scan(a.scan_points, s) for s in scan_ids]
-    n_down = 0
-    t_pre = t_upd = t_inc = 0.0
-    prev = None
-    for rep in range(2):  # first pass warms the allocations
-        t_pre = t_upd = t_inc = 0.0
+    # ---- the drop-in regime: one scan at a time through livo_iekf_update (the
+    # facade's iterate()), resident scan; and with livo_scan_upload of the
+    # host points (Morton order on the device) inside the timed region
+    if "latency" in legs:
+        one = (livo_amd.State * 1)()
+        for _ in range(2):
+            for j in range(a.batch):
+                C.memmove(one, C.byref(init, j * C.sizeof(livo_amd.State)), C.sizeof(livo_amd.State))
+                ctx.iekf_update_batch([sids[j]], one, raw=True)
+        reps = max(2, a.steps // a.batch) * a.batch
         sync()
         t = time.perf_counter()
-        for (raw, poses, Re, pe), s in zip(raws, st0):
-            t1 = time.perf_counter()
-            sid, _, down = ctx.scan_preprocess(raw, poses, Re, pe, leaf_size=0.5)
-            t2 = time.perf_counter()
-            if prev is not None:
-                ctx.scan_inherit_neighbors(sid, prev)
-                ctx.scan_release(prev)
-            st, _ = ctx.iekf_update(sid, s)
-            t3 = time.perf_counter()
-            ctx.map_incremental(sid, st, filter_size_map=0.5)
-            t4 = time.perf_counter()
-            t_pre += t2 - t1
-            t_upd += t3 - t2
-            t_inc += t4 - t3
-            n_down += len(down)
-            prev = sid
+        for k in range(reps):
+            j = k % a.batch
+            C.memmove(one, C.byref(init, j * C.sizeof(livo_amd.State)), C.sizeof(livo_amd.State))
+            ctx.iekf_update_batch([sids[j]], one, raw=True)
         sync()
-        pipe_elapsed = time.perf_counter() - t
-    ctx.scan_release(prev)
-    ctx.set_backend(livo_amd.BACKEND_IKDTREE)
-    if rank == 0:
-        result["ivox"] = {
-            "updates_per_s": round(iv_total.scans / iv_elapsed, 3),
-            "ms_per_step": round(iv_elapsed / iv_steps * 1e3, 4),
-            "evals_per_scan": round(iv_total.evals / max(iv_total.scans, 1), 3),
-            "effct_first_eval_scan0": iv_first[0]["effct_feat_num"][0],
-            "map": {"points": iv_info["num_points"], "grids": iv_info["num_grids"],
-                    "max_grid_points": iv_info["max_grid_points"], "add_points_s": round(iv_build_s, 3)},
-            "odometry": {"scans_per_s": round(len(odo_sids) / odo_elapsed, 3),
-                         "ms_per_scan": round(odo_elapsed / len(odo_sids) * 1e3, 3),
-                         "map_incremental_ms_per_scan": round(t_incr / len(odo_sids) * 1e3, 3),
-                         "points_added_per_scan": round(added / len(odo_sids), 1),
-                         "note": "sequential: livo_iekf_update + livo_map_incremental per scan (map grows)"},
-            "pipeline": {"frames_per_s": round(len(raws) / pipe_elapsed, 3),
-                         "ms_per_frame": round(pipe_elapsed / len(raws) * 1e3, 3),
-                         "preprocess_ms": round(t_pre / len(raws) * 1e3, 3),
-                         "iekf_ms": round(t_upd / len(raws) * 1e3, 3),
-                         "map_incremental_ms": round(t_inc / len(raws) * 1e3, 3),
-                         "points_after_voxel_grid": round(n_down / (2 * len(raws)), 1),
-                         "note": f"raw {a.scan_points // 1000}k-pt frame with 21 IMU poses -> livo_scan_preprocess "
-                                 "(de-skew + VoxelGrid 0.5 m) -> livo_iekf_update (iVox) -> livo_map_incremental, "
-                                 "host-timed per call (includes the host<->device copies of the raw frame)"},
-            "note": "LIVO_BACKEND_IVOX: IVox GetClosestPoint (NEARBY18, 0.2 m grids, 5 m range) on the same "
-                    f"{a.batch} scans per GPU, {iv_steps} steps after the IKFoM run; not part of `value`"}
+        lat = (time.perf_counter() - t) / reps
+        sync()
+        t = time.perf_counter()
+        for k in range(a.batch):
+            C.memmove(one, C.byref(init, k * C.sizeof(livo_amd.State)), C.sizeof(livo_amd.State))
+            sid = ctx.scan_upload(scans[k])
+            ctx.iekf_update_batch([sid], one, raw=True)
+            ctx.scan_release(sid)
+        sync()
+        lat_up = (time.perf_counter() - t) / a.batch
+        if rank == 0:
+            result["drop_in"] = {"ms_per_scan": round(lat * 1e3, 4), "updates_per_s": round(1.0 / lat, 2),
+                                 "ms_per_scan_with_upload": round(lat_up * 1e3, 4),
+                                 "note": "batch 1, sequential: livo_iekf_update on a resident scan; then "
+                                         "livo_scan_upload (host points -> HBM, device Morton sort) + update + "
+                                         "release per scan, host-timed"}
+
+    # ---- config 5 (BASELINE configs[4]): 10M-point map, 200k-point scans, the
+    # HBM-bound stress case (the map no longer fits the 256 MB MALL)
+    if "config5" in legs and a.map_points == 1_000_000:
+        m5 = synth.cached_map(10_000_000)
+        c5 = livo_amd.Context(device, t_LI=synth.T_LI, max_iterations=a.max_iter)
+        t = time.time()
+        c5.map_build(m5)
+        b5 = time.time() - t
+        del m5
+        n5 = min(a.batch, 8)
+        s5 = [c5.scan_upload(synth.make_scan(200_000, 1000 + s)[0]) for s in scan_ids[:n5]]
+        i5 = (livo_amd.State * n5)(*[livo_amd.state_to_c(synth.make_state(1000 + s)) for s in scan_ids[:n5]])
+        w5 = (livo_amd.State * n5)()
+
+        def step5():
+            C.memmove(w5, i5, C.sizeof(i5))
+            return c5.iekf_update_batch(s5, w5, raw=True)[1]
+
+        step5()
+        c5.set_profiling(1)
+        k5 = max(3, a.steps // 4)
+        kms = kv = kp = kq = 0
+        ev5 = 0
+        sync()
+        t = time.perf_counter()
+        for _ in range(k5):
+            st5 = step5()
+            ev5 += sum(s.iterations for s in st5)
+            tm = c5.last_timings()
+            kms += tm["knn_ms"]; kv += tm["knn_visits"]; kp += tm["knn_points"]; kq += tm["knn_queries"]
+        sync()
+        e5 = time.perf_counter() - t
+        c5.set_profiling(0)
+        lm = kms / k5
+        ab = (kv / k5) * B_SLOT + (kp / k5) * B_POINT + (kq / k5) * B_QUERY_IO
+        if rank == 0:
+            result["config5"] = {"updates_per_s": round(k5 * n5 / e5, 3), "ms_per_step": round(e5 / k5 * 1e3, 4),
+                                 "evals_per_scan": round(ev5 / (k5 * n5), 3), "map_build_s": round(b5, 2),
+                                 "knn_first_ms": round(lm, 4), "knn_alg_bytes_per_launch": int(ab),
+                                 "knn_achieved_GBps": round(ab / (lm * 1e-3) / 1e9, 1) if lm > 0 else None,
+                                 "points_per_query": round(kp / max(kq, 1), 2),
+                                 "note": f"10M-pt map, {n5} x 200k-pt scans per step, max_iteration={a.max_iter}; "
+                                         "rocprofv3 capture in profiles/ (r02_config5_*)"}
+        c5.close()
+
+    # ---- the IKFoM formulation on the same scans
+    if "ikfom" in legs:
+        ik_init = (livo_amd.IkfomState * a.batch)(*[livo_amd.ikfom_to_c(synth.make_ikfom_state(s)) for s in scan_ids])
+        ik_work = (livo_amd.IkfomState * a.batch)()
+        ik_bytes = C.sizeof(ik_init)
+
+        def ik_step():
+            C.memmove(ik_work, ik_init, ik_bytes)
+            return ctx.ikfom_update_batch(sids, ik_work, raw=True)[1]
+
+        for _ in range(2):
+            ik_step()
+        ik_steps = max(5, a.steps // 2)
+        sync()
+        t = time.perf_counter()
+        ik_evals = 0
+        for _ in range(ik_steps):
+            ik_evals += sum(s.iterations for s in ik_step())
+        sync()
+        ik_elapsed = farm.allreduce_max(time.perf_counter() - t, coll_dev)
+        ik_total = farm.allreduce_counters(farm.Counters(scans=ik_steps * a.batch, evals=ik_evals), coll_dev)
+        ik_first = livo_amd.ikfom_stats_from_c(ik_step()[0])
+        if rank == 0:
+            result["ikfom"] = {"updates_per_s": round(ik_total.scans / ik_elapsed, 3),
+                               "ms_per_step": round(ik_elapsed / ik_steps * 1e3, 4),
+                               "evals_per_scan": round(ik_total.evals / max(ik_total.scans, 1), 3),
+                               "note": "livo_ikfom_update_batch (state_ikfom, esekfom.hpp:1619-1928) on the same "
+                                       f"{a.batch} scans per GPU, {ik_steps} steps after the headline run"}
+
+    # ---- the iVox backend (the reference's default build)
+    if "ivox" in legs:
+        ctx.set_backend(livo_amd.BACKEND_IVOX)
+        t = time.perf_counter()
+        ctx.ivox_init()
+        ctx.ivox_add_points(m)
+        iv_build_s = time.perf_counter() - t
+        iv_info = ctx.ivox_info()
+        # fresh scan buffers: a point without iVox candidates keeps its cached
+        # neighbours (ivox3d.h:165-167), so the first update starts from empty caches
+        iv_sids = [ctx.scan_upload(sc) for sc in scans]
+
+        def iv_step():
+            C.memmove(work, init, nbytes)
+            return ctx.iekf_update_batch(iv_sids, work, raw=True)[1]
+
+        iv_first = [livo_amd.stats_from_c(s) for s in iv_step()]
+        for _ in range(2):
+            iv_step()
+        iv_steps = max(5, a.steps // 2)
+        sync()
+        t = time.perf_counter()
+        iv_evals = 0
+        for _ in range(iv_steps):
+            iv_evals += sum(s.iterations for s in iv_step())
+        sync()
+        iv_elapsed = farm.allreduce_max(time.perf_counter() - t, coll_dev)
+        iv_total = farm.allreduce_counters(farm.Counters(scans=iv_steps * a.batch, evals=iv_evals), coll_dev)
+        # odometry: one scan after the other, each updated then merged into the map
+        odo_sids = [ctx.scan_upload(sc) for sc in scans]
+        sync()
+        t = time.perf_counter()
+        t_incr = 0.0
+        added = 0
+        for sid, s in zip(odo_sids, st0):
+            st, _ = ctx.iekf_update(sid, s)
+            t1 = time.perf_counter()
+            _, cnt = ctx.map_incremental(sid, st, filter_size_map=0.5)
+            t_incr += time.perf_counter() - t1
+            added += cnt["added"] + cnt["no_downsample"]
+        sync()
+        odo_elapsed = time.perf_counter() - t
+        for sid in odo_sids + iv_sids:
+            ctx.scan_release(sid)
+        # the whole per-frame pipeline on the device: raw
+        # 100k-point frame -> UndistortPcl de-skew + VoxelGrid (filter_size_surf
+        # 0.5, livo_scan_preprocess) -> IEKF update (iVox) -> map_incremental
+        raws = [synth.make_raw_scan(a.scan_points, s) for s in scan_ids]
+        n_down = 0
+        prev = None
+        for rep in range(2):  # first pass warms the allocations
+            t_pre = t_upd = t_inc = 0.0
+            sync()
+            t = time.perf_counter()
+            for (raw, poses, Re, pe), s in zip(raws, st0):
+                t1 = time.perf_counter()
+                sid, _, down = ctx.scan_preprocess(raw, poses, Re, pe, leaf_size=0.5)
+                t2 = time.perf_counter()
+                if prev is not None:
+                    ctx.scan_inherit_neighbors(sid, prev)
+                    ctx.scan_release(prev)
+                st, _ = ctx.iekf_update(sid, s)
+                t3 = time.perf_counter()
+                ctx.map_incremental(sid, st, filter_size_map=0.5)
+                t4 = time.perf_counter()
+                t_pre += t2 - t1
+                t_upd += t3 - t2
+                t_inc += t4 - t3
+                n_down += len(down)
+                prev = sid
+            sync()
+            pipe_elapsed = time.perf_counter() - t
+        ctx.scan_release(prev)
+        ctx.set_backend(livo_amd.BACKEND_IKDTREE)
+        if rank == 0:
+            result["ivox"] = {
+                "updates_per_s": round(iv_total.scans / iv_elapsed, 3),
+                "ms_per_step": round(iv_elapsed / iv_steps * 1e3, 4),
+                "evals_per_scan": round(iv_total.evals / max(iv_total.scans, 1), 3),
+                "effct_first_eval_scan0": iv_first[0]["effct_feat_num"][0],
+                "map": {"points": iv_info["num_points"], "grids": iv_info["num_grids"],
+                        "max_grid_points": iv_info["max_grid_points"], "add_points_s": round(iv_build_s, 3)},
+                "odometry": {"scans_per_s": round(len(odo_sids) / odo_elapsed, 3),
+                             "ms_per_scan": round(odo_elapsed / len(odo_sids) * 1e3, 3),
+                             "map_incremental_ms_per_scan": round(t_incr / len(odo_sids) * 1e3, 3),
+                             "points_added_per_scan": round(added / len(odo_sids), 1),
+                             "note": "sequential: livo_iekf_update + livo_map_incremental per scan (map grows)"},
+                "pipeline": {"frames_per_s": round(len(raws) / pipe_elapsed, 3),
+                             "ms_per_frame": round(pipe_elapsed / len(raws) * 1e3, 3),
+                             "preprocess_ms": round(t_pre / len(raws) * 1e3, 3),
+                             "iekf_ms": round(t_upd / len(raws) * 1e3, 3),
+                             "map_incremental_ms": round(t_inc / len(raws) * 1e3, 3),
+                             "points_after_voxel_grid": round(n_down / (2 * len(raws)), 1),
+                             "note": f"raw {a.scan_points // 1000}k-pt frame with 21 IMU poses -> livo_scan_preprocess "
+                                     "(de-skew + VoxelGrid 0.5 m) -> livo_iekf_update (iVox) -> livo_map_incremental, "
+                                     "host-timed per call (includes the host<->device copies of the raw frame)"},
+                "note": "LIVO_BACKEND_IVOX: IVox GetClosestPoint (NEARBY18, 0.2 m grids, 5 m range) on the same "
+                        f"{a.batch} scans per GPU, {iv_steps} steps; not part of `value`"}
 
     # ---- the ikd-Tree incremental map (the USE_ikdtree
-    # branch of map_incremental): sequential odometry on a second context --
-    # per scan the IEKF update, then Add_Points(feats_down_world, true) at the
-    # updated state (filter_size_map 0.5) into the 1M-point map, which grows
-    ik_ctx = livo_amd.Context(device, t_LI=synth.T_LI, max_iterations=a.max_iter)
-    ik_ctx.map_build(m)
-    ikd_rows = []
-    for rep in range(2):  # the first pass warms the allocations and activates the incremental map
-        ik_sids = [ik_ctx.scan_upload(sc) for sc in scans]
-        t_upd = t_add = 0.0
-        events = added = deleted = 0
-        sync()
-        t = time.perf_counter()
-        for sid, s in zip(ik_sids, st0):
-            t1 = time.perf_counter()
-            stn, _ = ik_ctx.iekf_update(sid, s)
-            t2 = time.perf_counter()
-            _, ast = ik_ctx.map_incremental(sid, stn, filter_size_map=0.5)
-            t3 = time.perf_counter()
-            t_upd += t2 - t1
-            t_add += t3 - t2
-            events += ast["events"]
-            added += ast["added"]
-            deleted += ast["deleted"]
-        sync()
-        ikd_elapsed = time.perf_counter() - t
-        for sid in ik_sids:
-            ik_ctx.scan_release(sid)
-        ikd_rows.append((ikd_elapsed, t_upd, t_add, events, added, deleted))
-    ikd_elapsed, t_upd, t_add, events, added, deleted = ikd_rows[-1]
-    if rank == 0:
-        nsc = len(scans)
-        result["ikd_incremental"] = {
-            "scans_per_s": round(nsc / ikd_elapsed, 3),
-            "iekf_ms_per_scan": round(t_upd / nsc * 1e3, 3),
-            "add_points_ms_per_scan": round(t_add / nsc * 1e3, 3),
-            "add_points_events_per_scan": round(events / nsc, 1),
-            "points_added_per_scan": round(added / nsc, 1),
-            "points_deleted_per_scan": round(deleted / nsc, 1),
-            "map_points_after": ik_ctx.map_info()["num_points"],
-            "note": f"sequential odometry on the {a.map_points}-pt map: livo_iekf_update + livo_map_incremental "
-                    "(ikd-Tree backend: KD_TREE::Add_Points of all scan points, downsample 0.5 m) per scan, "
-                    "second pass over the scans (the map has grown), host-timed; not part of `value`"}
-    ik_ctx.close()
+    # branch of map_incremental): sequential odometry on a second context
+    if "ikd" in legs:
+        ik_ctx = livo_amd.Context(device, t_LI=synth.T_LI, max_iterations=a.max_iter)
+        ik_ctx.map_build(m)
+        ikd_rows = []
+        for rep in range(2):  # the first pass warms the allocations and activates the incremental map
+            ik_sids = [ik_ctx.scan_upload(sc) for sc in scans]
+            t_upd = t_add = 0.0
+            events = added = deleted = 0
+            sync()
+            t = time.perf_counter()
+            for sid, s in zip(ik_sids, st0):
+                t1 = time.perf_counter()
+                stn, _ = ik_ctx.iekf_update(sid, s)
+                t2 = time.perf_counter()
+                _, ast = ik_ctx.map_incremental(sid, stn, filter_size_map=0.5)
+                t3 = time.perf_counter()
+                t_upd += t2 - t1
+                t_add += t3 - t2
+                events += ast["events"]
+                added += ast["added"]
+                deleted += ast["deleted"]
+            sync()
+            ikd_elapsed = time.perf_counter() - t
+            for sid in ik_sids:
+                ik_ctx.scan_release(sid)
+            ikd_rows.append((ikd_elapsed, t_upd, t_add, events, added, deleted))
+        ikd_elapsed, t_upd, t_add, events, added, deleted = ikd_rows[-1]
+        if rank == 0:
+            nsc = len(scans)
+            result["ikd_incremental"] = {
+                "scans_per_s": round(nsc / ikd_elapsed, 3),
+                "iekf_ms_per_scan": round(t_upd / nsc * 1e3, 3),
+                "add_points_ms_per_scan": round(t_add / nsc * 1e3, 3),
+                "add_points_events_per_scan": round(events / nsc, 1),
+                "points_added_per_scan": round(added / nsc, 1),
+                "points_deleted_per_scan": round(deleted / nsc, 1),
+                "map_points_after": ik_ctx.map_info()["num_points"],
+                "note": f"sequential odometry on the {a.map_points}-pt map: livo_iekf_update + livo_map_incremental "
+                        "(ikd-Tree backend: KD_TREE::Add_Points of all scan points, downsample 0.5 m) per scan, "
+                        "second pass over the scans (the map has grown), host-timed; not part of `value`"}
+        ik_ctx.close()
 
-    # ---- the VIO photometric update: frames per second
-    # at the reference's size (a 40-px grid on 640x512: <= 192 visual points)
-    # and at 20k points; not part of `value`
-    vio = {}
+    # ---- the VIO photometric update
     vio_frames = {}
-    for nv in (192, 20000):
-        fr, vst, _ = synth.make_vio_frame(nv, 100 + rank)
-        vio_frames[nv] = (fr, vst)
-        ctx.vio_update(fr, vst)  # warm-up
-        reps = 20 if nv < 1000 else 10
-        sync()
-        t = time.perf_counter()
-        for _ in range(reps):
-            _, vstats, _ = ctx.vio_update(fr, vst)
-        sync()
-        dt = (time.perf_counter() - t) / reps
-        vio[str(len(fr["pos"]))] = {"frames_per_s": round(1.0 / dt, 2), "ms_per_frame": round(dt * 1e3, 4),
-                                    "iterations_per_level": vstats["iterations"]}
-    if rank == 0:
-        result["vio"] = {"by_points": vio,
-                         "note": "livo_vio_update (LidarSelector::ComputeJ/UpdateState, patch 4x4, 3 levels, "
-                                 "max_iteration 4) on synthetic 640x512 frames, host-timed incl. the frame upload"}
+    if "vio" in legs:
+        vio = {}
+        for nv in (192, 20000):
+            fr, vst, _ = synth.make_vio_frame(nv, 100 + rank)
+            vio_frames[nv] = (fr, vst)
+            ctx.vio_update(fr, vst)  # warm-up
+            reps = 20 if nv < 1000 else 10
+            sync()
+            t = time.perf_counter()
+            for _ in range(reps):
+                _, vstats, _ = ctx.vio_update(fr, vst)
+            sync()
+            dt = (time.perf_counter() - t) / reps
+            vio[str(len(fr["pos"]))] = {"frames_per_s": round(1.0 / dt, 2), "ms_per_frame": round(dt * 1e3, 4),
+                                        "iterations_per_level": vstats["iterations"]}
+        if rank == 0:
+            result["vio"] = {"by_points": vio,
+                             "note": "livo_vio_update (LidarSelector::ComputeJ/UpdateState, patch 4x4, 3 levels, "
+                                     "max_iteration 4) on synthetic 640x512 frames, host-timed incl. the frame upload"}
 
-    # ---- CPU baseline: the oracle (CPU restatement), 1 thread, bounded sample; + parity of scan 0
+    # ---- CPU baseline: the oracle (CPU restatement) on this host, bounded
+    # samples; + parity of scan 0 against it
     if rank == 0 and a.cpu_seconds > 0:
         import oracle
         tree = oracle.Tree(m)
@@ -453,43 +649,11 @@ def main():
         result["parity_scan0"] = {"iterations_equal": gs["iterations"] == rs["iterations"],
                                   "effct_equal": gs["effct_feat_num"] == rs["effct_feat_num"],
                                   "max_rel_state_delta": float(f"{rel:.3e}")}
-        # the IKFoM update of scan 0 against the oracle's
-        ir, irs = tree.ikfom_update(scans[0], synth.make_ikfom_state(scan_ids[0]), max_iter=a.max_iter, threads=8)
-        iscale = max(np.linalg.norm(d) for d in irs["dx"])  # relative to the scan's largest step
-        irel = max(np.linalg.norm(ik_first["dx"][e] - irs["dx"][e]) / iscale
-                   for e in range(min(ik_first["iterations"], irs["iterations"])))
-        # the iVox backend: one CPU scan update (1 thread) and parity of scan 0
-        ivo = oracle.Ivox()
-        ivo.add_points(m)
-        t = time.perf_counter()
-        ivs, ivst = ivo.iekf_update(scans[0], st0[0], oracle.new_cache(len(scans[0])), t_LI=synth.T_LI,
-                                    max_iter=a.max_iter, threads=1)
-        iv_cpu_s = time.perf_counter() - t
-        ig = iv_first[0]
-        ivrel = max(np.linalg.norm(ig["solution"][e] - ivst["solution"][e]) / np.linalg.norm(ivst["solution"][e])
-                    for e in range(min(ig["iterations"], ivst["iterations"])))
-        result["ivox"]["cpu_baseline"] = {"value": round(1.0 / iv_cpu_s, 4), "unit": "scan updates/s", "cores": 1,
-                                          "kind": "port", "sample": "1 full scan update of scan 0 by oracle/ (IVox "
-                                                                    f"restatement), 1 thread, {iv_cpu_s:.2f} s"}
-        # the front-end: de-skew + VoxelGrid of one raw frame by the oracle, 1 thread
-        raw, poses, Re, pe = raws[0]
-        t = time.perf_counter()
-        und = oracle.undistort(raw, poses, Re, pe, t_LI=synth.T_LI)
-        oracle.voxel_grid(und, 0.5)
-        fe_cpu = time.perf_counter() - t
-        result["ivox"]["pipeline"]["cpu_preprocess_ms"] = round(fe_cpu * 1e3, 3)
-        result["ivox"]["parity_scan0"] = {"iterations_equal": ig["iterations"] == ivst["iterations"],
-                                          "effct_equal": ig["effct_feat_num"] == ivst["effct_feat_num"],
-                                          "max_rel_state_delta": float(f"{ivrel:.3e}")}
-        # the ikd-Tree incremental map: Add_Points of scan 0 by the oracle, 1 thread
-        dyn = oracle.DynMap(m)
-        t = time.perf_counter()
-        dyn.map_incremental(scans[0], first_states[0], t_LI=synth.T_LI, filter_size_map=0.5)
-        result["ikd_incremental"]["cpu_add_points_ms"] = round((time.perf_counter() - t) * 1e3, 3)
-        del dyn
-        # the reference's thread counts (MP_PROC_NUM = 4, CMakeLists.txt:30-33) and 16 host threads
+        # the reference's thread count (MP_PROC_NUM = 4, CMakeLists.txt:30-33) and
+        # every core available to this job
+        all_t = host_threads()
         by_threads = {}
-        for nt in (4, 16):
+        for nt in sorted({4, all_t}):
             t = time.perf_counter()
             k = 0
             while k < 64:
@@ -500,18 +664,53 @@ def main():
                     break
             by_threads[str(nt)] = round(k / (time.perf_counter() - t), 4)
         result["cpu_baseline"]["by_threads"] = by_threads
-        # VIO: the oracle on the same frames (1 thread) and parity of the large one
+        result["cpu_baseline"]["host_threads_available"] = all_t
+        result["speedup_vs_cpu_all_threads"] = round(result["value"] / by_threads[str(all_t)], 1)
+        if "ikfom" in legs:
+            ir, irs = tree.ikfom_update(scans[0], synth.make_ikfom_state(scan_ids[0]), max_iter=a.max_iter, threads=8)
+            # per evaluation, relative to that evaluation's own step
+            irel = max(np.linalg.norm(ik_first["dx"][e] - irs["dx"][e]) / max(np.linalg.norm(irs["dx"][e]), 1e-300)
+                       for e in range(min(ik_first["iterations"], irs["iterations"])))
+            result["ikfom"]["parity_scan0"] = {"iterations_equal": ik_first["iterations"] == irs["iterations"],
+                                               "effct_equal": ik_first["effct_feat_num"] == irs["effct_feat_num"],
+                                               "max_rel_dx_per_eval": float(f"{irel:.3e}")}
+        if "ivox" in legs:
+            ivo = oracle.Ivox()
+            ivo.add_points(m)
+            t = time.perf_counter()
+            ivs, ivst = ivo.iekf_update(scans[0], st0[0], oracle.new_cache(len(scans[0])), t_LI=synth.T_LI,
+                                        max_iter=a.max_iter, threads=1)
+            iv_cpu_s = time.perf_counter() - t
+            ig = iv_first[0]
+            ivrel = max(np.linalg.norm(ig["solution"][e] - ivst["solution"][e]) / np.linalg.norm(ivst["solution"][e])
+                        for e in range(min(ig["iterations"], ivst["iterations"])))
+            result["ivox"]["cpu_baseline"] = {"value": round(1.0 / iv_cpu_s, 4), "unit": "scan updates/s",
+                                              "cores": 1, "kind": "port",
+                                              "sample": "1 full scan update of scan 0 by oracle/ (IVox "
+                                                        f"restatement), 1 thread, {iv_cpu_s:.2f} s"}
+            raw, poses, Re, pe = raws[0]
+            t = time.perf_counter()
+            und = oracle.undistort(raw, poses, Re, pe, t_LI=synth.T_LI)
+            oracle.voxel_grid(und, 0.5)
+            result["ivox"]["pipeline"]["cpu_preprocess_ms"] = round((time.perf_counter() - t) * 1e3, 3)
+            result["ivox"]["parity_scan0"] = {"iterations_equal": ig["iterations"] == ivst["iterations"],
+                                              "effct_equal": ig["effct_feat_num"] == ivst["effct_feat_num"],
+                                              "max_rel_state_delta": float(f"{ivrel:.3e}")}
+        if "ikd" in legs:
+            dyn = oracle.DynMap(m)
+            t = time.perf_counter()
+            dyn.map_incremental(scans[0], first_states[0], t_LI=synth.T_LI, filter_size_map=0.5)
+            result["ikd_incremental"]["cpu_add_points_ms"] = round((time.perf_counter() - t) * 1e3, 3)
+            del dyn
         for nv, (fr, vst) in vio_frames.items():
             t = time.perf_counter()
             vr, vrs, _ = oracle.vio_update(fr, vst)
             key = str(len(fr["pos"]))
             result["vio"]["by_points"][key]["cpu_ms_per_frame"] = round((time.perf_counter() - t) * 1e3, 3)
-        vg, vgs, _ = ctx.vio_update(*vio_frames[20000])
-        result["vio"]["parity_20k"] = {"iterations_equal": vgs["iterations"] == vrs["iterations"],
-                                       "max_abs_pos_delta": float(f"{np.abs(vg['pos'] - vr['pos']).max():.3e}")}
-        result["ikfom"]["parity_scan0"] = {"iterations_equal": ik_first["iterations"] == irs["iterations"],
-                                           "effct_equal": ik_first["effct_feat_num"] == irs["effct_feat_num"],
-                                           "max_dx_error_rel_to_largest_step": float(f"{irel:.3e}")}
+        if vio_frames:
+            vg, vgs, _ = ctx.vio_update(*vio_frames[20000])
+            result["vio"]["parity_20k"] = {"iterations_equal": vgs["iterations"] == vrs["iterations"],
+                                           "max_abs_pos_delta": float(f"{np.abs(vg['pos'] - vr['pos']).max():.3e}")}
     if rank == 0:
         print(json.dumps(result), flush=True)
     ctx.close()

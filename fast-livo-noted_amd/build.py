@@ -5,6 +5,7 @@ fast-livo-noted_amd/lib/liblivo_hip.so, exporting the C ABI of include/livo.h.
 """
 from __future__ import annotations
 
+import concurrent.futures
 import os
 import subprocess
 import sys
@@ -53,7 +54,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     newest = max(os.path.getmtime(d) for d in deps)
     if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= newest:
         return LIB
-    objs = []
+    objs, cmds = [], []
     for src, is_dev in SOURCES:
         obj = os.path.join(OBJ_DIR, src + ".o")
         cmd = [HIPCC] + COMMON + (DEVICE + ["-x", "hip"] if is_dev else ["-D__HIP_PLATFORM_AMD__"]) + \
@@ -62,8 +63,11 @@ def build(force: bool = False, verbose: bool = False) -> str:
             cmd.insert(1, "-pthread")
         if verbose:
             print(" ".join(cmd))
-        _run(cmd)
+        cmds.append(cmd)
         objs.append(obj)
+    # one compiler process per source (a few CPUs: each hipcc holds ~1 GB)
+    with concurrent.futures.ThreadPoolExecutor(max_workers=min(4, os.cpu_count() or 1)) as ex:
+        list(ex.map(_run, cmds))
     cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-pthread", "-o", LIB + ".tmp"] + objs
     _run(cmd)
     os.replace(LIB + ".tmp", LIB)

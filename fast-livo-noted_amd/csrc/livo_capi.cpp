@@ -34,6 +34,8 @@ struct ScanBuf {
     int32_t* d_perm = nullptr;  // the same on the device
     int32_t* d_iperm = nullptr; // caller's point index -> stored position
     double* partial = nullptr;  // nblk x kIkCols (the A-path uses kRedCols of each)
+    float* plane = nullptr;     // N x 4: planes of the cached neighbours (k_hshare)
+    uint8_t* pstate = nullptr;  // N: plane state (0: not fitted since the neighbours changed)
     bool searched = false;      // a search has filled the neighbour cache
 };
 
@@ -311,6 +313,8 @@ static void fill_job(HsJob& j, ScanBuf& s, IekfSlot* slot) {
     j.pts = s.pts;
     j.nn = s.nn;
     j.partial = s.partial;
+    j.plane = s.plane;
+    j.pstate = s.pstate;
     j.slot = slot;
     j.n = (int32_t)s.n;
     j.nblk = s.nblk;
@@ -1085,6 +1089,7 @@ static int32_t register_scan(livo_ctx* c, const ScanBuf& s) {
 
 static void free_scan_buf(ScanBuf& s) {
     dev_free(s.pts); dev_free(s.nn); dev_free(s.partial); dev_free(s.d_perm); dev_free(s.d_iperm);
+    dev_free(s.plane); dev_free(s.pstate);
 }
 
 // A resident scan from N device points (x, y, z at d_src + stride * i floats):
@@ -1100,6 +1105,8 @@ static int scan_create_device(livo_ctx* c, const float* d_src, int stride, int64
     rc |= dev_alloc(&s.partial, (size_t)std::max(s.nblk, 1) * kIkCols);
     rc |= dev_alloc(&s.d_perm, (size_t)N);
     rc |= dev_alloc(&s.d_iperm, (size_t)N);
+    rc |= dev_alloc(&s.plane, (size_t)N * 4);
+    rc |= dev_alloc(&s.pstate, (size_t)N);
     if (rc) {
         free_scan_buf(s);
         return LIVO_E_OOM;
@@ -1126,6 +1133,7 @@ static int scan_create_device(livo_ctx* c, const float* d_src, int stride, int64
         if (!rc && (hipMemcpyAsync(s.d_perm, perm, (size_t)N * 4, hipMemcpyDeviceToDevice, c->stream) != hipSuccess ||
                     hipMemcpyAsync(s.perm.data(), perm, (size_t)N * 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
                     hipMemsetAsync(s.nn, 0, (size_t)N * sizeof(NNRec), c->stream) != hipSuccess ||
+                    hipMemsetAsync(s.pstate, 0, (size_t)N, c->stream) != hipSuccess ||
                     hipStreamSynchronize(c->stream) != hipSuccess))
             rc = LIVO_E_HIP;
         dev_free(codes); dev_free(scodes); dev_free(iota); dev_free(perm); dev_free(mm);
@@ -1153,9 +1161,10 @@ int livo_scan_upload(livo_ctx* c, const float* xyz, int64_t N, int64_t stride_by
     rc |= dev_alloc(&s.pts, (size_t)N * 4);
     rc |= dev_alloc(&s.nn, (size_t)N);
     rc |= dev_alloc(&s.partial, (size_t)std::max(s.nblk, 1) * kIkCols);  // IKFoM partials are the wider
+    rc |= dev_alloc(&s.plane, (size_t)N * 4);
+    rc |= dev_alloc(&s.pstate, (size_t)N);
     if (rc) {
-        dev_free(s.pts); dev_free(s.nn);
-        dev_free(s.partial);
+        free_scan_buf(s);
         return LIVO_E_OOM;
     }
     if (N > 0) {
@@ -1173,11 +1182,13 @@ int livo_scan_upload(livo_ctx* c, const float* xyz, int64_t N, int64_t stride_by
         for (int64_t k = 0; k < N; k++)
             for (int a = 0; a < 4; a++) hs[4 * k + a] = h[4 * (int64_t)s.perm[k] + a];
         if (hipMemcpy(s.pts, hs.data(), hs.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) return LIVO_E_HIP;
-        if (hipMemset(s.nn, 0, (size_t)N * sizeof(NNRec)) != hipSuccess) return LIVO_E_HIP;
+        if (hipMemset(s.nn, 0, (size_t)N * sizeof(NNRec)) != hipSuccess ||
+            hipMemset(s.pstate, 0, (size_t)N) != hipSuccess)
+            return LIVO_E_HIP;
         std::vector<int32_t> iperm((size_t)N);
         for (int64_t k = 0; k < N; k++) iperm[(size_t)s.perm[(size_t)k]] = (int32_t)k;
         if (dev_alloc(&s.d_perm, (size_t)N) || dev_alloc(&s.d_iperm, (size_t)N)) {
-            dev_free(s.pts); dev_free(s.nn); dev_free(s.partial); dev_free(s.d_perm); dev_free(s.d_iperm);
+            free_scan_buf(s);
             return LIVO_E_OOM;
         }
         if (hipMemcpy(s.d_perm, s.perm.data(), (size_t)N * 4, hipMemcpyHostToDevice) != hipSuccess ||
@@ -1194,9 +1205,7 @@ int livo_scan_release(livo_ctx* c, int32_t id) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     ScanBuf& s = c->scans[id];
-    dev_free(s.pts); dev_free(s.nn);
-    dev_free(s.partial);
-    dev_free(s.d_perm); dev_free(s.d_iperm);
+    free_scan_buf(s);
     s = ScanBuf{};
     return LIVO_OK;
 }
@@ -1334,6 +1343,13 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
     if (model == kModelIkfom && c->backend != LIVO_BACKEND_IKDTREE) return LIVO_E_INVALID;  // ikd-Tree h-model only
     for (int32_t b = 0; b < n; b++)
         if (!get_scan(c, ids[b])) return LIVO_E_NOSCAN;
+    {
+        // a scan's neighbour records, plane cache and partials are per scan: the
+        // same id twice in one batch would have two updates write them concurrently
+        std::vector<int32_t> sorted(ids, ids + n);
+        std::sort(sorted.begin(), sorted.end());
+        if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end()) return LIVO_E_INVALID;
+    }
     if (set_device(c)) return LIVO_E_HIP;
     int rc = ensure_slots(c, n);
     if (rc) return rc;
@@ -1351,6 +1367,11 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
     }
     rc = ensure_replay(c, total_n);
     if (rc) return rc;
+    if (model == kModelIkfom)  // its searches rewrite the neighbours without refitting the cached planes
+        for (int32_t b = 0; b < n; b++) {
+            ScanBuf* s = get_scan(c, ids[b]);
+            if (s->n > 0) HIP_TRY(hipMemsetAsync(s->pstate, 0, (size_t)s->n, c->stream));
+        }
     HIP_TRY(hipMemcpyAsync(c->d_slots, c->h_slots, sizeof(IekfSlot) * n, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->d_jobs, c->h_jobs, sizeof(HsJob) * n, hipMemcpyHostToDevice, c->stream));
 
@@ -1465,6 +1486,7 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
         // the first evaluation searches for every point of every scan
         for (int32_t b = 0; b < n; b++) {
             t.knn_visits += (int64_t)c->h_slots[b].visits[0];
+            t.knn_points += (int64_t)c->h_slots[b].scanned[0];
             t.knn_queries += c->scans[ids[b]].n;
             t.effct_points += model == kModelIkfom ? c->h_slots[b].ik.stats.effct_feat_num[0]
                                                    : c->h_slots[b].stats.effct_feat_num[0];
@@ -1729,6 +1751,7 @@ int livo_scan_inherit_neighbors(livo_ctx* c, int32_t dst, int32_t src) {
     if (d->n == 0) return LIVO_OK;
     const int rc = launch_inherit_nn(d->nn, d->d_perm, d->n, s->nn, s->d_iperm, s->searched ? s->n : 0, c->stream);
     if (rc) return rc;
+    HIP_TRY(hipMemsetAsync(d->pstate, 0, (size_t)d->n, c->stream));  // new neighbours: planes to refit
     HIP_TRY(hipStreamSynchronize(c->stream));
     d->searched = true;  // the cache now holds the inherited entries
     return LIVO_OK;

@@ -197,7 +197,8 @@ struct alignas(16) IekfSlot {
     double red[kRedCols];       // last reduced h_share sums (for livo_h_share)
     livo_iter_stats stats;
     IekfCtrl ctrl;
-    unsigned long long visits[LIVO_MAX_EVALS];  // k-NN nodes visited per evaluation
+    unsigned long long visits[LIVO_MAX_EVALS];  // k-NN nodes visited (grid: hash slots probed) per evaluation
+    unsigned long long scanned[LIVO_MAX_EVALS]; // grid k-NN: map points read per evaluation
     int32_t eval_search[LIVO_MAX_EVALS];
     unsigned hs_ticket;         // k_hshare blocks done in the current pass (the last one reduces)
     int32_t model;              // SlotModel
@@ -222,6 +223,8 @@ struct HsJob {
     NNRec* nn;            // N neighbour records
     double* partial;      // nblk x kRedCols block partial sums
     IekfSlot* slot;
+    float* plane;         // N x 4: esti_plane of the cached neighbours (k_hshare)
+    uint8_t* pstate;      // N: 0 not fitted since the last search, 1 no plane, 2 plane
     int32_t n;
     int32_t nblk;
 };

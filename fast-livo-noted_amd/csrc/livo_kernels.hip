@@ -533,14 +533,19 @@ __device__ __forceinline__ void query_point(const KnnParams& P, const IekfSlot* 
     }
 }
 
-__device__ __forceinline__ void count_visits(const KnnParams& P, IekfSlot* slot, unsigned visits) {
-    unsigned long long wv = visits;
+__device__ __forceinline__ void count_visits(const KnnParams& P, IekfSlot* slot, unsigned visits,
+                                             unsigned points = 0u) {
+    unsigned long long wv = visits, wp = points;
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) wv += __shfl_xor(wv, off, 64);
-    if ((threadIdx.x & 63) == 0 && wv) {
+    for (int off = 32; off >= 1; off >>= 1) {
+        wv += __shfl_xor(wv, off, 64);
+        wp += __shfl_xor(wp, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0 && (wv || wp)) {
         int e = P.force >= 0 ? 0 : slot->ctrl.n_evals;
         e = e < LIVO_MAX_EVALS ? e : LIVO_MAX_EVALS - 1;
-        atomicAdd(&slot->visits[e], wv);
+        if (wv) atomicAdd(&slot->visits[e], wv);
+        if (wp) atomicAdd(&slot->scanned[e], wp);
     }
 }
 
@@ -963,7 +968,7 @@ __global__ __launch_bounds__(kKnnBlock, LIVO_GRID_WAVES) void k_knn_grid(KnnPara
         cell_of(q.qy, P.gorg[1], c1, s1);
         cell_of(q.qz, P.gorg[2], c2, s2);
     }
-    unsigned visits = 0;
+    unsigned visits = 0, npts = 0;  // hash slots and map points read
     auto visit = [&](int cx, int cy, int cz) __attribute__((always_inline)) {
         const float x0 = P.gorg[0] + (float)cx * h - eps, y0 = P.gorg[1] + (float)cy * h - eps;
         const float z0 = P.gorg[2] + (float)cz * h - eps;
@@ -977,9 +982,11 @@ __global__ __launch_bounds__(kKnnBlock, LIVO_GRID_WAVES) void k_knn_grid(KnnPara
         while (gs.key != key && gs.key != kGridEmpty) {  // linear probing (load factor <= 1/4)
             sl = (sl + 1) & mask;
             gs = slots[sl];
+            visits++;
         }
         if (gs.key != key) return;
         const int lo = (int)gs.start, hi = (int)(gs.start + gs.count);
+        npts += gs.count;
         for (int k0 = lo; k0 < hi; k0 += 4) {
             float4 v[4];
 #pragma unroll
@@ -1059,7 +1066,7 @@ __global__ __launch_bounds__(kKnnBlock, LIVO_GRID_WAVES) void k_knn_grid(KnnPara
         }
     }
     lq_finish(q, P, job, bjob, i, gpts, !certified);
-    count_visits(P, slot, visits);
+    count_visits(P, slot, visits, npts);
 }
 
 // Exact reference-order recomputation of the queries the fast pass flagged:
@@ -1410,16 +1417,20 @@ __device__ __forceinline__ bool esti_plane(const float (&px)[5], const float (&p
     return ok;
 }
 
-// ======================================================= reductions =======
-
-
-
-
 // ========================================================== solve =========
-// One wave per scan, the reference's algebra in the oracle's operation order
-// (laser_mapping.cpp:187-193): P^-1 once per update, K1 = (H_T_H + P^-1)^-1
-// (first 9 columns: all the update reads), G, solution, boxplus, control,
-// covariance, with the one-wave LU of device_linalg.h.
+// One wave per scan (laser_mapping.cpp:187-193).  The reference forms
+//   K1 = (H_T_H + P^-1)^-1,  G(:,0:9) = K1(:,0:9) HTH,
+//   solution = K1(:,0:9) HTL + vec - G(:,0:9) vec(0:9)
+// with two 18x18 PartialPivLU inversions.  H_T_H is non-zero only in its 6x6
+// block C (rows/cols 6..8 of HTH are zero without GNSS, :580-590), so with
+// U = [I6; 0]:  (P^-1 + U C U^T) K1 U = U  gives
+//   K1(:,0:6) = P(:,0:6) (I6 + C P66)^-1          (P66 = P(0:6,0:6))
+// and K1(:,6:9) only ever multiplies zeros.  Hence
+//   G(:,0:6) = K1(:,0:6) C,  solution = K1(:,0:6) (HTL6 - C vec6) + vec,
+//   state.cov = (I - G) P = P - G(:,0:6) P(0:6,:)
+// -- one 6x6 LU instead of two 18x18 ones and no P^-1 at all.  Same quantities
+// as the oracle's LU path to ~1e-13 relative (tests/test_gpu_parity.py bars:
+// state delta 1e-5, covariance 1e-9).
 #ifdef LIVO_SOLVE_PROF  // phase timestamps for tools/solve_lab (compiled out of the product)
 __device__ unsigned long long g_solve_prof[256][16];
 #define SOLVE_MARK(k) do { if (threadIdx.x == 0) g_solve_prof[blockIdx.x][k] = __builtin_amdgcn_s_memtime(); } while (0)
@@ -1430,111 +1441,88 @@ __device__ unsigned long long g_solve_prof[256][16];
 struct SolveLds {
     double sum[kRedCols];
     double P[kDim * kDim];      // state.cov
-    double Pinv[kDim * kDim];
-    double LU[kDim * kDim];
-    double K1[kDim * 9];        // K1(:, 0:9)
-    double G[kDim * 9];         // G(:, 0:9)
-    double HTH[81];
+    double C[36];               // H_T_H(0:6, 0:6)
+    double M[36];               // I6 + C P66
+    double LU[36];
+    double Minv[36];
+    double K6[kDim * 6];        // K1(:, 0:6)
+    double G6[kDim * 6];        // G(:, 0:6)
+    double w[6];                // HTL6 - C vec6
     double vec[kDim];
     double sol[kDim];
-    int piv[kDim];
+    int piv[6];
 };
 
-// One wave (lanes 0..63 of the calling block, the other waves idle): the
-// reference's algebra in the oracle's operation order (laser_mapping.cpp:187-238)
-// from the reduced h_share sums in L.sum.  Only this wave touches L, so LDS
-// hand-offs between lanes need a wave-level fence, not a block barrier.
+// One wave (lanes 0..63 of the calling block, the other waves idle), from the
+// reduced h_share sums in L.sum.  Only this wave touches L, so LDS hand-offs
+// between lanes need a wave-level fence, not a block barrier.
 __device__ __forceinline__ void solve_scan(IekfSlot* slot, SolveLds& L, const int lane) {
-    double* const s_sum = L.sum;
+    const double* const s_sum = L.sum;
     double* const s_P = L.P;
-    double* const s_Pinv = L.Pinv;
-    double* const s_LU = L.LU;
-    double* const s_K1 = L.K1;
-    double* const s_G = L.G;
-    double* const s_HTH = L.HTH;
-    double* const s_vec = L.vec;
-    double* const s_sol = L.sol;
-    int* const s_piv = L.piv;
     for (int t = lane; t < kDim * kDim; t += 64) s_P[t] = slot->state.cov[t];
-    WAVE_SYNC();
-    // 2. HTH (9x9, rows/cols 6..8 zero: gnss_en = 0)
-    for (int t = lane; t < 81; t += 64) {
-        const int r = t / 9, c = t % 9;
-        double v = 0.0;
-        if (r < 6 && c < 6) {
-            const int a = r < c ? r : c, b = r < c ? c : r;
-            v = s_sum[a * 6 - (a * (a - 1)) / 2 + (b - a)];  // upper-tri packed index
-        }
-        s_HTH[t] = v;
+    if (lane < 36) {
+        const int r = lane / 6, c = lane % 6;
+        const int a = r < c ? r : c, b = r < c ? c : r;
+        L.C[lane] = s_sum[a * 6 - (a * (a - 1)) / 2 + (b - a)];  // upper-tri packed index
     }
     const IekfCtrl ctrl0 = slot->ctrl;
-    SOLVE_MARK(2);
     const int e = ctrl0.n_evals;
-    const bool row = lane < kDim;
-    // 3. P^-1 once per update (state.cov does not change inside the loop)
-    if (e == 0) {
-        double A[kDim];
-#pragma unroll
-        for (int j = 0; j < kDim; j++) A[j] = row ? s_P[lane * kDim + j] : 0.0;
-        wave_lu_to_lds<kDim>(A, lane, s_LU, s_piv);
-        WAVE_SYNC();
-        if (lane < kDim) {
-            double y[kDim];
-            lds_lu_column<kDim>(s_LU, s_piv, lane, y);
-#pragma unroll
-            for (int i = 0; i < kDim; i++) s_Pinv[i * kDim + lane] = y[i];
-        }
-        WAVE_SYNC();
-        for (int t = lane; t < kDim * kDim; t += 64) slot->Pinv[t] = s_Pinv[t];
-    } else {
-        for (int t = lane; t < kDim * kDim; t += 64) s_Pinv[t] = slot->Pinv[t];
-    }
     WAVE_SYNC();
-    SOLVE_MARK(3);
-    // 4. K1 = (H_T_H + P^-1)^-1, columns 0..8
+    SOLVE_MARK(2);
+    // M = I6 + C P66
+    if (lane < 36) {
+        const int r = lane / 6, c = lane % 6;
+        double m = L.C[r * 6 + 0] * s_P[0 * kDim + c];
+#pragma unroll
+        for (int k = 1; k < 6; k++) m = m + L.C[r * 6 + k] * s_P[k * kDim + c];
+        L.M[lane] = (r == c ? 1.0 : 0.0) + m;
+    }
+    // vec = state_propagat - state
+    if (lane == 0) state_minus_d(slot->prior, slot->state, L.vec);
+    WAVE_SYNC();
     {
-        double A[kDim];
+        double A[6];
 #pragma unroll
-        for (int j = 0; j < kDim; j++)
-            A[j] = row ? (((lane < 9 && j < 9) ? s_HTH[lane * 9 + j] : 0.0) + s_Pinv[lane * kDim + j]) : 0.0;
-        wave_lu_to_lds<kDim>(A, lane, s_LU, s_piv);
-        WAVE_SYNC();
-        SOLVE_MARK(4);
-        if (lane < 9) {
-            double y[kDim];
-            lds_lu_column<kDim>(s_LU, s_piv, lane, y);
-#pragma unroll
-            for (int i = 0; i < kDim; i++) s_K1[i * 9 + lane] = y[i];
-        }
-        WAVE_SYNC();
+        for (int j = 0; j < 6; j++) A[j] = lane < 6 ? L.M[lane * 6 + j] : 0.0;
+        wave_lu_to_lds<6>(A, lane, L.LU, L.piv);
     }
-    SOLVE_MARK(5);
-    // 5. G(:,0:9) = K1(:,0:9) * HTH ; columns 9..17 stay zero
-    for (int t = lane; t < kDim * 9; t += 64) {
-        const int i = t / 9, j = t % 9;
-        double g = s_K1[i * 9 + 0] * s_HTH[0 * 9 + j];
-#pragma unroll
-        for (int l = 1; l < 9; l++) g = g + s_K1[i * 9 + l] * s_HTH[l * 9 + j];
-        s_G[t] = g;
-    }
-    // 6. vec = state_propagat - state
-    if (lane == 0) state_minus_d(slot->prior, slot->state, s_vec);
     WAVE_SYNC();
-    SOLVE_MARK(6);
-    // 7. solution = K1(:,0:9) HTL + vec - G(:,0:9) vec(0:9)
-    if (row) {
-        const int i = lane;
-        double a = s_K1[i * 9 + 0] * s_sum[21 + 0];
+    if (lane < 6) {
+        double y[6];
+        lds_lu_column<6>(L.LU, L.piv, lane, y);
 #pragma unroll
-        for (int l = 1; l < 9; l++) a = a + s_K1[i * 9 + l] * (l < 6 ? s_sum[21 + l] : 0.0);
-        double g = s_G[i * 9 + 0] * s_vec[0];
-#pragma unroll
-        for (int l = 1; l < 9; l++) g = g + s_G[i * 9 + l] * s_vec[l];
-        s_sol[i] = (a + s_vec[i]) - g;
+        for (int i = 0; i < 6; i++) L.Minv[i * 6 + lane] = y[i];
     }
-    for (int t = lane; t < kDim * kDim; t += 64) {
-        const int i = t / kDim, j = t % kDim;
-        slot->G[t] = j < 9 ? s_G[i * 9 + j] : 0.0;
+    if (lane < 6) {
+        double wv = s_sum[21 + lane];
+#pragma unroll
+        for (int k = 0; k < 6; k++) wv = wv - L.C[lane * 6 + k] * L.vec[k];
+        L.w[lane] = wv;
+    }
+    WAVE_SYNC();
+    SOLVE_MARK(4);
+    // K1(:, 0:6) = P(:, 0:6) M^-1
+    for (int t = lane; t < kDim * 6; t += 64) {
+        const int r = t / 6, c = t % 6;
+        double k6 = s_P[r * kDim + 0] * L.Minv[0 * 6 + c];
+#pragma unroll
+        for (int k = 1; k < 6; k++) k6 = k6 + s_P[r * kDim + k] * L.Minv[k * 6 + c];
+        L.K6[t] = k6;
+    }
+    WAVE_SYNC();
+    // G(:, 0:6) = K1(:, 0:6) C ;  solution = K1(:, 0:6) w + vec
+    for (int t = lane; t < kDim * 6; t += 64) {
+        const int r = t / 6, c = t % 6;
+        double g = L.K6[r * 6 + 0] * L.C[0 * 6 + c];
+#pragma unroll
+        for (int k = 1; k < 6; k++) g = g + L.K6[r * 6 + k] * L.C[k * 6 + c];
+        L.G6[t] = g;
+    }
+    if (lane < kDim) {
+        double a = L.K6[lane * 6 + 0] * L.w[0];
+#pragma unroll
+        for (int k = 1; k < 6; k++) a = a + L.K6[lane * 6 + k] * L.w[k];
+        L.sol[lane] = a + L.vec[lane];
     }
     WAVE_SYNC();
 
@@ -1544,7 +1532,7 @@ __device__ __forceinline__ void solve_scan(IekfSlot* slot, SolveLds& L, const in
     if (lane == 0) {
         double sol[kDim];
 #pragma unroll
-        for (int k = 0; k < kDim; k++) sol[k] = s_sol[k];
+        for (int k = 0; k < kDim; k++) sol[k] = L.sol[k];
         IekfCtrl ctrl = ctrl0;
         state_boxplus_d(slot->state, sol);
         const double rn = sqrt((sol[0] * sol[0] + sol[1] * sol[1]) + sol[2] * sol[2]);
@@ -1581,16 +1569,14 @@ __device__ __forceinline__ void solve_scan(IekfSlot* slot, SolveLds& L, const in
     }
     stop_now = __builtin_amdgcn_readfirstlane(stop_now);
     SOLVE_MARK(8);
-    // 9. covariance update state.cov = (I - G) * state.cov (:224-227)
+    // 9. covariance update state.cov = (I - G) * state.cov (:224-227) = P - G(:,0:6) P(0:6,:)
     if (stop_now) {
         for (int t = lane; t < kDim * kDim; t += 64) {
             const int i = t / kDim, j = t % kDim;
-            double acc = (((i == 0) ? 1.0 : 0.0) - s_G[i * 9 + 0]) * s_P[0 * kDim + j];
-            for (int l = 1; l < kDim; l++) {
-                const double gl = l < 9 ? s_G[i * 9 + l] : 0.0;
-                acc = acc + (((i == l) ? 1.0 : 0.0) - gl) * s_P[l * kDim + j];
-            }
-            slot->state.cov[t] = acc;
+            double gp = L.G6[i * 6 + 0] * s_P[0 * kDim + j];
+#pragma unroll
+            for (int l = 1; l < 6; l++) gp = gp + L.G6[i * 6 + l] * s_P[l * kDim + j];
+            slot->state.cov[t] = s_P[t] - gp;
         }
     }
     SOLVE_MARK(9);
@@ -1634,30 +1620,50 @@ __global__ __launch_bounds__(kBlock) void k_hshare(HsParams P) {
             P.dbg.world[3 * i + 1] = wy;
             P.dbg.world[3 * i + 2] = wz;
         }
-        const float4* rec = reinterpret_cast<const float4*>(job.nn + i);
-        float nx[kNN], ny[kNN], nz[kNN];
-        float d4 = 0.0f;
-#pragma unroll
-        for (int k = 0; k < kNN; k++) {
-            const float4 v = rec[k];
-            nx[k] = v.x; ny[k] = v.y; nz[k] = v.z;
-            if (k == kNN - 1) d4 = v.w;
-        }
-        const int cnt = reinterpret_cast<const int4*>(job.nn + i)[6].y;
-        // point_selected_surf: sqdis[4] > 5 => false after a search (:518); true otherwise (:490)
-        const bool sel = search ? ((cnt == kNN) && !(d4 > P.max_sqd)) : true;
-        bool accepted = false, keep = false;
+        // esti_plane depends only on the 5 cached neighbours (Nearest_Points),
+        // so an evaluation without a search refits exactly the plane of the
+        // last one: the plane is kept per point (job.plane / job.pstate:
+        // 0 not fitted yet, 1 no plane, 2 plane) and reused bit for bit.
+        bool plane_ok = false;
         float pa[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        float pd2 = 0.0f;
-        if (sel && cnt >= kNN) {
-            if (esti_plane(nx, ny, nz, P.plane_thr, pa)) {
-                pd2 = ((pa[0] * wx + pa[1] * wy) + pa[2] * wz) + pa[3];
-                const double bx = pb.x, by = pb.y, bz = pb.z;
-                const double bn = sqrt((bx * bx + by * by) + bz * bz);
-                const float s = (float)(1 - 0.9 * (double)fabsf(pd2) / sqrt(bn));
-                accepted = (double)s > 0.9;                          // :535-542
-                keep = accepted && (double)fabsf(pd2) <= P.max_res;  // :552
+        uint8_t ps = search ? 0 : job.pstate[i];
+        if (ps == 0) {
+            const float4* rec = reinterpret_cast<const float4*>(job.nn + i);
+            float nx[kNN], ny[kNN], nz[kNN];
+            float d4 = 0.0f;
+#pragma unroll
+            for (int k = 0; k < kNN; k++) {
+                const float4 v = rec[k];
+                nx[k] = v.x; ny[k] = v.y; nz[k] = v.z;
+                if (k == kNN - 1) d4 = v.w;
             }
+            const int cnt = reinterpret_cast<const int4*>(job.nn + i)[6].y;
+            // point_selected_surf: sqdis[4] > 5 => false after a search (:518); true otherwise (:490)
+            const bool sel = search ? ((cnt == kNN) && !(d4 > P.max_sqd)) : true;
+            if (cnt < kNN) {
+                ps = 1;  // points_near.size() < 5 (:525) until the next search
+            } else if (sel) {
+                plane_ok = esti_plane(nx, ny, nz, P.plane_thr, pa);
+                ps = plane_ok ? 2 : 1;
+            }
+            // (a searched point beyond the sqdist gate stays 0: the next
+            // evaluation without a search fits it, as the reference does)
+            job.pstate[i] = ps;
+            if (plane_ok) reinterpret_cast<float4*>(job.plane)[i] = make_float4(pa[0], pa[1], pa[2], pa[3]);
+        } else if (ps == 2) {
+            const float4 v = reinterpret_cast<const float4*>(job.plane)[i];
+            pa[0] = v.x; pa[1] = v.y; pa[2] = v.z; pa[3] = v.w;
+            plane_ok = true;
+        }
+        bool accepted = false, keep = false;
+        float pd2 = 0.0f;
+        if (plane_ok) {
+            pd2 = ((pa[0] * wx + pa[1] * wy) + pa[2] * wz) + pa[3];
+            const double bx = pb.x, by = pb.y, bz = pb.z;
+            const double bn = sqrt((bx * bx + by * by) + bz * bz);
+            const float s = (float)(1 - 0.9 * (double)fabsf(pd2) / sqrt(bn));
+            accepted = (double)s > 0.9;                          // :535-542
+            keep = accepted && (double)fabsf(pd2) <= P.max_res;  // :552
         }
         if (P.dbg.normvec)
             reinterpret_cast<float4*>(P.dbg.normvec)[i] =

@@ -74,7 +74,7 @@ class Timings(C.Structure):
     _fields_ = [("knn_ms", C.c_double), ("rematch_knn_ms", C.c_double), ("plane_ms", C.c_double),
                 ("solve_ms", C.c_double),
                 ("knn_launches", C.c_int64), ("knn_visits", C.c_int64), ("knn_queries", C.c_int64),
-                ("effct_points", C.c_int64), ("knn_replays", C.c_int64)]
+                ("effct_points", C.c_int64), ("knn_replays", C.c_int64), ("knn_points", C.c_int64)]
 
 
 # every entry point of include/livo.h, with its ctypes signature

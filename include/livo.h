@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define LIVO_ABI_VERSION 1
+#define LIVO_ABI_VERSION 2
 #define LIVO_DIM_STATE 18        /* DIM_STATE, include/common_lib.h:32 */
 #define LIVO_NUM_MATCH_POINTS 5  /* NUM_MATCH_POINTS, include/common_lib.h:37 */
 #define LIVO_MAX_EVALS 16        /* max h_share/solve evaluations per scan update */
@@ -137,6 +137,7 @@ typedef struct livo_timings {
     int64_t knn_queries;   /* points those launches processed                          */
     int64_t effct_points;  /* effective points of the first evaluation                 */
     int64_t knn_replays;   /* queries recomputed by the exact tie-order replay (all passes) */
+    int64_t knn_points;    /* map points those launches read (cell grid; 0 for tree passes) */
 } livo_timings;
 
 int livo_abi_version(void);
@@ -183,7 +184,9 @@ int livo_h_share(livo_ctx* ctx, int32_t scan_id, const livo_state* state, int ne
 int livo_iekf_update(livo_ctx* ctx, int32_t scan_id, livo_state* state, const livo_state* prior,
                      livo_iter_stats* stats);
 
-/* n independent scan updates in one batched pass (states/priors/stats arrays of n). */
+/* n independent scan updates in one batched pass (states/priors/stats arrays of n).
+ * The ids must be distinct (LIVO_E_INVALID otherwise): a scan's neighbour cache
+ * belongs to one update at a time. */
 int livo_iekf_update_batch(livo_ctx* ctx, int32_t n, const int32_t* scan_ids, livo_state* states,
                            const livo_state* priors, livo_iter_stats* stats);
 
