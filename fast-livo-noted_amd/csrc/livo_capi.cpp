@@ -36,6 +36,8 @@ struct ScanBuf {
     double* partial = nullptr;  // nblk x kIkCols (the A-path uses kRedCols of each)
     float* plane = nullptr;     // N x 4: planes of the cached neighbours (k_hshare)
     uint8_t* pstate = nullptr;  // N: plane state (0: not fitted since the neighbours changed)
+    double* ikrows = nullptr;   // IKFoM few-point rows (nblk x kIkFewRows x 13)
+    uint32_t* ikcnt = nullptr;  // per block
     bool searched = false;      // a search has filled the neighbour cache
 };
 
@@ -122,7 +124,8 @@ struct livo_ctx {
     float* lpts = nullptr;
     int32_t leaf_depth = 0;
     int64_t leaf_bytes = 0;
-    int knn_kind = 1;                  // batched search structure: 0 leaf map, 1 cell grid (LIVO_KNN_KIND)
+    int knn_kind = 2;                  // batched search: 0 leaf map, 1 cell grid, 2 cell grid + LDS tiles (LIVO_KNN_KIND)
+    bool fused = true;                 // kind 2: one k_iekf_eval launch per evaluation (LIVO_FUSED=0: separate passes)
     float grid_cell = 0.f;             // cell edge (LIVO_GRID_CELL; 0: from the map)
     GridSlot* gslots = nullptr;        // cell grid
     float* gpts = nullptr;
@@ -252,7 +255,7 @@ static KnnParams make_knn_params(livo_ctx* c) {
 static int knn_pass(const KnnParams& kp, int n_jobs, int64_t max_n, hipStream_t st) {
     HIP_TRY(hipMemsetAsync(kp.replay_count, 0, sizeof(unsigned), st));
     // the incremental map has no reference-order tree: the grid search + canonical replay
-    if (kp.canon) return launch_knn_grid(kp, n_jobs, max_n, false, st);
+    if (kp.canon) return launch_knn_grid(kp, n_jobs, max_n, false, false, st);
     return launch_knn_pass(kp, n_jobs, max_n, st);
 }
 
@@ -263,35 +266,6 @@ static float morton_scale() {
         return v > 0.0f ? v : 4.0f;
     }();
     return scale;
-}
-
-// Morton (Z-order) permutation of the body points: 0.25 m cells, 20 bits/axis.
-// (k_fe_morton computes the same keys on the device for livo_scan_preprocess.)
-static std::vector<int32_t> morton_order(const std::vector<float>& p4, int64_t n) {
-    const float scale = morton_scale();
-    std::vector<std::pair<uint64_t, int32_t>> key((size_t)n);
-    float lo[3] = {INFINITY, INFINITY, INFINITY};
-    for (int64_t i = 0; i < n; i++)
-        for (int a = 0; a < 3; a++) lo[a] = std::min(lo[a], p4[4 * i + a]);
-    for (int64_t i = 0; i < n; i++) {
-        uint64_t code = 0;
-        uint32_t q[3];
-        for (int a = 0; a < 3; a++) {
-            float f = (p4[4 * i + a] - lo[a]) * scale;
-            if (!(f >= 0.0f)) f = 0.0f;
-            q[a] = (uint32_t)std::min(f, 1048575.0f);
-        }
-        for (int b = 0; b < 20; b++)
-            for (int a = 0; a < 3; a++) code |= (uint64_t)((q[a] >> b) & 1u) << (3 * b + a);
-        key[i] = {code, (int32_t)i};
-    }
-    std::stable_sort(key.begin(), key.end(),
-                     [](const std::pair<uint64_t, int32_t>& x, const std::pair<uint64_t, int32_t>& y) {
-                         return x.first < y.first;
-                     });
-    std::vector<int32_t> perm((size_t)n);
-    for (int64_t i = 0; i < n; i++) perm[i] = key[i].second;
-    return perm;
 }
 
 static HsParams make_hs_params(livo_ctx* c) {
@@ -309,12 +283,22 @@ static HsParams make_hs_params(livo_ctx* c) {
     return hp;
 }
 
+// doubles of a scan's block-partial buffer: the plane pass (kIkCols per
+// kBlock * kPtsPerThread points) or the fused evaluation (kRedCols per kEvalBlock)
+static size_t partial_doubles(int64_t N) {
+    const int64_t a = std::max<int64_t>(1, (N + kBlock * kPtsPerThread - 1) / (kBlock * kPtsPerThread)) * kIkCols;
+    const int64_t b = std::max<int64_t>(1, (N + kEvalBlock - 1) / kEvalBlock) * kRedCols;
+    return (size_t)std::max(a, b);
+}
+
 static void fill_job(HsJob& j, ScanBuf& s, IekfSlot* slot) {
     j.pts = s.pts;
     j.nn = s.nn;
     j.partial = s.partial;
     j.plane = s.plane;
     j.pstate = s.pstate;
+    j.ikrows = s.ikrows;
+    j.ikcnt = s.ikcnt;
     j.slot = slot;
     j.n = (int32_t)s.n;
     j.nblk = s.nblk;
@@ -558,7 +542,7 @@ static bool map_ready(const livo_ctx* c) {
 // overflow pass); `later`: an evaluation after the first (seeded / gated).
 static int backend_knn(livo_ctx* c, const KnnParams& kp, int n_jobs, int64_t max_n, bool later, hipStream_t st) {
     if (c->backend == LIVO_BACKEND_IVOX) return launch_ivox_knn(kp, n_jobs, max_n, later, c->iv.big_threads, st);
-    return c->knn_kind == 1 ? launch_knn_grid(kp, n_jobs, max_n, later, st)
+    return c->knn_kind >= 1 ? launch_knn_grid(kp, n_jobs, max_n, later, c->knn_kind == 2, st)
                             : launch_knn_leaf(kp, n_jobs, max_n, later, st);
 }
 
@@ -646,7 +630,7 @@ static int dyn_activate(livo_ctx* c) {
     DynDev& d = c->dyn;
     if (d.active) return LIVO_OK;
     if (!c->has_map) return LIVO_E_NOMAP;
-    if (c->knn_kind != 1) return LIVO_E_INVALID;  // kept on the cell grid (not LIVO_KNN_KIND=leaf)
+    if (c->knn_kind == 0) return LIVO_E_INVALID;  // kept on the cell grid (not LIVO_KNN_KIND=leaf)
     if (!d.ctr && (dev_alloc(&d.ctr, kDynCtrN) || dev_alloc(&d.dirty, kDynDirtyCap))) return LIVO_E_OOM;
     const int64_t M = c->map_points;
     d.n_ids = d.n_alive = 0;
@@ -869,7 +853,9 @@ int livo_ctx_create(int device, const livo_params* p, livo_ctx** out) {
         const int v = std::atoi(env);
         if (v >= 2 && v <= 256) c->leaf_size = v;
     }
-    if (const char* env = std::getenv("LIVO_KNN_KIND")) c->knn_kind = std::strcmp(env, "leaf") == 0 ? 0 : 1;
+    if (const char* env = std::getenv("LIVO_FUSED")) c->fused = std::atoi(env) != 0;
+    if (const char* env = std::getenv("LIVO_KNN_KIND"))
+        c->knn_kind = std::strcmp(env, "leaf") == 0 ? 0 : std::strcmp(env, "grid") == 0 ? 1 : 2;
     if (const char* env = std::getenv("LIVO_GRID_CELL")) {
         const float v = (float)std::atof(env);
         if (v > 0.f) c->grid_cell = v;
@@ -956,7 +942,7 @@ int livo_map_build(livo_ctx* c, const float* xyz, int64_t M, int64_t stride_byte
     if (rc) return rc;
     HostLeafMap lm;
     HostGridMap gm;
-    rc = c->knn_kind == 1 ? build_grid_map(xyz, M, stride_bytes, c->grid_cell, &gm)
+    rc = c->knn_kind >= 1 ? build_grid_map(xyz, M, stride_bytes, c->grid_cell, &gm)
                           : build_leaf_map(xyz, M, stride_bytes, c->leaf_size, &lm);
     if (rc) {
         free_host_map(&hm);
@@ -983,7 +969,7 @@ int livo_map_build(livo_ctx* c, const float* xyz, int64_t M, int64_t stride_byte
     const size_t ppb = (size_t)(M + 3) * 4 * sizeof(float);  // chunk padding
     hipError_t e = hipSuccess;
     bool oom = hipMalloc((void**)&c->nodes, bytes) != hipSuccess;
-    if (c->knn_kind == 1) {
+    if (c->knn_kind >= 1) {
         const size_t gsb = ((size_t)1 << gm.log2_slots) * sizeof(GridSlot);
         oom = oom || hipMalloc((void**)&c->gslots, gsb) != hipSuccess || hipMalloc((void**)&c->gpts, ppb) != hipSuccess;
         if (!oom) e = hipMemcpy(c->gslots, gm.slots, gsb, hipMemcpyHostToDevice);
@@ -1089,7 +1075,7 @@ static int32_t register_scan(livo_ctx* c, const ScanBuf& s) {
 
 static void free_scan_buf(ScanBuf& s) {
     dev_free(s.pts); dev_free(s.nn); dev_free(s.partial); dev_free(s.d_perm); dev_free(s.d_iperm);
-    dev_free(s.plane); dev_free(s.pstate);
+    dev_free(s.plane); dev_free(s.pstate); dev_free(s.ikrows); dev_free(s.ikcnt);
 }
 
 // A resident scan from N device points (x, y, z at d_src + stride * i floats):
@@ -1102,11 +1088,13 @@ static int scan_create_device(livo_ctx* c, const float* d_src, int stride, int64
     int rc = 0;
     rc |= dev_alloc(&s.pts, (size_t)N * 4);
     rc |= dev_alloc(&s.nn, (size_t)N);
-    rc |= dev_alloc(&s.partial, (size_t)std::max(s.nblk, 1) * kIkCols);
+    rc |= dev_alloc(&s.partial, partial_doubles(N));
     rc |= dev_alloc(&s.d_perm, (size_t)N);
     rc |= dev_alloc(&s.d_iperm, (size_t)N);
     rc |= dev_alloc(&s.plane, (size_t)N * 4);
     rc |= dev_alloc(&s.pstate, (size_t)N);
+    rc |= dev_alloc(&s.ikrows, (size_t)std::max(s.nblk, 1) * kIkFewRows * 13);
+    rc |= dev_alloc(&s.ikcnt, (size_t)std::max(s.nblk, 1));
     if (rc) {
         free_scan_buf(s);
         return LIVO_E_OOM;
@@ -1152,51 +1140,35 @@ int livo_scan_upload(livo_ctx* c, const float* xyz, int64_t N, int64_t stride_by
     if (stride_bytes == 0) stride_bytes = 3 * sizeof(float);
     if (stride_bytes < (int64_t)(3 * sizeof(float))) return LIVO_E_INVALID;
     if (set_device(c)) return LIVO_E_HIP;
-    ScanBuf s;
-    s.used = true;
-    s.n = N;
-    // at least one plane-pass block: its last block also runs the scan's solve
-    s.nblk = (int32_t)std::max<int64_t>(1, (N + kBlock * kPtsPerThread - 1) / (kBlock * kPtsPerThread));
-    int rc = 0;
-    rc |= dev_alloc(&s.pts, (size_t)N * 4);
-    rc |= dev_alloc(&s.nn, (size_t)N);
-    rc |= dev_alloc(&s.partial, (size_t)std::max(s.nblk, 1) * kIkCols);  // IKFoM partials are the wider
-    rc |= dev_alloc(&s.plane, (size_t)N * 4);
-    rc |= dev_alloc(&s.pstate, (size_t)N);
-    if (rc) {
-        free_scan_buf(s);
-        return LIVO_E_OOM;
-    }
+    // the caller's points packed to x, y, z (a strided PointType array is
+    // read once), copied to HBM, then Morton-ordered on the device
+    // (scan_create_device: the same keys and stable order as a host sort)
+    float* d_src = nullptr;
     if (N > 0) {
-        std::vector<float> h((size_t)N * 4), hs((size_t)N * 4);
         const char* base = (const char*)xyz;
-        for (int64_t i = 0; i < N; i++) {
-            const float* p = (const float*)(base + i * stride_bytes);
-            h[4 * i + 0] = p[0];
-            h[4 * i + 1] = p[1];
-            h[4 * i + 2] = p[2];
-            h[4 * i + 3] = 0.0f;
+        float* h = nullptr;
+        const bool packed = stride_bytes == (int64_t)(3 * sizeof(float));
+        if (!packed) {
+            h = (float*)std::malloc((size_t)N * 3 * sizeof(float));
+            if (!h) return LIVO_E_OOM;
+            for (int64_t i = 0; i < N; i++) std::memcpy(h + 3 * i, base + i * stride_bytes, 3 * sizeof(float));
         }
-        // stored in Morton order: neighbouring threads search neighbouring regions
-        s.perm = morton_order(h, N);
-        for (int64_t k = 0; k < N; k++)
-            for (int a = 0; a < 4; a++) hs[4 * k + a] = h[4 * (int64_t)s.perm[k] + a];
-        if (hipMemcpy(s.pts, hs.data(), hs.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) return LIVO_E_HIP;
-        if (hipMemset(s.nn, 0, (size_t)N * sizeof(NNRec)) != hipSuccess ||
-            hipMemset(s.pstate, 0, (size_t)N) != hipSuccess)
-            return LIVO_E_HIP;
-        std::vector<int32_t> iperm((size_t)N);
-        for (int64_t k = 0; k < N; k++) iperm[(size_t)s.perm[(size_t)k]] = (int32_t)k;
-        if (dev_alloc(&s.d_perm, (size_t)N) || dev_alloc(&s.d_iperm, (size_t)N)) {
-            free_scan_buf(s);
+        if (dev_alloc(&d_src, (size_t)N * 3)) {
+            std::free(h);
             return LIVO_E_OOM;
         }
-        if (hipMemcpy(s.d_perm, s.perm.data(), (size_t)N * 4, hipMemcpyHostToDevice) != hipSuccess ||
-            hipMemcpy(s.d_iperm, iperm.data(), (size_t)N * 4, hipMemcpyHostToDevice) != hipSuccess)
+        const hipError_t e = hipMemcpyAsync(d_src, packed ? xyz : h, (size_t)N * 3 * sizeof(float),
+                                            hipMemcpyHostToDevice, c->stream);
+        const hipError_t e2 = hipStreamSynchronize(c->stream);
+        std::free(h);
+        if (e != hipSuccess || e2 != hipSuccess) {
+            dev_free(d_src);
             return LIVO_E_HIP;
+        }
     }
-    *scan_id = register_scan(c, s);
-    return LIVO_OK;
+    const int rc = scan_create_device(c, d_src, 3, N, scan_id);
+    dev_free(d_src);
+    return rc;
 }
 
 int livo_scan_release(livo_ctx* c, int32_t id) {
@@ -1372,7 +1344,10 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
             ScanBuf* s = get_scan(c, ids[b]);
             if (s->n > 0) HIP_TRY(hipMemsetAsync(s->pstate, 0, (size_t)s->n, c->stream));
         }
-    HIP_TRY(hipMemcpyAsync(c->d_slots, c->h_slots, sizeof(IekfSlot) * n, hipMemcpyHostToDevice, c->stream));
+    // the LaserMapping model uses only the part of a slot before the IKFoM block
+    const size_t slot_w = model == kModelIkfom ? sizeof(IekfSlot) : kSlotLmBytes;
+    HIP_TRY(hipMemcpy2DAsync(c->d_slots, sizeof(IekfSlot), c->h_slots, sizeof(IekfSlot), slot_w, n,
+                             hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->d_jobs, c->h_jobs, sizeof(HsJob) * n, hipMemcpyHostToDevice, c->stream));
 
     // The batch in groups on separate streams: the latency-bound kernels of
@@ -1402,7 +1377,10 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
             off += s->n;
         }
     }
-    HIP_TRY(hipMemsetAsync(c->d_replay_count, 0, sizeof(unsigned) * kMaxGroups, c->stream));
+    // the fused evaluation: search + replay + plane pass + solve in one launch
+    const bool fused = c->fused && model == kModelLaserMapping && c->backend == LIVO_BACKEND_IKDTREE &&
+                       c->knn_kind == 2;
+    if (!fused) HIP_TRY(hipMemsetAsync(c->d_replay_count, 0, sizeof(unsigned) * kMaxGroups, c->stream));
     const bool prof = c->profiling && c->events_ready;  // 1: first-search events only
     const bool full = prof && c->profiling >= 2;         // 2: every evaluation's stages too
     // profiling: the batch's first search starts at ev[0][0], before the fork
@@ -1427,7 +1405,15 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
         hp[gi].replay_count = c->d_replay_count + gi;
     }
     for (int e = 0; e < evals; e++) {
-        for (int gi = 0; gi < ngroups; gi++) {
+        for (int gi = 0; gi < ngroups && fused; gi++) {
+            hipStream_t st = g[gi].st;
+            if (full && (e > 0 || gi > 0)) HIP_TRY(hipEventRecord(c->ev[gi][3 * e], st));
+            if (full && e > 0) HIP_TRY(hipEventRecord(c->ev[gi][3 * e + 1], st));
+            rc = launch_iekf_eval(kp[gi], hp[gi], g[gi].count, g[gi].max_n, e == 0, st);
+            if (rc) return rc;
+            if (prof && e == 0) HIP_TRY(hipEventRecord(c->ev[gi][1], st));
+        }
+        for (int gi = 0; gi < ngroups && !fused; gi++) {
             hipStream_t st = g[gi].st;
             if (full && (e > 0 || gi > 0)) HIP_TRY(hipEventRecord(c->ev[gi][3 * e], st));
             // leaf-map search; rematch passes are bounded by the previous neighbours
@@ -1442,17 +1428,17 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
     }
     for (int gi = 0; gi < ngroups; gi++)
         if (full) HIP_TRY(hipEventRecord(c->ev[gi][3 * LIVO_MAX_EVALS], g[gi].st));
-    for (int gi = 1; gi < ngroups; gi++) {
-        HIP_TRY(hipEventRecord(c->xjoin[gi - 1], g[gi].st));
-        HIP_TRY(hipStreamWaitEvent(c->stream, c->xjoin[gi - 1], 0));
-    }
-    HIP_TRY(hipMemcpyAsync(c->h_slots, c->d_slots, sizeof(IekfSlot) * n, hipMemcpyDeviceToHost, c->stream));
+    // each group copies its own slots back on its own stream (no cross-stream
+    // join before the copy); the host then waits for every group's stream
+    for (int gi = 0; gi < ngroups; gi++)
+        HIP_TRY(hipMemcpy2DAsync(c->h_slots + g[gi].first, sizeof(IekfSlot), c->d_slots + g[gi].first,
+                                 sizeof(IekfSlot), slot_w, g[gi].count, hipMemcpyDeviceToHost, g[gi].st));
     unsigned long long replays = 0;
-    if (prof) {
+    if (full) {
         HIP_TRY(hipMemcpyAsync(&replays, c->d_replay_total, 8, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipMemsetAsync(c->d_replay_total, 0, 8, c->stream));
     }
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (int gi = ngroups - 1; gi >= 0; gi--) HIP_TRY(hipStreamSynchronize(g[gi].st));
     for (int32_t b = 0; b < n; b++) {
         const IekfSlot& s = c->h_slots[b];
         if (model == kModelIkfom) {
@@ -2105,7 +2091,7 @@ int livo_map_dump(livo_ctx* c, float* xyz, int32_t* ids, int64_t cap, int64_t* n
             }
     } else {  // the static map: its search structure's points (x, y, z, index) by index
         const int64_t M = c->map_points;
-        const float* src = c->knn_kind == 1 ? c->gpts : c->lpts;
+        const float* src = c->knn_kind >= 1 ? c->gpts : c->lpts;
         std::vector<float> pts((size_t)M * 4);
         if (M > 0) HIP_TRY(hipMemcpy(pts.data(), src, pts.size() * sizeof(float), hipMemcpyDeviceToHost));
         p.resize((size_t)M * 3);

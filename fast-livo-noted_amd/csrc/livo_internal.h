@@ -8,7 +8,7 @@
 #include "stl_select.h"
 
 #ifndef LIVO_PTS_PER_THREAD
-#define LIVO_PTS_PER_THREAD 4
+#define LIVO_PTS_PER_THREAD 1  // plane pass: 1 point per thread (A/B on MI355X: 4 -> 1 = +7 % at config 2)
 #endif
 
 namespace livo {
@@ -173,6 +173,7 @@ struct IekfCtrl {
 };
 
 constexpr int kIkDim = LIVO_IKFOM_DOF;  // 23
+constexpr int kIkFewRows = kIkDim - 1;  // below 23 effective points the gain is formed in measurement space
 constexpr int kIkCols = 96;             // doubles per IKFoM block partial (92 used)
 constexpr int kIkUsed = 92;             // 78 HTH upper-tri + 12 HTh + residual sum + count
 
@@ -192,8 +193,6 @@ enum SlotModel { kModelLaserMapping = 0, kModelIkfom = 1 };
 struct alignas(16) IekfSlot {
     livo_state state;     // in/out
     livo_state prior;     // state_propagat
-    double G[kDim * kDim];
-    double Pinv[kDim * kDim];   // state.cov^-1, constant over one update
     double red[kRedCols];       // last reduced h_share sums (for livo_h_share)
     livo_iter_stats stats;
     IekfCtrl ctrl;
@@ -203,8 +202,9 @@ struct alignas(16) IekfSlot {
     unsigned hs_ticket;         // k_hshare blocks done in the current pass (the last one reduces)
     int32_t model;              // SlotModel
     unsigned pad_[2];
-    IkBlock ik;                 // model == kModelIkfom
+    IkBlock ik;                 // model == kModelIkfom (last: the LaserMapping model copies only the part before it)
 };
+constexpr size_t kSlotLmBytes = offsetof(IekfSlot, ik);  // bytes of a slot the LaserMapping model reads / writes
 
 // Nearest_Points[i] + pointSearchSqDis for one point: 128 B, written by the
 // k-NN pass, read by every plane-fit pass until the next search.
@@ -225,6 +225,8 @@ struct HsJob {
     IekfSlot* slot;
     float* plane;         // N x 4: esti_plane of the cached neighbours (k_hshare)
     uint8_t* pstate;      // N: 0 not fitted since the last search, 1 no plane, 2 plane
+    double* ikrows;       // IKFoM: nblk x kIkFewRows x 13 effective rows (h_x row, h) per block
+    uint32_t* ikcnt;      // IKFoM: nblk: effective rows of the block (capped at kIkFewRows + 1)
     int32_t n;
     int32_t nblk;
 };
@@ -303,8 +305,12 @@ int launch_knn_pass(const KnnParams& p, int n_jobs, int64_t max_n, void* stream)
 // Batched IEKF k-NN on the leaf map; seeded: rematch pass bounded by the
 // point's previous neighbours.  Both are followed by the exact tie replay.
 int launch_knn_leaf(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, void* stream);
-int launch_knn_grid(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, void* stream);
+// tile: the LDS-tiled variant (one wave per block), same answers
+int launch_knn_grid(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, bool tile, void* stream);
 int launch_hshare(const HsParams& p, int n_jobs, int max_nblk, bool first, void* stream);
+// One whole IEKF evaluation (search if due + plane pass + reduction + solve) per launch.
+constexpr int kEvalBlock = 256;  // threads (points) per block of k_iekf_eval
+int launch_iekf_eval(const KnnParams& kp, const HsParams& hp, int n_jobs, int64_t max_n, bool first, void* stream);
 // IKFoM plane pass (12-wide rows) with the manifold update in each scan's last block.
 int launch_hshare_ik(const HsParams& p, int n_jobs, int max_nblk, bool first, void* stream);
 int launch_solve(const SolveParams& p, int n_jobs, void* stream);

@@ -398,7 +398,7 @@ __device__ __forceinline__ int level_of(uint32_t h) { return 31 - __clz(h + 1); 
 // record for the son's box distance and re-checks it, which is exactly the
 // check a stack pop makes.  Same visits, same candidates, same order, ties
 // included.  Used for the rare queries the fast pass flags (k_knn_replay).
-__device__ __noinline__ void knn_exact(const MapNode* __restrict__ nodes, int has_map, float qx, float qy, float qz,
+__device__ __forceinline__ void knn_exact(const MapNode* __restrict__ nodes, int has_map, float qx, float qy, float qz,
                                        Cands& c) {
     KHeap h;
 #pragma unroll
@@ -747,8 +747,8 @@ __device__ __forceinline__ void lq_point(LeafQuery& q, const float4 v, uint32_t 
 // is a strict total order on the 5 points, so sorting by (dist, x) gives the
 // reference's order.  A gap in (0, 1e-10] (CMP not transitive) or an exact tie
 // with equal x (neither point "less") still goes to the exact replay.
-__device__ __forceinline__ void lq_finish(LeafQuery& q, const KnnParams& P, const HsJob& job, unsigned bjob,
-                                          int i, const float4* __restrict__ lpts, bool overrun) {
+__device__ __forceinline__ bool lq_finish(LeafQuery& q, const KnnParams& P, const HsJob& job, unsigned bjob,
+                                          int i, const float4* __restrict__ lpts, bool overrun, bool enqueue = true) {
     const int cnt = (int)min<int64_t>(P.lM, (int64_t)kNN);
     float4 a[kNN];
 #pragma unroll
@@ -802,7 +802,8 @@ __device__ __forceinline__ void lq_finish(LeafQuery& q, const KnnParams& P, cons
     oi[0] = make_int4(idx[0], idx[1], idx[2], idx[3]);
     oi[1] = make_int4(idx[4], cnt, flag, (int)q.nd[0]);
     oi[2] = make_int4((int)q.nd[1], (int)q.nd[2], (int)q.nd[3], (int)q.nd[4]);
-    if (amb) flag_for_replay(P, bjob, i);
+    if (amb && enqueue) flag_for_replay(P, bjob, i);
+    return amb;
 }
 
 // Q queries per thread walk the tree together (a box is entered if any of them
@@ -934,47 +935,270 @@ __device__ __forceinline__ unsigned long long grid_key_d(int cx, int cy, int cz)
 #ifndef LIVO_GRID_WAVES
 #define LIVO_GRID_WAVES 5  // waves per SIMD (VGPR budget 96: no spills)
 #endif
-template <bool SEEDED>
-__global__ __launch_bounds__(kKnnBlock, LIVO_GRID_WAVES) void k_knn_grid(KnnParams P) {
-    unsigned bjob, bx;
-    xcd_block(P.nb, bjob, bx);
-    const HsJob job = P.jobs[bjob];
-    IekfSlot* slot = job.slot;
-    if (P.force >= 0) {
-        if (!P.force) return;
-    } else {
-        if (slot->ctrl.stop) return;
-        if (SEEDED && !slot->ctrl.search_en) return;
+
+// --- LDS tiles ---------------------------------------------------------------
+// The scan is Morton-ordered, so the queries of a block lie a few cells
+// apart.  The block takes the box of cells within one cell of any of its
+// queries (at most CELLS cells), resolves every cell of the box through the
+// hash at once (threads probe in parallel), and copies the box's points into
+// LDS in cell order in one pass of independent loads.  Each thread then runs
+// exactly the stages of grid_search -- same cells, same order, same pruning,
+// so the same list, e6 and flags -- reading its cells from LDS instead of
+// chasing hash probe -> cell run -> points through L2.  Stage-2 or sparse-map
+// cells outside the box, and blocks whose box or points do not fit, take the
+// global path.
+template <int CELLS, int PTS>
+struct TileLds {
+    float4 pts[PTS + 4];      // the box's points (x, y, z, gpts index bits); +4: chunked reads
+    uint32_t off[CELLS + 1];  // LDS start of each cell's run
+    uint32_t start[CELLS];    // its start in gpts
+    uint32_t wred[16];        // per-wave partials of the block scans
+    int box[6 * 16];          // per-wave cell bounds
+};
+struct TileView {
+    bool on = false;
+    int lo0 = 0, lo1 = 0, lo2 = 0, hi0 = -1, hi1 = -1, hi2 = -1, d0 = 0, d1 = 0;
+    const float4* pts = nullptr;
+    const uint32_t* off = nullptr;
+};
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+// Block-wide inclusive scan (sum or max) of one value per thread; NT threads.
+template <int NT, bool MAX>
+__device__ __forceinline__ uint32_t block_incl_scan(uint32_t v, uint32_t* wred, uint32_t& total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(v, o, 64);
+        if (lane >= o) v = MAX ? (y > v ? y : v) : v + y;
     }
-    const int i = (int)bx * kKnnBlock + threadIdx.x;
-    if (i >= job.n) return;
+    if constexpr (NT == 64) {
+        total = __shfl(v, 63, 64);
+        return v;
+    } else {
+        if (lane == 63) wred[wave] = v;
+        __syncthreads();
+        uint32_t before = 0u, all = 0u;
+#pragma unroll
+        for (int w = 0; w < NT / 64; w++) {
+            const uint32_t t = wred[w];
+            if (w < wave) before = MAX ? (t > before ? t : before) : before + t;
+            all = MAX ? (t > all ? t : all) : all + t;
+        }
+        __syncthreads();
+        total = all;
+        return MAX ? (before > v ? before : v) : before + v;
+    }
+}
+
+// Builds the block's tile for the cells (c0, c1, c2) of its valid threads.
+// Every thread of the block calls it (NT threads).
+template <int NT, int CELLS, int PTS>
+__device__ __forceinline__ TileView build_tile(TileLds<CELLS, PTS>& L, const KnnParams& P, bool valid, int c0, int c1,
+                                               int c2, unsigned& visits, unsigned& npts) {
+    static_assert(CELLS % NT == 0 && PTS % NT == 0, "tile sizes");
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    TileView tv;
+    int b[6] = {wave_min_i(valid ? c0 : INT_MAX), wave_min_i(valid ? c1 : INT_MAX), wave_min_i(valid ? c2 : INT_MAX),
+                wave_max_i(valid ? c0 : INT_MIN), wave_max_i(valid ? c1 : INT_MIN), wave_max_i(valid ? c2 : INT_MIN)};
+    if constexpr (NT > 64) {
+        if (lane == 0)
+#pragma unroll
+            for (int k = 0; k < 6; k++) L.box[6 * wave + k] = b[k];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            int v = L.box[k];
+#pragma unroll
+            for (int w = 1; w < NT / 64; w++) v = k < 3 ? min(v, L.box[6 * w + k]) : max(v, L.box[6 * w + k]);
+            b[k] = v;
+        }
+        __syncthreads();
+    }
+    if (b[0] > b[3]) return tv;  // no valid thread
+    tv.lo0 = b[0] - 1; tv.lo1 = b[1] - 1; tv.lo2 = b[2] - 1;
+    tv.hi0 = b[3] + 1; tv.hi1 = b[4] + 1; tv.hi2 = b[5] + 1;
+    tv.d0 = tv.hi0 - tv.lo0 + 1;
+    tv.d1 = tv.hi1 - tv.lo1 + 1;
+    const long long vol = (long long)tv.d0 * tv.d1 * (long long)(tv.hi2 - tv.lo2 + 1);
+    if (!(P.lM > 0 && vol <= CELLS)) return tv;
+    const int V = (int)vol;
+    const GridSlot* __restrict__ slots = P.gslots;
+    const float4* __restrict__ gpts = reinterpret_cast<const float4*>(P.gpts);
+    const uint64_t mask = (1ull << P.glog2) - 1ull;
+    constexpr int kPer = CELLS / NT;
+    // 1. directory: every cell of the box through the hash, first probes in flight together
+    unsigned long long key[kPer];
+    uint64_t sl[kPer];
+    GridSlot gs[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; u++) {
+        const int t = tid + NT * u;
+        if (t < V) {
+            key[u] = grid_key_d(tv.lo0 + t % tv.d0, tv.lo1 + (t / tv.d0) % tv.d1, tv.lo2 + t / (tv.d0 * tv.d1));
+            sl[u] = (uint64_t)((key[u] * 0x9E3779B97F4A7C15ull) >> (64 - P.glog2));
+            gs[u] = slots[sl[u]];
+            visits++;
+        }
+    }
+    uint32_t cnt_u[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; u++) {
+        const int t = tid + NT * u;
+        cnt_u[u] = 0u;
+        if (t < V) {
+            while (gs[u].key != key[u] && gs[u].key != kGridEmpty) {  // linear probing
+                sl[u] = (sl[u] + 1) & mask;
+                gs[u] = slots[sl[u]];
+                visits++;
+            }
+            const bool hit = gs[u].key == key[u];
+            L.start[t] = hit ? gs[u].start : 0u;
+            cnt_u[u] = hit ? gs[u].count : 0u;
+            L.off[t] = cnt_u[u];
+        }
+    }
+    __syncthreads();
+    // 2. exclusive scan of the counts (thread: cells kPer*tid .. kPer*tid + kPer - 1)
+    uint32_t cc[kPer], loc = 0;
+#pragma unroll
+    for (int u = 0; u < kPer; u++) {
+        const int t = kPer * tid + u;
+        cc[u] = t < V ? L.off[t] : 0u;
+        loc += cc[u];
+    }
+    uint32_t total;
+    const uint32_t incl = block_incl_scan<NT, false>(loc, L.wred, total);
+    __syncthreads();  // every count read before the offsets overwrite them
+    uint32_t run = incl - loc;
+#pragma unroll
+    for (int u = 0; u < kPer; u++) {
+        const int t = kPer * tid + u;
+        if (t < V) L.off[t] = run;
+        run += cc[u];
+    }
+    if (tid == 0) L.off[V] = total;
+    if (total > (uint32_t)PTS) return tv;  // (block-uniform)
+    const int npt = (int)total;
+    for (int p = tid; p < npt; p += NT) L.pts[p].w = __uint_as_float(0u);
+    __syncthreads();
+    // 3. owner cell of every LDS point: each non-empty cell marks its first
+    // point, then an inclusive max-scan over the points
+#pragma unroll
+    for (int u = 0; u < kPer; u++) {
+        const int t = tid + NT * u;
+        if (t < V && cnt_u[u] > 0u) L.pts[L.off[t]].w = __uint_as_float((uint32_t)t);
+    }
+    __syncthreads();
+    constexpr int kPP = PTS / NT;
+    uint32_t ow[kPP], mx = 0u;
+#pragma unroll
+    for (int k = 0; k < kPP; k++) {
+        const int p = kPP * tid + k;
+        const uint32_t o = p < npt ? __float_as_uint(L.pts[p].w) : 0u;
+        mx = o > mx ? o : mx;
+        ow[k] = mx;
+    }
+    uint32_t all;
+    const uint32_t mi = block_incl_scan<NT, true>(mx, L.wred, all);
+    uint32_t carry = NT == 64 ? __shfl_up(mi, 1, 64) : 0u;
+    if constexpr (NT > 64) {
+        // exclusive max = the inclusive max of the previous thread
+        if (lane == 63) L.wred[wave] = mi;  // (block_incl_scan's own barriers are done)
+        const uint32_t up = __shfl_up(mi, 1, 64);
+        __syncthreads();
+        carry = lane > 0 ? up : (wave > 0 ? L.wred[wave - 1] : 0u);
+        __syncthreads();
+    } else if (lane == 0) {
+        carry = 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kPP; k++) {
+        const int p = kPP * tid + k;
+        if (p < npt) L.pts[p].w = __uint_as_float(ow[k] > carry ? ow[k] : carry);
+    }
+    __syncthreads();
+    // 4. copy: LDS point p = gpts[start[cell] + p - off[cell]], 8 loads in flight per thread
+    for (int p0 = 0; p0 < npt; p0 += NT * 8) {
+        uint32_t src[8];
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int p = p0 + NT * u + tid;
+            src[u] = 0u;
+            if (p < npt) {
+                const uint32_t t = __float_as_uint(L.pts[p].w);
+                src[u] = L.start[t] + (uint32_t)p - L.off[t];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+            if (p0 + NT * u + tid < npt) v[u] = gpts[src[u]];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int p = p0 + NT * u + tid;
+            if (p < npt) L.pts[p] = make_float4(v[u].x, v[u].y, v[u].z, __uint_as_float(src[u]));
+        }
+    }
+    if (tid == 0) npts += total;
+    __syncthreads();
+    tv.on = true;
+    tv.pts = L.pts;
+    tv.off = L.off;
+    return tv;
+}
+
+// Query cell and the side of it the query lies in (dir = -1 / +1 per axis).
+__device__ __forceinline__ void grid_cell(const KnnParams& P, const LeafQuery& q, int& c0, int& c1, int& c2, int& s0,
+                                          int& s1, int& s2) {
+    const float inv = 1.0f / P.gh;
+    auto cell_of = [&](float v, float o, int& c, int& dir) {
+        const float t = (v - o) * inv;
+        float f = floorf(t);
+        f = fminf(fmaxf(f, (float)(8 - kGridBias)), (float)(kGridBias - 8));  // NaN -> 8 - bias
+        c = (int)f;
+        dir = (t - f < 0.5f) ? -1 : 1;
+    };
+    cell_of(q.qx, P.gorg[0], c0, s0);
+    cell_of(q.qy, P.gorg[1], c1, s1);
+    cell_of(q.qz, P.gorg[2], c2, s2);
+}
+
+// The exact 5-NN of one query on the cell grid (stages 0-2 above); cells of an
+// active tile come from LDS.  Returns whether the list is certified exact.
+__device__ __forceinline__ bool grid_search(LeafQuery& q, const KnnParams& P, int c0, int c1, int c2, int s0, int s1,
+                                            int s2, const TileView& tv, unsigned& visits, unsigned& npts) {
     const float4* __restrict__ gpts = reinterpret_cast<const float4*>(P.gpts);
     const GridSlot* __restrict__ slots = P.gslots;
-    LeafQuery q;
-    lq_init<SEEDED>(q, P, slot, job, i, true);
-    const float h = P.gh, inv = 1.0f / h, eps = P.geps;
+    const float h = P.gh, eps = P.geps;
     const uint64_t mask = (1ull << P.glog2) - 1ull;
-    // query cell and the side of it the query lies in (dir = -1 / +1 per axis)
-    int c0, c1, c2, s0, s1, s2;
-    {
-        auto cell_of = [&](float v, float o, int& c, int& dir) {
-            const float t = (v - o) * inv;
-            float f = floorf(t);
-            f = fminf(fmaxf(f, (float)(8 - kGridBias)), (float)(kGridBias - 8));  // NaN -> 8 - bias
-            c = (int)f;
-            dir = (t - f < 0.5f) ? -1 : 1;
-        };
-        cell_of(q.qx, P.gorg[0], c0, s0);
-        cell_of(q.qy, P.gorg[1], c1, s1);
-        cell_of(q.qz, P.gorg[2], c2, s2);
-    }
-    unsigned visits = 0, npts = 0;  // hash slots and map points read
     auto visit = [&](int cx, int cy, int cz) __attribute__((always_inline)) {
         const float x0 = P.gorg[0] + (float)cx * h - eps, y0 = P.gorg[1] + (float)cy * h - eps;
         const float z0 = P.gorg[2] + (float)cz * h - eps;
         const float w = h + 2 * eps;
         const float bd = box_dist(q.qx, q.qy, q.qz, x0, x0 + w, y0, y0 + w, z0, z0 + w);
         if (bd - lq_thr(q) > kFuzz) return;
+        if (tv.on && cx >= tv.lo0 && cx <= tv.hi0 && cy >= tv.lo1 && cy <= tv.hi1 && cz >= tv.lo2 && cz <= tv.hi2) {
+            const int t = ((cz - tv.lo2) * tv.d1 + (cy - tv.lo1)) * tv.d0 + (cx - tv.lo0);
+            const int lo = (int)tv.off[t], hi = (int)tv.off[t + 1];
+            for (int k0 = lo; k0 < hi; k0 += 4) {
+                float4 v[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) v[u] = tv.pts[k0 + u];  // padded by 4 points
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    if (k0 + u < hi) lq_point(q, v[u], __float_as_uint(v[u].w));
+            }
+            return;
+        }
         const unsigned long long key = grid_key_d(cx, cy, cz);
         uint64_t sl = (uint64_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - P.glog2));
         GridSlot gs = slots[sl];
@@ -1024,48 +1248,91 @@ __global__ __launch_bounds__(kKnnBlock, LIVO_GRID_WAVES) void k_knn_grid(KnnPara
         r = CBox{(int)l0, (int)h0, (int)l1, (int)h1, (int)l2, (int)h2};
         return true;
     };
-    bool certified = false;
-    if (P.lM > 0) {
-        // stage 0: the 2x2x2 block, own cell first
+    if (!(P.lM > 0)) return false;
+    // stage 0: the 2x2x2 block, own cell first
 #pragma unroll 1
-        for (int b = 0; b < 8; b++)
-            visit(c0 + ((b & 1) ? s0 : 0), c1 + ((b & 2) ? s1 : 0), c2 + ((b & 4) ? s2 : 0));
-        const CBox blk{c0 + min(s0, 0), c0 + max(s0, 0), c1 + min(s1, 0), c1 + max(s1, 0), c2 + min(s2, 0),
-                       c2 + max(s2, 0)};
-        const CBox cube{c0 - 1, c0 + 1, c1 - 1, c1 + 1, c2 - 1, c2 + 1};
-        // stage 1: within the 3x3x3 cube, the cells the current bound still
-        // reaches (all of them while fewer than 5 points are known)
-        CBox r1 = cube;
-        if (lq_thr(q) < INFINITY && range_of(lq_thr(q), r1)) {
-            r1.l0 = max(r1.l0, cube.l0); r1.h0 = min(r1.h0, cube.h0);
-            r1.l1 = max(r1.l1, cube.l1); r1.h1 = min(r1.h1, cube.h1);
-            r1.l2 = max(r1.l2, cube.l2); r1.h2 = min(r1.h2, cube.h2);
-        } else {
-            r1 = cube;
-        }
-        scan_box(r1, blk);
-        // still fewer than 5 points (sparse map): cubes of radius 2, 3, ...
-        CBox vis = cube;
+    for (int b = 0; b < 8; b++)
+        visit(c0 + ((b & 1) ? s0 : 0), c1 + ((b & 2) ? s1 : 0), c2 + ((b & 4) ? s2 : 0));
+    const CBox blk{c0 + min(s0, 0), c0 + max(s0, 0), c1 + min(s1, 0), c1 + max(s1, 0), c2 + min(s2, 0),
+                   c2 + max(s2, 0)};
+    const CBox cube{c0 - 1, c0 + 1, c1 - 1, c1 + 1, c2 - 1, c2 + 1};
+    // stage 1: within the 3x3x3 cube, the cells the current bound still
+    // reaches (all of them while fewer than 5 points are known)
+    CBox r1 = cube;
+    if (lq_thr(q) < INFINITY && range_of(lq_thr(q), r1)) {
+        r1.l0 = max(r1.l0, cube.l0); r1.h0 = min(r1.h0, cube.h0);
+        r1.l1 = max(r1.l1, cube.l1); r1.h1 = min(r1.h1, cube.h1);
+        r1.l2 = max(r1.l2, cube.l2); r1.h2 = min(r1.h2, cube.h2);
+    } else {
+        r1 = cube;
+    }
+    scan_box(r1, blk);
+    // still fewer than 5 points (sparse map): cubes of radius 2, 3, ...
+    CBox vis = cube;
 #pragma unroll 1
-        for (int rr = 2; rr <= kGridMaxRing && !(lq_thr(q) < INFINITY); rr++) {
-            const CBox nb{c0 - rr, c0 + rr, c1 - rr, c1 + rr, c2 - rr, c2 + rr};
-            scan_box(nb, vis);
-            vis = nb;
-        }
-        // stage 2: every cell the final bound reaches; the list is then exact.
-        // The bound only shrank, so the cells of `vis` it reaches are scanned
-        // (r1 / the block / the cubes; a cell skipped there was beyond the bound)
-        CBox r2;
-        const float t = lq_thr(q);
-        if (t < INFINITY && range_of(t, r2)) {
-            const double span = (double)(r2.h0 - r2.l0 + 1) * (double)(r2.h1 - r2.l1 + 1) * (double)(r2.h2 - r2.l2 + 1);
-            if (span <= (double)kGridMaxCells) {
-                scan_box(r2, vis);
-                certified = true;
-            }
+    for (int rr = 2; rr <= kGridMaxRing && !(lq_thr(q) < INFINITY); rr++) {
+        const CBox nb{c0 - rr, c0 + rr, c1 - rr, c1 + rr, c2 - rr, c2 + rr};
+        scan_box(nb, vis);
+        vis = nb;
+    }
+    // stage 2: every cell the final bound reaches; the list is then exact.
+    // The bound only shrank, so the cells of `vis` it reaches are scanned
+    // (r1 / the block / the cubes; a cell skipped there was beyond the bound)
+    CBox r2;
+    const float t = lq_thr(q);
+    if (t < INFINITY && range_of(t, r2)) {
+        const double span = (double)(r2.h0 - r2.l0 + 1) * (double)(r2.h1 - r2.l1 + 1) * (double)(r2.h2 - r2.l2 + 1);
+        if (span <= (double)kGridMaxCells) {
+            scan_box(r2, vis);
+            return true;
         }
     }
-    lq_finish(q, P, job, bjob, i, gpts, !certified);
+    return false;
+}
+
+// 512 points / 128 cells per wave (10.5 KB): 4 waves per SIMD (VGPR-bound);
+// on MI355X 1024 / 256 (18.5 KB, 2 waves per SIMD) was 12 % slower at config 2
+#ifndef LIVO_TILE_CELLS
+#define LIVO_TILE_CELLS 128
+#endif
+#ifndef LIVO_TILE_PTS
+#define LIVO_TILE_PTS 512
+#endif
+using WaveTile = TileLds<LIVO_TILE_CELLS, LIVO_TILE_PTS>;
+// the block's tile (instantiated only by the TILE kernels)
+__device__ __forceinline__ WaveTile& wave_tile_lds() {
+    __shared__ WaveTile t;
+    return t;
+}
+
+template <bool SEEDED, bool TILE>
+__global__ __launch_bounds__(TILE ? 64 : kKnnBlock, TILE ? 4 : LIVO_GRID_WAVES) void k_knn_grid(KnnParams P) {
+    constexpr int kB = TILE ? 64 : kKnnBlock;
+    unsigned bjob, bx;
+    xcd_block(P.nb, bjob, bx);
+    const HsJob job = P.jobs[bjob];
+    IekfSlot* slot = job.slot;
+    if (P.force >= 0) {
+        if (!P.force) return;
+    } else {
+        if (slot->ctrl.stop) return;
+        if (SEEDED && !slot->ctrl.search_en) return;
+    }
+    const int i = (int)bx * kB + threadIdx.x;
+    // the tile is built by the whole block: threads past the scan's end stay
+    if (TILE ? (int)bx * kB >= job.n : i >= job.n) return;
+    const bool valid = i < job.n;
+    LeafQuery q;
+    lq_init<SEEDED>(q, P, slot, job, i, valid);
+    int c0 = 0, c1 = 0, c2 = 0, s0 = 1, s1 = 1, s2 = 1;
+    if (valid) grid_cell(P, q, c0, c1, c2, s0, s1, s2);
+    unsigned visits = 0, npts = 0;  // hash slots and map points read from global memory
+    TileView tv;
+    if constexpr (TILE) tv = build_tile<64>(wave_tile_lds(), P, valid, c0, c1, c2, visits, npts);
+    if (valid) {
+        const bool certified = grid_search(q, P, c0, c1, c2, s0, s1, s2, tv, visits, npts);
+        lq_finish(q, P, job, bjob, i, reinterpret_cast<const float4*>(P.gpts), !certified);
+    }
     count_visits(P, slot, visits, npts);
 }
 
@@ -1073,7 +1340,8 @@ __global__ __launch_bounds__(kKnnBlock, LIVO_GRID_WAVES) void k_knn_grid(KnnPara
 // KD_TREE::Search's visiting order with the far sons on an LDS stack and the
 // exact MANUAL_HEAP (rare: ties / duplicates; one query per thread).
 __global__ __launch_bounds__(64) void k_knn_replay(KnnParams P) {
-    __shared__ uint2 st_lds[kMaxDepth * 64];
+    extern __shared__ __attribute__((aligned(16))) unsigned char replay_smem[];  // (tree depth) x 64 stack entries
+    uint2* const st_lds = reinterpret_cast<uint2*>(replay_smem);
     const unsigned n = *P.replay_count;
     if (blockIdx.x == 0 && threadIdx.x == 0 && n) atomicAdd(P.replay_total, (unsigned long long)n);
     uint2* stack = st_lds + threadIdx.x;
@@ -1143,15 +1411,10 @@ constexpr int kCanonMaxCells = 1 << 15;
 __device__ __forceinline__ bool canon_less(float d1, float x1, uint32_t i1, float d2, float x2, uint32_t i2) {
     return d1 < d2 || (d1 == d2 && (x1 < x2 || (x1 == x2 && i1 < i2)));
 }
-__global__ __launch_bounds__(64) void k_knn_canon(KnnParams P) {
-    const unsigned n = *P.replay_count;
-    if (blockIdx.x == 0 && threadIdx.x == 0 && n) atomicAdd(P.replay_total, (unsigned long long)n);
+__device__ __forceinline__ void canon_query(const KnnParams& P, const HsJob& job, int i) {
     const float4* __restrict__ gpts = reinterpret_cast<const float4*>(P.gpts);
     const uint64_t mask = (1ull << P.glog2) - 1ull;
-    for (unsigned t = blockIdx.x * 64 + threadIdx.x; t < n; t += gridDim.x * 64) {
-        const unsigned long long e = P.replay_list[t];
-        const HsJob job = P.jobs[(unsigned)(e >> 32)];
-        const int i = (int)(unsigned)(e & 0xffffffffu);
+    {
         float qx, qy, qz;
         query_point(P, job.slot, reinterpret_cast<const float4*>(job.pts)[i], qx, qy, qz);
         NNRec* rec = job.nn + i;
@@ -1237,6 +1500,14 @@ __global__ __launch_bounds__(64) void k_knn_canon(KnnParams P) {
         oi[0] = make_int4(idx[0], idx[1], idx[2], idx[3]);
         oi[1] = make_int4(idx[4], cnt, flag, (int)bs[0]);
         oi[2] = make_int4((int)bs[1], (int)bs[2], (int)bs[3], (int)bs[4]);
+    }
+}
+__global__ __launch_bounds__(64) void k_knn_canon(KnnParams P) {
+    const unsigned n = *P.replay_count;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && n) atomicAdd(P.replay_total, (unsigned long long)n);
+    for (unsigned t = blockIdx.x * 64 + threadIdx.x; t < n; t += gridDim.x * 64) {
+        const unsigned long long e = P.replay_list[t];
+        canon_query(P, P.jobs[(unsigned)(e >> 32)], (int)(unsigned)(e & 0xffffffffu));
     }
 }
 
@@ -1583,12 +1854,193 @@ __device__ __forceinline__ void solve_scan(IekfSlot* slot, SolveLds& L, const in
 }
 
 // ===================================================== per-point pass =====
+// One point of h_share_model (laser_mapping.cpp:503-593): world point, gate,
+// plane (esti_plane, or the plane cached since the last search), residual
+// gates, Jacobian row and its HᵀH / HᵀL terms added to acc.
+__device__ __forceinline__ void hshare_point(const HsParams& P, const HsJob& job, const livo_state& S, int i,
+                                             int search, double (&acc)[kRedUsed]) {
+            const float4 pb = reinterpret_cast<const float4*>(job.pts)[i];
+            const double* R = S.rot;
+            float wx, wy, wz;
+            world_point(R, S.pos, P.R_LI, P.t_LI, pb.x, pb.y, pb.z, wx, wy, wz);
+            if (P.dbg.world) {
+                P.dbg.world[3 * i + 0] = wx;
+                P.dbg.world[3 * i + 1] = wy;
+                P.dbg.world[3 * i + 2] = wz;
+            }
+            // esti_plane depends only on the 5 cached neighbours (Nearest_Points),
+            // so an evaluation without a search refits exactly the plane of the
+            // last one: the plane is kept per point (job.plane / job.pstate:
+            // 0 not fitted yet, 1 no plane, 2 plane) and reused bit for bit.
+            bool plane_ok = false;
+            float pa[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+            uint8_t ps = search ? 0 : job.pstate[i];
+            if (ps == 0) {
+                const float4* rec = reinterpret_cast<const float4*>(job.nn + i);
+                float nx[kNN], ny[kNN], nz[kNN];
+                float d4 = 0.0f;
+    #pragma unroll
+                for (int k = 0; k < kNN; k++) {
+                    const float4 v = rec[k];
+                    nx[k] = v.x; ny[k] = v.y; nz[k] = v.z;
+                    if (k == kNN - 1) d4 = v.w;
+                }
+                const int cnt = reinterpret_cast<const int4*>(job.nn + i)[6].y;
+                // point_selected_surf: sqdis[4] > 5 => false after a search (:518); true otherwise (:490)
+                const bool sel = search ? ((cnt == kNN) && !(d4 > P.max_sqd)) : true;
+                if (cnt < kNN) {
+                    ps = 1;  // points_near.size() < 5 (:525) until the next search
+                } else if (sel) {
+                    plane_ok = esti_plane(nx, ny, nz, P.plane_thr, pa);
+                    ps = plane_ok ? 2 : 1;
+                }
+                // (a searched point beyond the sqdist gate stays 0: the next
+                // evaluation without a search fits it, as the reference does)
+                job.pstate[i] = ps;
+                if (plane_ok) reinterpret_cast<float4*>(job.plane)[i] = make_float4(pa[0], pa[1], pa[2], pa[3]);
+            } else if (ps == 2) {
+                const float4 v = reinterpret_cast<const float4*>(job.plane)[i];
+                pa[0] = v.x; pa[1] = v.y; pa[2] = v.z; pa[3] = v.w;
+                plane_ok = true;
+            }
+            bool accepted = false, keep = false;
+            float pd2 = 0.0f;
+            if (plane_ok) {
+                pd2 = ((pa[0] * wx + pa[1] * wy) + pa[2] * wz) + pa[3];
+                const double bx = pb.x, by = pb.y, bz = pb.z;
+                const double bn = sqrt((bx * bx + by * by) + bz * bz);
+                const float s = (float)(1 - 0.9 * (double)fabsf(pd2) / sqrt(bn));
+                accepted = (double)s > 0.9;                          // :535-542
+                keep = accepted && (double)fabsf(pd2) <= P.max_res;  // :552
+            }
+            if (P.dbg.normvec)
+                reinterpret_cast<float4*>(P.dbg.normvec)[i] =
+                    accepted ? make_float4(pa[0], pa[1], pa[2], pd2) : make_float4(0.f, 0.f, 0.f, 0.f);
+            if (P.dbg.sel) P.dbg.sel[i] = keep ? 1 : 0;
+            if (keep) {
+                // Jacobian row (laser_mapping.cpp:564-593): p_I = R_LI p_b + t_LI;
+                // A = [p_I]x * rot^T * n;  Hsub = [A, n]
+                const double bx = pb.x, by = pb.y, bz = pb.z;
+                const double* RL = P.R_LI;
+                const double ix = ((RL[0] * bx + RL[1] * by) + RL[2] * bz) + P.t_LI[0];
+                const double iy = ((RL[3] * bx + RL[4] * by) + RL[5] * bz) + P.t_LI[1];
+                const double iz = ((RL[6] * bx + RL[7] * by) + RL[8] * bz) + P.t_LI[2];
+                const double cr[9] = {0.0, -iz, iy, iz, 0.0, -ix, -iy, ix, 0.0};
+                double M[9];
+    #pragma unroll
+                for (int r = 0; r < 3; r++)
+    #pragma unroll
+                    for (int cI = 0; cI < 3; cI++)
+                        M[r * 3 + cI] = (cr[r * 3 + 0] * R[cI * 3 + 0] + cr[r * 3 + 1] * R[cI * 3 + 1]) +
+                                        cr[r * 3 + 2] * R[cI * 3 + 2];
+                const double n0 = pa[0], n1 = pa[1], n2 = pa[2];
+                double H[6];
+                H[0] = (M[0] * n0 + M[1] * n1) + M[2] * n2;
+                H[1] = (M[3] * n0 + M[4] * n1) + M[5] * n2;
+                H[2] = (M[6] * n0 + M[7] * n1) + M[8] * n2;
+                H[3] = n0; H[4] = n1; H[5] = n2;
+                const double err = -(double)pd2;
+                int q = 0;
+    #pragma unroll
+                for (int r = 0; r < 6; r++) {
+                    const double hs = H[r] * P.inv_r;
+    #pragma unroll
+                    for (int cI = r; cI < 6; cI++) acc[q++] += hs * H[cI];
+                }
+    #pragma unroll
+                for (int r = 0; r < 6; r++) acc[21 + r] += (H[r] * P.inv_r) * err;
+                acc[27] += (double)fabsf(pd2);
+                acc[28] += 1.0;
+            }
+}
+
+// Block partials of a scan's h_share sums -> the last block of the scan
+// reduces every partial in a fixed order and (P.solve) its wave 0 runs the
+// scan's solve.  nblk = blocks of the scan in this launch, NT threads.
+struct HsReduceLds {
+    double red[16 * kRedCols];
+    double fin[8 * kRedCols];
+    int last;
+};
+template <int NT>
+__device__ __forceinline__ void hshare_reduce_solve(const HsParams& P, const HsJob& job, IekfSlot* slot,
+                                                    double (&acc)[kRedUsed], int nblk, unsigned blk, HsReduceLds& R,
+                                                    SolveLds& L) {
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    constexpr int NW = NT / 64;
+#pragma unroll
+    for (int j = 0; j < kRedUsed; j++) {
+        const double v = wave_sum(acc[j]);
+        if (lane == 0) R.red[wave * kRedCols + j] = v;
+    }
+    __syncthreads();
+    // Wave 0 stores the block partial write-through (sc1) and, once the store
+    // has drained, takes the scan's ticket; the last block of the scan then
+    // reduces every partial with sc1 loads in a fixed order and its wave 0 runs
+    // the scan's solve (MI355X_MICROARCH.md §Workgroup dispatch: sc1 hand-off,
+    // no L2 write-back fence).  One launch less per evaluation than a separate
+    // solve kernel.
+    if (tid < 64) {
+        if (tid < kRedUsed) {
+            double v = R.red[tid];
+#pragma unroll
+            for (int w = 1; w < NW; w++) v = v + R.red[w * kRedCols + tid];
+            __hip_atomic_store(job.partial + (size_t)blk * kRedCols + tid, v, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (tid == 0)
+            R.last = __hip_atomic_fetch_add(&slot->hs_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                     (unsigned)nblk - 1u;
+    }
+    __syncthreads();
+    if (!R.last) return;
+    {
+        // thread (g, c) sums blocks g, g+G, ... of column c, 16 loads in flight (G = NT / 32 groups)
+        constexpr int G = NT / 32;
+        const int c = tid & 31, g = tid >> 5;
+        double acc16 = 0.0;
+        if (c < kRedUsed) {
+            double* src = job.partial + c;
+            for (int b0 = g; b0 < nblk; b0 += 16 * G) {
+                double v[16];
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    const int b = b0 + G * k;
+                    v[k] = b < nblk ? __hip_atomic_load(src + (size_t)b * kRedCols, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT)
+                                    : 0.0;
+                }
+#pragma unroll
+                for (int k = 0; k < 16; k++) acc16 += v[k];
+            }
+        }
+        R.fin[g * kRedCols + c] = acc16;
+    }
+    __syncthreads();
+    if (tid >= 64) return;  // the solve is one wave's work
+    if (tid < kRedCols) {
+        double v = 0.0;
+        if (tid < kRedUsed) {
+            double f[8];
+#pragma unroll
+            for (int g = 0; g < 8; g++) f[g] = g < NT / 32 ? R.fin[g * kRedCols + tid] : 0.0;
+            v = ((f[0] + f[1]) + (f[2] + f[3])) + ((f[4] + f[5]) + (f[6] + f[7]));
+        }
+        L.sum[tid] = v;
+        slot->red[tid] = v;
+    }
+    if (tid == 0) slot->hs_ticket = 0u;  // ready for the next pass
+    if (!P.solve) return;  // livo_h_share: the sums only
+    WAVE_SYNC();
+    solve_scan(slot, L, tid);
+}
+
 template <bool FIRST>
 __global__ __launch_bounds__(kBlock) void k_hshare(HsParams P) {
-    __shared__ double red_lds[4 * kRedCols];
-    __shared__ double fin_lds[8 * kRedCols];
+    __shared__ HsReduceLds R;
     __shared__ SolveLds L;
-    __shared__ int last_lds;
     const HsJob job = P.jobs[blockIdx.y];
     // the k-NN replay of this evaluation has run (stream order): reset its count
     if (P.replay_count && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *P.replay_count = 0u;
@@ -1601,176 +2053,104 @@ __global__ __launch_bounds__(kBlock) void k_hshare(HsParams P) {
         if (slot->ctrl.stop) return;  // block-uniform
         search = FIRST ? 1 : slot->ctrl.search_en;
     }
-    const int tid = threadIdx.x;
     const livo_state& S = slot->state;
     double acc[kRedUsed];
 #pragma unroll
     for (int j = 0; j < kRedUsed; j++) acc[j] = 0.0;
-
     for (int rep = 0; rep < kPtsPerThread; rep++) {  // points of this block: strided for coalescing
-    const int i = (blockIdx.x * kPtsPerThread + rep) * kBlock + tid;
+        const int i = (blockIdx.x * kPtsPerThread + rep) * kBlock + threadIdx.x;
+        if (i < job.n) hshare_point(P, job, S, i, search, acc);
+    }
+    hshare_reduce_solve<kBlock>(P, job, slot, acc, job.nblk, blockIdx.x, R, L);
+}
+
+// ================================================ fused evaluation =======
+// k_iekf_eval<FIRST>: one evaluation of the IEKF loop (laser_mapping.cpp:
+// 178-237) for every point of a batch of scans in ONE launch per stream group.
+// Each 256-thread block takes 256 Morton-consecutive points of one scan:
+//   - if the evaluation searches (the first one, or nearest_search_en set by
+//     the previous solve): the LDS-tiled cell-grid k-NN of its points (one
+//     block-wide tile of the box of cells within one cell of any of them),
+//     seeded by the previous neighbours after the first evaluation; the rare
+//     queries whose answer depends on the reference's tie order are recomputed
+//     in place by the same thread (knn_exact on the ikd-Tree records, or the
+//     canonical order on an incremental map);
+//   - the plane fit / residual / Jacobian of each point (hshare_point);
+//   - block partials, and the scan's last block reduces them and runs the solve.
+// Evaluations of a stopped scan exit at the first instruction.  Replaces the
+// k-NN launch, the replay launch and the plane-pass launch of each
+// evaluation; answers identical to those kernels.
+#ifndef LIVO_EVAL_TILE_CELLS
+#define LIVO_EVAL_TILE_CELLS 256
+#endif
+#ifndef LIVO_EVAL_TILE_PTS
+#define LIVO_EVAL_TILE_PTS 1024
+#endif
+using BlockTile = TileLds<LIVO_EVAL_TILE_CELLS, LIVO_EVAL_TILE_PTS>;
+
+__device__ __forceinline__ void replay_query(const KnnParams& P, const HsJob& job, int i) {
+    float qx, qy, qz;
+    query_point(P, job.slot, reinterpret_cast<const float4*>(job.pts)[i], qx, qy, qz);
+    Cands c;
+    knn_exact(P.nodes, P.has_map, qx, qy, qz, c);
+    float od[kNN];
+    uint32_t on[kNN];
+#pragma unroll
+    for (int k = 0; k < kNN; k++) { od[k] = c.d[k]; on[k] = c.node[k]; }
+    write_nnrec(job.nn + i, P.nodes, c.n, od, on, job.nn[i].flag | 0x100);
+}
+
+struct EvalParams {
+    KnnParams k;
+    HsParams h;
+};
+
+#ifndef LIVO_EVAL_WAVES
+#define LIVO_EVAL_WAVES 4  // waves per SIMD the VGPR budget must allow (<= 128 VGPRs)
+#endif
+template <bool FIRST>
+__global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalParams E) {
+    const KnnParams& P = E.k;
+    __shared__ union {
+        BlockTile tile;
+        SolveLds solve;  // the scan's last block solves after its search is done
+    } U;
+    __shared__ HsReduceLds R;
+    unsigned bjob, bx;
+    xcd_block(P.nb, bjob, bx);
+    const HsJob job = P.jobs[bjob];
+    IekfSlot* slot = job.slot;
+    if (slot->ctrl.stop) return;  // block-uniform
+    if (bx > 0 && (int)bx * kEvalBlock >= job.n) return;  // (an empty scan keeps one block: it solves)
+    const int search = FIRST ? 1 : slot->ctrl.search_en;
+    const int i = (int)bx * kEvalBlock + threadIdx.x;
     const bool valid = i < job.n;
-    if (valid) {
-        const float4 pb = reinterpret_cast<const float4*>(job.pts)[i];
-        const double* R = S.rot;
-        float wx, wy, wz;
-        world_point(R, S.pos, P.R_LI, P.t_LI, pb.x, pb.y, pb.z, wx, wy, wz);
-        if (P.dbg.world) {
-            P.dbg.world[3 * i + 0] = wx;
-            P.dbg.world[3 * i + 1] = wy;
-            P.dbg.world[3 * i + 2] = wz;
+    if (search) {
+        LeafQuery q;
+        lq_init<!FIRST>(q, P, slot, job, i, valid);
+        int c0 = 0, c1 = 0, c2 = 0, s0 = 1, s1 = 1, s2 = 1;
+        if (valid) grid_cell(P, q, c0, c1, c2, s0, s1, s2);
+        unsigned visits = 0, npts = 0;
+        const TileView tv = build_tile<kEvalBlock>(U.tile, P, valid, c0, c1, c2, visits, npts);
+        bool amb = false;
+        if (valid) {
+            const bool certified = grid_search(q, P, c0, c1, c2, s0, s1, s2, tv, visits, npts);
+            amb = lq_finish(q, P, job, bjob, i, reinterpret_cast<const float4*>(P.gpts), !certified, false);
         }
-        // esti_plane depends only on the 5 cached neighbours (Nearest_Points),
-        // so an evaluation without a search refits exactly the plane of the
-        // last one: the plane is kept per point (job.plane / job.pstate:
-        // 0 not fitted yet, 1 no plane, 2 plane) and reused bit for bit.
-        bool plane_ok = false;
-        float pa[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        uint8_t ps = search ? 0 : job.pstate[i];
-        if (ps == 0) {
-            const float4* rec = reinterpret_cast<const float4*>(job.nn + i);
-            float nx[kNN], ny[kNN], nz[kNN];
-            float d4 = 0.0f;
-#pragma unroll
-            for (int k = 0; k < kNN; k++) {
-                const float4 v = rec[k];
-                nx[k] = v.x; ny[k] = v.y; nz[k] = v.z;
-                if (k == kNN - 1) d4 = v.w;
-            }
-            const int cnt = reinterpret_cast<const int4*>(job.nn + i)[6].y;
-            // point_selected_surf: sqdis[4] > 5 => false after a search (:518); true otherwise (:490)
-            const bool sel = search ? ((cnt == kNN) && !(d4 > P.max_sqd)) : true;
-            if (cnt < kNN) {
-                ps = 1;  // points_near.size() < 5 (:525) until the next search
-            } else if (sel) {
-                plane_ok = esti_plane(nx, ny, nz, P.plane_thr, pa);
-                ps = plane_ok ? 2 : 1;
-            }
-            // (a searched point beyond the sqdist gate stays 0: the next
-            // evaluation without a search fits it, as the reference does)
-            job.pstate[i] = ps;
-            if (plane_ok) reinterpret_cast<float4*>(job.plane)[i] = make_float4(pa[0], pa[1], pa[2], pa[3]);
-        } else if (ps == 2) {
-            const float4 v = reinterpret_cast<const float4*>(job.plane)[i];
-            pa[0] = v.x; pa[1] = v.y; pa[2] = v.z; pa[3] = v.w;
-            plane_ok = true;
+        count_visits(P, slot, visits, npts);
+        if (amb) {
+            atomicAdd(P.replay_total, 1ull);
+            if (P.canon) canon_query(P, job, i);
+            else replay_query(P, job, i);
         }
-        bool accepted = false, keep = false;
-        float pd2 = 0.0f;
-        if (plane_ok) {
-            pd2 = ((pa[0] * wx + pa[1] * wy) + pa[2] * wz) + pa[3];
-            const double bx = pb.x, by = pb.y, bz = pb.z;
-            const double bn = sqrt((bx * bx + by * by) + bz * bz);
-            const float s = (float)(1 - 0.9 * (double)fabsf(pd2) / sqrt(bn));
-            accepted = (double)s > 0.9;                          // :535-542
-            keep = accepted && (double)fabsf(pd2) <= P.max_res;  // :552
-        }
-        if (P.dbg.normvec)
-            reinterpret_cast<float4*>(P.dbg.normvec)[i] =
-                accepted ? make_float4(pa[0], pa[1], pa[2], pd2) : make_float4(0.f, 0.f, 0.f, 0.f);
-        if (P.dbg.sel) P.dbg.sel[i] = keep ? 1 : 0;
-        if (keep) {
-            // Jacobian row (laser_mapping.cpp:564-593): p_I = R_LI p_b + t_LI;
-            // A = [p_I]x * rot^T * n;  Hsub = [A, n]
-            const double bx = pb.x, by = pb.y, bz = pb.z;
-            const double* RL = P.R_LI;
-            const double ix = ((RL[0] * bx + RL[1] * by) + RL[2] * bz) + P.t_LI[0];
-            const double iy = ((RL[3] * bx + RL[4] * by) + RL[5] * bz) + P.t_LI[1];
-            const double iz = ((RL[6] * bx + RL[7] * by) + RL[8] * bz) + P.t_LI[2];
-            const double cr[9] = {0.0, -iz, iy, iz, 0.0, -ix, -iy, ix, 0.0};
-            double M[9];
-#pragma unroll
-            for (int r = 0; r < 3; r++)
-#pragma unroll
-                for (int cI = 0; cI < 3; cI++)
-                    M[r * 3 + cI] = (cr[r * 3 + 0] * R[cI * 3 + 0] + cr[r * 3 + 1] * R[cI * 3 + 1]) +
-                                    cr[r * 3 + 2] * R[cI * 3 + 2];
-            const double n0 = pa[0], n1 = pa[1], n2 = pa[2];
-            double H[6];
-            H[0] = (M[0] * n0 + M[1] * n1) + M[2] * n2;
-            H[1] = (M[3] * n0 + M[4] * n1) + M[5] * n2;
-            H[2] = (M[6] * n0 + M[7] * n1) + M[8] * n2;
-            H[3] = n0; H[4] = n1; H[5] = n2;
-            const double err = -(double)pd2;
-            int q = 0;
-#pragma unroll
-            for (int r = 0; r < 6; r++) {
-                const double hs = H[r] * P.inv_r;
-#pragma unroll
-                for (int cI = r; cI < 6; cI++) acc[q++] += hs * H[cI];
-            }
-#pragma unroll
-            for (int r = 0; r < 6; r++) acc[21 + r] += (H[r] * P.inv_r) * err;
-            acc[27] += (double)fabsf(pd2);
-            acc[28] += 1.0;
-        }
+        __syncthreads();  // the tile's LDS is reused by the solve
     }
-    }
-    // block reduction: wave shuffle tree, then waves in order
-    const int lane = tid & 63, wave = tid >> 6;
+    double acc[kRedUsed];
 #pragma unroll
-    for (int j = 0; j < kRedUsed; j++) {
-        const double v = wave_sum(acc[j]);
-        if (lane == 0) red_lds[wave * kRedCols + j] = v;
-    }
-    __syncthreads();
-    // Wave 0 stores the block partial write-through (sc1) and, once the store
-    // has drained, takes the scan's ticket; the last block of the scan then
-    // reduces every partial with sc1 loads in a fixed order and its wave 0 runs
-    // the scan's solve (MI355X_MICROARCH.md §Workgroup dispatch: sc1 hand-off,
-    // no L2 write-back fence).  One launch less per evaluation than a separate
-    // solve kernel.
-    if (tid < 64) {
-        if (tid < kRedUsed) {
-            const double v = ((red_lds[0 * kRedCols + tid] + red_lds[1 * kRedCols + tid]) +
-                              red_lds[2 * kRedCols + tid]) + red_lds[3 * kRedCols + tid];
-            __hip_atomic_store(job.partial + (size_t)blockIdx.x * kRedCols + tid, v, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (tid == 0)
-            last_lds = __hip_atomic_fetch_add(&slot->hs_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                       (unsigned)job.nblk - 1u;
-    }
-    __syncthreads();
-    if (!last_lds) return;
-    {
-        // thread (g, c) sums blocks g, g+8, ... of column c, 16 loads in flight
-        const int c = tid & 31, g = tid >> 5;
-        double acc16 = 0.0;
-        if (c < kRedUsed) {
-            double* src = job.partial + c;
-            for (int b0 = g; b0 < job.nblk; b0 += 128) {
-                double v[16];
-#pragma unroll
-                for (int k = 0; k < 16; k++) {
-                    const int b = b0 + 8 * k;
-                    v[k] = b < job.nblk ? __hip_atomic_load(src + (size_t)b * kRedCols, __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_AGENT)
-                                        : 0.0;
-                }
-#pragma unroll
-                for (int k = 0; k < 16; k++) acc16 += v[k];
-            }
-        }
-        fin_lds[g * kRedCols + c] = acc16;
-    }
-    __syncthreads();
-    if (tid >= 64) return;  // the solve is one wave's work
-    if (tid < kRedCols) {
-        double v = 0.0;
-        if (tid < kRedUsed)
-            v = ((fin_lds[0 * kRedCols + tid] + fin_lds[1 * kRedCols + tid]) +
-                 (fin_lds[2 * kRedCols + tid] + fin_lds[3 * kRedCols + tid])) +
-                ((fin_lds[4 * kRedCols + tid] + fin_lds[5 * kRedCols + tid]) +
-                 (fin_lds[6 * kRedCols + tid] + fin_lds[7 * kRedCols + tid]));
-        L.sum[tid] = v;
-        slot->red[tid] = v;
-    }
-    if (tid == 0) slot->hs_ticket = 0u;  // ready for the next pass
-    if (!P.solve) return;  // livo_h_share: the sums only
-    WAVE_SYNC();
-    solve_scan(slot, L, tid);
+    for (int j = 0; j < kRedUsed; j++) acc[j] = 0.0;
+    if (valid) hshare_point(E.h, job, slot->state, i, search, acc);
+    const int nblk = max(1, (job.n + kEvalBlock - 1) / kEvalBlock);
+    hshare_reduce_solve<kEvalBlock>(E.h, job, slot, acc, nblk, bx, R, U.solve);
 }
 
 // Per-point persistent selection of the IKFoM h-model: point_selected_surf is a
@@ -1788,13 +2168,16 @@ struct IkSolveLds {
     double sum[kIkCols];
     double dx[kIkDim], dxn[kIkDim], dxu[kIkDim], Kh[kIkDim];
     double J[9];
+    double Hm[kIkFewRows * 13];   // measurement-space branch: the m < 23 effective rows (h_x row, h)
+    double Km[kIkDim * kIkFewRows];
     int piv[kIkDim];
+    int m;                        // effective rows; < 23: measurement-space gain
     int stop;
 };
 constexpr int kIkRow = 15;  // 12 row + h + |pd2| + keep
 
 // One wave: esekfom.hpp:1638-1921 from the reduced sums in S.sum.
-__device__ void ik_solve(IekfSlot* slot, IkSolveLds& S, const int lane, const double R) {
+__device__ void ik_solve(IekfSlot* slot, const HsJob& job, IkSolveLds& S, const int lane, const double R) {
     IkBlock& K = slot->ik;
     const IekfCtrl ctrl0 = slot->ctrl;
     const int e = ctrl0.n_evals;
@@ -1844,10 +2227,65 @@ __device__ void ik_solve(IekfSlot* slot, IkSolveLds& S, const int lane, const do
         }
         WAVE_SYNC();
     }
-    // gain, information form (:1775-1787): P_temp = (P_/R)^-1 + HTH, P_inv = P_temp^-1.
-    // (The reference takes the equivalent measurement-space form when fewer than
-    // 23 points are effective, :1701-1736; oracle and tests check both agree.)
-    double HT[12];  // the row's part of h_x^T h_x is read from S.sum below
+    auto hth = [&](int r, int c) {
+        const int a = r < c ? r : c, bb = r < c ? c : r;
+        return S.sum[a * 12 - (a * (a - 1)) / 2 + (bb - a)];
+    };
+    if (S.m < kIkDim) {
+        // measurement-space gain (:1701-1736) for m < 23 effective points:
+        // K = P Hc^T (Hc P Hc^T / R + I)^-1 / R, K_h = K h, K_x = K Hc
+        const int m = S.m;
+        double* PHt = S.L;  // 23 x m (S.L is rebuilt from S.P for the covariance)
+        for (int t = lane; t < N * m; t += 64) {
+            const int r = t / m, j = t % m;
+            double acc = S.P[r * N + 0] * S.Hm[j * 13 + 0];
+            for (int k = 1; k < 12; k++) acc = acc + S.P[r * N + k] * S.Hm[j * 13 + k];
+            PHt[r * m + j] = acc;
+        }
+        WAVE_SYNC();
+        {
+            // S = Hc PHt / R + I, padded with the identity to 22 x 22 (the
+            // padding neither pivots nor eliminates: the m x m LU and inverse)
+            double A[kIkFewRows];
+            for (int bcol = 0; bcol < kIkFewRows; bcol++) {
+                double v = lane == bcol ? 1.0 : 0.0;
+                if (lane < m && bcol < m) {
+                    double acc = S.Hm[lane * 13 + 0] * PHt[0 * m + bcol];
+                    for (int k = 1; k < 12; k++) acc = acc + S.Hm[lane * 13 + k] * PHt[k * m + bcol];
+                    v = acc / R + (lane == bcol ? 1.0 : 0.0);
+                }
+                A[bcol] = lane < kIkFewRows ? v : 0.0;
+            }
+            wave_lu_to_lds<kIkFewRows>(A, lane, S.LU, S.piv);
+            WAVE_SYNC();
+            if (lane < m) {
+                double y[kIkFewRows];
+                lds_lu_column<kIkFewRows>(S.LU, S.piv, lane, y);
+                for (int i = 0; i < kIkFewRows; i++) S.Pinv[i * kIkFewRows + lane] = y[i];  // Sinv(i, lane)
+            }
+            WAVE_SYNC();
+        }
+        for (int t = lane; t < N * m; t += 64) {  // K = PHt Sinv / R
+            const int r = t / m, j = t % m;
+            double acc = PHt[r * m + 0] * S.Pinv[0 * kIkFewRows + j];
+            for (int k = 1; k < m; k++) acc = acc + PHt[r * m + k] * S.Pinv[k * kIkFewRows + j];
+            S.Km[r * kIkFewRows + j] = acc / R;
+        }
+        WAVE_SYNC();
+        if (lane < N) {
+            const int r = lane;
+            double kh = 0.0;
+            for (int j = 0; j < m; j++) kh = (j == 0) ? S.Km[r * kIkFewRows] * S.Hm[12] : kh + S.Km[r * kIkFewRows + j] * S.Hm[j * 13 + 12];
+            S.Kh[r] = kh;
+            for (int c = 0; c < 12; c++) {
+                double acc = 0.0;
+                for (int j = 0; j < m; j++) acc = (j == 0) ? S.Km[r * kIkFewRows] * S.Hm[c] : acc + S.Km[r * kIkFewRows + j] * S.Hm[j * 13 + c];
+                S.Kx[r * 12 + c] = acc;
+            }
+        }
+        WAVE_SYNC();
+    } else {
+    // gain, information form (:1775-1787): P_temp = (P_/R)^-1 + HTH, P_inv = P_temp^-1
     {
         double A[N];
         for (int j = 0; j < N; j++) A[j] = lane < N ? S.P[lane * N + j] / R : 0.0;
@@ -1875,11 +2313,6 @@ __device__ void ik_solve(IekfSlot* slot, IkSolveLds& S, const int lane, const do
         }
         WAVE_SYNC();
     }
-    (void)HT;
-    auto hth = [&](int r, int c) {
-        const int a = r < c ? r : c, bb = r < c ? c : r;
-        return S.sum[a * 12 - (a * (a - 1)) / 2 + (bb - a)];
-    };
     if (lane < N) {
         const int r = lane;
         double kh = S.Pinv[r * N] * S.sum[78];
@@ -1892,6 +2325,7 @@ __device__ void ik_solve(IekfSlot* slot, IkSolveLds& S, const int lane, const do
         }
     }
     WAVE_SYNC();
+    }
     if (lane < N) {  // dx_ = K_h + (K_x - I) dx_new
         const int r = lane;
         double acc = 0.0;
@@ -2016,6 +2450,8 @@ __global__ __launch_bounds__(kBlock) void k_hshare_ik(HsParams P) {
         ob = a + t;
     }
     double acc = 0.0;
+    __shared__ uint32_t wcnt[kBlock / 64];
+    uint32_t bcnt = 0;  // effective rows of this block so far (point order)
     for (int rep = 0; rep < kPtsPerThread; rep++) {
         const int i = (blockIdx.x * kPtsPerThread + rep) * kBlock + tid;
         double row[kIkRow];
@@ -2077,7 +2513,25 @@ __global__ __launch_bounds__(kBlock) void k_hshare_ik(HsParams P) {
             }
         }
         for (int k = 0; k < kIkRow; k++) rows[tid * kIkRow + k] = row[k];
+        // the block's first kIkFewRows effective rows in point order: with fewer
+        // than 23 effective points in the whole scan every block has fewer, and
+        // the solve forms the reference's measurement-space gain from them
+        const bool eff = row[14] != 0.0;
+        const unsigned long long bal = __ballot(eff);
+        const int lane = tid & 63;
+        if (lane == 0) wcnt[tid >> 6] = (uint32_t)__popcll(bal);
         __syncthreads();
+        uint32_t pos = bcnt + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+        uint32_t tot = 0;
+        for (int w = 0; w < kBlock / 64; w++) {
+            if (w < (tid >> 6)) pos += wcnt[w];
+            tot += wcnt[w];
+        }
+        if (eff && pos < (uint32_t)kIkFewRows) {
+            double* dst = job.ikrows + ((size_t)blockIdx.x * kIkFewRows + pos) * 13;
+            for (int k = 0; k < 13; k++) dst[k] = row[k];
+        }
+        bcnt += tot;
         if (tid < kIkUsed) {  // rows in point order
             for (int r = 0; r < kBlock; r++) {
                 const double* q = rows + r * kIkRow;
@@ -2091,6 +2545,7 @@ __global__ __launch_bounds__(kBlock) void k_hshare_ik(HsParams P) {
         __syncthreads();
     }
     if (tid < kIkUsed) job.partial[(size_t)blockIdx.x * kIkCols + tid] = acc;
+    if (tid == 0) job.ikcnt[blockIdx.x] = bcnt < (uint32_t)kIkFewRows ? bcnt : (uint32_t)kIkFewRows + 1u;
 }
 
 // One 64-thread block per scan: fixed-order reduction of the IKFoM partials,
@@ -2119,7 +2574,21 @@ __global__ __launch_bounds__(64) void k_solve_ik(HsParams P) {
         S.sum[c] = ((acc8[0] + acc8[1]) + (acc8[2] + acc8[3])) + ((acc8[4] + acc8[5]) + (acc8[6] + acc8[7]));
     }
     WAVE_SYNC();
-    ik_solve(slot, S, lane, P.lpc);
+    if (lane == 0) {
+        // fewer than 23 effective points: their rows, in point order (blocks in order)
+        const int m = (int)S.sum[91];
+        S.m = m;
+        if (m < kIkDim) {
+            int k = 0;
+            for (int b = 0; b < job.nblk && k < m; b++) {
+                const int cb = (int)job.ikcnt[b];
+                for (int r = 0; r < cb && k < m; r++, k++)
+                    for (int c = 0; c < 13; c++) S.Hm[k * 13 + c] = job.ikrows[((size_t)b * kIkFewRows + r) * 13 + c];
+            }
+        }
+    }
+    WAVE_SYNC();
+    ik_solve(slot, job, S, lane, P.lpc);
 }
 
 __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
@@ -2163,6 +2632,14 @@ __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
 }
 
 // ======================================================== launchers =======
+// The replay follows every search but usually has 0-5 queries: a few small
+// blocks (a 64-block grid waited ~10 us for LDS behind the concurrent stream
+// groups' searches), stack LDS sized to the tree's depth.
+constexpr int kReplayBlocks = 8;
+static size_t replay_lds_bytes(int depth) {
+    return (size_t)std::max(1, std::min(depth, kMaxDepth)) * 64 * sizeof(uint2);
+}
+
 size_t knn_lds_bytes(int depth) {
     const int entries = depth > 1 ? depth - 1 : 1;  // son levels 1 .. depth-1
     return (size_t)entries * kKnnBlock * sizeof(float);
@@ -2176,7 +2653,7 @@ int launch_knn_pass(const KnnParams& p, int n_jobs, int64_t max_n, void* stream)
     hipLaunchKernelGGL(k_knn_pass, dim3((unsigned)(q.nb * n_jobs)), dim3(kKnnBlock), knn_lds_bytes(p.depth),
                        (hipStream_t)stream, q);
     if (hipGetLastError() != hipSuccess) return LIVO_E_HIP;
-    hipLaunchKernelGGL(k_knn_replay, dim3(64), dim3(64), 0, (hipStream_t)stream, q);
+    hipLaunchKernelGGL(k_knn_replay, dim3(kReplayBlocks), dim3(64), replay_lds_bytes(q.depth), (hipStream_t)stream, q);
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 
@@ -2192,25 +2669,47 @@ int launch_knn_leaf(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, 
     else
         hipLaunchKernelGGL((k_knn_leaf<false, 1>), grid, block, lds, (hipStream_t)stream, q);
     if (hipGetLastError() != hipSuccess) return LIVO_E_HIP;
-    hipLaunchKernelGGL(k_knn_replay, dim3(64), dim3(64), 0, (hipStream_t)stream, q);
+    hipLaunchKernelGGL(k_knn_replay, dim3(kReplayBlocks), dim3(64), replay_lds_bytes(q.depth), (hipStream_t)stream, q);
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 
-int launch_knn_grid(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, void* stream) {
+int launch_knn_grid(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, bool tile, void* stream) {
     if (n_jobs <= 0 || max_n <= 0) return LIVO_OK;
     KnnParams q = p;
-    q.nb = (int32_t)((max_n + kKnnBlock - 1) / kKnnBlock);
+    const int B = tile ? 64 : kKnnBlock;
+    q.nb = (int32_t)((max_n + B - 1) / B);
     if ((int64_t)q.nb * n_jobs >= (1ll << 31)) return LIVO_E_RANGE;
-    const dim3 grid((unsigned)(q.nb * n_jobs)), block(kKnnBlock);
-    if (seeded)
-        hipLaunchKernelGGL((k_knn_grid<true>), grid, block, 0, (hipStream_t)stream, q);
-    else
-        hipLaunchKernelGGL((k_knn_grid<false>), grid, block, 0, (hipStream_t)stream, q);
+    const dim3 grid((unsigned)(q.nb * n_jobs)), block(B);
+    if (tile) {
+        if (seeded)
+            hipLaunchKernelGGL((k_knn_grid<true, true>), grid, block, 0, (hipStream_t)stream, q);
+        else
+            hipLaunchKernelGGL((k_knn_grid<false, true>), grid, block, 0, (hipStream_t)stream, q);
+    } else if (seeded) {
+        hipLaunchKernelGGL((k_knn_grid<true, false>), grid, block, 0, (hipStream_t)stream, q);
+    } else {
+        hipLaunchKernelGGL((k_knn_grid<false, false>), grid, block, 0, (hipStream_t)stream, q);
+    }
     if (hipGetLastError() != hipSuccess) return LIVO_E_HIP;
     if (q.canon)
-        hipLaunchKernelGGL(k_knn_canon, dim3(64), dim3(64), 0, (hipStream_t)stream, q);
+        hipLaunchKernelGGL(k_knn_canon, dim3(kReplayBlocks), dim3(64), 0, (hipStream_t)stream, q);
     else
-        hipLaunchKernelGGL(k_knn_replay, dim3(64), dim3(64), 0, (hipStream_t)stream, q);
+        hipLaunchKernelGGL(k_knn_replay, dim3(kReplayBlocks), dim3(64), replay_lds_bytes(q.depth), (hipStream_t)stream, q);
+    return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+
+int launch_iekf_eval(const KnnParams& kp, const HsParams& hp, int n_jobs, int64_t max_n, bool first, void* stream) {
+    if (n_jobs <= 0 || max_n <= 0) return LIVO_OK;
+    EvalParams E;
+    E.k = kp;
+    E.h = hp;
+    E.k.nb = (int32_t)((max_n + kEvalBlock - 1) / kEvalBlock);
+    if ((int64_t)E.k.nb * n_jobs >= (1ll << 31)) return LIVO_E_RANGE;
+    const dim3 grid((unsigned)(E.k.nb * n_jobs)), block(kEvalBlock);
+    if (first)
+        hipLaunchKernelGGL(k_iekf_eval<true>, grid, block, 0, (hipStream_t)stream, E);
+    else
+        hipLaunchKernelGGL(k_iekf_eval<false>, grid, block, 0, (hipStream_t)stream, E);
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 

@@ -1,0 +1,98 @@
+"""GPU parity of the exact modes the bench measures and of the committed fixture.
+
+  * the golden fixture (tests/golden/config1_small.npz, made by
+    tests/golden/make_golden.py from the oracle): the HIP path through the
+    C ABI reproduces it -- k-NN, normals, flags bit-exact; HᵀH 1e-9; the IEKF
+    update's counts exact and its per-evaluation state delta within 1e-5;
+  * the bench's headline mode (bench.py, config 2 as the config-4 shard of one
+    GPU): 8 x 100k-point scans vs the 1M-point map in ONE batched call over
+    4 stream groups, every scan against the oracle's own update;
+  * the bench's N-GPU launcher: `bench.py --gpus 2` starts two ranks (here
+    sharing one GPU, gloo for the counter all-reduce) and reports both.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REL_HTH = 1e-9
+REL_STATE = 1e-5
+
+
+def _rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
+
+
+def test_golden_fixture(built):
+    import livo_amd
+    g = np.load(os.path.join(ROOT, "tests", "golden", "config1_small.npz"))
+    st0 = {k[6:]: g[k] for k in g.files if k.startswith("state_")}
+    with livo_amd.Context(0, t_LI=g["t_LI"], max_iterations=int(g["max_iter"])) as ctx:
+        ctx.map_build(g["map"])
+        sid = ctx.scan_upload(g["scan"])
+        hs = ctx.h_share(sid, st0, search_en=True)
+        assert np.array_equal(hs["nn_idx"], g["nn_idx"])
+        assert np.array_equal(hs["nn_d"].view(np.uint32), g["nn_d"].view(np.uint32))
+        assert np.array_equal(hs["normvec"].view(np.uint32), g["normvec"].view(np.uint32))
+        assert np.array_equal(hs["sel"], g["sel"])
+        assert hs["effct"] == int(g["effct"]) and hs["visits"] == int(g["visits"])
+        assert _rel(hs["HTH"], g["HTH"]) < REL_HTH and _rel(hs["HTL"], g["HTL"]) < REL_HTH
+        out, stats = ctx.iekf_update(sid, st0)
+    assert stats["iterations"] == int(g["iterations"])
+    assert stats["knn_passes"] == int(g["knn_passes"])
+    assert stats["effct_feat_num"] == list(g["effct_feat_num"])
+    for e in range(stats["iterations"]):
+        assert _rel(stats["solution"][e], g["solution"][e]) < REL_STATE, e
+    assert _rel(out["pos"] - st0["pos"], g["out_pos"] - st0["pos"]) < REL_STATE
+    assert np.linalg.norm(out["cov"] - g["out_cov"]) / np.linalg.norm(st0["cov"]) < 1e-9
+
+
+@pytest.mark.slow
+def test_bench_headline_mode_parity(built):
+    """8 x 100k scans, 1M map, one livo_iekf_update_batch over 4 stream groups
+    (the bench's step): per scan, the oracle's iterations, k-NN passes,
+    effective points and per-evaluation state deltas."""
+    import livo_amd
+    import oracle
+    from livo_amd import synth
+    m = synth.cached_map(1_000_000)
+    scans = [synth.make_scan(100_000, s)[0] for s in range(8)]
+    states = [synth.make_state(s) for s in range(8)]
+    with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=4) as ctx:
+        ctx.map_build(m)
+        sids = [ctx.scan_upload(b) for b in scans]
+        outs, stats = ctx.iekf_update_batch(sids, states)
+    tree = oracle.Tree(m)
+    for s in range(8):
+        sr, rs = tree.iekf_update(scans[s], states[s], R_LI=np.eye(3), t_LI=synth.T_LI, max_iter=4, threads=8)
+        gs = stats[s]
+        assert gs["iterations"] == rs["iterations"], s
+        assert gs["knn_passes"] == rs["knn_passes"], s
+        assert gs["effct_feat_num"] == rs["effct_feat_num"], s
+        for e in range(gs["iterations"]):
+            assert _rel(gs["solution"][e], rs["solution"][e]) < REL_STATE, (s, e)
+        assert _rel(outs[s]["pos"] - states[s]["pos"], sr["pos"] - states[s]["pos"]) < REL_STATE, s
+
+
+def test_bench_two_ranks(built):
+    """bench.py --gpus 2 without a launcher starts 2 rank processes (both on this
+    box's GPU; gloo all-reduce since RCCL refuses two ranks on one device)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+                        "--cpu-seconds", "0", "--legs", "headline", "--pmc", "off"],
+                       capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(line) == 1, r.stdout[-2000:]
+    j = json.loads(line[0])
+    assert j["n_gpus"] == 2
+    assert j["total_scans"] == 2 * 8 * 2
+    assert j["config"]["parallelism"] == "scan farm x2"
+    assert j["value"] > 0

@@ -3,11 +3,13 @@
 state_ikfom (use-ikfom.hpp:12-21), the legacy h-model
 (origin_laserMapping.cpp:916-1048) and update_iterated_dyn_share_modified
 (esekfom.hpp:1619-1928).  Bars: iteration / search / convergence control and
-effective-point counts exact; per-evaluation dx within 1e-5 of the scan's
-largest dx (a converged step is a ~1e5-fold cancellation in this form, see
-_compare); covariance within 1e-9 of the prior's norm.  Fewer than 23 effective points:
-the reference's measurement-space gain, restated by the oracle; the device
-uses the equivalent information form (agreement pinned in test_oracle.py).
+effective-point counts exact; per-evaluation dx within 1e-5 of its own norm
+for every step that is not a converged near-zero step (|dx| < 1e-2 of the
+scan's largest), those within 1e-5 of the scan's largest dx (a converged step
+is a ~1e5-fold cancellation in this form, see _compare); covariance within
+1e-9 of the prior's norm.  Fewer than 23 effective points: the reference's
+measurement-space gain (:1701-1736) on both sides (the device collects the
+effective rows of such scans in point order, k_hshare_ik / k_solve_ik).
 """
 import numpy as np
 import pytest
@@ -42,7 +44,12 @@ def _compare(g, gs, r, rs, st0):
     # order than the oracle's serial loop) are amplified ~1e5-fold
     scale = max(np.linalg.norm(d) for d in rs["dx"])
     for e in range(gs["iterations"]):
-        assert np.linalg.norm(gs["dx"][e] - rs["dx"][e]) <= REL * scale, e
+        err = np.linalg.norm(gs["dx"][e] - rs["dx"][e])
+        own = np.linalg.norm(rs["dx"][e])
+        if own >= 1e-2 * scale:  # a real step: relative to itself
+            assert err <= REL * own, (e, err / own)
+        else:  # a converged near-zero step
+            assert err <= REL * scale, e
     upd = np.linalg.norm(r["pos"] - st0["pos"])
     assert np.linalg.norm(g["pos"] - r["pos"]) <= REL * max(upd, 1e-12)
     for k in ("rot", "offset_R"):
@@ -87,7 +94,8 @@ def test_ikfom_batch_equals_single(ctx, tree100k):
 
 @pytest.mark.parametrize("n", [12, 40])
 def test_ikfom_few_points(ctx, tree100k, n):
-    """12 points: fewer than 23 effective (the reference's measurement-space gain)."""
+    """12 points: fewer than 23 effective (the reference's measurement-space gain
+    on the device too); 40: the information form."""
     from livo_amd import synth
     body, _, _ = synth.make_scan(4000, 3)
     body = body[:n]

@@ -285,6 +285,15 @@ def test_config5_10M_properties(built):
         sid = ctx.scan_upload(body)
         sg, stg = ctx.iekf_update(sid, st0)
         assert stg["iterations"] >= 2 and stg["effct_feat_num"][0] > 150_000
+        # the full IEKF update against the oracle's at 10M / 200k: counts exact,
+        # per-evaluation state delta within the north_star's 1e-5
+        sr, str_ = tree.iekf_update(body, st0, R_LI=np.eye(3), t_LI=synth.T_LI, max_iter=4, threads=8)
+        assert stg["iterations"] == str_["iterations"]
+        assert stg["knn_passes"] == str_["knn_passes"]
+        assert stg["effct_feat_num"] == str_["effct_feat_num"]
+        for e in range(stg["iterations"]):
+            assert _rel(stg["solution"][e], str_["solution"][e]) < REL_STATE, e
+        assert _rel(sg["pos"] - st0["pos"], sr["pos"] - st0["pos"]) < REL_STATE
 
 
 def test_iekf_duplicate_map_replays(built):
@@ -392,14 +401,18 @@ def test_profiling_levels(ctx100k):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["grid", "tile"])
 @pytest.mark.parametrize("cell", [0.0, 0.05, 0.3, 2.0])
-def test_iekf_grid(built, map100k, tree100k, cell, monkeypatch):
-    """The cell-grid search (LIVO_KNN_KIND=grid; LIVO_GRID_CELL metres, 0: chosen
-    from the map) certifies the 5 nearest by ring distance and replays the rest
-    on the ikd-Tree; any cell size must give the oracle's answer."""
+def test_iekf_grid(built, map100k, tree100k, cell, kind, monkeypatch):
+    """The cell-grid search (LIVO_KNN_KIND=grid, or tile: the same search with a
+    wave's cells staged in LDS; LIVO_GRID_CELL metres, 0: chosen from the map)
+    certifies the 5 nearest by ring distance and replays the rest on the
+    ikd-Tree; any cell size must give the oracle's answer.  0.05 m cells make
+    most waves' boxes too large for a tile and 2 m cells too many points: the
+    global path."""
     import livo_amd
     synth = _synth()
-    monkeypatch.setenv("LIVO_KNN_KIND", "grid")
+    monkeypatch.setenv("LIVO_KNN_KIND", kind)
     monkeypatch.setenv("LIVO_GRID_CELL", str(cell))
     with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=4) as ctx:
         ctx.map_build(map100k)
@@ -414,13 +427,14 @@ def test_iekf_grid(built, map100k, tree100k, cell, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["grid", "tile"])
 @pytest.mark.parametrize("n_map", [5, 17, 1000])
-def test_iekf_grid_small_maps(built, n_map, monkeypatch):
+def test_iekf_grid_small_maps(built, n_map, kind, monkeypatch):
     """Cell grids of a handful of points: lists that never fill are replayed."""
     import livo_amd
     import oracle
     synth = _synth()
-    monkeypatch.setenv("LIVO_KNN_KIND", "grid")
+    monkeypatch.setenv("LIVO_KNN_KIND", kind)
     m = synth.make_map(100_000)[:: 100_000 // n_map][:n_map].copy()
     body, _, _ = synth.make_scan(2_000, 6)
     st0 = synth.make_state(6)
@@ -440,16 +454,20 @@ def test_grid_batch_equals_leaf(built, map100k, monkeypatch):
     scans[5] = scans[5] + np.float32(30.0)
     states = [synth.make_state(s) for s in range(6)]
     out = {}
-    for kind in ("leaf", "grid"):
+    for kind in ("leaf", "grid", "tile"):
         monkeypatch.setenv("LIVO_KNN_KIND", kind)
         with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=4) as ctx:
             ctx.map_build(map100k)
             sids = [ctx.scan_upload(b) for b in scans]
             out[kind] = ctx.iekf_update_batch(sids, states)
-    for i in range(6):
-        a, b = out["leaf"][0][i], out["grid"][0][i]
-        assert all(np.array_equal(a[k], b[k]) for k in a), i
-        assert out["leaf"][1][i]["iterations"] == out["grid"][1][i]["iterations"]
+            out[kind + "_nn"] = [ctx.scan_neighbors(sid) for sid in sids]
+    for kind in ("grid", "tile"):
+        for i in range(6):
+            a, b = out["leaf"][0][i], out[kind][0][i]
+            assert all(np.array_equal(a[k], b[k]) for k in a), (kind, i)
+            assert out["leaf"][1][i]["iterations"] == out[kind][1][i]["iterations"]
+            np.testing.assert_array_equal(out["leaf_nn"][i][0], out[kind + "_nn"][i][0])
+            np.testing.assert_array_equal(out["leaf_nn"][i][1], out[kind + "_nn"][i][1])
 
 
 def _tie_map(seed=7, n_base=20_000, n_q=2_000):
@@ -469,7 +487,7 @@ def _tie_map(seed=7, n_base=20_000, n_q=2_000):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind", ["leaf", "grid"])
+@pytest.mark.parametrize("kind", ["leaf", "grid", "tile"])
 def test_exact_ties_resolved_in_kernel(built, kind, monkeypatch):
     """Exact distance ties inside the 5-NN list (distinct x) are ordered by
     PointType_CMP's x rule in the batched search itself, without the replay; the

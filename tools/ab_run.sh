@@ -1,6 +1,6 @@
 #!/bin/bash
-# A/B of variant libraries on one box: bench (no CPU baseline) for each variant,
-# repeated in rounds so box drift hits all of them alike.
+# A/B of variant libraries on one box: bench headline leg (no CPU baseline, no
+# PMC) for each variant, repeated in rounds so box drift hits all alike.
 # usage: tools/ab_run.sh ROUNDS spec1 spec2 ...
 #   spec = LIB[@VAR=VAL,VAR=VAL]   LIB "base" = the regular library, else
 #          fast-livo-noted_amd/lib/variants/LIB.so; the env assignments apply to that run
@@ -15,6 +15,6 @@ for r in $(seq 1 $R); do
     if [ "$n" = base ]; then lib=""; else lib=fast-livo-noted_amd/lib/variants/$n.so; fi
     tag=$(echo "$spec" | tr '@=,/' '+-+-')
     env LIVO_LIB=$lib $envs timeout -k 10 120 python bench.py --steps 40 --warmup 10 --cpu-seconds 0 \
-        > gpurun_out/ab_${tag}_$r.log 2>&1 || exit $?
+        --legs headline --pmc off > gpurun_out/ab_${tag}_$r.log 2>&1 || exit $?
   done
 done
