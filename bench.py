@@ -46,10 +46,12 @@ for p in (os.path.join(ROOT, "fast-livo-noted_amd"), os.path.join(ROOT, "oracle"
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
-# Bytes of the grid k-NN that the algorithm moves: per query the
-# body point in (16 B) and the 5 indices + squared distances out (40 B); per
-# hash slot read 16 B; per map point read 16 B (both counted by the kernel).
-B_QUERY_IO = 16 + 5 * 8
+# Bytes the first evaluation moves by algorithm, the roofline
+# unit of the fused kernel k_iekf_eval<true> (search + plane pass + solve):
+# per point the body point in (16 B), the 5 neighbour indices + squared
+# distances out (40 B) and the plane cache out (16 B + 1 B state); per hash
+# slot read 16 B and per map point read 16 B (both counted by the kernel).
+B_QUERY_IO = 16 + 5 * 8 + 17
 B_SLOT = 16
 B_POINT = 16
 # SURVEY.md §8d's reference-equivalent pricing (the reference tree's traversal):
@@ -107,6 +109,11 @@ def launch_ranks(a) -> int:
     return rc
 
 
+def stream_groups() -> int:
+    """Stream groups of a batched update (livo_capi.cpp default 2, LIVO_STREAM_GROUPS)."""
+    return int(os.environ.get("LIVO_STREAM_GROUPS", "2"))
+
+
 def host_threads() -> int:
     """Cores this job may use: the affinity set, capped by the cgroup CPU quota."""
     n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
@@ -161,7 +168,7 @@ def pmc_traffic(a, kernel_key: str):
     if "FETCH_SIZE" not in mean or "WRITE_SIZE" not in mean:
         return None
     disp = len(per["FETCH_SIZE"])
-    groups = min(4, a.batch)  # one first-search dispatch per stream group and batch
+    groups = min(stream_groups(), a.batch)  # one first-search dispatch per stream group and batch
     res = {"hbm_bytes_per_launch": groups * (2 * mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024,
            "fetch_kib_per_dispatch": round(mean["FETCH_SIZE"], 1), "write_kib_per_dispatch": round(mean["WRITE_SIZE"], 1),
            "dispatches_sampled": disp}
@@ -193,7 +200,9 @@ def main():
     scans = [synth.make_scan(a.scan_points, s)[0] for s in scan_ids]
     st0 = [synth.make_state(s) for s in scan_ids]
     kind = os.environ.get("LIVO_KNN_KIND", "tile")
-    unit_kernel = {"leaf": "k_knn_leaf<false", "grid": "k_knn_grid<false, false>"}.get(kind, "k_knn_grid<false, true>")
+    fused = kind == "tile" and os.environ.get("LIVO_FUSED", "1") != "0"
+    unit_kernel = {"leaf": "k_knn_leaf<false", "grid": "k_knn_grid<false, false>"}.get(
+        kind, "k_iekf_eval<true>" if fused else "k_knn_grid<false, true>")
     pmc = pmc_traffic(a, unit_kernel) if (rank == 0 and world == 1) else None
 
     import torch
@@ -302,8 +311,11 @@ def main():
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": round(pmc["hbm_bytes_per_launch"]) if pmc else None,
-                "kernel": f"first-evaluation k-NN of the batch: {min(4, a.batch)} concurrent {unit_kernel} dispatches "
-                          "(one per stream group: transform + exact 5-NN of every point) + their tie replays",
+                "kernel": (f"first evaluation of the batch: {min(stream_groups(), a.batch)} concurrent {unit_kernel} dispatches (one "
+                           "per stream group: transform + exact 5-NN of every point with in-place tie replay + plane "
+                           "fit + Jacobian + HTH reduction + solve)") if fused else
+                          (f"first-evaluation k-NN of the batch: {min(stream_groups(), a.batch)} concurrent {unit_kernel} dispatches "
+                           "(one per stream group: transform + exact 5-NN of every point) + their tie replays"),
                 "avg_launch_ms": round(launch_ms, 4),
                 "alg_bytes_per_launch": int(alg_bytes),
                 "alg_bytes_terms": {"slots_per_query": round(knn_visits / max(knn_queries, 1), 3),

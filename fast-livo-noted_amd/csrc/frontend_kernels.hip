@@ -240,6 +240,49 @@ __global__ void k_fe_gather(const float* __restrict__ pts, int64_t n, int stride
     iperm[j] = (int32_t)k;
 }
 
+// RGBpointBodyToWorld (laser_mapping.cpp:647-660) over laserCloudFullRes
+// (:258-265): p_w = rot (R_LI p_b + t_LI) + pos in double, stored as float;
+// intensity copied (column 3 of a 5-float source, 0 for a 4-float scan),
+// curvature 0 (a fresh PointType).  perm: source position -> output index.
+__global__ void k_to_world(const float* __restrict__ src, int64_t n, int stride, const int32_t* __restrict__ perm,
+                           WorldParams W, float* __restrict__ out5) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const float* p = src + stride * k;
+    float wx, wy, wz;
+    world_point(W.rot, W.pos, W.R_LI, W.t_LI, p[0], p[1], p[2], wx, wy, wz);
+    const int64_t o = perm ? (int64_t)perm[k] : k;
+    float* q = out5 + 5 * o;
+    q[0] = wx;
+    q[1] = wy;
+    q[2] = wz;
+    q[3] = stride >= 5 ? p[3] : 0.0f;
+    q[4] = 0.0f;
+}
+
+// laserCloudOri / corr_normvect (laser_mapping.cpp:547-561): the effective
+// points in the caller's point order.  flags[caller index] = effective; an
+// exclusive scan gives each its place; then body point and normvec scattered.
+__global__ void k_ori_flags(const uint8_t* __restrict__ sel, const int32_t* __restrict__ perm, int64_t n,
+                            uint32_t* __restrict__ flags) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    flags[perm[k]] = sel[k] ? 1u : 0u;
+}
+__global__ void k_ori_scatter(const float* __restrict__ pts4, const float* __restrict__ normvec,
+                              const uint8_t* __restrict__ sel, const int32_t* __restrict__ perm,
+                              const uint32_t* __restrict__ pos, int64_t n, float* __restrict__ ori3,
+                              float* __restrict__ corr4) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n || !sel[k]) return;
+    const int64_t o = pos[perm[k]];
+    const float4 p = reinterpret_cast<const float4*>(pts4)[k];
+    ori3[3 * o + 0] = p.x;
+    ori3[3 * o + 1] = p.y;
+    ori3[3 * o + 2] = p.z;
+    reinterpret_cast<float4*>(corr4)[o] = reinterpret_cast<const float4*>(normvec)[k];
+}
+
 static inline dim3 fe_blocks(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }
 #define FE_LAUNCH(kernel, n, ...)                                                                   \
     do {                                                                                            \
@@ -273,5 +316,16 @@ int launch_fe_morton(const float* pts, int64_t n, int stride, const unsigned* mi
 int launch_fe_gather(const float* pts, int64_t n, int stride, const uint32_t* perm, float* pts4, int32_t* iperm,
                      void* stream) {
     FE_LAUNCH(k_fe_gather, n, pts, n, stride, perm, pts4, iperm);
+}
+int launch_to_world(const float* src, int64_t n, int stride, const int32_t* perm, const WorldParams& W, float* out5,
+                    void* stream) {
+    FE_LAUNCH(k_to_world, n, src, n, stride, perm, W, out5);
+}
+int launch_ori_flags(const uint8_t* sel, const int32_t* perm, int64_t n, uint32_t* flags, void* stream) {
+    FE_LAUNCH(k_ori_flags, n, sel, perm, n, flags);
+}
+int launch_ori_scatter(const float* pts4, const float* normvec, const uint8_t* sel, const int32_t* perm,
+                       const uint32_t* pos, int64_t n, float* ori3, float* corr4, void* stream) {
+    FE_LAUNCH(k_ori_scatter, n, pts4, normvec, sel, perm, pos, n, ori3, corr4);
 }
 }  // namespace livo

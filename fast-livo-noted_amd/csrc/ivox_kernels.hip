@@ -572,6 +572,8 @@ __global__ void k_iv_insert(IvoxParams P) {
     }
     P.slot_of[i] = (uint32_t)sl;
     atomicAdd(P.addcnt + sl, 1u);
+    atomicMin(P.first + sl, (uint32_t)i);
+    atomicMax(P.lastp1 + sl, (uint32_t)i + 1u);
 }
 
 // The batch's new grids removed again (capacity reached): a new grid is a
@@ -581,12 +583,16 @@ __global__ void k_iv_rollback(IvoxParams P) {
     if (s >= P.table) return;
     if (P.slots[s].key != kGridEmpty && P.slots[s].count == 0u) P.slots[s] = GridSlot{kGridEmpty, 0u, 0u};
     P.addcnt[s] = 0u;
+    P.first[s] = 0xFFFFFFFFu;
+    P.lastp1[s] = 0u;
+    P.evict[s] = 0u;
 }
 
 __global__ void k_iv_prepare(IvoxParams P) {
     const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= P.table) return;
-    P.tot[s] = (P.slots[s].key != kGridEmpty ? P.slots[s].count : 0u) + P.addcnt[s];
+    // an evicted grid leaves with every point it held, this batch's included
+    P.tot[s] = P.evict[s] ? 0u : (P.slots[s].key != kGridEmpty ? P.slots[s].count : 0u) + P.addcnt[s];
 }
 
 // Old runs moved to their new start (one thread per grid).
@@ -594,7 +600,7 @@ __global__ void k_iv_move(IvoxParams P) {
     const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= P.table) return;
     const GridSlot g = P.slots[s];
-    if (g.key == kGridEmpty || g.count == 0u) return;
+    if (g.key == kGridEmpty || g.count == 0u || P.evict[s]) return;
     const float4* __restrict__ src = reinterpret_cast<const float4*>(P.pts) + g.start;
     float4* __restrict__ dst = reinterpret_cast<float4*>(P.npts) + P.newstart[s];
     for (uint32_t k = 0; k < g.count; k++) dst[k] = src[k];
@@ -606,7 +612,7 @@ __global__ void k_iv_place(IvoxParams P) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= P.n_src) return;
     const uint32_t sl = P.skeys[k];
-    if ((int64_t)sl >= P.table) return;
+    if ((int64_t)sl >= P.table || P.evict[sl]) return;
     const uint32_t i = P.svals[k];
     const uint32_t rank = (uint32_t)k - P.addstart[sl];
     const float4 p = reinterpret_cast<const float4*>(P.src)[i];
@@ -620,7 +626,9 @@ __global__ void k_iv_fix(IvoxParams P) {
     unsigned cnt = 0;
     if (s < P.table) {
         GridSlot g = P.slots[s];
-        if (g.key != kGridEmpty) {
+        if (P.evict[s]) {
+            P.addcnt[s] = 0u;  // (k_iv_drop empties the slot)
+        } else if (g.key != kGridEmpty) {
             g.start = P.newstart[s];
             g.count += P.addcnt[s];
             P.slots[s] = g;
@@ -636,7 +644,8 @@ __global__ void k_iv_fix(IvoxParams P) {
         atomicMax(P.ctr + 2, (unsigned long long)cnt);
 }
 
-__global__ void k_iv_rehash(const GridSlot* __restrict__ old_slots, int64_t old_table, GridSlot* slots, int log2) {
+__global__ void k_iv_rehash(const GridSlot* __restrict__ old_slots, const unsigned long long* __restrict__ old_t,
+                            int64_t old_table, GridSlot* slots, unsigned long long* tlast, int log2) {
     const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= old_table) return;
     const GridSlot g = old_slots[s];
@@ -646,6 +655,89 @@ __global__ void k_iv_rehash(const GridSlot* __restrict__ old_slots, int64_t old_
     while (atomicCAS(&slots[sl].key, kGridEmpty, g.key) != kGridEmpty) sl = (sl + 1) & mask;
     slots[sl].start = g.start;
     slots[sl].count = g.count;
+    tlast[sl] = old_t[s];
+}
+
+// ---- LRU eviction (ivox3d.h:263-275): when a batch takes the grid count to
+// the capacity, each new grid past that point evicts grids_cache_.back(), the
+// grid whose last added point is the oldest.  Grids the batch touches before
+// an eviction are no longer the oldest; the fast path applies when every
+// victim is a grid the batch never touches (the host splits the batch
+// otherwise, see ivox_add_dev).
+__global__ void k_iv_newfirst(IvoxParams P, uint32_t* out, unsigned long long* n) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= P.table) return;
+    if (P.slots[s].key != kGridEmpty && P.slots[s].count == 0u)  // created by this batch
+        out[atomicAdd(n, 1ull)] = P.first[s];
+}
+__global__ void k_iv_oldkeys(IvoxParams P, unsigned long long* keys, uint32_t* slot, unsigned long long* n) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= P.table) return;
+    if (P.slots[s].key != kGridEmpty && P.slots[s].count > 0u) {
+        const unsigned long long k = atomicAdd(n, 1ull);
+        keys[k] = P.tlast[s];
+        slot[k] = (uint32_t)s;
+    }
+}
+__global__ void k_iv_untouched(IvoxParams P, const uint32_t* sorted_slot, int64_t n, uint32_t* flags) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n) flags[k] = P.lastp1[sorted_slot[k]] == 0u ? 1u : 0u;
+}
+// Oldest first: the first ev untouched grids are the victims, unless a grid the
+// batch touches only at or after the first eviction is older than the last of
+// them (it would be evicted and re-created): that is flagged (ctr[0] bit 2).
+__global__ void k_iv_victims(IvoxParams P, const uint32_t* sorted_slot, const uint32_t* rank, int64_t n, int64_t ev,
+                             uint32_t j_first) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint32_t s = sorted_slot[k];
+    if (P.lastp1[s] == 0u) {
+        if ((int64_t)rank[k] < ev) P.evict[s] = 1u;
+        if ((int64_t)rank[k] == ev - 1) P.ctr[3] = (unsigned long long)k;
+    }
+}
+__global__ void k_iv_conflict(IvoxParams P, const uint32_t* sorted_slot, int64_t n, uint32_t j_first) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n || (unsigned long long)k >= P.ctr[3]) return;
+    const uint32_t s = sorted_slot[k];
+    if (P.lastp1[s] != 0u && P.first[s] >= j_first) atomicOr(P.ctr, 2ull);
+}
+// Single eviction at the batch's last point: grids_cache_.back() among every
+// grid then in the map, new ones included (their last touch this batch).
+__device__ __forceinline__ unsigned long long iv_tcur(const IvoxParams& P, int64_t s) {
+    return P.lastp1[s] ? (unsigned long long)P.base_id + P.lastp1[s] - 1ull : P.tlast[s];
+}
+__global__ void k_iv_tcur_min(IvoxParams P) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long t = ~0ull;
+    if (s < P.table && P.slots[s].key != kGridEmpty) t = iv_tcur(P, s);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const unsigned long long o = __shfl_xor(t, off, 64);
+        t = o < t ? o : t;
+    }
+    if ((threadIdx.x & 63) == 0 && t != ~0ull) atomicMin(P.ctr + 4, t);
+}
+__global__ void k_iv_mark_min(IvoxParams P) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < P.table && P.slots[s].key != kGridEmpty && iv_tcur(P, s) == P.ctr[4]) P.evict[s] = 1u;
+}
+// After the CSR rebuild: evicted grids leave the table (the host rehashes to
+// mend the probe chains).  A grid evicted by its own creation (capacity 1)
+// got no points either.
+__global__ void k_iv_drop(IvoxParams P) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= P.table || !P.evict[s]) return;
+    P.slots[s] = GridSlot{kGridEmpty, 0u, 0u};
+    P.evict[s] = 0u;
+}
+// The batch's touches become each grid's last-use id; per-batch marks reset.
+__global__ void k_iv_commit(IvoxParams P) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= P.table) return;
+    if (P.lastp1[s]) P.tlast[s] = (unsigned long long)P.base_id + P.lastp1[s] - 1ull;
+    P.first[s] = 0xFFFFFFFFu;
+    P.lastp1[s] = 0u;
 }
 
 static inline dim3 blocks_for(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }
@@ -664,9 +756,32 @@ int launch_ivox_prepare(const IvoxParams& p, void* stream) { LAUNCH_CHECKED(k_iv
 int launch_ivox_move(const IvoxParams& p, void* stream) { LAUNCH_CHECKED(k_iv_move, p.table, p); }
 int launch_ivox_place(const IvoxParams& p, void* stream) { LAUNCH_CHECKED(k_iv_place, p.n_src, p); }
 int launch_ivox_fix(const IvoxParams& p, void* stream) { LAUNCH_CHECKED(k_iv_fix, p.table, p); }
-int launch_ivox_rehash(const GridSlot* old_slots, int64_t old_table, GridSlot* slots, int log2, void* stream) {
-    LAUNCH_CHECKED(k_iv_rehash, old_table, old_slots, old_table, slots, log2);
+int launch_ivox_rehash(const GridSlot* old_slots, const unsigned long long* old_t, int64_t old_table, GridSlot* slots,
+                       unsigned long long* tlast, int log2, void* stream) {
+    LAUNCH_CHECKED(k_iv_rehash, old_table, old_slots, old_t, old_table, slots, tlast, log2);
 }
+int launch_ivox_newfirst(const IvoxParams& p, uint32_t* out, unsigned long long* n, void* stream) {
+    LAUNCH_CHECKED(k_iv_newfirst, p.table, p, out, n);
+}
+int launch_ivox_oldkeys(const IvoxParams& p, unsigned long long* keys, uint32_t* slot, unsigned long long* n,
+                        void* stream) {
+    LAUNCH_CHECKED(k_iv_oldkeys, p.table, p, keys, slot, n);
+}
+int launch_ivox_untouched(const IvoxParams& p, const uint32_t* sorted_slot, int64_t n, uint32_t* flags, void* stream) {
+    LAUNCH_CHECKED(k_iv_untouched, n, p, sorted_slot, n, flags);
+}
+int launch_ivox_victims(const IvoxParams& p, const uint32_t* sorted_slot, const uint32_t* rank, int64_t n, int64_t ev,
+                        uint32_t j_first, void* stream) {
+    if (n <= 0) return LIVO_OK;
+    hipLaunchKernelGGL(k_iv_victims, blocks_for(n), dim3(256), 0, (hipStream_t)stream, p, sorted_slot, rank, n, ev,
+                       j_first);
+    if (hipGetLastError() != hipSuccess) return LIVO_E_HIP;
+    LAUNCH_CHECKED(k_iv_conflict, n, p, sorted_slot, n, j_first);
+}
+int launch_ivox_tcur_min(const IvoxParams& p, void* stream) { LAUNCH_CHECKED(k_iv_tcur_min, p.table, p); }
+int launch_ivox_mark_min(const IvoxParams& p, void* stream) { LAUNCH_CHECKED(k_iv_mark_min, p.table, p); }
+int launch_ivox_drop(const IvoxParams& p, void* stream) { LAUNCH_CHECKED(k_iv_drop, p.table, p); }
+int launch_ivox_commit(const IvoxParams& p, void* stream) { LAUNCH_CHECKED(k_iv_commit, p.table, p); }
 
 // ---------------------------------------------------- map_incremental ----
 // laser_mapping.cpp:343-380 for one point (stored position j).

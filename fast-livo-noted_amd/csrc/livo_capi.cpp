@@ -82,6 +82,14 @@ struct IvoxDev {
     // overflow pass of the search
     SelElem* big = nullptr;
     int64_t big_threads = 0, big_slice = 0;
+    // LRU grid cache: per slot last-use id, per-batch first / last touch, eviction mark
+    unsigned long long* tlast = nullptr;
+    uint32_t *first = nullptr, *lastp1 = nullptr;
+    uint8_t* evict = nullptr;
+    // eviction scratch (allocated the first time the capacity is reached)
+    unsigned long long *ev_k = nullptr, *ev_k2 = nullptr;
+    uint32_t *ev_a = nullptr, *ev_b = nullptr, *ev_c = nullptr, *ev_d = nullptr;
+    int64_t ev_cap = 0;
 };
 
 // The ikd-Tree incremental map (ikd_incr_kernels.hip): the point set by id
@@ -111,7 +119,7 @@ struct livo_ctx {
     // extra streams for the groups of a batch (overlap of latency-bound kernels)
     hipStream_t xstream[kMaxGroups - 1] = {};
     hipEvent_t xjoin[kMaxGroups - 1] = {};
-    int groups = 4;                    // stream groups per batch (LIVO_STREAM_GROUPS)
+    int groups = 2;                    // stream groups per batch (LIVO_STREAM_GROUPS; MI355X, 8 x 100k scans: 1 / 2 / 4 groups 8884 / 9503 / 9145 updates/s)
     int leaf_size = kLeafSize;         // leaf-map points per leaf (LIVO_LEAF_SIZE)
     hipEvent_t fork = nullptr;
     livo_params params{};
@@ -139,6 +147,8 @@ struct livo_ctx {
     IvoxDev iv;                        // iVox map (LIVO_BACKEND_IVOX)
     void* fe_buf = nullptr;            // scan front-end scratch (livo_scan_preprocess)
     size_t fe_bytes = 0;
+    const float* fe_raw = nullptr;     // the last preprocessed frame, de-skewed, full resolution (5 floats a point)
+    int64_t fe_n = 0;
     void* vio_buf = nullptr;           // VIO frame (image, points, partials, slot)
     size_t vio_bytes = 0;
     void* prim_tmp = nullptr;          // rocPRIM scratch (sorts, scans)
@@ -170,6 +180,16 @@ struct livo_ctx {
     do {                                            \
         if ((x) != hipSuccess) return LIVO_E_HIP;   \
     } while (0)
+
+// Host wait for a stream: spin on hipStreamQuery (microseconds to notice
+// completion), then fall back to the blocking wait after ~50 ms.
+static hipError_t stream_wait(hipStream_t st) {
+    for (int k = 0; k < 200000; k++) {
+        const hipError_t e = hipStreamQuery(st);
+        if (e != hipErrorNotReady) return e;
+    }
+    return hipStreamSynchronize(st);
+}
 
 static int set_device(livo_ctx* c) {
     return hipSetDevice(c->device) == hipSuccess ? LIVO_OK : LIVO_E_HIP;
@@ -345,6 +365,9 @@ static void ivox_free(IvoxDev& v) {
     dev_free(v.ctr);
     dev_free(v.src); dev_free(v.slot_of); dev_free(v.iota); dev_free(v.skeys); dev_free(v.svals);
     dev_free(v.big);
+    dev_free(v.tlast); dev_free(v.first); dev_free(v.lastp1); dev_free(v.evict);
+    dev_free(v.ev_k); dev_free(v.ev_k2);
+    dev_free(v.ev_a); dev_free(v.ev_b); dev_free(v.ev_c); dev_free(v.ev_d);
     v = IvoxDev{};
 }
 
@@ -354,23 +377,35 @@ static int ivox_rehash_to(livo_ctx* c, int log2) {
     if (log2 > 31) return LIVO_E_RANGE;
     const int64_t table = (int64_t)1 << log2;
     GridSlot* slots = nullptr;
-    if (dev_alloc(&slots, (size_t)table)) return LIVO_E_OOM;
+    unsigned long long* tlast = nullptr;
+    if (dev_alloc(&slots, (size_t)table) || dev_alloc(&tlast, (size_t)table)) {
+        dev_free(slots);
+        return LIVO_E_OOM;
+    }
     int rc = launch_ivox_clear(slots, table, c->stream);
-    if (!rc && v.slots) rc = launch_ivox_rehash(v.slots, v.table, slots, log2, c->stream);
+    if (!rc && v.slots) rc = launch_ivox_rehash(v.slots, v.tlast, v.table, slots, tlast, log2, c->stream);
     if (rc) {
         dev_free(slots);
+        dev_free(tlast);
         return rc;
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
     dev_free(v.slots);
+    dev_free(v.tlast);
     dev_free(v.addcnt); dev_free(v.tot); dev_free(v.newstart); dev_free(v.addstart);
+    dev_free(v.first); dev_free(v.lastp1); dev_free(v.evict);
     v.slots = slots;
+    v.tlast = tlast;
     v.table = table;
     v.log2 = log2;
     if (dev_alloc(&v.addcnt, table) || dev_alloc(&v.tot, table) || dev_alloc(&v.newstart, table) ||
-        dev_alloc(&v.addstart, table))
+        dev_alloc(&v.addstart, table) || dev_alloc(&v.first, table) || dev_alloc(&v.lastp1, table) ||
+        dev_alloc(&v.evict, table))
         return LIVO_E_OOM;
     HIP_TRY(hipMemsetAsync(v.addcnt, 0, (size_t)table * sizeof(uint32_t), c->stream));
+    HIP_TRY(hipMemsetAsync(v.first, 0xFF, (size_t)table * sizeof(uint32_t), c->stream));
+    HIP_TRY(hipMemsetAsync(v.lastp1, 0, (size_t)table * sizeof(uint32_t), c->stream));
+    HIP_TRY(hipMemsetAsync(v.evict, 0, (size_t)table, c->stream));
     return LIVO_OK;
 }
 
@@ -453,6 +488,10 @@ static IvoxParams ivox_params(livo_ctx* c) {
     P.range2 = 5.0 * 5.0;  // GetClosestPoint's default max_range (ivox3d.h:79), laser_mapping.cpp:520
     P.scratch = v.big;
     P.slice = v.big_slice;
+    P.tlast = v.tlast;
+    P.first = v.first;
+    P.lastp1 = v.lastp1;
+    P.evict = v.evict;
     return P;
 }
 
@@ -474,31 +513,117 @@ static int ivox_ensure_big(livo_ctx* c) {
 }
 
 // IVox::AddPoints of the n points in v.src (insertion order), on the device.
-static int ivox_add_dev(livo_ctx* c, int64_t n) {
+static int ivox_ev_scratch(livo_ctx* c, int64_t need) {
     IvoxDev& v = c->iv;
-    if (n == 0) return LIVO_OK;
+    if (need <= v.ev_cap) return LIVO_OK;
+    dev_free(v.ev_k); dev_free(v.ev_k2);
+    dev_free(v.ev_a); dev_free(v.ev_b); dev_free(v.ev_c); dev_free(v.ev_d);
+    v.ev_cap = 0;
+    const size_t cap = (size_t)need;
+    if (dev_alloc(&v.ev_k, cap) || dev_alloc(&v.ev_k2, cap) || dev_alloc(&v.ev_a, cap) || dev_alloc(&v.ev_b, cap) ||
+        dev_alloc(&v.ev_c, cap) || dev_alloc(&v.ev_d, cap))
+        return LIVO_E_OOM;
+    v.ev_cap = need;
+    return LIVO_OK;
+}
+
+// IVox::AddPoints (ivox3d.h:256-281) of the points src[off, off + n) as one
+// device batch, with the LRU eviction at capacity.  *done = points consumed:
+// all of them, or (when an eviction would hit a grid the batch itself touches
+// later, or every old grid is touched first) the prefix up to and including
+// the first evicting point, processed with its single eviction -- AddPoints of
+// a prefix then of the rest is AddPoints of the whole.
+static int ivox_add_part(livo_ctx* c, int64_t off, int64_t n, int64_t* done) {
+    IvoxDev& v = c->iv;
+    *done = 0;
     if (v.npts + n > (int64_t)0xFFFFFFFF || v.next_id + n > (int64_t)0x7FFFFFFF) return LIVO_E_RANGE;
     int rc = ivox_ensure_table(c, v.ngrids + n);
     if (rc) return rc;
-    HIP_TRY(hipMemsetAsync(v.ctr, 0, 3 * sizeof(unsigned long long), c->stream));
+    HIP_TRY(hipMemsetAsync(v.ctr, 0, 5 * sizeof(unsigned long long), c->stream));
     IvoxParams P = ivox_params(c);
+    P.src = v.src + 4 * off;
     P.n_src = n;
     rc = launch_ivox_insert(P, c->stream);
     if (rc) return rc;
-    unsigned long long ctr[3];
+    unsigned long long ctr[5];
     HIP_TRY(hipMemcpyAsync(ctr, v.ctr, sizeof(ctr), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    // the largest size the grid map reaches is ngrids + new grids: the LRU
-    // eviction (ivox3d.h:271-274) happens iff that reaches the capacity
-    const bool full = v.ngrids + (int64_t)ctr[1] >= v.prm.capacity;
-    if ((ctr[0] & 1ull) || full) {
+    if (ctr[0] & 1ull) {
         rc = launch_ivox_rollback(P, c->stream);
         if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = LIVO_E_HIP;
-        return rc ? rc : ((ctr[0] & 1ull) ? LIVO_E_RANGE : LIVO_E_CAPACITY);
+        return rc ? rc : LIVO_E_RANGE;
     }
+    const int64_t E = v.ngrids, N_new = (int64_t)ctr[1], C = v.prm.capacity;
+    int64_t ev = std::max<int64_t>(0, E + N_new - (C - 1));  // grids_map_.size() >= capacity_ after a creation
+    int64_t consumed = n;
+    if (ev > 0) {
+        rc = ivox_ev_scratch(c, std::max<int64_t>(v.table, n));
+        if (rc) return rc;
+        // the point of the first eviction: the (C - 1 - E)-th new grid by creation
+        unsigned long long* cnt = v.ctr + 3;  // (scratch counter; ctr[3] is set again below)
+        HIP_TRY(hipMemsetAsync(cnt, 0, sizeof(unsigned long long), c->stream));
+        rc = launch_ivox_newfirst(P, v.ev_a, cnt, c->stream);
+        size_t tb = 0;
+        if (!rc) rc = prim_sort_pairs_u32(nullptr, &tb, v.ev_a, v.ev_b, v.ev_a, v.ev_c, N_new, 32, c->stream);
+        if (!rc) rc = ensure_prim(c, tb);
+        tb = c->prim_bytes;
+        if (!rc) rc = prim_sort_pairs_u32(c->prim_tmp, &tb, v.ev_a, v.ev_b, v.ev_a, v.ev_c, N_new, 32, c->stream);
+        if (rc) return rc;
+        uint32_t j_first = 0;
+        const int64_t c0 = std::max<int64_t>(0, C - 1 - E);
+        HIP_TRY(hipMemcpyAsync(&j_first, v.ev_b + c0, 4, hipMemcpyDeviceToHost, c->stream));
+        // the old grids from the least recently used: victims and the conflict check
+        HIP_TRY(hipMemsetAsync(cnt, 0, sizeof(unsigned long long), c->stream));
+        rc = launch_ivox_oldkeys(P, v.ev_k, v.ev_a, cnt, c->stream);
+        if (rc) return rc;
+        const int64_t n_old = E;
+        tb = 0;
+        rc = prim_sort_pairs_u64(nullptr, &tb, v.ev_k, v.ev_k2, v.ev_a, v.ev_b, n_old, 64, c->stream);
+        if (!rc) rc = ensure_prim(c, tb);
+        tb = c->prim_bytes;
+        if (!rc) rc = prim_sort_pairs_u64(c->prim_tmp, &tb, v.ev_k, v.ev_k2, v.ev_a, v.ev_b, n_old, 64, c->stream);
+        if (!rc) rc = launch_ivox_untouched(P, v.ev_b, n_old, v.ev_c, c->stream);
+        if (!rc) rc = ivox_scan(c, v.ev_c, v.ev_d, n_old);
+        if (rc) return rc;
+        uint32_t tail[2] = {0u, 0u};
+        if (n_old > 0) {
+            HIP_TRY(hipMemcpyAsync(&tail[0], v.ev_d + n_old - 1, 4, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipMemcpyAsync(&tail[1], v.ev_c + n_old - 1, 4, hipMemcpyDeviceToHost, c->stream));
+        }
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        const int64_t untouched = (int64_t)tail[0] + tail[1];
+        bool conflict = ev > untouched;
+        if (!conflict) {
+            HIP_TRY(hipMemsetAsync(v.ctr + 3, 0, sizeof(unsigned long long), c->stream));
+            rc = launch_ivox_victims(P, v.ev_b, v.ev_d, n_old, ev, j_first, c->stream);
+            if (rc) return rc;
+            HIP_TRY(hipMemcpyAsync(ctr, v.ctr, sizeof(ctr), hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            conflict = (ctr[0] & 2ull) != 0;
+        }
+        if (conflict) {
+            // undo, then the prefix [0, j_first] alone: one eviction, of the grid
+            // least recently used at its last point (new grids included)
+            rc = launch_ivox_rollback(P, c->stream);
+            if (rc) return rc;
+            consumed = (int64_t)j_first + 1;
+            P.n_src = consumed;
+            HIP_TRY(hipMemsetAsync(v.ctr, 0, 5 * sizeof(unsigned long long), c->stream));
+            rc = launch_ivox_insert(P, c->stream);
+            if (rc) return rc;
+            HIP_TRY(hipMemsetAsync(v.ctr + 4, 0xFF, sizeof(unsigned long long), c->stream));
+            rc = launch_ivox_tcur_min(P, c->stream);
+            if (!rc) rc = launch_ivox_mark_min(P, c->stream);
+            if (rc) return rc;
+            HIP_TRY(hipMemcpyAsync(ctr, v.ctr, sizeof(ctr), hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            ev = 1;
+        }
+    }
+    const int64_t N_new_b = (int64_t)ctr[1];
     // new CSR buffer
     const int other = 1 - v.cur;
-    const int64_t need = v.npts + n + 3;
+    const int64_t need = v.npts + consumed + 3;
     if (v.pts_cap[other] < need) {
         dev_free(v.pts[other]);
         v.pts_cap[other] = 0;
@@ -514,23 +639,54 @@ static int ivox_add_dev(livo_ctx* c, int64_t n) {
         int bits = 1;
         while (((int64_t)1 << bits) <= v.table) bits++;  // the out-of-range key `table` included
         size_t tb = 0;
-        rc = prim_sort_pairs_u32(nullptr, &tb, v.slot_of, v.skeys, v.iota, v.svals, n, bits, c->stream);
+        rc = prim_sort_pairs_u32(nullptr, &tb, v.slot_of, v.skeys, v.iota, v.svals, consumed, bits, c->stream);
         if (!rc) rc = ensure_prim(c, tb);
         tb = c->prim_bytes;
-        if (!rc) rc = prim_sort_pairs_u32(c->prim_tmp, &tb, v.slot_of, v.skeys, v.iota, v.svals, n, bits, c->stream);
+        if (!rc)
+            rc = prim_sort_pairs_u32(c->prim_tmp, &tb, v.slot_of, v.skeys, v.iota, v.svals, consumed, bits, c->stream);
     }
     if (!rc) rc = launch_ivox_move(P, c->stream);
     if (!rc) rc = launch_ivox_place(P, c->stream);
     if (!rc) rc = launch_ivox_fix(P, c->stream);
+    if (!rc) rc = launch_ivox_commit(P, c->stream);
+    if (!rc && ev > 0) rc = launch_ivox_drop(P, c->stream);
     if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(ctr, v.ctr, sizeof(ctr), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    // the number of points the evicted grids held leaves the map
+    unsigned long long gone = 0;
+    int64_t npts_new = 0;
+    {
+        uint32_t tail[2];
+        HIP_TRY(hipMemcpyAsync(&tail[0], v.newstart + v.table - 1, 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(&tail[1], v.tot + v.table - 1, 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(ctr, v.ctr, sizeof(ctr), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        npts_new = (int64_t)tail[0] + tail[1];
+        (void)gone;
+    }
     v.cur = other;
-    v.npts += n;
-    v.ngrids += (int64_t)ctr[1];
-    v.next_id += n;
+    v.npts = npts_new;
+    v.ngrids += N_new_b - ev;
+    v.next_id += consumed;
     v.max_grid = (int64_t)ctr[2];
-    rc = ivox_trim_table(c);
+    if (ev > 0) {
+        rc = ivox_rehash_to(c, v.log2);  // evicted slots leave holes in the probe chains
+        if (rc) return rc;
+    }
+    *done = consumed;
+    return LIVO_OK;
+}
+
+static int ivox_add_dev(livo_ctx* c, int64_t n) {
+    IvoxDev& v = c->iv;
+    int64_t off = 0;
+    while (off < n) {
+        int64_t done = 0;
+        const int rc = ivox_add_part(c, off, n - off, &done);
+        if (rc) return rc;
+        off += done;
+    }
+    (void)v;
+    const int rc = ivox_trim_table(c);
     return rc ? rc : ivox_ensure_big(c);
 }
 
@@ -814,7 +970,7 @@ const char* livo_error_string(int code) {
         case LIVO_E_NOSCAN: return "unknown scan id";
         case LIVO_E_OOM: return "device allocation failed";
         case LIVO_E_RANGE: return "size out of supported range";
-        case LIVO_E_CAPACITY: return "iVox grid capacity reached (LRU eviction is not done on the device)";
+        case LIVO_E_CAPACITY: return "capacity exceeded";
         default: return "unknown error";
     }
 }
@@ -1217,9 +1373,13 @@ int livo_h_share(livo_ctx* c, int32_t id, const livo_state* state, int search_en
     int rc = ensure_slots(c, 1);
     if (rc) return rc;
     const int64_t N = s->n;
-    // debug scratch: normvec N*4, world N*3, sel N
-    const size_t nvb = (size_t)N * 16, wb = (size_t)N * 12, sb = (size_t)N;
-    rc = ensure_scratch(c, nvb + wb + sb + 64);
+    // debug scratch: normvec N*4, world N*3, sel N; laserCloudOri compaction: flags N, pos N, ori N*3, corr N*4
+    const bool want_ori = out && (out->ori_xyz || out->corr_normvec || out->n_ori);
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t nvb = al((size_t)N * 16), wb = al((size_t)N * 12), sb = al((size_t)N);
+    const size_t fb = want_ori ? al((size_t)N * 4) : 0, ob = want_ori ? al((size_t)N * 12) : 0,
+                 cb = want_ori ? al((size_t)N * 16) : 0;
+    rc = ensure_scratch(c, nvb + wb + sb + 2 * fb + ob + cb + 64);
     if (rc) return rc;
     char* base = (char*)c->scratch;
     init_slot(c->h_slots[0], *state, *state, c->params.max_iterations);
@@ -1229,9 +1389,9 @@ int livo_h_share(livo_ctx* c, int32_t id, const livo_state* state, int search_en
     HsParams hp = make_hs_params(c);
     hp.force = search_en ? 1 : 0;
     const bool want_nv = out && out->normvec, want_sel = out && out->selected, want_w = out && out->world_xyz;
-    hp.dbg.normvec = want_nv ? (float*)base : nullptr;
+    hp.dbg.normvec = (want_nv || want_ori) ? (float*)base : nullptr;
     hp.dbg.world = want_w ? (float*)(base + nvb) : nullptr;
-    hp.dbg.sel = want_sel ? (uint8_t*)(base + nvb + wb) : nullptr;
+    hp.dbg.sel = (want_sel || want_ori) ? (uint8_t*)(base + nvb + wb) : nullptr;
     if (search_en) {
         rc = ensure_replay(c, N);
         if (rc) return rc;
@@ -1250,6 +1410,29 @@ int livo_h_share(livo_ctx* c, int32_t id, const livo_state* state, int search_en
     }
     rc = launch_hshare(hp, 1, std::max(s->nblk, 1), search_en != 0, c->stream);
     if (rc) return rc;
+    // laserCloudOri / corr_normvect: the effective points in the caller's order (:547-561)
+    int64_t n_ori = 0;
+    float *d_ori = nullptr, *d_corr = nullptr;
+    if (want_ori && N > 0) {
+        uint32_t* flags = (uint32_t*)(base + nvb + wb + sb);
+        uint32_t* pos = (uint32_t*)(base + nvb + wb + sb + fb);
+        d_ori = (float*)(base + nvb + wb + sb + 2 * fb);
+        d_corr = (float*)(base + nvb + wb + sb + 2 * fb + ob);
+        rc = launch_ori_flags(hp.dbg.sel, s->d_perm, N, flags, c->stream);
+        if (!rc) rc = ivox_scan(c, flags, pos, N);
+        if (!rc) rc = launch_ori_scatter(s->pts, hp.dbg.normvec, hp.dbg.sel, s->d_perm, pos, N, d_ori, d_corr, c->stream);
+        if (rc) return rc;
+        uint32_t tail[2];
+        HIP_TRY(hipMemcpyAsync(&tail[0], pos + N - 1, 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(&tail[1], flags + N - 1, 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        n_ori = (int64_t)tail[0] + tail[1];
+        if (out->ori_xyz && n_ori > 0)
+            HIP_TRY(hipMemcpyAsync(out->ori_xyz, d_ori, (size_t)n_ori * 12, hipMemcpyDeviceToHost, c->stream));
+        if (out->corr_normvec && n_ori > 0)
+            HIP_TRY(hipMemcpyAsync(out->corr_normvec, d_corr, (size_t)n_ori * 16, hipMemcpyDeviceToHost, c->stream));
+    }
+    if (want_ori && out->n_ori) *out->n_ori = n_ori;
     // the last plane-pass block has reduced the sums into slot->red (hp.solve = 0)
     HIP_TRY(hipMemcpyAsync(c->h_slots, c->d_slots, sizeof(IekfSlot), hipMemcpyDeviceToHost, c->stream));
     std::vector<float> h_nv, h_w;
@@ -1257,15 +1440,15 @@ int livo_h_share(livo_ctx* c, int32_t id, const livo_state* state, int search_en
     if (N > 0 && out) {
         if (want_nv) {
             h_nv.resize((size_t)N * 4);
-            HIP_TRY(hipMemcpyAsync(h_nv.data(), hp.dbg.normvec, nvb, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipMemcpyAsync(h_nv.data(), hp.dbg.normvec, (size_t)N * 16, hipMemcpyDeviceToHost, c->stream));
         }
         if (want_w) {
             h_w.resize((size_t)N * 3);
-            HIP_TRY(hipMemcpyAsync(h_w.data(), hp.dbg.world, wb, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipMemcpyAsync(h_w.data(), hp.dbg.world, (size_t)N * 12, hipMemcpyDeviceToHost, c->stream));
         }
         if (want_sel) {
             h_sel.resize((size_t)N);
-            HIP_TRY(hipMemcpyAsync(h_sel.data(), hp.dbg.sel, sb, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipMemcpyAsync(h_sel.data(), hp.dbg.sel, (size_t)N, hipMemcpyDeviceToHost, c->stream));
         }
     }
     std::vector<NNRec> recs;
@@ -1438,7 +1621,9 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
         HIP_TRY(hipMemcpyAsync(&replays, c->d_replay_total, 8, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipMemsetAsync(c->d_replay_total, 0, 8, c->stream));
     }
-    for (int gi = ngroups - 1; gi >= 0; gi--) HIP_TRY(hipStreamSynchronize(g[gi].st));
+    // wait by polling: the batch is short, and a blocking wait's wake-up
+    // latency was a visible part of the gap between two batches
+    for (int gi = ngroups - 1; gi >= 0; gi--) HIP_TRY(stream_wait(g[gi].st));
     for (int32_t b = 0; b < n; b++) {
         const IekfSlot& s = c->h_slots[b];
         if (model == kModelIkfom) {
@@ -1540,7 +1725,7 @@ int livo_ivox_init(livo_ctx* c, const livo_ivox_params* p) {
     v.prm = prm;
     v.inv_res = (float)(1.0 / (double)prm.resolution);  // options_.inv_resolution_ = 1.0 / resolution_
     v.nearby = nearby;
-    if (dev_alloc(&v.ctr, 3)) return LIVO_E_OOM;
+    if (dev_alloc(&v.ctr, 5)) return LIVO_E_OOM;  // the counters of IvoxParams::ctr
     int rc = ivox_ensure_table(c, 1024);
     if (!rc) rc = ivox_ensure_big(c);
     if (rc) return rc;
@@ -1643,13 +1828,20 @@ int livo_ivox_dump(livo_ctx* c, float* xyz, int32_t* ids, int32_t* keys, int64_t
     if (cap < v.npts) return LIVO_E_RANGE;
     if (set_device(c)) return LIVO_E_HIP;
     std::vector<GridSlot> slots((size_t)v.table);
+    std::vector<unsigned long long> tl((size_t)v.table);
     std::vector<float> pts((size_t)v.npts * 4);
     HIP_TRY(hipStreamSynchronize(c->stream));
     HIP_TRY(hipMemcpy(slots.data(), v.slots, slots.size() * sizeof(GridSlot), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(tl.data(), v.tlast, tl.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     if (v.npts) HIP_TRY(hipMemcpy(pts.data(), v.pts[v.cur], pts.size() * sizeof(float), hipMemcpyDeviceToHost));
+    // grids_cache_ order: most recently used first (the id of each grid's last added point)
+    std::vector<int64_t> order;
+    for (int64_t s2 = 0; s2 < v.table; s2++)
+        if (slots[(size_t)s2].key != kGridEmpty) order.push_back(s2);
+    std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return tl[(size_t)a] > tl[(size_t)b]; });
     int64_t k = 0;
-    for (const GridSlot& g : slots) {
-        if (g.key == kGridEmpty) continue;
+    for (const int64_t s2 : order) {
+        const GridSlot& g = slots[(size_t)s2];
         const int kx = (int)(g.key & 0x1FFFFFull) - kIvBias, ky = (int)((g.key >> 21) & 0x1FFFFFull) - kIvBias,
                   kz = (int)((g.key >> 42) & 0x1FFFFFull) - kIvBias;
         for (uint32_t t = 0; t < g.count && k < v.npts; t++, k++) {
@@ -1821,6 +2013,8 @@ int livo_scan_preprocess(livo_ctx* c, const livo_raw_point* raw, int64_t n, cons
         if (!rc) rc = launch_fe_undistort(F, c->stream);
         if (rc) return rc;
     }
+    c->fe_raw = F.raw;  // feats_undistort stays resident until the next frame (livo_frame_to_world)
+    c->fe_n = n;
     if (undistorted && n > 0)
         HIP_TRY(hipMemcpyAsync(undistorted, F.raw, (size_t)n * 20, hipMemcpyDeviceToHost, c->stream));
     // downSizeFilterSurf: PCL VoxelGrid::applyFilter
@@ -2116,6 +2310,44 @@ int livo_map_dump(livo_ctx* c, float* xyz, int32_t* ids, int64_t cap, int64_t* n
 int livo_map_last_add_stats(livo_ctx* c, livo_map_add_stats* out) {
     if (!c || !out) return LIVO_E_INVALID;
     *out = c->dyn.last;
+    return LIVO_OK;
+}
+
+int livo_frame_to_world(livo_ctx* c, int32_t scan_id, const livo_state* state, livo_raw_point* out, int64_t cap,
+                        int64_t* n_out) {
+    if (!c || !state || !n_out) return LIVO_E_INVALID;
+    const float* src;
+    int64_t n;
+    int stride;
+    const int32_t* perm = nullptr;
+    if (scan_id < 0) {
+        src = c->fe_raw;
+        n = c->fe_raw ? c->fe_n : 0;
+        stride = 5;
+    } else {
+        ScanBuf* s = get_scan(c, scan_id);
+        if (!s) return LIVO_E_NOSCAN;
+        src = s->pts;
+        n = s->n;
+        stride = 4;
+        perm = s->d_perm;
+    }
+    *n_out = n;
+    if (!out || n == 0) return LIVO_OK;
+    if (cap < n) return LIVO_E_RANGE;
+    if (set_device(c)) return LIVO_E_HIP;
+    WorldParams W;
+    std::memcpy(W.rot, state->rot, sizeof(W.rot));
+    std::memcpy(W.pos, state->pos, sizeof(W.pos));
+    std::memcpy(W.R_LI, c->params.R_LI, sizeof(W.R_LI));
+    std::memcpy(W.t_LI, c->params.t_LI, sizeof(W.t_LI));
+    int rc = ensure_scratch(c, (size_t)n * 5 * sizeof(float));
+    if (rc) return rc;
+    float* d_out = (float*)c->scratch;
+    rc = launch_to_world(src, n, stride, perm, W, d_out, c->stream);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(out, d_out, (size_t)n * 5 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
     return LIVO_OK;
 }
 

@@ -149,7 +149,8 @@ struct IvoxParams {
     uint32_t* iota;           // per src point: its index
     const uint32_t* skeys;    // batch sorted by slot (stable)
     const uint32_t* svals;
-    unsigned long long* ctr;  // [0] error bits, [1] new grids, [2] max points per grid
+    unsigned long long* ctr;  // [0] error bits (1 key range, 2 LRU conflict), [1] new grids, [2] max points
+                              // per grid, [3] last victim's sorted position, [4] LRU minimum (single eviction)
     int64_t base_id;          // id of src[0]
     float inv_res;            // Options::inv_resolution_ (float of 1.0 / resolution)
     int32_t log2;
@@ -158,6 +159,13 @@ struct IvoxParams {
     double range2;            // max_range * max_range
     SelElem* scratch;         // overflow pass: one slice per thread
     int64_t slice;            // elements per slice
+    // LRU grid cache (ivox3d.h:256-281): per slot the id of the last point
+    // added to the grid (its place in grids_cache_), and within one AddPoints
+    // batch the first / last (+1) batch index touching it
+    unsigned long long* tlast;
+    uint32_t* first;
+    uint32_t* lastp1;
+    uint8_t* evict;           // per slot: evicted by this batch
 };
 
 // IEKF control block (the loop variables of laser_mapping.cpp:166-238).
@@ -326,7 +334,20 @@ int launch_ivox_prepare(const IvoxParams& p, void* stream);
 int launch_ivox_move(const IvoxParams& p, void* stream);
 int launch_ivox_place(const IvoxParams& p, void* stream);
 int launch_ivox_fix(const IvoxParams& p, void* stream);
-int launch_ivox_rehash(const GridSlot* old_slots, int64_t old_table, GridSlot* slots, int log2, void* stream);
+int launch_ivox_rehash(const GridSlot* old_slots, const unsigned long long* old_t, int64_t old_table, GridSlot* slots,
+                       unsigned long long* tlast, int log2, void* stream);
+// LRU eviction at capacity: the new grids' first touches and the old grids'
+// (last id, slot) compacted for sorting; victims marked; slots dropped; ids committed.
+int launch_ivox_newfirst(const IvoxParams& p, uint32_t* out, unsigned long long* n, void* stream);
+int launch_ivox_oldkeys(const IvoxParams& p, unsigned long long* keys, uint32_t* slot, unsigned long long* n,
+                        void* stream);
+int launch_ivox_untouched(const IvoxParams& p, const uint32_t* sorted_slot, int64_t n, uint32_t* flags, void* stream);
+int launch_ivox_victims(const IvoxParams& p, const uint32_t* sorted_slot, const uint32_t* rank, int64_t n, int64_t ev,
+                        uint32_t j_first, void* stream);
+int launch_ivox_tcur_min(const IvoxParams& p, void* stream);
+int launch_ivox_mark_min(const IvoxParams& p, void* stream);
+int launch_ivox_drop(const IvoxParams& p, void* stream);
+int launch_ivox_commit(const IvoxParams& p, void* stream);
 // GetClosestPoint of every point of every job (+ the overflow pass).
 int launch_ivox_knn(const KnnParams& p, int n_jobs, int64_t max_n, bool later, int64_t overflow_threads,
                     void* stream);
@@ -391,6 +412,16 @@ int launch_fe_morton(const float* pts, int64_t n, int stride, const unsigned* mi
                      unsigned long long* codes, uint32_t* iota, void* stream);
 int launch_fe_gather(const float* pts, int64_t n, int stride, const uint32_t* perm, float* pts4, int32_t* iperm,
                      void* stream);
+struct WorldParams {
+    double rot[9], pos[3], R_LI[9], t_LI[3];
+};
+// RGBpointBodyToWorld of n points (stride floats each, x y z [intensity]) -> n x 5 floats.
+int launch_to_world(const float* src, int64_t n, int stride, const int32_t* perm, const WorldParams& W, float* out5,
+                    void* stream);
+// laserCloudOri / corr_normvect compaction in the caller's order (stored-order sel / normvec / points).
+int launch_ori_flags(const uint8_t* sel, const int32_t* perm, int64_t n, uint32_t* flags, void* stream);
+int launch_ori_scatter(const float* pts4, const float* normvec, const uint8_t* sel, const int32_t* perm,
+                       const uint32_t* pos, int64_t n, float* ori3, float* corr4, void* stream);
 int prim_inclusive_min_scan_i32(void* temp, size_t* temp_bytes, const int32_t* in, int32_t* out, int64_t n,
                                 void* stream);
 int prim_sort_pairs_u64(void* temp, size_t* temp_bytes, const unsigned long long* keys_in,

@@ -67,7 +67,8 @@ class MapInfo(C.Structure):
 
 class PointOut(C.Structure):
     _fields_ = [("normvec", C.c_void_p), ("selected", C.c_void_p), ("nn_idx", C.c_void_p),
-                ("nn_sqdist", C.c_void_p), ("world_xyz", C.c_void_p), ("visits", C.c_void_p)]
+                ("nn_sqdist", C.c_void_p), ("world_xyz", C.c_void_p), ("visits", C.c_void_p),
+                ("ori_xyz", C.c_void_p), ("corr_normvec", C.c_void_p), ("n_ori", C.c_void_p)]
 
 
 class Timings(C.Structure):
@@ -189,6 +190,7 @@ SIGNATURES = {
     "livo_map_delete_boxes": (C.c_int, [_P, _P, C.c_int64, C.POINTER(C.c_int64)]),
     "livo_map_dump": (C.c_int, [_P, _P, _P, C.c_int64, C.POINTER(C.c_int64)]),
     "livo_map_last_add_stats": (C.c_int, [_P, C.POINTER(MapAddStats)]),
+    "livo_frame_to_world": (C.c_int, [_P, C.c_int32, C.POINTER(State), _P, C.c_int64, C.POINTER(C.c_int64)]),
     "livo_sync": (C.c_int, [_P]),
 }
 
@@ -347,16 +349,33 @@ class Context:
         if outputs:
             res = {"normvec": np.zeros((n, 4), np.float32), "sel": np.zeros(n, np.uint8),
                    "nn_idx": np.zeros((n, 5), np.int32), "nn_d": np.zeros((n, 5), np.float32),
-                   "world": np.zeros((n, 3), np.float32), "visits": np.zeros(1, np.int64)}
+                   "world": np.zeros((n, 3), np.float32), "visits": np.zeros(1, np.int64),
+                   "ori": np.zeros((n, 3), np.float32), "corr_normvec": np.zeros((n, 4), np.float32),
+                   "n_ori": np.zeros(1, np.int64)}
             po = PointOut(_ptr(res["normvec"]), _ptr(res["sel"]), _ptr(res["nn_idx"]), _ptr(res["nn_d"]),
-                          _ptr(res["world"]), _ptr(res["visits"]))
+                          _ptr(res["world"]), _ptr(res["visits"]), _ptr(res["ori"]), _ptr(res["corr_normvec"]),
+                          _ptr(res["n_ori"]))
         st = state_to_c(state)
         _check("livo_h_share", self._L.livo_h_share(self.h, sid, C.byref(st), int(bool(search_en)), _ptr(HTH),
                                                     _ptr(HTL), C.byref(eff), C.byref(po) if po else None))
         res.update({"HTH": HTH.reshape(9, 9), "HTL": HTL, "effct": eff.value})
         if outputs:
             res["visits"] = int(res["visits"][0])
+            k = int(res.pop("n_ori")[0])
+            res["ori"] = res["ori"][:k]                    # laserCloudOri
+            res["corr_normvec"] = res["corr_normvec"][:k]  # corr_normvect
         return res
+
+    def frame_to_world(self, state: dict, sid: int = -1) -> np.ndarray:
+        """RGBpointBodyToWorld of the last preprocessed full-res frame (sid < 0) or a resident
+        scan: (n, 5) float32 x, y, z (world), intensity, curvature (livo_frame_to_world)."""
+        st = state_to_c(state)
+        n = C.c_int64()
+        _check("livo_frame_to_world", self._L.livo_frame_to_world(self.h, sid, C.byref(st), None, 0, C.byref(n)))
+        out = np.zeros((n.value, 5), np.float32)
+        _check("livo_frame_to_world", self._L.livo_frame_to_world(self.h, sid, C.byref(st), _ptr(out), n.value,
+                                                                  C.byref(n)))
+        return out
 
     def iekf_update(self, sid: int, state: dict, prior: dict | None = None):
         st = state_to_c(state)

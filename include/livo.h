@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define LIVO_ABI_VERSION 2
+#define LIVO_ABI_VERSION 3
 #define LIVO_DIM_STATE 18        /* DIM_STATE, include/common_lib.h:32 */
 #define LIVO_NUM_MATCH_POINTS 5  /* NUM_MATCH_POINTS, include/common_lib.h:37 */
 #define LIVO_MAX_EVALS 16        /* max h_share/solve evaluations per scan update */
@@ -64,8 +64,7 @@ enum {
     LIVO_E_NOSCAN = -4,    /* unknown / released scan id */
     LIVO_E_OOM = -5,       /* device allocation failed */
     LIVO_E_RANGE = -6,     /* size beyond the supported range */
-    LIVO_E_CAPACITY = -7   /* iVox grid count would reach Options::capacity_ (LRU eviction
-                              is not done on the device; the map is left unchanged) */
+    LIVO_E_CAPACITY = -7   /* capacity exceeded (reserved) */
 };
 
 typedef struct livo_ctx livo_ctx;
@@ -120,6 +119,11 @@ typedef struct livo_point_out {
     float* nn_sqdist;     /* N*5: squared distances (pointSearchSqDis), +inf pad                */
     float* world_xyz;     /* N*3: feats_down_world (pointBodyToWorld, :508)                      */
     int64_t* visits;      /* 1:   k-NN nodes visited over all points (the V_ref yardstick)       */
+    /* laserCloudOri / corr_normvect (:547-561): the effective points (selected and
+     * |pd2| <= 2), compacted in the caller's point order; capacity N each. */
+    float* ori_xyz;       /* n_ori*3: body points (laserCloudOri)                                */
+    float* corr_normvec;  /* n_ori*4: their plane normal and pd2 (corr_normvect)                 */
+    int64_t* n_ori;       /* 1:   effct_feat_num                                                 */
 } livo_point_out;
 
 /* Device time of the kernels of the last livo_iekf_update* call (profiling mode only).
@@ -267,8 +271,11 @@ int livo_ivox_params_default(livo_ivox_params* p);
 /* IVox(Options) (ivox3d.h:64-67, laser_mapping.cpp:776): an empty map. */
 int livo_ivox_init(livo_ctx* ctx, const livo_ivox_params* p);
 /* IVox::AddPoints (ivox3d.h:256-281) of n host points, in order (the first
- * scan's feats_down_body, laser_mapping.cpp:147).  Point ids continue from
- * ids_issued.  LIVO_E_CAPACITY / LIVO_E_RANGE leave the map unchanged. */
+ * scan's feats_down_body, laser_mapping.cpp:147), with the LRU grid cache:
+ * once a new grid takes the grid count to capacity, the grid whose last added
+ * point is the oldest is evicted with its points (:270-274).  Point ids
+ * continue from ids_issued.  LIVO_E_RANGE (a key beyond the supported cell
+ * range) leaves the map unchanged. */
 int livo_ivox_add_points(livo_ctx* ctx, const float* xyz, int64_t n, int64_t stride_bytes);
 /* IVox::GetClosestPoint(pt, closest_pt, max_num, max_range) (ivox3d.h:132-204)
  * for n host queries: idx / sqdist n*max_num in the reference's order (the
@@ -277,8 +284,9 @@ int livo_ivox_add_points(livo_ctx* ctx, const float* xyz, int64_t n, int64_t str
 int livo_ivox_knn(livo_ctx* ctx, const float* q_xyz, int64_t n, int32_t max_num, double max_range, int32_t* idx,
                   float* sqdist, int32_t* cnt);
 int livo_ivox_get_info(livo_ctx* ctx, livo_ivox_info* out);
-/* Every point, grid by grid (grid order unspecified, insertion order inside a
- * grid): xyz n*3, ids n, keys n*3 (the grid of each point); any may be NULL.
+/* Every point, grid by grid in grids_cache_ order (most recently used grid
+ * first, insertion order inside a grid): xyz n*3, ids n, keys n*3 (the grid
+ * of each point); any may be NULL.
  * *n = points; LIVO_E_RANGE if cap < *n (nothing written). */
 int livo_ivox_dump(livo_ctx* ctx, float* xyz, int32_t* ids, int32_t* keys, int64_t cap, int64_t* n);
 
@@ -414,6 +422,15 @@ int livo_map_dump(livo_ctx* ctx, float* xyz, int32_t* ids, int64_t cap, int64_t*
 /* Statistics of the last livo_map_add_points / ikd-Tree livo_map_incremental. */
 int livo_map_last_add_stats(livo_ctx* ctx, livo_map_add_stats* out);
 
+/* RGBpointBodyToWorld (src/laser_mapping.cpp:647-660) over laserCloudFullRes
+ * (:258-265) at `state`: scan_id < 0 takes the last livo_scan_preprocess frame
+ * at full resolution (feats_undistort, dense_map_en; resident until the next
+ * frame), scan_id >= 0 a resident scan (feats_down_body, in the caller's point
+ * order; intensity 0: a resident scan keeps x, y, z only).  out: n points
+ * (world x, y, z; intensity copied; curvature 0), *n = their count; out may be
+ * NULL to query the count, else cap >= *n (LIVO_E_RANGE otherwise). */
+int livo_frame_to_world(livo_ctx* ctx, int32_t scan_id, const livo_state* state, livo_raw_point* out, int64_t cap,
+                        int64_t* n);
 int livo_sync(livo_ctx* ctx);
 
 #ifdef __cplusplus

@@ -90,6 +90,7 @@ def lib():
         L.orc_knn.argtypes = [P, P, C.c_int64, C.c_int, P, P, P, C.c_int]
         L.orc_knn_brute.argtypes = [P, C.c_int64, P, C.c_int64, C.c_int, P, P, C.c_int]
         L.orc_esti_plane.argtypes = [P, C.c_float, P]
+        L.orc_to_world.argtypes = [P, C.c_int64, C.c_int, P, P, P, P, P]
         L.orc_h_share.argtypes = [P, P, C.c_int64, P, P, P, P, C.c_int, C.c_double, P, P, P, P, P, P, P, P,
                                   P, P, C.c_int]
         L.orc_iekf_update.argtypes = [P, P, C.c_int64, P, P, C.c_double, C.c_int, C.POINTER(OrcState),
@@ -239,6 +240,19 @@ def mtk(op: int, a, b):
         out = np.zeros({0: 3, 1: 2, 2: 9}[op])
     b_buf = np.ascontiguousarray(b, np.float64)
     assert lib().orc_ikfom_mtk(op, _p(a_buf), _p(b_buf), _p(out)) == 0
+    return out
+
+
+def to_world(pts, state: dict, R_LI=None, t_LI=None) -> np.ndarray:
+    """RGBpointBodyToWorld of (n, 3) or (n, 5) points -> (n, 5) float32 (orc_to_world)."""
+    pts = np.ascontiguousarray(pts, np.float32)
+    n, stride = pts.shape
+    out = np.zeros((n, 5), np.float32)
+    rot = np.ascontiguousarray(state["rot"], np.float64)
+    pos = np.ascontiguousarray(state["pos"], np.float64)
+    R_LI = np.ascontiguousarray(np.eye(3) if R_LI is None else R_LI, np.float64)
+    t_LI = np.ascontiguousarray(np.zeros(3) if t_LI is None else t_LI, np.float64)
+    assert lib().orc_to_world(_p(pts), n, stride, _p(rot), _p(pos), _p(R_LI), _p(t_LI), _p(out)) == 0
     return out
 
 

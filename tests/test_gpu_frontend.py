@@ -123,3 +123,28 @@ def test_preprocess_edge_cases(fctx):
     sid, und, _ = fctx.scan_preprocess(raw, poses[:1], Re, pe, leaf_size=0.0)  # one pose: nothing to undo
     fctx.scan_release(sid)
     assert np.array_equal(und, raw)
+
+
+@pytest.mark.parametrize("n", [30_000, 0])
+def test_frame_to_world(fctx, n):
+    """RGBpointBodyToWorld over laserCloudFullRes (laser_mapping.cpp:258-265, 647-660):
+    the de-skewed full-resolution frame (feats_undistort, kept on the device by
+    livo_scan_preprocess) and the downsampled resident scan (feats_down_body, in the
+    caller's point order), at the updated state: bit-exact against the oracle's
+    transform of the same body points."""
+    import oracle
+    from livo_amd import synth
+    raw, poses, Re, pe = synth.make_raw_scan(max(n, 1), 4)
+    raw = raw[:n]
+    sid, und, down = fctx.scan_preprocess(raw, poses, Re, pe, leaf_size=0.5)
+    try:
+        st = synth.make_state(4)
+        w = fctx.frame_to_world(st)  # the full-resolution frame
+        ref = oracle.to_world(und, st, t_LI=synth.T_LI)
+        assert w.shape == (n, 5)
+        assert np.array_equal(w.view(np.uint32), ref.view(np.uint32))
+        wd = fctx.frame_to_world(st, sid)  # the resident scan (x, y, z only: intensity 0)
+        refd = oracle.to_world(down[:, :3], st, t_LI=synth.T_LI)
+        assert np.array_equal(wd.view(np.uint32), refd.view(np.uint32))
+    finally:
+        fctx.scan_release(sid)

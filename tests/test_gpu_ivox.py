@@ -134,19 +134,32 @@ def test_ivox_add_points_batches_match_oracle(ivctx):
     assert ivctx.ivox_info()["ids_issued"] == iv.info()["ids_issued"]
 
 
-def test_ivox_capacity_leaves_map_unchanged(ivctx):
-    import livo_amd
-    rng = np.random.default_rng(2)
-    ivctx.ivox_init(resolution=0.5, nearby_type=6, capacity=200)
-    a = rng.uniform(-1, 1, size=(50, 3)).astype(np.float32)
-    ivctx.ivox_add_points(a)
-    before = ivctx.ivox_dump()
-    with pytest.raises(livo_amd.LivoError) as e:
-        ivctx.ivox_add_points(rng.uniform(-50, 50, size=(5000, 3)).astype(np.float32))
-    assert e.value.code == -7
-    after = ivctx.ivox_dump()
-    assert all(np.array_equal(x, y) for x, y in zip(before, after))
-    assert ivctx.ivox_info()["ids_issued"] == 50
+@pytest.mark.parametrize("cap", [1, 7, 50, 200, 10_000])
+def test_ivox_lru_eviction_matches_oracle(ivctx, cap):
+    """IVox::AddPoints' LRU grid cache at capacity (ivox3d.h:256-281): batches
+    that evict (untouched old grids: one device pass; grids the batch touches
+    before or after an eviction: split at the eviction), including capacity 1
+    (a new grid evicts itself).  Grids, their points, ids and the
+    most-recently-used order equal the oracle's after every batch."""
+    import oracle
+    rng = np.random.default_rng(11 + cap)
+    ivctx.ivox_init(resolution=0.5, nearby_type=6, capacity=cap)
+    iv = oracle.Ivox(resolution=0.5, nearby_type=6, capacity=cap)
+    near = rng.uniform(-2, 2, size=(3000, 3)).astype(np.float32)   # revisits grids
+    far = rng.uniform(-40, 40, size=(3000, 3)).astype(np.float32)  # mostly new grids
+    for pts in (near[:400], far[:1500], near[400:1000], far[1500:1501], near[1000:], far[1501:]):
+        ivctx.ivox_add_points(pts)
+        iv.add_points(pts)
+        gx, gi, gk = ivctx.ivox_dump()
+        rx, ri, rg, rk = iv.dump()
+        assert np.array_equal(gi, ri)
+        assert np.array_equal(gx.view(np.uint32), rx.view(np.uint32))
+        assert np.array_equal(gk, rk[rg])
+        assert ivctx.ivox_info()["num_grids"] == iv.info()["num_grids"]
+    assert ivctx.ivox_info()["ids_issued"] == iv.info()["ids_issued"]
+    # the searches see the evicted map
+    q = rng.uniform(-3, 3, size=(2000, 3)).astype(np.float32)
+    _knn_equal(ivctx, iv, q, max_range=5.0)
 
 
 def _hs_equal(g, r):

@@ -104,7 +104,12 @@ def test_knn_empty_map(built):
         assert np.all(idx == -1) and np.all(np.isinf(d))
 
 
-def _hshare_compare(g, r, n):
+def _hshare_compare(g, r, n, body=None):
+    # laserCloudOri / corr_normvect (laser_mapping.cpp:547-561): the effective points in point order
+    if body is not None:
+        eff = r["sel"] != 0
+        assert np.array_equal(g["ori"], np.asarray(body, np.float32)[eff])
+        assert np.array_equal(g["corr_normvec"].view(np.uint32), r["normvec"][eff].view(np.uint32))
     assert np.array_equal(g["nn_idx"], r["cache"]["idx"])
     assert np.array_equal(g["nn_d"].view(np.uint32), r["cache"]["d"].view(np.uint32))
     assert np.array_equal(g["normvec"].view(np.uint32), r["normvec"].view(np.uint32))
@@ -124,14 +129,14 @@ def test_h_share_parity(ctx100k, tree100k):
         r = tree100k.h_share(body, st["rot"], st["pos"], np.eye(3), synth.T_LI, True)
         world = ((body.astype(np.float64) + synth.T_LI) @ st["rot"].T + st["pos"]).astype(np.float32)
         assert np.abs(g["world"] - world).max() <= 1e-5
-        _hshare_compare(g, r, len(body))
+        _hshare_compare(g, r, len(body), body)
         assert g["visits"] == r["visits"]  # identical traversal => identical node visits
         # re-fit at a moved state, reusing the cached neighbours (nearest_search_en = false)
         st2 = dict(st)
         st2["pos"] = st["pos"] + np.array([0.01, -0.02, 0.005])
         g2 = ctx100k.h_share(sid, st2, search_en=False)
         r2 = tree100k.h_share(body, st2["rot"], st2["pos"], np.eye(3), synth.T_LI, False, cache=r["cache"])
-        _hshare_compare(g2, r2, len(body))
+        _hshare_compare(g2, r2, len(body), body)
     finally:
         ctx100k.scan_release(sid)
 
@@ -223,7 +228,7 @@ def test_ragged_scans(ctx100k, tree100k, n):
     try:
         g = ctx100k.h_share(sid, st0, True)
         r = tree100k.h_share(body, st0["rot"], st0["pos"], np.eye(3), synth.T_LI, True)
-        _hshare_compare(g, r, n)
+        _hshare_compare(g, r, n, body)
         sg, stg = ctx100k.iekf_update(sid, st0)
         assert stg["iterations"] >= 1
     finally:
