@@ -148,6 +148,15 @@ __global__ void k_add_prep(DynAddParams P) {
         return;
     }
     const unsigned long long k = pack_key(j[0], j[1], j[2]);
+    // every later pass reads the grid cells of this point's box: check their
+    // range here, so that an out-of-range batch is refused before anything changes
+    {
+        int l[3], h[3];
+        if (!box_cells(P, dbox(k, P.ds), l, h)) {
+            atomicOr(P.ctr + kDynError, 1ull);
+            return;
+        }
+    }
     P.keys[i] = k;
     if (clean) return;
     // processed in box k, lying inside the boxes of `mem`: all of them go to the sequential pass

@@ -897,7 +897,9 @@ static int dyn_add(livo_ctx* c, int64_t n, float ds, bool downsample, livo_map_a
         HIP_TRY(hipMemcpyAsync(&tail[1], d.keep + n - 1, 4, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipMemcpyAsync(h, d.ctr, sizeof(h), hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
-        if (h[kDynError]) return LIVO_E_RANGE;
+        // k_add_prep checked the range of every box the later passes read, so
+        // the group / sequential passes cannot fail once the map is modified
+        if (h[kDynError]) return LIVO_E_HIP;
         const int64_t added = (int64_t)tail[0] + tail[1];
         rc = launch_add_append(d.W, d.keep, d.apos, n, d.n_ids, d.all, d.alive, c->stream);
         if (rc) return rc;

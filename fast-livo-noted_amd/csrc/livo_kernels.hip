@@ -713,11 +713,33 @@ __device__ __forceinline__ void lq_init(LeafQuery& q, const KnnParams& P, const 
 
 __device__ __forceinline__ float lq_thr(const LeafQuery& q) { return fminf(q.d[kNN - 1], q.B); }
 
+#ifndef LIVO_INSERT_POS
+#define LIVO_INSERT_POS 0  // 1: position-compare insertion (shorter dependency chain)
+#endif
+#ifndef LIVO_TILE_CHUNK
+#define LIVO_TILE_CHUNK 8  // LDS points read per step of a cell's run
+#endif
 __device__ __forceinline__ void lq_point(LeafQuery& q, const float4 v, uint32_t slot) {
     const float dx = q.qx - v.x, dy = q.qy - v.y, dz = q.qz - v.z;
     const float dist = (dx * dx + dy * dy) + dz * dz;  // calc_dist (:1291-1295)
     if (dist < q.d[kNN - 1]) {
         q.e6 = fminf(q.e6, q.d[kNN - 1]);  // evicted (+inf while not full)
+#if LIVO_INSERT_POS
+        // stable insertion after every entry <= dist, all positions at once:
+        // c[k] = d[k-1] <= dist (monotone in k); entry k shifts down where !c[k]
+        bool c[kNN + 1];
+#pragma unroll
+        for (int k = 1; k < kNN; k++) c[k] = q.d[k - 1] <= dist;
+        c[kNN] = false;
+#pragma unroll
+        for (int k = kNN - 1; k >= 1; k--) {
+            const bool here = c[k] && !c[k + 1];
+            q.d[k] = !c[k] ? q.d[k - 1] : (here ? dist : q.d[k]);
+            q.nd[k] = !c[k] ? q.nd[k - 1] : (here ? slot : q.nd[k]);
+        }
+        q.d[0] = c[1] ? q.d[0] : dist;
+        q.nd[0] = c[1] ? q.nd[0] : slot;
+#else
         q.d[kNN - 1] = dist;
         q.nd[kNN - 1] = slot;
 #pragma unroll
@@ -730,6 +752,7 @@ __device__ __forceinline__ void lq_point(LeafQuery& q, const float4 v, uint32_t 
             q.d[k - 1] = sw ? td : q.d[k - 1];
             q.nd[k - 1] = sw ? tn : q.nd[k - 1];
         }
+#endif
     } else {
         q.e6 = fminf(q.e6, dist);
     }
@@ -949,7 +972,7 @@ __device__ __forceinline__ unsigned long long grid_key_d(int cx, int cy, int cz)
 // global path.
 template <int CELLS, int PTS>
 struct TileLds {
-    float4 pts[PTS + 4];      // the box's points (x, y, z, gpts index bits); +4: chunked reads
+    float4 pts[PTS + 8];      // the box's points (x, y, z, gpts index bits); +8: chunked reads
     uint32_t off[CELLS + 1];  // LDS start of each cell's run
     uint32_t start[CELLS];    // its start in gpts
     uint32_t wred[16];        // per-wave partials of the block scans
@@ -1175,7 +1198,17 @@ __device__ __forceinline__ void grid_cell(const KnnParams& P, const LeafQuery& q
 // The exact 5-NN of one query on the cell grid (stages 0-2 above); cells of an
 // active tile come from LDS.  Returns whether the list is certified exact.
 __device__ __forceinline__ bool grid_search(LeafQuery& q, const KnnParams& P, int c0, int c1, int c2, int s0, int s1,
-                                            int s2, const TileView& tv, unsigned& visits, unsigned& npts) {
+                                            int s2, const TileView& tv, unsigned& visits, unsigned& npts,
+                                            unsigned long long* prof = nullptr) {
+    // (prof: profiling builds, thread 0's stage cycles)
+    unsigned long long pt = prof ? __builtin_amdgcn_s_memtime() : 0ull;
+    auto mark = [&](int k) {
+        if (prof) {
+            const unsigned long long now = __builtin_amdgcn_s_memtime();
+            atomicAdd(prof + k, now - pt);
+            pt = now;
+        }
+    };
     const float4* __restrict__ gpts = reinterpret_cast<const float4*>(P.gpts);
     const GridSlot* __restrict__ slots = P.gslots;
     const float h = P.gh, eps = P.geps;
@@ -1189,12 +1222,13 @@ __device__ __forceinline__ bool grid_search(LeafQuery& q, const KnnParams& P, in
         if (tv.on && cx >= tv.lo0 && cx <= tv.hi0 && cy >= tv.lo1 && cy <= tv.hi1 && cz >= tv.lo2 && cz <= tv.hi2) {
             const int t = ((cz - tv.lo2) * tv.d1 + (cy - tv.lo1)) * tv.d0 + (cx - tv.lo0);
             const int lo = (int)tv.off[t], hi = (int)tv.off[t + 1];
-            for (int k0 = lo; k0 < hi; k0 += 4) {
-                float4 v[4];
+            constexpr int CH = LIVO_TILE_CHUNK;
+            for (int k0 = lo; k0 < hi; k0 += CH) {
+                float4 v[CH];
 #pragma unroll
-                for (int u = 0; u < 4; u++) v[u] = tv.pts[k0 + u];  // padded by 4 points
+                for (int u = 0; u < CH; u++) v[u] = tv.pts[k0 + u];  // padded by CH points
 #pragma unroll
-                for (int u = 0; u < 4; u++)
+                for (int u = 0; u < CH; u++)
                     if (k0 + u < hi) lq_point(q, v[u], __float_as_uint(v[u].w));
             }
             return;
@@ -1253,6 +1287,7 @@ __device__ __forceinline__ bool grid_search(LeafQuery& q, const KnnParams& P, in
 #pragma unroll 1
     for (int b = 0; b < 8; b++)
         visit(c0 + ((b & 1) ? s0 : 0), c1 + ((b & 2) ? s1 : 0), c2 + ((b & 4) ? s2 : 0));
+    mark(0);
     const CBox blk{c0 + min(s0, 0), c0 + max(s0, 0), c1 + min(s1, 0), c1 + max(s1, 0), c2 + min(s2, 0),
                    c2 + max(s2, 0)};
     const CBox cube{c0 - 1, c0 + 1, c1 - 1, c1 + 1, c2 - 1, c2 + 1};
@@ -1267,6 +1302,7 @@ __device__ __forceinline__ bool grid_search(LeafQuery& q, const KnnParams& P, in
         r1 = cube;
     }
     scan_box(r1, blk);
+    mark(1);
     // still fewer than 5 points (sparse map): cubes of radius 2, 3, ...
     CBox vis = cube;
 #pragma unroll 1
@@ -1284,9 +1320,11 @@ __device__ __forceinline__ bool grid_search(LeafQuery& q, const KnnParams& P, in
         const double span = (double)(r2.h0 - r2.l0 + 1) * (double)(r2.h1 - r2.l1 + 1) * (double)(r2.h2 - r2.l2 + 1);
         if (span <= (double)kGridMaxCells) {
             scan_box(r2, vis);
+            mark(2);
             return true;
         }
     }
+    mark(2);
     return false;
 }
 
@@ -1857,9 +1895,22 @@ __device__ __forceinline__ void solve_scan(IekfSlot* slot, SolveLds& L, const in
 // One point of h_share_model (laser_mapping.cpp:503-593): world point, gate,
 // plane (esti_plane, or the plane cached since the last search), residual
 // gates, Jacobian row and its HᵀH / HᵀL terms added to acc.
+// Point i's loads, issued together (one memory round trip): the body point and,
+// for an evaluation without a search, the cached plane state and plane.
+struct HsPointIn {
+    float4 pb, plane;
+    uint8_t ps;
+};
+__device__ __forceinline__ HsPointIn hshare_load(const HsJob& job, int i, bool cached) {
+    HsPointIn in;
+    in.pb = reinterpret_cast<const float4*>(job.pts)[i];
+    in.ps = cached ? job.pstate[i] : 0;
+    in.plane = cached ? reinterpret_cast<const float4*>(job.plane)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    return in;
+}
 __device__ __forceinline__ void hshare_point(const HsParams& P, const HsJob& job, const livo_state& S, int i,
-                                             int search, double (&acc)[kRedUsed]) {
-            const float4 pb = reinterpret_cast<const float4*>(job.pts)[i];
+                                             int search, double (&acc)[kRedUsed], const HsPointIn& in) {
+            const float4 pb = in.pb;
             const double* R = S.rot;
             float wx, wy, wz;
             world_point(R, S.pos, P.R_LI, P.t_LI, pb.x, pb.y, pb.z, wx, wy, wz);
@@ -1874,7 +1925,7 @@ __device__ __forceinline__ void hshare_point(const HsParams& P, const HsJob& job
             // 0 not fitted yet, 1 no plane, 2 plane) and reused bit for bit.
             bool plane_ok = false;
             float pa[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-            uint8_t ps = search ? 0 : job.pstate[i];
+            uint8_t ps = search ? 0 : in.ps;
             if (ps == 0) {
                 const float4* rec = reinterpret_cast<const float4*>(job.nn + i);
                 float nx[kNN], ny[kNN], nz[kNN];
@@ -1899,7 +1950,7 @@ __device__ __forceinline__ void hshare_point(const HsParams& P, const HsJob& job
                 job.pstate[i] = ps;
                 if (plane_ok) reinterpret_cast<float4*>(job.plane)[i] = make_float4(pa[0], pa[1], pa[2], pa[3]);
             } else if (ps == 2) {
-                const float4 v = reinterpret_cast<const float4*>(job.plane)[i];
+                const float4 v = in.plane;
                 pa[0] = v.x; pa[1] = v.y; pa[2] = v.z; pa[3] = v.w;
                 plane_ok = true;
             }
@@ -1958,7 +2009,7 @@ __device__ __forceinline__ void hshare_point(const HsParams& P, const HsJob& job
 // reduces every partial in a fixed order and (P.solve) its wave 0 runs the
 // scan's solve.  nblk = blocks of the scan in this launch, NT threads.
 struct HsReduceLds {
-    double red[16 * kRedCols];
+    double red[16 * kRedCols];  // one partial per 16-lane row (NT = 256)
     double fin[8 * kRedCols];
     int last;
 };
@@ -1967,12 +2018,12 @@ __device__ __forceinline__ void hshare_reduce_solve(const HsParams& P, const HsJ
                                                     double (&acc)[kRedUsed], int nblk, unsigned blk, HsReduceLds& R,
                                                     SolveLds& L) {
     const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
-    constexpr int NW = NT / 64;
+    constexpr int NR = NT / 16;  // 16-lane rows of the block
+    static_assert(NR <= 16, "HsReduceLds holds 16 row partials");
 #pragma unroll
     for (int j = 0; j < kRedUsed; j++) {
-        const double v = wave_sum(acc[j]);
-        if (lane == 0) R.red[wave * kRedCols + j] = v;
+        const double v = row_sum16(acc[j]);
+        if ((tid & 15) == 0) R.red[(tid >> 4) * kRedCols + j] = v;
     }
     __syncthreads();
     // Wave 0 stores the block partial write-through (sc1) and, once the store
@@ -1983,9 +2034,14 @@ __device__ __forceinline__ void hshare_reduce_solve(const HsParams& P, const HsJ
     // solve kernel.
     if (tid < 64) {
         if (tid < kRedUsed) {
-            double v = R.red[tid];
+            double r[16];
 #pragma unroll
-            for (int w = 1; w < NW; w++) v = v + R.red[w * kRedCols + tid];
+            for (int w = 0; w < 16; w++) r[w] = w < NR ? R.red[w * kRedCols + tid] : 0.0;
+#pragma unroll
+            for (int h = 8; h >= 1; h >>= 1)  // fixed pairwise tree
+#pragma unroll
+                for (int w = 0; w < h; w++) r[w] = r[w] + r[w + h];
+            const double v = r[0];
             __hip_atomic_store(job.partial + (size_t)blk * kRedCols + tid, v, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -2059,7 +2115,7 @@ __global__ __launch_bounds__(kBlock) void k_hshare(HsParams P) {
     for (int j = 0; j < kRedUsed; j++) acc[j] = 0.0;
     for (int rep = 0; rep < kPtsPerThread; rep++) {  // points of this block: strided for coalescing
         const int i = (blockIdx.x * kPtsPerThread + rep) * kBlock + threadIdx.x;
-        if (i < job.n) hshare_point(P, job, S, i, search, acc);
+        if (i < job.n) hshare_point(P, job, S, i, search, acc, hshare_load(job, i, !search));
     }
     hshare_reduce_solve<kBlock>(P, job, slot, acc, job.nblk, blockIdx.x, R, L);
 }
@@ -2105,12 +2161,32 @@ struct EvalParams {
     HsParams h;
 };
 
+#ifdef LIVO_EVAL_PROF  // per-phase block time of k_iekf_eval (tools/eval_prof.py; compiled out of the product)
+// [search][phase]: cycles summed over blocks (thread 0's s_memtime deltas) and block counts
+__device__ unsigned long long g_eval_prof[2][8];
+#define EVAL_MARK(k)                                                                                   \
+    do {                                                                                               \
+        if (threadIdx.x == 0) {                                                                        \
+            const unsigned long long now = __builtin_amdgcn_s_memtime();                              \
+            if ((k) > 0) atomicAdd(&g_eval_prof[search ? 1 : 0][(k)], now - prof_t);                  \
+            else atomicAdd(&g_eval_prof[search ? 1 : 0][0], 1ull);                                     \
+            prof_t = now;                                                                              \
+        }                                                                                              \
+    } while (0)
+#define EVAL_MARK_SYNC(k) do { __syncthreads(); EVAL_MARK(k); } while (0)
+#define EVAL_PROF_DECL unsigned long long prof_t = 0
+#else
+#define EVAL_MARK(k) do { } while (0)
+#define EVAL_MARK_SYNC(k) do { } while (0)
+#define EVAL_PROF_DECL do { } while (0)
+#endif
 #ifndef LIVO_EVAL_WAVES
 #define LIVO_EVAL_WAVES 4  // waves per SIMD the VGPR budget must allow (<= 128 VGPRs)
 #endif
 template <bool FIRST>
 __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalParams E) {
     const KnnParams& P = E.k;
+    EVAL_PROF_DECL;
     __shared__ union {
         BlockTile tile;
         SolveLds solve;  // the scan's last block solves after its search is done
@@ -2120,11 +2196,15 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
     xcd_block(P.nb, bjob, bx);
     const HsJob job = P.jobs[bjob];
     IekfSlot* slot = job.slot;
-    if (slot->ctrl.stop) return;  // block-uniform
     if (bx > 0 && (int)bx * kEvalBlock >= job.n) return;  // (an empty scan keeps one block: it solves)
-    const int search = FIRST ? 1 : slot->ctrl.search_en;
     const int i = (int)bx * kEvalBlock + threadIdx.x;
     const bool valid = i < job.n;
+    // the point's loads go out with the slot's control reads (after the first
+    // evaluation the plane cache too: used unless this evaluation searches)
+    const HsPointIn pin = valid ? hshare_load(job, i, !FIRST) : HsPointIn{};
+    if (slot->ctrl.stop) return;  // block-uniform
+    const int search = FIRST ? 1 : slot->ctrl.search_en;
+    EVAL_MARK(0);
     if (search) {
         LeafQuery q;
         lq_init<!FIRST>(q, P, slot, job, i, valid);
@@ -2132,9 +2212,15 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
         if (valid) grid_cell(P, q, c0, c1, c2, s0, s1, s2);
         unsigned visits = 0, npts = 0;
         const TileView tv = build_tile<kEvalBlock>(U.tile, P, valid, c0, c1, c2, visits, npts);
+        EVAL_MARK(1);
         bool amb = false;
         if (valid) {
-            const bool certified = grid_search(q, P, c0, c1, c2, s0, s1, s2, tv, visits, npts);
+#ifdef LIVO_EVAL_PROF
+            unsigned long long* sp = threadIdx.x == 0 ? g_eval_prof[0] + 5 : nullptr;  // (no-search row: spare slots)
+#else
+            unsigned long long* sp = nullptr;
+#endif
+            const bool certified = grid_search(q, P, c0, c1, c2, s0, s1, s2, tv, visits, npts, sp);
             amb = lq_finish(q, P, job, bjob, i, reinterpret_cast<const float4*>(P.gpts), !certified, false);
         }
         count_visits(P, slot, visits, npts);
@@ -2144,13 +2230,16 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
             else replay_query(P, job, i);
         }
         __syncthreads();  // the tile's LDS is reused by the solve
+        EVAL_MARK(2);
     }
     double acc[kRedUsed];
 #pragma unroll
     for (int j = 0; j < kRedUsed; j++) acc[j] = 0.0;
-    if (valid) hshare_point(E.h, job, slot->state, i, search, acc);
+    if (valid) hshare_point(E.h, job, slot->state, i, search, acc, pin);
+    EVAL_MARK_SYNC(3);
     const int nblk = max(1, (job.n + kEvalBlock - 1) / kEvalBlock);
     hshare_reduce_solve<kEvalBlock>(E.h, job, slot, acc, nblk, bx, R, U.solve);
+    EVAL_MARK(4);
 }
 
 // Per-point persistent selection of the IKFoM h-model: point_selected_surf is a
@@ -2697,6 +2786,18 @@ int launch_knn_grid(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, 
         hipLaunchKernelGGL(k_knn_replay, dim3(kReplayBlocks), dim3(64), replay_lds_bytes(q.depth), (hipStream_t)stream, q);
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
+
+// per-phase profile of k_iekf_eval (LIVO_EVAL_PROF builds only): out[16], reset after reading
+#ifdef LIVO_EVAL_PROF
+// Profiling builds only (not part of livo.h): per-phase block cycles of the
+// fused evaluation since the last call (tools/eval_prof.py).
+extern "C" int livo_debug_eval_prof(unsigned long long* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return LIVO_E_HIP;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_eval_prof), sizeof(g_eval_prof)) != hipSuccess) return LIVO_E_HIP;
+    static const unsigned long long zero[16] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_eval_prof), zero, sizeof(zero)) == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+#endif
 
 int launch_iekf_eval(const KnnParams& kp, const HsParams& hp, int n_jobs, int64_t max_n, bool first, void* stream) {
     if (n_jobs <= 0 || max_n <= 0) return LIVO_OK;

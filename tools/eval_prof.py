@@ -1,0 +1,44 @@
+"""Per-phase block time of the fused evaluation kernel (k_iekf_eval) on the bench's batch.
+
+Build the profiling variant first:  python tools/ab_build.py evprof -DLIVO_EVAL_PROF
+then on the GPU box:  LIVO_LIB=fast-livo-noted_amd/lib/variants/evprof.so python tools/eval_prof.py
+Phases (thread 0 of each block, s_memtime cycles): 1 build_tile, 2 search + tie replay,
+3 plane pass (hshare_point), 4 block reduction + ticket (+ the last block's solve).
+"""
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fast-livo-noted_amd"))
+import livo_amd  # noqa: E402
+from livo_amd import synth  # noqa: E402
+
+
+def main():
+    m = synth.cached_map(1_000_000)
+    with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=4) as ctx:
+        ctx.map_build(m)
+        sids = [ctx.scan_upload(synth.make_scan(100_000, s)[0]) for s in range(8)]
+        st0 = [synth.make_state(s) for s in range(8)]
+        L = ctx._L
+        L.livo_debug_eval_prof.argtypes = [C.c_void_p]
+        buf = (C.c_ulonglong * 16)()
+        ctx.iekf_update_batch(sids, st0)
+        L.livo_debug_eval_prof(buf)  # reset after the warm-up
+        steps = 10
+        for _ in range(steps):
+            ctx.iekf_update_batch(sids, st0)
+        assert L.livo_debug_eval_prof(buf) == 0
+        for s, name in ((1, "search evals"), (0, "no-search evals")):
+            row = buf[8 * s: 8 * s + 8]
+            nb = max(row[0], 1)
+            print(f"{name}: blocks {row[0]}  per block (kcycles): " +
+                  "  ".join(f"ph{k} {row[k] / nb / 1e3:.2f}" for k in range(1, 5)))
+        nb = max(buf[8], 1)
+        print("search stages of thread 0 (kcycles per search block): " +
+              "  ".join(f"{n} {buf[5 + k] / nb / 1e3:.2f}" for k, n in enumerate(("stage0", "stage1", "stage2"))))
+
+
+if __name__ == "__main__":
+    main()
