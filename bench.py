@@ -110,8 +110,12 @@ def launch_ranks(a) -> int:
 
 
 def stream_groups() -> int:
-    """Stream groups of a batched update (livo_capi.cpp default 2, LIVO_STREAM_GROUPS)."""
-    return int(os.environ.get("LIVO_STREAM_GROUPS", "2"))
+    """Stream groups of a batched update (LIVO_STREAM_GROUPS; livo_capi.cpp's default:
+    1 for the fused evaluation, 2 for the unfused kernels)."""
+    if os.environ.get("LIVO_STREAM_GROUPS"):
+        return int(os.environ["LIVO_STREAM_GROUPS"])
+    fused = os.environ.get("LIVO_KNN_KIND", "tile") == "tile" and os.environ.get("LIVO_FUSED", "1") != "0"
+    return 1 if fused else 2
 
 
 def host_threads() -> int:
@@ -311,8 +315,8 @@ def main():
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": round(pmc["hbm_bytes_per_launch"]) if pmc else None,
-                "kernel": (f"first evaluation of the batch: {min(stream_groups(), a.batch)} concurrent {unit_kernel} dispatches (one "
-                           "per stream group: transform + exact 5-NN of every point with in-place tie replay + plane "
+                "kernel": (f"first evaluation of the batch: {min(stream_groups(), a.batch)} {unit_kernel} dispatch(es) (one "
+                           "per stream group, concurrent; every scan of the group: transform + exact 5-NN of every point with in-place tie replay + plane "
                            "fit + Jacobian + HTH reduction + solve)") if fused else
                           (f"first-evaluation k-NN of the batch: {min(stream_groups(), a.batch)} concurrent {unit_kernel} dispatches "
                            "(one per stream group: transform + exact 5-NN of every point) + their tie replays"),

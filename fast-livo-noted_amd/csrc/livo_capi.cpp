@@ -39,6 +39,7 @@ struct ScanBuf {
     double* ikrows = nullptr;   // IKFoM few-point rows (nblk x kIkFewRows x 13)
     uint32_t* ikcnt = nullptr;  // per block
     bool searched = false;      // a search has filled the neighbour cache
+    int64_t cap = 0;            // points the buffers were sized for (>= n; reused after a release)
 };
 
 template <typename T>
@@ -56,6 +57,11 @@ template <typename T>
 static void dev_free(T*& p) {
     if (p) (void)hipFree((void*)p);
     p = nullptr;
+}
+
+static void free_scan_buf(ScanBuf& s) {
+    dev_free(s.pts); dev_free(s.nn); dev_free(s.partial); dev_free(s.d_perm); dev_free(s.d_iperm);
+    dev_free(s.plane); dev_free(s.pstate); dev_free(s.ikrows); dev_free(s.ikcnt);
 }
 
 }  // namespace
@@ -119,7 +125,10 @@ struct livo_ctx {
     // extra streams for the groups of a batch (overlap of latency-bound kernels)
     hipStream_t xstream[kMaxGroups - 1] = {};
     hipEvent_t xjoin[kMaxGroups - 1] = {};
-    int groups = 2;                    // stream groups per batch (LIVO_STREAM_GROUPS; MI355X, 8 x 100k scans: 1 / 2 / 4 groups 8884 / 9503 / 9145 updates/s)
+    // stream groups per batch (LIVO_STREAM_GROUPS; 0: 1 for the fused evaluation,
+    // 2 otherwise).  MI355X, 8 x 100k scans: unfused 1 / 2 / 4 groups 8884 / 9503 /
+    // 9145 updates/s; fused 12020 / 11883 / 11777 (profiles/r02_ab_groups.txt)
+    int groups = 0;
     int leaf_size = kLeafSize;         // leaf-map points per leaf (LIVO_LEAF_SIZE)
     hipEvent_t fork = nullptr;
     livo_params params{};
@@ -155,6 +164,13 @@ struct livo_ctx {
     size_t prim_bytes = 0;
     // scans
     std::vector<ScanBuf> scans;
+    // released scans' device buffers, reused by the next upload of a scan that
+    // fits (a drop-in run uploads and releases one scan per frame: hipMalloc /
+    // hipFree of its buffers cost more than the update itself)
+    std::vector<ScanBuf> spare;
+    // upload scratch: Morton keys, sort buffers, bounds and the packed source points
+    void* up_tmp = nullptr;
+    size_t up_tmp_bytes = 0;
     // batch resources
     int32_t slot_cap = 0;
     IekfSlot* d_slots = nullptr;
@@ -1031,11 +1047,9 @@ int livo_ctx_destroy(livo_ctx* c) {
     if (!c) return LIVO_E_INVALID;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (auto& s : c->scans) {
-        dev_free(s.pts); dev_free(s.nn);
-        dev_free(s.partial);
-        dev_free(s.d_perm); dev_free(s.d_iperm);
-    }
+    for (auto& s : c->scans) free_scan_buf(s);
+    for (auto& s : c->spare) free_scan_buf(s);
+    if (c->up_tmp) (void)hipFree(c->up_tmp);
     ivox_free(c->iv);
     dyn_free(c->dyn);
     if (c->fe_buf) (void)hipFree(c->fe_buf);
@@ -1231,40 +1245,94 @@ static int32_t register_scan(livo_ctx* c, const ScanBuf& s) {
     return id;
 }
 
-static void free_scan_buf(ScanBuf& s) {
-    dev_free(s.pts); dev_free(s.nn); dev_free(s.partial); dev_free(s.d_perm); dev_free(s.d_iperm);
-    dev_free(s.plane); dev_free(s.pstate); dev_free(s.ikrows); dev_free(s.ikcnt);
+// The device buffers of a scan of N points: a released scan's when one fits
+// (capacity N .. 2N + 4096), else fresh allocations sized for N.
+static constexpr size_t kMaxSpareScans = 16;
+static int alloc_scan_buf(livo_ctx* c, ScanBuf& s, int64_t N) {
+    int best = -1;
+    for (size_t k = 0; k < c->spare.size(); k++) {
+        const int64_t cap = c->spare[k].cap;
+        if (cap >= N && cap <= 2 * N + 4096 && (best < 0 || cap < c->spare[best].cap)) best = (int)k;
+    }
+    if (best >= 0) {
+        s = c->spare[best];
+        c->spare.erase(c->spare.begin() + best);
+    } else {
+        const int64_t cap = N;
+        const int32_t cblk = (int32_t)std::max<int64_t>(1, (cap + kBlock * kPtsPerThread - 1) / (kBlock * kPtsPerThread));
+        s = ScanBuf{};
+        int rc = 0;
+        rc |= dev_alloc(&s.pts, (size_t)cap * 4);
+        rc |= dev_alloc(&s.nn, (size_t)cap);
+        rc |= dev_alloc(&s.partial, partial_doubles(cap));
+        rc |= dev_alloc(&s.d_perm, (size_t)cap);
+        rc |= dev_alloc(&s.d_iperm, (size_t)cap);
+        rc |= dev_alloc(&s.plane, (size_t)cap * 4);
+        rc |= dev_alloc(&s.pstate, (size_t)cap);
+        rc |= dev_alloc(&s.ikrows, (size_t)cblk * kIkFewRows * 13);
+        rc |= dev_alloc(&s.ikcnt, (size_t)cblk);
+        if (rc) {
+            free_scan_buf(s);
+            return LIVO_E_OOM;
+        }
+        s.cap = cap;
+    }
+    s.used = true;
+    s.searched = false;
+    s.n = N;
+    s.nblk = (int32_t)std::max<int64_t>(1, (N + kBlock * kPtsPerThread - 1) / (kBlock * kPtsPerThread));
+    s.perm.clear();
+    return LIVO_OK;
+}
+
+// Back to the spare list (the caller has synchronised the context's streams).
+static void release_scan_buf(livo_ctx* c, ScanBuf& s) {
+    if (c->spare.size() >= kMaxSpareScans) {
+        free_scan_buf(c->spare.front());
+        c->spare.erase(c->spare.begin());
+    }
+    ScanBuf r = s;
+    r.used = false;
+    r.perm = std::vector<int32_t>();
+    c->spare.push_back(r);
+    s = ScanBuf{};
+}
+
+// Upload scratch of N points: [keys | sorted keys | iota | perm | bounds], then
+// (livo_scan_upload) the packed source points.
+static size_t up_tmp_bytes(int64_t N) { return (size_t)N * (8 + 8 + 4 + 4) + 256; }
+static int ensure_up_tmp(livo_ctx* c, size_t bytes) {
+    if (bytes <= c->up_tmp_bytes) return LIVO_OK;
+    if (c->up_tmp) (void)hipFree(c->up_tmp);  // (synchronous: no upload is in flight)
+    c->up_tmp = nullptr;
+    c->up_tmp_bytes = 0;
+    if (hipMalloc(&c->up_tmp, bytes) != hipSuccess) return LIVO_E_OOM;
+    c->up_tmp_bytes = bytes;
+    return LIVO_OK;
 }
 
 // A resident scan from N device points (x, y, z at d_src + stride * i floats):
 // the same Morton order as livo_scan_upload's host sort, computed on the device.
 static int scan_create_device(livo_ctx* c, const float* d_src, int stride, int64_t N, int32_t* scan_id) {
     ScanBuf s;
-    s.used = true;
-    s.n = N;
-    s.nblk = (int32_t)std::max<int64_t>(1, (N + kBlock * kPtsPerThread - 1) / (kBlock * kPtsPerThread));
-    int rc = 0;
-    rc |= dev_alloc(&s.pts, (size_t)N * 4);
-    rc |= dev_alloc(&s.nn, (size_t)N);
-    rc |= dev_alloc(&s.partial, partial_doubles(N));
-    rc |= dev_alloc(&s.d_perm, (size_t)N);
-    rc |= dev_alloc(&s.d_iperm, (size_t)N);
-    rc |= dev_alloc(&s.plane, (size_t)N * 4);
-    rc |= dev_alloc(&s.pstate, (size_t)N);
-    rc |= dev_alloc(&s.ikrows, (size_t)std::max(s.nblk, 1) * kIkFewRows * 13);
-    rc |= dev_alloc(&s.ikcnt, (size_t)std::max(s.nblk, 1));
-    if (rc) {
-        free_scan_buf(s);
-        return LIVO_E_OOM;
-    }
+    int rc = alloc_scan_buf(c, s, N);
+    if (rc) return rc;
     if (N > 0) {
-        unsigned long long *codes = nullptr, *scodes = nullptr;
-        uint32_t *iota = nullptr, *perm = nullptr;
-        unsigned* mm = nullptr;
-        rc = dev_alloc(&codes, (size_t)N) | dev_alloc(&scodes, (size_t)N) | dev_alloc(&iota, (size_t)N) |
-             dev_alloc(&perm, (size_t)N) | dev_alloc(&mm, 6);
-        const unsigned init[6] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u};
-        if (!rc && hipMemcpyAsync(mm, init, sizeof(init), hipMemcpyHostToDevice, c->stream) != hipSuccess) rc = LIVO_E_HIP;
+        rc = ensure_up_tmp(c, up_tmp_bytes(N));
+        if (rc) {
+            release_scan_buf(c, s);
+            return rc;
+        }
+        char* base = (char*)c->up_tmp;
+        auto* codes = (unsigned long long*)base;
+        auto* scodes = codes + N;
+        auto* iota = (uint32_t*)(scodes + N);
+        auto* perm = iota + N;
+        auto* mm = (unsigned*)(((uintptr_t)(perm + N) + 15) & ~(uintptr_t)15);
+        // bounds start at (+max, -max) in the order-preserving encoding
+        if (hipMemsetD32Async((hipDeviceptr_t)mm, 0xFFFFFFFFu, 3, c->stream) != hipSuccess ||
+            hipMemsetD32Async((hipDeviceptr_t)(mm + 3), 0u, 3, c->stream) != hipSuccess)
+            rc = LIVO_E_HIP;
         if (!rc) rc = launch_fe_minmax(d_src, N, stride, mm, c->stream);
         if (!rc) rc = launch_fe_morton(d_src, N, stride, mm, morton_scale(), codes, iota, c->stream);
         if (!rc) {
@@ -1279,12 +1347,11 @@ static int scan_create_device(livo_ctx* c, const float* d_src, int stride, int64
         if (!rc && (hipMemcpyAsync(s.d_perm, perm, (size_t)N * 4, hipMemcpyDeviceToDevice, c->stream) != hipSuccess ||
                     hipMemcpyAsync(s.perm.data(), perm, (size_t)N * 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
                     hipMemsetAsync(s.nn, 0, (size_t)N * sizeof(NNRec), c->stream) != hipSuccess ||
-                    hipMemsetAsync(s.pstate, 0, (size_t)N, c->stream) != hipSuccess ||
-                    hipStreamSynchronize(c->stream) != hipSuccess))
+                    hipMemsetAsync(s.pstate, 0, (size_t)N, c->stream) != hipSuccess))
             rc = LIVO_E_HIP;
-        dev_free(codes); dev_free(scodes); dev_free(iota); dev_free(perm); dev_free(mm);
+        if (hipStreamSynchronize(c->stream) != hipSuccess && !rc) rc = LIVO_E_HIP;
         if (rc) {
-            free_scan_buf(s);
+            release_scan_buf(c, s);
             return rc;
         }
     }
@@ -1299,10 +1366,14 @@ int livo_scan_upload(livo_ctx* c, const float* xyz, int64_t N, int64_t stride_by
     if (stride_bytes < (int64_t)(3 * sizeof(float))) return LIVO_E_INVALID;
     if (set_device(c)) return LIVO_E_HIP;
     // the caller's points packed to x, y, z (a strided PointType array is
-    // read once), copied to HBM, then Morton-ordered on the device
-    // (scan_create_device: the same keys and stable order as a host sort)
+    // read once), copied to HBM behind the upload scratch, then Morton-ordered
+    // on the device (scan_create_device: the same keys and stable order as a host sort)
     float* d_src = nullptr;
     if (N > 0) {
+        const size_t off = (up_tmp_bytes(N) + 255) & ~(size_t)255;
+        int rc = ensure_up_tmp(c, off + (size_t)N * 3 * sizeof(float));
+        if (rc) return rc;
+        d_src = (float*)((char*)c->up_tmp + off);
         const char* base = (const char*)xyz;
         float* h = nullptr;
         const bool packed = stride_bytes == (int64_t)(3 * sizeof(float));
@@ -1311,22 +1382,13 @@ int livo_scan_upload(livo_ctx* c, const float* xyz, int64_t N, int64_t stride_by
             if (!h) return LIVO_E_OOM;
             for (int64_t i = 0; i < N; i++) std::memcpy(h + 3 * i, base + i * stride_bytes, 3 * sizeof(float));
         }
-        if (dev_alloc(&d_src, (size_t)N * 3)) {
-            std::free(h);
-            return LIVO_E_OOM;
-        }
         const hipError_t e = hipMemcpyAsync(d_src, packed ? xyz : h, (size_t)N * 3 * sizeof(float),
                                             hipMemcpyHostToDevice, c->stream);
         const hipError_t e2 = hipStreamSynchronize(c->stream);
         std::free(h);
-        if (e != hipSuccess || e2 != hipSuccess) {
-            dev_free(d_src);
-            return LIVO_E_HIP;
-        }
+        if (e != hipSuccess || e2 != hipSuccess) return LIVO_E_HIP;
     }
-    const int rc = scan_create_device(c, d_src, 3, N, scan_id);
-    dev_free(d_src);
-    return rc;
+    return scan_create_device(c, d_src, 3, N, scan_id);
 }
 
 int livo_scan_release(livo_ctx* c, int32_t id) {
@@ -1334,9 +1396,9 @@ int livo_scan_release(livo_ctx* c, int32_t id) {
     if (id < 0 || id >= (int32_t)c->scans.size() || !c->scans[id].used) return LIVO_E_NOSCAN;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    ScanBuf& s = c->scans[id];
-    free_scan_buf(s);
-    s = ScanBuf{};
+    for (int k = 0; k < kMaxGroups - 1; k++)
+        if (c->xstream[k]) (void)hipStreamSynchronize(c->xstream[k]);
+    release_scan_buf(c, c->scans[id]);
     return LIVO_OK;
 }
 
@@ -1546,7 +1608,10 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
         hipStream_t st;
     };
     Group g[kMaxGroups];
-    const int ngroups = std::max(1, std::min<int>(c->groups, n));
+    // the fused evaluation: search + replay + plane pass + solve in one launch
+    const bool fused = c->fused && model == kModelLaserMapping && c->backend == LIVO_BACKEND_IKDTREE &&
+                       c->knn_kind == 2;
+    const int ngroups = std::max(1, std::min<int>(c->groups > 0 ? c->groups : (fused ? 1 : 2), n));
     int64_t off = 0;
     for (int gi = 0; gi < ngroups; gi++) {
         g[gi].first = (int32_t)((int64_t)n * gi / ngroups);
@@ -1562,9 +1627,6 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
             off += s->n;
         }
     }
-    // the fused evaluation: search + replay + plane pass + solve in one launch
-    const bool fused = c->fused && model == kModelLaserMapping && c->backend == LIVO_BACKEND_IKDTREE &&
-                       c->knn_kind == 2;
     if (!fused) HIP_TRY(hipMemsetAsync(c->d_replay_count, 0, sizeof(unsigned) * kMaxGroups, c->stream));
     const bool prof = c->profiling && c->events_ready;  // 1: first-search events only
     const bool full = prof && c->profiling >= 2;         // 2: every evaluation's stages too

@@ -1908,8 +1908,10 @@ __device__ __forceinline__ HsPointIn hshare_load(const HsJob& job, int i, bool c
     in.plane = cached ? reinterpret_cast<const float4*>(job.plane)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
     return in;
 }
+template <int NU>
 __device__ __forceinline__ void hshare_point(const HsParams& P, const HsJob& job, const livo_state& S, int i,
-                                             int search, double (&acc)[kRedUsed], const HsPointIn& in) {
+                                             int search, double (&acc)[NU], const HsPointIn& in) {
+    static_assert(NU >= kRedUsed, "h_share sums");
             const float4 pb = in.pb;
             const double* R = S.rot;
             float wx, wy, wz;
@@ -2013,15 +2015,21 @@ struct HsReduceLds {
     double fin[8 * kRedCols];
     int last;
 };
-template <int NT>
+// NU = kRedUsed + 2 (the fused evaluation): columns 29 / 30 carry the search's
+// hash-slot and map-point counts (integers, exact in double), reduced with the
+// sums instead of per-wave device atomics on two addresses per scan (those
+// serialise across the XCDs); the last block adds them to slot->visits /
+// scanned of this evaluation.
+template <int NT, int NU = kRedUsed>
 __device__ __forceinline__ void hshare_reduce_solve(const HsParams& P, const HsJob& job, IekfSlot* slot,
-                                                    double (&acc)[kRedUsed], int nblk, unsigned blk, HsReduceLds& R,
+                                                    double (&acc)[NU], int nblk, unsigned blk, HsReduceLds& R,
                                                     SolveLds& L) {
+    static_assert(NU == kRedUsed || NU == kRedUsed + 2, "h_share sums (+ search counts)");
     const int tid = threadIdx.x;
     constexpr int NR = NT / 16;  // 16-lane rows of the block
     static_assert(NR <= 16, "HsReduceLds holds 16 row partials");
 #pragma unroll
-    for (int j = 0; j < kRedUsed; j++) {
+    for (int j = 0; j < NU; j++) {
         const double v = row_sum16(acc[j]);
         if ((tid & 15) == 0) R.red[(tid >> 4) * kRedCols + j] = v;
     }
@@ -2033,7 +2041,7 @@ __device__ __forceinline__ void hshare_reduce_solve(const HsParams& P, const HsJ
     // no L2 write-back fence).  One launch less per evaluation than a separate
     // solve kernel.
     if (tid < 64) {
-        if (tid < kRedUsed) {
+        if (tid < NU) {
             double r[16];
 #pragma unroll
             for (int w = 0; w < 16; w++) r[w] = w < NR ? R.red[w * kRedCols + tid] : 0.0;
@@ -2057,7 +2065,7 @@ __device__ __forceinline__ void hshare_reduce_solve(const HsParams& P, const HsJ
         constexpr int G = NT / 32;
         const int c = tid & 31, g = tid >> 5;
         double acc16 = 0.0;
-        if (c < kRedUsed) {
+        if (c < NU) {
             double* src = job.partial + c;
             for (int b0 = g; b0 < nblk; b0 += 16 * G) {
                 double v[16];
@@ -2078,11 +2086,19 @@ __device__ __forceinline__ void hshare_reduce_solve(const HsParams& P, const HsJ
     if (tid >= 64) return;  // the solve is one wave's work
     if (tid < kRedCols) {
         double v = 0.0;
-        if (tid < kRedUsed) {
+        if (tid < NU) {
             double f[8];
 #pragma unroll
             for (int g = 0; g < 8; g++) f[g] = g < NT / 32 ? R.fin[g * kRedCols + tid] : 0.0;
             v = ((f[0] + f[1]) + (f[2] + f[3])) + ((f[4] + f[5]) + (f[6] + f[7]));
+        }
+        if (NU > kRedUsed && tid >= kRedUsed) {
+            if (tid < NU && v > 0.0) {
+                int e = slot->ctrl.n_evals;
+                e = e < LIVO_MAX_EVALS ? e : LIVO_MAX_EVALS - 1;
+                (tid == kRedUsed ? slot->visits : slot->scanned)[e] += (unsigned long long)v;
+            }
+            v = 0.0;
         }
         L.sum[tid] = v;
         slot->red[tid] = v;
@@ -2205,6 +2221,7 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
     if (slot->ctrl.stop) return;  // block-uniform
     const int search = FIRST ? 1 : slot->ctrl.search_en;
     EVAL_MARK(0);
+    unsigned n_slots = 0u, n_pts = 0u;  // hash slots and map points this thread's search read
     if (search) {
         LeafQuery q;
         lq_init<!FIRST>(q, P, slot, job, i, valid);
@@ -2223,7 +2240,8 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
             const bool certified = grid_search(q, P, c0, c1, c2, s0, s1, s2, tv, visits, npts, sp);
             amb = lq_finish(q, P, job, bjob, i, reinterpret_cast<const float4*>(P.gpts), !certified, false);
         }
-        count_visits(P, slot, visits, npts);
+        n_slots = visits;
+        n_pts = npts;
         if (amb) {
             atomicAdd(P.replay_total, 1ull);
             if (P.canon) canon_query(P, job, i);
@@ -2232,13 +2250,15 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
         __syncthreads();  // the tile's LDS is reused by the solve
         EVAL_MARK(2);
     }
-    double acc[kRedUsed];
+    double acc[kRedUsed + 2];
 #pragma unroll
     for (int j = 0; j < kRedUsed; j++) acc[j] = 0.0;
+    acc[kRedUsed] = (double)n_slots;  // the search's counts ride in the block partials
+    acc[kRedUsed + 1] = (double)n_pts;
     if (valid) hshare_point(E.h, job, slot->state, i, search, acc, pin);
     EVAL_MARK_SYNC(3);
     const int nblk = max(1, (job.n + kEvalBlock - 1) / kEvalBlock);
-    hshare_reduce_solve<kEvalBlock>(E.h, job, slot, acc, nblk, bx, R, U.solve);
+    hshare_reduce_solve<kEvalBlock, kRedUsed + 2>(E.h, job, slot, acc, nblk, bx, R, U.solve);
     EVAL_MARK(4);
 }
 
