@@ -2179,13 +2179,13 @@ struct EvalParams {
 
 #ifdef LIVO_EVAL_PROF  // per-phase block time of k_iekf_eval (tools/eval_prof.py; compiled out of the product)
 // [search][phase]: cycles summed over blocks (thread 0's s_memtime deltas) and block counts
-__device__ unsigned long long g_eval_prof[2][8];
+__device__ unsigned long long g_eval_prof[3][8];  // [no search / rematch / first search][phase]
 #define EVAL_MARK(k)                                                                                   \
     do {                                                                                               \
         if (threadIdx.x == 0) {                                                                        \
             const unsigned long long now = __builtin_amdgcn_s_memtime();                              \
-            if ((k) > 0) atomicAdd(&g_eval_prof[search ? 1 : 0][(k)], now - prof_t);                  \
-            else atomicAdd(&g_eval_prof[search ? 1 : 0][0], 1ull);                                     \
+            if ((k) > 0) atomicAdd(&g_eval_prof[FIRST ? 2 : (search ? 1 : 0)][(k)], now - prof_t);     \
+            else atomicAdd(&g_eval_prof[FIRST ? 2 : (search ? 1 : 0)][0], 1ull);       \
             prof_t = now;                                                                              \
         }                                                                                              \
     } while (0)
@@ -2233,7 +2233,7 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
         bool amb = false;
         if (valid) {
 #ifdef LIVO_EVAL_PROF
-            unsigned long long* sp = threadIdx.x == 0 ? g_eval_prof[0] + 5 : nullptr;  // (no-search row: spare slots)
+            unsigned long long* sp = threadIdx.x == 0 ? g_eval_prof[FIRST ? 2 : 1] + 5 : nullptr;  // (stage slots 5-7)
 #else
             unsigned long long* sp = nullptr;
 #endif
@@ -2807,14 +2807,14 @@ int launch_knn_grid(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, 
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 
-// per-phase profile of k_iekf_eval (LIVO_EVAL_PROF builds only): out[16], reset after reading
+// per-phase profile of k_iekf_eval (LIVO_EVAL_PROF builds only): out[24], reset after reading
 #ifdef LIVO_EVAL_PROF
 // Profiling builds only (not part of livo.h): per-phase block cycles of the
 // fused evaluation since the last call (tools/eval_prof.py).
 extern "C" int livo_debug_eval_prof(unsigned long long* out) {
     if (hipDeviceSynchronize() != hipSuccess) return LIVO_E_HIP;
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_eval_prof), sizeof(g_eval_prof)) != hipSuccess) return LIVO_E_HIP;
-    static const unsigned long long zero[16] = {};
+    static const unsigned long long zero[24] = {};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_eval_prof), zero, sizeof(zero)) == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 #endif

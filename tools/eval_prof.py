@@ -23,22 +23,21 @@ def main():
         st0 = [synth.make_state(s) for s in range(8)]
         L = ctx._L
         L.livo_debug_eval_prof.argtypes = [C.c_void_p]
-        buf = (C.c_ulonglong * 16)()
+        buf = (C.c_ulonglong * 24)()
         ctx.iekf_update_batch(sids, st0)
         L.livo_debug_eval_prof(buf)  # reset after the warm-up
         steps = 10
         for _ in range(steps):
             ctx.iekf_update_batch(sids, st0)
         assert L.livo_debug_eval_prof(buf) == 0
-        for s, name in ((1, "search evals"), (0, "no-search evals")):
+        for s, name in ((2, "first-search evals"), (1, "rematch evals"), (0, "no-search evals")):
             row = buf[8 * s: 8 * s + 8]
             nb = max(row[0], 1)
             print(f"{name}: blocks {row[0]}  per block (kcycles): " +
                   "  ".join(f"ph{k} {row[k] / nb / 1e3:.2f}" for k in range(1, 5)))
-        nb = max(buf[8], 1)
-        print("search stages of thread 0 (kcycles per search block): " +
-              "  ".join(f"{n} {buf[5 + k] / nb / 1e3:.2f}" for k, n in enumerate(("stage0", "stage1", "stage2"))))
-
+            if s:
+                print("  search stages of thread 0 (kcycles per block): " +
+                      "  ".join(f"{n} {row[5 + k] / nb / 1e3:.2f}" for k, n in enumerate(("stage0", "stage1", "stage2"))))
 
 if __name__ == "__main__":
     main()

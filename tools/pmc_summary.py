@@ -1,8 +1,8 @@
 """Summarise rocprofv3 --pmc passes (tools/pmc_passes.sh) per kernel -> JSON.
 
-HBM traffic of the bench's roofline unit (the first-evaluation k-NN of one
-batch): the batch runs as `groups` half-batches on two streams, each with one
-k_knn_leaf<false> dispatch, so
+HBM traffic of the bench's roofline unit (the first evaluation of one batch):
+the batch runs as `groups` stream groups, each with one k_iekf_eval<true>
+dispatch (k_knn_grid<false> / k_knn_leaf<false> in the unfused builds), so
 
     traffic = groups * (2 * FETCH_SIZE + WRITE_SIZE) KiB * 1024
 
@@ -11,7 +11,7 @@ wide coalesced streaming read (doubled here); other access widths are
 uncalibrated, so the raw figure is recorded alongside.  Dispatches are grouped
 by (kernel, grid size) and the most frequent grid of each kernel is taken: the
 timed steps' dispatches, not the bench's one-off V_ref passes.
-usage: python tools/pmc_summary.py <pmc_dir> <workload tag> <out.json> [groups=2]
+usage: python tools/pmc_summary.py <pmc_dir> <workload tag> <out.json> [groups=1]
 """
 import collections
 import csv
@@ -20,10 +20,10 @@ import json
 import os
 import sys
 
-UNIT_KERNELS = ("k_knn_leaf<false>", "k_knn_grid<false>")
+UNIT_KERNELS = ("k_iekf_eval<true>", "k_knn_leaf<false>", "k_knn_grid<false>")
 
 
-def main(d, workload, out, groups="2"):
+def main(d, workload, out, groups="1"):
     groups = int(groups)
     per = collections.defaultdict(lambda: collections.defaultdict(list))
     grids = collections.defaultdict(collections.Counter)
