@@ -109,13 +109,13 @@ def launch_ranks(a) -> int:
     return rc
 
 
-def stream_groups() -> int:
+def stream_groups(batch_points: int = 800_000) -> int:
     """Stream groups of a batched update (LIVO_STREAM_GROUPS; livo_capi.cpp's default:
-    1 for the fused evaluation, 2 for the unfused kernels)."""
+    1 for a fused evaluation of <= 1.2M points, else 2)."""
     if os.environ.get("LIVO_STREAM_GROUPS"):
         return int(os.environ["LIVO_STREAM_GROUPS"])
     fused = os.environ.get("LIVO_KNN_KIND", "tile") == "tile" and os.environ.get("LIVO_FUSED", "1") != "0"
-    return 1 if fused else 2
+    return 1 if fused and batch_points <= 1_200_000 else 2
 
 
 def host_threads() -> int:
@@ -172,7 +172,7 @@ def pmc_traffic(a, kernel_key: str):
     if "FETCH_SIZE" not in mean or "WRITE_SIZE" not in mean:
         return None
     disp = len(per["FETCH_SIZE"])
-    groups = min(stream_groups(), a.batch)  # one first-search dispatch per stream group and batch
+    groups = min(stream_groups(a.batch * a.scan_points), a.batch)  # one first-search dispatch per stream group and batch
     res = {"hbm_bytes_per_launch": groups * (2 * mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024,
            "fetch_kib_per_dispatch": round(mean["FETCH_SIZE"], 1), "write_kib_per_dispatch": round(mean["WRITE_SIZE"], 1),
            "dispatches_sampled": disp}
@@ -315,10 +315,10 @@ def main():
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": round(pmc["hbm_bytes_per_launch"]) if pmc else None,
-                "kernel": (f"first evaluation of the batch: {min(stream_groups(), a.batch)} {unit_kernel} dispatch(es) (one "
+                "kernel": (f"first evaluation of the batch: {min(stream_groups(a.batch * a.scan_points), a.batch)} {unit_kernel} dispatch(es) (one "
                            "per stream group, concurrent; every scan of the group: transform + exact 5-NN of every point with in-place tie replay + plane "
                            "fit + Jacobian + HTH reduction + solve)") if fused else
-                          (f"first-evaluation k-NN of the batch: {min(stream_groups(), a.batch)} concurrent {unit_kernel} dispatches "
+                          (f"first-evaluation k-NN of the batch: {min(stream_groups(a.batch * a.scan_points), a.batch)} concurrent {unit_kernel} dispatches "
                            "(one per stream group: transform + exact 5-NN of every point) + their tie replays"),
                 "avg_launch_ms": round(launch_ms, 4),
                 "alg_bytes_per_launch": int(alg_bytes),
@@ -439,7 +439,7 @@ def main():
                                  "knn_achieved_GBps": round(ab / (lm * 1e-3) / 1e9, 1) if lm > 0 else None,
                                  "points_per_query": round(kp / max(kq, 1), 2),
                                  "note": f"10M-pt map, {n5} x 200k-pt scans per step, max_iteration={a.max_iter}; "
-                                         "rocprofv3 capture in profiles/ (r02_config5_*)"}
+                                         "rocprofv3 trace: the second phase of profiles/r02_phases_*.txt"}
         c5.close()
 
     # ---- the IKFoM formulation on the same scans

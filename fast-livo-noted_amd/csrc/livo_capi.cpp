@@ -125,8 +125,8 @@ struct livo_ctx {
     // extra streams for the groups of a batch (overlap of latency-bound kernels)
     hipStream_t xstream[kMaxGroups - 1] = {};
     hipEvent_t xjoin[kMaxGroups - 1] = {};
-    // stream groups per batch (LIVO_STREAM_GROUPS; 0: 1 for the fused evaluation,
-    // 2 otherwise).  MI355X, 8 x 100k scans: unfused 1 / 2 / 4 groups 8884 / 9503 /
+    // stream groups per batch (LIVO_STREAM_GROUPS; 0: 1 for a fused evaluation
+    // of <= 1.2M points, 2 otherwise).  MI355X, 8 x 100k scans: unfused 1 / 2 / 4 groups 8884 / 9503 /
     // 9145 updates/s; fused 12020 / 11883 / 11777 (profiles/r02_ab_groups.txt)
     int groups = 0;
     int leaf_size = kLeafSize;         // leaf-map points per leaf (LIVO_LEAF_SIZE)
@@ -1611,7 +1611,13 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
     // the fused evaluation: search + replay + plane pass + solve in one launch
     const bool fused = c->fused && model == kModelLaserMapping && c->backend == LIVO_BACKEND_IKDTREE &&
                        c->knn_kind == 2;
-    const int ngroups = std::max(1, std::min<int>(c->groups > 0 ? c->groups : (fused ? 1 : 2), n));
+    // default groups: the fused evaluation runs a batch of up to ~1.2M points
+    // in one group (8 x 100k: 1 / 2 groups 12020 / 11883 updates/s), larger
+    // batches in two (8 x 200k on the 10M map: 2132 / 2316, profiles/r02_*)
+    int64_t batch_pts = 0;
+    for (int32_t b = 0; b < n; b++) batch_pts += get_scan(c, ids[b])->n;
+    const int auto_groups = fused && batch_pts <= 1200000 ? 1 : 2;
+    const int ngroups = std::max(1, std::min<int>(c->groups > 0 ? c->groups : auto_groups, n));
     int64_t off = 0;
     for (int gi = 0; gi < ngroups; gi++) {
         g[gi].first = (int32_t)((int64_t)n * gi / ngroups);
