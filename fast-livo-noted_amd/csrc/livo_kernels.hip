@@ -719,9 +719,46 @@ __device__ __forceinline__ float lq_thr(const LeafQuery& q) { return fminf(q.d[k
 #ifndef LIVO_TILE_CHUNK
 #define LIVO_TILE_CHUNK 8  // LDS points read per step of a cell's run
 #endif
-__device__ __forceinline__ void lq_point(LeafQuery& q, const float4 v, uint32_t slot) {
+#ifndef LIVO_LQ_FAST
+#define LIVO_LQ_FAST 0  // 1: e6 update hoisted out of the insertion branch, run guard as +inf distance
+#endif
+#ifndef LIVO_LQ_PK
+#define LIVO_LQ_PK 0  // 1: x and y differences / squares as packed-f32 pairs (same IEEE ops)
+#endif
+typedef float lq_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void lq_point(LeafQuery& q, const float4 v, uint32_t slot, bool ok = true) {
+#if LIVO_LQ_PK
+    const lq_f2 dxy = lq_f2{q.qx, q.qy} - lq_f2{v.x, v.y};
+    const lq_f2 sxy = dxy * dxy;
+    const float dz = q.qz - v.z;
+    float dist = (sxy.x + sxy.y) + dz * dz;  // calc_dist (:1291-1295)
+#else
     const float dx = q.qx - v.x, dy = q.qy - v.y, dz = q.qz - v.z;
-    const float dist = (dx * dx + dy * dy) + dz * dz;  // calc_dist (:1291-1295)
+    float dist = (dx * dx + dy * dy) + dz * dz;  // calc_dist (:1291-1295)
+#endif
+#if LIVO_LQ_FAST
+    // a point past the cell's run (ok false) counts as +inf: never inserted, e6 unchanged.
+    // e6 = min(e6, evicted 5th if inserted, else dist) = min(e6, max(dist, d5))
+    dist = ok ? dist : INFINITY;
+    const bool ins = dist < q.d[kNN - 1];
+    const float m = ins ? q.d[kNN - 1] : dist;
+    q.e6 = m < q.e6 ? m : q.e6;
+    if (ins) {
+        q.d[kNN - 1] = dist;
+        q.nd[kNN - 1] = slot;
+#pragma unroll
+        for (int k = kNN - 1; k > 0; k--) {
+            const bool sw = q.d[k] < q.d[k - 1];
+            const float td = q.d[k];
+            const uint32_t tn = q.nd[k];
+            q.d[k] = sw ? q.d[k - 1] : td;
+            q.nd[k] = sw ? q.nd[k - 1] : tn;
+            q.d[k - 1] = sw ? td : q.d[k - 1];
+            q.nd[k - 1] = sw ? tn : q.nd[k - 1];
+        }
+    }
+    return;
+#endif
     if (dist < q.d[kNN - 1]) {
         q.e6 = fminf(q.e6, q.d[kNN - 1]);  // evicted (+inf while not full)
 #if LIVO_INSERT_POS
@@ -1229,7 +1266,11 @@ __device__ __forceinline__ bool grid_search(LeafQuery& q, const KnnParams& P, in
                 for (int u = 0; u < CH; u++) v[u] = tv.pts[k0 + u];  // padded by CH points
 #pragma unroll
                 for (int u = 0; u < CH; u++)
+#if LIVO_LQ_FAST
+                    lq_point(q, v[u], __float_as_uint(v[u].w), k0 + u < hi);
+#else
                     if (k0 + u < hi) lq_point(q, v[u], __float_as_uint(v[u].w));
+#endif
             }
             return;
         }
@@ -1251,7 +1292,11 @@ __device__ __forceinline__ bool grid_search(LeafQuery& q, const KnnParams& P, in
             for (int u = 0; u < 4; u++) v[u] = gpts[k0 + u];  // padded by 3 points
 #pragma unroll
             for (int u = 0; u < 4; u++)
+#if LIVO_LQ_FAST
+                lq_point(q, v[u], (uint32_t)(k0 + u), k0 + u < hi);
+#else
                 if (k0 + u < hi) lq_point(q, v[u], (uint32_t)(k0 + u));
+#endif
         }
     };
     // Cell boxes are int3 ranges [lo, hi]; a box with lo > hi is empty.
