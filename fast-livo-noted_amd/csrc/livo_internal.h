@@ -317,7 +317,10 @@ int launch_knn_leaf(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, 
 int launch_knn_grid(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, bool tile, void* stream);
 int launch_hshare(const HsParams& p, int n_jobs, int max_nblk, bool first, void* stream);
 // One whole IEKF evaluation (search if due + plane pass + reduction + solve) per launch.
-constexpr int kEvalBlock = 256;  // threads (points) per block of k_iekf_eval
+#ifndef LIVO_EVAL_BLOCK
+#define LIVO_EVAL_BLOCK 256
+#endif
+constexpr int kEvalBlock = LIVO_EVAL_BLOCK;  // threads (points) per block of k_iekf_eval
 int launch_iekf_eval(const KnnParams& kp, const HsParams& hp, int n_jobs, int64_t max_n, bool first, void* stream);
 // IKFoM plane pass (12-wide rows) with the manifold update in each scan's last block.
 int launch_hshare_ik(const HsParams& p, int n_jobs, int max_nblk, bool first, void* stream);

@@ -739,8 +739,12 @@ __device__ __forceinline__ void lq_point(LeafQuery& q, const float4 v, uint32_t 
 #if LIVO_LQ_FAST
     // a point past the cell's run (ok false) counts as +inf: never inserted, e6 unchanged.
     // e6 = min(e6, evicted 5th if inserted, else dist) = min(e6, max(dist, d5))
+    // A seeded search (B = the previous 5 neighbours re-measured) never keeps a
+    // point beyond B: at least 5 points within B are visited, so such a point is
+    // always evicted again (its distance reaches e6 either way) and skipping its
+    // insertion leaves the final list and e6 unchanged.
     dist = ok ? dist : INFINITY;
-    const bool ins = dist < q.d[kNN - 1];
+    const bool ins = dist < q.d[kNN - 1] && dist <= q.B;
     const float m = ins ? q.d[kNN - 1] : dist;
     q.e6 = m < q.e6 ? m : q.e6;
     if (ins) {
@@ -2055,9 +2059,10 @@ __device__ __forceinline__ void hshare_point(const HsParams& P, const HsJob& job
 // Block partials of a scan's h_share sums -> the last block of the scan
 // reduces every partial in a fixed order and (P.solve) its wave 0 runs the
 // scan's solve.  nblk = blocks of the scan in this launch, NT threads.
+constexpr int kRedRows = kEvalBlock > 256 ? kEvalBlock / 16 : 16;  // 16-lane rows of the largest block
 struct HsReduceLds {
-    double red[16 * kRedCols];  // one partial per 16-lane row (NT = 256)
-    double fin[8 * kRedCols];
+    double red[kRedRows * kRedCols];      // one partial per 16-lane row
+    double fin[kRedRows / 2 * kRedCols];  // the last block: one sum per 32-thread group
     int last;
 };
 // NU = kRedUsed + 2 (the fused evaluation): columns 29 / 30 carry the search's
@@ -2072,7 +2077,8 @@ __device__ __forceinline__ void hshare_reduce_solve(const HsParams& P, const HsJ
     static_assert(NU == kRedUsed || NU == kRedUsed + 2, "h_share sums (+ search counts)");
     const int tid = threadIdx.x;
     constexpr int NR = NT / 16;  // 16-lane rows of the block
-    static_assert(NR <= 16, "HsReduceLds holds 16 row partials");
+    static_assert(NR <= kRedRows, "HsReduceLds row partials");
+    constexpr int NRM = NR > 16 ? NR : 16;  // rows of the fixed pairwise tree (16 for NT <= 256)
 #pragma unroll
     for (int j = 0; j < NU; j++) {
         const double v = row_sum16(acc[j]);
@@ -2087,11 +2093,11 @@ __device__ __forceinline__ void hshare_reduce_solve(const HsParams& P, const HsJ
     // solve kernel.
     if (tid < 64) {
         if (tid < NU) {
-            double r[16];
+            double r[NRM];
 #pragma unroll
-            for (int w = 0; w < 16; w++) r[w] = w < NR ? R.red[w * kRedCols + tid] : 0.0;
+            for (int w = 0; w < NRM; w++) r[w] = w < NR ? R.red[w * kRedCols + tid] : 0.0;
 #pragma unroll
-            for (int h = 8; h >= 1; h >>= 1)  // fixed pairwise tree
+            for (int h = NRM / 2; h >= 1; h >>= 1)  // fixed pairwise tree
 #pragma unroll
                 for (int w = 0; w < h; w++) r[w] = r[w] + r[w + h];
             const double v = r[0];
@@ -2132,10 +2138,15 @@ __device__ __forceinline__ void hshare_reduce_solve(const HsParams& P, const HsJ
     if (tid < kRedCols) {
         double v = 0.0;
         if (tid < NU) {
-            double f[8];
+            constexpr int NG = NT / 32 > 8 ? NT / 32 : 8;
+            double f[NG];
 #pragma unroll
-            for (int g = 0; g < 8; g++) f[g] = g < NT / 32 ? R.fin[g * kRedCols + tid] : 0.0;
-            v = ((f[0] + f[1]) + (f[2] + f[3])) + ((f[4] + f[5]) + (f[6] + f[7]));
+            for (int g = 0; g < NG; g++) f[g] = g < NT / 32 ? R.fin[g * kRedCols + tid] : 0.0;
+#pragma unroll
+            for (int h = NG / 2; h >= 1; h >>= 1)  // ((f0 + f1) + (f2 + f3)) + ... for NG = 8
+#pragma unroll
+                for (int g = 0; g < h; g++) f[g] = f[2 * g] + f[2 * g + 1];
+            v = f[0];
         }
         if (NU > kRedUsed && tid >= kRedUsed) {
             if (tid < NU && v > 0.0) {

@@ -1,9 +1,8 @@
 """Build variant libraries for on-GPU A/B runs (LIVO_LIB selects one).
 
 usage: python tools/ab_build.py NAME [-DMACRO=VALUE ...] [ENV=VALUE ...]
-Writes fast-livo-noted_amd/lib/variants/NAME.so: every device source compiled
-with the extra -D flags (the tuning macros of livo_internal.h and the kernel
-files), linked with the host objects of the regular build.  Run A/B on one box, e.g.
+Writes fast-livo-noted_amd/lib/variants/NAME.so: every source compiled with
+the extra -D flags (the tuning macros of livo_internal.h and the kernel files).  Run A/B on one box, e.g.
   LIVO_LIB=fast-livo-noted_amd/lib/variants/NAME.so python bench.py
 """
 import os
@@ -21,10 +20,13 @@ def main(name, *flags):
     os.makedirs(vdir, exist_ok=True)
     objs = []
     for src, dev in B.SOURCES:
-        if not dev:
-            objs.append(os.path.join(B.OBJ_DIR, src + ".o"))
-            continue
         obj = os.path.join(vdir, name + "." + src + ".o")
+        if not dev:
+            # host objects too: some macros (LIVO_EVAL_BLOCK) size host-side buffers
+            B._run([B.HIPCC, "-pthread"] + B.COMMON + ["-D__HIP_PLATFORM_AMD__"] + list(flags) +
+                   ["-c", "-o", obj, os.path.join(B.CSRC, src)])
+            objs.append(obj)
+            continue
         B._run([B.HIPCC] + B.COMMON + B.DEVICE + ["-x", "hip"] + list(flags) + ["-c", "-o", obj, os.path.join(B.CSRC, src)])
         objs.append(obj)
     out = os.path.join(vdir, name + ".so")
