@@ -2252,6 +2252,9 @@ __device__ unsigned long long g_eval_prof[3][8];  // [no search / rematch / firs
 #define EVAL_MARK_SYNC(k) do { } while (0)
 #define EVAL_PROF_DECL do { } while (0)
 #endif
+#ifndef LIVO_EVAL_RR
+#define LIVO_EVAL_RR 0  // 1: evaluations after the first map blocks to XCDs round-robin
+#endif
 #ifndef LIVO_EVAL_WAVES
 #define LIVO_EVAL_WAVES 4  // waves per SIMD the VGPR budget must allow (<= 128 VGPRs)
 #endif
@@ -2265,7 +2268,15 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
     } U;
     __shared__ HsReduceLds R;
     unsigned bjob, bx;
-    xcd_block(P.nb, bjob, bx);
+    if (FIRST || !LIVO_EVAL_RR) {
+        xcd_block(P.nb, bjob, bx);  // every scan searches: scan j's blocks on one XCD (its L2)
+    } else {
+        // later evaluations: only the scans whose solve asked for a rematch
+        // search; blockIdx order spreads each scan over all 8 XCDs, so a
+        // rematch of a few scans does not run on a few XCDs alone
+        bjob = blockIdx.x / (unsigned)P.nb;
+        bx = blockIdx.x % (unsigned)P.nb;
+    }
     const HsJob job = P.jobs[bjob];
     IekfSlot* slot = job.slot;
     if (bx > 0 && (int)bx * kEvalBlock >= job.n) return;  // (an empty scan keeps one block: it solves)
