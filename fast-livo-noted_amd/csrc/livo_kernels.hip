@@ -2252,6 +2252,9 @@ __device__ unsigned long long g_eval_prof[3][8];  // [no search / rematch / firs
 #define EVAL_MARK_SYNC(k) do { } while (0)
 #define EVAL_PROF_DECL do { } while (0)
 #endif
+#ifndef LIVO_NOSEARCH_K
+#define LIVO_NOSEARCH_K 1  // K > 1: an evaluation without a search runs K chunks of 256 points per block
+#endif
 #ifndef LIVO_EVAL_RR
 #define LIVO_EVAL_RR 0  // 1: evaluations after the first map blocks to XCDs round-robin
 #endif
@@ -2322,9 +2325,24 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
     for (int j = 0; j < kRedUsed; j++) acc[j] = 0.0;
     acc[kRedUsed] = (double)n_slots;  // the search's counts ride in the block partials
     acc[kRedUsed + 1] = (double)n_pts;
-    if (valid) hshare_point(E.h, job, slot->state, i, search, acc, pin);
+    int nblk = max(1, (job.n + kEvalBlock - 1) / kEvalBlock);
+    if (!FIRST && LIVO_NOSEARCH_K > 1 && !search) {
+        // an evaluation without a search is a cached-plane pass: block bx takes
+        // chunks bx*K .. bx*K + K - 1 of 256 points, so K times fewer blocks
+        // reduce partials and take tickets; the others leave at once
+        constexpr int K = LIVO_NOSEARCH_K;
+        const int nb_k = (nblk + K - 1) / K;
+        if ((int)bx >= nb_k) return;  // block-uniform
+#pragma unroll 1
+        for (int c = 0; c < K; c++) {
+            const int ic = ((int)bx * K + c) * kEvalBlock + threadIdx.x;
+            if (ic < job.n) hshare_point(E.h, job, slot->state, ic, 0, acc, hshare_load(job, ic, true));
+        }
+        nblk = nb_k;
+    } else if (valid) {
+        hshare_point(E.h, job, slot->state, i, search, acc, pin);
+    }
     EVAL_MARK_SYNC(3);
-    const int nblk = max(1, (job.n + kEvalBlock - 1) / kEvalBlock);
     hshare_reduce_solve<kEvalBlock, kRedUsed + 2>(E.h, job, slot, acc, nblk, bx, R, U.solve);
     EVAL_MARK(4);
 }
