@@ -143,6 +143,9 @@ struct livo_ctx {
     int64_t leaf_bytes = 0;
     int knn_kind = 2;                  // batched search: 0 leaf map, 1 cell grid, 2 cell grid + LDS tiles (LIVO_KNN_KIND)
     bool fused = true;                 // kind 2: one k_iekf_eval launch per evaluation (LIVO_FUSED=0: separate passes)
+    bool zc = false;                   // batch slot / job transfers by k_copy_rows over host-mapped memory (LIVO_ZC)
+    IekfSlot* h_slots_dev = nullptr;   // device addresses of the pinned h_slots / h_jobs
+    HsJob* h_jobs_dev = nullptr;
     float grid_cell = 0.f;             // cell edge (LIVO_GRID_CELL; 0: from the map)
     GridSlot* gslots = nullptr;        // cell grid
     float* gpts = nullptr;
@@ -232,8 +235,18 @@ static int ensure_slots(livo_ctx* c, int32_t n) {
     c->h_jobs = nullptr;
     c->slot_cap = 0;
     if (dev_alloc(&c->d_slots, cap) || dev_alloc(&c->d_jobs, cap)) return LIVO_E_OOM;
-    if (hipHostMalloc((void**)&c->h_slots, sizeof(IekfSlot) * cap, 0) != hipSuccess) return LIVO_E_OOM;
-    if (hipHostMalloc((void**)&c->h_jobs, sizeof(HsJob) * cap, 0) != hipSuccess) return LIVO_E_OOM;
+    // mapped + coherent: k_copy_rows (LIVO_ZC) reads and writes them from the device uncached
+    const unsigned hflags = hipHostMallocMapped | hipHostMallocCoherent;
+    if (hipHostMalloc((void**)&c->h_slots, sizeof(IekfSlot) * cap, hflags) != hipSuccess) return LIVO_E_OOM;
+    if (hipHostMalloc((void**)&c->h_jobs, sizeof(HsJob) * cap, hflags) != hipSuccess) return LIVO_E_OOM;
+    c->h_slots_dev = nullptr;
+    c->h_jobs_dev = nullptr;
+    if (hipHostGetDevicePointer((void**)&c->h_slots_dev, c->h_slots, 0) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&c->h_jobs_dev, c->h_jobs, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        c->h_slots_dev = nullptr;
+        c->h_jobs_dev = nullptr;
+    }
     c->slot_cap = cap;
     return LIVO_OK;
 }
@@ -1028,6 +1041,7 @@ int livo_ctx_create(int device, const livo_params* p, livo_ctx** out) {
         if (v >= 2 && v <= 256) c->leaf_size = v;
     }
     if (const char* env = std::getenv("LIVO_FUSED")) c->fused = std::atoi(env) != 0;
+    if (const char* env = std::getenv("LIVO_ZC")) c->zc = std::atoi(env) != 0;
     if (const char* env = std::getenv("LIVO_KNN_KIND"))
         c->knn_kind = std::strcmp(env, "leaf") == 0 ? 0 : std::strcmp(env, "grid") == 0 ? 1 : 2;
     if (const char* env = std::getenv("LIVO_GRID_CELL")) {
@@ -1593,9 +1607,16 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
         }
     // the LaserMapping model uses only the part of a slot before the IKFoM block
     const size_t slot_w = model == kModelIkfom ? sizeof(IekfSlot) : kSlotLmBytes;
-    HIP_TRY(hipMemcpy2DAsync(c->d_slots, sizeof(IekfSlot), c->h_slots, sizeof(IekfSlot), slot_w, n,
-                             hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->d_jobs, c->h_jobs, sizeof(HsJob) * n, hipMemcpyHostToDevice, c->stream));
+    const bool zc = c->zc && c->h_slots_dev && c->h_jobs_dev;
+    if (zc) {
+        rc = launch_copy_rows(c->h_slots_dev, sizeof(IekfSlot), c->d_slots, sizeof(IekfSlot), slot_w, n, c->stream);
+        if (!rc) rc = launch_copy_rows(c->h_jobs_dev, 0, c->d_jobs, 0, sizeof(HsJob) * n, 1, c->stream);
+        if (rc) return rc;
+    } else {
+        HIP_TRY(hipMemcpy2DAsync(c->d_slots, sizeof(IekfSlot), c->h_slots, sizeof(IekfSlot), slot_w, n,
+                                 hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(c->d_jobs, c->h_jobs, sizeof(HsJob) * n, hipMemcpyHostToDevice, c->stream));
+    }
 
     // The batch in groups on separate streams: the latency-bound kernels of
     // one group (18x18 solve, tie replay, launch gaps) overlap the
@@ -1683,9 +1704,16 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
         if (full) HIP_TRY(hipEventRecord(c->ev[gi][3 * LIVO_MAX_EVALS], g[gi].st));
     // each group copies its own slots back on its own stream (no cross-stream
     // join before the copy); the host then waits for every group's stream
-    for (int gi = 0; gi < ngroups; gi++)
-        HIP_TRY(hipMemcpy2DAsync(c->h_slots + g[gi].first, sizeof(IekfSlot), c->d_slots + g[gi].first,
-                                 sizeof(IekfSlot), slot_w, g[gi].count, hipMemcpyDeviceToHost, g[gi].st));
+    for (int gi = 0; gi < ngroups; gi++) {
+        if (zc) {
+            rc = launch_copy_rows(c->d_slots + g[gi].first, sizeof(IekfSlot), c->h_slots_dev + g[gi].first,
+                                  sizeof(IekfSlot), slot_w, g[gi].count, g[gi].st);
+            if (rc) return rc;
+        } else {
+            HIP_TRY(hipMemcpy2DAsync(c->h_slots + g[gi].first, sizeof(IekfSlot), c->d_slots + g[gi].first,
+                                     sizeof(IekfSlot), slot_w, g[gi].count, hipMemcpyDeviceToHost, g[gi].st));
+        }
+    }
     unsigned long long replays = 0;
     if (full) {
         HIP_TRY(hipMemcpyAsync(&replays, c->d_replay_total, 8, hipMemcpyDeviceToHost, c->stream));

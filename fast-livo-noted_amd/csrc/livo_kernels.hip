@@ -2892,6 +2892,26 @@ int launch_knn_grid(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, 
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 
+// Row copy by a kernel (rows x width bytes, 4-B words, strided), for the
+// small per-batch slot / job transfers between pinned host memory and HBM:
+// the device reads or writes the host-mapped rows directly, one launch instead
+// of a DMA copy and its completion latency.  Block r copies row r.
+__global__ __launch_bounds__(256) void k_copy_rows(const uint32_t* __restrict__ src, size_t src_stride,
+                                                   uint32_t* __restrict__ dst, size_t dst_stride, int words) {
+    const uint32_t* s = src + (size_t)blockIdx.x * (src_stride / 4);
+    uint32_t* d = dst + (size_t)blockIdx.x * (dst_stride / 4);
+    for (int w = threadIdx.x; w < words; w += 256) d[w] = s[w];
+}
+
+int launch_copy_rows(const void* src, size_t src_stride, void* dst, size_t dst_stride, size_t width, int rows,
+                     void* stream) {
+    if (rows <= 0) return LIVO_OK;
+    if (width % 4 || src_stride % 4 || dst_stride % 4) return LIVO_E_INVALID;
+    hipLaunchKernelGGL(k_copy_rows, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream,
+                       (const uint32_t*)src, src_stride, (uint32_t*)dst, dst_stride, (int)(width / 4));
+    return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+
 // per-phase profile of k_iekf_eval (LIVO_EVAL_PROF builds only): out[24], reset after reading
 #ifdef LIVO_EVAL_PROF
 // Profiling builds only (not part of livo.h): per-phase block cycles of the
