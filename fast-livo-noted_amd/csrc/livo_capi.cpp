@@ -365,8 +365,14 @@ static void init_slot_ik(IekfSlot& s, const livo_ikfom_state& st, int max_iter) 
     s.ctrl.max_iter = max_iter;
 }
 
-static void init_slot(IekfSlot& s, const livo_state& st, const livo_state& prior, int max_iter) {
-    std::memset(&s, 0, sizeof(IekfSlot));
+// bytes: how much of the slot to clear; the batched LaserMapping update uploads
+// and reads only its first kSlotLmBytes (8.8 of 20.9 KB), so it clears only those
+#ifndef LIVO_SLOT_CLEAR_FULL
+#define LIVO_SLOT_CLEAR_FULL 0  // 1: the batched update clears whole slots (A/B reference)
+#endif
+static void init_slot(IekfSlot& s, const livo_state& st, const livo_state& prior, int max_iter,
+                      size_t bytes = sizeof(IekfSlot)) {
+    std::memset(&s, 0, bytes);
     s.state = st;
     s.prior = prior;
     s.ctrl.stop = 0;
@@ -1593,7 +1599,8 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
         if (model == kModelIkfom) {
             init_slot_ik(c->h_slots[b], ik_states[b], max_iter);
         } else {
-            init_slot(c->h_slots[b], states[b], priors ? priors[b] : states[b], max_iter);
+            init_slot(c->h_slots[b], states[b], priors ? priors[b] : states[b], max_iter,
+                      LIVO_SLOT_CLEAR_FULL ? sizeof(IekfSlot) : kSlotLmBytes);
         }
         fill_job(c->h_jobs[b], *s, c->d_slots + b);
         total_n += s->n;
