@@ -388,21 +388,29 @@ class Context:
 
     def iekf_update_batch(self, sids, states, priors=None, raw: bool = False):
         n = len(sids)
+        if raw:
+            # hot loop (bench): states / priors are ctypes State arrays; the id
+            # and stats buffers are the context's own, reused while the ids
+            # repeat, and the returned stats stay valid until the next raw call
+            key = tuple(sids)
+            cache = getattr(self, "_raw_batch", None)
+            if cache is None or cache[0] != key:
+                ids = (C.c_int32 * n)(*sids)
+                stats = (IterStats * n)()
+                cache = self._raw_batch = (key, ids, stats, C.addressof(ids), C.addressof(stats))
+            _, ids, stats, p_ids, p_stats = cache
+            _check("livo_iekf_update_batch",
+                   self._L.livo_iekf_update_batch(self.h, n, p_ids, C.addressof(states),
+                                                  C.addressof(priors) if priors is not None else None, p_stats))
+            return states, stats
         ids = (C.c_int32 * n)(*sids)
-        if raw:  # states is already a ctypes State array (bench hot loop)
-            sts = states
-        else:
-            sts = (State * n)(*[state_to_c(s) for s in states])
-        prs = None
-        if priors is not None:
-            prs = priors if raw else (State * n)(*[state_to_c(s) for s in priors])
+        sts = (State * n)(*[state_to_c(s) for s in states])
+        prs = (State * n)(*[state_to_c(s) for s in priors]) if priors is not None else None
         stats = (IterStats * n)()
         _check("livo_iekf_update_batch",
                self._L.livo_iekf_update_batch(self.h, n, C.cast(ids, C.c_void_p), C.cast(sts, C.c_void_p),
                                               C.cast(prs, C.c_void_p) if prs is not None else None,
                                               C.cast(stats, C.c_void_p)))
-        if raw:
-            return sts, stats
         return [state_from_c(s) for s in sts], [stats_from_c(s) for s in stats]
 
     # ------------------------------------------------------------ IKFoM ----
