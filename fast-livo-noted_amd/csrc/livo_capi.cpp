@@ -147,6 +147,12 @@ struct livo_ctx {
     IekfSlot* h_slots_dev = nullptr;   // device addresses of the pinned h_slots / h_jobs
     HsJob* h_jobs_dev = nullptr;
     float grid_cell = 0.f;             // cell edge (LIVO_GRID_CELL; 0: from the map)
+    float grid_ppc = 0.f;              // target points per occupied cell when chosen from the map (LIVO_GRID_PPC)
+    bool vruns = true;                 // vertex runs on a static map (LIVO_VRUNS=0: the cell walk)
+    GridSlot* vslots = nullptr;        // vertex runs (static map only)
+    float* vpts = nullptr;
+    uint32_t* vidx = nullptr;
+    int32_t vlog2 = 0;
     GridSlot* gslots = nullptr;        // cell grid
     float* gpts = nullptr;
     float gorg[3] = {0.f, 0.f, 0.f};
@@ -294,6 +300,12 @@ static KnnParams make_knn_params(livo_ctx* c) {
     kp.gh = c->gh;
     kp.geps = c->geps;
     kp.glog2 = c->glog2;
+    // the incremental map keeps the cell walk (its grid is rebuilt on the device)
+    const bool vr = c->vslots && !c->dyn.active;
+    kp.vslots = vr ? c->vslots : nullptr;
+    kp.vpts = vr ? c->vpts : nullptr;
+    kp.vidx = vr ? c->vidx : nullptr;
+    kp.vlog2 = c->vlog2;
     kp.identity = 0;
     kp.iv = ivox_params(c);
     kp.canon = c->dyn.active ? 1 : 0;
@@ -1050,6 +1062,11 @@ int livo_ctx_create(int device, const livo_params* p, livo_ctx** out) {
     if (const char* env = std::getenv("LIVO_ZC")) c->zc = std::atoi(env) != 0;
     if (const char* env = std::getenv("LIVO_KNN_KIND"))
         c->knn_kind = std::strcmp(env, "leaf") == 0 ? 0 : std::strcmp(env, "grid") == 0 ? 1 : 2;
+    if (const char* env = std::getenv("LIVO_VRUNS")) c->vruns = std::atoi(env) != 0;
+    if (const char* env = std::getenv("LIVO_GRID_PPC")) {  // tuning knob
+        const float v = (float)std::atof(env);
+        if (v > 0.f) c->grid_ppc = v;
+    }
     if (const char* env = std::getenv("LIVO_GRID_CELL")) {
         const float v = (float)std::atof(env);
         if (v > 0.f) c->grid_cell = v;
@@ -1080,6 +1097,9 @@ int livo_ctx_destroy(livo_ctx* c) {
     dev_free(c->lpts);
     dev_free(c->gslots);
     dev_free(c->gpts);
+    dev_free(c->vslots);
+    dev_free(c->vpts);
+    dev_free(c->vidx);
     dev_free(c->d_replay_count);
     dev_free(c->d_replay_total);
     dev_free(c->d_replay_list);
@@ -1134,10 +1154,15 @@ int livo_map_build(livo_ctx* c, const float* xyz, int64_t M, int64_t stride_byte
     if (rc) return rc;
     HostLeafMap lm;
     HostGridMap gm;
-    rc = c->knn_kind >= 1 ? build_grid_map(xyz, M, stride_bytes, c->grid_cell, &gm)
+    const bool vr = c->knn_kind == 2 && c->vruns;
+    rc = c->knn_kind >= 1 ? build_grid_map(xyz, M, stride_bytes, c->grid_cell, &gm, c->grid_ppc > 0.f ? c->grid_ppc
+                                                                                    : (vr ? kVrunPpc : 0.f))
                           : build_leaf_map(xyz, M, stride_bytes, c->leaf_size, &lm);
+    HostVertexRuns vrh;
+    if (!rc && vr) rc = build_vertex_runs(gm, &vrh, 1);
     if (rc) {
         free_host_map(&hm);
+        free_grid_map(&gm);
         return rc;
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1147,6 +1172,9 @@ int livo_map_build(livo_ctx* c, const float* xyz, int64_t M, int64_t stride_byte
     dev_free(c->lpts);
     dev_free(c->gslots);
     dev_free(c->gpts);
+    dev_free(c->vslots);
+    dev_free(c->vpts);
+    dev_free(c->vidx);
     c->nodes = nullptr;
     c->lnodes = nullptr;
     c->lpts = nullptr;
@@ -1173,6 +1201,17 @@ int livo_map_build(livo_ctx* c, const float* xyz, int64_t M, int64_t stride_byte
         // slack for float rounding in the cell assignment (host) and cell bounds (device)
         c->geps = (float)(32.0 * std::ldexp(1.0, -24) * (double)gm.cmax + 1e-7);
         c->gcmax = gm.cmax;
+        if (vr && !oom && e == hipSuccess) {
+            const size_t vsb = ((size_t)1 << vrh.log2_slots) * sizeof(GridSlot);
+            const size_t vpb = (size_t)(vrh.n + 8) * 4 * sizeof(float), vib = (size_t)(vrh.n + 8) * sizeof(uint32_t);
+            oom = hipMalloc((void**)&c->vslots, vsb) != hipSuccess || hipMalloc((void**)&c->vpts, vpb) != hipSuccess ||
+                  hipMalloc((void**)&c->vidx, vib) != hipSuccess;
+            if (!oom) e = hipMemcpy(c->vslots, vrh.slots, vsb, hipMemcpyHostToDevice);
+            if (!oom && e == hipSuccess) e = hipMemcpy(c->vpts, vrh.pts, vpb, hipMemcpyHostToDevice);
+            if (!oom && e == hipSuccess) e = hipMemcpy(c->vidx, vrh.idx, vib, hipMemcpyHostToDevice);
+            c->vlog2 = vrh.log2_slots;
+            c->grid_bytes += (int64_t)(vsb + vpb + vib);
+        }
     } else {
         const size_t lnb = (size_t)std::max<int64_t>(((int64_t)1 << lm.depth) - 1, 1) * sizeof(LeafNode);
         oom = oom || hipMalloc((void**)&c->lnodes, lnb) != hipSuccess || hipMalloc((void**)&c->lpts, ppb) != hipSuccess;
@@ -1185,6 +1224,7 @@ int livo_map_build(livo_ctx* c, const float* xyz, int64_t M, int64_t stride_byte
     free_host_map(&hm);
     free_leaf_map(&lm);
     free_grid_map(&gm);
+    free_vertex_runs(&vrh);
     if (oom) return LIVO_E_OOM;
     if (e != hipSuccess) return LIVO_E_HIP;
     c->map_points = M;
@@ -2053,6 +2093,11 @@ int livo_scan_preprocess(livo_ctx* c, const livo_raw_point* raw, int64_t n, cons
         if (!(poses[k].offset_time >= poses[k - 1].offset_time)) return LIVO_E_INVALID;  // the walk needs sorted segments
     if (n > (int64_t)0x7FFFFFFF - kBlock) return LIVO_E_RANGE;
     if (set_device(c)) return LIVO_E_HIP;
+    // the previous frame's feats_undistort is gone from here on (its buffer may be
+    // freed or overwritten below): livo_frame_to_world(-1) sees no frame until this
+    // one has been processed completely
+    c->fe_raw = nullptr;
+    c->fe_n = 0;
     // scratch: raw 20n, poses, seg 2x4n, keys/iota/skeys/svals 4x4n, flags/vid 2x4n, starts 4(n+1), down 20n
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t nb = (size_t)std::max<int64_t>(n, 1);
@@ -2118,8 +2163,6 @@ int livo_scan_preprocess(livo_ctx* c, const livo_raw_point* raw, int64_t n, cons
         if (!rc) rc = launch_fe_undistort(F, c->stream);
         if (rc) return rc;
     }
-    c->fe_raw = F.raw;  // feats_undistort stays resident until the next frame (livo_frame_to_world)
-    c->fe_n = n;
     if (undistorted && n > 0)
         HIP_TRY(hipMemcpyAsync(undistorted, F.raw, (size_t)n * 20, hipMemcpyDeviceToHost, c->stream));
     // downSizeFilterSurf: PCL VoxelGrid::applyFilter
@@ -2190,6 +2233,8 @@ int livo_scan_preprocess(livo_ctx* c, const livo_raw_point* raw, int64_t n, cons
         if (down_cap < n_kept) return LIVO_E_RANGE;
         if (n_kept > 0) HIP_TRY(hipMemcpyAsync(down, kept, (size_t)n_kept * 20, hipMemcpyDeviceToHost, c->stream));
     }
+    c->fe_raw = F.raw;  // feats_undistort stays resident until the next frame (livo_frame_to_world)
+    c->fe_n = n;
     return scan_create_device(c, kept, 5, n_kept, scan_id);
 }
 

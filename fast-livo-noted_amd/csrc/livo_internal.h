@@ -115,9 +115,28 @@ struct HostGridMap {
     float h = 1.f;
     float cmax = 0.f;           // largest |coordinate| (bounds the float rounding of cell bounds)
 };
-// cell_h <= 0: chosen from the map (about 20 points per occupied cell)
-int build_grid_map(const float* xyz, int64_t M, int64_t stride_bytes, float cell_h, HostGridMap* out);
+// cell_h <= 0: chosen from the map (about ppc_target points per occupied cell, 20 if 0)
+int build_grid_map(const float* xyz, int64_t M, int64_t stride_bytes, float cell_h, HostGridMap* out,
+                   float ppc_target = 0.f);
+constexpr float kVrunPpc = 14.0f;  // cell occupancy the cell runs are sized for (0.3 m cells on the config-2 map)
 void free_grid_map(HostGridMap* m);
+
+// Vertex runs: the search structure of the batched IEKF k-NN.  Vertex v of
+// the cell grid (position org + v h) owns the 2x2x2 cells that share it;
+// every map point is stored in the run of each of the 8 vertices of its cell
+// (8x the points: 128 MB for a 1M map), a run sorted by the distance rho to
+// its vertex.  A query takes the vertex nearest to it: one hash probe, one
+// contiguous run that covers the ball of radius h - |q - v|_inf around it,
+// scanned until rho exceeds |q - v| + the current bound.
+struct HostVertexRuns {
+    GridSlot* slots = nullptr;  // 2^log2_slots: vertex key -> run
+    float* pts = nullptr;       // (n + 8) x 4 floats: x, y, z, rho
+    uint32_t* idx = nullptr;    // n + 8: the point's index in the grid's point array
+    int64_t n = 0;
+    int32_t log2_slots = 0;
+};
+int build_vertex_runs(const HostGridMap& gm, HostVertexRuns* out, int mode = 0);  // mode 1: 27-cell runs
+void free_vertex_runs(HostVertexRuns* v);
 
 // ---------------------------------------------------------------------------
 // iVox map (faster_lio::IVox<3, DEFAULT>, include/ivox3d/ivox3d.h): the
@@ -284,6 +303,10 @@ struct KnnParams {
     float gh;               // cell edge
     float geps;             // cell-bound slack for float rounding of the cell assignment
     int32_t glog2;          // log2 of the hash table size
+    const GridSlot* vslots; // vertex runs (null: the cell walk of grid_search)
+    const float* vpts;      // x, y, z, rho
+    const uint32_t* vidx;   // grid point index of each run entry
+    int32_t vlog2;
     IvoxParams iv;          // iVox backend (LIVO_BACKEND_IVOX)
     int32_t canon;          // incremental map: flagged queries -> k_knn_canon instead of the ikd-Tree replay
 };

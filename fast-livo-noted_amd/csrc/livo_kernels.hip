@@ -713,74 +713,12 @@ __device__ __forceinline__ void lq_init(LeafQuery& q, const KnnParams& P, const 
 
 __device__ __forceinline__ float lq_thr(const LeafQuery& q) { return fminf(q.d[kNN - 1], q.B); }
 
-#ifndef LIVO_INSERT_POS
-#define LIVO_INSERT_POS 0  // 1: position-compare insertion (shorter dependency chain)
-#endif
-#ifndef LIVO_TILE_CHUNK
-#define LIVO_TILE_CHUNK 8  // LDS points read per step of a cell's run
-#endif
-#ifndef LIVO_LQ_FAST
-#define LIVO_LQ_FAST 0  // 1: e6 update hoisted out of the insertion branch, run guard as +inf distance
-#endif
-#ifndef LIVO_LQ_PK
-#define LIVO_LQ_PK 0  // 1: x and y differences / squares as packed-f32 pairs (same IEEE ops)
-#endif
-typedef float lq_f2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void lq_point(LeafQuery& q, const float4 v, uint32_t slot, bool ok = true) {
-#if LIVO_LQ_PK
-    const lq_f2 dxy = lq_f2{q.qx, q.qy} - lq_f2{v.x, v.y};
-    const lq_f2 sxy = dxy * dxy;
-    const float dz = q.qz - v.z;
-    float dist = (sxy.x + sxy.y) + dz * dz;  // calc_dist (:1291-1295)
-#else
-    const float dx = q.qx - v.x, dy = q.qy - v.y, dz = q.qz - v.z;
-    float dist = (dx * dx + dy * dy) + dz * dz;  // calc_dist (:1291-1295)
-#endif
-#if LIVO_LQ_FAST
-    // a point past the cell's run (ok false) counts as +inf: never inserted, e6 unchanged.
-    // e6 = min(e6, evicted 5th if inserted, else dist) = min(e6, max(dist, d5))
-    // A seeded search (B = the previous 5 neighbours re-measured) never keeps a
-    // point beyond B: at least 5 points within B are visited, so such a point is
-    // always evicted again (its distance reaches e6 either way) and skipping its
-    // insertion leaves the final list and e6 unchanged.
-    dist = ok ? dist : INFINITY;
-    const bool ins = dist < q.d[kNN - 1] && dist <= q.B;
-    const float m = ins ? q.d[kNN - 1] : dist;
-    q.e6 = m < q.e6 ? m : q.e6;
-    if (ins) {
-        q.d[kNN - 1] = dist;
-        q.nd[kNN - 1] = slot;
-#pragma unroll
-        for (int k = kNN - 1; k > 0; k--) {
-            const bool sw = q.d[k] < q.d[k - 1];
-            const float td = q.d[k];
-            const uint32_t tn = q.nd[k];
-            q.d[k] = sw ? q.d[k - 1] : td;
-            q.nd[k] = sw ? q.nd[k - 1] : tn;
-            q.d[k - 1] = sw ? td : q.d[k - 1];
-            q.nd[k - 1] = sw ? tn : q.nd[k - 1];
-        }
-    }
-    return;
-#endif
+// One scanned point: inserted into the sorted list if below the 5th (the
+// evicted 5th, +inf while the list is not full, becomes a candidate for e6),
+// else a candidate for e6 itself.
+__device__ __forceinline__ void lq_offer(LeafQuery& q, float dist, uint32_t slot) {
     if (dist < q.d[kNN - 1]) {
-        q.e6 = fminf(q.e6, q.d[kNN - 1]);  // evicted (+inf while not full)
-#if LIVO_INSERT_POS
-        // stable insertion after every entry <= dist, all positions at once:
-        // c[k] = d[k-1] <= dist (monotone in k); entry k shifts down where !c[k]
-        bool c[kNN + 1];
-#pragma unroll
-        for (int k = 1; k < kNN; k++) c[k] = q.d[k - 1] <= dist;
-        c[kNN] = false;
-#pragma unroll
-        for (int k = kNN - 1; k >= 1; k--) {
-            const bool here = c[k] && !c[k + 1];
-            q.d[k] = !c[k] ? q.d[k - 1] : (here ? dist : q.d[k]);
-            q.nd[k] = !c[k] ? q.nd[k - 1] : (here ? slot : q.nd[k]);
-        }
-        q.d[0] = c[1] ? q.d[0] : dist;
-        q.nd[0] = c[1] ? q.nd[0] : slot;
-#else
+        q.e6 = fminf(q.e6, q.d[kNN - 1]);
         q.d[kNN - 1] = dist;
         q.nd[kNN - 1] = slot;
 #pragma unroll
@@ -793,10 +731,13 @@ __device__ __forceinline__ void lq_point(LeafQuery& q, const float4 v, uint32_t 
             q.d[k - 1] = sw ? td : q.d[k - 1];
             q.nd[k - 1] = sw ? tn : q.nd[k - 1];
         }
-#endif
     } else {
         q.e6 = fminf(q.e6, dist);
     }
+}
+__device__ __forceinline__ void lq_point(LeafQuery& q, const float4 v, uint32_t slot) {
+    const float dx = q.qx - v.x, dy = q.qy - v.y, dz = q.qz - v.z;
+    lq_offer(q, (dx * dx + dy * dy) + dz * dz, slot);  // calc_dist (:1291-1295)
 }
 
 // C1/C2 check, neighbour record, replay flag.
@@ -1238,9 +1179,13 @@ __device__ __forceinline__ void grid_cell(const KnnParams& P, const LeafQuery& q
 
 // The exact 5-NN of one query on the cell grid (stages 0-2 above); cells of an
 // active tile come from LDS.  Returns whether the list is certified exact.
+// cube_done: every cell of the 3x3x3 cube was already scanned or pruned (the
+// wave search below), so only the rings and stage 2 outside it remain.
+// stage0_done: the 2x2x2 block was already scanned (vrun_search).
 __device__ __forceinline__ bool grid_search(LeafQuery& q, const KnnParams& P, int c0, int c1, int c2, int s0, int s1,
                                             int s2, const TileView& tv, unsigned& visits, unsigned& npts,
-                                            unsigned long long* prof = nullptr) {
+                                            unsigned long long* prof = nullptr, bool cube_done = false,
+                                            bool stage0_done = false) {
     // (prof: profiling builds, thread 0's stage cycles)
     unsigned long long pt = prof ? __builtin_amdgcn_s_memtime() : 0ull;
     auto mark = [&](int k) {
@@ -1263,18 +1208,14 @@ __device__ __forceinline__ bool grid_search(LeafQuery& q, const KnnParams& P, in
         if (tv.on && cx >= tv.lo0 && cx <= tv.hi0 && cy >= tv.lo1 && cy <= tv.hi1 && cz >= tv.lo2 && cz <= tv.hi2) {
             const int t = ((cz - tv.lo2) * tv.d1 + (cy - tv.lo1)) * tv.d0 + (cx - tv.lo0);
             const int lo = (int)tv.off[t], hi = (int)tv.off[t + 1];
-            constexpr int CH = LIVO_TILE_CHUNK;
+            constexpr int CH = 8;
             for (int k0 = lo; k0 < hi; k0 += CH) {
                 float4 v[CH];
 #pragma unroll
                 for (int u = 0; u < CH; u++) v[u] = tv.pts[k0 + u];  // padded by CH points
 #pragma unroll
                 for (int u = 0; u < CH; u++)
-#if LIVO_LQ_FAST
-                    lq_point(q, v[u], __float_as_uint(v[u].w), k0 + u < hi);
-#else
                     if (k0 + u < hi) lq_point(q, v[u], __float_as_uint(v[u].w));
-#endif
             }
             return;
         }
@@ -1296,11 +1237,7 @@ __device__ __forceinline__ bool grid_search(LeafQuery& q, const KnnParams& P, in
             for (int u = 0; u < 4; u++) v[u] = gpts[k0 + u];  // padded by 3 points
 #pragma unroll
             for (int u = 0; u < 4; u++)
-#if LIVO_LQ_FAST
-                lq_point(q, v[u], (uint32_t)(k0 + u), k0 + u < hi);
-#else
                 if (k0 + u < hi) lq_point(q, v[u], (uint32_t)(k0 + u));
-#endif
         }
     };
     // Cell boxes are int3 ranges [lo, hi]; a box with lo > hi is empty.
@@ -1332,26 +1269,30 @@ __device__ __forceinline__ bool grid_search(LeafQuery& q, const KnnParams& P, in
         return true;
     };
     if (!(P.lM > 0)) return false;
-    // stage 0: the 2x2x2 block, own cell first
-#pragma unroll 1
-    for (int b = 0; b < 8; b++)
-        visit(c0 + ((b & 1) ? s0 : 0), c1 + ((b & 2) ? s1 : 0), c2 + ((b & 4) ? s2 : 0));
-    mark(0);
-    const CBox blk{c0 + min(s0, 0), c0 + max(s0, 0), c1 + min(s1, 0), c1 + max(s1, 0), c2 + min(s2, 0),
-                   c2 + max(s2, 0)};
     const CBox cube{c0 - 1, c0 + 1, c1 - 1, c1 + 1, c2 - 1, c2 + 1};
-    // stage 1: within the 3x3x3 cube, the cells the current bound still
-    // reaches (all of them while fewer than 5 points are known)
-    CBox r1 = cube;
-    if (lq_thr(q) < INFINITY && range_of(lq_thr(q), r1)) {
-        r1.l0 = max(r1.l0, cube.l0); r1.h0 = min(r1.h0, cube.h0);
-        r1.l1 = max(r1.l1, cube.l1); r1.h1 = min(r1.h1, cube.h1);
-        r1.l2 = max(r1.l2, cube.l2); r1.h2 = min(r1.h2, cube.h2);
-    } else {
-        r1 = cube;
+    if (!cube_done) {
+        // stage 0: the 2x2x2 block, own cell first
+        if (!stage0_done) {
+#pragma unroll 1
+            for (int b = 0; b < 8; b++)
+                visit(c0 + ((b & 1) ? s0 : 0), c1 + ((b & 2) ? s1 : 0), c2 + ((b & 4) ? s2 : 0));
+        }
+        mark(0);
+        const CBox blk{c0 + min(s0, 0), c0 + max(s0, 0), c1 + min(s1, 0), c1 + max(s1, 0), c2 + min(s2, 0),
+                       c2 + max(s2, 0)};
+        // stage 1: within the 3x3x3 cube, the cells the current bound still
+        // reaches (all of them while fewer than 5 points are known)
+        CBox r1 = cube;
+        if (lq_thr(q) < INFINITY && range_of(lq_thr(q), r1)) {
+            r1.l0 = max(r1.l0, cube.l0); r1.h0 = min(r1.h0, cube.h0);
+            r1.l1 = max(r1.l1, cube.l1); r1.h1 = min(r1.h1, cube.h1);
+            r1.l2 = max(r1.l2, cube.l2); r1.h2 = min(r1.h2, cube.h2);
+        } else {
+            r1 = cube;
+        }
+        scan_box(r1, blk);
+        mark(1);
     }
-    scan_box(r1, blk);
-    mark(1);
     // still fewer than 5 points (sparse map): cubes of radius 2, 3, ...
     CBox vis = cube;
 #pragma unroll 1
@@ -1375,6 +1316,83 @@ __device__ __forceinline__ bool grid_search(LeafQuery& q, const KnnParams& P, in
     }
     mark(2);
     return false;
+}
+
+// ------------------------------------------------------------ cell-run search ----
+// The batched IEKF search on the cell runs (livo_internal.h): the run of the
+// query's own cell c holds every map point of the 3x3x3 cells around c (the
+// cube grid_search's stages 0-1 walk), sorted by the distance rho to c's
+// centre.  One hash probe, then one contiguous scan.  By the triangle
+// inequality a point with rho > |q - centre| + sqrt(bound) is farther than the
+// bound min(5th candidate, seed bound), so the scan stops at the first such
+// entry (with a 1e-4 m margin over every float rounding involved: a point left
+// out is farther than bound + 1e-10, so it could neither enter the list nor
+// make e6 - d5 <= 1e-10, exactly as a pruned cell of grid_search).  Within a
+// chunk of 8 entries a lane takes the per-point insertion path only when one
+// of them is below its e6.  If the ball of the final bound lies in the cube
+// the list is certified (every point within the bound was scanned); else the
+// lane continues with grid_search's stage 2 outside the cube.
+__device__ __forceinline__ bool vrun_search(LeafQuery& q, const KnnParams& P, bool valid, int c0, int c1, int c2,
+                                            int s0, int s1, int s2, unsigned& visits, unsigned& npts) {
+    if (!valid || !(P.lM > 0)) return false;
+    const unsigned long long key = grid_key_d(c0, c1, c2);
+    const uint64_t mask = (1ull << P.vlog2) - 1ull;
+    uint64_t sl = (uint64_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - P.vlog2));
+    GridSlot g = P.vslots[sl];
+    visits++;
+    while (g.key != key && g.key != kGridEmpty) {  // linear probing (load factor <= 1/4)
+        sl = (sl + 1) & mask;
+        g = P.vslots[sl];
+        visits++;
+    }
+    const uint32_t lo = g.key == key ? g.start : 0u, cnt = g.key == key ? g.count : 0u;
+    const float h = P.gh;
+    const float ex = q.qx - (P.gorg[0] + ((float)c0 + 0.5f) * h), ey = q.qy - (P.gorg[1] + ((float)c1 + 0.5f) * h);
+    const float ez = q.qz - (P.gorg[2] + ((float)c2 + 0.5f) * h);
+    const float dqv = sqrtf((ex * ex + ey * ey) + ez * ez);
+    const float4* __restrict__ run = reinterpret_cast<const float4*>(P.vpts) + lo;
+    const uint32_t* __restrict__ rid = P.vidx + lo;
+    uint32_t k0 = 0;
+#pragma unroll 1
+    for (; k0 < cnt; k0 += 8) {
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = run[k0 + u];  // padded by 8 entries
+        const float thr = lq_thr(q);
+        if (thr < INFINITY && v[0].w > dqv + sqrtf(thr) * (1.0f + 1e-6f) + 1e-4f) break;
+        float dist[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const float dx = q.qx - v[u].x, dy = q.qy - v[u].y, dz = q.qz - v[u].z;
+            const float d = (dx * dx + dy * dy) + dz * dz;  // calc_dist (:1291-1295)
+            dist[u] = k0 + u < cnt ? d : INFINITY;
+        }
+        const float m = fminf(fminf(fminf(dist[0], dist[1]), fminf(dist[2], dist[3])),
+                              fminf(fminf(dist[4], dist[5]), fminf(dist[6], dist[7])));
+        if (m < q.e6) {
+#pragma unroll
+            for (int u = 0; u < 8; u++) lq_offer(q, dist[u], rid[k0 + u]);
+        }
+    }
+    npts += min(k0, cnt);
+    // certified when the ball of the final bound lies in the cube [c - 1, c + 1]
+    const float t = lq_thr(q);
+    if (t < INFINITY) {
+        const double rad = sqrt((double)t + 1e-9) * (1.0 + 1e-5) + (double)P.geps;
+        const double ih = 1.0 / (double)P.gh;
+        const double q3[3] = {(double)q.qx, (double)q.qy, (double)q.qz};
+        const int cc[3] = {c0, c1, c2};
+        bool inside = true;
+#pragma unroll
+        for (int a = 0; a < 3; a++) {
+            const double l = floor((q3[a] - rad - (double)P.gorg[a]) * ih);
+            const double hh = floor((q3[a] + rad - (double)P.gorg[a]) * ih);
+            inside = inside && l >= (double)(cc[a] - 1) && hh <= (double)(cc[a] + 1);
+        }
+        if (inside) return true;
+    }
+    TileView none;
+    return grid_search(q, P, c0, c1, c2, s0, s1, s2, none, visits, npts, nullptr, true);
 }
 
 // 512 points / 128 cells per wave (10.5 KB): 4 waves per SIMD (VGPR-bound);
@@ -2265,11 +2283,14 @@ template <bool FIRST>
 __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalParams E) {
     const KnnParams& P = E.k;
     EVAL_PROF_DECL;
+    // the search's LDS is dead (block barrier) before the reduction and solve use theirs
     __shared__ union {
-        BlockTile tile;
-        SolveLds solve;  // the scan's last block solves after its search is done
+        BlockTile tile;  // the cell walk's block tile (no vertex runs: an incremental map)
+        struct {
+            HsReduceLds R;
+            SolveLds solve;  // the scan's last block solves after its search is done
+        } rs;
     } U;
-    __shared__ HsReduceLds R;
     unsigned bjob, bx;
     if (FIRST || !LIVO_EVAL_RR) {
         xcd_block(P.nb, bjob, bx);  // every scan searches: scan j's blocks on one XCD (its L2)
@@ -2298,17 +2319,33 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
         int c0 = 0, c1 = 0, c2 = 0, s0 = 1, s1 = 1, s2 = 1;
         if (valid) grid_cell(P, q, c0, c1, c2, s0, s1, s2);
         unsigned visits = 0, npts = 0;
-        const TileView tv = build_tile<kEvalBlock>(U.tile, P, valid, c0, c1, c2, visits, npts);
-        EVAL_MARK(1);
         bool amb = false;
-        if (valid) {
+        if (P.vslots) {  // (kernel parameter: uniform)
+            EVAL_MARK(1);
+            const bool certified = vrun_search(q, P, valid, c0, c1, c2, s0, s1, s2, visits, npts);
 #ifdef LIVO_EVAL_PROF
-            unsigned long long* sp = threadIdx.x == 0 ? g_eval_prof[FIRST ? 2 : 1] + 5 : nullptr;  // (stage slots 5-7)
-#else
-            unsigned long long* sp = nullptr;
+            {  // block totals: lanes past the 2x2x2 block, run entries scanned, ambiguous
+                const unsigned long long nf = __ballot(valid && !certified);
+                if ((threadIdx.x & 63) == 0) {
+                    atomicAdd(&g_eval_prof[FIRST ? 2 : 1][7], (unsigned long long)__popcll(nf));
+                }
+            }
+            EVAL_MARK(5);
 #endif
-            const bool certified = grid_search(q, P, c0, c1, c2, s0, s1, s2, tv, visits, npts, sp);
-            amb = lq_finish(q, P, job, bjob, i, reinterpret_cast<const float4*>(P.gpts), !certified, false);
+            if (valid) amb = lq_finish(q, P, job, bjob, i, reinterpret_cast<const float4*>(P.gpts), !certified, false);
+            EVAL_MARK(6);
+        } else {
+            const TileView tv = build_tile<kEvalBlock>(U.tile, P, valid, c0, c1, c2, visits, npts);
+            EVAL_MARK(1);
+            if (valid) {
+#ifdef LIVO_EVAL_PROF
+                unsigned long long* sp = threadIdx.x == 0 ? g_eval_prof[FIRST ? 2 : 1] + 5 : nullptr;  // (stage slots 5-7)
+#else
+                unsigned long long* sp = nullptr;
+#endif
+                const bool certified = grid_search(q, P, c0, c1, c2, s0, s1, s2, tv, visits, npts, sp);
+                amb = lq_finish(q, P, job, bjob, i, reinterpret_cast<const float4*>(P.gpts), !certified, false);
+            }
         }
         n_slots = visits;
         n_pts = npts;
@@ -2343,7 +2380,7 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
         hshare_point(E.h, job, slot->state, i, search, acc, pin);
     }
     EVAL_MARK_SYNC(3);
-    hshare_reduce_solve<kEvalBlock, kRedUsed + 2>(E.h, job, slot, acc, nblk, bx, R, U.solve);
+    hshare_reduce_solve<kEvalBlock, kRedUsed + 2>(E.h, job, slot, acc, nblk, bx, U.rs.R, U.rs.solve);
     EVAL_MARK(4);
 }
 

@@ -389,9 +389,14 @@ class Context:
     def iekf_update_batch(self, sids, states, priors=None, raw: bool = False):
         n = len(sids)
         if raw:
-            # hot loop (bench): states / priors are ctypes State arrays; the id
-            # and stats buffers are the context's own, reused while the ids
-            # repeat, and the returned stats stay valid until the next raw call
+            # hot loop (bench): states / priors are ctypes State arrays (at least
+            # n entries each: the library reads and writes n); the id and stats
+            # buffers are the context's own, reused while the ids repeat, so the
+            # returned stats array is overwritten by the next raw call (copy it
+            # to keep it)
+            nb = n * C.sizeof(State)
+            if C.sizeof(states) < nb or (priors is not None and C.sizeof(priors) < nb):
+                raise ValueError(f"iekf_update_batch(raw): states/priors hold fewer than {n} State entries")
             key = tuple(sids)
             cache = getattr(self, "_raw_batch", None)
             if cache is None or cache[0] != key:

@@ -148,3 +148,28 @@ def test_frame_to_world(fctx, n):
         assert np.array_equal(wd.view(np.uint32), refd.view(np.uint32))
     finally:
         fctx.scan_release(sid)
+
+
+@pytest.mark.gpu
+def test_failed_preprocess_drops_frame(fctx):
+    """A livo_scan_preprocess that fails part-way leaves no frame behind: the
+    previous frame's feats_undistort is not readable through
+    livo_frame_to_world(-1) any more (its buffer may have been reused), and the
+    new one is not published until it has been processed completely."""
+    import ctypes as C
+
+    from livo_amd import _ptr, synth
+    raw, poses, Re, pe = synth.make_raw_scan(4000, 5)
+    sid, _, _ = fctx.scan_preprocess(raw, poses, Re, pe, leaf_size=0.5)
+    fctx.scan_release(sid)
+    st = synth.make_state(5)
+    assert fctx.frame_to_world(st).shape == (4000, 5)
+    raw2 = np.ascontiguousarray(raw[:3000], np.float32)
+    down = np.zeros((1, 5), np.float32)  # too small: LIVO_E_RANGE after the frame was de-skewed
+    nd, sid2 = C.c_int64(), C.c_int32()
+    rc = fctx._L.livo_scan_preprocess(fctx.h, _ptr(raw2), 3000, _ptr(np.ascontiguousarray(poses, np.float64)),
+                                      len(poses), _ptr(np.ascontiguousarray(Re, np.float64).reshape(9)),
+                                      _ptr(np.ascontiguousarray(pe, np.float64).reshape(3)), C.c_float(0.5),
+                                      C.byref(sid2), None, _ptr(down), 1, C.byref(nd))
+    assert rc == -6  # LIVO_E_RANGE
+    assert fctx.frame_to_world(st).shape == (0, 5)
