@@ -582,6 +582,70 @@ __global__ void k_dyn_slots(const unsigned long long* __restrict__ skeys, const 
     slots[sl].count = s1 - s0;
 }
 
+// ---- cell runs (livo_internal.h), built on the device from the cell grid ----
+// Entry e = 27 j + b: grid point j in the run of the b-th cell around its own
+// cell (offset (b % 3, b / 3 % 3, b / 9) - 1).  The run of cell v is sorted by
+// rho, the distance to v's centre, then by e; the same float operations as
+// build_vertex_runs (mode 1), so the same bits.
+struct CrGeo {
+    float org[3];
+    float h, inv;
+};
+__device__ __forceinline__ void cr_entry(const CrGeo& G, const float4 p, uint32_t b, int v[3], float& rho) {
+    const float q[3] = {p.x, p.y, p.z};
+    const int o[3] = {(int)(b % 3u) - 1, (int)((b / 3u) % 3u) - 1, (int)(b / 9u) - 1};
+    float d2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        v[k] = (int)floorf((q[k] - G.org[k]) * G.inv) + o[k];  // as build_grid_map's cell
+        const float t = q[k] - (G.org[k] + ((float)v[k] + 0.5f) * G.h);
+        d2 = d2 + t * t;
+    }
+    rho = sqrtf(d2);
+}
+__device__ __forceinline__ unsigned long long cr_key(const int v[3]) {
+    return (unsigned long long)(v[0] + kGridBias) | ((unsigned long long)(v[1] + kGridBias) << 21) |
+           ((unsigned long long)(v[2] + kGridBias) << 42);
+}
+__global__ void k_cr_rho(const float4* __restrict__ gpts, int64_t n, CrGeo G, uint32_t* rho_bits, uint32_t* iota) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    int v[3];
+    float rho;
+    cr_entry(G, gpts[e / 27], (uint32_t)(e % 27), v, rho);
+    rho_bits[e] = __float_as_uint(rho);  // non-negative: the bits sort as the values
+    iota[e] = (uint32_t)e;
+}
+__global__ void k_cr_key(const float4* __restrict__ gpts, const uint32_t* __restrict__ e1, int64_t n, CrGeo G,
+                         unsigned long long* keys) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t e = e1[i];
+    int v[3];
+    float rho;
+    cr_entry(G, gpts[e / 27u], e % 27u, v, rho);
+    keys[i] = cr_key(v);
+}
+__global__ void k_cr_fill(const float4* __restrict__ gpts, const uint32_t* __restrict__ e2,
+                          const unsigned long long* __restrict__ skeys, int64_t n, CrGeo G, float4* vpts,
+                          uint32_t* vidx, uint32_t* heads) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n + 8) return;
+    if (i >= n) {  // chunk padding of the run scan
+        vpts[i] = make_float4(0.f, 0.f, 0.f, INFINITY);
+        vidx[i] = 0u;
+        return;
+    }
+    const uint32_t e = e2[i], j = e / 27u;
+    const float4 p = gpts[j];
+    int v[3];
+    float rho;
+    cr_entry(G, p, e % 27u, v, rho);
+    vpts[i] = make_float4(p.x, p.y, p.z, rho);
+    vidx[i] = j;
+    heads[i] = (i == 0 || skeys[i] != skeys[i - 1]) ? 1u : 0u;
+}
+
 // Delete_Point_Boxes (:501-521): boxes as BoxPointType {vertex_min[3], vertex_max[3]}, half open.
 __global__ void k_dyn_delete_boxes(const float4* __restrict__ all, uint8_t* alive, int64_t n_ids,
                                    const float* __restrict__ boxes, int64_t nb, unsigned long long* cnt) {
@@ -651,6 +715,22 @@ int launch_dyn_runs(const uint32_t* heads, const uint32_t* runid, int64_t na, ui
 int launch_dyn_slots(const unsigned long long* skeys, const uint32_t* starts, int64_t cells, GridSlot* slots, int log2,
                      void* stream) {
     DYN_LAUNCH(k_dyn_slots, cells, skeys, starts, cells, slots, log2);
+}
+int launch_cr_rho(const float* gpts, int64_t n, const float org[3], float h, uint32_t* rho_bits, uint32_t* iota,
+                  void* stream) {
+    const CrGeo G{{org[0], org[1], org[2]}, h, 1.0f / h};
+    DYN_LAUNCH(k_cr_rho, n, reinterpret_cast<const float4*>(gpts), n, G, rho_bits, iota);
+}
+int launch_cr_key(const float* gpts, const uint32_t* e1, int64_t n, const float org[3], float h,
+                  unsigned long long* keys, void* stream) {
+    const CrGeo G{{org[0], org[1], org[2]}, h, 1.0f / h};
+    DYN_LAUNCH(k_cr_key, n, reinterpret_cast<const float4*>(gpts), e1, n, G, keys);
+}
+int launch_cr_fill(const float* gpts, const uint32_t* e2, const unsigned long long* skeys, int64_t n,
+                   const float org[3], float h, float* vpts, uint32_t* vidx, uint32_t* heads, void* stream) {
+    const CrGeo G{{org[0], org[1], org[2]}, h, 1.0f / h};
+    DYN_LAUNCH(k_cr_fill, n + 8, reinterpret_cast<const float4*>(gpts), e2, skeys, n, G,
+               reinterpret_cast<float4*>(vpts), vidx, heads);
 }
 int launch_dyn_delete_boxes(const float* all, uint8_t* alive, int64_t n_ids, const float* boxes, int64_t nb,
                             unsigned long long* cnt, void* stream) {

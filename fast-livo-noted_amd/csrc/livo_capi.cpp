@@ -197,6 +197,9 @@ struct livo_ctx {
     // profiling
     int profiling = 0;
     hipEvent_t ev[kMaxGroups][3 * LIVO_MAX_EVALS + 2] = {};
+    hipEvent_t b_start = nullptr, b_end[2] = {};  // profiling level 2: batch span and the gap before it
+    int b_par = 0;
+    bool b_prev = false;
     bool events_ready = false;
     livo_timings last{};
 };
@@ -1108,9 +1111,13 @@ int livo_ctx_destroy(livo_ctx* c) {
     if (c->h_slots) (void)hipHostFree(c->h_slots);
     if (c->h_jobs) (void)hipHostFree(c->h_jobs);
     if (c->scratch) (void)hipFree(c->scratch);
-    if (c->events_ready)
+    if (c->events_ready) {
         for (auto& g : c->ev)
             for (auto& e : g) (void)hipEventDestroy(e);
+        (void)hipEventDestroy(c->b_start);
+        (void)hipEventDestroy(c->b_end[0]);
+        (void)hipEventDestroy(c->b_end[1]);
+    }
     for (int k = 0; k < kMaxGroups - 1; k++) {
         if (c->xstream[k]) (void)hipStreamSynchronize(c->xstream[k]);
         if (c->xjoin[k]) (void)hipEventDestroy(c->xjoin[k]);
@@ -1134,15 +1141,82 @@ int livo_ctx_set_profiling(livo_ctx* c, int enable) {
     if (enable && !c->events_ready) {
         for (auto& g : c->ev)
             for (auto& e : g) HIP_TRY(hipEventCreate(&e));
+        HIP_TRY(hipEventCreate(&c->b_start));
+        HIP_TRY(hipEventCreate(&c->b_end[0]));
+        HIP_TRY(hipEventCreate(&c->b_end[1]));
         c->events_ready = true;
     }
     c->profiling = enable < 0 ? 0 : (enable > 2 ? 2 : enable);
+    c->b_prev = false;
     return LIVO_OK;
 }
 
 int livo_last_timings(livo_ctx* c, livo_timings* out) {
     if (!c || !out) return LIVO_E_INVALID;
     *out = c->last;
+    return LIVO_OK;
+}
+
+// The cell runs of the static map's grid (livo_internal.h), built on the
+// device: two stable radix sorts (rho, then the run key) of the 27 M entries,
+// the runs' heads and starts, and their hash table (load factor <= 1/4).
+static int build_cell_runs(livo_ctx* c, int64_t M) {
+    dev_free(c->vslots);
+    dev_free(c->vpts);
+    dev_free(c->vidx);
+    if (M <= 0) return LIVO_OK;
+    const int64_t n = M * 27;
+    if (n >= (int64_t)0xFFFFFFFF) return LIVO_E_RANGE;  // 32-bit entry ids
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t b4 = al((size_t)n * 4), b8 = al((size_t)n * 8);
+    char* scr = nullptr;
+    if (hipMalloc((void**)&scr, 7 * b4 + 2 * b8 + al(((size_t)n + 1) * 4) + 256) != hipSuccess) return LIVO_E_OOM;
+    char* p = scr;
+    uint32_t* rho = (uint32_t*)p; p += b4;
+    uint32_t* iota = (uint32_t*)p; p += b4;
+    uint32_t* srho = (uint32_t*)p; p += b4;
+    uint32_t* e1 = (uint32_t*)p; p += b4;
+    uint32_t* e2 = (uint32_t*)p; p += b4;
+    uint32_t* heads = (uint32_t*)p; p += b4;
+    uint32_t* runid = (uint32_t*)p; p += b4;
+    unsigned long long* keys = (unsigned long long*)p; p += b8;
+    unsigned long long* skeys = (unsigned long long*)p; p += b8;
+    uint32_t* starts = (uint32_t*)p; p += al(((size_t)n + 1) * 4);
+    unsigned long long* nruns = (unsigned long long*)p;
+    int rc = LIVO_OK;
+    if (dev_alloc(&c->vpts, (size_t)(n + 8) * 4) || dev_alloc(&c->vidx, (size_t)(n + 8))) rc = LIVO_E_OOM;
+    if (!rc) rc = launch_cr_rho(c->gpts, n, c->gorg, c->gh, rho, iota, c->stream);
+    if (!rc) {
+        size_t tb = 0;
+        rc = prim_sort_pairs_u32(nullptr, &tb, rho, srho, iota, e1, n, 32, c->stream);
+        if (!rc) rc = ensure_prim(c, tb);
+        tb = c->prim_bytes;
+        if (!rc) rc = prim_sort_pairs_u32(c->prim_tmp, &tb, rho, srho, iota, e1, n, 32, c->stream);
+    }
+    if (!rc) rc = launch_cr_key(c->gpts, e1, n, c->gorg, c->gh, keys, c->stream);
+    if (!rc) rc = sort_u64(c, keys, skeys, e1, e2, n);
+    if (!rc) rc = launch_cr_fill(c->gpts, e2, skeys, n, c->gorg, c->gh, c->vpts, c->vidx, heads, c->stream);
+    if (!rc) rc = ivox_scan(c, heads, runid, n);
+    if (!rc) rc = launch_dyn_runs(heads, runid, n, starts, nruns, c->stream);
+    unsigned long long runs = 0;
+    if (!rc && hipMemcpyAsync(&runs, nruns, 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess) rc = LIVO_E_HIP;
+    if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = LIVO_E_HIP;
+    int log2 = 4;
+    while (((int64_t)1 << log2) < 4 * (int64_t)runs) log2++;
+    const int64_t table = (int64_t)1 << log2;
+    if (!rc && dev_alloc(&c->vslots, (size_t)table)) rc = LIVO_E_OOM;
+    if (!rc) rc = launch_ivox_clear(c->vslots, table, c->stream);
+    if (!rc) rc = launch_dyn_slots(skeys, starts, (int64_t)runs, c->vslots, log2, c->stream);
+    if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = LIVO_E_HIP;
+    (void)hipFree(scr);
+    if (rc) {
+        dev_free(c->vslots);
+        dev_free(c->vpts);
+        dev_free(c->vidx);
+        return rc;
+    }
+    c->vlog2 = log2;
+    c->grid_bytes += (int64_t)(table * sizeof(GridSlot) + (size_t)(n + 8) * 20);
     return LIVO_OK;
 }
 
@@ -1158,8 +1232,6 @@ int livo_map_build(livo_ctx* c, const float* xyz, int64_t M, int64_t stride_byte
     rc = c->knn_kind >= 1 ? build_grid_map(xyz, M, stride_bytes, c->grid_cell, &gm, c->grid_ppc > 0.f ? c->grid_ppc
                                                                                     : (vr ? kVrunPpc : 0.f))
                           : build_leaf_map(xyz, M, stride_bytes, c->leaf_size, &lm);
-    HostVertexRuns vrh;
-    if (!rc && vr) rc = build_vertex_runs(gm, &vrh, 1);
     if (rc) {
         free_host_map(&hm);
         free_grid_map(&gm);
@@ -1201,17 +1273,6 @@ int livo_map_build(livo_ctx* c, const float* xyz, int64_t M, int64_t stride_byte
         // slack for float rounding in the cell assignment (host) and cell bounds (device)
         c->geps = (float)(32.0 * std::ldexp(1.0, -24) * (double)gm.cmax + 1e-7);
         c->gcmax = gm.cmax;
-        if (vr && !oom && e == hipSuccess) {
-            const size_t vsb = ((size_t)1 << vrh.log2_slots) * sizeof(GridSlot);
-            const size_t vpb = (size_t)(vrh.n + 8) * 4 * sizeof(float), vib = (size_t)(vrh.n + 8) * sizeof(uint32_t);
-            oom = hipMalloc((void**)&c->vslots, vsb) != hipSuccess || hipMalloc((void**)&c->vpts, vpb) != hipSuccess ||
-                  hipMalloc((void**)&c->vidx, vib) != hipSuccess;
-            if (!oom) e = hipMemcpy(c->vslots, vrh.slots, vsb, hipMemcpyHostToDevice);
-            if (!oom && e == hipSuccess) e = hipMemcpy(c->vpts, vrh.pts, vpb, hipMemcpyHostToDevice);
-            if (!oom && e == hipSuccess) e = hipMemcpy(c->vidx, vrh.idx, vib, hipMemcpyHostToDevice);
-            c->vlog2 = vrh.log2_slots;
-            c->grid_bytes += (int64_t)(vsb + vpb + vib);
-        }
     } else {
         const size_t lnb = (size_t)std::max<int64_t>(((int64_t)1 << lm.depth) - 1, 1) * sizeof(LeafNode);
         oom = oom || hipMalloc((void**)&c->lnodes, lnb) != hipSuccess || hipMalloc((void**)&c->lpts, ppb) != hipSuccess;
@@ -1224,9 +1285,12 @@ int livo_map_build(livo_ctx* c, const float* xyz, int64_t M, int64_t stride_byte
     free_host_map(&hm);
     free_leaf_map(&lm);
     free_grid_map(&gm);
-    free_vertex_runs(&vrh);
     if (oom) return LIVO_E_OOM;
     if (e != hipSuccess) return LIVO_E_HIP;
+    if (vr) {
+        rc = build_cell_runs(c, M);
+        if (rc) return rc;
+    }
     c->map_points = M;
     c->map_slots = hm.num_slots;
     c->map_depth = hm.depth;
@@ -1652,6 +1716,13 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
             ScanBuf* s = get_scan(c, ids[b]);
             if (s->n > 0) HIP_TRY(hipMemsetAsync(s->pstate, 0, (size_t)s->n, c->stream));
         }
+    const bool prof = c->profiling && c->events_ready;  // 1: first-search events only
+    const bool full = prof && c->profiling >= 2;         // 2: every evaluation, the batch span and the gap
+    if (full) {
+        HIP_TRY(hipEventRecord(c->b_start, c->stream));
+        // the replay count of this batch only (every batch's replays add to it)
+        HIP_TRY(hipMemsetAsync(c->d_replay_total, 0, 8, c->stream));
+    }
     // the LaserMapping model uses only the part of a slot before the IKFoM block
     const size_t slot_w = model == kModelIkfom ? sizeof(IekfSlot) : kSlotLmBytes;
     const bool zc = c->zc && c->h_slots_dev && c->h_jobs_dev;
@@ -1702,8 +1773,6 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
         }
     }
     if (!fused) HIP_TRY(hipMemsetAsync(c->d_replay_count, 0, sizeof(unsigned) * kMaxGroups, c->stream));
-    const bool prof = c->profiling && c->events_ready;  // 1: first-search events only
-    const bool full = prof && c->profiling >= 2;         // 2: every evaluation's stages too
     // profiling: the batch's first search starts at ev[0][0], before the fork
     if (prof) HIP_TRY(hipEventRecord(c->ev[0][0], c->stream));
     if (ngroups > 1) {
@@ -1728,11 +1797,11 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
     for (int e = 0; e < evals; e++) {
         for (int gi = 0; gi < ngroups && fused; gi++) {
             hipStream_t st = g[gi].st;
-            if (full && (e > 0 || gi > 0)) HIP_TRY(hipEventRecord(c->ev[gi][3 * e], st));
-            if (full && e > 0) HIP_TRY(hipEventRecord(c->ev[gi][3 * e + 1], st));
+            // full: ev[gi][e] before evaluation e, ev[gi][evals] after the last
+            if (full && (e > 0 || gi > 0)) HIP_TRY(hipEventRecord(c->ev[gi][e], st));
             rc = launch_iekf_eval(kp[gi], hp[gi], g[gi].count, g[gi].max_n, e == 0, st);
             if (rc) return rc;
-            if (prof && e == 0) HIP_TRY(hipEventRecord(c->ev[gi][1], st));
+            if (prof && !full && e == 0) HIP_TRY(hipEventRecord(c->ev[gi][1], st));
         }
         for (int gi = 0; gi < ngroups && !fused; gi++) {
             hipStream_t st = g[gi].st;
@@ -1748,7 +1817,7 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
         }
     }
     for (int gi = 0; gi < ngroups; gi++)
-        if (full) HIP_TRY(hipEventRecord(c->ev[gi][3 * LIVO_MAX_EVALS], g[gi].st));
+        if (full) HIP_TRY(hipEventRecord(c->ev[gi][fused ? evals : 3 * LIVO_MAX_EVALS], g[gi].st));
     // each group copies its own slots back on its own stream (no cross-stream
     // join before the copy); the host then waits for every group's stream
     for (int gi = 0; gi < ngroups; gi++) {
@@ -1763,8 +1832,14 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
     }
     unsigned long long replays = 0;
     if (full) {
+        // the replay counter: every group's searches have run (joined into the main stream)
+        for (int gi = 1; gi < ngroups; gi++) {
+            HIP_TRY(hipEventRecord(c->xjoin[gi - 1], g[gi].st));
+            HIP_TRY(hipStreamWaitEvent(c->stream, c->xjoin[gi - 1], 0));
+        }
         HIP_TRY(hipMemcpyAsync(&replays, c->d_replay_total, 8, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipMemsetAsync(c->d_replay_total, 0, 8, c->stream));
+        HIP_TRY(hipEventRecord(c->b_end[c->b_par], c->stream));
     }
     // wait by polling: the batch is short, and a blocking wait's wake-up
     // latency was a visible part of the gap between two batches
@@ -1790,7 +1865,38 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
             t.knn_ms = std::max(t.knn_ms, (double)ms);
         }
         t.knn_launches = 1;
-        for (int gi = 0; gi < ngroups && full; gi++)
+        if (full && fused) {
+            // every evaluation launch: max over the concurrent groups
+            t.knn_ms = 0.0;
+            t.n_evals = std::min(evals, LIVO_MAX_EVALS);
+            for (int e = 0; e < t.n_evals; e++) {
+                double m = 0.0;
+                for (int gi = 0; gi < ngroups; gi++) {
+                    float ms = 0.f;
+                    (void)hipEventElapsedTime(&ms, (e == 0 && gi == 0) ? c->ev[0][0] : c->ev[gi][e], c->ev[gi][e + 1]);
+                    m = std::max(m, (double)ms);
+                }
+                t.eval_ms[e] = m;
+                int searched = 0;
+                for (int32_t b = 0; b < n; b++) searched += c->h_slots[b].eval_search[e] != 0;
+                t.eval_searched[e] = searched;
+                if (e == 0) t.knn_ms = m;
+                else if (searched) t.rematch_knn_ms += m;
+                else t.plane_ms += m;
+            }
+        }
+        if (full) {
+            float ms = 0.f;
+            (void)hipEventElapsedTime(&ms, c->b_start, c->b_end[c->b_par]);
+            t.batch_ms = ms;
+            if (c->b_prev) {
+                (void)hipEventElapsedTime(&ms, c->b_end[c->b_par ^ 1], c->b_start);
+                t.gap_ms = ms;
+            }
+            c->b_prev = true;
+            c->b_par ^= 1;
+        }
+        for (int gi = 0; gi < ngroups && full && !fused; gi++)
             for (int e = 0; e < evals; e++) {
                 float ms_k = 0.f, ms_h = 0.f;
                 if (e > 0) (void)hipEventElapsedTime(&ms_k, c->ev[gi][3 * e], c->ev[gi][3 * e + 1]);

@@ -118,7 +118,7 @@ struct HostGridMap {
 // cell_h <= 0: chosen from the map (about ppc_target points per occupied cell, 20 if 0)
 int build_grid_map(const float* xyz, int64_t M, int64_t stride_bytes, float cell_h, HostGridMap* out,
                    float ppc_target = 0.f);
-constexpr float kVrunPpc = 14.0f;  // cell occupancy the cell runs are sized for (0.3 m cells on the config-2 map)
+constexpr float kVrunPpc = 20.0f;  // cell occupancy the cell runs are sized for (0.35 m cells on the config-2 map)
 void free_grid_map(HostGridMap* m);
 
 // Vertex runs: the search structure of the batched IEKF k-NN.  Vertex v of
@@ -566,6 +566,16 @@ int launch_dyn_slots(const unsigned long long* skeys, const uint32_t* starts, in
                      void* stream);
 int launch_dyn_delete_boxes(const float* all, uint8_t* alive, int64_t n_ids, const float* boxes, int64_t nb,
                             unsigned long long* cnt, void* stream);
+
+// Cell runs on the device from the cell grid (gpts: n / 27 points): entry e's
+// rho (bits) and e; the run key of pass-1-sorted entries; the final runs
+// (x, y, z, rho), their grid indices and the run heads.
+int launch_cr_rho(const float* gpts, int64_t n, const float org[3], float h, uint32_t* rho_bits, uint32_t* iota,
+                  void* stream);
+int launch_cr_key(const float* gpts, const uint32_t* e1, int64_t n, const float org[3], float h,
+                  unsigned long long* keys, void* stream);
+int launch_cr_fill(const float* gpts, const uint32_t* e2, const unsigned long long* skeys, int64_t n,
+                   const float org[3], float h, float* vpts, uint32_t* vidx, uint32_t* heads, void* stream);
 
 // Nearest_Points carried over by point index (laser_mapping.cpp:165 resize keeps entries).
 int launch_inherit_nn(NNRec* dst, const int32_t* dst_perm, int64_t n_dst, const NNRec* src,

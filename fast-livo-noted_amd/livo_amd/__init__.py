@@ -75,7 +75,9 @@ class Timings(C.Structure):
     _fields_ = [("knn_ms", C.c_double), ("rematch_knn_ms", C.c_double), ("plane_ms", C.c_double),
                 ("solve_ms", C.c_double),
                 ("knn_launches", C.c_int64), ("knn_visits", C.c_int64), ("knn_queries", C.c_int64),
-                ("effct_points", C.c_int64), ("knn_replays", C.c_int64), ("knn_points", C.c_int64)]
+                ("effct_points", C.c_int64), ("knn_replays", C.c_int64), ("knn_points", C.c_int64),
+                ("eval_ms", C.c_double * 16), ("eval_searched", C.c_int32 * 16), ("n_evals", C.c_int32),
+                ("reserved_", C.c_int32), ("batch_ms", C.c_double), ("gap_ms", C.c_double)]
 
 
 # every entry point of include/livo.h, with its ctypes signature
@@ -588,7 +590,11 @@ class Context:
     def last_timings(self) -> dict:
         t = Timings()
         _check("livo_last_timings", self._L.livo_last_timings(self.h, C.byref(t)))
-        return {f: getattr(t, f) for f, _ in Timings._fields_}
+        out = {}
+        for f, _ in Timings._fields_:
+            v = getattr(t, f)
+            out[f] = list(v)[:t.n_evals] if f in ("eval_ms", "eval_searched") else v
+        return out
 
     def sync(self):
         _check("livo_sync", self._L.livo_sync(self.h))

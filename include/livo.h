@@ -142,6 +142,18 @@ typedef struct livo_timings {
     int64_t effct_points;  /* effective points of the first evaluation                 */
     int64_t knn_replays;   /* queries recomputed by the exact tie-order replay (all passes) */
     int64_t knn_points;    /* map points those launches read (cell grid; 0 for tree passes) */
+    /* level 2, fused evaluation: device time of each evaluation launch (max over
+     * the stream groups) and the scans that searched in it; the batch from its
+     * first copy to its last, and the device idle time since the previous
+     * batch ended (host time between calls; 0 for the first profiled batch).
+     * Then knn_ms = eval_ms[0], rematch_knn_ms = the evaluations after the
+     * first that searched, plane_ms = those that did not. */
+    double eval_ms[LIVO_MAX_EVALS];
+    int32_t eval_searched[LIVO_MAX_EVALS];
+    int32_t n_evals;
+    int32_t reserved_;
+    double batch_ms;
+    double gap_ms;
 } livo_timings;
 
 int livo_abi_version(void);

@@ -16,15 +16,17 @@ def main(d="gpurun_out"):
             continue
         j = json.loads(lines[-1])
         dm = j.get("device_ms_per_step", {})
-        res.setdefault(name, []).append((j["value"], dm.get("knn_first", 0), dm.get("knn_rematch", 0),
-                                         dm.get("plane_H_solve", 0), j.get("knn_replays_per_step", 0)))
-    print(f"{'variant':12s} {'n':>2s} {'value mean':>10s} {'min':>8s} {'max':>8s} {'knn1':>6s} {'rematch':>7s} "
-          f"{'plane':>6s} {'replays':>7s}")
+        res.setdefault(name, []).append((j["value"], dm.get("eval_first", dm.get("knn_first", 0)),
+                                         dm.get("eval_rematch", dm.get("knn_rematch", 0)),
+                                         dm.get("eval_nosearch", dm.get("plane_H_solve", 0)),
+                                         dm.get("host_gap", 0), j.get("knn_replays_per_step", 0)))
+    print(f"{'variant':12s} {'n':>2s} {'value mean':>10s} {'min':>8s} {'max':>8s} {'first':>6s} {'rematch':>7s} "
+          f"{'nosrch':>6s} {'gap':>6s} {'replays':>7s}")
     for k, v in res.items():
         n = len(v)
-        m = [sum(x[i] for x in v) / n for i in range(5)]
+        m = [sum(x[i] for x in v) / n for i in range(6)]
         print(f"{k:12s} {n:2d} {m[0]:10.1f} {min(x[0] for x in v):8.1f} {max(x[0] for x in v):8.1f} "
-              f"{m[1]:6.3f} {m[2]:7.3f} {m[3]:6.3f} {m[4]:7.1f}")
+              f"{m[1]:6.3f} {m[2]:7.3f} {m[3]:6.3f} {m[4]:6.3f} {m[5]:7.1f}")
 
 
 if __name__ == "__main__":
