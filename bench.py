@@ -194,6 +194,8 @@ def main():
         sys.stderr.write(f"note: --gpus {a.gpus} but WORLD_SIZE {world}; {world} ranks run\n")
     legs = set(a.legs.split(",")) if a.legs != "all" else {"headline", "latency", "config5", "ikfom", "ivox", "ikd",
                                                            "vio"}
+    if rank > 0:
+        legs = {"headline"}  # the side legs are rank 0's report: other ranks only run the headline
     import livo_amd
     from livo_amd import farm, synth
 
@@ -482,15 +484,15 @@ def main():
         for _ in range(ik_steps):
             ik_evals += sum(s.iterations for s in ik_step())
         sync()
-        ik_elapsed = farm.allreduce_max(time.perf_counter() - t, coll_dev)
-        ik_total = farm.allreduce_counters(farm.Counters(scans=ik_steps * a.batch, evals=ik_evals), coll_dev)
+        ik_elapsed = time.perf_counter() - t  # (rank 0 only: no collective)
+        ik_total = farm.Counters(scans=ik_steps * a.batch, evals=ik_evals)
         ik_first = livo_amd.ikfom_stats_from_c(ik_step()[0])
         if rank == 0:
             result["ikfom"] = {"updates_per_s": round(ik_total.scans / ik_elapsed, 3),
                                "ms_per_step": round(ik_elapsed / ik_steps * 1e3, 4),
                                "evals_per_scan": round(ik_total.evals / max(ik_total.scans, 1), 3),
                                "note": "livo_ikfom_update_batch (state_ikfom, esekfom.hpp:1619-1928) on the same "
-                                       f"{a.batch} scans per GPU, {ik_steps} steps after the headline run"}
+                                       f"{a.batch} scans (rank 0 only), {ik_steps} steps after the headline run"}
 
     # ---- the iVox backend (the reference's default build)
     if "ivox" in legs:
@@ -518,8 +520,8 @@ def main():
         for _ in range(iv_steps):
             iv_evals += sum(s.iterations for s in iv_step())
         sync()
-        iv_elapsed = farm.allreduce_max(time.perf_counter() - t, coll_dev)
-        iv_total = farm.allreduce_counters(farm.Counters(scans=iv_steps * a.batch, evals=iv_evals), coll_dev)
+        iv_elapsed = time.perf_counter() - t
+        iv_total = farm.Counters(scans=iv_steps * a.batch, evals=iv_evals)
         # odometry: one scan after the other, each updated then merged into the map
         odo_sids = [ctx.scan_upload(sc) for sc in scans]
         sync()
@@ -589,7 +591,7 @@ def main():
                                      "(de-skew + VoxelGrid 0.5 m) -> livo_iekf_update (iVox) -> livo_map_incremental, "
                                      "host-timed per call (includes the host<->device copies of the raw frame)"},
                 "note": "LIVO_BACKEND_IVOX: IVox GetClosestPoint (NEARBY18, 0.2 m grids, 5 m range) on the same "
-                        f"{a.batch} scans per GPU, {iv_steps} steps; not part of `value`"}
+                        f"{a.batch} scans (rank 0 only), {iv_steps} steps; not part of `value`"}
 
     # ---- the ikd-Tree incremental map (the USE_ikdtree
     # branch of map_incremental): sequential odometry on a second context

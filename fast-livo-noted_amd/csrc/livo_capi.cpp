@@ -143,9 +143,6 @@ struct livo_ctx {
     int64_t leaf_bytes = 0;
     int knn_kind = 2;                  // batched search: 0 leaf map, 1 cell grid, 2 cell grid + LDS tiles (LIVO_KNN_KIND)
     bool fused = true;                 // kind 2: one k_iekf_eval launch per evaluation (LIVO_FUSED=0: separate passes)
-    bool zc = false;                   // batch slot / job transfers by k_copy_rows over host-mapped memory (LIVO_ZC)
-    IekfSlot* h_slots_dev = nullptr;   // device addresses of the pinned h_slots / h_jobs
-    HsJob* h_jobs_dev = nullptr;
     float grid_cell = 0.f;             // cell edge (LIVO_GRID_CELL; 0: from the map)
     float grid_ppc = 0.f;              // target points per occupied cell when chosen from the map (LIVO_GRID_PPC)
     bool vruns = true;                 // vertex runs on a static map (LIVO_VRUNS=0: the cell walk)
@@ -244,18 +241,8 @@ static int ensure_slots(livo_ctx* c, int32_t n) {
     c->h_jobs = nullptr;
     c->slot_cap = 0;
     if (dev_alloc(&c->d_slots, cap) || dev_alloc(&c->d_jobs, cap)) return LIVO_E_OOM;
-    // mapped + coherent: k_copy_rows (LIVO_ZC) reads and writes them from the device uncached
-    const unsigned hflags = hipHostMallocMapped | hipHostMallocCoherent;
-    if (hipHostMalloc((void**)&c->h_slots, sizeof(IekfSlot) * cap, hflags) != hipSuccess) return LIVO_E_OOM;
-    if (hipHostMalloc((void**)&c->h_jobs, sizeof(HsJob) * cap, hflags) != hipSuccess) return LIVO_E_OOM;
-    c->h_slots_dev = nullptr;
-    c->h_jobs_dev = nullptr;
-    if (hipHostGetDevicePointer((void**)&c->h_slots_dev, c->h_slots, 0) != hipSuccess ||
-        hipHostGetDevicePointer((void**)&c->h_jobs_dev, c->h_jobs, 0) != hipSuccess) {
-        (void)hipGetLastError();
-        c->h_slots_dev = nullptr;
-        c->h_jobs_dev = nullptr;
-    }
+    if (hipHostMalloc((void**)&c->h_slots, sizeof(IekfSlot) * cap, hipHostMallocDefault) != hipSuccess) return LIVO_E_OOM;
+    if (hipHostMalloc((void**)&c->h_jobs, sizeof(HsJob) * cap, hipHostMallocDefault) != hipSuccess) return LIVO_E_OOM;
     c->slot_cap = cap;
     return LIVO_OK;
 }
@@ -382,9 +369,6 @@ static void init_slot_ik(IekfSlot& s, const livo_ikfom_state& st, int max_iter) 
 
 // bytes: how much of the slot to clear; the batched LaserMapping update uploads
 // and reads only its first kSlotLmBytes (8.8 of 20.9 KB), so it clears only those
-#ifndef LIVO_SLOT_CLEAR_FULL
-#define LIVO_SLOT_CLEAR_FULL 0  // 1: the batched update clears whole slots (A/B reference)
-#endif
 static void init_slot(IekfSlot& s, const livo_state& st, const livo_state& prior, int max_iter,
                       size_t bytes = sizeof(IekfSlot)) {
     std::memset(&s, 0, bytes);
@@ -1062,7 +1046,6 @@ int livo_ctx_create(int device, const livo_params* p, livo_ctx** out) {
         if (v >= 2 && v <= 256) c->leaf_size = v;
     }
     if (const char* env = std::getenv("LIVO_FUSED")) c->fused = std::atoi(env) != 0;
-    if (const char* env = std::getenv("LIVO_ZC")) c->zc = std::atoi(env) != 0;
     if (const char* env = std::getenv("LIVO_KNN_KIND"))
         c->knn_kind = std::strcmp(env, "leaf") == 0 ? 0 : std::strcmp(env, "grid") == 0 ? 1 : 2;
     if (const char* env = std::getenv("LIVO_VRUNS")) c->vruns = std::atoi(env) != 0;
@@ -1704,7 +1687,7 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
             init_slot_ik(c->h_slots[b], ik_states[b], max_iter);
         } else {
             init_slot(c->h_slots[b], states[b], priors ? priors[b] : states[b], max_iter,
-                      LIVO_SLOT_CLEAR_FULL ? sizeof(IekfSlot) : kSlotLmBytes);
+                      kSlotLmBytes);
         }
         fill_job(c->h_jobs[b], *s, c->d_slots + b);
         total_n += s->n;
@@ -1725,16 +1708,9 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
     }
     // the LaserMapping model uses only the part of a slot before the IKFoM block
     const size_t slot_w = model == kModelIkfom ? sizeof(IekfSlot) : kSlotLmBytes;
-    const bool zc = c->zc && c->h_slots_dev && c->h_jobs_dev;
-    if (zc) {
-        rc = launch_copy_rows(c->h_slots_dev, sizeof(IekfSlot), c->d_slots, sizeof(IekfSlot), slot_w, n, c->stream);
-        if (!rc) rc = launch_copy_rows(c->h_jobs_dev, 0, c->d_jobs, 0, sizeof(HsJob) * n, 1, c->stream);
-        if (rc) return rc;
-    } else {
-        HIP_TRY(hipMemcpy2DAsync(c->d_slots, sizeof(IekfSlot), c->h_slots, sizeof(IekfSlot), slot_w, n,
-                                 hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(hipMemcpyAsync(c->d_jobs, c->h_jobs, sizeof(HsJob) * n, hipMemcpyHostToDevice, c->stream));
-    }
+    HIP_TRY(hipMemcpy2DAsync(c->d_slots, sizeof(IekfSlot), c->h_slots, sizeof(IekfSlot), slot_w, n,
+                             hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->d_jobs, c->h_jobs, sizeof(HsJob) * n, hipMemcpyHostToDevice, c->stream));
 
     // The batch in groups on separate streams: the latency-bound kernels of
     // one group (18x18 solve, tie replay, launch gaps) overlap the
@@ -1820,16 +1796,9 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
         if (full) HIP_TRY(hipEventRecord(c->ev[gi][fused ? evals : 3 * LIVO_MAX_EVALS], g[gi].st));
     // each group copies its own slots back on its own stream (no cross-stream
     // join before the copy); the host then waits for every group's stream
-    for (int gi = 0; gi < ngroups; gi++) {
-        if (zc) {
-            rc = launch_copy_rows(c->d_slots + g[gi].first, sizeof(IekfSlot), c->h_slots_dev + g[gi].first,
-                                  sizeof(IekfSlot), slot_w, g[gi].count, g[gi].st);
-            if (rc) return rc;
-        } else {
-            HIP_TRY(hipMemcpy2DAsync(c->h_slots + g[gi].first, sizeof(IekfSlot), c->d_slots + g[gi].first,
-                                     sizeof(IekfSlot), slot_w, g[gi].count, hipMemcpyDeviceToHost, g[gi].st));
-        }
-    }
+    for (int gi = 0; gi < ngroups; gi++)
+        HIP_TRY(hipMemcpy2DAsync(c->h_slots + g[gi].first, sizeof(IekfSlot), c->d_slots + g[gi].first,
+                                 sizeof(IekfSlot), slot_w, g[gi].count, hipMemcpyDeviceToHost, g[gi].st));
     unsigned long long replays = 0;
     if (full) {
         // the replay counter: every group's searches have run (joined into the main stream)

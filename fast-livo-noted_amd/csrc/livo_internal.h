@@ -345,9 +345,6 @@ int launch_hshare(const HsParams& p, int n_jobs, int max_nblk, bool first, void*
 #endif
 constexpr int kEvalBlock = LIVO_EVAL_BLOCK;  // threads (points) per block of k_iekf_eval
 int launch_iekf_eval(const KnnParams& kp, const HsParams& hp, int n_jobs, int64_t max_n, bool first, void* stream);
-// rows x width bytes between strided buffers by a kernel (either side may be host-mapped pinned memory)
-int launch_copy_rows(const void* src, size_t src_stride, void* dst, size_t dst_stride, size_t width, int rows,
-                     void* stream);
 // IKFoM plane pass (12-wide rows) with the manifold update in each scan's last block.
 int launch_hshare_ik(const HsParams& p, int n_jobs, int max_nblk, bool first, void* stream);
 int launch_solve(const SolveParams& p, int n_jobs, void* stream);

@@ -954,7 +954,8 @@ __device__ __forceinline__ unsigned long long grid_key_d(int cx, int cy, int cz)
 // global path.
 template <int CELLS, int PTS>
 struct TileLds {
-    float4 pts[PTS + 8];      // the box's points (x, y, z, gpts index bits); +8: chunked reads
+    static constexpr int kChunk = 8;  // points per chunked read of a cell (grid_search)
+    float4 pts[PTS + kChunk];  // the box's points (x, y, z, gpts index bits); padded for the chunked reads
     uint32_t off[CELLS + 1];  // LDS start of each cell's run
     uint32_t start[CELLS];    // its start in gpts
     uint32_t wred[16];        // per-wave partials of the block scans
@@ -1208,7 +1209,7 @@ __device__ __forceinline__ bool grid_search(LeafQuery& q, const KnnParams& P, in
         if (tv.on && cx >= tv.lo0 && cx <= tv.hi0 && cy >= tv.lo1 && cy <= tv.hi1 && cz >= tv.lo2 && cz <= tv.hi2) {
             const int t = ((cz - tv.lo2) * tv.d1 + (cy - tv.lo1)) * tv.d0 + (cx - tv.lo0);
             const int lo = (int)tv.off[t], hi = (int)tv.off[t + 1];
-            constexpr int CH = 8;
+            constexpr int CH = TileLds<8, 8>::kChunk;  // every tile is padded by CH points
             for (int k0 = lo; k0 < hi; k0 += CH) {
                 float4 v[CH];
 #pragma unroll
@@ -2270,12 +2271,6 @@ __device__ unsigned long long g_eval_prof[3][8];  // [no search / rematch / firs
 #define EVAL_MARK_SYNC(k) do { } while (0)
 #define EVAL_PROF_DECL do { } while (0)
 #endif
-#ifndef LIVO_NOSEARCH_K
-#define LIVO_NOSEARCH_K 1  // K > 1: an evaluation without a search runs K chunks of 256 points per block
-#endif
-#ifndef LIVO_EVAL_RR
-#define LIVO_EVAL_RR 0  // 1: evaluations after the first map blocks to XCDs round-robin
-#endif
 #ifndef LIVO_EVAL_WAVES
 #define LIVO_EVAL_WAVES 4  // waves per SIMD the VGPR budget must allow (<= 128 VGPRs)
 #endif
@@ -2292,15 +2287,9 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
         } rs;
     } U;
     unsigned bjob, bx;
-    if (FIRST || !LIVO_EVAL_RR) {
-        xcd_block(P.nb, bjob, bx);  // every scan searches: scan j's blocks on one XCD (its L2)
-    } else {
-        // later evaluations: only the scans whose solve asked for a rematch
-        // search; blockIdx order spreads each scan over all 8 XCDs, so a
-        // rematch of a few scans does not run on a few XCDs alone
-        bjob = blockIdx.x / (unsigned)P.nb;
-        bx = blockIdx.x % (unsigned)P.nb;
-    }
+    // scan j's blocks on one XCD (its L2) in every evaluation: the neighbour
+    // records and plane caches stay in the L2 that wrote them
+    xcd_block(P.nb, bjob, bx);
     const HsJob job = P.jobs[bjob];
     IekfSlot* slot = job.slot;
     if (bx > 0 && (int)bx * kEvalBlock >= job.n) return;  // (an empty scan keeps one block: it solves)
@@ -2362,21 +2351,8 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
     for (int j = 0; j < kRedUsed; j++) acc[j] = 0.0;
     acc[kRedUsed] = (double)n_slots;  // the search's counts ride in the block partials
     acc[kRedUsed + 1] = (double)n_pts;
-    int nblk = max(1, (job.n + kEvalBlock - 1) / kEvalBlock);
-    if (!FIRST && LIVO_NOSEARCH_K > 1 && !search) {
-        // an evaluation without a search is a cached-plane pass: block bx takes
-        // chunks bx*K .. bx*K + K - 1 of 256 points, so K times fewer blocks
-        // reduce partials and take tickets; the others leave at once
-        constexpr int K = LIVO_NOSEARCH_K;
-        const int nb_k = (nblk + K - 1) / K;
-        if ((int)bx >= nb_k) return;  // block-uniform
-#pragma unroll 1
-        for (int c = 0; c < K; c++) {
-            const int ic = ((int)bx * K + c) * kEvalBlock + threadIdx.x;
-            if (ic < job.n) hshare_point(E.h, job, slot->state, ic, 0, acc, hshare_load(job, ic, true));
-        }
-        nblk = nb_k;
-    } else if (valid) {
+    const int nblk = max(1, (job.n + kEvalBlock - 1) / kEvalBlock);
+    if (valid) {
         hshare_point(E.h, job, slot->state, i, search, acc, pin);
     }
     EVAL_MARK_SYNC(3);
@@ -2926,26 +2902,6 @@ int launch_knn_grid(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, 
         hipLaunchKernelGGL(k_knn_canon, dim3(kReplayBlocks), dim3(64), 0, (hipStream_t)stream, q);
     else
         hipLaunchKernelGGL(k_knn_replay, dim3(kReplayBlocks), dim3(64), replay_lds_bytes(q.depth), (hipStream_t)stream, q);
-    return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
-}
-
-// Row copy by a kernel (rows x width bytes, 4-B words, strided), for the
-// small per-batch slot / job transfers between pinned host memory and HBM:
-// the device reads or writes the host-mapped rows directly, one launch instead
-// of a DMA copy and its completion latency.  Block r copies row r.
-__global__ __launch_bounds__(256) void k_copy_rows(const uint32_t* __restrict__ src, size_t src_stride,
-                                                   uint32_t* __restrict__ dst, size_t dst_stride, int words) {
-    const uint32_t* s = src + (size_t)blockIdx.x * (src_stride / 4);
-    uint32_t* d = dst + (size_t)blockIdx.x * (dst_stride / 4);
-    for (int w = threadIdx.x; w < words; w += 256) d[w] = s[w];
-}
-
-int launch_copy_rows(const void* src, size_t src_stride, void* dst, size_t dst_stride, size_t width, int rows,
-                     void* stream) {
-    if (rows <= 0) return LIVO_OK;
-    if (width % 4 || src_stride % 4 || dst_stride % 4) return LIVO_E_INVALID;
-    hipLaunchKernelGGL(k_copy_rows, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream,
-                       (const uint32_t*)src, src_stride, (uint32_t*)dst, dst_stride, (int)(width / 4));
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 

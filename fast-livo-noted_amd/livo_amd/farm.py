@@ -68,7 +68,7 @@ def allreduce_counters(c: Counters, device=None) -> Counters:
     import torch
     import torch.distributed as dist
     t = torch.tensor(c.as_array(), dtype=torch.int64, device=device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_available() and dist.is_initialized():  # (a world of 1 still runs the collective)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return Counters.from_array(t.cpu().numpy())
 
@@ -77,6 +77,6 @@ def allreduce_max(x: float, device=None) -> float:
     import torch
     import torch.distributed as dist
     t = torch.tensor([x], dtype=torch.float64, device=device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_available() and dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())

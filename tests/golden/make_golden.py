@@ -5,7 +5,8 @@ The reference has no golden vectors for this path and cannot be built here
 (oracle/livo_oracle.cpp) on deterministic synthetic inputs, and stores the
 inputs themselves so that it does not depend on the generator staying
 unchanged.  It pins the oracle (tests/test_oracle.py::test_oracle_matches_golden)
-and the HIP path (tests/test_gpu_golden.py) against regressions.
+and the HIP path (tests/test_gpu_bench_mode.py::test_golden_fixture) against
+regressions.
 
 Run:  python tests/golden/make_golden.py
 """

@@ -5,10 +5,12 @@
     C ABI reproduces it -- k-NN, normals, flags bit-exact; HᵀH 1e-9; the IEKF
     update's counts exact and its per-evaluation state delta within 1e-5;
   * the bench's headline mode (bench.py, config 2 as the config-4 shard of one
-    GPU): 8 x 100k-point scans vs the 1M-point map in ONE batched call over
-    4 stream groups, every scan against the oracle's own update;
+    GPU): 8 x 100k-point scans vs the 1M-point map in ONE batched call in
+    the default stream grouping, every scan against the oracle's own update;
   * the bench's N-GPU launcher: `bench.py --gpus 2` starts two ranks (here
-    sharing one GPU, gloo for the counter all-reduce) and reports both.
+    sharing one GPU, gloo for the counter all-reduce) and reports both;
+  * the farm's counter all-reduce over RCCL (backend "nccl") on device
+    tensors at world size 1.
 """
 import json
 import os
@@ -57,8 +59,8 @@ def test_golden_fixture(built):
 
 @pytest.mark.slow
 def test_bench_headline_mode_parity(built):
-    """8 x 100k scans, 1M map, one livo_iekf_update_batch over 4 stream groups
-    (the bench's step): per scan, the oracle's iterations, k-NN passes,
+    """8 x 100k scans, 1M map, one livo_iekf_update_batch in the default stream
+    grouping (one group at 800k points: the bench's step): per scan, the oracle's iterations, k-NN passes,
     effective points and per-evaluation state deltas."""
     import livo_amd
     import oracle
@@ -96,3 +98,37 @@ def test_bench_two_ranks(built):
     assert j["total_scans"] == 2 * 8 * 2
     assert j["config"]["parallelism"] == "scan farm x2"
     assert j["value"] > 0
+
+
+_RCCL_SCRIPT = r"""
+import os, sys
+sys.path.insert(0, os.path.join(os.environ["LIVO_ROOT"], "fast-livo-noted_amd"))
+import torch
+import torch.distributed as dist
+from livo_amd import farm
+torch.cuda.set_device(0)
+dev = torch.device("cuda", 0)
+dist.init_process_group("nccl", init_method="tcp://127.0.0.1:" + os.environ["LIVO_PORT"], rank=0, world_size=1,
+                        device_id=dev)
+c = farm.Counters(scans=8, evals=40, knn_passes=16, effct_points=123456, knn_visits=77, knn_queries=800000)
+tot = farm.allreduce_counters(c, dev)
+tmax = farm.allreduce_max(0.125, dev)
+dist.barrier()
+print("BACKEND", dist.get_backend(), tot.as_array().tolist(), tmax, flush=True)
+dist.destroy_process_group()
+"""
+
+
+def test_rccl_counter_allreduce_world1(built):
+    """The farm's collectives on device tensors over backend "nccl" (RCCL) at
+    world size 1: the code path bench.py --gpus N takes on the 8-GPU node
+    (one rank per GPU), here on this box's single GPU."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, LIVO_ROOT=ROOT, LIVO_PORT=str(port))
+    r = subprocess.run([sys.executable, "-c", _RCCL_SCRIPT], capture_output=True, text=True, timeout=180, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("BACKEND")]
+    assert line == ["BACKEND nccl [8, 40, 16, 123456, 77, 800000] 0.125"], r.stdout[-1000:]
