@@ -1,4 +1,4 @@
-// device_common.h — device helpers shared by livo_kernels.hip and ivox_kernels.hip.
+// device_common.h — device helpers shared by the kernel files.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -25,6 +25,20 @@ __device__ __forceinline__ void xcd_block(int nb, unsigned& job, unsigned& bx) {
     const unsigned wgid = (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q) + orig / 8u;
     job = wgid / (unsigned)nb;
     bx = wgid % (unsigned)nb;
+}
+
+// Centre of grid cell v along one axis, and the squared distance of a point to
+// a cell centre: the cell runs' sort key (k_cr_rho) and the search's
+// termination test (vrun_search) use exactly these operations, so both see
+// the same bits.
+__device__ __forceinline__ float cell_centre(float org, float h, int v) { return org + ((float)v + 0.5f) * h; }
+__device__ __forceinline__ float centre_d2(float cx, float cy, float cz, float x, float y, float z) {
+    const float t0 = x - cx, t1 = y - cy, t2 = z - cz;
+    return (t0 * t0 + t1 * t1) + t2 * t2;
+}
+__device__ __forceinline__ float cr_rho2(const float org[3], float h, int v0, int v1, int v2, float x, float y,
+                                         float z) {
+    return centre_d2(cell_centre(org[0], h, v0), cell_centre(org[1], h, v1), cell_centre(org[2], h, v2), x, y, z);
 }
 
 }  // namespace livo

@@ -585,23 +585,19 @@ __global__ void k_dyn_slots(const unsigned long long* __restrict__ skeys, const 
 // ---- cell runs (livo_internal.h), built on the device from the cell grid ----
 // Entry e = 27 j + b: grid point j in the run of the b-th cell around its own
 // cell (offset (b % 3, b / 3 % 3, b / 9) - 1).  The run of cell v is sorted by
-// rho, the distance to v's centre, then by e; the same float operations as
-// build_vertex_runs (mode 1), so the same bits.
+// rho2, the squared distance to v's centre, then by e.  cr_rho2 is also the
+// search's termination test (vrun_search): the same float operations, so the
+// same bits, and the scan order is exactly the order the test assumes.
 struct CrGeo {
     float org[3];
     float h, inv;
 };
-__device__ __forceinline__ void cr_entry(const CrGeo& G, const float4 p, uint32_t b, int v[3], float& rho) {
-    const float q[3] = {p.x, p.y, p.z};
+__device__ __forceinline__ void cr_entry(const CrGeo& G, const float4 p, uint32_t b, int v[3], float& rho2) {
     const int o[3] = {(int)(b % 3u) - 1, (int)((b / 3u) % 3u) - 1, (int)(b / 9u) - 1};
-    float d2 = 0.f;
+    const float q[3] = {p.x, p.y, p.z};
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
-        v[k] = (int)floorf((q[k] - G.org[k]) * G.inv) + o[k];  // as build_grid_map's cell
-        const float t = q[k] - (G.org[k] + ((float)v[k] + 0.5f) * G.h);
-        d2 = d2 + t * t;
-    }
-    rho = sqrtf(d2);
+    for (int k = 0; k < 3; k++) v[k] = (int)floorf((q[k] - G.org[k]) * G.inv) + o[k];  // as build_grid_map's cell
+    rho2 = cr_rho2(G.org, G.h, v[0], v[1], v[2], p.x, p.y, p.z);
 }
 __device__ __forceinline__ unsigned long long cr_key(const int v[3]) {
     return (unsigned long long)(v[0] + kGridBias) | ((unsigned long long)(v[1] + kGridBias) << 21) |
@@ -611,9 +607,9 @@ __global__ void k_cr_rho(const float4* __restrict__ gpts, int64_t n, CrGeo G, ui
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= n) return;
     int v[3];
-    float rho;
-    cr_entry(G, gpts[e / 27], (uint32_t)(e % 27), v, rho);
-    rho_bits[e] = __float_as_uint(rho);  // non-negative: the bits sort as the values
+    float rho2;
+    cr_entry(G, gpts[e / 27], (uint32_t)(e % 27), v, rho2);
+    rho_bits[e] = __float_as_uint(rho2);  // non-negative: the bits sort as the values
     iota[e] = (uint32_t)e;
 }
 __global__ void k_cr_key(const float4* __restrict__ gpts, const uint32_t* __restrict__ e1, int64_t n, CrGeo G,
@@ -622,27 +618,19 @@ __global__ void k_cr_key(const float4* __restrict__ gpts, const uint32_t* __rest
     if (i >= n) return;
     const uint32_t e = e1[i];
     int v[3];
-    float rho;
-    cr_entry(G, gpts[e / 27u], e % 27u, v, rho);
+    float rho2;
+    cr_entry(G, gpts[e / 27u], e % 27u, v, rho2);
     keys[i] = cr_key(v);
 }
 __global__ void k_cr_fill(const float4* __restrict__ gpts, const uint32_t* __restrict__ e2,
-                          const unsigned long long* __restrict__ skeys, int64_t n, CrGeo G, float4* vpts,
-                          uint32_t* vidx, uint32_t* heads) {
+                          const unsigned long long* __restrict__ skeys, int64_t n, float4* vpts, uint32_t* heads) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n + 8) return;
-    if (i >= n) {  // chunk padding of the run scan
-        vpts[i] = make_float4(0.f, 0.f, 0.f, INFINITY);
-        vidx[i] = 0u;
+    if (i >= n) {  // chunk padding of the run scan (never inside a run: masked by the run length)
+        vpts[i] = make_float4(0.f, 0.f, 0.f, 0.f);
         return;
     }
-    const uint32_t e = e2[i], j = e / 27u;
-    const float4 p = gpts[j];
-    int v[3];
-    float rho;
-    cr_entry(G, p, e % 27u, v, rho);
-    vpts[i] = make_float4(p.x, p.y, p.z, rho);
-    vidx[i] = j;
+    vpts[i] = gpts[e2[i] / 27u];  // x, y, z, map index bits
     heads[i] = (i == 0 || skeys[i] != skeys[i - 1]) ? 1u : 0u;
 }
 
@@ -727,10 +715,11 @@ int launch_cr_key(const float* gpts, const uint32_t* e1, int64_t n, const float 
     DYN_LAUNCH(k_cr_key, n, reinterpret_cast<const float4*>(gpts), e1, n, G, keys);
 }
 int launch_cr_fill(const float* gpts, const uint32_t* e2, const unsigned long long* skeys, int64_t n,
-                   const float org[3], float h, float* vpts, uint32_t* vidx, uint32_t* heads, void* stream) {
-    const CrGeo G{{org[0], org[1], org[2]}, h, 1.0f / h};
-    DYN_LAUNCH(k_cr_fill, n + 8, reinterpret_cast<const float4*>(gpts), e2, skeys, n, G,
-               reinterpret_cast<float4*>(vpts), vidx, heads);
+                   const float org[3], float h, float* vpts, uint32_t* heads, void* stream) {
+    (void)org;
+    (void)h;
+    DYN_LAUNCH(k_cr_fill, n + 8, reinterpret_cast<const float4*>(gpts), e2, skeys, n,
+               reinterpret_cast<float4*>(vpts), heads);
 }
 int launch_dyn_delete_boxes(const float* all, uint8_t* alive, int64_t n_ids, const float* boxes, int64_t nb,
                             unsigned long long* cnt, void* stream) {

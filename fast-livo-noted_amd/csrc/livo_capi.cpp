@@ -147,8 +147,7 @@ struct livo_ctx {
     float grid_ppc = 0.f;              // target points per occupied cell when chosen from the map (LIVO_GRID_PPC)
     bool vruns = true;                 // vertex runs on a static map (LIVO_VRUNS=0: the cell walk)
     GridSlot* vslots = nullptr;        // vertex runs (static map only)
-    float* vpts = nullptr;
-    uint32_t* vidx = nullptr;
+    float* vpts = nullptr;             // run entries (x, y, z, map index bits)
     int32_t vlog2 = 0;
     GridSlot* gslots = nullptr;        // cell grid
     float* gpts = nullptr;
@@ -294,7 +293,6 @@ static KnnParams make_knn_params(livo_ctx* c) {
     const bool vr = c->vslots && !c->dyn.active;
     kp.vslots = vr ? c->vslots : nullptr;
     kp.vpts = vr ? c->vpts : nullptr;
-    kp.vidx = vr ? c->vidx : nullptr;
     kp.vlog2 = c->vlog2;
     kp.identity = 0;
     kp.iv = ivox_params(c);
@@ -1085,7 +1083,6 @@ int livo_ctx_destroy(livo_ctx* c) {
     dev_free(c->gpts);
     dev_free(c->vslots);
     dev_free(c->vpts);
-    dev_free(c->vidx);
     dev_free(c->d_replay_count);
     dev_free(c->d_replay_total);
     dev_free(c->d_replay_list);
@@ -1141,15 +1138,14 @@ int livo_last_timings(livo_ctx* c, livo_timings* out) {
 }
 
 // The cell runs of the static map's grid (livo_internal.h), built on the
-// device: two stable radix sorts (rho, then the run key) of the 27 M entries,
+// device: two stable radix sorts (rho2, then the run key) of the 27 M entries,
 // the runs' heads and starts, and their hash table (load factor <= 1/4).
 static int build_cell_runs(livo_ctx* c, int64_t M) {
     dev_free(c->vslots);
     dev_free(c->vpts);
-    dev_free(c->vidx);
     if (M <= 0) return LIVO_OK;
     const int64_t n = M * 27;
-    if (n >= (int64_t)0xFFFFFFFF) return LIVO_E_RANGE;  // 32-bit entry ids
+    if (n + 8 >= (int64_t)kRunPosLimit) return LIVO_E_RANGE;  // 31-bit run positions (kRunPos)
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t b4 = al((size_t)n * 4), b8 = al((size_t)n * 8);
     char* scr = nullptr;
@@ -1167,7 +1163,7 @@ static int build_cell_runs(livo_ctx* c, int64_t M) {
     uint32_t* starts = (uint32_t*)p; p += al(((size_t)n + 1) * 4);
     unsigned long long* nruns = (unsigned long long*)p;
     int rc = LIVO_OK;
-    if (dev_alloc(&c->vpts, (size_t)(n + 8) * 4) || dev_alloc(&c->vidx, (size_t)(n + 8))) rc = LIVO_E_OOM;
+    if (dev_alloc(&c->vpts, (size_t)(n + 8) * 4)) rc = LIVO_E_OOM;
     if (!rc) rc = launch_cr_rho(c->gpts, n, c->gorg, c->gh, rho, iota, c->stream);
     if (!rc) {
         size_t tb = 0;
@@ -1178,7 +1174,7 @@ static int build_cell_runs(livo_ctx* c, int64_t M) {
     }
     if (!rc) rc = launch_cr_key(c->gpts, e1, n, c->gorg, c->gh, keys, c->stream);
     if (!rc) rc = sort_u64(c, keys, skeys, e1, e2, n);
-    if (!rc) rc = launch_cr_fill(c->gpts, e2, skeys, n, c->gorg, c->gh, c->vpts, c->vidx, heads, c->stream);
+    if (!rc) rc = launch_cr_fill(c->gpts, e2, skeys, n, c->gorg, c->gh, c->vpts, heads, c->stream);
     if (!rc) rc = ivox_scan(c, heads, runid, n);
     if (!rc) rc = launch_dyn_runs(heads, runid, n, starts, nruns, c->stream);
     unsigned long long runs = 0;
@@ -1195,11 +1191,10 @@ static int build_cell_runs(livo_ctx* c, int64_t M) {
     if (rc) {
         dev_free(c->vslots);
         dev_free(c->vpts);
-        dev_free(c->vidx);
         return rc;
     }
     c->vlog2 = log2;
-    c->grid_bytes += (int64_t)(table * sizeof(GridSlot) + (size_t)(n + 8) * 20);
+    c->grid_bytes += (int64_t)(table * sizeof(GridSlot) + (size_t)(n + 8) * 16);
     return LIVO_OK;
 }
 
@@ -1211,7 +1206,8 @@ int livo_map_build(livo_ctx* c, const float* xyz, int64_t M, int64_t stride_byte
     if (rc) return rc;
     HostLeafMap lm;
     HostGridMap gm;
-    const bool vr = c->knn_kind == 2 && c->vruns;
+    // (a map of more than ~79M points keeps the cell walk: run positions are 31-bit)
+    const bool vr = c->knn_kind == 2 && c->vruns && M * 27 + 8 < (int64_t)kRunPosLimit;
     rc = c->knn_kind >= 1 ? build_grid_map(xyz, M, stride_bytes, c->grid_cell, &gm, c->grid_ppc > 0.f ? c->grid_ppc
                                                                                     : (vr ? kVrunPpc : 0.f))
                           : build_leaf_map(xyz, M, stride_bytes, c->leaf_size, &lm);
@@ -1229,7 +1225,6 @@ int livo_map_build(livo_ctx* c, const float* xyz, int64_t M, int64_t stride_byte
     dev_free(c->gpts);
     dev_free(c->vslots);
     dev_free(c->vpts);
-    dev_free(c->vidx);
     c->nodes = nullptr;
     c->lnodes = nullptr;
     c->lpts = nullptr;

@@ -118,25 +118,18 @@ struct HostGridMap {
 // cell_h <= 0: chosen from the map (about ppc_target points per occupied cell, 20 if 0)
 int build_grid_map(const float* xyz, int64_t M, int64_t stride_bytes, float cell_h, HostGridMap* out,
                    float ppc_target = 0.f);
+constexpr int64_t kRunPosLimit = 0x7FFFFFFF;  // run entries a search can address (31-bit positions)
 constexpr float kVrunPpc = 20.0f;  // cell occupancy the cell runs are sized for (0.35 m cells on the config-2 map)
 void free_grid_map(HostGridMap* m);
 
-// Vertex runs: the search structure of the batched IEKF k-NN.  Vertex v of
-// the cell grid (position org + v h) owns the 2x2x2 cells that share it;
-// every map point is stored in the run of each of the 8 vertices of its cell
-// (8x the points: 128 MB for a 1M map), a run sorted by the distance rho to
-// its vertex.  A query takes the vertex nearest to it: one hash probe, one
-// contiguous run that covers the ball of radius h - |q - v|_inf around it,
-// scanned until rho exceeds |q - v| + the current bound.
-struct HostVertexRuns {
-    GridSlot* slots = nullptr;  // 2^log2_slots: vertex key -> run
-    float* pts = nullptr;       // (n + 8) x 4 floats: x, y, z, rho
-    uint32_t* idx = nullptr;    // n + 8: the point's index in the grid's point array
-    int64_t n = 0;
-    int32_t log2_slots = 0;
-};
-int build_vertex_runs(const HostGridMap& gm, HostVertexRuns* out, int mode = 0);  // mode 1: 27-cell runs
-void free_vertex_runs(HostVertexRuns* v);
+// Cell runs: the search structure of the batched IEKF k-NN on a static map.
+// The run of cell c holds every map point of the 3x3x3 cells around c (27x
+// the points: 432 MB for a 1M map), sorted by the squared distance rho2 to
+// c's centre.  Entry: (x, y, z, map index bits) -- the coordinates and index
+// the neighbour record needs, so a search reads nothing else; rho2 is
+// recomputed from the entry with the build's float operations (same bits).
+// A query takes its own cell's run: one hash probe, one contiguous scan that
+// stops at the first entry with rho > |q - centre| + the current bound.
 
 // ---------------------------------------------------------------------------
 // iVox map (faster_lio::IVox<3, DEFAULT>, include/ivox3d/ivox3d.h): the
@@ -303,9 +296,8 @@ struct KnnParams {
     float gh;               // cell edge
     float geps;             // cell-bound slack for float rounding of the cell assignment
     int32_t glog2;          // log2 of the hash table size
-    const GridSlot* vslots; // vertex runs (null: the cell walk of grid_search)
-    const float* vpts;      // x, y, z, rho
-    const uint32_t* vidx;   // grid point index of each run entry
+    const GridSlot* vslots; // cell runs (null: the cell walk of grid_search)
+    const float* vpts;      // run entries: x, y, z, map index bits
     int32_t vlog2;
     IvoxParams iv;          // iVox backend (LIVO_BACKEND_IVOX)
     int32_t canon;          // incremental map: flagged queries -> k_knn_canon instead of the ikd-Tree replay
@@ -565,14 +557,14 @@ int launch_dyn_delete_boxes(const float* all, uint8_t* alive, int64_t n_ids, con
                             unsigned long long* cnt, void* stream);
 
 // Cell runs on the device from the cell grid (gpts: n / 27 points): entry e's
-// rho (bits) and e; the run key of pass-1-sorted entries; the final runs
-// (x, y, z, rho), their grid indices and the run heads.
+// rho2 (bits) and e; the run key of pass-1-sorted entries; the final runs
+// (x, y, z, map index bits) and the run heads.
 int launch_cr_rho(const float* gpts, int64_t n, const float org[3], float h, uint32_t* rho_bits, uint32_t* iota,
                   void* stream);
 int launch_cr_key(const float* gpts, const uint32_t* e1, int64_t n, const float org[3], float h,
                   unsigned long long* keys, void* stream);
 int launch_cr_fill(const float* gpts, const uint32_t* e2, const unsigned long long* skeys, int64_t n,
-                   const float org[3], float h, float* vpts, uint32_t* vidx, uint32_t* heads, void* stream);
+                   const float org[3], float h, float* vpts, uint32_t* heads, void* stream);
 
 // Nearest_Points carried over by point index (laser_mapping.cpp:165 resize keeps entries).
 int launch_inherit_nn(NNRec* dst, const int32_t* dst_perm, int64_t n_dst, const NNRec* src,

@@ -675,6 +675,9 @@ __global__ __launch_bounds__(kKnnBlock, 8) void k_knn_pass(KnnParams P) {  // 8 
 // query (exact replay on the ikd-Tree) if C1 or C2 fails.
 // One query of the leaf-map search: its world point, seed bound, sorted
 // 5-candidate list and e6 (smallest distance rejected or evicted).
+// A candidate's position in the cell runs (vrun_search) rather than a grid /
+// leaf-map slot: lq_finish reads it from P.vpts.
+constexpr uint32_t kRunPos = 0x80000000u;
 struct LeafQuery {
     float qx, qy, qz, B, e6;
     float d[kNN];
@@ -752,12 +755,21 @@ __device__ __forceinline__ void lq_point(LeafQuery& q, const float4 v, uint32_t 
 // is a strict total order on the 5 points, so sorting by (dist, x) gives the
 // reference's order.  A gap in (0, 1e-10] (CMP not transitive) or an exact tie
 // with equal x (neither point "less") still goes to the exact replay.
+// RUNS: candidates may be cell-run positions (kRunPos, vrun_search) besides slots of lpts
+template <bool RUNS>
+__device__ __forceinline__ float4 cand_point(const float4* __restrict__ lpts, const float4* __restrict__ vpts,
+                                             uint32_t nd) {
+    if constexpr (RUNS) return (nd & kRunPos) ? vpts[nd & ~kRunPos] : lpts[nd];
+    return lpts[nd];
+}
+template <bool RUNS = false>
 __device__ __forceinline__ bool lq_finish(LeafQuery& q, const KnnParams& P, const HsJob& job, unsigned bjob,
-                                          int i, const float4* __restrict__ lpts, bool overrun, bool enqueue = true) {
+                                          int i, const float4* __restrict__ lpts, bool overrun, bool enqueue = true,
+                                          const float4* __restrict__ vpts = nullptr) {
     const int cnt = (int)min<int64_t>(P.lM, (int64_t)kNN);
     float4 a[kNN];
 #pragma unroll
-    for (int k = 0; k < kNN; k++) a[k] = k < cnt ? lpts[q.nd[k]] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < kNN; k++) a[k] = k < cnt ? cand_point<RUNS>(lpts, vpts, q.nd[k]) : make_float4(0.f, 0.f, 0.f, 0.f);
     bool amb = overrun || q.e6 - q.d[kNN - 1] <= kFuzz;  // C1 (false while e6 = +inf)
     bool tie = false;
 #pragma unroll
@@ -787,7 +799,7 @@ __device__ __forceinline__ bool lq_finish(LeafQuery& q, const KnnParams& P, cons
         }
 #pragma unroll
         for (int k = 0; k < kNN; k++)
-            if (k < cnt) a[k] = lpts[q.nd[k]];
+            if (k < cnt) a[k] = cand_point<RUNS>(lpts, vpts, q.nd[k]);
     }
     // neighbour record: points, distances, original indices; node[] = leaf-map slots
     float4* o4 = reinterpret_cast<float4*>(job.nn + i);
@@ -1322,17 +1334,20 @@ __device__ __forceinline__ bool grid_search(LeafQuery& q, const KnnParams& P, in
 // ------------------------------------------------------------ cell-run search ----
 // The batched IEKF search on the cell runs (livo_internal.h): the run of the
 // query's own cell c holds every map point of the 3x3x3 cells around c (the
-// cube grid_search's stages 0-1 walk), sorted by the distance rho to c's
-// centre.  One hash probe, then one contiguous scan.  By the triangle
+// cube grid_search's stages 0-1 walk), sorted by rho2, the squared distance to
+// c's centre.  One hash probe, then one contiguous scan.  By the triangle
 // inequality a point with rho > |q - centre| + sqrt(bound) is farther than the
-// bound min(5th candidate, seed bound), so the scan stops at the first such
-// entry (with a 1e-4 m margin over every float rounding involved: a point left
-// out is farther than bound + 1e-10, so it could neither enter the list nor
-// make e6 - d5 <= 1e-10, exactly as a pruned cell of grid_search).  Within a
-// chunk of 8 entries a lane takes the per-point insertion path only when one
-// of them is below its e6.  If the ball of the final bound lies in the cube
-// the list is certified (every point within the bound was scanned); else the
-// lane continues with grid_search's stage 2 outside the cube.
+// bound min(5th candidate, seed bound), so the scan stops at the first chunk
+// whose first entry is such a point (with a 1e-4 m margin over every float
+// rounding involved, the approximate square root included: a point left out
+// is farther than bound + 1e-10, so it could neither enter the list nor make
+// e6 - d5 <= 1e-10, exactly as a pruned cell of grid_search).  Within a chunk
+// of 8 entries a lane takes the per-point insertion path only when one of
+// them is below its e6.  Candidates carry their run position (kRunPos bit
+// set); lq_finish reads coordinates and map index from the run entry.  If the
+// ball of the final bound lies in the cube the list is certified (every point
+// within the bound was scanned); else the lane continues with grid_search's
+// stage 2 outside the cube (candidates there are cell-grid slots).
 __device__ __forceinline__ bool vrun_search(LeafQuery& q, const KnnParams& P, bool valid, int c0, int c1, int c2,
                                             int s0, int s1, int s2, unsigned& visits, unsigned& npts) {
     if (!valid || !(P.lM > 0)) return false;
@@ -1348,11 +1363,10 @@ __device__ __forceinline__ bool vrun_search(LeafQuery& q, const KnnParams& P, bo
     }
     const uint32_t lo = g.key == key ? g.start : 0u, cnt = g.key == key ? g.count : 0u;
     const float h = P.gh;
-    const float ex = q.qx - (P.gorg[0] + ((float)c0 + 0.5f) * h), ey = q.qy - (P.gorg[1] + ((float)c1 + 0.5f) * h);
-    const float ez = q.qz - (P.gorg[2] + ((float)c2 + 0.5f) * h);
-    const float dqv = sqrtf((ex * ex + ey * ey) + ez * ez);
+    const float cx = cell_centre(P.gorg[0], h, c0), cy = cell_centre(P.gorg[1], h, c1);
+    const float cz = cell_centre(P.gorg[2], h, c2);
+    const float dqv = __builtin_amdgcn_sqrtf(centre_d2(cx, cy, cz, q.qx, q.qy, q.qz)) * (1.0f + 1e-6f);
     const float4* __restrict__ run = reinterpret_cast<const float4*>(P.vpts) + lo;
-    const uint32_t* __restrict__ rid = P.vidx + lo;
     uint32_t k0 = 0;
 #pragma unroll 1
     for (; k0 < cnt; k0 += 8) {
@@ -1360,7 +1374,10 @@ __device__ __forceinline__ bool vrun_search(LeafQuery& q, const KnnParams& P, bo
 #pragma unroll
         for (int u = 0; u < 8; u++) v[u] = run[k0 + u];  // padded by 8 entries
         const float thr = lq_thr(q);
-        if (thr < INFINITY && v[0].w > dqv + sqrtf(thr) * (1.0f + 1e-6f) + 1e-4f) break;
+        if (thr < INFINITY) {
+            const float b = dqv + __builtin_amdgcn_sqrtf(thr) * (1.0f + 1e-6f) + 1e-4f;
+            if (centre_d2(cx, cy, cz, v[0].x, v[0].y, v[0].z) > b * b) break;  // rho of every later entry > b
+        }
         float dist[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) {
@@ -1372,7 +1389,7 @@ __device__ __forceinline__ bool vrun_search(LeafQuery& q, const KnnParams& P, bo
                               fminf(fminf(dist[4], dist[5]), fminf(dist[6], dist[7])));
         if (m < q.e6) {
 #pragma unroll
-            for (int u = 0; u < 8; u++) lq_offer(q, dist[u], rid[k0 + u]);
+            for (int u = 0; u < 8; u++) lq_offer(q, dist[u], kRunPos | (lo + k0 + u));
         }
     }
     npts += min(k0, cnt);
@@ -2321,7 +2338,9 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
             }
             EVAL_MARK(5);
 #endif
-            if (valid) amb = lq_finish(q, P, job, bjob, i, reinterpret_cast<const float4*>(P.gpts), !certified, false);
+            if (valid)
+                amb = lq_finish<true>(q, P, job, bjob, i, reinterpret_cast<const float4*>(P.gpts), !certified, false,
+                                      reinterpret_cast<const float4*>(P.vpts));
             EVAL_MARK(6);
         } else {
             const TileView tv = build_tile<kEvalBlock>(U.tile, P, valid, c0, c1, c2, visits, npts);

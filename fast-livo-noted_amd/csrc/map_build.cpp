@@ -410,96 +410,4 @@ void free_grid_map(HostGridMap* m) {
 }
 
 
-// Vertex runs (livo_internal.h): every point of the grid in the runs of the 8
-// vertices of its cell, each run sorted by the distance to its vertex.
-int build_vertex_runs(const HostGridMap& gm, HostVertexRuns* out, int mode) {
-    if (!out) return LIVO_E_INVALID;
-    free_vertex_runs(out);
-    const int64_t M = gm.num_points;
-    const int per = mode == 1 ? 27 : 8;
-    const float h = gm.h, inv = 1.0f / gm.h;
-    struct E {
-        unsigned long long key;
-        float rho;
-        uint32_t j;
-    };
-    std::vector<E> e((size_t)M * per);
-    for (int64_t j = 0; j < M; j++) {
-        const float* p = gm.pts + 4 * j;
-        int64_t c[3];
-        for (int k = 0; k < 3; k++) c[k] = (int64_t)std::floor((p[k] - gm.org[k]) * inv);  // as build_grid_map
-        for (int b = 0; b < per; b++) {
-            int64_t v[3];
-            float ctr[3];
-            if (mode == 1) {  // cell runs: the 27 cells around the point's cell, centre of the run's cell
-                v[0] = c[0] + b % 3 - 1; v[1] = c[1] + (b / 3) % 3 - 1; v[2] = c[2] + b / 9 - 1;
-                for (int k = 0; k < 3; k++) ctr[k] = gm.org[k] + ((float)v[k] + 0.5f) * h;
-            } else {
-                v[0] = c[0] + (b & 1); v[1] = c[1] + ((b >> 1) & 1); v[2] = c[2] + ((b >> 2) & 1);
-                for (int k = 0; k < 3; k++) ctr[k] = gm.org[k] + (float)v[k] * h;
-            }
-            float d2 = 0.f;
-            for (int k = 0; k < 3; k++) {
-                const float t = p[k] - ctr[k];
-                d2 = d2 + t * t;
-            }
-            e[(size_t)j * per + b] = E{grid_key(v[0], v[1], v[2]), std::sqrt(d2), (uint32_t)j};
-        }
-    }
-    std::sort(e.begin(), e.end(), [](const E& a, const E& b) {
-        if (a.key != b.key) return a.key < b.key;
-        if (a.rho != b.rho) return a.rho < b.rho;
-        return a.j < b.j;
-    });
-    int64_t runs = 0;
-    for (size_t i = 0; i < e.size(); i++)
-        if (i == 0 || e[i].key != e[i - 1].key) runs++;
-    int log2 = 4;
-    while (((int64_t)1 << log2) < 4 * runs) log2++;
-    const int64_t nslots = (int64_t)1 << log2;
-    const int64_t n = M * per;
-    GridSlot* slots = (GridSlot*)std::malloc((size_t)nslots * sizeof(GridSlot));
-    float* pts = (float*)std::calloc((size_t)(n + 8), 4 * sizeof(float));
-    uint32_t* idx = (uint32_t*)std::calloc((size_t)(n + 8), sizeof(uint32_t));
-    if (!slots || !pts || !idx) {
-        std::free(slots);
-        std::free(pts);
-        std::free(idx);
-        return LIVO_E_OOM;
-    }
-    for (int64_t k = 0; k < nslots; k++) slots[k] = GridSlot{kGridEmpty, 0u, 0u};
-    for (int64_t i = 0; i < n;) {
-        int64_t j = i;
-        while (j < n && e[j].key == e[i].key) j++;
-        uint64_t sl = grid_hash(e[i].key, log2);
-        while (slots[sl].key != kGridEmpty) sl = (sl + 1) & (uint64_t)(nslots - 1);
-        slots[sl] = GridSlot{e[i].key, (uint32_t)i, (uint32_t)(j - i)};
-        i = j;
-    }
-    for (int64_t i = 0; i < n; i++) {
-        const float* p = gm.pts + 4 * (int64_t)e[i].j;
-        pts[4 * i + 0] = p[0];
-        pts[4 * i + 1] = p[1];
-        pts[4 * i + 2] = p[2];
-        pts[4 * i + 3] = e[i].rho;
-        idx[i] = e[i].j;
-    }
-    out->slots = slots;
-    out->pts = pts;
-    out->idx = idx;
-    out->n = n;
-    out->log2_slots = log2;
-    return LIVO_OK;
-}
-
-void free_vertex_runs(HostVertexRuns* v) {
-    if (!v) return;
-    std::free(v->slots);
-    std::free(v->pts);
-    std::free(v->idx);
-    v->slots = nullptr;
-    v->pts = nullptr;
-    v->idx = nullptr;
-}
-
 }  // namespace livo

@@ -33,11 +33,13 @@ def main():
         for s, name in ((2, "first-search evals"), (1, "rematch evals"), (0, "no-search evals")):
             row = buf[8 * s: 8 * s + 8]
             nb = max(row[0], 1)
+            # cell-run path: ph1 loads + slot control, ph5 vrun search, ph6 lq_finish (record),
+            # ph2 tie replay + barrier, ph3 plane pass, ph4 reduction + ticket (+ solve); slot 7:
+            # lanes not certified inside the cube (a count, per block)
             print(f"{name}: blocks {row[0]}  per block (kcycles): " +
-                  "  ".join(f"ph{k} {row[k] / nb / 1e3:.2f}" for k in range(1, 5)))
-            if s:
-                print("  search stages of thread 0 (kcycles per block): " +
-                      "  ".join(f"{n} {row[5 + k] / nb / 1e3:.2f}" for k, n in enumerate(("stage0", "stage1", "stage2"))))
+                  "  ".join(f"ph{k} {row[k] / nb / 1e3:.2f}" for k in (1, 5, 6, 2, 3, 4)) +
+                  f"  uncertified lanes/block {row[7] / nb:.2f}")
+
 
 if __name__ == "__main__":
     main()
