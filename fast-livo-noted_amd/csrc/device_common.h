@@ -27,6 +27,29 @@ __device__ __forceinline__ void xcd_block(int nb, unsigned& job, unsigned& bx) {
     bx = wgid % (unsigned)nb;
 }
 
+// XCD-interleaved block order in chunks of C consecutive blocks: XCD x takes
+// chunks x, x + 8, x + 16, ... of the (scan, block) ids, so every XCD holds a
+// share of every scan (a batch's scans cost different amounts in a search:
+// with one contiguous range per XCD the most expensive scan's XCD is the
+// straggler), while a chunk of C Morton-consecutive blocks keeps its map
+// region in one L2.  The order is the same in every evaluation, so a block's
+// plane cache is re-read on the XCD that wrote it.  C = 0: xcd_block.
+__device__ __forceinline__ void xcd_chunk_block(int nb, int C, unsigned& job, unsigned& bx) {
+    if (C <= 0) {
+        xcd_block(nb, job, bx);
+        return;
+    }
+    const unsigned c = (unsigned)C, orig = blockIdx.x, span = 8u * c;
+    const unsigned full = gridDim.x / span * span;
+    unsigned wgid = orig;
+    if (orig < full) {
+        const unsigned k = orig / 8u;
+        wgid = ((k / c) * 8u + orig % 8u) * c + k % c;
+    }
+    job = wgid / (unsigned)nb;
+    bx = wgid % (unsigned)nb;
+}
+
 // Centre of grid cell v along one axis, and the squared distance of a point to
 // a cell centre: the cell runs' sort key (k_cr_rho) and the search's
 // termination test (vrun_search) use exactly these operations, so both see

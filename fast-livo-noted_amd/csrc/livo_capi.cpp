@@ -145,7 +145,8 @@ struct livo_ctx {
     bool fused = true;                 // kind 2: one k_iekf_eval launch per evaluation (LIVO_FUSED=0: separate passes)
     float grid_cell = 0.f;             // cell edge (LIVO_GRID_CELL; 0: from the map)
     float grid_ppc = 0.f;              // target points per occupied cell when chosen from the map (LIVO_GRID_PPC)
-    bool vruns = true;                 // vertex runs on a static map (LIVO_VRUNS=0: the cell walk)
+    bool vruns = true;                 // cell runs on a static map (LIVO_VRUNS=0: the cell walk)
+    int xcd_chunk = 0;                 // k_iekf_eval block order (LIVO_XCD_CHUNK; 0: one range per XCD)
     GridSlot* vslots = nullptr;        // vertex runs (static map only)
     float* vpts = nullptr;             // run entries (x, y, z, map index bits)
     int32_t vlog2 = 0;
@@ -279,6 +280,7 @@ static KnnParams make_knn_params(livo_ctx* c) {
     kp.has_map = c->has_map && c->map_points > 0 ? 1 : 0;
     kp.force = -1;
     kp.depth = c->map_depth;
+    kp.n_nodes = c->has_map ? c->map_slots : 0;
     kp.lnodes = c->lnodes;
     kp.lpts = c->lpts;
     kp.ldepth = c->leaf_depth;
@@ -294,6 +296,7 @@ static KnnParams make_knn_params(livo_ctx* c) {
     kp.vslots = vr ? c->vslots : nullptr;
     kp.vpts = vr ? c->vpts : nullptr;
     kp.vlog2 = c->vlog2;
+    kp.xcd_chunk = c->xcd_chunk;
     kp.identity = 0;
     kp.iv = ivox_params(c);
     kp.canon = c->dyn.active ? 1 : 0;
@@ -1047,6 +1050,7 @@ int livo_ctx_create(int device, const livo_params* p, livo_ctx** out) {
     if (const char* env = std::getenv("LIVO_KNN_KIND"))
         c->knn_kind = std::strcmp(env, "leaf") == 0 ? 0 : std::strcmp(env, "grid") == 0 ? 1 : 2;
     if (const char* env = std::getenv("LIVO_VRUNS")) c->vruns = std::atoi(env) != 0;
+    if (const char* env = std::getenv("LIVO_XCD_CHUNK")) c->xcd_chunk = std::max(0, std::atoi(env));  // tuning knob
     if (const char* env = std::getenv("LIVO_GRID_PPC")) {  // tuning knob
         const float v = (float)std::atof(env);
         if (v > 0.f) c->grid_ppc = v;

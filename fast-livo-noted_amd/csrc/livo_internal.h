@@ -284,8 +284,10 @@ struct KnnParams {
     int32_t has_map;
     int32_t force;          // -1: follow ctrl; 0: skip; 1: search
     int32_t depth;          // tree levels (LDS stack entries of the full search)
+    int64_t n_nodes;        // heap slots of the ikd-Tree records (the replay's subtree loads stay below)
     int32_t identity;       // 1: pts are world points already (livo_knn)
     int32_t nb;             // blocks per scan (set by the launcher)
+    int32_t xcd_chunk;      // k_iekf_eval block order: XCD-interleaved chunks of this many blocks (0: one range per XCD)
     int32_t ldepth;         // leaf map depth D
     const LeafNode* lnodes; // leaf map internal records
     const float* lpts;      // leaf map points, 4 floats each (x, y, z, index bits)

@@ -398,8 +398,13 @@ __device__ __forceinline__ int level_of(uint32_t h) { return 31 - __clz(h + 1); 
 // record for the son's box distance and re-checks it, which is exactly the
 // check a stack pop makes.  Same visits, same candidates, same order, ties
 // included.  Used for the rare queries the fast pass flags (k_knn_replay).
-__device__ __forceinline__ void knn_exact(const MapNode* __restrict__ nodes, int has_map, float qx, float qy, float qz,
-                                       Cands& c) {
+// The record fetch is a parameter: one lane's loads (knn_exact) or a wave's
+// subtree cache (knn_exact_wave); the traversal is the same code.
+struct NodeRec {
+    float4 a, b, c, d;
+};
+template <class Fetch>
+__device__ __forceinline__ void knn_exact_t(Fetch&& fetch, int has_map, float qx, float qy, float qz, Cands& c) {
     KHeap h;
 #pragma unroll
     for (int j = 0; j < kNN; j++) { h.d[j] = INFINITY; h.x[j] = 0.0f; h.node[j] = 0u; }
@@ -407,8 +412,8 @@ __device__ __forceinline__ void knn_exact(const MapNode* __restrict__ nodes, int
     uint32_t cur = 0, trail = 0;
     bool down = true;
     while (has_map) {
-        const float4* rp = rec_ptr(nodes, cur);
-        const float4 a = rp[0], b = rp[1], cc = rp[2], dd = rp[3];
+        const NodeRec r = fetch(cur);
+        const float4 a = r.a, b = r.b, cc = r.c, dd = r.d;
         const uint32_t meta = __float_as_uint(a.w);
         const bool hl = (meta & kLeftBit) != 0u, hr = (meta & kRightBit) != 0u;
         const float dl = hl ? box_dist(qx, qy, qz, b.x, b.y, b.z, b.w, cc.x, cc.y) : INFINITY;
@@ -447,6 +452,56 @@ __device__ __forceinline__ void knn_exact(const MapNode* __restrict__ nodes, int
         down = false;
     }
     kh_extract(h, c);
+}
+__device__ __forceinline__ void knn_exact(const MapNode* __restrict__ nodes, int has_map, float qx, float qy, float qz,
+                                          Cands& c) {
+    knn_exact_t(
+        [&](uint32_t hn) {
+            const float4* rp = rec_ptr(nodes, hn);
+            return NodeRec{rp[0], rp[1], rp[2], rp[3]};
+        },
+        has_map, qx, qy, qz, c);
+}
+
+// knn_exact for one query by a whole wave (every lane active, the query
+// wave-uniform): the traversal is a chain of dependent record loads (~50 per
+// query on a 1M-point tree), so the wave loads the 63 records of the K = 6
+// levels below the current node in one round trip (heap order: the
+// descendants of h at depth d are (h + 1) 2^d - 1 + 0 .. 2^d - 1) into its 4 KB
+// of LDS, walks them from there, and reloads only when the walk leaves that
+// subtree.  Every lane runs the same walk on the same LDS words, so every lane
+// ends with the same candidates as knn_exact.
+constexpr int kReplayLevels = 6;
+__device__ __forceinline__ void knn_exact_wave(const MapNode* __restrict__ nodes, int64_t n_nodes, int has_map, float qx,
+                                               float qy, float qz, float4* __restrict__ cache, Cands& c) {
+    const unsigned lane = threadIdx.x & 63u;
+    uint32_t root = 0xFFFFFFFFu;
+    int root_lev = 0;
+    auto reload = [&](uint32_t hn) {
+        root = hn;
+        root_lev = level_of(hn);
+        if (lane < (1u << kReplayLevels) - 1u) {
+            const int lv = 31 - __clz(lane + 1u);
+            const uint64_t node = ((uint64_t)(hn + 1u) << lv) - 1u + (lane - ((1u << lv) - 1u));
+            if (node < (uint64_t)n_nodes) {
+                const float4* rp = rec_ptr(nodes, (uint32_t)node);
+#pragma unroll
+                for (int k = 0; k < 4; k++) cache[lane * 4u + k] = rp[k];
+            }
+        }
+        WAVE_SYNC();
+    };
+    knn_exact_t(
+        [&](uint32_t hn) {
+            const int d = level_of(hn) - root_lev;
+            if (root == 0xFFFFFFFFu || d < 0 || d >= kReplayLevels || ((hn + 1u) >> d) != root + 1u) reload(hn);
+            const int dd = level_of(hn) - root_lev;
+            const uint32_t loc = (1u << dd) - 1u + ((hn + 1u) - ((root + 1u) << dd));
+            const float4* rp = cache + loc * 4u;
+            return NodeRec{rp[0], rp[1], rp[2], rp[3]};
+        },
+        has_map, qx, qy, qz, c);
+    WAVE_SYNC();  // every lane has read the cache before the next query reloads it
 }
 
 // ------------------------------------------------------- fast candidates --
@@ -2252,16 +2307,27 @@ __global__ __launch_bounds__(kBlock) void k_hshare(HsParams P) {
 #endif
 using BlockTile = TileLds<LIVO_EVAL_TILE_CELLS, LIVO_EVAL_TILE_PTS>;
 
-__device__ __forceinline__ void replay_query(const KnnParams& P, const HsJob& job, int i) {
-    float qx, qy, qz;
-    query_point(P, job.slot, reinterpret_cast<const float4*>(job.pts)[i], qx, qy, qz);
-    Cands c;
-    knn_exact(P.nodes, P.has_map, qx, qy, qz, c);
-    float od[kNN];
-    uint32_t on[kNN];
+// The flagged queries of one wave (amb), each replayed by the whole wave
+// (knn_exact_wave) with `cache` (4 KB of LDS) as its subtree cache.
+__device__ __forceinline__ void replay_wave(const KnnParams& P, const HsJob& job, int i, bool amb, float4* cache) {
+    unsigned long long m = __ballot(amb);
+    const int lane = (int)(threadIdx.x & 63u);
+    while (m) {  // wave-uniform
+        const int l = __ffsll((long long)m) - 1;
+        m &= m - 1ull;
+        const int il = __shfl(i, l);
+        float qx, qy, qz;
+        query_point(P, job.slot, reinterpret_cast<const float4*>(job.pts)[il], qx, qy, qz);
+        Cands c;
+        knn_exact_wave(P.nodes, P.n_nodes, P.has_map, qx, qy, qz, cache, c);
+        if (lane == l) {
+            float od[kNN];
+            uint32_t on[kNN];
 #pragma unroll
-    for (int k = 0; k < kNN; k++) { od[k] = c.d[k]; on[k] = c.node[k]; }
-    write_nnrec(job.nn + i, P.nodes, c.n, od, on, job.nn[i].flag | 0x100);
+            for (int k = 0; k < kNN; k++) { od[k] = c.d[k]; on[k] = c.node[k]; }
+            write_nnrec(job.nn + il, P.nodes, c.n, od, on, job.nn[il].flag | 0x100);
+        }
+    }
 }
 
 struct EvalParams {
@@ -2304,9 +2370,8 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
         } rs;
     } U;
     unsigned bjob, bx;
-    // scan j's blocks on one XCD (its L2) in every evaluation: the neighbour
-    // records and plane caches stay in the L2 that wrote them
-    xcd_block(P.nb, bjob, bx);
+    // the same block order in every evaluation: the plane caches stay in the L2 that wrote them
+    xcd_chunk_block(P.nb, P.xcd_chunk, bjob, bx);
     const HsJob job = P.jobs[bjob];
     IekfSlot* slot = job.slot;
     if (bx > 0 && (int)bx * kEvalBlock >= job.n) return;  // (an empty scan keeps one block: it solves)
@@ -2357,12 +2422,18 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
         }
         n_slots = visits;
         n_pts = npts;
-        if (amb) {
-            atomicAdd(P.replay_total, 1ull);
-            if (P.canon) canon_query(P, job, i);
-            else replay_query(P, job, i);
+        if (amb) atomicAdd(P.replay_total, 1ull);
+        if (P.canon) {  // (kernel parameter: uniform) the incremental map's exact resolution
+            if (amb) canon_query(P, job, i);
+            __syncthreads();  // the tile's LDS is reused by the solve
+        } else if (__syncthreads_or(amb)) {  // block-uniform: some query of this block is flagged
+            // the tile's LDS is free after the barrier: 4 KB per wave of subtree cache
+            static_assert(sizeof(U) >= (size_t)(kEvalBlock / 64) * (4u << kReplayLevels) * sizeof(float4),
+                          "replay caches do not fit the evaluation's LDS");
+            float4* cache = reinterpret_cast<float4*>(&U) + (threadIdx.x >> 6) * (4u << kReplayLevels);
+            replay_wave(P, job, i, amb, cache);
+            __syncthreads();  // the caches' LDS is reused by the solve
         }
-        __syncthreads();  // the tile's LDS is reused by the solve
         EVAL_MARK(2);
     }
     double acc[kRedUsed + 2];

@@ -1,21 +1,23 @@
 """One batch step's kernel timeline from a rocprofv3 --kernel-trace CSV.
 
-A step starts at a first-evaluation k-NN dispatch (k_knn_leaf<false> or
-k_knn_grid<false>); the window runs to the next such dispatch group.  Prints
+A step starts at a first-evaluation dispatch (k_iekf_eval<true>, or
+k_knn_leaf<false> / k_knn_grid<false> in the unfused builds); the window runs
+to the next such dispatch group.  Copies (__amd_rocclr_copyBuffer) are listed
+with the kernels.  Prints
 every dispatch in the window (queue, start offset, duration, name) and a
 per-kernel-name summary of busy time, so launch gaps and the critical path
 of the stream groups are visible.
-usage: python tools/kt_timeline.py <kernel_trace.csv> [step_index=-3] [groups=4]
+usage: python tools/kt_timeline.py <kernel_trace.csv> [step_index=-3] [groups=1]
 """
 import csv
 import sys
 
 
-def main(path, step="-3", groups="4"):
+def main(path, step="-3", groups="1"):
     step, groups = int(step), int(groups)
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    firsts = [r for r in rows if "<false>" in r["Kernel_Name"] and "k_knn_" in r["Kernel_Name"]
-              and "replay" not in r["Kernel_Name"]]
+    firsts = [r for r in rows if "k_iekf_eval<true>" in r["Kernel_Name"]] or \
+        [r for r in rows if "<false>" in r["Kernel_Name"] and "k_knn_" in r["Kernel_Name"] and "replay" not in r["Kernel_Name"]]
     starts = [int(r["Start_Timestamp"]) for r in firsts[::groups]]
     t0 = starts[step]
     t1 = starts[step + 1] if step + 1 < len(starts) and step != -1 else None
