@@ -180,6 +180,11 @@ struct livo_ctx {
     // batch resources
     int32_t slot_cap = 0;
     IekfSlot* d_slots = nullptr;
+    // LaserMapping batches: slots packed at kLmStride (the part before the IKFoM
+    // block) followed by the jobs, one contiguous staging area each way
+    char* h_lm = nullptr;
+    char* d_lm = nullptr;
+    size_t lm_cap = 0;
     IekfSlot* h_slots = nullptr;  // pinned
     HsJob* d_jobs = nullptr;
     HsJob* h_jobs = nullptr;      // pinned
@@ -244,6 +249,29 @@ static int ensure_slots(livo_ctx* c, int32_t n) {
     if (hipHostMalloc((void**)&c->h_slots, sizeof(IekfSlot) * cap, hipHostMallocDefault) != hipSuccess) return LIVO_E_OOM;
     if (hipHostMalloc((void**)&c->h_jobs, sizeof(HsJob) * cap, hipHostMallocDefault) != hipSuccess) return LIVO_E_OOM;
     c->slot_cap = cap;
+    return LIVO_OK;
+}
+
+// kLmStride-packed LaserMapping slots + jobs of a batch of n (host pinned and device).
+constexpr size_t kLmStride = (kSlotLmBytes + 255) & ~(size_t)255;
+static_assert(kLmStride % alignof(HsJob) == 0 && kLmStride % alignof(IekfSlot) == 0, "packed slot alignment");
+static int ensure_lm(livo_ctx* c, int32_t n) {
+    const size_t need = (size_t)n * (kLmStride + sizeof(HsJob));
+    if (need <= c->lm_cap) return LIVO_OK;
+    const size_t cap = std::max(need, (size_t)8 * (kLmStride + sizeof(HsJob)));
+    dev_free(c->d_lm);
+    if (c->h_lm) (void)hipHostFree(c->h_lm);
+    c->h_lm = nullptr;
+    c->lm_cap = 0;
+    if (hipMalloc((void**)&c->d_lm, cap) != hipSuccess) {
+        c->d_lm = nullptr;
+        return LIVO_E_OOM;
+    }
+    if (hipHostMalloc((void**)&c->h_lm, cap, hipHostMallocDefault) != hipSuccess) {
+        c->h_lm = nullptr;
+        return LIVO_E_OOM;
+    }
+    c->lm_cap = cap;
     return LIVO_OK;
 }
 
@@ -1092,8 +1120,10 @@ int livo_ctx_destroy(livo_ctx* c) {
     dev_free(c->d_replay_list);
     dev_free(c->d_slots);
     dev_free(c->d_jobs);
+    dev_free(c->d_lm);
     if (c->h_slots) (void)hipHostFree(c->h_slots);
     if (c->h_jobs) (void)hipHostFree(c->h_jobs);
+    if (c->h_lm) (void)hipHostFree(c->h_lm);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->events_ready) {
         for (auto& g : c->ev)
@@ -1676,19 +1706,31 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
         if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end()) return LIVO_E_INVALID;
     }
     if (set_device(c)) return LIVO_E_HIP;
-    int rc = ensure_slots(c, n);
+    const bool lm = model != kModelIkfom;
+    int rc = lm ? ensure_lm(c, n) : ensure_slots(c, n);
     if (rc) return rc;
+    // Slots and jobs: the IKFoM model uses whole slots (c->h_slots / d_slots);
+    // the LaserMapping model only the part before the IKFoM block, packed at
+    // kLmStride with the jobs behind them, so the batch crosses PCIe in one
+    // copy each way.  (A packed slot is addressed as an IekfSlot whose IKFoM
+    // block lies outside the buffer; the LaserMapping kernels never touch it.)
+    const size_t stride = lm ? kLmStride : sizeof(IekfSlot);
+    char* const hbase = lm ? c->h_lm : reinterpret_cast<char*>(c->h_slots);
+    char* const dbase = lm ? c->d_lm : reinterpret_cast<char*>(c->d_slots);
+    HsJob* const hjobs = lm ? reinterpret_cast<HsJob*>(c->h_lm + (size_t)n * kLmStride) : c->h_jobs;
+    HsJob* const djobs = lm ? reinterpret_cast<HsJob*>(c->d_lm + (size_t)n * kLmStride) : c->d_jobs;
+    auto hslot = [&](int32_t b) -> IekfSlot& { return *reinterpret_cast<IekfSlot*>(hbase + (size_t)b * stride); };
+    auto dslot = [&](int32_t b) { return reinterpret_cast<IekfSlot*>(dbase + (size_t)b * stride); };
     const int max_iter = c->params.max_iterations;
     int64_t total_n = 0;
     for (int32_t b = 0; b < n; b++) {
         ScanBuf* s = get_scan(c, ids[b]);
         if (model == kModelIkfom) {
-            init_slot_ik(c->h_slots[b], ik_states[b], max_iter);
+            init_slot_ik(hslot(b), ik_states[b], max_iter);
         } else {
-            init_slot(c->h_slots[b], states[b], priors ? priors[b] : states[b], max_iter,
-                      kSlotLmBytes);
+            init_slot(hslot(b), states[b], priors ? priors[b] : states[b], max_iter, kSlotLmBytes);
         }
-        fill_job(c->h_jobs[b], *s, c->d_slots + b);
+        fill_job(hjobs[b], *s, dslot(b));
         total_n += s->n;
     }
     rc = ensure_replay(c, total_n);
@@ -1705,11 +1747,13 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
         // the replay count of this batch only (every batch's replays add to it)
         HIP_TRY(hipMemsetAsync(c->d_replay_total, 0, 8, c->stream));
     }
-    // the LaserMapping model uses only the part of a slot before the IKFoM block
-    const size_t slot_w = model == kModelIkfom ? sizeof(IekfSlot) : kSlotLmBytes;
-    HIP_TRY(hipMemcpy2DAsync(c->d_slots, sizeof(IekfSlot), c->h_slots, sizeof(IekfSlot), slot_w, n,
-                             hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->d_jobs, c->h_jobs, sizeof(HsJob) * n, hipMemcpyHostToDevice, c->stream));
+    if (lm) {
+        HIP_TRY(hipMemcpyAsync(c->d_lm, c->h_lm, (size_t)n * (kLmStride + sizeof(HsJob)), hipMemcpyHostToDevice,
+                               c->stream));
+    } else {
+        HIP_TRY(hipMemcpyAsync(c->d_slots, c->h_slots, sizeof(IekfSlot) * n, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(c->d_jobs, c->h_jobs, sizeof(HsJob) * n, hipMemcpyHostToDevice, c->stream));
+    }
 
     // The batch in groups on separate streams: the latency-bound kernels of
     // one group (18x18 solve, tie replay, launch gaps) overlap the
@@ -1759,9 +1803,9 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
     KnnParams kp[kMaxGroups];
     for (int gi = 0; gi < ngroups; gi++) {
         hp[gi] = make_hs_params(c);
-        hp[gi].jobs = c->d_jobs + g[gi].first;
+        hp[gi].jobs = djobs + g[gi].first;
         kp[gi] = make_knn_params(c);
-        kp[gi].jobs = c->d_jobs + g[gi].first;
+        kp[gi].jobs = djobs + g[gi].first;
         kp[gi].replay_count = c->d_replay_count + gi;
         kp[gi].replay_list = c->d_replay_list + g[gi].off;
         // the iVox overflow pass of each group has its own scratch slices (groups run concurrently)
@@ -1796,8 +1840,8 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
     // each group copies its own slots back on its own stream (no cross-stream
     // join before the copy); the host then waits for every group's stream
     for (int gi = 0; gi < ngroups; gi++)
-        HIP_TRY(hipMemcpy2DAsync(c->h_slots + g[gi].first, sizeof(IekfSlot), c->d_slots + g[gi].first,
-                                 sizeof(IekfSlot), slot_w, g[gi].count, hipMemcpyDeviceToHost, g[gi].st));
+        HIP_TRY(hipMemcpyAsync(&hslot(g[gi].first), dslot(g[gi].first), stride * g[gi].count, hipMemcpyDeviceToHost,
+                               g[gi].st));
     unsigned long long replays = 0;
     if (full) {
         // the replay counter: every group's searches have run (joined into the main stream)
@@ -1813,7 +1857,7 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
     // latency was a visible part of the gap between two batches
     for (int gi = ngroups - 1; gi >= 0; gi--) HIP_TRY(stream_wait(g[gi].st));
     for (int32_t b = 0; b < n; b++) {
-        const IekfSlot& s = c->h_slots[b];
+        const IekfSlot& s = hslot(b);
         if (model == kModelIkfom) {
             ik_states[b] = s.ik.x;
             if (ik_stats) ik_stats[b] = s.ik.stats;
@@ -1846,7 +1890,7 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
                 }
                 t.eval_ms[e] = m;
                 int searched = 0;
-                for (int32_t b = 0; b < n; b++) searched += c->h_slots[b].eval_search[e] != 0;
+                for (int32_t b = 0; b < n; b++) searched += hslot(b).eval_search[e] != 0;
                 t.eval_searched[e] = searched;
                 if (e == 0) t.knn_ms = m;
                 else if (searched) t.rematch_knn_ms += m;
@@ -1875,11 +1919,11 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
             }
         // the first evaluation searches for every point of every scan
         for (int32_t b = 0; b < n; b++) {
-            t.knn_visits += (int64_t)c->h_slots[b].visits[0];
-            t.knn_points += (int64_t)c->h_slots[b].scanned[0];
+            t.knn_visits += (int64_t)hslot(b).visits[0];
+            t.knn_points += (int64_t)hslot(b).scanned[0];
             t.knn_queries += c->scans[ids[b]].n;
-            t.effct_points += model == kModelIkfom ? c->h_slots[b].ik.stats.effct_feat_num[0]
-                                                   : c->h_slots[b].stats.effct_feat_num[0];
+            t.effct_points += model == kModelIkfom ? hslot(b).ik.stats.effct_feat_num[0]
+                                                   : hslot(b).stats.effct_feat_num[0];
         }
         t.knn_replays = (int64_t)replays;
         c->last = t;

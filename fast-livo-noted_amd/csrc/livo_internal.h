@@ -194,7 +194,8 @@ struct IekfCtrl {
 
 constexpr int kIkDim = LIVO_IKFOM_DOF;  // 23
 constexpr int kIkFewRows = kIkDim - 1;  // below 23 effective points the gain is formed in measurement space
-constexpr int kIkCols = 96;             // doubles per IKFoM block partial (92 used)
+constexpr int kIkCols = 192;            // doubles per IKFoM block partial: 92 sums, then their 92 compensations
+constexpr int kIkCompOff = 96;          // offset of the compensation terms in a partial
 constexpr int kIkUsed = 92;             // 78 HTH upper-tri + 12 HTh + residual sum + count
 
 // IKFoM update state (esekfom.hpp:1619-1928): x_, x_propagated (its cov is

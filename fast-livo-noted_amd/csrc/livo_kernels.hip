@@ -2724,6 +2724,17 @@ __device__ void ik_solve(IekfSlot* slot, const HsJob& job, IkSolveLds& S, const 
     }
 }
 
+// Compensated (Neumaier) sum, as oracle/livo_oracle.cpp's CompSum: s + c is
+// the sum to ~1e-27 relative in any order, so the block partials merged here
+// round to the same doubles as the oracle's serial sum.  The IKFoM update's
+// converged steps cancel ~1e5-fold (dx = K_h + (K_x - I) dx_new), which would
+// show summation-order rounding of h_x^T h_x.
+__device__ __forceinline__ void comp_add(double& s, double& c, double x) {
+    const double t = s + x;
+    c += (fabs(s) >= fabs(x)) ? (s - t) + x : (x - t) + s;
+    s = t;
+}
+
 // IKFoM plane pass (origin_laserMapping.cpp:916-1048): 4 points per thread as
 // k_hshare; each point's 12-wide row [n, A, B, C], h = -pd2 goes to LDS and the
 // block's 92 sums (h_x^T h_x upper triangle, h_x^T h, residual sum, count) are
@@ -2746,7 +2757,7 @@ __global__ __launch_bounds__(kBlock) void k_hshare_ik(HsParams P) {
         oa = a;
         ob = a + t;
     }
-    double acc = 0.0;
+    double acc = 0.0, acc_c = 0.0;  // compensated
     __shared__ uint32_t wcnt[kBlock / 64];
     uint32_t bcnt = 0;  // effective rows of this block so far (point order)
     for (int rep = 0; rep < kPtsPerThread; rep++) {
@@ -2836,12 +2847,15 @@ __global__ __launch_bounds__(kBlock) void k_hshare_ik(HsParams P) {
                 if (tid < 78) v = q[oa] * q[ob];
                 else if (tid < 90) v = q[tid - 78] * q[12];
                 else v = q[tid == 90 ? 13 : 14];
-                acc += v;
+                comp_add(acc, acc_c, v);
             }
         }
         __syncthreads();
     }
-    if (tid < kIkUsed) job.partial[(size_t)blockIdx.x * kIkCols + tid] = acc;
+    if (tid < kIkUsed) {
+        job.partial[(size_t)blockIdx.x * kIkCols + tid] = acc;
+        job.partial[(size_t)blockIdx.x * kIkCols + kIkCompOff + tid] = acc_c;
+    }
     if (tid == 0) job.ikcnt[blockIdx.x] = bcnt < (uint32_t)kIkFewRows ? bcnt : (uint32_t)kIkFewRows + 1u;
 }
 
@@ -2856,19 +2870,27 @@ __global__ __launch_bounds__(64) void k_solve_ik(HsParams P) {
     if (P.replay_count && blockIdx.x == 0 && lane == 0) *P.replay_count = 0u;
     if (slot->ctrl.stop) return;
     for (int c = lane; c < kIkCols; c += 64) {
-        double acc8[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) acc8[k] = 0.0;
+        // the blocks' compensated partials merged in block order (order-free to ~1e-27)
+        double sc = 0.0, cc = 0.0;
         if (c < kIkUsed) {
             const double* src = job.partial + c;
             int b = 0;
-            for (; b + 7 < job.nblk; b += 8) {
+            for (; b < job.nblk; b += 8) {
+                double v[8], w[8];
 #pragma unroll
-                for (int k = 0; k < 8; k++) acc8[k] += src[(size_t)(b + k) * kIkCols];
+                for (int k = 0; k < 8; k++) {
+                    const bool in = b + k < job.nblk;
+                    v[k] = in ? src[(size_t)(b + k) * kIkCols] : 0.0;
+                    w[k] = in ? src[(size_t)(b + k) * kIkCols + kIkCompOff] : 0.0;
+                }
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    comp_add(sc, cc, v[k]);
+                    cc += w[k];
+                }
             }
-            for (int k = 0; b + k < job.nblk; k++) acc8[k] += src[(size_t)(b + k) * kIkCols];
         }
-        S.sum[c] = ((acc8[0] + acc8[1]) + (acc8[2] + acc8[3])) + ((acc8[4] + acc8[5]) + (acc8[6] + acc8[7]));
+        S.sum[c] = sc + cc;
     }
     WAVE_SYNC();
     if (lane == 0) {

@@ -285,14 +285,17 @@ def cached_map(n_points: int) -> np.ndarray:
     return m
 
 
-def make_raw_scan(n_points: int, scan_id: int = 0, n_imu: int = 21, scene: Scene | None = None):
+def make_raw_scan(n_points: int, scan_id: int = 0, n_imu: int = 21, scene: Scene | None = None,
+                  still: bool = False):
     """A raw (not yet de-skewed) scan and the IMU poses of its frame.
 
     Points (n, 5) float32: x, y, z, intensity, curvature = offset time in ms
     (preprocess.cpp:346), sorted by time as the Livox handler delivers them.
     poses (n_imu, 22) float64: Pose6D rows (offset_time s, acc, gyr, vel, pos,
     rot), offset 0 first, one per 5 ms, a smooth synthetic motion.  Returns
-    (raw, poses, rot_end, pos_end).
+    (raw, poses, rot_end, pos_end).  still: the sensor does not move during
+    the frame (every pose is the scan's ground-truth pose), so the de-skew
+    leaves the points where make_scan put them.
     """
     body, R, p = make_scan(n_points, scan_id, scene)
     rng = np.random.default_rng(SEED_SCAN + 7919 * (scan_id + 1))
@@ -302,6 +305,8 @@ def make_raw_scan(n_points: int, scan_id: int = 0, n_imu: int = 21, scene: Scene
     w = rng.normal(0, 0.3, size=3)          # rad/s
     v = rng.normal(0, 1.0, size=3)          # m/s
     acc = rng.normal(0, 0.2, size=3)
+    if still:
+        w, v, acc = np.zeros(3), np.zeros(3), np.zeros(3)
     poses = np.zeros((n_imu, 22))
     for k in range(n_imu):
         t = 0.005 * k
@@ -315,6 +320,20 @@ def make_raw_scan(n_points: int, scan_id: int = 0, n_imu: int = 21, scene: Scene
     rot_end = R @ so3_exp(w * t_end)
     pos_end = p + v * t_end + 0.5 * acc * t_end * t_end
     return np.ascontiguousarray(raw), poses, rot_end, pos_end
+
+
+# BASELINE configs[4]: a 200k-point scan at filter_size_surf = 0.05, i.e. the
+# output of downSizeFilterSurf (laser_mapping.cpp:129-130,1111) on a raw frame
+# dense enough to leave about 200k points (the rosette's centre is denser than
+# a 5 cm voxel, so the frame has more raw points than that).
+CONFIG5_RAW_POINTS = 720_000
+CONFIG5_LEAF = 0.05
+
+
+def make_config5_frame(scan_id: int):
+    """Raw still frame of config 5 (make_raw_scan(CONFIG5_RAW_POINTS, still=True));
+    livo_scan_preprocess(leaf_size=CONFIG5_LEAF) turns it into the ~200k-point scan."""
+    return make_raw_scan(CONFIG5_RAW_POINTS, scan_id, still=True)
 
 
 # ---------------------------------------------------------------- VIO ----

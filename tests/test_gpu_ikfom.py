@@ -4,10 +4,10 @@ state_ikfom (use-ikfom.hpp:12-21), the legacy h-model
 (origin_laserMapping.cpp:916-1048) and update_iterated_dyn_share_modified
 (esekfom.hpp:1619-1928).  Bars: iteration / search / convergence control and
 effective-point counts exact; per-evaluation dx within 1e-5 of its own norm
-for every step that is not a converged near-zero step (|dx| < 1e-2 of the
-scan's largest), those within 1e-5 of the scan's largest dx (a converged step
-is a ~1e5-fold cancellation in this form, see _compare); covariance within
-1e-9 of the prior's norm.  Fewer than 23 effective points: the reference's
+for every step, the converged near-zero ones included (a converged step is a
+~1e5-fold cancellation in this form, see _compare: both sides form the
+h_x^T h_x sums as compensated sums, so their summation orders do not show);
+covariance within 1e-9 of the prior's norm.  Fewer than 23 effective points: the reference's
 measurement-space gain (:1701-1736) on both sides (the device collects the
 effective rows of such scans in point order, k_hshare_ik / k_solve_ik).
 """
@@ -38,18 +38,15 @@ def _compare(g, gs, r, rs, st0):
     assert gs["knn_passes"] == rs["knn_passes"]
     assert gs["converged"] == rs["converged"] and gs["t"] == rs["t"]
     assert gs["effct_feat_num"] == rs["effct_feat_num"]
-    # per-evaluation dx against the scan's update scale (the largest dx): a
-    # converged step (|dx| ~ 1e-6 of the first) is dx = K_h + (K_x - I) dx_new
-    # with K_x ~ I, where the last bits of the H^T H sums (summed in a different
-    # order than the oracle's serial loop) are amplified ~1e5-fold
-    scale = max(np.linalg.norm(d) for d in rs["dx"])
+    # per-evaluation dx against its own norm, every step: a converged step
+    # (|dx| ~ 1e-4 of the first) is dx = K_h + (K_x - I) dx_new with K_x ~ I,
+    # which amplifies the last bits of the h_x^T h_x sums ~1e5-fold; both sides
+    # form them as compensated sums (device partials vs the oracle's serial
+    # loop round to the same doubles), so the summation order does not show
     for e in range(gs["iterations"]):
         err = np.linalg.norm(gs["dx"][e] - rs["dx"][e])
         own = np.linalg.norm(rs["dx"][e])
-        if own >= 1e-2 * scale:  # a real step: relative to itself
-            assert err <= REL * own, (e, err / own)
-        else:  # a converged near-zero step
-            assert err <= REL * scale, e
+        assert err <= REL * max(own, 1e-300), (e, err / max(own, 1e-300))
     upd = np.linalg.norm(r["pos"] - st0["pos"])
     assert np.linalg.norm(g["pos"] - r["pos"]) <= REL * max(upd, 1e-12)
     for k in ("rot", "offset_R"):

@@ -301,6 +301,41 @@ def test_config5_10M_properties(built):
         assert _rel(sg["pos"] - st0["pos"], sr["pos"] - st0["pos"]) < REL_STATE
 
 
+@pytest.mark.slow
+def test_config5_batch_voxelgrid(built):
+    """Config 5 as the bench runs it: 8 raw still frames -> the device VoxelGrid
+    at leaf 0.05 (~200k points each) -> ONE batched update of the 8 scans on the
+    10M-point map (1.6M points: two stream groups by default).  Every scan
+    against the oracle's update of the same downsampled points: iterations,
+    k-NN passes, effective points exact, per-evaluation state delta within 1e-5."""
+    import livo_amd
+    import oracle
+    synth = _synth()
+    m = synth.cached_map(10_000_000)
+    frames = [synth.make_config5_frame(1000 + s) for s in range(8)]
+    states = [synth.make_state(1000 + s) for s in range(8)]
+    with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=4) as ctx:
+        ctx.map_build(m)
+        sids, downs = [], []
+        for raw, poses, Re, pe in frames:
+            sid, _, down = ctx.scan_preprocess(raw, poses, Re, pe, leaf_size=synth.CONFIG5_LEAF)
+            sids.append(sid)
+            downs.append(np.ascontiguousarray(down[:, :3]))
+        assert sum(len(d) for d in downs) > 1_200_000  # the two-group default
+        outs, stats = ctx.iekf_update_batch(sids, states)
+    assert all(150_000 < len(d) < 260_000 for d in downs)
+    tree = oracle.Tree(m)
+    for s in range(8):
+        sr, rs = tree.iekf_update(downs[s], states[s], R_LI=np.eye(3), t_LI=synth.T_LI, max_iter=4, threads=8)
+        gs = stats[s]
+        assert gs["iterations"] == rs["iterations"], s
+        assert gs["knn_passes"] == rs["knn_passes"], s
+        assert gs["effct_feat_num"] == rs["effct_feat_num"], s
+        for e in range(gs["iterations"]):
+            assert _rel(gs["solution"][e], rs["solution"][e]) < REL_STATE, (s, e)
+        assert _rel(outs[s]["pos"] - states[s]["pos"], sr["pos"] - states[s]["pos"]) < REL_STATE, s
+
+
 def test_iekf_duplicate_map_replays(built):
     """Every map point duplicated: every k-NN answer hinges on PointType_CMP ties, so the
     fast pass flags the queries and the exact replay (reference heap + visiting order)
