@@ -1243,7 +1243,7 @@ int livo_map_build(livo_ctx* c, const float* xyz, int64_t M, int64_t stride_byte
     // (a map of more than ~79M points keeps the cell walk: run positions are 31-bit)
     const bool vr = c->knn_kind == 2 && c->vruns && M * 27 + 8 < (int64_t)kRunPosLimit;
     rc = c->knn_kind >= 1 ? build_grid_map(xyz, M, stride_bytes, c->grid_cell, &gm, c->grid_ppc > 0.f ? c->grid_ppc
-                                                                                    : (vr ? kVrunPpc : 0.f))
+                                                                                    : (vr ? -kVrunPpc : 0.f))
                           : build_leaf_map(xyz, M, stride_bytes, c->leaf_size, &lm);
     if (rc) {
         free_host_map(&hm);
@@ -1769,12 +1769,14 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
     // the fused evaluation: search + replay + plane pass + solve in one launch
     const bool fused = c->fused && model == kModelLaserMapping && c->backend == LIVO_BACKEND_IKDTREE &&
                        c->knn_kind == 2;
-    // default groups: the fused evaluation runs a batch of up to ~1.2M points
-    // in one group (8 x 100k: 1 / 2 groups 12020 / 11883 updates/s), larger
-    // batches in two (8 x 200k on the 10M map: 2132 / 2316, profiles/r02_*)
+    // default: two groups (8 x 100k: 1 / 2 / 3 / 4 groups 15463 / 16566 /
+    // 15602 / 16365 updates/s, profiles/r03_ab_groups.txt), four beyond 1.2M
+    // points (8 x 200k on the 10M map: 4437 vs 3960 with two): one group's
+    // latency-bound evaluations (no search: launch, reduction, solve) and its
+    // replay tail overlap the other groups' searches
     int64_t batch_pts = 0;
     for (int32_t b = 0; b < n; b++) batch_pts += get_scan(c, ids[b])->n;
-    const int auto_groups = fused && batch_pts <= 1200000 ? 1 : 2;
+    const int auto_groups = batch_pts > 1200000 ? 4 : 2;
     const int ngroups = std::max(1, std::min<int>(c->groups > 0 ? c->groups : auto_groups, n));
     int64_t off = 0;
     for (int gi = 0; gi < ngroups; gi++) {

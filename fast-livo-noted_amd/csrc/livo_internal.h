@@ -115,11 +115,12 @@ struct HostGridMap {
     float h = 1.f;
     float cmax = 0.f;           // largest |coordinate| (bounds the float rounding of cell bounds)
 };
-// cell_h <= 0: chosen from the map (about ppc_target points per occupied cell, 20 if 0)
+// cell_h <= 0: chosen from the map (about ppc_target points per occupied cell, 20 if 0;
+// ppc_target < 0: -ppc_target x clamp((M / 1M)^0.3, 1, 4), the cell runs' sizing)
 int build_grid_map(const float* xyz, int64_t M, int64_t stride_bytes, float cell_h, HostGridMap* out,
                    float ppc_target = 0.f);
 constexpr int64_t kRunPosLimit = 0x7FFFFFFF;  // run entries a search can address (31-bit positions)
-constexpr float kVrunPpc = 20.0f;  // cell occupancy the cell runs are sized for (0.35 m cells on the config-2 map)
+constexpr float kVrunPpc = 20.0f;  // cell occupancy of the cell runs at 1M points (0.35 m cells on the config-2 map)
 void free_grid_map(HostGridMap* m);
 
 // Cell runs: the search structure of the batched IEKF k-NN on a static map.

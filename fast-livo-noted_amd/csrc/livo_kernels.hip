@@ -2348,6 +2348,9 @@ __device__ unsigned long long g_eval_prof[3][8];  // [no search / rematch / firs
         }                                                                                              \
     } while (0)
 #define EVAL_MARK_SYNC(k) do { __syncthreads(); EVAL_MARK(k); } while (0)
+// block timeline of the last batch: [evaluation][block] = (start, end) s_memtime of thread 0
+constexpr int kTlBlocks = 4096;
+__device__ unsigned long long g_eval_tl[LIVO_MAX_EVALS][kTlBlocks][2];
 #define EVAL_PROF_DECL unsigned long long prof_t = 0
 #else
 #define EVAL_MARK(k) do { } while (0)
@@ -2361,6 +2364,9 @@ template <bool FIRST>
 __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalParams E) {
     const KnnParams& P = E.k;
     EVAL_PROF_DECL;
+#ifdef LIVO_EVAL_PROF
+    const unsigned long long tl_start = __builtin_amdgcn_s_memtime();
+#endif
     // the search's LDS is dead (block barrier) before the reduction and solve use theirs
     __shared__ union {
         BlockTile tile;  // the cell walk's block tile (no vertex runs: an incremental map)
@@ -2382,11 +2388,18 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
     const HsPointIn pin = valid ? hshare_load(job, i, !FIRST) : HsPointIn{};
     if (slot->ctrl.stop) return;  // block-uniform
     const int search = FIRST ? 1 : slot->ctrl.search_en;
+#ifdef LIVO_EVAL_PROF
+    const int tl_e = min(slot->ctrl.n_evals, LIVO_MAX_EVALS - 1);
+#endif
     EVAL_MARK(0);
     unsigned n_slots = 0u, n_pts = 0u;  // hash slots and map points this thread's search read
     if (search) {
         LeafQuery q;
+#ifdef LIVO_AB_NOSEED  // A/B only: rematch searches without the previous neighbours' bound
+        lq_init<false>(q, P, slot, job, i, valid);
+#else
         lq_init<!FIRST>(q, P, slot, job, i, valid);
+#endif
         int c0 = 0, c1 = 0, c2 = 0, s0 = 1, s1 = 1, s2 = 1;
         if (valid) grid_cell(P, q, c0, c1, c2, s0, s1, s2);
         unsigned visits = 0, npts = 0;
@@ -2448,6 +2461,12 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
     EVAL_MARK_SYNC(3);
     hshare_reduce_solve<kEvalBlock, kRedUsed + 2>(E.h, job, slot, acc, nblk, bx, U.rs.R, U.rs.solve);
     EVAL_MARK(4);
+#ifdef LIVO_EVAL_PROF
+    if (threadIdx.x == 0 && blockIdx.x < (unsigned)kTlBlocks) {
+        g_eval_tl[tl_e][blockIdx.x][0] = tl_start;
+        g_eval_tl[tl_e][blockIdx.x][1] = __builtin_amdgcn_s_memtime();
+    }
+#endif
 }
 
 // Per-point persistent selection of the IKFoM h-model: point_selected_surf is a
@@ -3021,6 +3040,11 @@ int launch_knn_grid(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, 
 #ifdef LIVO_EVAL_PROF
 // Profiling builds only (not part of livo.h): per-phase block cycles of the
 // fused evaluation since the last call (tools/eval_prof.py).
+extern "C" int livo_debug_eval_timeline(unsigned long long* out, int64_t bytes) {  // LIVO_MAX_EVALS x kTlBlocks x 2
+    if (bytes != (int64_t)sizeof(g_eval_tl)) return LIVO_E_INVALID;
+    if (hipDeviceSynchronize() != hipSuccess) return LIVO_E_HIP;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_eval_tl), sizeof(g_eval_tl)) == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
 extern "C" int livo_debug_eval_prof(unsigned long long* out) {
     if (hipDeviceSynchronize() != hipSuccess) return LIVO_E_HIP;
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_eval_prof), sizeof(g_eval_prof)) != hipSuccess) return LIVO_E_HIP;

@@ -338,7 +338,12 @@ int build_grid_map(const float* xyz, int64_t M, int64_t stride_bytes, float cell
         // points per occupied cell grows about as h^2 on surface-like maps:
         // a few multiplicative steps towards 20 (measured on MI355X: 0.35-0.4 m
         // cells, 20-27 points each, searched fastest on the config-2 map)
-        const double target = ppc_target > 0.f ? (double)ppc_target : 20.0;
+        // ppc_target < 0: the cell runs' rule (livo_internal.h kVrunPpc): -ppc_target
+        // at 1M points, growing as M^0.3 (x2 at 10M: on the config-5 map 20 / 40 / 80
+        // points per cell gave 1339 / 4079 / 3960 updates/s, profiles/r03_c5_sweep_*)
+        double target = ppc_target > 0.f ? (double)ppc_target : 20.0;
+        if (ppc_target < 0.f)
+            target = -(double)ppc_target * std::min(4.0, std::max(1.0, std::pow((double)M / 1e6, 0.3)));
         for (int it = 0; it < 6 && M > 0; it++) {
             assign(h);
             const double ppc = (double)M / (double)std::max<int64_t>(occupied(), 1);

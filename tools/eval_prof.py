@@ -1,7 +1,7 @@
 """Per-phase block time of the fused evaluation kernel (k_iekf_eval) on the bench's batch.
 
 Build the profiling variant first:  python tools/ab_build.py evprof -DLIVO_EVAL_PROF
-then on the GPU box:  LIVO_LIB=fast-livo-noted_amd/lib/variants/evprof.so python tools/eval_prof.py
+then on the GPU box:  LIVO_LIB=fast-livo-noted_amd/lib/variants/evprof.so python tools/eval_prof.py [--config5]
 Phases (thread 0 of each block, s_memtime cycles): 1 build_tile, 2 search + tie replay,
 3 plane pass (hshare_point), 4 block reduction + ticket (+ the last block's solve).
 """
@@ -16,11 +16,19 @@ from livo_amd import synth  # noqa: E402
 
 
 def main():
-    m = synth.cached_map(1_000_000)
+    config5 = "--config5" in sys.argv  # 10M map, the bench's VoxelGrid scans
+    m = synth.cached_map(10_000_000 if config5 else 1_000_000)
     with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=4) as ctx:
         ctx.map_build(m)
-        sids = [ctx.scan_upload(synth.make_scan(100_000, s)[0]) for s in range(8)]
-        st0 = [synth.make_state(s) for s in range(8)]
+        if config5:
+            sids = []
+            for s in range(8):
+                raw, poses, Re, pe = synth.make_config5_frame(1000 + s)
+                sids.append(ctx.scan_preprocess(raw, poses, Re, pe, leaf_size=synth.CONFIG5_LEAF)[0])
+            st0 = [synth.make_state(1000 + s) for s in range(8)]
+        else:
+            sids = [ctx.scan_upload(synth.make_scan(100_000, s)[0]) for s in range(8)]
+            st0 = [synth.make_state(s) for s in range(8)]
         L = ctx._L
         L.livo_debug_eval_prof.argtypes = [C.c_void_p]
         buf = (C.c_ulonglong * 24)()
