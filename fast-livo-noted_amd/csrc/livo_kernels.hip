@@ -28,6 +28,8 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <utility>
+
 #include "livo_internal.h"
 #include "device_common.h"
 #include "device_linalg.h"
@@ -2048,10 +2050,62 @@ __device__ __forceinline__ HsPointIn hshare_load(const HsJob& job, int i, bool c
     in.plane = cached ? reinterpret_cast<const float4*>(job.plane)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
     return in;
 }
-template <int NU>
+// One point's contribution to the h_share sums: its Jacobian row H, the
+// residual term err = -pd2 and |pd2|; all zero unless the point is kept.  The
+// sums' columns are formed from it where they are reduced (hs_col), so the 29
+// double terms are never live in registers at once.
+struct HsRow {
+    double H[6];
+    double err;
+    float apd;
+    bool keep;
+};
+__device__ __forceinline__ void hs_row_clear(HsRow& w) {
+#pragma unroll
+    for (int k = 0; k < 6; k++) w.H[k] = 0.0;
+    w.err = 0.0;
+    w.apd = 0.0f;
+    w.keep = false;
+}
+// Column j (0..kRedUsed-1) of the sums for one point: 21 HTH upper-triangle
+// terms (H[r] / R) * H[c], 6 HTL terms (H[r] / R) * err, |pd2|, 1.  Each is
+// 0.0 + term, the value a zeroed accumulator holds after one point.
+template <int J>
+__device__ __forceinline__ double hs_col(const HsRow& w, double inv_r) {
+    if constexpr (J < 21) {
+        constexpr int r = J < 6 ? 0 : J < 11 ? 1 : J < 15 ? 2 : J < 18 ? 3 : J < 20 ? 4 : 5;
+        constexpr int base = r * 6 - (r * (r - 1)) / 2;
+        constexpr int c = r + (J - base);
+        return w.keep ? 0.0 + (w.H[r] * inv_r) * w.H[c] : 0.0;
+    } else if constexpr (J < 27) {
+        return w.keep ? 0.0 + (w.H[J - 21] * inv_r) * w.err : 0.0;
+    } else if constexpr (J == 27) {
+        return w.keep ? 0.0 + (double)w.apd : 0.0;
+    } else {
+        return w.keep ? 0.0 + 1.0 : 0.0;
+    }
+}
+// acc[j] += column j (the unfused plane pass: several points per thread)
+template <int J = 0>
+__device__ __forceinline__ void hs_accumulate(double (&acc)[kRedUsed], const HsRow& w, double inv_r) {
+    if constexpr (J < kRedUsed) {
+        if constexpr (J < 21) {
+            constexpr int r = J < 6 ? 0 : J < 11 ? 1 : J < 15 ? 2 : J < 18 ? 3 : J < 20 ? 4 : 5;
+            constexpr int base = r * 6 - (r * (r - 1)) / 2;
+            constexpr int c = r + (J - base);
+            if (w.keep) acc[J] += (w.H[r] * inv_r) * w.H[c];
+        } else if constexpr (J < 27) {
+            if (w.keep) acc[J] += (w.H[J - 21] * inv_r) * w.err;
+        } else if constexpr (J == 27) {
+            if (w.keep) acc[J] += (double)w.apd;
+        } else {
+            if (w.keep) acc[J] += 1.0;
+        }
+        hs_accumulate<J + 1>(acc, w, inv_r);
+    }
+}
 __device__ __forceinline__ void hshare_point(const HsParams& P, const HsJob& job, const livo_state& S, int i,
-                                             int search, double (&acc)[NU], const HsPointIn& in) {
-    static_assert(NU >= kRedUsed, "h_share sums");
+                                             int search, HsRow& w, const HsPointIn& in) {
             const float4 pb = in.pb;
             const double* R = S.rot;
             float wx, wy, wz;
@@ -2132,18 +2186,11 @@ __device__ __forceinline__ void hshare_point(const HsParams& P, const HsJob& job
                 H[1] = (M[3] * n0 + M[4] * n1) + M[5] * n2;
                 H[2] = (M[6] * n0 + M[7] * n1) + M[8] * n2;
                 H[3] = n0; H[4] = n1; H[5] = n2;
-                const double err = -(double)pd2;
-                int q = 0;
-    #pragma unroll
-                for (int r = 0; r < 6; r++) {
-                    const double hs = H[r] * P.inv_r;
-    #pragma unroll
-                    for (int cI = r; cI < 6; cI++) acc[q++] += hs * H[cI];
-                }
-    #pragma unroll
-                for (int r = 0; r < 6; r++) acc[21 + r] += (H[r] * P.inv_r) * err;
-                acc[27] += (double)fabsf(pd2);
-                acc[28] += 1.0;
+#pragma unroll
+                for (int r = 0; r < 6; r++) w.H[r] = H[r];
+                w.err = -(double)pd2;
+                w.apd = fabsf(pd2);
+                w.keep = true;
             }
 }
 
@@ -2161,20 +2208,27 @@ struct HsReduceLds {
 // sums instead of per-wave device atomics on two addresses per scan (those
 // serialise across the XCDs); the last block adds them to slot->visits /
 // scanned of this evaluation.
-template <int NT, int NU = kRedUsed>
+// col(std::integral_constant<int, j>) gives this thread's value of column j:
+// each column is formed, row-summed and stored in turn.
+template <class Col, int... J>
+__device__ __forceinline__ void hs_row_sums(const Col& col, HsReduceLds& R, int tid, std::integer_sequence<int, J...>) {
+    auto one = [&](auto jc) __attribute__((always_inline)) {
+        constexpr int j = decltype(jc)::value;
+        const double v = row_sum16(col(jc));
+        if ((tid & 15) == 0) R.red[(tid >> 4) * kRedCols + j] = v;
+    };
+    (one(std::integral_constant<int, J>{}), ...);
+}
+template <int NT, int NU = kRedUsed, class Col>
 __device__ __forceinline__ void hshare_reduce_solve(const HsParams& P, const HsJob& job, IekfSlot* slot,
-                                                    double (&acc)[NU], int nblk, unsigned blk, HsReduceLds& R,
+                                                    const Col& col, int nblk, unsigned blk, HsReduceLds& R,
                                                     SolveLds& L) {
     static_assert(NU == kRedUsed || NU == kRedUsed + 2, "h_share sums (+ search counts)");
     const int tid = threadIdx.x;
     constexpr int NR = NT / 16;  // 16-lane rows of the block
     static_assert(NR <= kRedRows, "HsReduceLds row partials");
     constexpr int NRM = NR > 16 ? NR : 16;  // rows of the fixed pairwise tree (16 for NT <= 256)
-#pragma unroll
-    for (int j = 0; j < NU; j++) {
-        const double v = row_sum16(acc[j]);
-        if ((tid & 15) == 0) R.red[(tid >> 4) * kRedCols + j] = v;
-    }
+    hs_row_sums(col, R, tid, std::make_integer_sequence<int, NU>{});
     __syncthreads();
     // Wave 0 stores the block partial write-through (sc1) and, once the store
     // has drained, takes the scan's ticket; the last block of the scan then
@@ -2278,9 +2332,15 @@ __global__ __launch_bounds__(kBlock) void k_hshare(HsParams P) {
     for (int j = 0; j < kRedUsed; j++) acc[j] = 0.0;
     for (int rep = 0; rep < kPtsPerThread; rep++) {  // points of this block: strided for coalescing
         const int i = (blockIdx.x * kPtsPerThread + rep) * kBlock + threadIdx.x;
-        if (i < job.n) hshare_point(P, job, S, i, search, acc, hshare_load(job, i, !search));
+        if (i < job.n) {
+            HsRow w;
+            hs_row_clear(w);
+            hshare_point(P, job, S, i, search, w, hshare_load(job, i, !search));
+            hs_accumulate(acc, w, P.inv_r);
+        }
     }
-    hshare_reduce_solve<kBlock>(P, job, slot, acc, job.nblk, blockIdx.x, R, L);
+    hshare_reduce_solve<kBlock>(P, job, slot, [&](auto jc) { return acc[decltype(jc)::value]; }, job.nblk,
+                                blockIdx.x, R, L);
 }
 
 // ================================================ fused evaluation =======
@@ -2449,17 +2509,22 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
         }
         EVAL_MARK(2);
     }
-    double acc[kRedUsed + 2];
-#pragma unroll
-    for (int j = 0; j < kRedUsed; j++) acc[j] = 0.0;
-    acc[kRedUsed] = (double)n_slots;  // the search's counts ride in the block partials
-    acc[kRedUsed + 1] = (double)n_pts;
+    HsRow w;
+    hs_row_clear(w);
     const int nblk = max(1, (job.n + kEvalBlock - 1) / kEvalBlock);
     if (valid) {
-        hshare_point(E.h, job, slot->state, i, search, acc, pin);
+        hshare_point(E.h, job, slot->state, i, search, w, pin);
     }
     EVAL_MARK_SYNC(3);
-    hshare_reduce_solve<kEvalBlock, kRedUsed + 2>(E.h, job, slot, acc, nblk, bx, U.rs.R, U.rs.solve);
+    const double inv_r = E.h.inv_r;
+    // the sums' columns, then the search's counts (they ride in the block partials)
+    auto col = [&](auto jc) -> double {
+        constexpr int j = decltype(jc)::value;
+        if constexpr (j < kRedUsed) return hs_col<j>(w, inv_r);
+        else if constexpr (j == kRedUsed) return (double)n_slots;
+        else return (double)n_pts;
+    };
+    hshare_reduce_solve<kEvalBlock, kRedUsed + 2>(E.h, job, slot, col, nblk, bx, U.rs.R, U.rs.solve);
     EVAL_MARK(4);
 #ifdef LIVO_EVAL_PROF
     if (threadIdx.x == 0 && blockIdx.x < (unsigned)kTlBlocks) {
