@@ -8,7 +8,10 @@ laser_mapping.cpp:171-238 with max_iteration = 4 (k-NN + plane fit + Jacobian
 device).  A step = one batched pass over --batch independent scans per GPU
 (the scan farm of config 4, §8e: 64 scans over 8 GPUs = 8 per GPU); value =
 scan updates per second over the whole job, with scans and map already
-resident in HBM when the timed region starts.
+resident in HBM when the timed region starts.  The farm keeps two batches in
+flight per GPU (livo_iekf_update_batch_submit / _wait over two alternating
+sets of scans): while the host collects one batch the device already runs the
+next.  `sync_value` is the same steps one synchronous batch at a time.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
@@ -147,6 +150,9 @@ def ref_calibration() -> dict:
         return {"ref_calibration_ratio": None, "ref_calibration_note": "tests/golden/knn_calibration.json missing"}
 
 
+SET2_SEED = 100_000  # synth scan seeds of the second set of scans (pipelined farm)
+
+
 # ------------------------------------------------------------------- PMC ----
 PMC_PASSES = (("FETCH_SIZE",), ("WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"),
               ("SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_BUSY_CYCLES"))
@@ -221,6 +227,11 @@ def main():
     scan_ids = [rank * a.batch + j for j in range(a.batch)]
     scans = [synth.make_scan(a.scan_points, s)[0] for s in scan_ids]
     st0 = [synth.make_state(s) for s in scan_ids]
+    # a second set of scans: the pipelined farm alternates two batches in flight,
+    # and a scan belongs to one of them at a time
+    scan_ids2 = [SET2_SEED + rank * a.batch + j for j in range(a.batch)]
+    scans2 = [synth.make_scan(a.scan_points, s)[0] for s in scan_ids2]
+    st02 = [synth.make_state(s) for s in scan_ids2]
     kind = os.environ.get("LIVO_KNN_KIND", "tile")
     fused = kind == "tile" and os.environ.get("LIVO_FUSED", "1") != "0"
     unit_kernel = {"leaf": "k_knn_leaf<false", "grid": "k_knn_grid<false, false>"}.get(
@@ -258,49 +269,82 @@ def main():
     ctx.map_build(m)
     map_build_s = time.time() - t
     sids = [ctx.scan_upload(s) for s in scans]
+    sids2 = [ctx.scan_upload(s) for s in scans2]
     # V_ref: nodes the reference traversal visits for the first search of these
     # scans (the reference-order pass k_knn_pass, outside the timed region):
     # the reference-equivalent pricing of SURVEY.md §8d
     v_ref = sum(ctx.h_share(sid, s, search_en=True)["visits"] for sid, s in zip(sids, st0))
     init = (livo_amd.State * a.batch)(*[livo_amd.state_to_c(s) for s in st0])
+    init2 = (livo_amd.State * a.batch)(*[livo_amd.state_to_c(s) for s in st02])
     work = (livo_amd.State * a.batch)()
     nbytes = C.sizeof(init)
 
     def step():
+        """One synchronous batch (livo_iekf_update_batch): the profiled legs."""
         C.memmove(work, init, nbytes)  # every step restarts the same scans from their priors
         _, stats = ctx.iekf_update_batch(sids, work, raw=True)
         return stats
 
+    # The farm's steady state: each step submits one batch of a.batch scans
+    # (livo_iekf_update_batch_submit) and collects the batch submitted two steps
+    # earlier, so the device always holds the next batch while the host collects
+    # one; the two sets of scans alternate.  Every submitted batch is collected
+    # before the clock stops.
+    sets = ((sids, init), (sids2, init2))
+    outs = [((livo_amd.State * a.batch)(), (livo_amd.IterStats * a.batch)()) for _ in range(2)]
+
+    def pipeline(nsteps, counters=None):
+        pending = []
+        for k in range(nsteps):
+            if len(pending) == livo_amd.MAX_INFLIGHT:
+                t, j = pending.pop(0)
+                _, st = ctx.iekf_update_batch_wait(t, a.batch, *outs[j])
+                if counters is not None:
+                    counters.add_stats(st)
+            j = k % 2
+            pending.append((ctx.iekf_update_batch_submit(sets[j][0], sets[j][1]), j))
+        for t, j in pending:
+            _, st = ctx.iekf_update_batch_wait(t, a.batch, *outs[j])
+            if counters is not None:
+                counters.add_stats(st)
+
+    pipeline(max(a.warmup, 2))
     for _ in range(a.warmup):
         step()
     first_stats = [livo_amd.stats_from_c(s) for s in step()]
     first_states = [livo_amd.state_from_c(s) for s in work]
 
     counters = farm.Counters()
-    # level 1: HIP events around the batch's first-evaluation k-NN only (the
-    # roofline unit); the per-stage breakdown (level 2) costs ~10% and is taken
-    # from extra untimed steps below
-    ctx.set_profiling(1)
-    knn_ms = 0.0
-    knn_launches = knn_visits = knn_points = knn_queries = replays = 0
     sync()
     barrier()
     sync()
     t0 = time.perf_counter()
+    pipeline(a.steps, counters)
+    sync()
+    barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+
+    # The same steps one synchronous batch at a time (the host waits for each
+    # batch before the next is queued), untimed for the headline and reported
+    # as sync_value; level-1 profiling: HIP events around the batch's
+    # first-evaluation launch only (the roofline unit).  The per-stage
+    # breakdown (level 2) costs ~10% and is taken from extra steps below.
+    ctx.set_profiling(1)
+    knn_ms = 0.0
+    knn_launches = knn_visits = knn_points = knn_queries = replays = 0
+    sync()
+    t0s = time.perf_counter()
     for _ in range(a.steps):
-        stats = step()
-        counters.add_stats(stats)
+        step()
         tm = ctx.last_timings()
         knn_ms += tm["knn_ms"]
         knn_launches += tm["knn_launches"]
         knn_visits += tm["knn_visits"]
         knn_points += tm["knn_points"]
         knn_queries += tm["knn_queries"]
-        replays += tm["knn_replays"]  # (0 unless level 2)
     sync()
-    barrier()
-    sync()
-    elapsed = time.perf_counter() - t0
+    elapsed_sync = time.perf_counter() - t0s
     # per-stage device time (summed over the concurrent stream groups), untimed
     ctx.set_profiling(2)
     n_prof = 10
@@ -324,6 +368,7 @@ def main():
     ctx.set_profiling(0)
     counters.knn_visits, counters.knn_queries = knn_visits, knn_queries
     elapsed_max = farm.allreduce_max(elapsed, coll_dev)
+    elapsed_sync_max = farm.allreduce_max(elapsed_sync, coll_dev)
     total = farm.allreduce_counters(counters, coll_dev)
 
     # roofline of the dominant kernel (rank-local): the first-evaluation k-NN of
@@ -379,6 +424,12 @@ def main():
                        "scans_per_step_per_gpu": a.batch, "parallelism": f"scan farm x{world}",
                        "collective": backend if world > 1 else None},
             "total_scans": total.scans,
+            "mode": ("pipelined farm: livo_iekf_update_batch_submit / _wait, two batches in flight per GPU "
+                     "(two alternating sets of scans), every batch collected inside the timed region"),
+            "sync_value": round(world * a.batch * a.steps / elapsed_sync_max, 3),
+            "sync_ms_per_step": round(elapsed_sync_max / a.steps * 1e3, 4),
+            "sync_note": ("the same steps with livo_iekf_update_batch (one batch at a time, the host waits for each); "
+                          "untimed for value"),
             "iekf_steps_per_s": round(total.evals / elapsed_max, 3),
             "knn_queries_per_s": round((total.knn_passes * a.scan_points) / elapsed_max, 1),
             "evals_per_scan": round(total.evals / max(total.scans, 1), 3),

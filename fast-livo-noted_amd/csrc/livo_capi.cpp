@@ -119,6 +119,26 @@ struct DynDev {
     livo_map_add_stats last{};
 };
 
+// One batch's staging and streams.  LaserMapping batches: slots packed at
+// kLmStride (the part before the IKFoM block) followed by the jobs, one
+// contiguous staging area each way.  Lane 0 borrows the context's streams;
+// the other lanes own theirs (created on first use).
+struct BatchLane {
+    char* h_lm = nullptr;
+    char* d_lm = nullptr;
+    size_t lm_cap = 0;
+    hipStream_t st[kMaxGroups] = {};
+    hipEvent_t fork = nullptr;
+    bool owned = false;  // streams / event created for this lane
+    bool busy = false;   // submitted, not yet collected
+    int32_t ticket = -1;
+    int32_t n = 0;
+    int model = 0;
+    int ngroups = 0;
+    int32_t gfirst[kMaxGroups] = {}, gcount[kMaxGroups] = {};
+    std::vector<int32_t> ids;
+};
+
 struct livo_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -180,11 +200,11 @@ struct livo_ctx {
     // batch resources
     int32_t slot_cap = 0;
     IekfSlot* d_slots = nullptr;
-    // LaserMapping batches: slots packed at kLmStride (the part before the IKFoM
-    // block) followed by the jobs, one contiguous staging area each way
-    char* h_lm = nullptr;
-    char* d_lm = nullptr;
-    size_t lm_cap = 0;
+    // batches in flight (livo_iekf_update_batch_submit): lane 0 also carries
+    // every synchronous batch
+    BatchLane lane[LIVO_MAX_INFLIGHT];
+    int32_t lane_gen = 0;  // tickets: generation * LIVO_MAX_INFLIGHT + lane
+    unsigned long long last_replays = 0;  // profiled batches: the replay counter read back
     IekfSlot* h_slots = nullptr;  // pinned
     HsJob* d_jobs = nullptr;
     HsJob* h_jobs = nullptr;      // pinned
@@ -255,24 +275,47 @@ static int ensure_slots(livo_ctx* c, int32_t n) {
 // kLmStride-packed LaserMapping slots + jobs of a batch of n (host pinned and device).
 constexpr size_t kLmStride = (kSlotLmBytes + 255) & ~(size_t)255;
 static_assert(kLmStride % alignof(HsJob) == 0 && kLmStride % alignof(IekfSlot) == 0, "packed slot alignment");
-static int ensure_lm(livo_ctx* c, int32_t n) {
+static int ensure_lm(BatchLane& B, int32_t n) {
     const size_t need = (size_t)n * (kLmStride + sizeof(HsJob));
-    if (need <= c->lm_cap) return LIVO_OK;
+    if (need <= B.lm_cap) return LIVO_OK;
     const size_t cap = std::max(need, (size_t)8 * (kLmStride + sizeof(HsJob)));
-    dev_free(c->d_lm);
-    if (c->h_lm) (void)hipHostFree(c->h_lm);
-    c->h_lm = nullptr;
-    c->lm_cap = 0;
-    if (hipMalloc((void**)&c->d_lm, cap) != hipSuccess) {
-        c->d_lm = nullptr;
+    dev_free(B.d_lm);
+    if (B.h_lm) (void)hipHostFree(B.h_lm);
+    B.h_lm = nullptr;
+    B.lm_cap = 0;
+    if (hipMalloc((void**)&B.d_lm, cap) != hipSuccess) {
+        B.d_lm = nullptr;
         return LIVO_E_OOM;
     }
-    if (hipHostMalloc((void**)&c->h_lm, cap, hipHostMallocDefault) != hipSuccess) {
-        c->h_lm = nullptr;
+    if (hipHostMalloc((void**)&B.h_lm, cap, hipHostMallocDefault) != hipSuccess) {
+        B.h_lm = nullptr;
         return LIVO_E_OOM;
     }
-    c->lm_cap = cap;
+    B.lm_cap = cap;
     return LIVO_OK;
+}
+
+// A lane's group streams: lane 0 the context's, the others their own.
+static int lane_streams(livo_ctx* c, int L) {
+    BatchLane& B = c->lane[L];
+    if (B.st[0]) return LIVO_OK;
+    if (L == 0) {
+        B.st[0] = c->stream;
+        for (int k = 0; k < kMaxGroups - 1; k++) B.st[k + 1] = c->xstream[k];
+        B.fork = c->fork;
+        return LIVO_OK;
+    }
+    B.owned = true;
+    for (int k = 0; k < kMaxGroups; k++)
+        if (hipStreamCreateWithFlags(&B.st[k], hipStreamNonBlocking) != hipSuccess) return LIVO_E_HIP;
+    if (hipEventCreateWithFlags(&B.fork, hipEventDisableTiming) != hipSuccess) return LIVO_E_HIP;
+    return LIVO_OK;
+}
+
+static bool any_inflight(const livo_ctx* c) {
+    for (const BatchLane& B : c->lane)
+        if (B.busy) return true;
+    return false;
 }
 
 static bool params_valid(const livo_params* p) {
@@ -1100,6 +1143,12 @@ int livo_ctx_destroy(livo_ctx* c) {
     if (!c) return LIVO_E_INVALID;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (BatchLane& B : c->lane) {  // batches never collected: let them finish
+        for (int k = 0; k < kMaxGroups && B.owned; k++)
+            if (B.st[k]) (void)hipStreamSynchronize(B.st[k]);
+    }
+    for (int k = 0; k < kMaxGroups - 1; k++)
+        if (c->xstream[k]) (void)hipStreamSynchronize(c->xstream[k]);
     for (auto& s : c->scans) free_scan_buf(s);
     for (auto& s : c->spare) free_scan_buf(s);
     if (c->up_tmp) (void)hipFree(c->up_tmp);
@@ -1120,10 +1169,17 @@ int livo_ctx_destroy(livo_ctx* c) {
     dev_free(c->d_replay_list);
     dev_free(c->d_slots);
     dev_free(c->d_jobs);
-    dev_free(c->d_lm);
     if (c->h_slots) (void)hipHostFree(c->h_slots);
     if (c->h_jobs) (void)hipHostFree(c->h_jobs);
-    if (c->h_lm) (void)hipHostFree(c->h_lm);
+    for (BatchLane& B : c->lane) {
+        dev_free(B.d_lm);
+        if (B.h_lm) (void)hipHostFree(B.h_lm);
+        if (B.owned) {
+            for (int k = 0; k < kMaxGroups; k++)
+                if (B.st[k]) (void)hipStreamDestroy(B.st[k]);
+            if (B.fork) (void)hipEventDestroy(B.fork);
+        }
+    }
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->events_ready) {
         for (auto& g : c->ev)
@@ -1145,12 +1201,14 @@ int livo_ctx_destroy(livo_ctx* c) {
 
 int livo_ctx_set_params(livo_ctx* c, const livo_params* p) {
     if (!c || !params_valid(p)) return LIVO_E_INVALID;
+    if (any_inflight(c)) return LIVO_E_BUSY;  // submitted batches are collected first
     c->params = *p;
     return LIVO_OK;
 }
 
 int livo_ctx_set_profiling(livo_ctx* c, int enable) {
     if (!c) return LIVO_E_INVALID;
+    if (any_inflight(c)) return LIVO_E_BUSY;  // submitted batches are collected first
     if (set_device(c)) return LIVO_E_HIP;
     if (enable && !c->events_ready) {
         for (auto& g : c->ev)
@@ -1234,6 +1292,7 @@ static int build_cell_runs(livo_ctx* c, int64_t M) {
 
 int livo_map_build(livo_ctx* c, const float* xyz, int64_t M, int64_t stride_bytes) {
     if (!c || M < 0 || (M > 0 && !xyz)) return LIVO_E_INVALID;
+    if (any_inflight(c)) return LIVO_E_BUSY;  // submitted batches are collected first
     if (set_device(c)) return LIVO_E_HIP;
     HostMap hm;
     int rc = build_host_map(xyz, M, stride_bytes, &hm);
@@ -1325,6 +1384,7 @@ int livo_map_get_info(livo_ctx* c, livo_map_info* out) {
 
 int livo_knn(livo_ctx* c, const float* q, int64_t n, int32_t k, int32_t* idx, float* d) {
     if (!c || n < 0 || k < 1 || k > kNN || (n > 0 && (!q || !idx || !d))) return LIVO_E_INVALID;
+    if (any_inflight(c)) return LIVO_E_BUSY;  // submitted batches are collected first
     if (!c->has_map) return LIVO_E_NOMAP;
     if (n == 0) return LIVO_OK;
     if (n > (int64_t)0x7FFFFFFF - kBlock) return LIVO_E_RANGE;
@@ -1529,6 +1589,7 @@ int livo_scan_upload(livo_ctx* c, const float* xyz, int64_t N, int64_t stride_by
 
 int livo_scan_release(livo_ctx* c, int32_t id) {
     if (!c) return LIVO_E_INVALID;
+    if (any_inflight(c)) return LIVO_E_BUSY;  // submitted batches are collected first
     if (id < 0 || id >= (int32_t)c->scans.size() || !c->scans[id].used) return LIVO_E_NOSCAN;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
@@ -1566,6 +1627,7 @@ int livo_scan_neighbors(livo_ctx* c, int32_t id, int32_t* idx, float* sqdist) {
 int livo_h_share(livo_ctx* c, int32_t id, const livo_state* state, int search_en, double HTH[81], double HTL[9],
                  int64_t* effct, const livo_point_out* out) {
     if (!c || !state || !HTH || !HTL) return LIVO_E_INVALID;
+    if (any_inflight(c)) return LIVO_E_BUSY;  // submitted batches are collected first
     ScanBuf* s = get_scan(c, id);
     if (!s) return LIVO_E_NOSCAN;
     if (!map_ready(c)) return LIVO_E_NOMAP;
@@ -1688,11 +1750,16 @@ int livo_h_share(livo_ctx* c, int32_t id, const livo_state* state, int search_en
 }
 
 // The batched iterated update of both formulations: the LaserMapping IEKF
-// (states/priors/stats, model 0) or the IKFoM update (ik_states/ik_stats, model 1).
-static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, livo_state* states,
-                        const livo_state* priors, livo_iter_stats* stats, livo_ikfom_state* ik_states,
-                        livo_ikfom_stats* ik_stats) {
+// (states/priors/stats, model 0) or the IKFoM update (ik_states/ik_stats, model 1),
+// in two halves over one batch lane: batch_enqueue puts the whole loop, and the
+// copies of the slots back, on the lane's streams; batch_collect waits for them
+// and unpacks the results.  Profiling (events, timings) on synchronous batches only.
+static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int model, const livo_state* states,
+                         const livo_state* priors, const livo_ikfom_state* ik_states, bool sync) {
     if (!c || n < 0 || (n > 0 && (!ids || (model == kModelIkfom ? !ik_states : !states)))) return LIVO_E_INVALID;
+    BatchLane& B = c->lane[L];
+    if (B.busy) return LIVO_E_BUSY;
+    B.n = 0;
     if (n == 0) return LIVO_OK;
     if (!map_ready(c)) return LIVO_E_NOMAP;
     if (model == kModelIkfom && c->backend != LIVO_BACKEND_IKDTREE) return LIVO_E_INVALID;  // ikd-Tree h-model only
@@ -1704,10 +1771,19 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
         std::vector<int32_t> sorted(ids, ids + n);
         std::sort(sorted.begin(), sorted.end());
         if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end()) return LIVO_E_INVALID;
+        // nor may a scan be in two batches in flight
+        for (int l = 0; l < LIVO_MAX_INFLIGHT; l++)
+            if (l != L && c->lane[l].busy)
+                for (int32_t id : c->lane[l].ids)
+                    if (std::binary_search(sorted.begin(), sorted.end(), id)) return LIVO_E_INVALID;
     }
     if (set_device(c)) return LIVO_E_HIP;
     const bool lm = model != kModelIkfom;
-    int rc = lm ? ensure_lm(c, n) : ensure_slots(c, n);
+    // the IKFoM model stages in the context's whole slots: synchronous batches on lane 0 only
+    if (!lm && (L != 0 || !sync)) return LIVO_E_INVALID;
+    int rc = lane_streams(c, L);
+    if (rc) return rc;
+    rc = lm ? ensure_lm(B, n) : ensure_slots(c, n);
     if (rc) return rc;
     // Slots and jobs: the IKFoM model uses whole slots (c->h_slots / d_slots);
     // the LaserMapping model only the part before the IKFoM block, packed at
@@ -1715,10 +1791,10 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
     // copy each way.  (A packed slot is addressed as an IekfSlot whose IKFoM
     // block lies outside the buffer; the LaserMapping kernels never touch it.)
     const size_t stride = lm ? kLmStride : sizeof(IekfSlot);
-    char* const hbase = lm ? c->h_lm : reinterpret_cast<char*>(c->h_slots);
-    char* const dbase = lm ? c->d_lm : reinterpret_cast<char*>(c->d_slots);
-    HsJob* const hjobs = lm ? reinterpret_cast<HsJob*>(c->h_lm + (size_t)n * kLmStride) : c->h_jobs;
-    HsJob* const djobs = lm ? reinterpret_cast<HsJob*>(c->d_lm + (size_t)n * kLmStride) : c->d_jobs;
+    char* const hbase = lm ? B.h_lm : reinterpret_cast<char*>(c->h_slots);
+    char* const dbase = lm ? B.d_lm : reinterpret_cast<char*>(c->d_slots);
+    HsJob* const hjobs = lm ? reinterpret_cast<HsJob*>(B.h_lm + (size_t)n * kLmStride) : c->h_jobs;
+    HsJob* const djobs = lm ? reinterpret_cast<HsJob*>(B.d_lm + (size_t)n * kLmStride) : c->d_jobs;
     auto hslot = [&](int32_t b) -> IekfSlot& { return *reinterpret_cast<IekfSlot*>(hbase + (size_t)b * stride); };
     auto dslot = [&](int32_t b) { return reinterpret_cast<IekfSlot*>(dbase + (size_t)b * stride); };
     const int max_iter = c->params.max_iterations;
@@ -1738,9 +1814,9 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
     if (model == kModelIkfom)  // its searches rewrite the neighbours without refitting the cached planes
         for (int32_t b = 0; b < n; b++) {
             ScanBuf* s = get_scan(c, ids[b]);
-            if (s->n > 0) HIP_TRY(hipMemsetAsync(s->pstate, 0, (size_t)s->n, c->stream));
+            if (s->n > 0) HIP_TRY(hipMemsetAsync(s->pstate, 0, (size_t)s->n, B.st[0]));
         }
-    const bool prof = c->profiling && c->events_ready;  // 1: first-search events only
+    const bool prof = sync && L == 0 && c->profiling && c->events_ready;  // 1: first-search events only
     const bool full = prof && c->profiling >= 2;         // 2: every evaluation, the batch span and the gap
     if (full) {
         HIP_TRY(hipEventRecord(c->b_start, c->stream));
@@ -1748,8 +1824,8 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
         HIP_TRY(hipMemsetAsync(c->d_replay_total, 0, 8, c->stream));
     }
     if (lm) {
-        HIP_TRY(hipMemcpyAsync(c->d_lm, c->h_lm, (size_t)n * (kLmStride + sizeof(HsJob)), hipMemcpyHostToDevice,
-                               c->stream));
+        HIP_TRY(hipMemcpyAsync(B.d_lm, B.h_lm, (size_t)n * (kLmStride + sizeof(HsJob)), hipMemcpyHostToDevice,
+                               B.st[0]));
     } else {
         HIP_TRY(hipMemcpyAsync(c->d_slots, c->h_slots, sizeof(IekfSlot) * n, hipMemcpyHostToDevice, c->stream));
         HIP_TRY(hipMemcpyAsync(c->d_jobs, c->h_jobs, sizeof(HsJob) * n, hipMemcpyHostToDevice, c->stream));
@@ -1785,7 +1861,7 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
         g[gi].max_nblk = 1;
         g[gi].max_n = 1;
         g[gi].off = off;
-        g[gi].st = gi == 0 ? c->stream : c->xstream[gi - 1];
+        g[gi].st = B.st[gi];
         for (int32_t b = g[gi].first; b < g[gi].first + g[gi].count; b++) {
             const ScanBuf* s = get_scan(c, ids[b]);
             g[gi].max_nblk = std::max(g[gi].max_nblk, (int)s->nblk);
@@ -1793,12 +1869,14 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
             off += s->n;
         }
     }
+    // the unfused passes' replay lists are per context: synchronous batches only
+    if (!fused && (L != 0 || !sync)) return LIVO_E_INVALID;
     if (!fused) HIP_TRY(hipMemsetAsync(c->d_replay_count, 0, sizeof(unsigned) * kMaxGroups, c->stream));
     // profiling: the batch's first search starts at ev[0][0], before the fork
     if (prof) HIP_TRY(hipEventRecord(c->ev[0][0], c->stream));
     if (ngroups > 1) {
-        HIP_TRY(hipEventRecord(c->fork, c->stream));
-        for (int gi = 1; gi < ngroups; gi++) HIP_TRY(hipStreamWaitEvent(g[gi].st, c->fork, 0));
+        HIP_TRY(hipEventRecord(B.fork, B.st[0]));
+        for (int gi = 1; gi < ngroups; gi++) HIP_TRY(hipStreamWaitEvent(g[gi].st, B.fork, 0));
     }
     const int evals = max_iter + 1;
     HsParams hp[kMaxGroups];
@@ -1844,17 +1922,53 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
     for (int gi = 0; gi < ngroups; gi++)
         HIP_TRY(hipMemcpyAsync(&hslot(g[gi].first), dslot(g[gi].first), stride * g[gi].count, hipMemcpyDeviceToHost,
                                g[gi].st));
-    unsigned long long replays = 0;
     if (full) {
         // the replay counter: every group's searches have run (joined into the main stream)
         for (int gi = 1; gi < ngroups; gi++) {
             HIP_TRY(hipEventRecord(c->xjoin[gi - 1], g[gi].st));
             HIP_TRY(hipStreamWaitEvent(c->stream, c->xjoin[gi - 1], 0));
         }
-        HIP_TRY(hipMemcpyAsync(&replays, c->d_replay_total, 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(&c->last_replays, c->d_replay_total, 8, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipMemsetAsync(c->d_replay_total, 0, 8, c->stream));
         HIP_TRY(hipEventRecord(c->b_end[c->b_par], c->stream));
     }
+    B.busy = true;
+    B.n = n;
+    B.model = model;
+    B.ngroups = ngroups;
+    B.ids.assign(ids, ids + n);
+    for (int gi = 0; gi < ngroups; gi++) {
+        B.gfirst[gi] = g[gi].first;
+        B.gcount[gi] = g[gi].count;
+    }
+    return LIVO_OK;
+}
+
+static int batch_collect(livo_ctx* c, int L, livo_state* states, livo_iter_stats* stats,
+                         livo_ikfom_state* ik_states, livo_ikfom_stats* ik_stats, bool sync) {
+    BatchLane& B = c->lane[L];
+    const int32_t n = B.n;
+    if (n == 0) return LIVO_OK;
+    if (!B.busy) return LIVO_E_INVALID;
+    const std::vector<int32_t> idv = std::move(B.ids);
+    B.ids.clear();
+    const int32_t* ids = idv.data();
+    const int model = B.model;
+    const int ngroups = B.ngroups;
+    const bool lm = model != kModelIkfom;
+    const size_t stride = lm ? kLmStride : sizeof(IekfSlot);
+    char* const hbase = lm ? B.h_lm : reinterpret_cast<char*>(c->h_slots);
+    auto hslot = [&](int32_t b) -> IekfSlot& { return *reinterpret_cast<IekfSlot*>(hbase + (size_t)b * stride); };
+    const bool fused = c->fused && model == kModelLaserMapping && c->backend == LIVO_BACKEND_IKDTREE &&
+                       c->knn_kind == 2;
+    const int evals = c->params.max_iterations + 1;
+    const bool prof = sync && L == 0 && c->profiling && c->events_ready;
+    const bool full = prof && c->profiling >= 2;
+    struct { hipStream_t st; } g[kMaxGroups];
+    for (int gi = 0; gi < ngroups; gi++) g[gi].st = B.st[gi];
+    const unsigned long long replays = c->last_replays;
+    B.busy = false;  // collected (or failed): the lane is free either way
+    B.n = 0;
     // wait by polling: the batch is short, and a blocking wait's wake-up
     // latency was a visible part of the gap between two batches
     for (int gi = ngroups - 1; gi >= 0; gi--) HIP_TRY(stream_wait(g[gi].st));
@@ -1933,9 +2047,64 @@ static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, l
     return LIVO_OK;
 }
 
+static int batch_update(livo_ctx* c, int32_t n, const int32_t* ids, int model, livo_state* states,
+                        const livo_state* priors, livo_iter_stats* stats, livo_ikfom_state* ik_states,
+                        livo_ikfom_stats* ik_stats) {
+    if (c && any_inflight(c)) return LIVO_E_BUSY;  // submitted batches are collected first
+    int rc = batch_enqueue(c, 0, n, ids, model, states, priors, ik_states, true);
+    if (rc) {
+        if (c) {  // an enqueue that failed half-way: let the lane's queued work finish
+            for (int k = 0; k < kMaxGroups && c->lane[0].st[k]; k++) (void)hipStreamSynchronize(c->lane[0].st[k]);
+            c->lane[0].busy = false;
+            c->lane[0].ids.clear();
+        }
+        return rc;
+    }
+    return batch_collect(c, 0, states, stats, ik_states, ik_stats, true);
+}
+
+
 int livo_iekf_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_state* states, const livo_state* priors,
                            livo_iter_stats* stats) {
     return batch_update(c, n, ids, kModelLaserMapping, states, priors, stats, nullptr, nullptr);
+}
+
+int livo_iekf_update_batch_submit(livo_ctx* c, int32_t n, const int32_t* ids, const livo_state* states,
+                                  const livo_state* priors, int32_t* ticket) {
+    if (!c || !ticket) return LIVO_E_INVALID;
+    int L = -1;
+    for (int l = 0; l < LIVO_MAX_INFLIGHT && L < 0; l++)
+        if (!c->lane[l].busy) L = l;
+    if (L < 0) return LIVO_E_BUSY;
+    int rc = batch_enqueue(c, L, n, ids, kModelLaserMapping, states, priors, nullptr, false);
+    if (rc) {
+        BatchLane& B = c->lane[L];
+        for (int k = 0; k < kMaxGroups && B.st[k]; k++) (void)hipStreamSynchronize(B.st[k]);
+        B.busy = false;
+        B.n = 0;
+        B.ids.clear();
+        return rc;
+    }
+    c->lane[L].busy = true;  // (an empty batch too: its ticket is waited for like any other)
+    c->lane_gen = (c->lane_gen + 1) & 0x3fffffff;
+    c->lane[L].ticket = c->lane_gen * LIVO_MAX_INFLIGHT + L;
+    *ticket = c->lane[L].ticket;
+    return LIVO_OK;
+}
+
+int livo_iekf_update_batch_wait(livo_ctx* c, int32_t ticket, livo_state* states, livo_iter_stats* stats) {
+    if (!c || ticket < 0) return LIVO_E_INVALID;
+    const int L = ticket % LIVO_MAX_INFLIGHT;
+    BatchLane& B = c->lane[L];
+    if (!B.busy || B.ticket != ticket) return LIVO_E_INVALID;
+    if (B.n > 0 && !states) return LIVO_E_INVALID;
+    if (set_device(c)) return LIVO_E_HIP;
+    B.ticket = -1;
+    if (B.n == 0) {
+        B.busy = false;
+        return LIVO_OK;
+    }
+    return batch_collect(c, L, states, stats, nullptr, nullptr, false);
 }
 
 int livo_iekf_update(livo_ctx* c, int32_t id, livo_state* state, const livo_state* prior, livo_iter_stats* stats) {
@@ -1955,6 +2124,7 @@ int livo_ikfom_update(livo_ctx* c, int32_t id, livo_ikfom_state* state, livo_ikf
 
 int livo_ctx_set_backend(livo_ctx* c, int backend) {
     if (!c || (backend != LIVO_BACKEND_IKDTREE && backend != LIVO_BACKEND_IVOX)) return LIVO_E_INVALID;
+    if (any_inflight(c)) return LIVO_E_BUSY;  // submitted batches are collected first
     if (backend != c->backend)
         for (auto& s : c->scans) s.searched = false;  // cached neighbours belong to the other map
     c->backend = backend;
@@ -1971,6 +2141,7 @@ int livo_ivox_params_default(livo_ivox_params* p) {
 
 int livo_ivox_init(livo_ctx* c, const livo_ivox_params* p) {
     if (!c) return LIVO_E_INVALID;
+    if (any_inflight(c)) return LIVO_E_BUSY;  // submitted batches are collected first
     livo_ivox_params prm;
     livo_ivox_params_default(&prm);
     if (p) prm = *p;
@@ -2002,6 +2173,7 @@ int livo_ivox_init(livo_ctx* c, const livo_ivox_params* p) {
 
 int livo_ivox_add_points(livo_ctx* c, const float* xyz, int64_t n, int64_t stride_bytes) {
     if (!c || n < 0 || (n > 0 && !xyz)) return LIVO_E_INVALID;
+    if (any_inflight(c)) return LIVO_E_BUSY;  // submitted batches are collected first
     if (stride_bytes == 0) stride_bytes = 3 * sizeof(float);
     if (stride_bytes < (int64_t)(3 * sizeof(float))) return LIVO_E_INVALID;
     if (!c->iv.ready) return LIVO_E_NOMAP;
@@ -2122,6 +2294,7 @@ int livo_ivox_dump(livo_ctx* c, float* xyz, int32_t* ids, int32_t* keys, int64_t
 int livo_map_incremental(livo_ctx* c, int32_t id, const livo_state* state, double fs, int ekf_inited, uint8_t* cat,
                          int64_t counts[2]) {
     if (!c || !state || !(fs > 0.0)) return LIVO_E_INVALID;
+    if (any_inflight(c)) return LIVO_E_BUSY;  // submitted batches are collected first
     if (c->backend != LIVO_BACKEND_IVOX) return map_incremental_ikd(c, id, state, fs, cat, counts);
     if (!c->iv.ready) return LIVO_E_NOMAP;
     ScanBuf* s = get_scan(c, id);
@@ -2186,6 +2359,7 @@ int livo_map_incremental(livo_ctx* c, int32_t id, const livo_state* state, doubl
 
 int livo_scan_inherit_neighbors(livo_ctx* c, int32_t dst, int32_t src) {
     if (!c) return LIVO_E_INVALID;
+    if (any_inflight(c)) return LIVO_E_BUSY;  // submitted batches are collected first
     ScanBuf* d = get_scan(c, dst);
     ScanBuf* s = get_scan(c, src);
     if (!d || !s) return LIVO_E_NOSCAN;
@@ -2485,6 +2659,7 @@ int livo_vio_update(livo_ctx* c, const livo_vio_params* p, const uint8_t* image,
 int livo_map_add_points(livo_ctx* c, const float* xyz, int64_t n, int64_t stride_bytes, float ds, int downsample_on,
                         livo_map_add_stats* stats) {
     if (!c || n < 0 || (n > 0 && !xyz)) return LIVO_E_INVALID;
+    if (any_inflight(c)) return LIVO_E_BUSY;  // submitted batches are collected first
     if (downsample_on && !(ds > 0.f && std::isfinite(ds))) return LIVO_E_INVALID;
     if (stride_bytes == 0) stride_bytes = 3 * sizeof(float);
     if (stride_bytes < (int64_t)(3 * sizeof(float))) return LIVO_E_INVALID;
@@ -2507,6 +2682,7 @@ int livo_map_add_points(livo_ctx* c, const float* xyz, int64_t n, int64_t stride
 
 int livo_map_delete_boxes(livo_ctx* c, const float* boxes, int64_t nb, int64_t* deleted) {
     if (!c || nb < 0 || (nb > 0 && !boxes)) return LIVO_E_INVALID;
+    if (any_inflight(c)) return LIVO_E_BUSY;  // submitted batches are collected first
     if (!c->has_map) return LIVO_E_NOMAP;
     if (set_device(c)) return LIVO_E_HIP;
     if (deleted) *deleted = 0;
@@ -2625,6 +2801,8 @@ int livo_sync(livo_ctx* c) {
     if (!c) return LIVO_E_INVALID;
     if (set_device(c)) return LIVO_E_HIP;
     HIP_TRY(hipStreamSynchronize(c->stream));
+    for (const BatchLane& B : c->lane)  // submitted batches run on their lanes' streams
+        for (int k = 0; k < kMaxGroups && B.st[k]; k++) HIP_TRY(hipStreamSynchronize(B.st[k]));
     return LIVO_OK;
 }
 

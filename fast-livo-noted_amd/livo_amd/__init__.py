@@ -31,7 +31,8 @@ MAX_EVALS = 16
 
 LIVO_OK = 0
 ERRORS = {-1: "LIVO_E_INVALID", -2: "LIVO_E_HIP", -3: "LIVO_E_NOMAP", -4: "LIVO_E_NOSCAN", -5: "LIVO_E_OOM",
-          -6: "LIVO_E_RANGE", -7: "LIVO_E_CAPACITY"}
+          -6: "LIVO_E_RANGE", -7: "LIVO_E_CAPACITY", -8: "LIVO_E_BUSY"}
+MAX_INFLIGHT = 2  # LIVO_MAX_INFLIGHT
 BACKEND_IKDTREE = 0  # -DUSE_ikdtree build (CMakeLists.txt:15)
 BACKEND_IVOX = 1     # the reference's default build: faster_lio::IVox
 
@@ -172,6 +173,8 @@ SIGNATURES = {
                                C.POINTER(PointOut)]),
     "livo_iekf_update": (C.c_int, [_P, C.c_int32, C.POINTER(State), C.POINTER(State), C.POINTER(IterStats)]),
     "livo_iekf_update_batch": (C.c_int, [_P, C.c_int32, _P, _P, _P, _P]),
+    "livo_iekf_update_batch_submit": (C.c_int, [_P, C.c_int32, _P, _P, _P, _P]),
+    "livo_iekf_update_batch_wait": (C.c_int, [_P, C.c_int32, _P, _P]),
     "livo_ikfom_update": (C.c_int, [_P, C.c_int32, C.POINTER(IkfomState), C.POINTER(IkfomStats)]),
     "livo_ikfom_update_batch": (C.c_int, [_P, C.c_int32, _P, _P, _P]),
     "livo_ctx_set_backend": (C.c_int, [_P, C.c_int]),
@@ -419,6 +422,43 @@ class Context:
                                               C.cast(prs, C.c_void_p) if prs is not None else None,
                                               C.cast(stats, C.c_void_p)))
         return [state_from_c(s) for s in sts], [stats_from_c(s) for s in stats]
+
+    def iekf_update_batch_submit(self, sids, states, priors=None) -> int:
+        """Enqueue a batched update and return its ticket (livo_iekf_update_batch_submit).
+        states / priors: dicts, or ctypes State arrays of at least len(sids) entries
+        (copied at the call); at most MAX_INFLIGHT batches are outstanding."""
+        n = len(sids)
+        ids = (C.c_int32 * n)(*sids)
+        if not isinstance(states, C.Array):
+            states = (State * n)(*[state_to_c(s) for s in states])
+        if priors is not None and not isinstance(priors, C.Array):
+            priors = (State * n)(*[state_to_c(s) for s in priors])
+        nb = n * C.sizeof(State)
+        if C.sizeof(states) < nb or (priors is not None and C.sizeof(priors) < nb):
+            raise ValueError(f"iekf_update_batch_submit: states/priors hold fewer than {n} State entries")
+        ticket = C.c_int32(-1)
+        _check("livo_iekf_update_batch_submit",
+               self._L.livo_iekf_update_batch_submit(self.h, n, C.addressof(ids), C.addressof(states),
+                                                     C.addressof(priors) if priors is not None else None,
+                                                     C.byref(ticket)))
+        return ticket.value
+
+    def iekf_update_batch_wait(self, ticket: int, n: int, out=None, stats=None):
+        """Collect a submitted batch of n scans (livo_iekf_update_batch_wait).  With out
+        (a ctypes State array of >= n entries) and stats (IterStats array or None) the
+        raw arrays are filled and returned; else lists of dicts."""
+        raw = out is not None
+        if out is None:
+            out = (State * max(n, 1))()
+            stats = (IterStats * max(n, 1))()
+        if C.sizeof(out) < n * C.sizeof(State) or (stats is not None and C.sizeof(stats) < n * C.sizeof(IterStats)):
+            raise ValueError(f"iekf_update_batch_wait: output arrays hold fewer than {n} entries")
+        _check("livo_iekf_update_batch_wait",
+               self._L.livo_iekf_update_batch_wait(self.h, ticket, C.addressof(out),
+                                                   C.addressof(stats) if stats is not None else None))
+        if raw:
+            return out, stats
+        return [state_from_c(out[b]) for b in range(n)], [stats_from_c(stats[b]) for b in range(n)]
 
     # ------------------------------------------------------------ IKFoM ----
     def ikfom_update(self, sid: int, state: dict):

@@ -64,7 +64,8 @@ enum {
     LIVO_E_NOSCAN = -4,    /* unknown / released scan id */
     LIVO_E_OOM = -5,       /* device allocation failed */
     LIVO_E_RANGE = -6,     /* size beyond the supported range */
-    LIVO_E_CAPACITY = -7   /* capacity exceeded (reserved) */
+    LIVO_E_CAPACITY = -7,  /* capacity exceeded (reserved) */
+    LIVO_E_BUSY = -8       /* batches in flight (livo_iekf_update_batch_submit) */
 };
 
 typedef struct livo_ctx livo_ctx;
@@ -205,6 +206,21 @@ int livo_iekf_update(livo_ctx* ctx, int32_t scan_id, livo_state* state, const li
  * belongs to one update at a time. */
 int livo_iekf_update_batch(livo_ctx* ctx, int32_t n, const int32_t* scan_ids, livo_state* states,
                            const livo_state* priors, livo_iter_stats* stats);
+
+/* The same batched update, split into enqueue and collect, so a scan farm keeps
+ * the next batch queued on the device while the host collects the last one
+ * (no replacement in the reference, which updates one scan per frame in
+ * LaserMapping::Run; this is the farm of SURVEY.md §8e).  submit copies
+ * states / priors (NULL: prior = state) at the call and returns a ticket;
+ * wait(ticket) blocks until that batch is done and writes its states and
+ * stats (may be NULL).  At most LIVO_MAX_INFLIGHT batches per context are
+ * submitted and not yet waited for (LIVO_E_BUSY beyond), and a scan may be in
+ * one of them only (LIVO_E_INVALID).  While a batch is in flight its scans
+ * may not be released, and the map may not be rebuilt or changed (LIVO_E_BUSY). */
+#define LIVO_MAX_INFLIGHT 2
+int livo_iekf_update_batch_submit(livo_ctx* ctx, int32_t n, const int32_t* scan_ids, const livo_state* states,
+                                  const livo_state* priors, int32_t* ticket);
+int livo_iekf_update_batch_wait(livo_ctx* ctx, int32_t ticket, livo_state* states, livo_iter_stats* stats);
 
 /* ------------------------------------------------------------------------
  * IKFoM formulation (the "solve in use-ikfom.hpp"):

@@ -60,7 +60,7 @@ def test_golden_fixture(built):
 @pytest.mark.slow
 def test_bench_headline_mode_parity(built):
     """8 x 100k scans, 1M map, one livo_iekf_update_batch in the default stream
-    grouping (one group at 800k points: the bench's step): per scan, the oracle's iterations, k-NN passes,
+    grouping (two groups at 800k points: the bench's step): per scan, the oracle's iterations, k-NN passes,
     effective points and per-evaluation state deltas."""
     import livo_amd
     import oracle
@@ -82,6 +82,70 @@ def test_bench_headline_mode_parity(built):
         for e in range(gs["iterations"]):
             assert _rel(gs["solution"][e], rs["solution"][e]) < REL_STATE, (s, e)
         assert _rel(outs[s]["pos"] - states[s]["pos"], sr["pos"] - states[s]["pos"]) < REL_STATE, s
+
+
+def _same_update(a, b):
+    import livo_amd
+    for k in ("rot", "pos", "vel", "bias_g", "bias_a", "gravity", "cov"):
+        assert np.array_equal(np.asarray(a[0][k]), np.asarray(b[0][k])), k
+    assert a[1]["iterations"] == b[1]["iterations"] and a[1]["effct_feat_num"] == b[1]["effct_feat_num"]
+    assert np.array_equal(np.asarray(a[1]["solution"]), np.asarray(b[1]["solution"]))
+
+
+def test_submit_wait_pipeline(built):
+    """livo_iekf_update_batch_submit / _wait (the bench's pipelined farm): two
+    batches in flight on their own lanes give bit for bit the synchronous
+    batch's states and stats, through several rounds of lane reuse; a third
+    submit is LIVO_E_BUSY, a scan in two batches in flight LIVO_E_INVALID, a
+    wrong ticket LIVO_E_INVALID, and the map / scans cannot change meanwhile."""
+    import livo_amd
+    from livo_amd import synth
+    m = synth.cached_map(1_000_000)
+    scans = [synth.make_scan(50_000, s)[0] for s in range(8)]
+    states = [synth.make_state(s) for s in range(8)]
+    with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=4) as ctx:
+        ctx.map_build(m)
+        sids = [ctx.scan_upload(b) for b in scans]
+        A, B = sids[:4], sids[4:]
+        ref = ctx.iekf_update_batch(sids, states)
+        ref = list(zip(*ref))
+        ta = ctx.iekf_update_batch_submit(A, states[:4])
+        tb = ctx.iekf_update_batch_submit(B, states[4:])
+        with pytest.raises(livo_amd.LivoError) as e:
+            ctx.iekf_update_batch_submit([sids[0]], states[:1])
+        assert e.value.code == -8  # LIVO_E_BUSY: both lanes in flight
+        with pytest.raises(livo_amd.LivoError) as e:
+            ctx.map_build(m[:1000])
+        assert e.value.code == -8
+        with pytest.raises(livo_amd.LivoError) as e:
+            ctx.scan_release(sids[0])
+        assert e.value.code == -8
+        with pytest.raises(livo_amd.LivoError) as e:
+            ctx.iekf_update_batch(A, states[:4])
+        assert e.value.code == -8
+        with pytest.raises(livo_amd.LivoError) as e:
+            ctx.iekf_update_batch_wait(tb + 2, 4)
+        assert e.value.code == -1
+        outs = {}
+        outs["a0"] = list(zip(*ctx.iekf_update_batch_wait(ta, 4)))
+        with pytest.raises(livo_amd.LivoError) as e:  # scan 4 is still in batch b
+            ctx.iekf_update_batch_submit([sids[0], sids[4]], states[:2])
+        assert e.value.code == -1
+        ta = ctx.iekf_update_batch_submit(A, states[:4])  # lane reuse while b runs
+        outs["b0"] = list(zip(*ctx.iekf_update_batch_wait(tb, 4)))
+        outs["a1"] = list(zip(*ctx.iekf_update_batch_wait(ta, 4)))
+        with pytest.raises(livo_amd.LivoError) as e:  # collected already
+            ctx.iekf_update_batch_wait(ta, 4)
+        assert e.value.code == -1
+        t0 = ctx.iekf_update_batch_submit([], [])  # an empty batch has a ticket too
+        ctx.iekf_update_batch_wait(t0, 0)
+        sync2 = list(zip(*ctx.iekf_update_batch(sids, states)))  # synchronous again afterwards
+    for k in range(4):
+        _same_update(outs["a0"][k], ref[k])
+        _same_update(outs["a1"][k], ref[k])
+        _same_update(outs["b0"][k], ref[4 + k])
+    for k in range(8):
+        _same_update(sync2[k], ref[k])
 
 
 def test_bench_two_ranks(built):
