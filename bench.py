@@ -227,11 +227,17 @@ def main():
     scan_ids = [rank * a.batch + j for j in range(a.batch)]
     scans = [synth.make_scan(a.scan_points, s)[0] for s in scan_ids]
     st0 = [synth.make_state(s) for s in scan_ids]
-    # a second set of scans: the pipelined farm alternates two batches in flight,
-    # and a scan belongs to one of them at a time
-    scan_ids2 = [SET2_SEED + rank * a.batch + j for j in range(a.batch)]
-    scans2 = [synth.make_scan(a.scan_points, s)[0] for s in scan_ids2]
-    st02 = [synth.make_state(s) for s in scan_ids2]
+    # a second set of resident scans: the pipelined farm alternates two batches
+    # in flight and a scan belongs to one of them at a time.  By default the set
+    # is a second upload of the same scans, so every step does the work of the
+    # synchronous step it is compared with (sync_value); LIVO_BENCH_SET2=seeds
+    # draws 8 other scans instead (other poses in the room: a different load)
+    if os.environ.get("LIVO_BENCH_SET2") == "seeds":
+        scan_ids2 = [SET2_SEED + rank * a.batch + j for j in range(a.batch)]
+        scans2 = [synth.make_scan(a.scan_points, s)[0] for s in scan_ids2]
+        st02 = [synth.make_state(s) for s in scan_ids2]
+    else:
+        scans2, st02 = scans, st0
     kind = os.environ.get("LIVO_KNN_KIND", "tile")
     fused = kind == "tile" and os.environ.get("LIVO_FUSED", "1") != "0"
     unit_kernel = {"leaf": "k_knn_leaf<false", "grid": "k_knn_grid<false, false>"}.get(
@@ -425,7 +431,10 @@ def main():
                        "collective": backend if world > 1 else None},
             "total_scans": total.scans,
             "mode": ("pipelined farm: livo_iekf_update_batch_submit / _wait, two batches in flight per GPU "
-                     "(two alternating sets of scans), every batch collected inside the timed region"),
+                     "(two alternating sets of resident scans, "
+                     + ("8 other scans" if os.environ.get("LIVO_BENCH_SET2") == "seeds" else
+                        "the second a second upload of the same 8") +
+                     "), every batch collected inside the timed region"),
             "sync_value": round(world * a.batch * a.steps / elapsed_sync_max, 3),
             "sync_ms_per_step": round(elapsed_sync_max / a.steps * 1e3, 4),
             "sync_note": ("the same steps with livo_iekf_update_batch (one batch at a time, the host waits for each); "

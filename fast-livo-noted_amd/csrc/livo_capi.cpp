@@ -126,10 +126,13 @@ struct DynDev {
 struct BatchLane {
     char* h_lm = nullptr;
     char* d_lm = nullptr;
+    char* h_lm_dev = nullptr;  // h_lm's device address (host-mapped), for the kernel copies
     size_t lm_cap = 0;
     hipStream_t st[kMaxGroups] = {};
     hipEvent_t fork = nullptr;
-    bool owned = false;  // streams / event created for this lane
+    hipEvent_t done[kMaxGroups] = {};  // each group's last operation (its slot copy back)
+    bool owned = false;       // streams created for this lane
+    bool owned_fork = false;  // fork event created for this lane
     bool busy = false;   // submitted, not yet collected
     int32_t ticket = -1;
     int32_t n = 0;
@@ -204,6 +207,10 @@ struct livo_ctx {
     // every synchronous batch
     BatchLane lane[LIVO_MAX_INFLIGHT];
     int32_t lane_gen = 0;  // tickets: generation * LIVO_MAX_INFLIGHT + lane
+    bool lane_own_streams = false;  // LIVO_LANE_STREAMS=own: lanes > 0 on streams of their own
+    bool lane_serial = true;        // LIVO_LANE_SERIAL=0: a queued batch's group 0 starts before the last batch ends
+    bool lane_zc = true;            // submitted batches: staging copies by kernel over host-mapped memory (LIVO_LANE_ZC)
+    int last_lane = -1;             // lane of the batch enqueued last
     unsigned long long last_replays = 0;  // profiled batches: the replay counter read back
     IekfSlot* h_slots = nullptr;  // pinned
     HsJob* d_jobs = nullptr;
@@ -241,6 +248,15 @@ static hipError_t stream_wait(hipStream_t st) {
     return hipStreamSynchronize(st);
 }
 
+// The same for an event (a batch's end when other work may queue behind it).
+static hipError_t event_wait(hipEvent_t ev) {
+    for (int k = 0; k < 200000; k++) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e != hipErrorNotReady) return e;
+    }
+    return hipEventSynchronize(ev);
+}
+
 static int set_device(livo_ctx* c) {
     return hipSetDevice(c->device) == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
@@ -275,10 +291,13 @@ static int ensure_slots(livo_ctx* c, int32_t n) {
 // kLmStride-packed LaserMapping slots + jobs of a batch of n (host pinned and device).
 constexpr size_t kLmStride = (kSlotLmBytes + 255) & ~(size_t)255;
 static_assert(kLmStride % alignof(HsJob) == 0 && kLmStride % alignof(IekfSlot) == 0, "packed slot alignment");
+static_assert(kLmStride % 16 == 0, "kernel staging copies move 16-B words");
+// bytes of a batch's packed staging area, rounded up to whole 16-B words
+static size_t lm_bytes(int32_t n) { return ((size_t)n * (kLmStride + sizeof(HsJob)) + 15) & ~(size_t)15; }
 static int ensure_lm(BatchLane& B, int32_t n) {
-    const size_t need = (size_t)n * (kLmStride + sizeof(HsJob));
+    const size_t need = lm_bytes(n);
     if (need <= B.lm_cap) return LIVO_OK;
-    const size_t cap = std::max(need, (size_t)8 * (kLmStride + sizeof(HsJob)));
+    const size_t cap = std::max(need, lm_bytes(8));
     dev_free(B.d_lm);
     if (B.h_lm) (void)hipHostFree(B.h_lm);
     B.h_lm = nullptr;
@@ -287,9 +306,15 @@ static int ensure_lm(BatchLane& B, int32_t n) {
         B.d_lm = nullptr;
         return LIVO_E_OOM;
     }
-    if (hipHostMalloc((void**)&B.h_lm, cap, hipHostMallocDefault) != hipSuccess) {
+    // mapped + coherent: the lane's kernel copies (launch_copy_words) read and write it
+    if (hipHostMalloc((void**)&B.h_lm, cap, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
         B.h_lm = nullptr;
         return LIVO_E_OOM;
+    }
+    B.h_lm_dev = nullptr;
+    if (hipHostGetDevicePointer((void**)&B.h_lm_dev, B.h_lm, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        B.h_lm_dev = nullptr;  // DMA copies then
     }
     B.lm_cap = cap;
     return LIVO_OK;
@@ -299,16 +324,29 @@ static int ensure_lm(BatchLane& B, int32_t n) {
 static int lane_streams(livo_ctx* c, int L) {
     BatchLane& B = c->lane[L];
     if (B.st[0]) return LIVO_OK;
+    for (int k = 0; k < kMaxGroups; k++)
+        if (!B.done[k] && hipEventCreateWithFlags(&B.done[k], hipEventDisableTiming) != hipSuccess) return LIVO_E_HIP;
     if (L == 0) {
         B.st[0] = c->stream;
         for (int k = 0; k < kMaxGroups - 1; k++) B.st[k + 1] = c->xstream[k];
         B.fork = c->fork;
         return LIVO_OK;
     }
-    B.owned = true;
-    for (int k = 0; k < kMaxGroups; k++)
-        if (hipStreamCreateWithFlags(&B.st[k], hipStreamNonBlocking) != hipSuccess) return LIVO_E_HIP;
+    // By default every lane queues on the context's streams: a batch submitted
+    // behind another starts the moment the device finishes the first (no host
+    // round trip, copy or launch latency in between), without running beside
+    // it (MI355X, 8 x 100k: two batches on their own streams, so concurrent,
+    // 10-13k updates/s against 16.9k for one at a time, profiles/r03_ab_lanes.txt).
+    // LIVO_LANE_STREAMS=own gives each lane its own streams.
+    if (!c->lane_own_streams) {
+        for (int k = 0; k < kMaxGroups; k++) B.st[k] = c->lane[0].st[k] ? c->lane[0].st[k] : (k ? c->xstream[k - 1] : c->stream);
+    } else {
+        B.owned = true;
+        for (int k = 0; k < kMaxGroups; k++)
+            if (hipStreamCreateWithFlags(&B.st[k], hipStreamNonBlocking) != hipSuccess) return LIVO_E_HIP;
+    }
     if (hipEventCreateWithFlags(&B.fork, hipEventDisableTiming) != hipSuccess) return LIVO_E_HIP;
+    B.owned_fork = true;
     return LIVO_OK;
 }
 
@@ -1121,6 +1159,9 @@ int livo_ctx_create(int device, const livo_params* p, livo_ctx** out) {
     if (const char* env = std::getenv("LIVO_KNN_KIND"))
         c->knn_kind = std::strcmp(env, "leaf") == 0 ? 0 : std::strcmp(env, "grid") == 0 ? 1 : 2;
     if (const char* env = std::getenv("LIVO_VRUNS")) c->vruns = std::atoi(env) != 0;
+    if (const char* env = std::getenv("LIVO_LANE_STREAMS")) c->lane_own_streams = std::strcmp(env, "own") == 0;
+    if (const char* env = std::getenv("LIVO_LANE_SERIAL")) c->lane_serial = std::atoi(env) != 0;
+    if (const char* env = std::getenv("LIVO_LANE_ZC")) c->lane_zc = std::atoi(env) != 0;
     if (const char* env = std::getenv("LIVO_XCD_CHUNK")) c->xcd_chunk = std::max(0, std::atoi(env));  // tuning knob
     if (const char* env = std::getenv("LIVO_GRID_PPC")) {  // tuning knob
         const float v = (float)std::atof(env);
@@ -1174,11 +1215,12 @@ int livo_ctx_destroy(livo_ctx* c) {
     for (BatchLane& B : c->lane) {
         dev_free(B.d_lm);
         if (B.h_lm) (void)hipHostFree(B.h_lm);
-        if (B.owned) {
+        if (B.owned)
             for (int k = 0; k < kMaxGroups; k++)
                 if (B.st[k]) (void)hipStreamDestroy(B.st[k]);
-            if (B.fork) (void)hipEventDestroy(B.fork);
-        }
+        if (B.owned_fork && B.fork) (void)hipEventDestroy(B.fork);
+        for (hipEvent_t e : B.done)
+            if (e) (void)hipEventDestroy(e);
     }
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->events_ready) {
@@ -1823,7 +1865,21 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
         // the replay count of this batch only (every batch's replays add to it)
         HIP_TRY(hipMemsetAsync(c->d_replay_total, 0, 8, c->stream));
     }
-    if (lm) {
+    // queued behind another lane's batch on shared streams: start only once all
+    // of its groups are done (LIVO_LANE_SERIAL=0: as soon as group 0's stream frees)
+    if (!c->lane_own_streams && c->lane_serial && c->last_lane >= 0 && c->last_lane != L &&
+        c->lane[c->last_lane].busy) {
+        const BatchLane& P = c->lane[c->last_lane];
+        for (int gi = 1; gi < P.ngroups; gi++) HIP_TRY(hipStreamWaitEvent(B.st[0], P.done[gi], 0));
+    }
+    c->last_lane = L;
+    // kernel copies for batches queued behind another on shared streams (a DMA
+    // copy there waits on an engine hand-off); LIVO_LANE_ZC=0: DMA copies always
+    const bool kcopy = lm && B.h_lm_dev && c->lane_zc && !sync;
+    if (lm && kcopy) {
+        rc = launch_copy_words(B.h_lm_dev, B.d_lm, lm_bytes(n), B.st[0]);
+        if (rc) return rc;
+    } else if (lm) {
         HIP_TRY(hipMemcpyAsync(B.d_lm, B.h_lm, (size_t)n * (kLmStride + sizeof(HsJob)), hipMemcpyHostToDevice,
                                B.st[0]));
     } else {
@@ -1919,9 +1975,18 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
         if (full) HIP_TRY(hipEventRecord(c->ev[gi][fused ? evals : 3 * LIVO_MAX_EVALS], g[gi].st));
     // each group copies its own slots back on its own stream (no cross-stream
     // join before the copy); the host then waits for every group's stream
-    for (int gi = 0; gi < ngroups; gi++)
-        HIP_TRY(hipMemcpyAsync(&hslot(g[gi].first), dslot(g[gi].first), stride * g[gi].count, hipMemcpyDeviceToHost,
-                               g[gi].st));
+    for (int gi = 0; gi < ngroups; gi++) {
+        if (kcopy) {
+            rc = launch_copy_words(dslot(g[gi].first), B.h_lm_dev + (size_t)g[gi].first * stride, stride * g[gi].count,
+                                   g[gi].st);
+            if (rc) return rc;
+        } else {
+            HIP_TRY(hipMemcpyAsync(&hslot(g[gi].first), dslot(g[gi].first), stride * g[gi].count,
+                                   hipMemcpyDeviceToHost, g[gi].st));
+        }
+        // this batch's end on the group's stream (another lane's batch may queue behind it)
+        HIP_TRY(hipEventRecord(B.done[gi], g[gi].st));
+    }
     if (full) {
         // the replay counter: every group's searches have run (joined into the main stream)
         for (int gi = 1; gi < ngroups; gi++) {
@@ -1966,12 +2031,13 @@ static int batch_collect(livo_ctx* c, int L, livo_state* states, livo_iter_stats
     const bool full = prof && c->profiling >= 2;
     struct { hipStream_t st; } g[kMaxGroups];
     for (int gi = 0; gi < ngroups; gi++) g[gi].st = B.st[gi];
-    const unsigned long long replays = c->last_replays;
     B.busy = false;  // collected (or failed): the lane is free either way
     B.n = 0;
     // wait by polling: the batch is short, and a blocking wait's wake-up
     // latency was a visible part of the gap between two batches
-    for (int gi = ngroups - 1; gi >= 0; gi--) HIP_TRY(stream_wait(g[gi].st));
+    for (int gi = ngroups - 1; gi >= 0; gi--) HIP_TRY(event_wait(B.done[gi]));
+    if (full) HIP_TRY(stream_wait(c->stream));  // the replay counter's read-back and the batch-end event
+    const unsigned long long replays = c->last_replays;
     for (int32_t b = 0; b < n; b++) {
         const IekfSlot& s = hslot(b);
         if (model == kModelIkfom) {

@@ -341,6 +341,7 @@ int launch_hshare(const HsParams& p, int n_jobs, int max_nblk, bool first, void*
 #endif
 constexpr int kEvalBlock = LIVO_EVAL_BLOCK;  // threads (points) per block of k_iekf_eval
 int launch_iekf_eval(const KnnParams& kp, const HsParams& hp, int n_jobs, int64_t max_n, bool first, void* stream);
+int launch_copy_words(const void* src, void* dst, size_t bytes, void* stream);  // 16-B aligned, bytes % 16 == 0
 // IKFoM plane pass (12-wide rows) with the manifold update in each scan's last block.
 int launch_hshare_ik(const HsParams& p, int n_jobs, int max_nblk, bool first, void* stream);
 int launch_solve(const SolveParams& p, int n_jobs, void* stream);

@@ -3118,6 +3118,25 @@ extern "C" int livo_debug_eval_prof(unsigned long long* out) {
 }
 #endif
 
+// Word copy by a kernel, for a batch lane's staging transfers between host-mapped
+// pinned memory and HBM (livo_capi.cpp batch_enqueue): on the compute queue
+// with the evaluations, so a batch queued behind another waits on no DMA-engine
+// hand-off.  Plain vector loads / stores, 16 B per lane.
+__global__ __launch_bounds__(256) void k_copy_words(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                    int64_t n16) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256) dst[i] = src[i];
+}
+
+int launch_copy_words(const void* src, void* dst, size_t bytes, void* stream) {
+    if (bytes == 0) return LIVO_OK;
+    if (bytes % 16 || (reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) % 16) return LIVO_E_INVALID;
+    const int64_t n16 = (int64_t)(bytes / 16);
+    const unsigned blocks = (unsigned)std::min<int64_t>((n16 + 255) / 256, 64);
+    hipLaunchKernelGGL(k_copy_words, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const uint4*>(src), reinterpret_cast<uint4*>(dst), n16);
+    return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+
 int launch_iekf_eval(const KnnParams& kp, const HsParams& hp, int n_jobs, int64_t max_n, bool first, void* stream) {
     if (n_jobs <= 0 || max_n <= 0) return LIVO_OK;
     EvalParams E;
