@@ -634,6 +634,86 @@ __global__ void k_cr_fill(const float4* __restrict__ gpts, const uint32_t* __res
     heads[i] = (i == 0 || skeys[i] != skeys[i - 1]) ? 1u : 0u;
 }
 
+// ---- ball runs (livo_internal.h), built on the device from the cell grid ----
+// The run of anchor cell a (edge G.h, same origin as the grid) holds every map
+// point whose squared distance to a's centre, cr_rho2 in float, is <= G.rmax2,
+// sorted by that value, then by (point, anchor) emission order.  A point emits
+// one entry per such anchor: k_br_count counts them, an exclusive scan places
+// them, k_br_emit writes (rho2 bits, anchor key, grid point).
+struct BrGeo {
+    float org[3];
+    float h, inv, rmax, rmax2;
+};
+template <class F>
+__device__ __forceinline__ void br_anchors(const BrGeo& G, const float4 p, F&& f) {
+    const float q[3] = {p.x, p.y, p.z};
+    int lo[3], hi[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {  // a cell range that holds every centre within rmax (one cell of slack)
+        lo[k] = (int)floorf((q[k] - G.org[k] - G.rmax) * G.inv) - 1;
+        hi[k] = (int)floorf((q[k] - G.org[k] + G.rmax) * G.inv) + 1;
+    }
+    for (int z = lo[2]; z <= hi[2]; z++)
+        for (int y = lo[1]; y <= hi[1]; y++)
+            for (int x = lo[0]; x <= hi[0]; x++) {
+                const float r2 = cr_rho2(G.org, G.h, x, y, z, p.x, p.y, p.z);
+                if (r2 <= G.rmax2) {
+                    const int v[3] = {x, y, z};
+                    f(v, r2);
+                }
+            }
+}
+__global__ void k_br_count(const float4* __restrict__ gpts, int64_t n, BrGeo G, uint32_t* cnt,
+                           unsigned long long* total) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t k = 0;
+    if (i < n) {
+        br_anchors(G, gpts[i], [&](const int*, float) { k++; });
+        cnt[i] = k;
+    }
+    // block total, one atomic per block (the u32 offsets must not overflow)
+    __shared__ unsigned long long part[4];
+    unsigned long long v = k;
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(total, part[0] + part[1] + part[2] + part[3]);
+}
+__global__ void k_br_emit(const float4* __restrict__ gpts, int64_t n, BrGeo G, const uint32_t* __restrict__ off,
+                          uint32_t* rho_bits, unsigned long long* keys, uint32_t* pt, uint32_t* iota) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t e = off[i];
+    br_anchors(G, gpts[i], [&](const int* v, float r2) {
+        rho_bits[e] = __float_as_uint(r2);  // non-negative: the bits sort as the values
+        keys[e] = cr_key(v);
+        pt[e] = (uint32_t)i;
+        iota[e] = e;
+        e++;
+    });
+}
+__global__ void k_br_gather_keys(const unsigned long long* __restrict__ keys, const uint32_t* __restrict__ e1,
+                                 int64_t n, unsigned long long* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = keys[e1[i]];
+}
+__global__ void k_br_fill(const float4* __restrict__ gpts, const uint32_t* __restrict__ pt,
+                          const uint32_t* __restrict__ e2, const unsigned long long* __restrict__ skeys, int64_t n,
+                          float4* bpts, uint32_t* heads) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n + 8) return;
+    if (i >= n) {  // chunk padding of the run scan
+        bpts[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        return;
+    }
+    bpts[i] = gpts[pt[e2[i]]];  // x, y, z, map index bits
+    heads[i] = (i == 0 || skeys[i] != skeys[i - 1]) ? 1u : 0u;
+}
+__global__ void k_add_u32(uint32_t* v, int64_t n, uint32_t add) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] += add;
+}
+
 // Delete_Point_Boxes (:501-521): boxes as BoxPointType {vertex_min[3], vertex_max[3]}, half open.
 __global__ void k_dyn_delete_boxes(const float4* __restrict__ all, uint8_t* alive, int64_t n_ids,
                                    const float* __restrict__ boxes, int64_t nb, unsigned long long* cnt) {
@@ -721,6 +801,28 @@ int launch_cr_fill(const float* gpts, const uint32_t* e2, const unsigned long lo
     DYN_LAUNCH(k_cr_fill, n + 8, reinterpret_cast<const float4*>(gpts), e2, skeys, n,
                reinterpret_cast<float4*>(vpts), heads);
 }
+static BrGeo br_geo(const float org[3], float h, float rmax) {
+    return BrGeo{{org[0], org[1], org[2]}, h, 1.0f / h, rmax, rmax * rmax};
+}
+int launch_br_count(const float* gpts, int64_t n, const float org[3], float h, float rmax, uint32_t* cnt,
+                    unsigned long long* total, void* stream) {
+    DYN_LAUNCH(k_br_count, n, reinterpret_cast<const float4*>(gpts), n, br_geo(org, h, rmax), cnt, total);
+}
+int launch_br_emit(const float* gpts, int64_t n, const float org[3], float h, float rmax, const uint32_t* off,
+                   uint32_t* rho_bits, unsigned long long* keys, uint32_t* pt, uint32_t* iota, void* stream) {
+    DYN_LAUNCH(k_br_emit, n, reinterpret_cast<const float4*>(gpts), n, br_geo(org, h, rmax), off, rho_bits, keys, pt,
+               iota);
+}
+int launch_br_gather_keys(const unsigned long long* keys, const uint32_t* e1, int64_t n, unsigned long long* out,
+                          void* stream) {
+    DYN_LAUNCH(k_br_gather_keys, n, keys, e1, n, out);
+}
+int launch_br_fill(const float* gpts, const uint32_t* pt, const uint32_t* e2, const unsigned long long* skeys,
+                   int64_t n, float* bpts, uint32_t* heads, void* stream) {
+    DYN_LAUNCH(k_br_fill, n + 8, reinterpret_cast<const float4*>(gpts), pt, e2, skeys, n,
+               reinterpret_cast<float4*>(bpts), heads);
+}
+int launch_add_u32(uint32_t* v, int64_t n, uint32_t add, void* stream) { DYN_LAUNCH(k_add_u32, n, v, n, add); }
 int launch_dyn_delete_boxes(const float* all, uint8_t* alive, int64_t n_ids, const float* boxes, int64_t nb,
                             unsigned long long* cnt, void* stream) {
     DYN_LAUNCH(k_dyn_delete_boxes, n_ids, reinterpret_cast<const float4*>(all), alive, n_ids, boxes, nb, cnt);

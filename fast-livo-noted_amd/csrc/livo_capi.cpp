@@ -173,6 +173,14 @@ struct livo_ctx {
     GridSlot* vslots = nullptr;        // vertex runs (static map only)
     float* vpts = nullptr;             // run entries (x, y, z, map index bits)
     int32_t vlog2 = 0;
+    // ball runs (static map only): anchor cells of edge bh, runs of radius brmax
+    bool bruns = true;                 // LIVO_BRUNS=0: the cell runs only
+    float br_ha = 2.0f, br_r = 3.2f;   // bh = br_ha r5, brmax = sqrt(3)/2 bh + br_r r5 (LIVO_BR_HA / LIVO_BR_R)
+    GridSlot* bslots = nullptr;
+    float* bpts = nullptr;
+    int32_t blog2 = 0;
+    float bh = 0.f, brmax = 0.f, br5 = 0.f;
+    int64_t bentries = 0;
     GridSlot* gslots = nullptr;        // cell grid
     float* gpts = nullptr;
     float gorg[3] = {0.f, 0.f, 0.f};
@@ -405,6 +413,14 @@ static KnnParams make_knn_params(livo_ctx* c) {
     kp.vslots = vr ? c->vslots : nullptr;
     kp.vpts = vr ? c->vpts : nullptr;
     kp.vlog2 = c->vlog2;
+    const bool br = vr && c->bslots;
+    kp.bslots = br ? c->bslots : nullptr;
+    kp.bpts = br ? c->bpts : nullptr;
+    kp.blog2 = c->blog2;
+    kp.bh = c->bh;
+    // certification: every point within the final bound lies in the ball (the build
+    // keeps points with cr_rho2 <= brmax^2 in float: a relative 1e-5 below covers its rounding)
+    kp.bcert2 = c->brmax * c->brmax * (1.0f - 1e-5f);
     kp.xcd_chunk = c->xcd_chunk;
     kp.identity = 0;
     kp.iv = ivox_params(c);
@@ -1160,6 +1176,15 @@ int livo_ctx_create(int device, const livo_params* p, livo_ctx** out) {
         c->knn_kind = std::strcmp(env, "leaf") == 0 ? 0 : std::strcmp(env, "grid") == 0 ? 1 : 2;
     if (const char* env = std::getenv("LIVO_VRUNS")) c->vruns = std::atoi(env) != 0;
     if (const char* env = std::getenv("LIVO_LANE_STREAMS")) c->lane_own_streams = std::strcmp(env, "own") == 0;
+    if (const char* env = std::getenv("LIVO_BRUNS")) c->bruns = std::atoi(env) != 0;
+    if (const char* env = std::getenv("LIVO_BR_HA")) {
+        const float v = (float)std::atof(env);
+        if (v > 0.2f && v < 20.f) c->br_ha = v;
+    }
+    if (const char* env = std::getenv("LIVO_BR_R")) {
+        const float v = (float)std::atof(env);
+        if (v > 0.5f && v < 20.f) c->br_r = v;
+    }
     if (const char* env = std::getenv("LIVO_LANE_SERIAL")) c->lane_serial = std::atoi(env) != 0;
     if (const char* env = std::getenv("LIVO_LANE_ZC")) c->lane_zc = std::atoi(env) != 0;
     if (const char* env = std::getenv("LIVO_XCD_CHUNK")) c->xcd_chunk = std::max(0, std::atoi(env));  // tuning knob
@@ -1205,6 +1230,8 @@ int livo_ctx_destroy(livo_ctx* c) {
     dev_free(c->gpts);
     dev_free(c->vslots);
     dev_free(c->vpts);
+    dev_free(c->bslots);
+    dev_free(c->bpts);
     dev_free(c->d_replay_count);
     dev_free(c->d_replay_total);
     dev_free(c->d_replay_list);
@@ -1332,6 +1359,103 @@ static int build_cell_runs(livo_ctx* c, int64_t M) {
     return LIVO_OK;
 }
 
+// The ball runs of the static map (livo_internal.h KnnParams::bslots), built on
+// the device: every grid point emits one entry per anchor cell (edge bh) whose
+// centre lies within brmax (k_br_count, a scan, k_br_emit); a stable radix sort
+// by rho2, a gather of the anchor keys and a stable sort by key leave each
+// anchor's run contiguous and sorted by rho2; heads, starts and the hash table
+// as for the cell runs.  r5: the map's median 5-NN distance (sample_knn_radius).
+static int build_ball_runs(livo_ctx* c, int64_t M, float r5) {
+    dev_free(c->bslots);
+    dev_free(c->bpts);
+    c->bentries = 0;
+    if (M <= 0 || !(r5 > 0.f)) return LIVO_OK;
+    const float bh = std::max(c->br_ha * r5, 1e-3f);
+    const float brmax = 0.8660254f * bh + c->br_r * r5;
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    uint32_t* cnt = nullptr;
+    uint32_t* off = nullptr;
+    unsigned long long* tot = nullptr;
+    if (dev_alloc(&cnt, (size_t)M) || dev_alloc(&off, (size_t)M) || dev_alloc(&tot, 1)) {
+        dev_free(cnt);
+        dev_free(off);
+        dev_free(tot);
+        return LIVO_E_OOM;
+    }
+    int rc = hipMemsetAsync(tot, 0, 8, c->stream) == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+    if (!rc) rc = launch_br_count(c->gpts, M, c->gorg, bh, brmax, cnt, tot, c->stream);
+    if (!rc) rc = ivox_scan(c, cnt, off, M);
+    unsigned long long n64 = 0;
+    if (!rc && hipMemcpyAsync(&n64, tot, 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess) rc = LIVO_E_HIP;
+    if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = LIVO_E_HIP;
+    dev_free(cnt);
+    dev_free(tot);
+    // 31-bit run positions (kRunPos) and u32 offsets; a map too dense for the ball keeps the cell runs
+    if (rc || n64 == 0 || (int64_t)n64 + 8 >= (int64_t)kRunPosLimit) {
+        dev_free(off);
+        return rc;
+    }
+    const int64_t n = (int64_t)n64;
+    const size_t b4 = al((size_t)n * 4), b8 = al((size_t)n * 8);
+    char* scr = nullptr;
+    if (hipMalloc((void**)&scr, 7 * b4 + 3 * b8 + al(((size_t)n + 1) * 4) + 256) != hipSuccess) {
+        dev_free(off);
+        return LIVO_E_OOM;
+    }
+    char* p = scr;
+    uint32_t* rho = (uint32_t*)p; p += b4;
+    uint32_t* iota = (uint32_t*)p; p += b4;
+    uint32_t* srho = (uint32_t*)p; p += b4;
+    uint32_t* e1 = (uint32_t*)p; p += b4;
+    uint32_t* e2 = (uint32_t*)p; p += b4;
+    uint32_t* pt = (uint32_t*)p; p += b4;
+    uint32_t* heads = (uint32_t*)p; p += b4;
+    unsigned long long* keys = (unsigned long long*)p; p += b8;
+    unsigned long long* key1 = (unsigned long long*)p; p += b8;
+    unsigned long long* skeys = (unsigned long long*)p; p += b8;
+    uint32_t* starts = (uint32_t*)p; p += al(((size_t)n + 1) * 4);
+    unsigned long long* nruns = (unsigned long long*)p;
+    uint32_t* runid = rho;  // (rho is dead after the first sort)
+    if (dev_alloc(&c->bpts, (size_t)(n + 8) * 4)) rc = LIVO_E_OOM;
+    if (!rc) rc = launch_br_emit(c->gpts, M, c->gorg, bh, brmax, off, rho, keys, pt, iota, c->stream);
+    if (!rc) {
+        size_t tb = 0;
+        rc = prim_sort_pairs_u32(nullptr, &tb, rho, srho, iota, e1, n, 32, c->stream);
+        if (!rc) rc = ensure_prim(c, tb);
+        tb = c->prim_bytes;
+        if (!rc) rc = prim_sort_pairs_u32(c->prim_tmp, &tb, rho, srho, iota, e1, n, 32, c->stream);
+    }
+    if (!rc) rc = launch_br_gather_keys(keys, e1, n, key1, c->stream);
+    if (!rc) rc = sort_u64(c, key1, skeys, e1, e2, n);
+    if (!rc) rc = launch_br_fill(c->gpts, pt, e2, skeys, n, c->bpts, heads, c->stream);
+    if (!rc) rc = ivox_scan(c, heads, runid, n);
+    if (!rc) rc = launch_dyn_runs(heads, runid, n, starts, nruns, c->stream);
+    unsigned long long runs = 0;
+    if (!rc && hipMemcpyAsync(&runs, nruns, 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess) rc = LIVO_E_HIP;
+    if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = LIVO_E_HIP;
+    int log2 = 4;
+    while (((int64_t)1 << log2) < 4 * (int64_t)runs) log2++;
+    const int64_t table = (int64_t)1 << log2;
+    if (!rc && dev_alloc(&c->bslots, (size_t)table)) rc = LIVO_E_OOM;
+    if (!rc) rc = launch_ivox_clear(c->bslots, table, c->stream);
+    if (!rc) rc = launch_dyn_slots(skeys, starts, (int64_t)runs, c->bslots, log2, c->stream);
+    if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = LIVO_E_HIP;
+    (void)hipFree(scr);
+    dev_free(off);
+    if (rc) {
+        dev_free(c->bslots);
+        dev_free(c->bpts);
+        return rc;
+    }
+    c->blog2 = log2;
+    c->bh = bh;
+    c->brmax = brmax;
+    c->br5 = r5;
+    c->bentries = n;
+    c->grid_bytes += (int64_t)(table * sizeof(GridSlot) + (size_t)(n + 8) * 16);
+    return LIVO_OK;
+}
+
 int livo_map_build(livo_ctx* c, const float* xyz, int64_t M, int64_t stride_bytes) {
     if (!c || M < 0 || (M > 0 && !xyz)) return LIVO_E_INVALID;
     if (any_inflight(c)) return LIVO_E_BUSY;  // submitted batches are collected first
@@ -1360,6 +1484,8 @@ int livo_map_build(livo_ctx* c, const float* xyz, int64_t M, int64_t stride_byte
     dev_free(c->gpts);
     dev_free(c->vslots);
     dev_free(c->vpts);
+    dev_free(c->bslots);
+    dev_free(c->bpts);
     c->nodes = nullptr;
     c->lnodes = nullptr;
     c->lpts = nullptr;
@@ -1395,6 +1521,7 @@ int livo_map_build(livo_ctx* c, const float* xyz, int64_t M, int64_t stride_byte
         c->leaf_bytes = (int64_t)(lnb + ppb);
     }
     if (!oom && e == hipSuccess) e = hipMemcpy(c->nodes, hm.nodes, bytes, hipMemcpyHostToDevice);
+    const float r5 = (vr && c->bruns && c->knn_kind >= 1) ? sample_knn_radius(gm, 8192) : 0.f;
     free_host_map(&hm);
     free_leaf_map(&lm);
     free_grid_map(&gm);
@@ -1402,6 +1529,7 @@ int livo_map_build(livo_ctx* c, const float* xyz, int64_t M, int64_t stride_byte
     if (e != hipSuccess) return LIVO_E_HIP;
     if (vr) {
         rc = build_cell_runs(c, M);
+        if (!rc && r5 > 0.f) rc = build_ball_runs(c, M, r5);
         if (rc) return rc;
     }
     c->map_points = M;

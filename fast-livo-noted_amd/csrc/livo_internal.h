@@ -119,6 +119,7 @@ struct HostGridMap {
 // ppc_target < 0: -ppc_target x clamp((M / 1M)^0.3, 1, 4), the cell runs' sizing)
 int build_grid_map(const float* xyz, int64_t M, int64_t stride_bytes, float cell_h, HostGridMap* out,
                    float ppc_target = 0.f);
+float sample_knn_radius(const HostGridMap& gm, int samples);  // median 5-NN distance of map points
 constexpr int64_t kRunPosLimit = 0x7FFFFFFF;  // run entries a search can address (31-bit positions)
 constexpr float kVrunPpc = 20.0f;  // cell occupancy of the cell runs at 1M points (0.35 m cells on the config-2 map)
 void free_grid_map(HostGridMap* m);
@@ -303,6 +304,11 @@ struct KnnParams {
     const GridSlot* vslots; // cell runs (null: the cell walk of grid_search)
     const float* vpts;      // run entries: x, y, z, map index bits
     int32_t vlog2;
+    const GridSlot* bslots; // ball runs (null: the cell runs only); entries in bpts
+    const float* bpts;
+    int32_t blog2;
+    float bh;               // anchor cell edge (origin gorg)
+    float bcert2;           // certified if the final scan bound b satisfies b * b <= bcert2
     IvoxParams iv;          // iVox backend (LIVO_BACKEND_IVOX)
     int32_t canon;          // incremental map: flagged queries -> k_knn_canon instead of the ikd-Tree replay
 };
@@ -564,6 +570,16 @@ int launch_dyn_delete_boxes(const float* all, uint8_t* alive, int64_t n_ids, con
 // Cell runs on the device from the cell grid (gpts: n / 27 points): entry e's
 // rho2 (bits) and e; the run key of pass-1-sorted entries; the final runs
 // (x, y, z, map index bits) and the run heads.
+// ball runs (k_br_*, ikd_incr_kernels.hip)
+int launch_br_count(const float* gpts, int64_t n, const float org[3], float h, float rmax, uint32_t* cnt,
+                    unsigned long long* total, void* stream);
+int launch_br_emit(const float* gpts, int64_t n, const float org[3], float h, float rmax, const uint32_t* off,
+                   uint32_t* rho_bits, unsigned long long* keys, uint32_t* pt, uint32_t* iota, void* stream);
+int launch_br_gather_keys(const unsigned long long* keys, const uint32_t* e1, int64_t n, unsigned long long* out,
+                          void* stream);
+int launch_br_fill(const float* gpts, const uint32_t* pt, const uint32_t* e2, const unsigned long long* skeys,
+                   int64_t n, float* bpts, uint32_t* heads, void* stream);
+int launch_add_u32(uint32_t* v, int64_t n, uint32_t add, void* stream);
 int launch_cr_rho(const float* gpts, int64_t n, const float org[3], float h, uint32_t* rho_bits, uint32_t* iota,
                   void* stream);
 int launch_cr_key(const float* gpts, const uint32_t* e1, int64_t n, const float org[3], float h,

@@ -1470,6 +1470,81 @@ __device__ __forceinline__ bool vrun_search(LeafQuery& q, const KnnParams& P, bo
     return grid_search(q, P, c0, c1, c2, s0, s1, s2, none, visits, npts, nullptr, true);
 }
 
+// ------------------------------------------------------------ ball-run search ----
+// The batched IEKF search on the ball runs (livo_internal.h KnnParams::bslots):
+// the run of the query's anchor cell a (edge P.bh) holds every map point within
+// brmax of a's centre, sorted by rho2 (cr_rho2, the build's float operations).
+// One hash probe, then one contiguous scan with vrun_search's stop rule: the
+// scan stops at the first chunk whose first entry has rho > b = |q - a| +
+// sqrt(bound) (+ the same margins), every later entry being farther than the
+// bound.  The anchor is nearer the query than a cell-run centre (anchors are
+// smaller than grid cells), so the scan reads fewer entries.  The list is
+// certified when the final b satisfies b^2 <= P.bcert2 (brmax^2 less a relative
+// 1e-5): every point within the bound (+ 1e-10) then lies in the ball, so it is
+// in the run and was scanned.  Points outside the ball are farther than b, so,
+// as a pruned cell of grid_search, they could neither enter the list nor make
+// e6 - d5 <= 1e-10.  Not certified (or no run): the caller searches the cell
+// runs from scratch.  Candidates carry their position in P.bpts (kRunPos set).
+__device__ __forceinline__ bool brun_search(LeafQuery& q, const KnnParams& P, bool valid, unsigned& visits,
+                                            unsigned& npts) {
+    if (!valid || !(P.lM > 0)) return false;
+    const float inv = 1.0f / P.bh;
+    int a[3];
+    const float qq[3] = {q.qx, q.qy, q.qz};
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        float f = floorf((qq[k] - P.gorg[k]) * inv);
+        f = fminf(fmaxf(f, (float)(8 - kGridBias)), (float)(kGridBias - 8));  // NaN -> 8 - bias
+        a[k] = (int)f;
+    }
+    const unsigned long long key = grid_key_d(a[0], a[1], a[2]);
+    const uint64_t mask = (1ull << P.blog2) - 1ull;
+    uint64_t sl = (uint64_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - P.blog2));
+    GridSlot g = P.bslots[sl];
+    visits++;
+    while (g.key != key && g.key != kGridEmpty) {  // linear probing (load factor <= 1/4)
+        sl = (sl + 1) & mask;
+        g = P.bslots[sl];
+        visits++;
+    }
+    if (g.key != key) return false;
+    const uint32_t lo = g.start, cnt = g.count;
+    const float cx = cell_centre(P.gorg[0], P.bh, a[0]), cy = cell_centre(P.gorg[1], P.bh, a[1]);
+    const float cz = cell_centre(P.gorg[2], P.bh, a[2]);
+    const float dqv = __builtin_amdgcn_sqrtf(centre_d2(cx, cy, cz, q.qx, q.qy, q.qz)) * (1.0f + 1e-6f);
+    const float4* __restrict__ run = reinterpret_cast<const float4*>(P.bpts) + lo;
+    uint32_t k0 = 0;
+#pragma unroll 1
+    for (; k0 < cnt; k0 += 8) {
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = run[k0 + u];  // padded by 8 entries
+        const float thr = lq_thr(q);
+        if (thr < INFINITY) {
+            const float b = dqv + __builtin_amdgcn_sqrtf(thr) * (1.0f + 1e-6f) + 1e-4f;
+            if (centre_d2(cx, cy, cz, v[0].x, v[0].y, v[0].z) > b * b) break;  // rho of every later entry > b
+        }
+        float dist[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const float dx = q.qx - v[u].x, dy = q.qy - v[u].y, dz = q.qz - v[u].z;
+            const float d = (dx * dx + dy * dy) + dz * dz;  // calc_dist (:1291-1295)
+            dist[u] = k0 + u < cnt ? d : INFINITY;
+        }
+        const float m = fminf(fminf(fminf(dist[0], dist[1]), fminf(dist[2], dist[3])),
+                              fminf(fminf(dist[4], dist[5]), fminf(dist[6], dist[7])));
+        if (m < q.e6) {
+#pragma unroll
+            for (int u = 0; u < 8; u++) lq_offer(q, dist[u], kRunPos | (lo + k0 + u));
+        }
+    }
+    npts += min(k0, cnt);
+    const float t = lq_thr(q);
+    if (!(t < INFINITY)) return false;
+    const float b = dqv + __builtin_amdgcn_sqrtf(t) * (1.0f + 1e-6f) + 1e-4f;
+    return b * b <= P.bcert2;
+}
+
 // 512 points / 128 cells per wave (10.5 KB): 4 waves per SIMD (VGPR-bound);
 // on MI355X 1024 / 256 (18.5 KB, 2 waves per SIMD) was 12 % slower at config 2
 #ifndef LIVO_TILE_CELLS
@@ -2466,7 +2541,20 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
         bool amb = false;
         if (P.vslots) {  // (kernel parameter: uniform)
             EVAL_MARK(1);
-            const bool certified = vrun_search(q, P, valid, c0, c1, c2, s0, s1, s2, visits, npts);
+            bool certified = false;
+            const float4* runs = reinterpret_cast<const float4*>(P.vpts);
+            if (P.bslots) {  // (uniform) the ball runs first; the cell runs for a query they do not certify
+                certified = brun_search(q, P, valid, visits, npts);
+                if (certified) runs = reinterpret_cast<const float4*>(P.bpts);
+                if (valid && !certified) {
+#ifdef LIVO_AB_NOSEED
+                    lq_init<false>(q, P, slot, job, i, valid);
+#else
+                    lq_init<!FIRST>(q, P, slot, job, i, valid);
+#endif
+                }
+            }
+            if (!certified) certified = vrun_search(q, P, valid, c0, c1, c2, s0, s1, s2, visits, npts);
 #ifdef LIVO_EVAL_PROF
             {  // block totals: lanes past the 2x2x2 block, run entries scanned, ambiguous
                 const unsigned long long nf = __ballot(valid && !certified);
@@ -2478,7 +2566,7 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
 #endif
             if (valid)
                 amb = lq_finish<true>(q, P, job, bjob, i, reinterpret_cast<const float4*>(P.gpts), !certified, false,
-                                      reinterpret_cast<const float4*>(P.vpts));
+                                      runs);
             EVAL_MARK(6);
         } else {
             const TileView tv = build_tile<kEvalBlock>(U.tile, P, valid, c0, c1, c2, visits, npts);

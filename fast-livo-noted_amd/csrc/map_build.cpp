@@ -406,6 +406,46 @@ int build_grid_map(const float* xyz, int64_t M, int64_t stride_bytes, float cell
     return LIVO_OK;
 }
 
+// Median distance from a map point to its 5th nearest other map point, over a
+// strided sample of the grid's points, searched in the 3x3x3 cells around the
+// point (a sample whose 5th neighbour lies farther than one cell is skipped):
+// the map's local density scale, which sizes the ball runs (livo_capi.cpp).
+float sample_knn_radius(const HostGridMap& gm, int samples) {
+    const int64_t M = gm.num_points;
+    if (M < 6 || samples <= 0) return 0.f;
+    const int64_t nslots = (int64_t)1 << gm.log2_slots;
+    const double inv = 1.0 / (double)gm.h;
+    std::vector<float> r;
+    r.reserve((size_t)samples);
+    const int64_t step = std::max<int64_t>(1, M / samples);
+    for (int64_t i = 0; i < M && (int64_t)r.size() < samples; i += step) {
+        const float* p = gm.pts + 4 * i;
+        int64_t c[3];
+        for (int k = 0; k < 3; k++) c[k] = (int64_t)std::floor(((double)p[k] - (double)gm.org[k]) * inv);
+        float best[6] = {INFINITY, INFINITY, INFINITY, INFINITY, INFINITY, INFINITY};  // incl. the point itself
+        for (int dz = -1; dz <= 1; dz++)
+            for (int dy = -1; dy <= 1; dy++)
+                for (int dx = -1; dx <= 1; dx++) {
+                    const unsigned long long key = grid_key(c[0] + dx, c[1] + dy, c[2] + dz);
+                    uint64_t sl = grid_hash(key, gm.log2_slots);
+                    while (gm.slots[sl].key != key && gm.slots[sl].key != kGridEmpty) sl = (sl + 1) & (uint64_t)(nslots - 1);
+                    if (gm.slots[sl].key != key) continue;
+                    const float* q = gm.pts + 4 * (int64_t)gm.slots[sl].start;
+                    for (uint32_t j = 0; j < gm.slots[sl].count; j++, q += 4) {
+                        const float ex = q[0] - p[0], ey = q[1] - p[1], ez = q[2] - p[2];
+                        float d = ex * ex + ey * ey + ez * ez;
+                        for (int k = 0; k < 6; k++)
+                            if (d < best[k]) std::swap(d, best[k]);
+                    }
+                }
+        const float r5 = std::sqrt(best[5]);
+        if (r5 <= gm.h) r.push_back(r5);
+    }
+    if (r.empty()) return 0.f;
+    std::nth_element(r.begin(), r.begin() + r.size() / 2, r.end());
+    return r[r.size() / 2];
+}
+
 void free_grid_map(HostGridMap* m) {
     if (!m) return;
     std::free(m->slots);
