@@ -822,7 +822,7 @@ __device__ __forceinline__ float4 cand_point(const float4* __restrict__ lpts, co
 template <bool RUNS = false>
 __device__ __forceinline__ bool lq_finish(LeafQuery& q, const KnnParams& P, const HsJob& job, unsigned bjob,
                                           int i, const float4* __restrict__ lpts, bool overrun, bool enqueue = true,
-                                          const float4* __restrict__ vpts = nullptr) {
+                                          const float4* __restrict__ vpts = nullptr, float4* nbr = nullptr) {
     const int cnt = (int)min<int64_t>(P.lM, (int64_t)kNN);
     float4 a[kNN];
 #pragma unroll
@@ -870,6 +870,7 @@ __device__ __forceinline__ bool lq_finish(LeafQuery& q, const KnnParams& P, cons
             idx[k] = (int32_t)__float_as_uint(a[k].w);
         }
         o4[k] = v;
+        if (nbr) nbr[k] = v;  // (x, y, z, sqdist) as the record holds them
     }
     const int flag = amb ? 4 : (tie ? 16 : 0);
     int4* oi = reinterpret_cast<int4*>(job.nn + i) + 5;
@@ -2179,8 +2180,37 @@ __device__ __forceinline__ void hs_accumulate(double (&acc)[kRedUsed], const HsR
         hs_accumulate<J + 1>(acc, w, inv_r);
     }
 }
+// The plane of point i from its 5 neighbours (x, y, z, sqdist) and their
+// count, after a search or (search = 0) from the cached neighbours:
+// point_selected_surf, esti_plane, and the plane state / plane cache stores.
+// Returns the plane state: 0 not selected (a searched point beyond the sqdist
+// gate: the next evaluation without a search fits it, as the reference does),
+// 1 no plane (fewer than 5 neighbours, :525, or esti_plane false), 2 plane.
+__device__ __forceinline__ uint8_t fit_plane(const HsParams& P, const HsJob& job, int i, int search,
+                                             const float4 (&nb)[kNN], int cnt, float4& plane) {
+    float nx[kNN], ny[kNN], nz[kNN];
+#pragma unroll
+    for (int k = 0; k < kNN; k++) { nx[k] = nb[k].x; ny[k] = nb[k].y; nz[k] = nb[k].z; }
+    const float d4 = nb[kNN - 1].w;
+    // point_selected_surf: sqdis[4] > 5 => false after a search (:518); true otherwise (:490)
+    const bool sel = search ? ((cnt == kNN) && !(d4 > P.max_sqd)) : true;
+    uint8_t ps = 0;
+    float pa[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    bool plane_ok = false;
+    if (cnt < kNN) {
+        ps = 1;  // points_near.size() < 5 (:525) until the next search
+    } else if (sel) {
+        plane_ok = esti_plane(nx, ny, nz, P.plane_thr, pa);
+        ps = plane_ok ? 2 : 1;
+    }
+    job.pstate[i] = ps;
+    plane = make_float4(pa[0], pa[1], pa[2], pa[3]);
+    if (plane_ok) reinterpret_cast<float4*>(job.plane)[i] = plane;
+    return ps;
+}
+
 __device__ __forceinline__ void hshare_point(const HsParams& P, const HsJob& job, const livo_state& S, int i,
-                                             int search, HsRow& w, const HsPointIn& in) {
+                                             int search, HsRow& w, const HsPointIn& in, bool prefit = false) {
             const float4 pb = in.pb;
             const double* R = S.rot;
             float wx, wy, wz;
@@ -2196,30 +2226,19 @@ __device__ __forceinline__ void hshare_point(const HsParams& P, const HsJob& job
             // 0 not fitted yet, 1 no plane, 2 plane) and reused bit for bit.
             bool plane_ok = false;
             float pa[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-            uint8_t ps = search ? 0 : in.ps;
-            if (ps == 0) {
+            // prefit: the fused search already fitted this evaluation's plane
+            // from its neighbours in registers (in.ps / in.plane, fit_plane)
+            uint8_t ps = (search && !prefit) ? 0 : in.ps;
+            if (ps == 0 && !prefit) {
                 const float4* rec = reinterpret_cast<const float4*>(job.nn + i);
-                float nx[kNN], ny[kNN], nz[kNN];
-                float d4 = 0.0f;
+                float4 nb[kNN];
     #pragma unroll
-                for (int k = 0; k < kNN; k++) {
-                    const float4 v = rec[k];
-                    nx[k] = v.x; ny[k] = v.y; nz[k] = v.z;
-                    if (k == kNN - 1) d4 = v.w;
-                }
+                for (int k = 0; k < kNN; k++) nb[k] = rec[k];
                 const int cnt = reinterpret_cast<const int4*>(job.nn + i)[6].y;
-                // point_selected_surf: sqdis[4] > 5 => false after a search (:518); true otherwise (:490)
-                const bool sel = search ? ((cnt == kNN) && !(d4 > P.max_sqd)) : true;
-                if (cnt < kNN) {
-                    ps = 1;  // points_near.size() < 5 (:525) until the next search
-                } else if (sel) {
-                    plane_ok = esti_plane(nx, ny, nz, P.plane_thr, pa);
-                    ps = plane_ok ? 2 : 1;
-                }
-                // (a searched point beyond the sqdist gate stays 0: the next
-                // evaluation without a search fits it, as the reference does)
-                job.pstate[i] = ps;
-                if (plane_ok) reinterpret_cast<float4*>(job.plane)[i] = make_float4(pa[0], pa[1], pa[2], pa[3]);
+                float4 pl;
+                ps = fit_plane(P, job, i, search, nb, cnt, pl);
+                plane_ok = ps == 2;
+                pa[0] = pl.x; pa[1] = pl.y; pa[2] = pl.z; pa[3] = pl.w;
             } else if (ps == 2) {
                 const float4 v = in.plane;
                 pa[0] = v.x; pa[1] = v.y; pa[2] = v.z; pa[3] = v.w;
@@ -2520,7 +2539,8 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
     const bool valid = i < job.n;
     // the point's loads go out with the slot's control reads (after the first
     // evaluation the plane cache too: used unless this evaluation searches)
-    const HsPointIn pin = valid ? hshare_load(job, i, !FIRST) : HsPointIn{};
+    HsPointIn pin = valid ? hshare_load(job, i, !FIRST) : HsPointIn{};
+    bool prefit = false;  // the plane of this evaluation fitted in the search branch
     if (slot->ctrl.stop) return;  // block-uniform
     const int search = FIRST ? 1 : slot->ctrl.search_en;
 #ifdef LIVO_EVAL_PROF
@@ -2529,12 +2549,12 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
     EVAL_MARK(0);
     unsigned n_slots = 0u, n_pts = 0u;  // hash slots and map points this thread's search read
     if (search) {
+        // Later searches start unseeded too: the previous neighbours' bound saved
+        // less than reading their record cost (rematch 0.156 vs 0.159 ms, 18991 vs
+        // 18643 updates/s, profiles/r03_ab_prefit_seed.txt); the answer is the
+        // same exact list either way
         LeafQuery q;
-#ifdef LIVO_AB_NOSEED  // A/B only: rematch searches without the previous neighbours' bound
         lq_init<false>(q, P, slot, job, i, valid);
-#else
-        lq_init<!FIRST>(q, P, slot, job, i, valid);
-#endif
         int c0 = 0, c1 = 0, c2 = 0, s0 = 1, s1 = 1, s2 = 1;
         if (valid) grid_cell(P, q, c0, c1, c2, s0, s1, s2);
         unsigned visits = 0, npts = 0;
@@ -2546,13 +2566,7 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
             if (P.bslots) {  // (uniform) the ball runs first; the cell runs for a query they do not certify
                 certified = brun_search(q, P, valid, visits, npts);
                 if (certified) runs = reinterpret_cast<const float4*>(P.bpts);
-                if (valid && !certified) {
-#ifdef LIVO_AB_NOSEED
-                    lq_init<false>(q, P, slot, job, i, valid);
-#else
-                    lq_init<!FIRST>(q, P, slot, job, i, valid);
-#endif
-                }
+                if (valid && !certified) lq_init<false>(q, P, slot, job, i, valid);
             }
             if (!certified) certified = vrun_search(q, P, valid, c0, c1, c2, s0, s1, s2, visits, npts);
 #ifdef LIVO_EVAL_PROF
@@ -2564,9 +2578,19 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
             }
             EVAL_MARK(5);
 #endif
-            if (valid)
+            if (valid) {
+                float4 nb[kNN];
                 amb = lq_finish<true>(q, P, job, bjob, i, reinterpret_cast<const float4*>(P.gpts), !certified, false,
-                                      runs);
+                                      runs, nb);
+#ifndef LIVO_AB_NOPREFIT  // A/B only: the plane pass re-reads the record it was just written
+                if (!amb && !P.canon) {  // (a replayed query's plane is fitted from its record below)
+                    float4 pl;
+                    pin.ps = fit_plane(E.h, job, i, 1, nb, (int)min<int64_t>(P.lM, (int64_t)kNN), pl);
+                    pin.plane = pl;
+                    prefit = true;
+                }
+#endif
+            }
             EVAL_MARK(6);
         } else {
             const TileView tv = build_tile<kEvalBlock>(U.tile, P, valid, c0, c1, c2, visits, npts);
@@ -2601,7 +2625,7 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
     hs_row_clear(w);
     const int nblk = max(1, (job.n + kEvalBlock - 1) / kEvalBlock);
     if (valid) {
-        hshare_point(E.h, job, slot->state, i, search, w, pin);
+        hshare_point(E.h, job, slot->state, i, search, w, pin, prefit);
     }
     EVAL_MARK_SYNC(3);
     const double inv_r = E.h.inv_r;
