@@ -2582,14 +2582,14 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
                 float4 nb[kNN];
                 amb = lq_finish<true>(q, P, job, bjob, i, reinterpret_cast<const float4*>(P.gpts), !certified, false,
                                       runs, nb);
-#ifndef LIVO_AB_NOPREFIT  // A/B only: the plane pass re-reads the record it was just written
+                // the plane from the neighbours in registers (18643 vs 18011 updates/s
+                // re-reading the record just written, profiles/r03_ab_prefit_seed.txt)
                 if (!amb && !P.canon) {  // (a replayed query's plane is fitted from its record below)
                     float4 pl;
                     pin.ps = fit_plane(E.h, job, i, 1, nb, (int)min<int64_t>(P.lM, (int64_t)kNN), pl);
                     pin.plane = pl;
                     prefit = true;
                 }
-#endif
             }
             EVAL_MARK(6);
         } else {
