@@ -2302,17 +2302,46 @@ struct HsReduceLds {
 // sums instead of per-wave device atomics on two addresses per scan (those
 // serialise across the XCDs); the last block adds them to slot->visits /
 // scanned of this evaluation.
-// col(std::integral_constant<int, j>) gives this thread's value of column j:
-// each column is formed, row-summed and stored in turn.
-template <class Col, int... J>
-__device__ __forceinline__ void hs_row_sums(const Col& col, HsReduceLds& R, int tid, std::integer_sequence<int, J...>) {
-    auto one = [&](auto jc) __attribute__((always_inline)) {
-        constexpr int j = decltype(jc)::value;
-        const double v = row_sum16(col(jc));
-        if ((tid & 15) == 0) R.red[(tid >> 4) * kRedCols + j] = v;
-    };
-    (one(std::integral_constant<int, J>{}), ...);
+// col(std::integral_constant<int, j>) gives this thread's value of column j;
+// the block partials per 16-lane row:
+// a reduce-scatter butterfly over the 16 lanes of a row: each of 4 DPP exchange stages (row_mirror, row_half_mirror, two quad
+// permutations: symmetric pairings of lanes that hold the same columns) halves
+// the columns a lane holds and adds its partner's half, so a row's 32 columns
+// cost 16 + 8 + 4 + 2 exchanges and adds instead of 4 per column; lane l of a
+// row ends with columns base(l) + {0, 1}.
+template <int CTRL>
+__device__ __forceinline__ void bfly_stage(double* x, int m, bool low) {
+    // x[0..2m): a low lane keeps x[0..m) and sends x[m..2m); a high lane the other way
+#pragma unroll
+    for (int j = 0; j < m; j++) {
+        const double send = low ? x[m + j] : x[j];
+        const double keep = low ? x[j] : x[m + j];
+        x[j] = keep + dpp_f64<CTRL>(send);
+    }
 }
+template <int NU, class Col, int... J>
+__device__ __forceinline__ void hs_row_sums_bfly(const Col& col, HsReduceLds& R, int tid,
+                                                 std::integer_sequence<int, J...>) {
+    static_assert(NU <= 32, "32 columns per row");
+    double x[32];
+    auto get = [&](auto jc) __attribute__((always_inline)) {
+        constexpr int j = decltype(jc)::value;
+        if constexpr (j < NU) x[j] = col(jc);
+        else x[j] = 0.0;
+    };
+    (get(std::integral_constant<int, J>{}), ...);
+    const int l = tid & 15;
+    // partners hold the same columns at every stage: l <-> 15 - l, then 7 - l within
+    // each half-row, 3 - l within each quad, l ^ 1; the halves split by bits 3, 2, 1, 0
+    bfly_stage<0x140>(x, 16, (l & 8) == 0);  // row_mirror
+    bfly_stage<0x141>(x, 8, (l & 4) == 0);   // row_half_mirror
+    bfly_stage<0x1B>(x, 4, (l & 2) == 0);    // quad_perm [3,2,1,0]
+    bfly_stage<0xB1>(x, 2, (l & 1) == 0);    // quad_perm [1,0,3,2]
+    const int base = ((l & 8) ? 16 : 0) + ((l & 4) ? 8 : 0) + ((l & 2) ? 4 : 0) + ((l & 1) ? 2 : 0);
+    if (base < NU) R.red[(tid >> 4) * kRedCols + base] = x[0];
+    if (base + 1 < NU) R.red[(tid >> 4) * kRedCols + base + 1] = x[1];
+}
+
 template <int NT, int NU = kRedUsed, class Col>
 __device__ __forceinline__ void hshare_reduce_solve(const HsParams& P, const HsJob& job, IekfSlot* slot,
                                                     const Col& col, int nblk, unsigned blk, HsReduceLds& R,
@@ -2322,7 +2351,9 @@ __device__ __forceinline__ void hshare_reduce_solve(const HsParams& P, const HsJ
     constexpr int NR = NT / 16;  // 16-lane rows of the block
     static_assert(NR <= kRedRows, "HsReduceLds row partials");
     constexpr int NRM = NR > 16 ? NR : 16;  // rows of the fixed pairwise tree (16 for NT <= 256)
-    hs_row_sums(col, R, tid, std::make_integer_sequence<int, NU>{});
+    // (21.0k vs 20.2k updates/s over row_sum16 per column, evaluations without a
+    // search 0.107 vs 0.116 ms per step: profiles/r03_ab_bfly.txt)
+    hs_row_sums_bfly<NU>(col, R, tid, std::make_integer_sequence<int, 32>{});
     __syncthreads();
     // Wave 0 stores the block partial write-through (sc1) and, once the store
     // has drained, takes the scan's ticket; the last block of the scan then
