@@ -1136,6 +1136,7 @@ const char* livo_error_string(int code) {
         case LIVO_E_OOM: return "device allocation failed";
         case LIVO_E_RANGE: return "size out of supported range";
         case LIVO_E_CAPACITY: return "capacity exceeded";
+        case LIVO_E_BUSY: return "batches in flight (collect them with livo_iekf_update_batch_wait first)";
         default: return "unknown error";
     }
 }

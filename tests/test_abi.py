@@ -73,6 +73,25 @@ def test_invalid_arguments_return_codes(built):
     assert L.livo_ctx_create(0, C.byref(bad), C.byref(h)) == -1
     assert L.livo_map_build(None, None, 0, 0) == -1
     assert L.livo_sync(None) == -1
+    t = C.c_int32(-1)
+    assert L.livo_iekf_update_batch_submit(None, 0, None, None, None, C.byref(t)) == -1
+    assert L.livo_iekf_update_batch_wait(None, 0, None, None) == -1
+    assert L.livo_error_string(-8).startswith(b"batches in flight")  # LIVO_E_BUSY
+
+
+def test_knn_calibration_fixture():
+    """tests/golden/knn_calibration.json (tools/calibrate_knn.py): a timing calibration
+    of the oracle's k-NN against BASELINE.md's survey timing of the reference
+    ikd_Tree.cpp, one row per survey size; bench.py carries the 1M ratio."""
+    import json
+    cal = json.load(open(os.path.join(ROOT, "tests", "golden", "knn_calibration.json")))
+    assert cal["pins_parity"] is False
+    sizes = {r["map_points"]: r for r in cal["rows"]}
+    assert set(sizes) == {100_000, 1_000_000, 10_000_000}
+    for r in cal["rows"]:
+        lo, hi = r["reference_us_per_query"]
+        ratio = r["oracle_us_per_query"] / (0.5 * (lo + hi))
+        assert abs(ratio - r["ratio_oracle_over_reference"]) < 1e-2 and 0.05 < ratio < 20
 
 
 def test_no_gpu_fails_loudly(built):
