@@ -150,7 +150,25 @@ def ref_calibration() -> dict:
         return {"ref_calibration_ratio": None, "ref_calibration_note": "tests/golden/knn_calibration.json missing"}
 
 
-SET2_SEED = 100_000  # synth scan seeds of the second set of scans (pipelined farm)
+POOL_CAP = 1024  # most distinct scans a rank keeps resident (~17 MB of HBM each at 100k points)
+
+
+def gen_scans(n_points: int, seeds, workers: int):
+    """synth.make_scan of every seed (body points only), in a process pool before any GPU call."""
+    from livo_amd import synth
+    seeds = list(seeds)
+    if workers <= 1 or len(seeds) < 4:
+        return [synth.make_scan(n_points, s)[0] for s in seeds]
+    import concurrent.futures
+    import multiprocessing
+    with concurrent.futures.ProcessPoolExecutor(max_workers=workers,
+                                                mp_context=multiprocessing.get_context("fork")) as ex:
+        return list(ex.map(_scan_body, [(n_points, s) for s in seeds], chunksize=2))
+
+
+def _scan_body(arg):
+    from livo_amd import synth
+    return synth.make_scan(arg[0], arg[1])[0]
 
 
 # ------------------------------------------------------------------- PMC ----
@@ -222,22 +240,22 @@ def main():
     from livo_amd import farm, synth
 
     # inputs (identical generator on every rank; each rank its own scans), made
-    # before any GPU call so that the PMC children find the map in the cache
+    # before any GPU call so that the PMC children find the map in the cache.
+    # A pool of distinct scans (config 4's independent scans, seeds rank * pool
+    # + j): every batch of the warm-up and of the timed region takes the next
+    # a.batch of them, so no scan repeats within the timed region (up to
+    # POOL_CAP scans; beyond that the pool rotates, and the line says so)
     m = synth.cached_map(a.map_points)
-    scan_ids = [rank * a.batch + j for j in range(a.batch)]
-    scans = [synth.make_scan(a.scan_points, s)[0] for s in scan_ids]
-    st0 = [synth.make_state(s) for s in scan_ids]
-    # a second set of resident scans: the pipelined farm alternates two batches
-    # in flight and a scan belongs to one of them at a time.  By default the set
-    # is a second upload of the same scans, so every step does the work of the
-    # synchronous step it is compared with (sync_value); LIVO_BENCH_SET2=seeds
-    # draws 8 other scans instead (other poses in the room: a different load)
-    if os.environ.get("LIVO_BENCH_SET2") == "seeds":
-        scan_ids2 = [SET2_SEED + rank * a.batch + j for j in range(a.batch)]
-        scans2 = [synth.make_scan(a.scan_points, s)[0] for s in scan_ids2]
-        st02 = [synth.make_state(s) for s in scan_ids2]
-    else:
-        scans2, st02 = scans, st0
+    n_batches = max(1, min(POOL_CAP // a.batch, a.steps + max(a.warmup, 2)))
+    pool_n = n_batches * a.batch
+    pool_seeds = [rank * pool_n + j for j in range(pool_n)]
+    t = time.time()
+    pool_scans = gen_scans(a.scan_points, pool_seeds, min(16, host_threads()))
+    pool_st0 = [synth.make_state(s) for s in pool_seeds]
+    gen_s = time.time() - t
+    scan_ids = pool_seeds[:a.batch]  # the first batch: parity, latency, IKFoM / iVox legs, CPU baseline
+    scans = pool_scans[:a.batch]
+    st0 = pool_st0[:a.batch]
     kind = os.environ.get("LIVO_KNN_KIND", "tile")
     fused = kind == "tile" and os.environ.get("LIVO_FUSED", "1") != "0"
     unit_kernel = {"leaf": "k_knn_leaf<false", "grid": "k_knn_grid<false, false>"}.get(
@@ -274,32 +292,41 @@ def main():
     t = time.time()
     ctx.map_build(m)
     map_build_s = time.time() - t
-    sids = [ctx.scan_upload(s) for s in scans]
-    sids2 = [ctx.scan_upload(s) for s in scans2]
-    # V_ref: nodes the reference traversal visits for the first search of these
-    # scans (the reference-order pass k_knn_pass, outside the timed region):
-    # the reference-equivalent pricing of SURVEY.md §8d
+    pool_sids = [ctx.scan_upload(s) for s in pool_scans]
+    del pool_scans[a.batch:]  # the device holds them now
+    sids = pool_sids[:a.batch]
+    # V_ref: nodes the reference traversal visits for the first search of the
+    # first batch (the reference-order pass k_knn_pass, outside the timed
+    # region): the reference-equivalent pricing of SURVEY.md §8d, per query
     v_ref = sum(ctx.h_share(sid, s, search_en=True)["visits"] for sid, s in zip(sids, st0))
-    init = (livo_amd.State * a.batch)(*[livo_amd.state_to_c(s) for s in st0])
-    init2 = (livo_amd.State * a.batch)(*[livo_amd.state_to_c(s) for s in st02])
+    vq_ref = v_ref / max(sum(len(s) for s in scans), 1)
+    batches = []  # (scan ids, initial states) of each batch of the pool
+    for b in range(n_batches):
+        ids = pool_sids[b * a.batch:(b + 1) * a.batch]
+        batches.append((ids, (livo_amd.State * a.batch)(*[livo_amd.state_to_c(s) for s in
+                                                          pool_st0[b * a.batch:(b + 1) * a.batch]])))
+    init = batches[0][1]
     work = (livo_amd.State * a.batch)()
     nbytes = C.sizeof(init)
+    # the round-3 mode beside it: the first 8 scans every step (two uploads, since
+    # a scan is in one batch in flight at a time)
+    fixed = [(sids, init), ([ctx.scan_upload(s) for s in scans], init)]
 
-    def step():
-        """One synchronous batch (livo_iekf_update_batch): the profiled legs."""
-        C.memmove(work, init, nbytes)  # every step restarts the same scans from their priors
-        _, stats = ctx.iekf_update_batch(sids, work, raw=True)
+    def step(b=0):
+        """One synchronous batch (livo_iekf_update_batch) of pool batch b: the profiled legs."""
+        ids, ini = batches[b % n_batches]
+        C.memmove(work, ini, nbytes)  # the scans start from their priors
+        _, stats = ctx.iekf_update_batch(ids, work, raw=True)
         return stats
 
     # The farm's steady state: each step submits one batch of a.batch scans
     # (livo_iekf_update_batch_submit) and collects the batch submitted two steps
     # earlier, so the device always holds the next batch while the host collects
-    # one; the two sets of scans alternate.  Every submitted batch is collected
-    # before the clock stops.
-    sets = ((sids, init), (sids2, init2))
+    # one.  Every submitted batch is collected before the clock stops.
     outs = [((livo_amd.State * a.batch)(), (livo_amd.IterStats * a.batch)()) for _ in range(2)]
 
-    def pipeline(nsteps, counters=None):
+    def pipeline(nsteps, first, counters=None, sets=None):
+        """nsteps batches: pool batches first, first + 1, ... (or the two `sets` alternating)."""
         pending = []
         for k in range(nsteps):
             if len(pending) == livo_amd.MAX_INFLIGHT:
@@ -307,17 +334,20 @@ def main():
                 _, st = ctx.iekf_update_batch_wait(t, a.batch, *outs[j])
                 if counters is not None:
                     counters.add_stats(st)
+            ids, ini = sets[k % 2] if sets else batches[(first + k) % n_batches]
             j = k % 2
-            pending.append((ctx.iekf_update_batch_submit(sets[j][0], sets[j][1]), j))
+            pending.append((ctx.iekf_update_batch_submit(ids, ini), j))
         for t, j in pending:
             _, st = ctx.iekf_update_batch_wait(t, a.batch, *outs[j])
             if counters is not None:
                 counters.add_stats(st)
 
-    pipeline(max(a.warmup, 2))
-    for _ in range(a.warmup):
-        step()
-    first_stats = [livo_amd.stats_from_c(s) for s in step()]
+    # warm-up on the pool's last batches (the timed region starts at batch 0)
+    n_warm = max(a.warmup, 2)
+    pipeline(n_warm, n_batches - n_warm)
+    for w in range(a.warmup):
+        step(n_batches - 1 - w)
+    first_stats = [livo_amd.stats_from_c(s) for s in step(0)]
     first_states = [livo_amd.state_from_c(s) for s in work]
 
     counters = farm.Counters()
@@ -325,11 +355,19 @@ def main():
     barrier()
     sync()
     t0 = time.perf_counter()
-    pipeline(a.steps, counters)
+    pipeline(a.steps, 0, counters)
     sync()
     barrier()
     sync()
     elapsed = time.perf_counter() - t0
+    # the fixed-8 rate of round 3 (the same 8 scans every step), untimed for value
+    fixed_counters = farm.Counters()
+    pipeline(2, 0, sets=fixed)
+    sync()
+    t0f = time.perf_counter()
+    pipeline(a.steps, 0, fixed_counters, sets=fixed)
+    sync()
+    elapsed_fixed = time.perf_counter() - t0f
 
     # The same steps one synchronous batch at a time (the host waits for each
     # batch before the next is queued), untimed for the headline and reported
@@ -341,8 +379,8 @@ def main():
     knn_launches = knn_visits = knn_points = knn_queries = replays = 0
     sync()
     t0s = time.perf_counter()
-    for _ in range(a.steps):
-        step()
+    for k in range(a.steps):
+        step(k)
         tm = ctx.last_timings()
         knn_ms += tm["knn_ms"]
         knn_launches += tm["knn_launches"]
@@ -358,8 +396,8 @@ def main():
     n_gap = n_remevals = 0
     replays = 0
     t0p = time.perf_counter()
-    for _ in range(n_prof):
-        step()
+    for k in range(n_prof):
+        step(k)
         tm = ctx.last_timings()
         t_first += tm["knn_ms"]
         t_rematch += tm["rematch_knn_ms"]
@@ -384,7 +422,7 @@ def main():
     q_launch = knn_queries / L
     alg_bytes = (knn_visits / L) * B_SLOT + (knn_points / L) * B_POINT + q_launch * B_QUERY_IO
     achieved = alg_bytes / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
-    ref_equiv = (v_ref * B_NODE + q_launch * B_QUERY_REF) / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
+    ref_equiv = (vq_ref * q_launch * B_NODE + q_launch * B_QUERY_REF) / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
 
     result = None
     if rank == 0:
@@ -407,7 +445,7 @@ def main():
                 "limiter": ("dependent-load latency: the priced roofline is HBM (bound), but the measured limiter is the "
                             "chain hash probe -> run chunks per query (L2/MALL hits), not bytes (frac_hbm_traffic)"),
                 "reference_equivalent_GBps": round(ref_equiv, 1),
-                "visits_per_query_ref": round(v_ref / max(q_launch, 1), 3)}
+                "visits_per_query_ref": round(vq_ref, 3)}
         if pmc:
             roof["pmc"] = {k: v for k, v in pmc.items() if k != "hbm_bytes_per_launch"}
         result = {
@@ -430,15 +468,23 @@ def main():
                        "scans_per_step_per_gpu": a.batch, "parallelism": f"scan farm x{world}",
                        "collective": backend if world > 1 else None},
             "total_scans": total.scans,
-            "mode": ("pipelined farm: livo_iekf_update_batch_submit / _wait, two batches in flight per GPU "
-                     "(two alternating sets of resident scans, "
-                     + ("8 other scans" if os.environ.get("LIVO_BENCH_SET2") == "seeds" else
-                        "the second a second upload of the same 8") +
+            "mode": ("pipelined farm: livo_iekf_update_batch_submit / _wait, two batches in flight per GPU, "
+                     f"every batch the next {a.batch} of a pool of {pool_n} distinct resident scans per GPU "
+                     f"(seeds rank*{pool_n}+j; warm-up on the pool's last {n_warm} batches, the timed region from "
+                     "batch 0"
+                     + (", no scan repeated within it" if a.steps <= n_batches else
+                        f", rotating: the pool holds {n_batches} batches") +
                      "), every batch collected inside the timed region"),
+            "scan_pool": {"distinct_scans_per_gpu": pool_n, "batches": n_batches,
+                          "repeats_in_timed_region": a.steps > n_batches,
+                          "generation_s": round(gen_s, 2)},
+            "fixed8_value": round(world * fixed_counters.scans / elapsed_fixed, 3),
+            "fixed8_note": ("round 3's headline mode on this rank's GPU (scaled by the rank count): the same first 8 "
+                            "scans every step (two uploads alternating), pipelined like value; untimed for value"),
             "sync_value": round(world * a.batch * a.steps / elapsed_sync_max, 3),
             "sync_ms_per_step": round(elapsed_sync_max / a.steps * 1e3, 4),
-            "sync_note": ("the same steps with livo_iekf_update_batch (one batch at a time, the host waits for each); "
-                          "untimed for value"),
+            "sync_note": ("the same pool batches with livo_iekf_update_batch (one batch at a time, the host waits for "
+                          "each); untimed for value"),
             "iekf_steps_per_s": round(total.evals / elapsed_max, 3),
             "knn_queries_per_s": round((total.knn_passes * a.scan_points) / elapsed_max, 1),
             "evals_per_scan": round(total.evals / max(total.scans, 1), 3),

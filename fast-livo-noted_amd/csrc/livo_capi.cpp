@@ -1369,13 +1369,18 @@ static int build_cell_runs(livo_ctx* c, int64_t M) {
 // by rho2, a gather of the anchor keys and a stable sort by key leave each
 // anchor's run contiguous and sorted by rho2; heads, starts and the hash table
 // as for the cell runs.  r5: the map's median 5-NN distance (sample_knn_radius).
-static int build_ball_runs(livo_ctx* c, int64_t M, float r5) {
+static int build_ball_runs(livo_ctx* c, int64_t M, float r5, double ext) {
     dev_free(c->bslots);
     dev_free(c->bpts);
     c->bentries = 0;
     if (M <= 0 || !(r5 > 0.f)) return LIVO_OK;
     const float bh = std::max(c->br_ha * r5, 1e-3f);
     const float brmax = 0.8660254f * bh + c->br_r * r5;
+    // anchor keys are 21-bit per axis (grid_key, kGridBias = 2^20) and the device
+    // clamps a query's anchor to +-(kGridBias - 8): a map whose extent (+ the
+    // ball radius) spans that many anchors keeps the cell runs only, rather
+    // than letting keys alias into a run not sorted about its own anchor
+    if ((ext + 2.0 * (double)brmax) / (double)bh + 4.0 >= (double)(kGridBias - 8)) return LIVO_OK;
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     uint32_t* cnt = nullptr;
     uint32_t* off = nullptr;
@@ -1526,6 +1531,7 @@ int livo_map_build(livo_ctx* c, const float* xyz, int64_t M, int64_t stride_byte
     }
     if (!oom && e == hipSuccess) e = hipMemcpy(c->nodes, hm.nodes, bytes, hipMemcpyHostToDevice);
     const float r5 = (vr && c->bruns && c->knn_kind >= 1) ? sample_knn_radius(gm, 8192) : 0.f;
+    const double gext = gm.ext;
     free_host_map(&hm);
     free_leaf_map(&lm);
     free_grid_map(&gm);
@@ -1533,8 +1539,21 @@ int livo_map_build(livo_ctx* c, const float* xyz, int64_t M, int64_t stride_byte
     if (e != hipSuccess) return LIVO_E_HIP;
     if (vr) {
         rc = build_cell_runs(c, M);
-        if (!rc && r5 > 0.f) rc = build_ball_runs(c, M, r5);
         if (rc) return rc;
+        if (r5 > 0.f) {
+            // the ball runs are a speed-up over the cell runs: a map they do not
+            // fit (their scratch is ~68 B per entry, ~60 entries per point) keeps
+            // the cell runs and builds; other errors still fail the build
+            const int brc = build_ball_runs(c, M, r5, gext);
+            if (brc == LIVO_E_OOM) {
+                (void)hipGetLastError();
+                dev_free(c->bslots);
+                dev_free(c->bpts);
+                c->bentries = 0;
+            } else if (brc) {
+                return brc;
+            }
+        }
     }
     c->map_points = M;
     c->map_slots = hm.num_slots;
@@ -1782,6 +1801,10 @@ int livo_scan_neighbors(livo_ctx* c, int32_t id, int32_t* idx, float* sqdist) {
     if (!c) return LIVO_E_INVALID;
     ScanBuf* s = get_scan(c, id);
     if (!s || !s->searched) return LIVO_E_NOSCAN;
+    // a scan of a submitted batch is being searched on a group stream: its
+    // records are collected with the batch (livo_iekf_update_batch_wait) first
+    for (const BatchLane& B : c->lane)
+        if (B.busy && std::find(B.ids.begin(), B.ids.end(), id) != B.ids.end()) return LIVO_E_BUSY;
     if (set_device(c)) return LIVO_E_HIP;
     std::vector<NNRec> rec((size_t)s->n);
     if (s->n > 0) {
@@ -1951,10 +1974,16 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
                 for (int32_t id : c->lane[l].ids)
                     if (std::binary_search(sorted.begin(), sorted.end(), id)) return LIVO_E_INVALID;
     }
-    if (set_device(c)) return LIVO_E_HIP;
     const bool lm = model != kModelIkfom;
     // the IKFoM model stages in the context's whole slots: synchronous batches on lane 0 only
     if (!lm && (L != 0 || !sync)) return LIVO_E_INVALID;
+    // the fused evaluation: search + replay + plane pass + solve in one launch
+    const bool fused = c->fused && model == kModelLaserMapping && c->backend == LIVO_BACKEND_IKDTREE &&
+                       c->knn_kind == 2;
+    // the unfused passes' replay lists are per context: synchronous batches only
+    // (checked before any device work, so a refused submit leaves nothing queued)
+    if (!fused && (L != 0 || !sync)) return LIVO_E_INVALID;
+    if (set_device(c)) return LIVO_E_HIP;
     int rc = lane_streams(c, L);
     if (rc) return rc;
     rc = lm ? ensure_lm(B, n) : ensure_slots(c, n);
@@ -2030,9 +2059,6 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
         hipStream_t st;
     };
     Group g[kMaxGroups];
-    // the fused evaluation: search + replay + plane pass + solve in one launch
-    const bool fused = c->fused && model == kModelLaserMapping && c->backend == LIVO_BACKEND_IKDTREE &&
-                       c->knn_kind == 2;
     // default: two groups (8 x 100k: 1 / 2 / 3 / 4 groups 15463 / 16566 /
     // 15602 / 16365 updates/s, profiles/r03_ab_groups.txt), four beyond 1.2M
     // points (8 x 200k on the 10M map: 4437 vs 3960 with two): one group's
@@ -2057,8 +2083,6 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
             off += s->n;
         }
     }
-    // the unfused passes' replay lists are per context: synchronous batches only
-    if (!fused && (L != 0 || !sync)) return LIVO_E_INVALID;
     if (!fused) HIP_TRY(hipMemsetAsync(c->d_replay_count, 0, sizeof(unsigned) * kMaxGroups, c->stream));
     // profiling: the batch's first search starts at ev[0][0], before the fork
     if (prof) HIP_TRY(hipEventRecord(c->ev[0][0], c->stream));

@@ -114,6 +114,7 @@ struct HostGridMap {
     float org[3] = {0.f, 0.f, 0.f};
     float h = 1.f;
     float cmax = 0.f;           // largest |coordinate| (bounds the float rounding of cell bounds)
+    double ext = 0.0;           // largest axis extent of the map's bounding box
 };
 // cell_h <= 0: chosen from the map (about ppc_target points per occupied cell, 20 if 0;
 // ppc_target < 0: -ppc_target x clamp((M / 1M)^0.3, 1, 4), the cell runs' sizing)

@@ -1389,6 +1389,87 @@ __device__ __forceinline__ bool grid_search(LeafQuery& q, const KnnParams& P, in
     return false;
 }
 
+// ------------------------------------------------------------ run scan ----
+// One query's scan of a run sorted by rho2 (the squared distance of each entry
+// to the run's centre (cx, cy, cz); dqv >= |q - centre|): chunks of 8 entries,
+// a chunk's 8 distances offered to the list only when one of them is below e6,
+// and the scan stops at the first chunk whose first entry has rho > b = dqv +
+// sqrt(bound) (+ margins), every later entry being farther than the bound.
+// Returns the entries read.  The run array is padded by kRunPad entries.
+//
+// LIVO_RUN_PIPE = 1: two chunks in flight (A / B ping-pong): the loads of
+// chunk k+2 are issued as soon as chunk k is consumed, so a lane waits for one
+// load round trip per two chunks.  Chunk k+2 is not loaded when the run ends
+// before it or when chunk k's last entry is already beyond b (the entries are
+// sorted, so the scan stops at chunk k+1 at the latest).
+#ifndef LIVO_RUN_PIPE
+#define LIVO_RUN_PIPE 0
+#endif
+__device__ __forceinline__ float run_bound(const LeafQuery& q, float dqv) {
+    const float thr = lq_thr(q);
+    return thr < INFINITY ? dqv + __builtin_amdgcn_sqrtf(thr) * (1.0f + 1e-6f) + 1e-4f : INFINITY;
+}
+__device__ __forceinline__ void run_chunk(LeafQuery& q, const float4 (&v)[8], uint32_t k0, uint32_t cnt,
+                                          uint32_t pos0) {
+    float dist[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+        const float dx = q.qx - v[u].x, dy = q.qy - v[u].y, dz = q.qz - v[u].z;
+        const float d = (dx * dx + dy * dy) + dz * dz;  // calc_dist (:1291-1295)
+        dist[u] = k0 + u < cnt ? d : INFINITY;
+    }
+    const float m = fminf(fminf(fminf(dist[0], dist[1]), fminf(dist[2], dist[3])),
+                          fminf(fminf(dist[4], dist[5]), fminf(dist[6], dist[7])));
+    if (m < q.e6) {
+#pragma unroll
+        for (int u = 0; u < 8; u++) lq_offer(q, dist[u], kRunPos | (pos0 + k0 + u));
+    }
+}
+__device__ __forceinline__ uint32_t scan_run(LeafQuery& q, const float4* __restrict__ run, uint32_t cnt, uint32_t lo,
+                                             float cx, float cy, float cz, float dqv) {
+    uint32_t k0 = 0;
+#if LIVO_RUN_PIPE
+    if (cnt == 0) return 0;
+    float4 A[8], B[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) A[u] = run[u];
+    if (cnt > 8) {
+#pragma unroll
+        for (int u = 0; u < 8; u++) B[u] = run[8 + u];
+    }
+    // one chunk: stop test, distances, then the loads two chunks ahead into the same registers
+    auto step = [&](float4 (&v)[8]) __attribute__((always_inline)) -> bool {
+        const float b = run_bound(q, dqv);
+        if (centre_d2(cx, cy, cz, v[0].x, v[0].y, v[0].z) > b * b) return false;  // rho of every later entry > b
+        run_chunk(q, v, k0, cnt, lo);
+        const float b2 = run_bound(q, dqv);
+        const bool more = k0 + 16 < cnt && !(centre_d2(cx, cy, cz, v[7].x, v[7].y, v[7].z) > b2 * b2);
+        if (more) {
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] = run[k0 + 16 + u];
+        }
+        k0 += 8;
+        return k0 < cnt;
+    };
+#pragma unroll 1
+    while (true) {
+        if (!step(A)) break;
+        if (!step(B)) break;
+    }
+#else
+#pragma unroll 1
+    for (; k0 < cnt; k0 += 8) {
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = run[k0 + u];  // padded by kRunPad entries
+        const float b = run_bound(q, dqv);
+        if (centre_d2(cx, cy, cz, v[0].x, v[0].y, v[0].z) > b * b) break;  // rho of every later entry > b
+        run_chunk(q, v, k0, cnt, lo);
+    }
+#endif
+    return min(k0, cnt);
+}
+
 // ------------------------------------------------------------ cell-run search ----
 // The batched IEKF search on the cell runs (livo_internal.h): the run of the
 // query's own cell c holds every map point of the 3x3x3 cells around c (the
@@ -1425,32 +1506,7 @@ __device__ __forceinline__ bool vrun_search(LeafQuery& q, const KnnParams& P, bo
     const float cz = cell_centre(P.gorg[2], h, c2);
     const float dqv = __builtin_amdgcn_sqrtf(centre_d2(cx, cy, cz, q.qx, q.qy, q.qz)) * (1.0f + 1e-6f);
     const float4* __restrict__ run = reinterpret_cast<const float4*>(P.vpts) + lo;
-    uint32_t k0 = 0;
-#pragma unroll 1
-    for (; k0 < cnt; k0 += 8) {
-        float4 v[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) v[u] = run[k0 + u];  // padded by 8 entries
-        const float thr = lq_thr(q);
-        if (thr < INFINITY) {
-            const float b = dqv + __builtin_amdgcn_sqrtf(thr) * (1.0f + 1e-6f) + 1e-4f;
-            if (centre_d2(cx, cy, cz, v[0].x, v[0].y, v[0].z) > b * b) break;  // rho of every later entry > b
-        }
-        float dist[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const float dx = q.qx - v[u].x, dy = q.qy - v[u].y, dz = q.qz - v[u].z;
-            const float d = (dx * dx + dy * dy) + dz * dz;  // calc_dist (:1291-1295)
-            dist[u] = k0 + u < cnt ? d : INFINITY;
-        }
-        const float m = fminf(fminf(fminf(dist[0], dist[1]), fminf(dist[2], dist[3])),
-                              fminf(fminf(dist[4], dist[5]), fminf(dist[6], dist[7])));
-        if (m < q.e6) {
-#pragma unroll
-            for (int u = 0; u < 8; u++) lq_offer(q, dist[u], kRunPos | (lo + k0 + u));
-        }
-    }
-    npts += min(k0, cnt);
+    npts += scan_run(q, run, cnt, lo, cx, cy, cz, dqv);
     // certified when the ball of the final bound lies in the cube [c - 1, c + 1]
     const float t = lq_thr(q);
     if (t < INFINITY) {
@@ -1514,32 +1570,7 @@ __device__ __forceinline__ bool brun_search(LeafQuery& q, const KnnParams& P, bo
     const float cz = cell_centre(P.gorg[2], P.bh, a[2]);
     const float dqv = __builtin_amdgcn_sqrtf(centre_d2(cx, cy, cz, q.qx, q.qy, q.qz)) * (1.0f + 1e-6f);
     const float4* __restrict__ run = reinterpret_cast<const float4*>(P.bpts) + lo;
-    uint32_t k0 = 0;
-#pragma unroll 1
-    for (; k0 < cnt; k0 += 8) {
-        float4 v[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) v[u] = run[k0 + u];  // padded by 8 entries
-        const float thr = lq_thr(q);
-        if (thr < INFINITY) {
-            const float b = dqv + __builtin_amdgcn_sqrtf(thr) * (1.0f + 1e-6f) + 1e-4f;
-            if (centre_d2(cx, cy, cz, v[0].x, v[0].y, v[0].z) > b * b) break;  // rho of every later entry > b
-        }
-        float dist[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const float dx = q.qx - v[u].x, dy = q.qy - v[u].y, dz = q.qz - v[u].z;
-            const float d = (dx * dx + dy * dy) + dz * dz;  // calc_dist (:1291-1295)
-            dist[u] = k0 + u < cnt ? d : INFINITY;
-        }
-        const float m = fminf(fminf(fminf(dist[0], dist[1]), fminf(dist[2], dist[3])),
-                              fminf(fminf(dist[4], dist[5]), fminf(dist[6], dist[7])));
-        if (m < q.e6) {
-#pragma unroll
-            for (int u = 0; u < 8; u++) lq_offer(q, dist[u], kRunPos | (lo + k0 + u));
-        }
-    }
-    npts += min(k0, cnt);
+    npts += scan_run(q, run, cnt, lo, cx, cy, cz, dqv);
     const float t = lq_thr(q);
     if (!(t < INFINITY)) return false;
     const float b = dqv + __builtin_amdgcn_sqrtf(t) * (1.0f + 1e-6f) + 1e-4f;

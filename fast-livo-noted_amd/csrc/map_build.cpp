@@ -402,6 +402,8 @@ int build_grid_map(const float* xyz, int64_t M, int64_t stride_bytes, float cell
     for (int k = 0; k < 3; k++) out->org[k] = mn[k];
     out->h = h;
     out->cmax = 0.f;
+    out->ext = 0.0;
+    for (int k = 0; k < 3; k++) out->ext = std::max(out->ext, (double)mx[k] - (double)mn[k]);
     for (int k = 0; k < 3; k++) out->cmax = std::max(out->cmax, std::max(std::fabs(mn[k]), std::fabs(mx[k])));
     return LIVO_OK;
 }

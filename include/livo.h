@@ -51,7 +51,10 @@
 extern "C" {
 #endif
 
-#define LIVO_ABI_VERSION 3
+/* 4: livo_timings grew the per-evaluation fields (eval_ms ... gap_ms), LIVO_E_BUSY
+ *    and the submit / wait pair were added (round 3); a binary built against 3
+ *    passes a smaller livo_timings. */
+#define LIVO_ABI_VERSION 4
 #define LIVO_DIM_STATE 18        /* DIM_STATE, include/common_lib.h:32 */
 #define LIVO_NUM_MATCH_POINTS 5  /* NUM_MATCH_POINTS, include/common_lib.h:37 */
 #define LIVO_MAX_EVALS 16        /* max h_share/solve evaluations per scan update */
@@ -216,7 +219,12 @@ int livo_iekf_update_batch(livo_ctx* ctx, int32_t n, const int32_t* scan_ids, li
  * stats (may be NULL).  At most LIVO_MAX_INFLIGHT batches per context are
  * submitted and not yet waited for (LIVO_E_BUSY beyond), and a scan may be in
  * one of them only (LIVO_E_INVALID).  While a batch is in flight its scans
- * may not be released, and the map may not be rebuilt or changed (LIVO_E_BUSY). */
+ * may not be released, and the map may not be rebuilt or changed (LIVO_E_BUSY),
+ * and livo_scan_neighbors of one of its scans returns LIVO_E_BUSY.  submit
+ * needs the fused ikd-Tree path (the default: LIVO_BACKEND_IKDTREE, no
+ * LIVO_FUSED=0 / LIVO_KNN_KIND override): otherwise it returns LIVO_E_INVALID
+ * before queuing anything, and livo_iekf_update_batch does the same update
+ * synchronously. */
 #define LIVO_MAX_INFLIGHT 2
 int livo_iekf_update_batch_submit(livo_ctx* ctx, int32_t n, const int32_t* scan_ids, const livo_state* states,
                                   const livo_state* priors, int32_t* ticket);

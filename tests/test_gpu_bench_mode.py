@@ -58,16 +58,18 @@ def test_golden_fixture(built):
 
 
 @pytest.mark.slow
-def test_bench_headline_mode_parity(built):
+@pytest.mark.parametrize("seed0", [0, 8, 176])
+def test_bench_headline_mode_parity(built, seed0):
     """8 x 100k scans, 1M map, one livo_iekf_update_batch in the default stream
     grouping (two groups at 800k points: the bench's step): per scan, the oracle's iterations, k-NN passes,
-    effective points and per-evaluation state deltas."""
+    effective points and per-evaluation state deltas.  seed0: the bench pool's
+    first batch (0), its second (8) and its last at the default 20 + 3 steps (176)."""
     import livo_amd
     import oracle
     from livo_amd import synth
     m = synth.cached_map(1_000_000)
-    scans = [synth.make_scan(100_000, s)[0] for s in range(8)]
-    states = [synth.make_state(s) for s in range(8)]
+    scans = [synth.make_scan(100_000, seed0 + s)[0] for s in range(8)]
+    states = [synth.make_state(seed0 + s) for s in range(8)]
     with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=4) as ctx:
         ctx.map_build(m)
         sids = [ctx.scan_upload(b) for b in scans]
@@ -146,6 +148,54 @@ def test_submit_wait_pipeline(built):
         _same_update(outs["b0"][k], ref[4 + k])
     for k in range(8):
         _same_update(sync2[k], ref[k])
+
+
+@pytest.mark.parametrize("serial", ["0", "1"])
+def test_submit_mixed_groups_out_of_order(built, monkeypatch, serial):
+    """Two batches in flight on the shared streams with different stream-group
+    counts (13 x 100k = 1.3M points -> 4 groups, beside 2 x 50k -> 2 groups),
+    the second ticket waited for first, with LIVO_LANE_SERIAL 0 (default) and
+    1: each batch equals its synchronous update bit for bit.  While the batches
+    are in flight livo_scan_neighbors of one of their scans is LIVO_E_BUSY; a
+    submit on the iVox backend is refused (LIVO_E_INVALID) before anything is
+    queued, and a synchronous batch runs right after it."""
+    import livo_amd
+    from livo_amd import synth
+    monkeypatch.setenv("LIVO_LANE_SERIAL", serial)
+    m = synth.cached_map(1_000_000)
+    big = [synth.make_scan(100_000, 300 + s)[0] for s in range(13)]
+    small = [synth.make_scan(50_000, 400 + s)[0] for s in range(2)]
+    st_big = [synth.make_state(300 + s) for s in range(13)]
+    st_small = [synth.make_state(400 + s) for s in range(2)]
+    with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=4) as ctx:
+        ctx.map_build(m)
+        sb = [ctx.scan_upload(b) for b in big]
+        ss = [ctx.scan_upload(b) for b in small]
+        ref_b = list(zip(*ctx.iekf_update_batch(sb, st_big)))
+        ref_s = list(zip(*ctx.iekf_update_batch(ss, st_small)))
+        for _ in range(2):
+            tb = ctx.iekf_update_batch_submit(sb, st_big)
+            ts = ctx.iekf_update_batch_submit(ss, st_small)
+            with pytest.raises(livo_amd.LivoError) as e:
+                ctx.scan_neighbors(ss[0])
+            assert e.value.code == -8
+            out_s = list(zip(*ctx.iekf_update_batch_wait(ts, 2)))  # the later ticket first
+            out_b = list(zip(*ctx.iekf_update_batch_wait(tb, 13)))
+            for k in range(2):
+                _same_update(out_s[k], ref_s[k])
+            for k in range(13):
+                _same_update(out_b[k], ref_b[k])
+        idx, _ = ctx.scan_neighbors(ss[0])  # collected: readable again
+        assert idx.shape == (50_000, 5)
+        ctx.set_backend(livo_amd.BACKEND_IVOX)
+        ctx.ivox_init()
+        ctx.ivox_add_points(m)
+        with pytest.raises(livo_amd.LivoError) as e:
+            ctx.iekf_update_batch_submit(ss, st_small)
+        assert e.value.code == -1
+        st_iv, stats_iv = ctx.iekf_update_batch(ss, st_small)  # nothing left queued
+        assert all(s["iterations"] >= 1 for s in stats_iv)
+        ctx.set_backend(livo_amd.BACKEND_IKDTREE)
 
 
 def test_bench_two_ranks(built):
