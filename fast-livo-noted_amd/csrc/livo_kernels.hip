@@ -2554,6 +2554,8 @@ struct EvalParams {
 #ifdef LIVO_EVAL_PROF  // per-phase block time of k_iekf_eval (tools/eval_prof.py; compiled out of the product)
 // [search][phase]: cycles summed over blocks (thread 0's s_memtime deltas) and block counts
 __device__ unsigned long long g_eval_prof[3][8];  // [no search / rematch / first search][phase]
+// [kind][stat]: lanes, ball-certified, cell-run lanes, ball entries (sum, wave max), cell entries (sum, wave max), waves
+__device__ unsigned long long g_eval_stats[3][8];
 #define EVAL_MARK(k)                                                                                   \
     do {                                                                                               \
         if (threadIdx.x == 0) {                                                                        \
@@ -2625,17 +2627,51 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
             EVAL_MARK(1);
             bool certified = false;
             const float4* runs = reinterpret_cast<const float4*>(P.vpts);
+#ifdef LIVO_EVAL_PROF
+            const unsigned np0 = npts;
+            bool ball_ok = false;
+#endif
             if (P.bslots) {  // (uniform) the ball runs first; the cell runs for a query they do not certify
                 certified = brun_search(q, P, valid, visits, npts);
                 if (certified) runs = reinterpret_cast<const float4*>(P.bpts);
                 if (valid && !certified) lq_init<false>(q, P, slot, job, i, valid);
+#ifdef LIVO_EVAL_PROF
+                ball_ok = certified;
+#endif
             }
+#ifdef LIVO_EVAL_PROF
+            const unsigned np1 = npts;
+#endif
             if (!certified) certified = vrun_search(q, P, valid, c0, c1, c2, s0, s1, s2, visits, npts);
 #ifdef LIVO_EVAL_PROF
             {  // block totals: lanes past the 2x2x2 block, run entries scanned, ambiguous
                 const unsigned long long nf = __ballot(valid && !certified);
                 if ((threadIdx.x & 63) == 0) {
                     atomicAdd(&g_eval_prof[FIRST ? 2 : 1][7], (unsigned long long)__popcll(nf));
+                }
+                // search statistics per evaluation kind: lanes, ball-certified lanes,
+                // entries scanned in the ball / cell stage (sum over lanes and the
+                // per-wave maximum: the wave runs its slowest lane's chunks)
+                const unsigned nb = valid ? np1 - np0 : 0u, nc = valid ? npts - np1 : 0u;
+                unsigned mb = nb, mc = nc, sb = nb, sc = nc;
+                for (int o = 1; o < 64; o <<= 1) {
+                    mb = max(mb, (unsigned)__shfl_xor((int)mb, o));
+                    mc = max(mc, (unsigned)__shfl_xor((int)mc, o));
+                    sb += (unsigned)__shfl_xor((int)sb, o);
+                    sc += (unsigned)__shfl_xor((int)sc, o);
+                }
+                const unsigned long long nv = __ballot(valid), nbo = __ballot(valid && ball_ok);
+                const unsigned long long ncr = __ballot(valid && !ball_ok && nc > 0);
+                if ((threadIdx.x & 63) == 0) {
+                    unsigned long long* g = g_eval_stats[FIRST ? 2 : (search ? 1 : 0)];
+                    atomicAdd(g + 0, (unsigned long long)__popcll(nv));
+                    atomicAdd(g + 1, (unsigned long long)__popcll(nbo));
+                    atomicAdd(g + 2, (unsigned long long)__popcll(ncr));
+                    atomicAdd(g + 3, (unsigned long long)sb);
+                    atomicAdd(g + 4, (unsigned long long)mb);
+                    atomicAdd(g + 5, (unsigned long long)sc);
+                    atomicAdd(g + 6, (unsigned long long)mc);
+                    atomicAdd(g + 7, 1ull);
                 }
             }
             EVAL_MARK(5);
@@ -3289,6 +3325,12 @@ extern "C" int livo_debug_eval_prof(unsigned long long* out) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_eval_prof), sizeof(g_eval_prof)) != hipSuccess) return LIVO_E_HIP;
     static const unsigned long long zero[24] = {};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_eval_prof), zero, sizeof(zero)) == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+extern "C" int livo_debug_eval_stats(unsigned long long* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return LIVO_E_HIP;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_eval_stats), sizeof(g_eval_stats)) != hipSuccess) return LIVO_E_HIP;
+    static const unsigned long long zero[24] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_eval_stats), zero, sizeof(zero)) == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 #endif
 

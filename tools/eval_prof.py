@@ -33,11 +33,21 @@ def main():
         L.livo_debug_eval_prof.argtypes = [C.c_void_p]
         buf = (C.c_ulonglong * 24)()
         ctx.iekf_update_batch(sids, st0)
+        L.livo_debug_eval_stats.argtypes = [C.c_void_p]
+        sbuf = (C.c_ulonglong * 24)()
         L.livo_debug_eval_prof(buf)  # reset after the warm-up
+        L.livo_debug_eval_stats(sbuf)
         steps = 10
         for _ in range(steps):
             ctx.iekf_update_batch(sids, st0)
         assert L.livo_debug_eval_prof(buf) == 0
+        assert L.livo_debug_eval_stats(sbuf) == 0
+        for s, name in ((2, "first-search evals"), (1, "rematch evals")):
+            r = sbuf[8 * s: 8 * s + 8]
+            lanes, waves = max(r[0], 1), max(r[7], 1)
+            print(f"{name} search: lanes {r[0]}  ball-certified {r[1] / lanes:.3f}  cell-run lanes {r[2] / lanes:.3f}  "
+                  f"ball entries/lane {r[3] / lanes:.1f} (wave max {r[4] / waves:.1f})  "
+                  f"cell entries/lane {r[5] / lanes:.1f} (wave max {r[6] / waves:.1f})")
         for s, name in ((2, "first-search evals"), (1, "rematch evals"), (0, "no-search evals")):
             row = buf[8 * s: 8 * s + 8]
             nb = max(row[0], 1)

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--max-iter", type=int, default=4)
     ap.add_argument("--seed0", type=int, default=0, help="first scan seed")
     ap.add_argument("--config5", action="store_true")
+    ap.add_argument("--fresh", action="store_true", help="every batch other scans (the bench's distinct-scan pool)")
     a = ap.parse_args()
     if a.config5:
         m = synth.cached_map(10_000_000)
@@ -42,6 +43,15 @@ def main():
                 raw, poses, Re, pe = synth.make_config5_frame(1000 + s)
                 sids.append(ctx.scan_preprocess(raw, poses, Re, pe, leaf_size=synth.CONFIG5_LEAF)[0])
             st0 = [synth.make_state(1000 + s) for s in seeds]
+        elif a.fresh:
+            nb = 1 + a.steps
+            seeds = [a.seed0 + s for s in range(nb * a.batch)]
+            sids = [ctx.scan_upload(synth.make_scan(a.scan_points, s)[0]) for s in seeds]
+            st0 = [synth.make_state(s) for s in seeds]
+            for b in range(nb):
+                ctx.iekf_update_batch(sids[b * a.batch:(b + 1) * a.batch], st0[b * a.batch:(b + 1) * a.batch])
+            print("probe done", flush=True)
+            return
         else:
             sids = [ctx.scan_upload(synth.make_scan(a.scan_points, s)[0]) for s in seeds]
             st0 = [synth.make_state(s) for s in seeds]
