@@ -709,6 +709,62 @@ __global__ void k_br_fill(const float4* __restrict__ gpts, const uint32_t* __res
     bpts[i] = gpts[pt[e2[i]]];  // x, y, z, map index bits
     heads[i] = (i == 0 || skeys[i] != skeys[i - 1]) ? 1u : 0u;
 }
+// ---- index runs (LIVO_IDX_RUNS): a run = an aligned segment of grid positions ----
+__global__ void k_run_heads(const unsigned long long* __restrict__ skeys, int64_t n, uint32_t* heads) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) heads[i] = (i == 0 || skeys[i] != skeys[i - 1]) ? 1u : 0u;
+}
+__global__ void k_run_plen(const uint32_t* __restrict__ starts, int64_t nruns, uint32_t* plen) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < nruns) plen[r] = (starts[r + 1] - starts[r] + 3u) & ~3u;
+}
+__global__ void k_run_place(const uint32_t* __restrict__ e2, const uint32_t* __restrict__ pt,
+                            const uint32_t* __restrict__ heads, const uint32_t* __restrict__ runid,
+                            const uint32_t* __restrict__ starts, const uint32_t* __restrict__ pstart, int64_t n,
+                            uint32_t* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t r = runid[i] + heads[i] - 1u;  // runid: exclusive scan of the heads
+    const uint32_t pos = pt ? pt[e2[i]] : e2[i] / 27u;
+    out[pstart[r] + ((uint32_t)i - starts[r])] = pos;
+}
+__global__ void k_run_slots(const unsigned long long* __restrict__ skeys, const uint32_t* __restrict__ starts,
+                            const uint32_t* __restrict__ pstart, int64_t nruns, GridSlot* slots, int log2) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nruns) return;
+    const uint32_t s0 = starts[r], s1 = starts[r + 1];
+    const unsigned long long key = skeys[s0];
+    const uint64_t mask = (1ull << log2) - 1ull;
+    uint64_t sl = (uint64_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - log2));
+    while (atomicCAS(&slots[sl].key, kGridEmpty, key) != kGridEmpty) sl = (sl + 1) & mask;
+    slots[sl].start = pstart[r];
+    slots[sl].count = s1 - s0;
+}
+// ---- runs on the incremental map: base point positions, deletion marks ----
+__global__ void k_dyn_rpos(const float4* __restrict__ rpts, int64_t base_n, uint32_t* rpos) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < base_n) rpos[__float_as_uint(rpts[k].w)] = (uint32_t)k;
+}
+__global__ void k_dyn_tomb(float4* rpts, uint32_t* rpos, const uint8_t* __restrict__ alive, int64_t base_ids,
+                           unsigned long long* ctr) {
+    const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t marked = 0;
+    if (id < base_ids) {
+        const uint32_t p = rpos[id];
+        if (p != 0xFFFFFFFFu && !alive[id]) {
+            rpts[p].x = __uint_as_float(0x7FC00000u);  // NaN: never a candidate (livo_kernels.hip scan_run)
+            rpos[id] = 0xFFFFFFFFu;
+            marked = 1;
+        }
+    }
+    const unsigned long long b = __ballot(marked);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(ctr + kDynTomb, (unsigned long long)__popcll(b));
+}
+__global__ void k_count_alive(const uint8_t* __restrict__ alive, int64_t n, unsigned long long* ctr) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned long long b = __ballot(i < n && alive[i]);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(ctr + kDynAliveCnt, (unsigned long long)__popcll(b));
+}
 __global__ void k_add_u32(uint32_t* v, int64_t n, uint32_t add) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) v[i] += add;
@@ -823,6 +879,30 @@ int launch_br_fill(const float* gpts, const uint32_t* pt, const uint32_t* e2, co
                reinterpret_cast<float4*>(bpts), heads);
 }
 int launch_add_u32(uint32_t* v, int64_t n, uint32_t add, void* stream) { DYN_LAUNCH(k_add_u32, n, v, n, add); }
+int launch_dyn_rpos(const float* rpts, int64_t base_n, uint32_t* rpos, void* stream) {
+    DYN_LAUNCH(k_dyn_rpos, base_n, reinterpret_cast<const float4*>(rpts), base_n, rpos);
+}
+int launch_dyn_tomb(float* rpts, uint32_t* rpos, const uint8_t* alive, int64_t base_ids, unsigned long long* ctr,
+                    void* stream) {
+    DYN_LAUNCH(k_dyn_tomb, base_ids, reinterpret_cast<float4*>(rpts), rpos, alive, base_ids, ctr);
+}
+int launch_count_alive(const uint8_t* alive, int64_t n, unsigned long long* ctr, void* stream) {
+    DYN_LAUNCH(k_count_alive, n, alive, n, ctr);
+}
+int launch_run_heads(const unsigned long long* skeys, int64_t n, uint32_t* heads, void* stream) {
+    DYN_LAUNCH(k_run_heads, n, skeys, n, heads);
+}
+int launch_run_plen(const uint32_t* starts, int64_t nruns, uint32_t* plen, void* stream) {
+    DYN_LAUNCH(k_run_plen, nruns, starts, nruns, plen);
+}
+int launch_run_place(const uint32_t* e2, const uint32_t* pt, const uint32_t* heads, const uint32_t* runid,
+                     const uint32_t* starts, const uint32_t* pstart, int64_t n, uint32_t* out, void* stream) {
+    DYN_LAUNCH(k_run_place, n, e2, pt, heads, runid, starts, pstart, n, out);
+}
+int launch_run_slots(const unsigned long long* skeys, const uint32_t* starts, const uint32_t* pstart, int64_t nruns,
+                     GridSlot* slots, int log2, void* stream) {
+    DYN_LAUNCH(k_run_slots, nruns, skeys, starts, pstart, nruns, slots, log2);
+}
 int launch_dyn_delete_boxes(const float* all, uint8_t* alive, int64_t n_ids, const float* boxes, int64_t nb,
                             unsigned long long* cnt, void* stream) {
     DYN_LAUNCH(k_dyn_delete_boxes, n_ids, reinterpret_cast<const float4*>(all), alive, n_ids, boxes, nb, cnt);

@@ -117,6 +117,24 @@ struct DynDev {
     unsigned long long *dirty = nullptr, *ctr = nullptr;
     int64_t gslot_cap = 0, gpts_cap = 0;  // capacities of ctx->gslots / ctx->gpts
     livo_map_add_stats last{};
+    // The IEKF search keeps the cell and ball runs on the incremental map
+    // (LIVO_IDX_RUNS): the runs index the base point set rpts (the map's points
+    // in grid order when the runs were built; ids below base_ids), a deleted
+    // base point is marked in rpts (x = NaN, never a candidate of the run scans), and
+    // the points added since are searched in the delta grid (dslots / dpts, the
+    // cell grid's layout).  When the delta or the deleted share grows past
+    // rebase_frac of the base the runs are rebuilt from the current points.
+    bool runs = false;
+    float* rpts = nullptr;           // base points: x, y, z, id bits (x = NaN once deleted)
+    uint32_t* rpos = nullptr;        // base id -> position in rpts (~0: not in the base / marked)
+    int64_t base_ids = 0, base_n = 0, rpts_cap = 0, rpos_cap = 0;
+    int64_t tomb = 0;                // base points marked deleted
+    GridSlot* dslots = nullptr;
+    float* dpts = nullptr;
+    int32_t dlog2 = 4;
+    int64_t d_n = 0, dslot_cap = 0, dpts_cap = 0;
+    int64_t rebases = 0;
+    double rebase_frac = 0.125;      // LIVO_DYN_REBASE
 };
 
 // One batch's staging and streams.  LaserMapping batches: slots packed at
@@ -171,13 +189,13 @@ struct livo_ctx {
     bool vruns = true;                 // cell runs on a static map (LIVO_VRUNS=0: the cell walk)
     int xcd_chunk = 0;                 // k_iekf_eval block order (LIVO_XCD_CHUNK; 0: one range per XCD)
     GridSlot* vslots = nullptr;        // vertex runs (static map only)
-    float* vpts = nullptr;             // run entries (x, y, z, map index bits)
+    RunWord* vpts = nullptr;           // run entries (LIVO_IDX_RUNS: grid positions; else x, y, z, map index bits)
     int32_t vlog2 = 0;
     // ball runs (static map only): anchor cells of edge bh, runs of radius brmax
     bool bruns = true;                 // LIVO_BRUNS=0: the cell runs only
     float br_ha = 2.0f, br_r = 3.2f;   // bh = br_ha r5, brmax = sqrt(3)/2 bh + br_r r5 (LIVO_BR_HA / LIVO_BR_R)
     GridSlot* bslots = nullptr;
-    float* bpts = nullptr;
+    RunWord* bpts = nullptr;
     int32_t blog2 = 0;
     float bh = 0.f, brmax = 0.f, br5 = 0.f;
     int64_t bentries = 0;
@@ -411,8 +429,15 @@ static KnnParams make_knn_params(livo_ctx* c) {
     kp.gh = c->gh;
     kp.geps = c->geps;
     kp.glog2 = c->glog2;
-    // the incremental map keeps the cell walk (its grid is rebuilt on the device)
-    const bool vr = c->vslots && !c->dyn.active;
+    // the incremental map keeps the runs of its base point set (+ deletion marks
+    // and the delta grid, dyn_runs_update) or, without them, the cell walk
+    const bool dyn_runs = c->dyn.active && c->dyn.runs;
+    const bool vr = c->vslots && (!c->dyn.active || dyn_runs);
+    kp.rpts = dyn_runs ? c->dyn.rpts : c->gpts;
+    kp.dslots = dyn_runs && c->dyn.d_n > 0 ? c->dyn.dslots : nullptr;
+    kp.dpts = dyn_runs ? c->dyn.dpts : nullptr;
+    kp.dlog2 = c->dyn.dlog2;
+    kp.dyn_runs = dyn_runs ? 1 : 0;
     kp.vslots = vr ? c->vslots : nullptr;
     kp.vpts = vr ? c->vpts : nullptr;
     kp.vlog2 = c->vlog2;
@@ -869,6 +894,8 @@ static int backend_knn(livo_ctx* c, const KnnParams& kp, int n_jobs, int64_t max
 extern "C" {
 static ScanBuf* get_scan(livo_ctx* c, int32_t id);
 }
+static int build_cell_runs(livo_ctx* c, int64_t M);
+static int build_ball_runs(livo_ctx* c, int64_t M, float r5, double ext);
 static void dyn_free(DynDev& d) {
     dev_free(d.all); dev_free(d.alive);
     dev_free(d.keys); dev_free(d.skeys); dev_free(d.iota); dev_free(d.svals);
@@ -876,6 +903,7 @@ static void dyn_free(DynDev& d) {
     dev_free(d.W); dev_free(d.seq); dev_free(d.Ws);
     dev_free(d.defer); dev_free(d.dpos); dev_free(d.dlist); dev_free(d.keep); dev_free(d.apos);
     dev_free(d.boxes); dev_free(d.dirty); dev_free(d.ctr);
+    dev_free(d.rpts); dev_free(d.rpos); dev_free(d.dslots); dev_free(d.dpts);
     d = DynDev{};
 }
 
@@ -944,6 +972,131 @@ static int sort_u64(livo_ctx* c, const unsigned long long* kin, unsigned long lo
     return rc;
 }
 
+// The runs' base point set = the current cell grid (c->gpts, c->map_points
+// points in grid order; the runs were built on it): rpts a copy of it (the
+// grid itself is rebuilt by every change), rpos the position of each id,
+// ids below n_ids the base, no deletion marks, an empty delta.
+static int dyn_base_from_grid(livo_ctx* c) {
+    DynDev& d = c->dyn;
+    d.runs = false;
+    const int64_t na = c->map_points;
+    if (d.rpts_cap < na + 3) {
+        dev_free(d.rpts);
+        d.rpts_cap = 0;
+        const int64_t cap = (na + 3) + ((na + 3) >> 3);
+        if (dev_alloc(&d.rpts, (size_t)cap * 4)) return LIVO_E_OOM;
+        d.rpts_cap = cap;
+    }
+    if (d.rpos_cap < d.n_ids) {
+        dev_free(d.rpos);
+        d.rpos_cap = 0;
+        const int64_t cap = std::max<int64_t>(d.n_ids + (d.n_ids >> 3), 1);
+        if (dev_alloc(&d.rpos, (size_t)cap)) return LIVO_E_OOM;
+        d.rpos_cap = cap;
+    }
+    HIP_TRY(hipMemcpyAsync(d.rpts, c->gpts, (size_t)(na + 3) * 16, hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(hipMemsetAsync(d.rpos, 0xFF, (size_t)std::max<int64_t>(d.n_ids, 1) * 4, c->stream));
+    int rc = launch_dyn_rpos(d.rpts, na, d.rpos, c->stream);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    d.base_ids = d.n_ids;
+    d.base_n = na;
+    d.tomb = 0;
+    d.d_n = 0;
+    d.runs = true;
+    return LIVO_OK;
+}
+
+// The runs rebuilt from the current points (the grid just rebuilt by
+// dyn_rebuild): cell runs, ball runs with the build's r5, then the new base.
+static int dyn_rebase(livo_ctx* c) {
+    DynDev& d = c->dyn;
+    d.runs = false;
+    const int64_t na = c->map_points;
+    const bool balls = c->bslots != nullptr && c->br5 > 0.f;
+    int rc = na > 0 && na * 27 + kRunPad < (int64_t)0xFFFFFFFFll ? build_cell_runs(c, na) : LIVO_E_RANGE;
+    if (!rc && balls) {
+        const int brc = build_ball_runs(c, na, c->br5, 2.0 * (double)d.cmax);
+        if (brc == LIVO_E_OOM) {
+            (void)hipGetLastError();
+            dev_free(c->bslots);
+            dev_free(c->bpts);
+            c->bentries = 0;
+        } else if (brc) {
+            rc = brc;
+        }
+    }
+    if (!rc) rc = dyn_base_from_grid(c);
+    if (rc == LIVO_E_OOM || rc == LIVO_E_RANGE) {  // the cell walk serves the map from here on
+        (void)hipGetLastError();
+        dev_free(c->vslots);
+        dev_free(c->vpts);
+        dev_free(c->bslots);
+        dev_free(c->bpts);
+        c->bentries = 0;
+        d.runs = false;
+        return LIVO_OK;
+    }
+    if (!rc) d.rebases++;
+    return rc;
+}
+
+// After every change of the incremental map (dyn_rebuild): mark the base points
+// deleted since, count the delta, rebase when it or the marks outgrow the
+// base, else build the delta grid of the points added since the base.
+static int dyn_runs_update(livo_ctx* c) {
+    DynDev& d = c->dyn;
+    if (!d.runs) return LIVO_OK;
+    HIP_TRY(hipMemsetAsync(d.ctr + kDynTomb, 0, 2 * sizeof(unsigned long long), c->stream));
+    int rc = launch_dyn_tomb(d.rpts, d.rpos, d.alive, d.base_ids, d.ctr, c->stream);
+    const int64_t nd_ids = d.n_ids - d.base_ids;
+    if (!rc && nd_ids > 0) rc = launch_count_alive(d.alive + d.base_ids, nd_ids, d.ctr, c->stream);
+    if (rc) return rc;
+    unsigned long long h[2];
+    HIP_TRY(hipMemcpyAsync(h, d.ctr + kDynTomb, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    d.tomb += (int64_t)h[0];
+    const int64_t nd = (int64_t)h[1];
+    if ((double)nd > d.rebase_frac * (double)d.base_n || (double)d.tomb > 2.0 * d.rebase_frac * (double)d.base_n)
+        return dyn_rebase(c);
+    d.d_n = nd;
+    if (nd == 0) return LIVO_OK;
+    // the delta grid: cell keys of the ids since the base, sorted, gathered (k_dyn_gather pads 3)
+    rc = launch_dyn_cellkeys(d.all + 4 * d.base_ids, d.alive + d.base_ids, nd_ids, c->gorg, 1.0f / c->gh, d.keys, d.iota,
+                             d.ctr, c->stream);
+    if (!rc) rc = sort_u64(c, d.keys, d.skeys, d.iota, d.svals, nd_ids);
+    if (rc) return rc;
+    if (d.dpts_cap < nd + 3) {
+        dev_free(d.dpts);
+        d.dpts_cap = 0;
+        const int64_t cap = (nd + 3) + ((nd + 3) >> 1);
+        if (dev_alloc(&d.dpts, (size_t)cap * 4)) return LIVO_E_OOM;
+        d.dpts_cap = cap;
+    }
+    rc = launch_dyn_gather(d.skeys, d.svals, nd, d.all + 4 * d.base_ids, d.dpts, d.heads, c->stream);
+    if (!rc) rc = ivox_scan(c, d.heads, d.runid, nd);
+    if (!rc) rc = launch_dyn_runs(d.heads, d.runid, nd, d.starts, d.ctr + kDynRuns, c->stream);
+    if (rc) return rc;
+    unsigned long long cells = 0;
+    HIP_TRY(hipMemcpyAsync(&cells, d.ctr + kDynRuns, 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    int log2 = 4;
+    while (((int64_t)1 << log2) < 4 * (int64_t)cells) log2++;
+    const int64_t table = (int64_t)1 << log2;
+    if (d.dslot_cap < table) {
+        dev_free(d.dslots);
+        d.dslot_cap = 0;
+        if (dev_alloc(&d.dslots, (size_t)table)) return LIVO_E_OOM;
+        d.dslot_cap = table;
+    }
+    rc = launch_ivox_clear(d.dslots, table, c->stream);
+    if (!rc) rc = launch_dyn_slots(d.skeys, d.starts, (int64_t)cells, d.dslots, log2, c->stream);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    d.dlog2 = log2;
+    return LIVO_OK;
+}
+
 // The built map becomes the incremental point set (ids = build indices).
 static int dyn_activate(livo_ctx* c) {
     DynDev& d = c->dyn;
@@ -967,6 +1120,21 @@ static int dyn_activate(livo_ctx* c) {
     d.gslot_cap = (int64_t)1 << c->glog2;
     d.gpts_cap = M + 3;
     d.active = true;
+    d.runs = false;
+    d.d_n = 0;
+    if (const char* env = std::getenv("LIVO_DYN_REBASE")) {
+        const double v = std::atof(env);
+        if (v > 0.0 && v < 100.0) d.rebase_frac = v;
+    }
+    const char* env_runs = std::getenv("LIVO_DYN_RUNS");
+    if (LIVO_IDX_RUNS && c->vslots && c->vpts && M > 0 && !(env_runs && std::atoi(env_runs) == 0)) {
+        rc = dyn_base_from_grid(c);  // the built map's runs index its grid: the grid becomes the base
+        if (rc == LIVO_E_OOM) {
+            (void)hipGetLastError();
+            rc = LIVO_OK;  // (the cell walk then serves the incremental map, as without runs)
+        }
+        if (rc) return rc;
+    }
     return LIVO_OK;
 }
 
@@ -1014,7 +1182,7 @@ static int dyn_rebuild(livo_ctx* c) {
     c->geps = (float)(32.0 * std::ldexp(1.0, -24) * (double)d.cmax + 1e-7);
     c->grid_bytes = table * (int64_t)sizeof(GridSlot) + d.gpts_cap * 16;
     for (auto& s : c->scans) s.searched = false;  // cached neighbours refer to the old map
-    return LIVO_OK;
+    return dyn_runs_update(c);
 }
 
 // Add_Points of the n points in d.W (filled by the caller).
@@ -1302,6 +1470,57 @@ int livo_last_timings(livo_ctx* c, livo_timings* out) {
     return LIVO_OK;
 }
 
+#if LIVO_IDX_RUNS
+// Index runs from n key-sorted entries (skeys; e2 / pt give each entry's grid
+// position, as k_run_place): heads, run ids, run starts, lengths rounded up to
+// 4, their exclusive scan (pstart) and the placed positions in *out (the
+// padded total + kRunPad words, zero-filled), then the runs' hash slots
+// (load factor <= 1/4).  plen / pstart: scratch of n + 1 words each.
+static int build_index_runs(livo_ctx* c, int64_t n, const unsigned long long* skeys, const uint32_t* e2,
+                            const uint32_t* pt, uint32_t* heads, uint32_t* runid, uint32_t* starts,
+                            unsigned long long* nruns_dev, uint32_t* plen, uint32_t* pstart, RunWord** out,
+                            GridSlot** slots, int* log2_out, int64_t* words) {
+    int rc = launch_run_heads(skeys, n, heads, c->stream);
+    if (!rc) rc = ivox_scan(c, heads, runid, n);
+    if (!rc) rc = launch_dyn_runs(heads, runid, n, starts, nruns_dev, c->stream);
+    unsigned long long runs = 0;
+    if (!rc && hipMemcpyAsync(&runs, nruns_dev, 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess) rc = LIVO_E_HIP;
+    if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = LIVO_E_HIP;
+    if (rc) return rc;
+    if (runs == 0) return LIVO_E_INVALID;
+    rc = launch_run_plen(starts, (int64_t)runs, plen, c->stream);
+    if (!rc) rc = ivox_scan(c, plen, pstart, (int64_t)runs);
+    uint32_t tail[2] = {0u, 0u};
+    if (!rc && hipMemcpyAsync(&tail[0], pstart + runs - 1, 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+        rc = LIVO_E_HIP;
+    if (!rc && hipMemcpyAsync(&tail[1], plen + runs - 1, 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+        rc = LIVO_E_HIP;
+    if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = LIVO_E_HIP;
+    if (rc) return rc;
+    const int64_t total = (int64_t)tail[0] + tail[1];  // (u32 lengths: the scan wraps beyond 2^32 words)
+    if (total < n || total + kRunPad >= (int64_t)0xFFFFFFFFll) return LIVO_E_RANGE;
+    if (dev_alloc(out, (size_t)(total + kRunPad))) return LIVO_E_OOM;
+    rc = hipMemsetAsync(*out, 0, (size_t)(total + kRunPad) * sizeof(RunWord), c->stream) == hipSuccess ? LIVO_OK
+                                                                                                         : LIVO_E_HIP;
+    if (!rc) rc = launch_run_place(e2, pt, heads, runid, starts, pstart, n, *out, c->stream);
+    int log2 = 4;
+    while (((int64_t)1 << log2) < 4 * (int64_t)runs) log2++;
+    const int64_t table = (int64_t)1 << log2;
+    if (!rc && dev_alloc(slots, (size_t)table)) rc = LIVO_E_OOM;
+    if (!rc) rc = launch_ivox_clear(*slots, table, c->stream);
+    if (!rc) rc = launch_run_slots(skeys, starts, pstart, (int64_t)runs, *slots, log2, c->stream);
+    if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = LIVO_E_HIP;
+    if (rc) {
+        dev_free(*out);
+        dev_free(*slots);
+        return rc;
+    }
+    *log2_out = log2;
+    *words = total + kRunPad;
+    return LIVO_OK;
+}
+#endif
+
 // The cell runs of the static map's grid (livo_internal.h), built on the
 // device: two stable radix sorts (rho2, then the run key) of the 27 M entries,
 // the runs' heads and starts, and their hash table (load factor <= 1/4).
@@ -1328,7 +1547,9 @@ static int build_cell_runs(livo_ctx* c, int64_t M) {
     uint32_t* starts = (uint32_t*)p; p += al(((size_t)n + 1) * 4);
     unsigned long long* nruns = (unsigned long long*)p;
     int rc = LIVO_OK;
-    if (dev_alloc(&c->vpts, (size_t)(n + 8) * 4)) rc = LIVO_E_OOM;
+#if !LIVO_IDX_RUNS
+    if (dev_alloc(&c->vpts, (size_t)(n + kRunPad) * kRunWords)) rc = LIVO_E_OOM;
+#endif
     if (!rc) rc = launch_cr_rho(c->gpts, n, c->gorg, c->gh, rho, iota, c->stream);
     if (!rc) {
         size_t tb = 0;
@@ -1339,6 +1560,16 @@ static int build_cell_runs(livo_ctx* c, int64_t M) {
     }
     if (!rc) rc = launch_cr_key(c->gpts, e1, n, c->gorg, c->gh, keys, c->stream);
     if (!rc) rc = sort_u64(c, keys, skeys, e1, e2, n);
+#if LIVO_IDX_RUNS
+    int64_t words = 0;
+    // (rho, iota: dead after the sorts) the padded run lengths and their scan
+    if (!rc) rc = build_index_runs(c, n, skeys, e2, nullptr, heads, runid, starts, nruns, rho, iota, &c->vpts,
+                                   &c->vslots, &c->vlog2, &words);
+    (void)hipFree(scr);
+    if (rc) return rc;
+    c->grid_bytes += (int64_t)(((int64_t)1 << c->vlog2) * sizeof(GridSlot) + words * sizeof(RunWord));
+    return LIVO_OK;
+#else
     if (!rc) rc = launch_cr_fill(c->gpts, e2, skeys, n, c->gorg, c->gh, c->vpts, heads, c->stream);
     if (!rc) rc = ivox_scan(c, heads, runid, n);
     if (!rc) rc = launch_dyn_runs(heads, runid, n, starts, nruns, c->stream);
@@ -1359,8 +1590,9 @@ static int build_cell_runs(livo_ctx* c, int64_t M) {
         return rc;
     }
     c->vlog2 = log2;
-    c->grid_bytes += (int64_t)(table * sizeof(GridSlot) + (size_t)(n + 8) * 16);
+    c->grid_bytes += (int64_t)(table * sizeof(GridSlot) + (size_t)(n + kRunPad) * 16);
     return LIVO_OK;
+#endif
 }
 
 // The ball runs of the static map (livo_internal.h KnnParams::bslots), built on
@@ -1425,7 +1657,9 @@ static int build_ball_runs(livo_ctx* c, int64_t M, float r5, double ext) {
     uint32_t* starts = (uint32_t*)p; p += al(((size_t)n + 1) * 4);
     unsigned long long* nruns = (unsigned long long*)p;
     uint32_t* runid = rho;  // (rho is dead after the first sort)
-    if (dev_alloc(&c->bpts, (size_t)(n + 8) * 4)) rc = LIVO_E_OOM;
+#if !LIVO_IDX_RUNS
+    if (dev_alloc(&c->bpts, (size_t)(n + kRunPad) * kRunWords)) rc = LIVO_E_OOM;
+#endif
     if (!rc) rc = launch_br_emit(c->gpts, M, c->gorg, bh, brmax, off, rho, keys, pt, iota, c->stream);
     if (!rc) {
         size_t tb = 0;
@@ -1436,6 +1670,21 @@ static int build_ball_runs(livo_ctx* c, int64_t M, float r5, double ext) {
     }
     if (!rc) rc = launch_br_gather_keys(keys, e1, n, key1, c->stream);
     if (!rc) rc = sort_u64(c, key1, skeys, e1, e2, n);
+#if LIVO_IDX_RUNS
+    int64_t words = 0;
+    // (srho, iota: dead after the sorts) the padded run lengths and their scan
+    if (!rc) rc = build_index_runs(c, n, skeys, e2, pt, heads, runid, starts, nruns, srho, iota, &c->bpts,
+                                   &c->bslots, &c->blog2, &words);
+    (void)hipFree(scr);
+    dev_free(off);
+    if (rc) return rc;
+    c->bh = bh;
+    c->brmax = brmax;
+    c->br5 = r5;
+    c->bentries = n;
+    c->grid_bytes += (int64_t)(((int64_t)1 << c->blog2) * sizeof(GridSlot) + words * sizeof(RunWord));
+    return LIVO_OK;
+#else
     if (!rc) rc = launch_br_fill(c->gpts, pt, e2, skeys, n, c->bpts, heads, c->stream);
     if (!rc) rc = ivox_scan(c, heads, runid, n);
     if (!rc) rc = launch_dyn_runs(heads, runid, n, starts, nruns, c->stream);
@@ -1461,8 +1710,9 @@ static int build_ball_runs(livo_ctx* c, int64_t M, float r5, double ext) {
     c->brmax = brmax;
     c->br5 = r5;
     c->bentries = n;
-    c->grid_bytes += (int64_t)(table * sizeof(GridSlot) + (size_t)(n + 8) * 16);
+    c->grid_bytes += (int64_t)(table * sizeof(GridSlot) + (size_t)(n + kRunPad) * 16);
     return LIVO_OK;
+#endif
 }
 
 int livo_map_build(livo_ctx* c, const float* xyz, int64_t M, int64_t stride_bytes) {
@@ -1503,6 +1753,8 @@ int livo_map_build(livo_ctx* c, const float* xyz, int64_t M, int64_t stride_byte
     c->leaf_bytes = c->grid_bytes = 0;
     c->has_map = false;
     c->dyn.active = false;  // a new static map (the incremental buffers are kept for reuse)
+    c->dyn.runs = false;
+    c->dyn.d_n = 0;
     c->dyn.n_ids = c->dyn.n_alive = 0;
     c->dyn.last = livo_map_add_stats{};
     const size_t bytes = (size_t)(hm.num_slots + 1) * sizeof(MapNode);

@@ -11,7 +11,26 @@
 #define LIVO_PTS_PER_THREAD 1  // plane pass: 1 point per thread (A/B on MI355X: 4 -> 1 = +7 % at config 2)
 #endif
 
+// Run entries (cell runs / ball runs, KnnParams::vpts / bpts).  1 (default):
+// one 4-B grid position (an index into the cell grid's points, gpts) per
+// entry, every run a 4-entry aligned segment, so a run scan reads 8 positions
+// (two aligned 16-B loads) and gathers their points from the 16 B x M cell grid
+// that stays cache-resident: a quarter of the bytes of 0, which stores the
+// point itself (x, y, z, map index bits: 16 B) in every run it belongs to.
+#ifndef LIVO_IDX_RUNS
+#define LIVO_IDX_RUNS 1
+#endif
+
 namespace livo {
+
+#if LIVO_IDX_RUNS
+using RunWord = uint32_t;
+constexpr int kRunWords = 1;  // words per run entry
+#else
+using RunWord = float;
+constexpr int kRunWords = 4;
+#endif
+constexpr int kRunPad = 8;    // entries of padding behind the last run (chunk reads)
 
 constexpr int kNN = LIVO_NUM_MATCH_POINTS;  // 5
 constexpr int kDim = LIVO_DIM_STATE;        // 18
@@ -303,15 +322,22 @@ struct KnnParams {
     float geps;             // cell-bound slack for float rounding of the cell assignment
     int32_t glog2;          // log2 of the hash table size
     const GridSlot* vslots; // cell runs (null: the cell walk of grid_search)
-    const float* vpts;      // run entries: x, y, z, map index bits
+    const RunWord* vpts;    // run entries (LIVO_IDX_RUNS: grid positions; else x, y, z, map index bits)
     int32_t vlog2;
     const GridSlot* bslots; // ball runs (null: the cell runs only); entries in bpts
-    const float* bpts;
+    const RunWord* bpts;
     int32_t blog2;
     float bh;               // anchor cell edge (origin gorg)
     float bcert2;           // certified if the final scan bound b satisfies b * b <= bcert2
     IvoxParams iv;          // iVox backend (LIVO_BACKEND_IVOX)
     int32_t canon;          // incremental map: flagged queries -> k_knn_canon instead of the ikd-Tree replay
+    // the points the runs index (grid positions): the cell grid's on a static map;
+    // the incremental map's base set (deleted ones with x = NaN) with its runs
+    const float* rpts;
+    int32_t dyn_runs;       // the incremental map searched on runs: marks skipped, delta grid, no cell walk
+    int32_t dlog2;
+    const GridSlot* dslots; // delta grid (null: no point added since the base); points in dpts
+    const float* dpts;
 };
 
 struct SolveParams {
@@ -507,7 +533,7 @@ int launch_vio_end(const VioParams& p, void* stream);
 // KD_TREE::Add_Points / Delete_Point_Boxes on the map's point set, then the
 // cell grid rebuilt from the surviving points.  Counters in DynAddParams::ctr:
 enum { kDynEvents = 0, kDynDeleted = 1, kDynAmbig = 2, kDynDeferred = 3, kDynError = 4, kDynDirty = 5,
-       kDynAbsMax = 6, kDynRuns = 7, kDynCtrN = 8 };
+       kDynAbsMax = 6, kDynRuns = 7, kDynTomb = 8, kDynAliveCnt = 9, kDynCtrN = 10 };
 constexpr uint32_t kDynDirtyCap = 4096;  // dirty boxes listed; beyond, every point takes the sequential pass
 struct DynAddParams {
     const float* W;             // n points to add (x, y, z, -), PointToAdd order
@@ -587,6 +613,23 @@ int launch_cr_key(const float* gpts, const uint32_t* e1, int64_t n, const float 
                   unsigned long long* keys, void* stream);
 int launch_cr_fill(const float* gpts, const uint32_t* e2, const unsigned long long* skeys, int64_t n,
                    const float org[3], float h, float* vpts, uint32_t* heads, void* stream);
+// Index runs (LIVO_IDX_RUNS): the run heads of key-sorted entries; each run's
+// length rounded up to 4; every entry's grid position (pt ? pt[e2[i]] :
+// e2[i] / 27) at pstart[run] + its offset in the run; the runs' hash slots
+// {key, pstart, length}.
+int launch_run_heads(const unsigned long long* skeys, int64_t n, uint32_t* heads, void* stream);
+// Runs on the incremental map: rpos[id] = position of id in rpts (base_n points);
+// k_dyn_tomb marks every base point deleted since (!alive) in rpts (x = NaN) and counts the
+// marks in ctr[kDynTomb]; k_count_alive counts alive[0, n) into ctr[kDynAliveCnt].
+int launch_dyn_rpos(const float* rpts, int64_t base_n, uint32_t* rpos, void* stream);
+int launch_dyn_tomb(float* rpts, uint32_t* rpos, const uint8_t* alive, int64_t base_ids, unsigned long long* ctr,
+                    void* stream);
+int launch_count_alive(const uint8_t* alive, int64_t n, unsigned long long* ctr, void* stream);
+int launch_run_plen(const uint32_t* starts, int64_t nruns, uint32_t* plen, void* stream);
+int launch_run_place(const uint32_t* e2, const uint32_t* pt, const uint32_t* heads, const uint32_t* runid,
+                     const uint32_t* starts, const uint32_t* pstart, int64_t n, uint32_t* out, void* stream);
+int launch_run_slots(const unsigned long long* skeys, const uint32_t* starts, const uint32_t* pstart, int64_t nruns,
+                     GridSlot* slots, int log2, void* stream);
 
 // Nearest_Points carried over by point index (laser_mapping.cpp:165 resize keeps entries).
 int launch_inherit_nn(NNRec* dst, const int32_t* dst_perm, int64_t n_dst, const NNRec* src,

@@ -1409,8 +1409,9 @@ __device__ __forceinline__ float run_bound(const LeafQuery& q, float dqv) {
     const float thr = lq_thr(q);
     return thr < INFINITY ? dqv + __builtin_amdgcn_sqrtf(thr) * (1.0f + 1e-6f) + 1e-4f : INFINITY;
 }
-__device__ __forceinline__ void run_chunk(LeafQuery& q, const float4 (&v)[8], uint32_t k0, uint32_t cnt,
-                                          uint32_t pos0) {
+// slot(u): the candidate tag of entry k0 + u (a run position or a grid position)
+template <class Slot>
+__device__ __forceinline__ void run_chunk(LeafQuery& q, const float4 (&v)[8], uint32_t k0, uint32_t cnt, Slot&& slot) {
     float dist[8];
 #pragma unroll
     for (int u = 0; u < 8; u++) {
@@ -1422,11 +1423,45 @@ __device__ __forceinline__ void run_chunk(LeafQuery& q, const float4 (&v)[8], ui
                           fminf(fminf(dist[4], dist[5]), fminf(dist[6], dist[7])));
     if (m < q.e6) {
 #pragma unroll
-        for (int u = 0; u < 8; u++) lq_offer(q, dist[u], kRunPos | (pos0 + k0 + u));
+        for (int u = 0; u < 8; u++) lq_offer(q, dist[u], slot(u));
     }
 }
+#if LIVO_IDX_RUNS
+// Index runs: the run holds grid positions (4-aligned run start); a chunk's 8
+// positions are two aligned 16-B loads, its points are gathered from the cell
+// grid (pts), and the next chunk's positions are loaded with this chunk's
+// points, so a chunk costs one gather round trip.  Candidates are grid
+// positions (lq_finish reads them from pts like the cell walk's).
+// On the incremental map's base set a point deleted after the runs were built
+// keeps its place with x = NaN (k_dyn_tomb): its distance is NaN, which no
+// comparison of the list admits (lq_offer: NaN < d is false, fminf drops it),
+// and as a chunk's first entry it never stops the scan (NaN > b is false).
+__device__ __forceinline__ uint32_t scan_run(LeafQuery& q, const uint32_t* __restrict__ run, uint32_t cnt,
+                                             const float4* __restrict__ pts, float cx, float cy, float cz, float dqv) {
+    if (cnt == 0) return 0;
+    const uint4* __restrict__ r4 = reinterpret_cast<const uint4*>(run);  // (run start: a multiple of 4 words)
+    uint4 ia = r4[0], ib = r4[1];  // (padded: kRunPad words behind the last run)
+    uint32_t k0 = 0;
+#pragma unroll 1
+    for (; k0 < cnt; k0 += 8) {
+        const uint32_t id[8] = {ia.x, ia.y, ia.z, ia.w, ib.x, ib.y, ib.z, ib.w};
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = pts[id[u]];  // (positions past the run: other runs' or 0, masked)
+        if (k0 + 8 < cnt) {
+            ia = r4[(k0 >> 2) + 2];
+            ib = r4[(k0 >> 2) + 3];
+        }
+        const float b = run_bound(q, dqv);
+        if (centre_d2(cx, cy, cz, v[0].x, v[0].y, v[0].z) > b * b) break;  // rho of every later entry > b
+        run_chunk(q, v, k0, cnt, [&](int u) { return id[u]; });
+    }
+    return min(k0, cnt);
+}
+#else
 __device__ __forceinline__ uint32_t scan_run(LeafQuery& q, const float4* __restrict__ run, uint32_t cnt, uint32_t lo,
                                              float cx, float cy, float cz, float dqv) {
+    auto slot = [&](uint32_t k0) { return [=](int u) { return kRunPos | (lo + k0 + (uint32_t)u); }; };
     uint32_t k0 = 0;
 #if LIVO_RUN_PIPE
     if (cnt == 0) return 0;
@@ -1441,7 +1476,7 @@ __device__ __forceinline__ uint32_t scan_run(LeafQuery& q, const float4* __restr
     auto step = [&](float4 (&v)[8]) __attribute__((always_inline)) -> bool {
         const float b = run_bound(q, dqv);
         if (centre_d2(cx, cy, cz, v[0].x, v[0].y, v[0].z) > b * b) return false;  // rho of every later entry > b
-        run_chunk(q, v, k0, cnt, lo);
+        run_chunk(q, v, k0, cnt, slot(k0));
         const float b2 = run_bound(q, dqv);
         const bool more = k0 + 16 < cnt && !(centre_d2(cx, cy, cz, v[7].x, v[7].y, v[7].z) > b2 * b2);
         if (more) {
@@ -1464,11 +1499,12 @@ __device__ __forceinline__ uint32_t scan_run(LeafQuery& q, const float4* __restr
         for (int u = 0; u < 8; u++) v[u] = run[k0 + u];  // padded by kRunPad entries
         const float b = run_bound(q, dqv);
         if (centre_d2(cx, cy, cz, v[0].x, v[0].y, v[0].z) > b * b) break;  // rho of every later entry > b
-        run_chunk(q, v, k0, cnt, lo);
+        run_chunk(q, v, k0, cnt, slot(k0));
     }
 #endif
     return min(k0, cnt);
 }
+#endif
 
 // ------------------------------------------------------------ cell-run search ----
 // The batched IEKF search on the cell runs (livo_internal.h): the run of the
@@ -1487,6 +1523,10 @@ __device__ __forceinline__ uint32_t scan_run(LeafQuery& q, const float4* __restr
 // ball of the final bound lies in the cube the list is certified (every point
 // within the bound was scanned); else the lane continues with grid_search's
 // stage 2 outside the cube (candidates there are cell-grid slots).
+// DYN (runs on the incremental map): the runs index P.rpts with deletion marks,
+// and a list the cube does not certify is left uncertified (the caller's
+// canonical resolution), since the cell walk's grid positions index another array.
+template <bool DYN = false>
 __device__ __forceinline__ bool vrun_search(LeafQuery& q, const KnnParams& P, bool valid, int c0, int c1, int c2,
                                             int s0, int s1, int s2, unsigned& visits, unsigned& npts) {
     if (!valid || !(P.lM > 0)) return false;
@@ -1505,8 +1545,12 @@ __device__ __forceinline__ bool vrun_search(LeafQuery& q, const KnnParams& P, bo
     const float cx = cell_centre(P.gorg[0], h, c0), cy = cell_centre(P.gorg[1], h, c1);
     const float cz = cell_centre(P.gorg[2], h, c2);
     const float dqv = __builtin_amdgcn_sqrtf(centre_d2(cx, cy, cz, q.qx, q.qy, q.qz)) * (1.0f + 1e-6f);
+#if LIVO_IDX_RUNS
+    npts += scan_run(q, P.vpts + lo, cnt, reinterpret_cast<const float4*>(P.rpts), cx, cy, cz, dqv);
+#else
     const float4* __restrict__ run = reinterpret_cast<const float4*>(P.vpts) + lo;
     npts += scan_run(q, run, cnt, lo, cx, cy, cz, dqv);
+#endif
     // certified when the ball of the final bound lies in the cube [c - 1, c + 1]
     const float t = lq_thr(q);
     if (t < INFINITY) {
@@ -1523,6 +1567,7 @@ __device__ __forceinline__ bool vrun_search(LeafQuery& q, const KnnParams& P, bo
         }
         if (inside) return true;
     }
+    if constexpr (DYN) return false;
     TileView none;
     return grid_search(q, P, c0, c1, c2, s0, s1, s2, none, visits, npts, nullptr, true);
 }
@@ -1542,6 +1587,7 @@ __device__ __forceinline__ bool vrun_search(LeafQuery& q, const KnnParams& P, bo
 // as a pruned cell of grid_search, they could neither enter the list nor make
 // e6 - d5 <= 1e-10.  Not certified (or no run): the caller searches the cell
 // runs from scratch.  Candidates carry their position in P.bpts (kRunPos set).
+template <bool DYN = false>
 __device__ __forceinline__ bool brun_search(LeafQuery& q, const KnnParams& P, bool valid, unsigned& visits,
                                             unsigned& npts) {
     if (!valid || !(P.lM > 0)) return false;
@@ -1569,12 +1615,66 @@ __device__ __forceinline__ bool brun_search(LeafQuery& q, const KnnParams& P, bo
     const float cx = cell_centre(P.gorg[0], P.bh, a[0]), cy = cell_centre(P.gorg[1], P.bh, a[1]);
     const float cz = cell_centre(P.gorg[2], P.bh, a[2]);
     const float dqv = __builtin_amdgcn_sqrtf(centre_d2(cx, cy, cz, q.qx, q.qy, q.qz)) * (1.0f + 1e-6f);
+#if LIVO_IDX_RUNS
+    npts += scan_run(q, P.bpts + lo, cnt, reinterpret_cast<const float4*>(P.rpts), cx, cy, cz, dqv);
+#else
     const float4* __restrict__ run = reinterpret_cast<const float4*>(P.bpts) + lo;
     npts += scan_run(q, run, cnt, lo, cx, cy, cz, dqv);
+#endif
     const float t = lq_thr(q);
     if (!(t < INFINITY)) return false;
     const float b = dqv + __builtin_amdgcn_sqrtf(t) * (1.0f + 1e-6f) + 1e-4f;
     return b * b <= P.bcert2;
+}
+
+// The delta grid of the incremental map (points added since its runs were
+// built; the cell grid's layout in P.dslots / P.dpts): every point of the
+// cells the ball of the current bound reaches (with grid_search's margins) is
+// offered, tagged kRunPos | its position in P.dpts.  The run search before it
+// certified the base points within the bound, so the list is then exact over
+// both sets (the bound only shrinks).  False when the ball spans more than
+// kDeltaMaxCells cells: the caller's canonical resolution takes the query.
+constexpr int kDeltaMaxCells = 64;
+__device__ __forceinline__ bool delta_search(LeafQuery& q, const KnnParams& P, unsigned& visits, unsigned& npts) {
+    const float t = lq_thr(q);
+    if (!(t < INFINITY)) return false;
+    const double rad = sqrt((double)t + 1e-9) * (1.0 + 1e-5) + (double)P.geps;
+    const double ih = 1.0 / (double)P.gh, lim = (double)(kGridBias - 8);
+    const double q3[3] = {(double)q.qx, (double)q.qy, (double)q.qz};
+    int l[3], h[3];
+    double span = 1.0;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const double lo = floor((q3[a] - rad - (double)P.gorg[a]) * ih), hi = floor((q3[a] + rad - (double)P.gorg[a]) * ih);
+        if (!(fabs(lo) < lim && fabs(hi) < lim)) return false;
+        l[a] = (int)lo;
+        h[a] = (int)hi;
+        span *= hi - lo + 1.0;
+    }
+    if (span > (double)kDeltaMaxCells) return false;
+    const float4* __restrict__ dp = reinterpret_cast<const float4*>(P.dpts);
+    const uint64_t mask = (1ull << P.dlog2) - 1ull;
+#pragma unroll 1
+    for (int cz = l[2]; cz <= h[2]; cz++)
+#pragma unroll 1
+        for (int cy = l[1]; cy <= h[1]; cy++)
+#pragma unroll 1
+            for (int cx = l[0]; cx <= h[0]; cx++) {
+                const unsigned long long key = grid_key_d(cx, cy, cz);
+                uint64_t sl = (uint64_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - P.dlog2));
+                GridSlot g = P.dslots[sl];
+                visits++;
+                while (g.key != key && g.key != kGridEmpty) {
+                    sl = (sl + 1) & mask;
+                    g = P.dslots[sl];
+                    visits++;
+                }
+                if (g.key != key) continue;
+                npts += g.count;
+#pragma unroll 1
+                for (uint32_t k = g.start; k < g.start + g.count; k++) lq_point(q, dp[k], kRunPos | k);
+            }
+    return true;
 }
 
 // 512 points / 128 cells per wave (10.5 KB): 4 waves per SIMD (VGPR-bound);
@@ -2626,14 +2726,19 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
         if (P.vslots) {  // (kernel parameter: uniform)
             EVAL_MARK(1);
             bool certified = false;
-            const float4* runs = reinterpret_cast<const float4*>(P.vpts);
+            const float4* runs = reinterpret_cast<const float4*>(P.vpts);  // (float4 run entries only)
 #ifdef LIVO_EVAL_PROF
             const unsigned np0 = npts;
             bool ball_ok = false;
 #endif
+#if LIVO_IDX_RUNS
+            const bool dyn = P.dyn_runs != 0;  // (uniform) runs on the incremental map
+#else
+            constexpr bool dyn = false;
+#endif
             if (P.bslots) {  // (uniform) the ball runs first; the cell runs for a query they do not certify
-                certified = brun_search(q, P, valid, visits, npts);
-                if (certified) runs = reinterpret_cast<const float4*>(P.bpts);
+                certified = dyn ? brun_search<true>(q, P, valid, visits, npts) : brun_search<false>(q, P, valid, visits, npts);
+                if (certified) runs = reinterpret_cast<const float4*>(P.bpts);  // (float4 run entries only)
                 if (valid && !certified) lq_init<false>(q, P, slot, job, i, valid);
 #ifdef LIVO_EVAL_PROF
                 ball_ok = certified;
@@ -2642,7 +2747,20 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
 #ifdef LIVO_EVAL_PROF
             const unsigned np1 = npts;
 #endif
-            if (!certified) certified = vrun_search(q, P, valid, c0, c1, c2, s0, s1, s2, visits, npts);
+            if (!certified)
+                certified = dyn ? vrun_search<true>(q, P, valid, c0, c1, c2, s0, s1, s2, visits, npts)
+                                : vrun_search<false>(q, P, valid, c0, c1, c2, s0, s1, s2, visits, npts);
+            // the incremental map's points added since its runs (none: no delta grid)
+            if (dyn && valid && certified && P.dslots) certified = delta_search(q, P, visits, npts);
+            // a query the runs (+ delta) do not certify on the incremental map: the
+            // cell walk of the current grid from scratch (its candidates index P.gpts)
+            bool walked = false;
+            if (dyn && valid && !certified) {
+                lq_init<false>(q, P, slot, job, i, valid);
+                TileView none;
+                certified = grid_search(q, P, c0, c1, c2, s0, s1, s2, none, visits, npts);
+                walked = true;
+            }
 #ifdef LIVO_EVAL_PROF
             {  // block totals: lanes past the 2x2x2 block, run entries scanned, ambiguous
                 const unsigned long long nf = __ballot(valid && !certified);
@@ -2678,11 +2796,17 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
 #endif
             if (valid) {
                 float4 nb[kNN];
-                amb = lq_finish<true>(q, P, job, bjob, i, reinterpret_cast<const float4*>(P.gpts), !certified, false,
-                                      runs, nb);
+                // candidates: grid positions (index runs, the cell walk), or run positions (float4 runs);
+                // on the incremental map positions in its base set rpts, or kRunPos | delta positions
+                if (dyn)
+                    amb = lq_finish<true>(q, P, job, bjob, i, reinterpret_cast<const float4*>(walked ? P.gpts : P.rpts),
+                                          !certified, false, reinterpret_cast<const float4*>(P.dpts), nb);
+                else
+                    amb = lq_finish<!LIVO_IDX_RUNS>(q, P, job, bjob, i, reinterpret_cast<const float4*>(P.gpts),
+                                                    !certified, false, runs, nb);
                 // the plane from the neighbours in registers (18643 vs 18011 updates/s
                 // re-reading the record just written, profiles/r03_ab_prefit_seed.txt)
-                if (!amb && !P.canon) {  // (a replayed query's plane is fitted from its record below)
+                if (!amb && (!P.canon || dyn)) {  // (a replayed query's plane is fitted from its record below)
                     float4 pl;
                     pin.ps = fit_plane(E.h, job, i, 1, nb, (int)min<int64_t>(P.lM, (int64_t)kNN), pl);
                     pin.plane = pl;

@@ -183,3 +183,73 @@ def test_add_points_crowded_boxes(ictx):
         W = W[rng.permutation(len(W))]
         _same_add(ictx.map_add_points(W, 0.5), dm.add_points(W, 0.5))
         _same_map(ictx, dm)
+
+
+@pytest.mark.parametrize("mode", ["runs", "rebase_every_change", "cell_walk"])
+def test_iekf_search_records_on_updated_map(built, monkeypatch, mode):
+    """The fused IEKF search on the incremental map: with the runs of the base
+    point set (deleted base points marked, points added since in the delta
+    grid), with a rebase of the runs at every change (LIVO_DYN_REBASE tiny),
+    and with the cell walk (LIVO_DYN_RUNS=0).  One evaluation (max_iteration
+    0: one search at the initial state) after each change: every point's
+    neighbour record (indices and squared distances, in order) equals the
+    oracle's k-NN of the world points on the updated map, bit for bit."""
+    import livo_amd
+    import oracle
+    from livo_amd import synth
+    if mode == "rebase_every_change":
+        monkeypatch.setenv("LIVO_DYN_REBASE", "1e-9")
+    if mode == "cell_walk":
+        monkeypatch.setenv("LIVO_DYN_RUNS", "0")
+    m = synth.make_map(200_000)
+    dm = oracle.DynMap(m)
+    rng = np.random.default_rng(77)
+    with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=0) as ctx:
+        ctx.map_build(m)
+        for k in range(4):
+            body, _, _ = synth.make_scan(20_000, 40 + k)
+            W = _world(body, synth.make_state(40 + k))
+            _same_add(ctx.map_add_points(W, 0.3), dm.add_points(W, 0.3))
+            if k == 1:
+                c = rng.uniform([-20, -12, 0], [20, 12, 2], (3, 3))
+                boxes = np.concatenate([c, c + 3.0], axis=1).astype(f32)
+                assert ctx.map_delete_boxes(boxes) == dm.delete_boxes(boxes)
+            q_body, _, _ = synth.make_scan(15_000, 60 + k)
+            st = synth.make_state(60 + k)
+            sid = ctx.scan_upload(q_body)
+            _, gst = ctx.iekf_update(sid, st)
+            _, rst = dm.iekf_update(q_body, st, t_LI=synth.T_LI, max_iter=0)
+            assert gst["iterations"] == rst["iterations"] == 1
+            assert gst["effct_feat_num"] == rst["effct_feat_num"]
+            gi, gd = ctx.scan_neighbors(sid)
+            ri, rd = dm.knn(oracle.to_world(q_body, st, np.eye(3), synth.T_LI)[:, :3])
+            assert np.array_equal(gi, ri), (mode, k, int((gi != ri).any(axis=1).sum()))
+            assert np.array_equal(gd.view(np.uint32), rd.view(np.uint32))
+            ctx.scan_release(sid)
+
+
+def test_odometry_with_rebases(built, monkeypatch):
+    """The odometry loop of test_odometry_with_ikd_map_incremental with the runs
+    rebuilt after every map change (LIVO_DYN_REBASE tiny): same updates as the oracle."""
+    import livo_amd
+    import oracle
+    from livo_amd import synth
+    monkeypatch.setenv("LIVO_DYN_REBASE", "1e-9")
+    m = synth.make_map(100_000)
+    dm = oracle.DynMap(m)
+    with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=4) as ctx:
+        ctx.map_build(m)
+        for k in range(3):
+            body, _, _ = synth.make_scan(20_000, 20 + k)
+            st0 = synth.make_state(20 + k)
+            sid = ctx.scan_upload(body)
+            gs, gst = ctx.iekf_update(sid, st0)
+            rs, rst = dm.iekf_update(body, st0, t_LI=synth.T_LI, max_iter=4)
+            assert gst["iterations"] == rst["iterations"] and gst["effct_feat_num"] == rst["effct_feat_num"]
+            for e in range(gst["iterations"]):
+                rel = np.linalg.norm(gst["solution"][e] - rst["solution"][e]) / np.linalg.norm(rst["solution"][e])
+                assert rel < REL_STATE, (k, e, rel)
+            _same_add(ctx.map_incremental(sid, gs, filter_size_map=0.3)[1],
+                      dm.map_incremental(body, gs, t_LI=synth.T_LI, filter_size_map=0.3))
+            _same_map(ctx, dm)
+            ctx.scan_release(sid)

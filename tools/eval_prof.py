@@ -17,6 +17,7 @@ from livo_amd import synth  # noqa: E402
 
 def main():
     config5 = "--config5" in sys.argv  # 10M map, the bench's VoxelGrid scans
+    seed0 = int(sys.argv[sys.argv.index("--seed0") + 1]) if "--seed0" in sys.argv else 0  # first scan seed (config 2)
     m = synth.cached_map(10_000_000 if config5 else 1_000_000)
     with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=4) as ctx:
         ctx.map_build(m)
@@ -27,8 +28,8 @@ def main():
                 sids.append(ctx.scan_preprocess(raw, poses, Re, pe, leaf_size=synth.CONFIG5_LEAF)[0])
             st0 = [synth.make_state(1000 + s) for s in range(8)]
         else:
-            sids = [ctx.scan_upload(synth.make_scan(100_000, s)[0]) for s in range(8)]
-            st0 = [synth.make_state(s) for s in range(8)]
+            sids = [ctx.scan_upload(synth.make_scan(100_000, seed0 + s)[0]) for s in range(8)]
+            st0 = [synth.make_state(seed0 + s) for s in range(8)]
         L = ctx._L
         L.livo_debug_eval_prof.argtypes = [C.c_void_p]
         buf = (C.c_ulonglong * 24)()
