@@ -819,6 +819,11 @@ __device__ __forceinline__ float4 cand_point(const float4* __restrict__ lpts, co
     if constexpr (RUNS) return (nd & kRunPos) ? vpts[nd & ~kRunPos] : lpts[nd];
     return lpts[nd];
 }
+#ifdef LIVO_EVAL_PROF
+// why queries were flagged for the exact replay: [uncertified, C1 (e6 - d5 <= 1e-10),
+// C2 gap in (0, 1e-10], C2 exact tie with equal x, C1 with e6 == d5 exactly]
+__device__ unsigned long long g_amb_reason[8];
+#endif
 template <bool RUNS = false>
 __device__ __forceinline__ bool lq_finish(LeafQuery& q, const KnnParams& P, const HsJob& job, unsigned bjob,
                                           int i, const float4* __restrict__ lpts, bool overrun, bool enqueue = true,
@@ -836,6 +841,20 @@ __device__ __forceinline__ bool lq_finish(LeafQuery& q, const KnnParams& P, cons
             else amb = true;
         }
     }
+#ifdef LIVO_EVAL_PROF
+    if (amb || tie) {
+        bool gap = false, eqx = false;
+        for (int k = 0; k + 1 < kNN; k++)
+            if (k + 1 < cnt && q.d[k + 1] - q.d[k] <= kFuzz) {
+                if (q.d[k + 1] == q.d[k] && a[k + 1].x == a[k].x) eqx = true;
+                else if (q.d[k + 1] != q.d[k]) gap = true;
+            }
+        if (overrun) atomicAdd(&g_amb_reason[0], 1ull);
+        else if (q.e6 - q.d[kNN - 1] <= kFuzz) atomicAdd(&g_amb_reason[q.e6 == q.d[kNN - 1] ? 4 : 1], 1ull);
+        if (gap) atomicAdd(&g_amb_reason[2], 1ull);
+        if (eqx) atomicAdd(&g_amb_reason[3], 1ull);
+    }
+#endif
     if (tie && !amb) {
         // (dist, x) order; the list is already sorted by dist
         float ax[kNN];
@@ -1722,6 +1741,44 @@ __global__ __launch_bounds__(TILE ? 64 : kKnnBlock, TILE ? 4 : LIVO_GRID_WAVES) 
     }
     count_visits(P, slot, visits, npts);
 }
+
+#if LIVO_IDX_RUNS
+// The runs' search as a pass of its own (the unfused paths: the IKFoM update,
+// LIVO_FUSED=0): k_iekf_eval's search stage -- ball run, cell run, the cell
+// walk past the cube -- for every point of the batch, the neighbour record
+// written, flagged queries queued for k_knn_replay.  LATER: a later
+// evaluation, run only for scans whose last solve asked for a search (the
+// search itself unseeded, as the fused kernel's).
+template <bool LATER>
+__global__ __launch_bounds__(kEvalBlock) void k_knn_runs(KnnParams P) {
+    unsigned bjob, bx;
+    xcd_block(P.nb, bjob, bx);
+    const HsJob job = P.jobs[bjob];
+    IekfSlot* slot = job.slot;
+    if (P.force >= 0) {
+        if (!P.force) return;
+    } else {
+        if (slot->ctrl.stop) return;
+        if (LATER && !slot->ctrl.search_en) return;
+    }
+    if ((int)bx * kEvalBlock >= job.n) return;  // (block-uniform)
+    const int i = (int)bx * kEvalBlock + threadIdx.x;
+    const bool valid = i < job.n;
+    LeafQuery q;
+    lq_init<false>(q, P, slot, job, i, valid);
+    int c0 = 0, c1 = 0, c2 = 0, s0 = 1, s1 = 1, s2 = 1;
+    if (valid) grid_cell(P, q, c0, c1, c2, s0, s1, s2);
+    unsigned visits = 0, npts = 0;
+    bool certified = false;
+    if (P.bslots) {
+        certified = brun_search(q, P, valid, visits, npts);
+        if (valid && !certified) lq_init<false>(q, P, slot, job, i, valid);
+    }
+    if (!certified) certified = vrun_search(q, P, valid, c0, c1, c2, s0, s1, s2, visits, npts);
+    if (valid) lq_finish<false>(q, P, job, bjob, i, reinterpret_cast<const float4*>(P.gpts), !certified, true);
+    count_visits(P, slot, visits, npts);
+}
+#endif
 
 // Exact reference-order recomputation of the queries the fast pass flagged:
 // KD_TREE::Search's visiting order with the far sons on an LDS stack and the
@@ -2695,7 +2752,15 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
     } U;
     unsigned bjob, bx;
     // the same block order in every evaluation: the plane caches stay in the L2 that wrote them
-    xcd_chunk_block(P.nb, P.xcd_chunk, bjob, bx);
+    if (P.xcd_chunk < 0) {  // (uniform) dynamic order: the next (scan, block) item of the launch's counter
+        __shared__ unsigned s_item;
+        if (threadIdx.x == 0) s_item = atomicAdd(P.work_ctr, 1u);
+        __syncthreads();
+        bjob = s_item / (unsigned)P.nb;
+        bx = s_item % (unsigned)P.nb;
+    } else {
+        xcd_chunk_block(P.nb, P.xcd_chunk, bjob, bx);
+    }
     const HsJob job = P.jobs[bjob];
     IekfSlot* slot = job.slot;
     if (bx > 0 && (int)bx * kEvalBlock >= job.n) return;  // (an empty scan keeps one block: it solves)
@@ -3277,37 +3342,52 @@ __global__ __launch_bounds__(kBlock) void k_hshare_ik(HsParams P) {
     if (tid == 0) job.ikcnt[blockIdx.x] = bcnt < (uint32_t)kIkFewRows ? bcnt : (uint32_t)kIkFewRows + 1u;
 }
 
-// One 64-thread block per scan: fixed-order reduction of the IKFoM partials,
-// then ik_solve (kept out of the plane pass: the 23-wide solve needs far more
-// registers than the per-point work).
-__global__ __launch_bounds__(64) void k_solve_ik(HsParams P) {
+// One block of kIkSolveWaves waves per scan: the IKFoM partials merged by every
+// wave over its share of the blocks (wave w: blocks w, w + W, ...; 8 loads in
+// flight per column), the waves' compensated sums then merged in wave order by
+// wave 0 (order-free to ~1e-27: the same doubles as one serial compensated
+// sum), and wave 0 runs ik_solve (kept out of the plane pass: the 23-wide solve
+// needs far more registers than the per-point work).  Measured before on one
+// wave: 149.5 us per call, the serial chain of 49 dependent rounds of loads.
+constexpr int kIkSolveWaves = 8;
+__global__ __launch_bounds__(64 * kIkSolveWaves) void k_solve_ik(HsParams P) {
     __shared__ IkSolveLds S;
+    __shared__ double wsum[kIkSolveWaves][2][kIkUsed];
     const HsJob job = P.jobs[blockIdx.x];
     IekfSlot* slot = job.slot;
-    const int lane = threadIdx.x;
-    if (P.replay_count && blockIdx.x == 0 && lane == 0) *P.replay_count = 0u;
-    if (slot->ctrl.stop) return;
-    for (int c = lane; c < kIkCols; c += 64) {
-        // the blocks' compensated partials merged in block order (order-free to ~1e-27)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (P.replay_count && blockIdx.x == 0 && threadIdx.x == 0) *P.replay_count = 0u;
+    if (slot->ctrl.stop) return;  // block-uniform
+    for (int c = lane; c < kIkUsed; c += 64) {
         double sc = 0.0, cc = 0.0;
-        if (c < kIkUsed) {
-            const double* src = job.partial + c;
-            int b = 0;
-            for (; b < job.nblk; b += 8) {
-                double v[8], w[8];
+        const double* src = job.partial + c;
+        for (int b = wave; b < job.nblk; b += 8 * kIkSolveWaves) {
+            double v[8], w[8];
 #pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    const bool in = b + k < job.nblk;
-                    v[k] = in ? src[(size_t)(b + k) * kIkCols] : 0.0;
-                    w[k] = in ? src[(size_t)(b + k) * kIkCols + kIkCompOff] : 0.0;
-                }
+            for (int k = 0; k < 8; k++) {
+                const int bb = b + k * kIkSolveWaves;
+                const bool in = bb < job.nblk;
+                v[k] = in ? src[(size_t)bb * kIkCols] : 0.0;
+                w[k] = in ? src[(size_t)bb * kIkCols + kIkCompOff] : 0.0;
+            }
 #pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    comp_add(sc, cc, v[k]);
-                    cc += w[k];
-                }
+            for (int k = 0; k < 8; k++) {
+                comp_add(sc, cc, v[k]);
+                cc += w[k];
             }
         }
+        wsum[wave][0][c] = sc;
+        wsum[wave][1][c] = cc;
+    }
+    __syncthreads();
+    if (wave > 0) return;
+    for (int c = lane; c < kIkCols; c += 64) {
+        double sc = 0.0, cc = 0.0;
+        if (c < kIkUsed)
+            for (int w = 0; w < kIkSolveWaves; w++) {
+                comp_add(sc, cc, wsum[w][0][c]);
+                cc += wsum[w][1][c];
+            }
         S.sum[c] = sc + cc;
     }
     WAVE_SYNC();
@@ -3417,6 +3497,16 @@ int launch_knn_grid(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, 
     q.nb = (int32_t)((max_n + B - 1) / B);
     if ((int64_t)q.nb * n_jobs >= (1ll << 31)) return LIVO_E_RANGE;
     const dim3 grid((unsigned)(q.nb * n_jobs)), block(B);
+#if LIVO_IDX_RUNS
+    if (q.vslots && !q.canon && !q.dyn_runs) {  // the runs of a static map: their search pass
+        q.nb = (int32_t)((max_n + kEvalBlock - 1) / kEvalBlock);
+        const dim3 rgrid((unsigned)(q.nb * n_jobs)), rblock(kEvalBlock);
+        if (seeded)
+            hipLaunchKernelGGL(k_knn_runs<true>, rgrid, rblock, 0, (hipStream_t)stream, q);
+        else
+            hipLaunchKernelGGL(k_knn_runs<false>, rgrid, rblock, 0, (hipStream_t)stream, q);
+    } else
+#endif
     if (tile) {
         if (seeded)
             hipLaunchKernelGGL((k_knn_grid<true, true>), grid, block, 0, (hipStream_t)stream, q);
@@ -3449,6 +3539,12 @@ extern "C" int livo_debug_eval_prof(unsigned long long* out) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_eval_prof), sizeof(g_eval_prof)) != hipSuccess) return LIVO_E_HIP;
     static const unsigned long long zero[24] = {};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_eval_prof), zero, sizeof(zero)) == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+extern "C" int livo_debug_amb_reason(unsigned long long* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return LIVO_E_HIP;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_amb_reason), sizeof(g_amb_reason)) != hipSuccess) return LIVO_E_HIP;
+    static const unsigned long long zero[8] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_amb_reason), zero, sizeof(zero)) == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 extern "C" int livo_debug_eval_stats(unsigned long long* out) {
     if (hipDeviceSynchronize() != hipSuccess) return LIVO_E_HIP;
@@ -3511,7 +3607,7 @@ int launch_hshare_ik(const HsParams& p, int n_jobs, int max_nblk, bool first, vo
         hipLaunchKernelGGL(k_hshare_ik<false>, grid, block, 0, (hipStream_t)stream, p);
     if (hipGetLastError() != hipSuccess) return LIVO_E_HIP;
     if (!p.solve) return LIVO_OK;
-    hipLaunchKernelGGL(k_solve_ik, dim3(n_jobs), dim3(64), 0, (hipStream_t)stream, p);
+    hipLaunchKernelGGL(k_solve_ik, dim3(n_jobs), dim3(64 * kIkSolveWaves), 0, (hipStream_t)stream, p);
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 

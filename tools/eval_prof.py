@@ -36,13 +36,19 @@ def main():
         ctx.iekf_update_batch(sids, st0)
         L.livo_debug_eval_stats.argtypes = [C.c_void_p]
         sbuf = (C.c_ulonglong * 24)()
+        L.livo_debug_amb_reason.argtypes = [C.c_void_p]
+        abuf = (C.c_ulonglong * 8)()
         L.livo_debug_eval_prof(buf)  # reset after the warm-up
         L.livo_debug_eval_stats(sbuf)
+        L.livo_debug_amb_reason(abuf)
         steps = 10
         for _ in range(steps):
             ctx.iekf_update_batch(sids, st0)
         assert L.livo_debug_eval_prof(buf) == 0
         assert L.livo_debug_eval_stats(sbuf) == 0
+        assert L.livo_debug_amb_reason(abuf) == 0
+        print(f"flagged queries per batch: uncertified {abuf[0] / steps:.2f}  C1 near-tie {abuf[1] / steps:.2f}  "
+              f"C1 exact tie {abuf[4] / steps:.2f}  C2 gap {abuf[2] / steps:.2f}  C2 equal x {abuf[3] / steps:.2f}")
         for s, name in ((2, "first-search evals"), (1, "rematch evals")):
             r = sbuf[8 * s: 8 * s + 8]
             lanes, waves = max(r[0], 1), max(r[7], 1)
