@@ -187,8 +187,7 @@ struct livo_ctx {
     float grid_cell = 0.f;             // cell edge (LIVO_GRID_CELL; 0: from the map)
     float grid_ppc = 0.f;              // target points per occupied cell when chosen from the map (LIVO_GRID_PPC)
     bool vruns = true;                 // cell runs on a static map (LIVO_VRUNS=0: the cell walk)
-    int xcd_chunk = 0;                 // k_iekf_eval block order (LIVO_XCD_CHUNK; 0: one range per XCD; -1: dynamic)
-    unsigned* d_wq = nullptr;          // xcd_chunk < 0: item counters [lane][group][evaluation]
+    int xcd_chunk = 0;                 // k_iekf_eval block order (LIVO_XCD_CHUNK; 0: one range per XCD)
     GridSlot* vslots = nullptr;        // vertex runs (static map only)
     RunWord* vpts = nullptr;           // run entries (LIVO_IDX_RUNS: grid positions; else x, y, z, map index bits)
     int32_t vlog2 = 0;
@@ -1362,7 +1361,7 @@ int livo_ctx_create(int device, const livo_params* p, livo_ctx** out) {
     if (const char* env = std::getenv("LIVO_LANE_SERIAL")) c->lane_serial = std::atoi(env) != 0;
     if (const char* env = std::getenv("LIVO_LANE_ZC")) c->lane_zc = std::atoi(env) != 0;
     if (const char* env = std::getenv("LIVO_SYNC_ZC")) c->sync_zc = std::atoi(env) != 0;
-    if (const char* env = std::getenv("LIVO_XCD_CHUNK")) c->xcd_chunk = std::max(-1, std::atoi(env));  // tuning knob
+    if (const char* env = std::getenv("LIVO_XCD_CHUNK")) c->xcd_chunk = std::max(0, std::atoi(env));  // tuning knob
     if (const char* env = std::getenv("LIVO_GRID_PPC")) {  // tuning knob
         const float v = (float)std::atof(env);
         if (v > 0.f) c->grid_ppc = v;
@@ -1408,7 +1407,6 @@ int livo_ctx_destroy(livo_ctx* c) {
     dev_free(c->bslots);
     dev_free(c->bpts);
     dev_free(c->d_replay_count);
-    dev_free(c->d_wq);
     dev_free(c->d_replay_total);
     dev_free(c->d_replay_list);
     dev_free(c->d_slots);
@@ -2342,11 +2340,6 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
     if (!fused) HIP_TRY(hipMemsetAsync(c->d_replay_count, 0, sizeof(unsigned) * kMaxGroups, c->stream));
     // profiling: the batch's first search starts at ev[0][0], before the fork
     if (prof) HIP_TRY(hipEventRecord(c->ev[0][0], c->stream));
-    const size_t wq_n = (size_t)kMaxGroups * LIVO_MAX_EVALS;
-    if (fused && c->xcd_chunk < 0) {
-        if (!c->d_wq && dev_alloc(&c->d_wq, wq_n * LIVO_MAX_INFLIGHT)) return LIVO_E_OOM;
-        HIP_TRY(hipMemsetAsync(c->d_wq + L * wq_n, 0, wq_n * sizeof(unsigned), B.st[0]));
-    }
     if (ngroups > 1) {
         HIP_TRY(hipEventRecord(B.fork, B.st[0]));
         for (int gi = 1; gi < ngroups; gi++) HIP_TRY(hipStreamWaitEvent(g[gi].st, B.fork, 0));
@@ -2371,7 +2364,6 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
             hipStream_t st = g[gi].st;
             // full: ev[gi][e] before evaluation e, ev[gi][evals] after the last
             if (full && (e > 0 || gi > 0)) HIP_TRY(hipEventRecord(c->ev[gi][e], st));
-            if (c->d_wq) kp[gi].work_ctr = c->d_wq + L * wq_n + (size_t)gi * LIVO_MAX_EVALS + e;
             rc = launch_iekf_eval(kp[gi], hp[gi], g[gi].count, g[gi].max_n, e == 0, st);
             if (rc) return rc;
             if (prof && !full && e == 0) HIP_TRY(hipEventRecord(c->ev[gi][1], st));

@@ -310,9 +310,7 @@ struct KnnParams {
     int64_t n_nodes;        // heap slots of the ikd-Tree records (the replay's subtree loads stay below)
     int32_t identity;       // 1: pts are world points already (livo_knn)
     int32_t nb;             // blocks per scan (set by the launcher)
-    int32_t xcd_chunk;      // k_iekf_eval block order: XCD-interleaved chunks of this many blocks (0: one range per XCD;
-                            // < 0: work items taken from *work_ctr in dispatch order)
-    unsigned* work_ctr;     // xcd_chunk < 0: this launch's item counter (zeroed before the launch)
+    int32_t xcd_chunk;      // k_iekf_eval block order: XCD-interleaved chunks of this many blocks (0: one range per XCD)
     int32_t ldepth;         // leaf map depth D
     const LeafNode* lnodes; // leaf map internal records
     const float* lpts;      // leaf map points, 4 floats each (x, y, z, index bits)

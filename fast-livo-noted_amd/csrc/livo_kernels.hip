@@ -772,6 +772,13 @@ __device__ __forceinline__ void lq_init(LeafQuery& q, const KnnParams& P, const 
 }
 
 __device__ __forceinline__ float lq_thr(const LeafQuery& q) { return fminf(q.d[kNN - 1], q.B); }
+// an empty list (the query point kept)
+__device__ __forceinline__ void lq_reset(LeafQuery& q) {
+#pragma unroll
+    for (int k = 0; k < kNN; k++) { q.d[k] = INFINITY; q.nd[k] = 0u; }
+    q.e6 = INFINITY;
+    q.B = INFINITY;
+}
 
 // One scanned point: inserted into the sorted list if below the 5th (the
 // evicted 5th, +inf while the list is not full, becomes a candidate for e6),
@@ -1545,7 +1552,9 @@ __device__ __forceinline__ uint32_t scan_run(LeafQuery& q, const float4* __restr
 // DYN (runs on the incremental map): the runs index P.rpts with deletion marks,
 // and a list the cube does not certify is left uncertified (the caller's
 // canonical resolution), since the cell walk's grid positions index another array.
-template <bool DYN = false>
+// NOWALK: a list the cube does not certify is returned uncertified (the caller
+// walks the cells wave-parallel, walk_wave) instead of walking them here.
+template <bool DYN = false, bool NOWALK = false>
 __device__ __forceinline__ bool vrun_search(LeafQuery& q, const KnnParams& P, bool valid, int c0, int c1, int c2,
                                             int s0, int s1, int s2, unsigned& visits, unsigned& npts) {
     if (!valid || !(P.lM > 0)) return false;
@@ -1587,6 +1596,9 @@ __device__ __forceinline__ bool vrun_search(LeafQuery& q, const KnnParams& P, bo
         if (inside) return true;
     }
     if constexpr (DYN) return false;
+    if constexpr (NOWALK) {
+        if (t < INFINITY) return false;  // (the wave walk; without 5 points in the cube, the walk below)
+    }
     TileView none;
     return grid_search(q, P, c0, c1, c2, s0, s1, s2, none, visits, npts, nullptr, true);
 }
@@ -1696,6 +1708,122 @@ __device__ __forceinline__ bool delta_search(LeafQuery& q, const KnnParams& P, u
     return true;
 }
 
+// The cell walk of the queries of a wave that the runs leave uncertified (the
+// ball of their bound leaves the 3x3x3 cube: queries far from the surfaces),
+// each by the whole wave: the cells within the query's bound T (finite: the
+// runs found 5 points, T >= d5) are dealt to the 64 lanes, 64 per round; a lane
+// skips a cell whose box lies beyond T (+ 1e-10, the margins of grid_search's
+// range), probes it and offers its points to a list of its own; the 64 lists
+// are then merged (5 extractions of the wave minimum, e6 = min of the sixth
+// extraction and every lane's e6).  Every point within T of the query was
+// offered, so the merged list is exact and e6 the smallest distance beyond it:
+// lq_finish's C1 / C2 checks hold as for grid_search's list.  The query's list
+// is rebuilt from scratch on the cell grid (candidates: grid positions; on an
+// incremental map the current grid).  One thread walking the same cells
+// serially (grid_search) took up to ~100 dependent round trips: one such query
+// held its block and its scan's solve (first evaluations of 0.35 vs 0.14 ms
+// on the batches with a query 0.5 m off the surfaces).  A query whose box
+// exceeds kWalkMaxCells stays uncertified (the exact replay).
+constexpr int kWalkMaxCells = 1024;
+__device__ __forceinline__ bool walk_wave(LeafQuery& q, const KnnParams& P, bool need, float Tl, unsigned& visits,
+                                          unsigned& npts) {
+    unsigned long long m = __ballot(need);
+    bool done = false;
+    const int lane = (int)(threadIdx.x & 63u);
+    const float4* __restrict__ gpts = reinterpret_cast<const float4*>(P.gpts);
+    const uint64_t mask = (1ull << P.glog2) - 1ull;
+    const float h = P.gh, eps = P.geps;
+    while (m) {  // wave-uniform
+        const int l = __ffsll((long long)m) - 1;
+        m &= m - 1ull;
+        LeafQuery w;
+        w.qx = __shfl(q.qx, l);
+        w.qy = __shfl(q.qy, l);
+        w.qz = __shfl(q.qz, l);
+        const float T = __shfl(Tl, l);  // (Tl: the lane's bound, lq_thr of its list before the walk)
+        if (!(T < INFINITY)) continue;
+        const double rad = sqrt((double)T + 1e-9) * (1.0 + 1e-5) + (double)eps;
+        const double ih = 1.0 / (double)h, lim = (double)(kGridBias - 8);
+        const double q3[3] = {(double)w.qx, (double)w.qy, (double)w.qz};
+        int lo[3], n[3];
+        double span = 1.0;
+        bool ok = true;
+#pragma unroll
+        for (int a = 0; a < 3; a++) {
+            const double a0 = floor((q3[a] - rad - (double)P.gorg[a]) * ih), a1 = floor((q3[a] + rad - (double)P.gorg[a]) * ih);
+            ok = ok && fabs(a0) < lim && fabs(a1) < lim;
+            lo[a] = ok ? (int)a0 : 0;
+            n[a] = ok ? (int)(a1 - a0) + 1 : 1;
+            span *= a1 - a0 + 1.0;
+        }
+        if (!ok || span > (double)kWalkMaxCells) continue;
+        const int cells = n[0] * n[1] * n[2];
+#pragma unroll
+        for (int k = 0; k < kNN; k++) { w.d[k] = INFINITY; w.nd[k] = 0u; }
+        w.e6 = INFINITY;
+        w.B = INFINITY;
+#pragma unroll 1
+        for (int t = lane; t < cells; t += 64) {
+            const int cx = lo[0] + t % n[0], cy = lo[1] + (t / n[0]) % n[1], cz = lo[2] + t / (n[0] * n[1]);
+            const float x0 = P.gorg[0] + (float)cx * h - eps, y0 = P.gorg[1] + (float)cy * h - eps;
+            const float z0 = P.gorg[2] + (float)cz * h - eps;
+            const float wd = h + 2 * eps;
+            if (box_dist(w.qx, w.qy, w.qz, x0, x0 + wd, y0, y0 + wd, z0, z0 + wd) - T > kFuzz) continue;
+            const unsigned long long key = grid_key_d(cx, cy, cz);
+            uint64_t sl = (uint64_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - P.glog2));
+            GridSlot g = P.gslots[sl];
+            visits++;
+            while (g.key != key && g.key != kGridEmpty) {
+                sl = (sl + 1) & mask;
+                g = P.gslots[sl];
+                visits++;
+            }
+            if (g.key != key) continue;
+            npts += g.count;
+            const uint32_t s0 = g.start, s1 = g.start + g.count;
+#pragma unroll 1
+            for (uint32_t k0 = s0; k0 < s1; k0 += 4) {
+                float4 v[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) v[u] = gpts[k0 + u];  // (the grid is padded by 3 points)
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    if (k0 + u < s1) lq_point(w, v[u], k0 + u);
+            }
+        }
+        // merge the 64 lists into the owner's: the wave minimum of the lists' heads, five times
+#pragma unroll
+        for (int r = 0; r < kNN; r++) {
+            float mn = w.d[0];
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) mn = fminf(mn, __shfl_xor(mn, o));
+            const unsigned long long who = __ballot(w.d[0] == mn);
+            const int wl = __ffsll((long long)who) - 1;
+            const uint32_t nd = (uint32_t)__shfl((int)w.nd[0], wl);
+            if (lane == l) {
+                q.d[r] = mn;
+                q.nd[r] = nd;
+            }
+            if (lane == wl) {  // pop the head
+#pragma unroll
+                for (int k = 0; k + 1 < kNN; k++) { w.d[k] = w.d[k + 1]; w.nd[k] = w.nd[k + 1]; }
+                w.d[kNN - 1] = w.e6;  // (the lane's sixth: its e6 moves up)
+                w.nd[kNN - 1] = 0u;
+                w.e6 = INFINITY;
+            }
+        }
+        float e6 = fminf(w.d[0], w.e6);  // heads left and the lanes' own sixth
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) e6 = fminf(e6, __shfl_xor(e6, o));
+        if (lane == l) {
+            q.e6 = e6;
+            q.B = INFINITY;
+            done = true;
+        }
+    }
+    return done;
+}
+
 // 512 points / 128 cells per wave (10.5 KB): 4 waves per SIMD (VGPR-bound);
 // on MI355X 1024 / 256 (18.5 KB, 2 waves per SIMD) was 12 % slower at config 2
 #ifndef LIVO_TILE_CELLS
@@ -1774,7 +1902,8 @@ __global__ __launch_bounds__(kEvalBlock) void k_knn_runs(KnnParams P) {
         certified = brun_search(q, P, valid, visits, npts);
         if (valid && !certified) lq_init<false>(q, P, slot, job, i, valid);
     }
-    if (!certified) certified = vrun_search(q, P, valid, c0, c1, c2, s0, s1, s2, visits, npts);
+    if (!certified) certified = vrun_search<false, true>(q, P, valid, c0, c1, c2, s0, s1, s2, visits, npts);
+    if (walk_wave(q, P, valid && !certified && lq_thr(q) < INFINITY, lq_thr(q), visits, npts)) certified = true;
     if (valid) lq_finish<false>(q, P, job, bjob, i, reinterpret_cast<const float4*>(P.gpts), !certified, true);
     count_visits(P, slot, visits, npts);
 }
@@ -2752,15 +2881,7 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
     } U;
     unsigned bjob, bx;
     // the same block order in every evaluation: the plane caches stay in the L2 that wrote them
-    if (P.xcd_chunk < 0) {  // (uniform) dynamic order: the next (scan, block) item of the launch's counter
-        __shared__ unsigned s_item;
-        if (threadIdx.x == 0) s_item = atomicAdd(P.work_ctr, 1u);
-        __syncthreads();
-        bjob = s_item / (unsigned)P.nb;
-        bx = s_item % (unsigned)P.nb;
-    } else {
-        xcd_chunk_block(P.nb, P.xcd_chunk, bjob, bx);
-    }
+    xcd_chunk_block(P.nb, P.xcd_chunk, bjob, bx);
     const HsJob job = P.jobs[bjob];
     IekfSlot* slot = job.slot;
     if (bx > 0 && (int)bx * kEvalBlock >= job.n) return;  // (an empty scan keeps one block: it solves)
@@ -2814,18 +2935,24 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
 #endif
             if (!certified)
                 certified = dyn ? vrun_search<true>(q, P, valid, c0, c1, c2, s0, s1, s2, visits, npts)
-                                : vrun_search<false>(q, P, valid, c0, c1, c2, s0, s1, s2, visits, npts);
+                                : vrun_search<false, true>(q, P, valid, c0, c1, c2, s0, s1, s2, visits, npts);
             // the incremental map's points added since its runs (none: no delta grid)
             if (dyn && valid && certified && P.dslots) certified = delta_search(q, P, visits, npts);
-            // a query the runs (+ delta) do not certify on the incremental map: the
-            // cell walk of the current grid from scratch (its candidates index P.gpts)
+            // a query the runs (+ delta) leave uncertified with a finite bound: the cell
+            // walk of the (current) grid by the whole wave, from scratch (candidates: grid
+            // positions); without 5 points in the cube, vrun_search's serial walk
             bool walked = false;
-            if (dyn && valid && !certified) {
-                lq_init<false>(q, P, slot, job, i, valid);
-                TileView none;
-                certified = grid_search(q, P, c0, c1, c2, s0, s1, s2, none, visits, npts);
+#ifndef LIVO_NO_WAVE_WALK
+            if (walk_wave(q, P, valid && !certified && lq_thr(q) < INFINITY, lq_thr(q), visits, npts)) {
+                certified = true;
                 walked = true;
             }
+#else
+            if (false) {
+            }
+#endif
+            // (on the incremental map a query without 5 base points in its cube stays
+            // uncertified: the canonical resolution of the current grid takes it)
 #ifdef LIVO_EVAL_PROF
             {  // block totals: lanes past the 2x2x2 block, run entries scanned, ambiguous
                 const unsigned long long nf = __ballot(valid && !certified);
@@ -2868,7 +2995,7 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
                                           !certified, false, reinterpret_cast<const float4*>(P.dpts), nb);
                 else
                     amb = lq_finish<!LIVO_IDX_RUNS>(q, P, job, bjob, i, reinterpret_cast<const float4*>(P.gpts),
-                                                    !certified, false, runs, nb);
+                                                    !certified, false, walked ? nullptr : runs, nb);
                 // the plane from the neighbours in registers (18643 vs 18011 updates/s
                 // re-reading the record just written, profiles/r03_ab_prefit_seed.txt)
                 if (!amb && (!P.canon || dyn)) {  // (a replayed query's plane is fitted from its record below)
