@@ -132,6 +132,9 @@ struct DynDev {
     GridSlot* dslots = nullptr;
     float* dpts = nullptr;
     int32_t dlog2 = 4;
+    GridSlot* dvslots = nullptr;     // the delta grid's cell runs (positions in dpts)
+    RunWord* dvidx = nullptr;
+    int32_t dvlog2 = 4;
     int64_t d_n = 0, dslot_cap = 0, dpts_cap = 0;
     int64_t rebases = 0;
     double rebase_frac = 0.125;      // LIVO_DYN_REBASE
@@ -187,7 +190,11 @@ struct livo_ctx {
     float grid_cell = 0.f;             // cell edge (LIVO_GRID_CELL; 0: from the map)
     float grid_ppc = 0.f;              // target points per occupied cell when chosen from the map (LIVO_GRID_PPC)
     bool vruns = true;                 // cell runs on a static map (LIVO_VRUNS=0: the cell walk)
-    int xcd_chunk = 0;                 // k_iekf_eval block order (LIVO_XCD_CHUNK; 0: one range per XCD)
+    // k_iekf_eval block order (LIVO_XCD_CHUNK): XCD-interleaved chunks of 8 blocks, so
+    // every XCD holds a share of every scan (distinct-scan pool: 18.6k vs 17.6k /
+    // 18.3k vs 17.1k / 17.1k vs 16.4k updates/s against 0, one range per XCD, whose
+    // most expensive scan's XCD was the straggler; profiles/r04_ab_block_order.txt)
+    int xcd_chunk = 8;
     GridSlot* vslots = nullptr;        // vertex runs (static map only)
     RunWord* vpts = nullptr;           // run entries (LIVO_IDX_RUNS: grid positions; else x, y, z, map index bits)
     int32_t vlog2 = 0;
@@ -438,6 +445,9 @@ static KnnParams make_knn_params(livo_ctx* c) {
     kp.dslots = dyn_runs && c->dyn.d_n > 0 ? c->dyn.dslots : nullptr;
     kp.dpts = dyn_runs ? c->dyn.dpts : nullptr;
     kp.dlog2 = c->dyn.dlog2;
+    kp.dvslots = dyn_runs && c->dyn.d_n > 0 ? c->dyn.dvslots : nullptr;
+    kp.dvidx = c->dyn.dvidx;
+    kp.dvlog2 = c->dyn.dvlog2;
     kp.dyn_runs = dyn_runs ? 1 : 0;
     kp.vslots = vr ? c->vslots : nullptr;
     kp.vpts = vr ? c->vpts : nullptr;
@@ -897,6 +907,10 @@ static ScanBuf* get_scan(livo_ctx* c, int32_t id);
 }
 static int build_cell_runs(livo_ctx* c, int64_t M);
 static int build_ball_runs(livo_ctx* c, int64_t M, float r5, double ext);
+#if LIVO_IDX_RUNS
+static int build_cell_runs_into(livo_ctx* c, const float* pts, int64_t M, GridSlot** slots, RunWord** idx,
+                                int32_t* log2, int64_t* words);
+#endif
 static void dyn_free(DynDev& d) {
     dev_free(d.all); dev_free(d.alive);
     dev_free(d.keys); dev_free(d.skeys); dev_free(d.iota); dev_free(d.svals);
@@ -905,6 +919,7 @@ static void dyn_free(DynDev& d) {
     dev_free(d.defer); dev_free(d.dpos); dev_free(d.dlist); dev_free(d.keep); dev_free(d.apos);
     dev_free(d.boxes); dev_free(d.dirty); dev_free(d.ctr);
     dev_free(d.rpts); dev_free(d.rpos); dev_free(d.dslots); dev_free(d.dpts);
+    dev_free(d.dvslots); dev_free(d.dvidx);
     d = DynDev{};
 }
 
@@ -1095,6 +1110,17 @@ static int dyn_runs_update(livo_ctx* c) {
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(c->stream));
     d.dlog2 = log2;
+#if LIVO_IDX_RUNS
+    // and its cell runs: a query scans its cube's delta points in one run, as the base's
+    int64_t words = 0;
+    rc = build_cell_runs_into(c, d.dpts, nd, &d.dvslots, &d.dvidx, &d.dvlog2, &words);
+    if (rc) {
+        (void)hipGetLastError();
+        dev_free(d.dvslots);
+        dev_free(d.dvidx);
+        return rc == LIVO_E_OOM || rc == LIVO_E_RANGE ? dyn_rebase(c) : rc;
+    }
+#endif
     return LIVO_OK;
 }
 
@@ -1526,10 +1552,29 @@ static int build_index_runs(livo_ctx* c, int64_t n, const unsigned long long* sk
 // The cell runs of the static map's grid (livo_internal.h), built on the
 // device: two stable radix sorts (rho2, then the run key) of the 27 M entries,
 // the runs' heads and starts, and their hash table (load factor <= 1/4).
+#if LIVO_IDX_RUNS
+static int build_cell_runs_into(livo_ctx* c, const float* pts, int64_t M, GridSlot** slots, RunWord** idx,
+                                int32_t* log2, int64_t* words);
 static int build_cell_runs(livo_ctx* c, int64_t M) {
+    int64_t words = 0;
+    const int rc = build_cell_runs_into(c, c->gpts, M, &c->vslots, &c->vpts, &c->vlog2, &words);
+    if (!rc && M > 0) c->grid_bytes += (int64_t)(((int64_t)1 << c->vlog2) * sizeof(GridSlot) + words * sizeof(RunWord));
+    return rc;
+}
+// The cell runs of M grid-ordered points pts (the map's grid; on the incremental
+// map also its delta grid): *slots / *idx replaced, run entries = positions in pts.
+static int build_cell_runs_into(livo_ctx* c, const float* pts, int64_t M, GridSlot** slots, RunWord** idx,
+                                int32_t* log2, int64_t* words) {
+    dev_free(*slots);
+    dev_free(*idx);
+    if (M <= 0) return LIVO_OK;
+#else
+static int build_cell_runs(livo_ctx* c, int64_t M) {
+    const float* pts = c->gpts;
     dev_free(c->vslots);
     dev_free(c->vpts);
     if (M <= 0) return LIVO_OK;
+#endif
     const int64_t n = M * 27;
     if (n + 8 >= (int64_t)kRunPosLimit) return LIVO_E_RANGE;  // 31-bit run positions (kRunPos)
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
@@ -1552,7 +1597,7 @@ static int build_cell_runs(livo_ctx* c, int64_t M) {
 #if !LIVO_IDX_RUNS
     if (dev_alloc(&c->vpts, (size_t)(n + kRunPad) * kRunWords)) rc = LIVO_E_OOM;
 #endif
-    if (!rc) rc = launch_cr_rho(c->gpts, n, c->gorg, c->gh, rho, iota, c->stream);
+    if (!rc) rc = launch_cr_rho(pts, n, c->gorg, c->gh, rho, iota, c->stream);
     if (!rc) {
         size_t tb = 0;
         rc = prim_sort_pairs_u32(nullptr, &tb, rho, srho, iota, e1, n, 32, c->stream);
@@ -1560,19 +1605,16 @@ static int build_cell_runs(livo_ctx* c, int64_t M) {
         tb = c->prim_bytes;
         if (!rc) rc = prim_sort_pairs_u32(c->prim_tmp, &tb, rho, srho, iota, e1, n, 32, c->stream);
     }
-    if (!rc) rc = launch_cr_key(c->gpts, e1, n, c->gorg, c->gh, keys, c->stream);
+    if (!rc) rc = launch_cr_key(pts, e1, n, c->gorg, c->gh, keys, c->stream);
     if (!rc) rc = sort_u64(c, keys, skeys, e1, e2, n);
 #if LIVO_IDX_RUNS
-    int64_t words = 0;
     // (rho, iota: dead after the sorts) the padded run lengths and their scan
-    if (!rc) rc = build_index_runs(c, n, skeys, e2, nullptr, heads, runid, starts, nruns, rho, iota, &c->vpts,
-                                   &c->vslots, &c->vlog2, &words);
+    if (!rc) rc = build_index_runs(c, n, skeys, e2, nullptr, heads, runid, starts, nruns, rho, iota, idx, slots, log2,
+                                   words);
     (void)hipFree(scr);
-    if (rc) return rc;
-    c->grid_bytes += (int64_t)(((int64_t)1 << c->vlog2) * sizeof(GridSlot) + words * sizeof(RunWord));
-    return LIVO_OK;
+    return rc;
 #else
-    if (!rc) rc = launch_cr_fill(c->gpts, e2, skeys, n, c->gorg, c->gh, c->vpts, heads, c->stream);
+    if (!rc) rc = launch_cr_fill(pts, e2, skeys, n, c->gorg, c->gh, c->vpts, heads, c->stream);
     if (!rc) rc = ivox_scan(c, heads, runid, n);
     if (!rc) rc = launch_dyn_runs(heads, runid, n, starts, nruns, c->stream);
     unsigned long long runs = 0;

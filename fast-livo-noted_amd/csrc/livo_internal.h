@@ -338,6 +338,9 @@ struct KnnParams {
     int32_t dlog2;
     const GridSlot* dslots; // delta grid (null: no point added since the base); points in dpts
     const float* dpts;
+    const GridSlot* dvslots;  // the delta grid's cell runs (null: none); entries = positions in dpts
+    const RunWord* dvidx;
+    int32_t dvlog2;
 };
 
 struct SolveParams {

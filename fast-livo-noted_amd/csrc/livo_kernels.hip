@@ -1463,7 +1463,8 @@ __device__ __forceinline__ void run_chunk(LeafQuery& q, const float4 (&v)[8], ui
 // comparison of the list admits (lq_offer: NaN < d is false, fminf drops it),
 // and as a chunk's first entry it never stops the scan (NaN > b is false).
 __device__ __forceinline__ uint32_t scan_run(LeafQuery& q, const uint32_t* __restrict__ run, uint32_t cnt,
-                                             const float4* __restrict__ pts, float cx, float cy, float cz, float dqv) {
+                                             const float4* __restrict__ pts, float cx, float cy, float cz, float dqv,
+                                             uint32_t tag = 0u) {
     if (cnt == 0) return 0;
     const uint4* __restrict__ r4 = reinterpret_cast<const uint4*>(run);  // (run start: a multiple of 4 words)
     uint4 ia = r4[0], ib = r4[1];  // (padded: kRunPad words behind the last run)
@@ -1480,7 +1481,7 @@ __device__ __forceinline__ uint32_t scan_run(LeafQuery& q, const uint32_t* __res
         }
         const float b = run_bound(q, dqv);
         if (centre_d2(cx, cy, cz, v[0].x, v[0].y, v[0].z) > b * b) break;  // rho of every later entry > b
-        run_chunk(q, v, k0, cnt, [&](int u) { return id[u]; });
+        run_chunk(q, v, k0, cnt, [&](int u) { return id[u] | tag; });
     }
     return min(k0, cnt);
 }
@@ -1552,9 +1553,7 @@ __device__ __forceinline__ uint32_t scan_run(LeafQuery& q, const float4* __restr
 // DYN (runs on the incremental map): the runs index P.rpts with deletion marks,
 // and a list the cube does not certify is left uncertified (the caller's
 // canonical resolution), since the cell walk's grid positions index another array.
-// NOWALK: a list the cube does not certify is returned uncertified (the caller
-// walks the cells wave-parallel, walk_wave) instead of walking them here.
-template <bool DYN = false, bool NOWALK = false>
+template <bool DYN = false>
 __device__ __forceinline__ bool vrun_search(LeafQuery& q, const KnnParams& P, bool valid, int c0, int c1, int c2,
                                             int s0, int s1, int s2, unsigned& visits, unsigned& npts) {
     if (!valid || !(P.lM > 0)) return false;
@@ -1596,9 +1595,6 @@ __device__ __forceinline__ bool vrun_search(LeafQuery& q, const KnnParams& P, bo
         if (inside) return true;
     }
     if constexpr (DYN) return false;
-    if constexpr (NOWALK) {
-        if (t < INFINITY) return false;  // (the wave walk; without 5 points in the cube, the walk below)
-    }
     TileView none;
     return grid_search(q, P, c0, c1, c2, s0, s1, s2, none, visits, npts, nullptr, true);
 }
@@ -1658,6 +1654,51 @@ __device__ __forceinline__ bool brun_search(LeafQuery& q, const KnnParams& P, bo
     return b * b <= P.bcert2;
 }
 
+#if LIVO_IDX_RUNS
+// The incremental map's delta (points added since its runs were built) has
+// cell runs of its own over the delta grid: the query's cell's run (its
+// 3x3x3 cube's delta points, sorted by rho2) scanned like the base's, its
+// candidates tagged kRunPos | position in P.dpts.  Together with the base's
+// run the cube's points are then all scanned: a list whose bound ball lies in
+// the cube (cube_inside) is exact over both sets.
+__device__ __forceinline__ void dvrun_scan(LeafQuery& q, const KnnParams& P, int c0, int c1, int c2, unsigned& visits,
+                                           unsigned& npts) {
+    const unsigned long long key = grid_key_d(c0, c1, c2);
+    const uint64_t mask = (1ull << P.dvlog2) - 1ull;
+    uint64_t sl = (uint64_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - P.dvlog2));
+    GridSlot g = P.dvslots[sl];
+    visits++;
+    while (g.key != key && g.key != kGridEmpty) {
+        sl = (sl + 1) & mask;
+        g = P.dvslots[sl];
+        visits++;
+    }
+    if (g.key != key) return;
+    const float h = P.gh;
+    const float cx = cell_centre(P.gorg[0], h, c0), cy = cell_centre(P.gorg[1], h, c1);
+    const float cz = cell_centre(P.gorg[2], h, c2);
+    const float dqv = __builtin_amdgcn_sqrtf(centre_d2(cx, cy, cz, q.qx, q.qy, q.qz)) * (1.0f + 1e-6f);
+    npts += scan_run(q, P.dvidx + g.start, g.count, reinterpret_cast<const float4*>(P.dpts), cx, cy, cz, dqv, kRunPos);
+}
+#endif
+// true when the ball of the list's bound (+ grid_search's margins) lies in the cube [c - 1, c + 1]
+__device__ __forceinline__ bool cube_inside(const LeafQuery& q, const KnnParams& P, int c0, int c1, int c2) {
+    const float t = lq_thr(q);
+    if (!(t < INFINITY)) return false;
+    const double rad = sqrt((double)t + 1e-9) * (1.0 + 1e-5) + (double)P.geps;
+    const double ih = 1.0 / (double)P.gh;
+    const double q3[3] = {(double)q.qx, (double)q.qy, (double)q.qz};
+    const int cc[3] = {c0, c1, c2};
+    bool inside = true;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const double l = floor((q3[a] - rad - (double)P.gorg[a]) * ih);
+        const double hh = floor((q3[a] + rad - (double)P.gorg[a]) * ih);
+        inside = inside && l >= (double)(cc[a] - 1) && hh <= (double)(cc[a] + 1);
+    }
+    return inside;
+}
+
 // The delta grid of the incremental map (points added since its runs were
 // built; the cell grid's layout in P.dslots / P.dpts): every point of the
 // cells the ball of the current bound reaches (with grid_search's margins) is
@@ -1706,122 +1747,6 @@ __device__ __forceinline__ bool delta_search(LeafQuery& q, const KnnParams& P, u
                 for (uint32_t k = g.start; k < g.start + g.count; k++) lq_point(q, dp[k], kRunPos | k);
             }
     return true;
-}
-
-// The cell walk of the queries of a wave that the runs leave uncertified (the
-// ball of their bound leaves the 3x3x3 cube: queries far from the surfaces),
-// each by the whole wave: the cells within the query's bound T (finite: the
-// runs found 5 points, T >= d5) are dealt to the 64 lanes, 64 per round; a lane
-// skips a cell whose box lies beyond T (+ 1e-10, the margins of grid_search's
-// range), probes it and offers its points to a list of its own; the 64 lists
-// are then merged (5 extractions of the wave minimum, e6 = min of the sixth
-// extraction and every lane's e6).  Every point within T of the query was
-// offered, so the merged list is exact and e6 the smallest distance beyond it:
-// lq_finish's C1 / C2 checks hold as for grid_search's list.  The query's list
-// is rebuilt from scratch on the cell grid (candidates: grid positions; on an
-// incremental map the current grid).  One thread walking the same cells
-// serially (grid_search) took up to ~100 dependent round trips: one such query
-// held its block and its scan's solve (first evaluations of 0.35 vs 0.14 ms
-// on the batches with a query 0.5 m off the surfaces).  A query whose box
-// exceeds kWalkMaxCells stays uncertified (the exact replay).
-constexpr int kWalkMaxCells = 1024;
-__device__ __forceinline__ bool walk_wave(LeafQuery& q, const KnnParams& P, bool need, float Tl, unsigned& visits,
-                                          unsigned& npts) {
-    unsigned long long m = __ballot(need);
-    bool done = false;
-    const int lane = (int)(threadIdx.x & 63u);
-    const float4* __restrict__ gpts = reinterpret_cast<const float4*>(P.gpts);
-    const uint64_t mask = (1ull << P.glog2) - 1ull;
-    const float h = P.gh, eps = P.geps;
-    while (m) {  // wave-uniform
-        const int l = __ffsll((long long)m) - 1;
-        m &= m - 1ull;
-        LeafQuery w;
-        w.qx = __shfl(q.qx, l);
-        w.qy = __shfl(q.qy, l);
-        w.qz = __shfl(q.qz, l);
-        const float T = __shfl(Tl, l);  // (Tl: the lane's bound, lq_thr of its list before the walk)
-        if (!(T < INFINITY)) continue;
-        const double rad = sqrt((double)T + 1e-9) * (1.0 + 1e-5) + (double)eps;
-        const double ih = 1.0 / (double)h, lim = (double)(kGridBias - 8);
-        const double q3[3] = {(double)w.qx, (double)w.qy, (double)w.qz};
-        int lo[3], n[3];
-        double span = 1.0;
-        bool ok = true;
-#pragma unroll
-        for (int a = 0; a < 3; a++) {
-            const double a0 = floor((q3[a] - rad - (double)P.gorg[a]) * ih), a1 = floor((q3[a] + rad - (double)P.gorg[a]) * ih);
-            ok = ok && fabs(a0) < lim && fabs(a1) < lim;
-            lo[a] = ok ? (int)a0 : 0;
-            n[a] = ok ? (int)(a1 - a0) + 1 : 1;
-            span *= a1 - a0 + 1.0;
-        }
-        if (!ok || span > (double)kWalkMaxCells) continue;
-        const int cells = n[0] * n[1] * n[2];
-#pragma unroll
-        for (int k = 0; k < kNN; k++) { w.d[k] = INFINITY; w.nd[k] = 0u; }
-        w.e6 = INFINITY;
-        w.B = INFINITY;
-#pragma unroll 1
-        for (int t = lane; t < cells; t += 64) {
-            const int cx = lo[0] + t % n[0], cy = lo[1] + (t / n[0]) % n[1], cz = lo[2] + t / (n[0] * n[1]);
-            const float x0 = P.gorg[0] + (float)cx * h - eps, y0 = P.gorg[1] + (float)cy * h - eps;
-            const float z0 = P.gorg[2] + (float)cz * h - eps;
-            const float wd = h + 2 * eps;
-            if (box_dist(w.qx, w.qy, w.qz, x0, x0 + wd, y0, y0 + wd, z0, z0 + wd) - T > kFuzz) continue;
-            const unsigned long long key = grid_key_d(cx, cy, cz);
-            uint64_t sl = (uint64_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - P.glog2));
-            GridSlot g = P.gslots[sl];
-            visits++;
-            while (g.key != key && g.key != kGridEmpty) {
-                sl = (sl + 1) & mask;
-                g = P.gslots[sl];
-                visits++;
-            }
-            if (g.key != key) continue;
-            npts += g.count;
-            const uint32_t s0 = g.start, s1 = g.start + g.count;
-#pragma unroll 1
-            for (uint32_t k0 = s0; k0 < s1; k0 += 4) {
-                float4 v[4];
-#pragma unroll
-                for (int u = 0; u < 4; u++) v[u] = gpts[k0 + u];  // (the grid is padded by 3 points)
-#pragma unroll
-                for (int u = 0; u < 4; u++)
-                    if (k0 + u < s1) lq_point(w, v[u], k0 + u);
-            }
-        }
-        // merge the 64 lists into the owner's: the wave minimum of the lists' heads, five times
-#pragma unroll
-        for (int r = 0; r < kNN; r++) {
-            float mn = w.d[0];
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) mn = fminf(mn, __shfl_xor(mn, o));
-            const unsigned long long who = __ballot(w.d[0] == mn);
-            const int wl = __ffsll((long long)who) - 1;
-            const uint32_t nd = (uint32_t)__shfl((int)w.nd[0], wl);
-            if (lane == l) {
-                q.d[r] = mn;
-                q.nd[r] = nd;
-            }
-            if (lane == wl) {  // pop the head
-#pragma unroll
-                for (int k = 0; k + 1 < kNN; k++) { w.d[k] = w.d[k + 1]; w.nd[k] = w.nd[k + 1]; }
-                w.d[kNN - 1] = w.e6;  // (the lane's sixth: its e6 moves up)
-                w.nd[kNN - 1] = 0u;
-                w.e6 = INFINITY;
-            }
-        }
-        float e6 = fminf(w.d[0], w.e6);  // heads left and the lanes' own sixth
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) e6 = fminf(e6, __shfl_xor(e6, o));
-        if (lane == l) {
-            q.e6 = e6;
-            q.B = INFINITY;
-            done = true;
-        }
-    }
-    return done;
 }
 
 // 512 points / 128 cells per wave (10.5 KB): 4 waves per SIMD (VGPR-bound);
@@ -1902,8 +1827,7 @@ __global__ __launch_bounds__(kEvalBlock) void k_knn_runs(KnnParams P) {
         certified = brun_search(q, P, valid, visits, npts);
         if (valid && !certified) lq_init<false>(q, P, slot, job, i, valid);
     }
-    if (!certified) certified = vrun_search<false, true>(q, P, valid, c0, c1, c2, s0, s1, s2, visits, npts);
-    if (walk_wave(q, P, valid && !certified && lq_thr(q) < INFINITY, lq_thr(q), visits, npts)) certified = true;
+    if (!certified) certified = vrun_search(q, P, valid, c0, c1, c2, s0, s1, s2, visits, npts);
     if (valid) lq_finish<false>(q, P, job, bjob, i, reinterpret_cast<const float4*>(P.gpts), !certified, true);
     count_visits(P, slot, visits, npts);
 }
@@ -2935,24 +2859,26 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
 #endif
             if (!certified)
                 certified = dyn ? vrun_search<true>(q, P, valid, c0, c1, c2, s0, s1, s2, visits, npts)
-                                : vrun_search<false, true>(q, P, valid, c0, c1, c2, s0, s1, s2, visits, npts);
-            // the incremental map's points added since its runs (none: no delta grid)
-            if (dyn && valid && certified && P.dslots) certified = delta_search(q, P, visits, npts);
-            // a query the runs (+ delta) leave uncertified with a finite bound: the cell
-            // walk of the (current) grid by the whole wave, from scratch (candidates: grid
-            // positions); without 5 points in the cube, vrun_search's serial walk
-            bool walked = false;
-#ifndef LIVO_NO_WAVE_WALK
-            if (walk_wave(q, P, valid && !certified && lq_thr(q) < INFINITY, lq_thr(q), visits, npts)) {
-                certified = true;
-                walked = true;
-            }
-#else
-            if (false) {
+                                : vrun_search<false>(q, P, valid, c0, c1, c2, s0, s1, s2, visits, npts);
+            // the incremental map's points added since its runs (none: no delta grid): the
+            // cube's delta run; the list is exact if the base was and its ball lies in the cube
+#if LIVO_IDX_RUNS
+            if (dyn && valid && P.dvslots) {
+                dvrun_scan(q, P, c0, c1, c2, visits, npts);
+                certified = certified && cube_inside(q, P, c0, c1, c2);
+            } else if (dyn && valid && certified && P.dslots) {
+                certified = delta_search(q, P, visits, npts);
             }
 #endif
-            // (on the incremental map a query without 5 base points in its cube stays
-            // uncertified: the canonical resolution of the current grid takes it)
+            // (a query the runs leave uncertified: vrun_search's serial walk beyond the cube; a
+            // wave-parallel walk of one query's cells was slower)
+            bool walked = false;
+            if (dyn && valid && !certified) {  // the incremental map: the current grid's serial walk
+                lq_init<false>(q, P, slot, job, i, valid);
+                TileView none;
+                certified = grid_search(q, P, c0, c1, c2, s0, s1, s2, none, visits, npts);
+                walked = true;
+            }
 #ifdef LIVO_EVAL_PROF
             {  // block totals: lanes past the 2x2x2 block, run entries scanned, ambiguous
                 const unsigned long long nf = __ballot(valid && !certified);
