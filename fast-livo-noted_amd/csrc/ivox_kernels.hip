@@ -683,6 +683,12 @@ __global__ void k_iv_untouched(IvoxParams P, const uint32_t* sorted_slot, int64_
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k < n) flags[k] = P.lastp1[sorted_slot[k]] == 0u ? 1u : 0u;
 }
+// Per old grid (oldest first) the batch's first touch (0xFFFFFFFF: untouched),
+// for the host's run-of-evictions scan (ivox_evict_prefix).
+__global__ void k_iv_oldfirst(IvoxParams P, const uint32_t* sorted_slot, int64_t n, uint32_t* out) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n) out[k] = P.first[sorted_slot[k]];
+}
 // Oldest first: the first ev untouched grids are the victims, unless a grid the
 // batch touches only at or after the first eviction is older than the last of
 // them (it would be evicted and re-created): that is flagged (ctr[0] bit 2).
@@ -769,6 +775,9 @@ int launch_ivox_oldkeys(const IvoxParams& p, unsigned long long* keys, uint32_t*
 }
 int launch_ivox_untouched(const IvoxParams& p, const uint32_t* sorted_slot, int64_t n, uint32_t* flags, void* stream) {
     LAUNCH_CHECKED(k_iv_untouched, n, p, sorted_slot, n, flags);
+}
+int launch_ivox_oldfirst(const IvoxParams& p, const uint32_t* sorted_slot, int64_t n, uint32_t* out, void* stream) {
+    LAUNCH_CHECKED(k_iv_oldfirst, n, p, sorted_slot, n, out);
 }
 int launch_ivox_victims(const IvoxParams& p, const uint32_t* sorted_slot, const uint32_t* rank, int64_t n, int64_t ev,
                         uint32_t j_first, void* stream) {

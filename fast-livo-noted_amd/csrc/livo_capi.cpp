@@ -69,6 +69,7 @@ static void free_scan_buf(ScanBuf& s) {
 // The device iVox map and its AddPoints / overflow-pass scratch.
 struct IvoxDev {
     bool ready = false;
+    int64_t add_passes = 0;  // device passes AddPoints took (one per batch, more at LRU conflicts)
     livo_ivox_params prm{};
     float inv_res = 5.0f;
     int nearby = 19;
@@ -726,6 +727,39 @@ static int ivox_ev_scratch(livo_ctx* c, int64_t need) {
     return LIVO_OK;
 }
 
+// The longest prefix [0, *pend) of the batch whose evictions all take old
+// grids the prefix never touches, and their count *evs (0: the first eviction
+// already needs a grid the batch touched before it).  At eviction k (the point
+// t_ev[k] creating a new grid) grids_cache_.back() is the oldest old grid the
+// batch has not touched before t_ev[k] (touched ones moved to the front,
+// ivox3d.h:263-268); a victim the batch touches again later would be
+// re-created, so the prefix ends before that touch.  Victims advance
+// monotonically along the LRU order: one host pass over the old grids' first
+// touches.
+static int ivox_evict_prefix(livo_ctx* c, const IvoxParams& P, int64_t n_old, const std::vector<uint32_t>& t_ev,
+                             int64_t n, int64_t* pend, int64_t* evs) {
+    IvoxDev& v = c->iv;
+    std::vector<uint32_t> f((size_t)n_old);
+    int rc = launch_ivox_oldfirst(P, v.ev_b, n_old, v.ev_a, c->stream);
+    if (rc) return rc;
+    if (n_old > 0) HIP_TRY(hipMemcpyAsync(f.data(), v.ev_a, (size_t)n_old * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    int64_t end = n, k = 0, i = 0;
+    for (; k < (int64_t)t_ev.size() && (int64_t)t_ev[k] < end; k++) {
+        const uint32_t t = t_ev[k];
+        while (i < n_old && f[(size_t)i] < t) i++;  // touched before this eviction: not the oldest
+        if (i == n_old) {                            // no untouched old grid left
+            end = t;
+            break;
+        }
+        if (f[(size_t)i] != 0xFFFFFFFFu) end = std::min<int64_t>(end, f[(size_t)i]);
+        i++;
+    }
+    *pend = end;
+    *evs = k;
+    return LIVO_OK;
+}
+
 // IVox::AddPoints (ivox3d.h:256-281) of the points src[off, off + n) as one
 // device batch, with the LRU eviction at capacity.  *done = points consumed:
 // all of them, or (when an eviction would hit a grid the batch itself touches
@@ -768,9 +802,10 @@ static int ivox_add_part(livo_ctx* c, int64_t off, int64_t n, int64_t* done) {
         tb = c->prim_bytes;
         if (!rc) rc = prim_sort_pairs_u32(c->prim_tmp, &tb, v.ev_a, v.ev_b, v.ev_a, v.ev_c, N_new, 32, c->stream);
         if (rc) return rc;
-        uint32_t j_first = 0;
+        // creation index of each new grid from the (C - 1 - E)-th: the eviction times
         const int64_t c0 = std::max<int64_t>(0, C - 1 - E);
-        HIP_TRY(hipMemcpyAsync(&j_first, v.ev_b + c0, 4, hipMemcpyDeviceToHost, c->stream));
+        std::vector<uint32_t> t_ev((size_t)(N_new - c0));
+        HIP_TRY(hipMemcpyAsync(t_ev.data(), v.ev_b + c0, t_ev.size() * 4, hipMemcpyDeviceToHost, c->stream));
         // the old grids from the least recently used: victims and the conflict check
         HIP_TRY(hipMemsetAsync(cnt, 0, sizeof(unsigned long long), c->stream));
         rc = launch_ivox_oldkeys(P, v.ev_k, v.ev_a, cnt, c->stream);
@@ -790,6 +825,7 @@ static int ivox_add_part(livo_ctx* c, int64_t off, int64_t n, int64_t* done) {
             HIP_TRY(hipMemcpyAsync(&tail[1], v.ev_c + n_old - 1, 4, hipMemcpyDeviceToHost, c->stream));
         }
         HIP_TRY(hipStreamSynchronize(c->stream));
+        const uint32_t j_first = t_ev[0];
         const int64_t untouched = (int64_t)tail[0] + tail[1];
         bool conflict = ev > untouched;
         if (!conflict) {
@@ -801,10 +837,35 @@ static int ivox_add_part(livo_ctx* c, int64_t off, int64_t n, int64_t* done) {
             conflict = (ctr[0] & 2ull) != 0;
         }
         if (conflict) {
-            // undo, then the prefix [0, j_first] alone: one eviction, of the grid
-            // least recently used at its last point (new grids included)
+            // A run of evictions: the longest prefix whose victims are old grids
+            // it leaves untouched (ivox_evict_prefix), inserted again alone.
+            int64_t pend = 0, evs = 0;
+            rc = ivox_evict_prefix(c, P, n_old, t_ev, n, &pend, &evs);
+            if (rc) return rc;
             rc = launch_ivox_rollback(P, c->stream);
             if (rc) return rc;
+            if (evs > 0) {
+                P.n_src = pend;
+                HIP_TRY(hipMemsetAsync(v.ctr, 0, 5 * sizeof(unsigned long long), c->stream));
+                rc = launch_ivox_insert(P, c->stream);
+                if (!rc) rc = launch_ivox_untouched(P, v.ev_b, n_old, v.ev_c, c->stream);
+                if (!rc) rc = ivox_scan(c, v.ev_c, v.ev_d, n_old);
+                // (the victims kernel's conflict flag is conservative -- it also flags
+                // an older grid touched between two evictions -- the scan is exact: off)
+                if (!rc) rc = launch_ivox_victims(P, v.ev_b, v.ev_d, n_old, evs, 0xFFFFFFFFu, c->stream);
+                if (rc) return rc;
+                HIP_TRY(hipMemcpyAsync(ctr, v.ctr, sizeof(ctr), hipMemcpyDeviceToHost, c->stream));
+                HIP_TRY(hipStreamSynchronize(c->stream));
+                if ((ctr[0] & 2ull) || E + (int64_t)ctr[1] - (C - 1) != evs) return LIVO_E_HIP;  // (the scan's invariant)
+                consumed = pend;
+                ev = evs;
+                conflict = false;
+            }
+        }
+        if (conflict) {
+            // the first eviction's victim is a grid the batch touched before it:
+            // the prefix [0, j_first] alone, one eviction, of the grid least
+            // recently used at its last point (new grids included)
             consumed = (int64_t)j_first + 1;
             P.n_src = consumed;
             HIP_TRY(hipMemsetAsync(v.ctr, 0, 5 * sizeof(unsigned long long), c->stream));
@@ -872,6 +933,7 @@ static int ivox_add_part(livo_ctx* c, int64_t off, int64_t n, int64_t* done) {
         if (rc) return rc;
     }
     *done = consumed;
+    v.add_passes++;
     return LIVO_OK;
 }
 
@@ -1123,6 +1185,8 @@ static int dyn_runs_update(livo_ctx* c) {
 #endif
     return LIVO_OK;
 }
+
+static int dyn_rebuild(livo_ctx* c);
 
 // The built map becomes the incremental point set (ids = build indices).
 static int dyn_activate(livo_ctx* c) {
@@ -2769,6 +2833,7 @@ int livo_ivox_get_info(livo_ctx* c, livo_ivox_info* out) {
     out->num_grids = v.ngrids;
     out->ids_issued = v.next_id;
     out->max_grid_points = v.max_grid;
+    out->add_passes = v.add_passes;
     out->device_bytes = v.table * (int64_t)(sizeof(GridSlot) + 4 * sizeof(uint32_t)) +
                         (v.pts_cap[0] + v.pts_cap[1]) * 16 +
                         kMaxGroups * v.big_threads * v.big_slice * (int64_t)sizeof(SelElem);

@@ -401,6 +401,7 @@ int launch_ivox_newfirst(const IvoxParams& p, uint32_t* out, unsigned long long*
 int launch_ivox_oldkeys(const IvoxParams& p, unsigned long long* keys, uint32_t* slot, unsigned long long* n,
                         void* stream);
 int launch_ivox_untouched(const IvoxParams& p, const uint32_t* sorted_slot, int64_t n, uint32_t* flags, void* stream);
+int launch_ivox_oldfirst(const IvoxParams& p, const uint32_t* sorted_slot, int64_t n, uint32_t* out, void* stream);
 int launch_ivox_victims(const IvoxParams& p, const uint32_t* sorted_slot, const uint32_t* rank, int64_t n, int64_t ev,
                         uint32_t j_first, void* stream);
 int launch_ivox_tcur_min(const IvoxParams& p, void* stream);

@@ -131,7 +131,7 @@ class IvoxParams(C.Structure):
 
 class IvoxInfo(C.Structure):
     _fields_ = [("num_points", C.c_int64), ("num_grids", C.c_int64), ("ids_issued", C.c_int64),
-                ("max_grid_points", C.c_int64), ("device_bytes", C.c_int64)]
+                ("max_grid_points", C.c_int64), ("device_bytes", C.c_int64), ("add_passes", C.c_int64)]
 
 
 class Cam(C.Structure):

@@ -51,10 +51,11 @@
 extern "C" {
 #endif
 
-/* 4: livo_timings grew the per-evaluation fields (eval_ms ... gap_ms), LIVO_E_BUSY
+/* 5: livo_ivox_info grew add_passes (round 4).
+ * 4: livo_timings grew the per-evaluation fields (eval_ms ... gap_ms), LIVO_E_BUSY
  *    and the submit / wait pair were added (round 3); a binary built against 3
  *    passes a smaller livo_timings. */
-#define LIVO_ABI_VERSION 4
+#define LIVO_ABI_VERSION 5
 #define LIVO_DIM_STATE 18        /* DIM_STATE, include/common_lib.h:32 */
 #define LIVO_NUM_MATCH_POINTS 5  /* NUM_MATCH_POINTS, include/common_lib.h:37 */
 #define LIVO_MAX_EVALS 16        /* max h_share/solve evaluations per scan update */
@@ -300,6 +301,8 @@ typedef struct livo_ivox_info {
     int64_t ids_issued;      /* points ever added = the id of the next point        */
     int64_t max_grid_points; /* largest grid                                        */
     int64_t device_bytes;    /* HBM held by the iVox map                            */
+    int64_t add_passes;      /* device passes AddPoints took since init: one per    */
+                             /* call, more when an LRU victim is re-touched         */
 } livo_ivox_info;
 
 int livo_ctx_set_backend(livo_ctx* ctx, int backend);

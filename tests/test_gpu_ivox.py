@@ -162,6 +162,46 @@ def test_ivox_lru_eviction_matches_oracle(ivctx, cap):
     _knn_equal(ivctx, iv, q, max_range=5.0)
 
 
+def test_ivox_lru_eviction_runs(ivctx):
+    """A batch whose evictions run far past the capacity (a sweep of 2000 new
+    grids at capacity 64), touching old grids just before they would be the
+    LRU victim and re-touching grids evicted a few creations earlier: the
+    device takes the longest prefix whose victims the prefix leaves untouched
+    per pass (ivox3d.h:263-275), so the pass count stays near N / C, not one
+    per eviction; grids, ids and order equal the oracle's after the batch."""
+    import oracle
+    cap = 64
+    rng = np.random.default_rng(64)
+    ivctx.ivox_init(resolution=1.0, nearby_type=6, capacity=cap)
+    iv = oracle.Ivox(resolution=1.0, nearby_type=6, capacity=cap)
+    a = np.stack([np.arange(cap - 1) + 0.5, np.full(cap - 1, 0.5), np.full(cap - 1, 0.5)], 1).astype(np.float32)
+    ivctx.ivox_add_points(a)
+    iv.add_points(a)
+    pts = []
+    retouch = 0
+    for j in range(2000):
+        pts.append((j + 0.5, 50.5, 0.5))                 # a new grid (one more eviction)
+        if j % 4 == 1 and j < 120:                       # an old grid, newest first: touched before its turn
+            pts.append((cap - 2 - j // 4 + 0.25, 0.5, 0.5))
+        if j % 50 == 25:                                 # a sweep grid evicted or about to be
+            pts.append((j - rng.integers(50, 90) + 0.5, 50.25, 0.5))
+            retouch += 1
+    b = np.asarray(pts, np.float32)
+    before = ivctx.ivox_info()["add_passes"]
+    ivctx.ivox_add_points(b)
+    iv.add_points(b)
+    passes = ivctx.ivox_info()["add_passes"] - before
+    gx, gi, gk = ivctx.ivox_dump()
+    rx, ri, rg, rk = iv.dump()
+    assert np.array_equal(gi, ri)
+    assert np.array_equal(gx.view(np.uint32), rx.view(np.uint32))
+    assert np.array_equal(gk, rk[rg])
+    assert ivctx.ivox_info()["num_grids"] == iv.info()["num_grids"]
+    assert passes <= 2 * 2000 // cap + 2 * retouch + 4, passes
+    q = np.concatenate([rng.uniform(0, 2000, size=(500, 1)), np.full((500, 1), 50.5), np.full((500, 1), 0.5)], 1)
+    _knn_equal(ivctx, iv, q.astype(np.float32), max_range=5.0)
+
+
 def _hs_equal(g, r):
     assert np.array_equal(g["nn_idx"], r["cache"]["idx"])
     assert np.array_equal(g["nn_d"].view(np.uint32), r["cache"]["d"].view(np.uint32))
