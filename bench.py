@@ -778,20 +778,26 @@ def main():
         # Add_Points with the 0.5 m box downsampling, so the map is the room at
         # one point per box.  Mapping scans (pool scans after the first batch,
         # at their true poses) build it up before the timed odometry passes.
-        room = livo_amd.Context(device, t_LI=synth.T_LI, max_iterations=a.max_iter)
         map_seeds = pool_seeds[a.batch:a.batch + 32]
         map_scans = pool_scans[a.batch:a.batch + 32]
         R0, p0, _ = synth.true_pose(map_seeds[0])
         w0 = (map_scans[0].astype(np.float64) @ synth.R_LI.T + synth.T_LI) @ R0.T + p0
         _, first = np.unique(np.floor(w0 / 0.5).astype(np.int64), axis=0, return_index=True)
-        room.map_build(np.ascontiguousarray(w0[np.sort(first)], dtype=np.float32))
-        for sd, sc in zip(map_seeds[1:], map_scans[1:]):
-            sid = room.scan_upload(sc)
-            room.map_incremental(sid, synth.make_state(sd, rot_deg=0.0, trans_m=0.0), filter_size_map=0.5)
-            room.scan_release(sid)
-        room_points = room.map_info()["num_points"]
-        room_row = odometry(room)
-        room.close()
+        room_rows = {}
+        for runs in ("0", "1"):  # the cell walk (default) / the runs kept on the incremental map (LIVO_DYN_RUNS=1)
+            os.environ["LIVO_DYN_RUNS"] = runs  # (read when the map first changes)
+            room = livo_amd.Context(device, t_LI=synth.T_LI, max_iterations=a.max_iter)
+            room.map_build(np.ascontiguousarray(w0[np.sort(first)], dtype=np.float32))
+            for sd, sc in zip(map_seeds[1:], map_scans[1:]):
+                sid = room.scan_upload(sc)
+                room.map_incremental(sid, synth.make_state(sd, rot_deg=0.0, trans_m=0.0), filter_size_map=0.5)
+                room.scan_release(sid)
+            room_points = room.map_info()["num_points"]
+            room_rows[runs] = odometry(room)
+            room.close()
+        os.environ.pop("LIVO_DYN_RUNS", None)
+        room_row = room_rows["0"]
+        room_row["with_runs"] = {k: room_rows["1"][k] for k in ("scans_per_s", "iekf_ms_per_scan", "add_points_ms_per_scan")}
         if rank == 0:
             result["ikd_incremental"] = dict(ikd_row, note=(
                 f"sequential odometry on the {a.map_points}-pt map: livo_iekf_update + livo_map_incremental "
@@ -800,7 +806,8 @@ def main():
             result["ikd_incremental"]["mapped_room"] = dict(room_row, map_points_before=room_points, note=(
                 f"the same odometry on the map the reference's ikd-Tree holds: built from the first scan "
                 f"(0.5 m voxel-downsampled) and grown by {len(map_scans) - 1} mapping scans through "
-                "livo_map_incremental at their true poses (one point per 0.5 m box)"))
+                "livo_map_incremental at their true poses (one point per 0.5 m box); with_runs: the same with "
+                "LIVO_DYN_RUNS=1 (the runs kept on the incremental map)"))
 
     # ---- the VIO photometric update
     vio_frames = {}

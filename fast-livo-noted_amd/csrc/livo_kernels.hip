@@ -3023,6 +3023,7 @@ __device__ void ik_solve(IekfSlot* slot, const HsJob& job, IkSolveLds& S, const 
     }
     for (int t = lane; t < N * N; t += 64) S.P[t] = K.xp.cov[t];  // P_ = P_propagated
     WAVE_SYNC();
+    SOLVE_MARK(3);
     // SO3 (idx 3, 6) and S2 (idx 21) corrections of dx_new and P_ (:1659-1697)
     for (int b = 0; b < 3; b++) {
         const int idx = b == 0 ? 3 : (b == 1 ? 6 : 21), d = b == 2 ? 2 : 3;
@@ -3060,6 +3061,7 @@ __device__ void ik_solve(IekfSlot* slot, const HsJob& job, IkSolveLds& S, const 
         }
         WAVE_SYNC();
     }
+    SOLVE_MARK(4);
     auto hth = [&](int r, int c) {
         const int a = r < c ? r : c, bb = r < c ? c : r;
         return S.sum[a * 12 - (a * (a - 1)) / 2 + (bb - a)];
@@ -3130,6 +3132,7 @@ __device__ void ik_solve(IekfSlot* slot, const HsJob& job, IkSolveLds& S, const 
             for (int i = 0; i < N; i++) S.Pinv[i * N + lane] = y[i];
         }
         WAVE_SYNC();
+        SOLVE_MARK(5);
         for (int t = lane; t < 144; t += 64) {
             const int r = t / 12, c = t % 12;
             const int a = r < c ? r : c, bb = r < c ? c : r;
@@ -3146,6 +3149,7 @@ __device__ void ik_solve(IekfSlot* slot, const HsJob& job, IkSolveLds& S, const 
         }
         WAVE_SYNC();
     }
+    SOLVE_MARK(6);
     if (lane < N) {
         const int r = lane;
         double kh = S.Pinv[r * N] * S.sum[78];
@@ -3159,6 +3163,7 @@ __device__ void ik_solve(IekfSlot* slot, const HsJob& job, IkSolveLds& S, const 
     }
     WAVE_SYNC();
     }
+    SOLVE_MARK(7);
     if (lane < N) {  // dx_ = K_h + (K_x - I) dx_new
         const int r = lane;
         double acc = 0.0;
@@ -3204,6 +3209,7 @@ __device__ void ik_solve(IekfSlot* slot, const HsJob& job, IkSolveLds& S, const 
         S.stop = stop ? 1 : 0;
     }
     WAVE_SYNC();
+    SOLVE_MARK(8);
     if (!S.stop) return;
     // covariance (:1838-1921): L_ = P_ with the corrections at dx_, P_ = L_ - K_x(:,0:12) P_(0:12,:)
     for (int t = lane; t < N * N; t += 64) S.L[t] = S.P[t];
@@ -3258,6 +3264,7 @@ __device__ void ik_solve(IekfSlot* slot, const HsJob& job, IkSolveLds& S, const 
         for (int k = 1; k < 12; k++) acc = acc + S.Kx[r * 12 + k] * S.P[k * N + c];
         K.x.cov[t] = S.L[t] - acc;
     }
+    SOLVE_MARK(9);
 }
 
 // Compensated (Neumaier) sum, as oracle/livo_oracle.cpp's CompSum: s + c is
@@ -3285,15 +3292,23 @@ __global__ __launch_bounds__(kBlock) void k_hshare_ik(HsParams P) {
     const int search = FIRST ? 1 : slot->ctrl.search_en;
     const int tid = threadIdx.x;
     const livo_ikfom_state& X = slot->ik.x;
-    // this thread's output of the block sums (t < 92): (a, b) of the upper triangle, or HTh / res / count
-    int oa = 0, ob = 0;
-    if (tid < 78) {
-        int t = tid, a = 0;
-        while (t >= 12 - a) { t -= 12 - a; a++; }
-        oa = a;
-        ob = a + t;
-    }
-    double acc = 0.0, acc_c = 0.0;  // compensated
+    // Each wave sums the rows of its own 64 points: lane l forms output l and
+    // (l < 28) output l + 64 of the block's 92 sums -- (a, b) of the upper
+    // triangle, or HTh / res / count -- over them, the four waves' compensated
+    // sums are merged at the end (order-free to ~1e-27, comp_add).
+    const int lane = tid & 63, wv = tid >> 6;
+    const int o1 = lane, o2 = lane + 64;
+    auto tri = [](int o, int& a, int& b) {
+        int t = o, r = 0;
+        while (t >= 12 - r) { t -= 12 - r; r++; }
+        a = r;
+        b = r + t;
+    };
+    int a1 = 0, b1 = 0, a2 = 0, b2 = 0;
+    tri(o1, a1, b1);
+    if (o2 < 78) tri(o2, a2, b2);
+    double acc1 = 0.0, acc1_c = 0.0, acc2 = 0.0, acc2_c = 0.0;  // compensated
+    __shared__ double wpart[kBlock / 64][2][kIkUsed];
     __shared__ uint32_t wcnt[kBlock / 64];
     uint32_t bcnt = 0;  // effective rows of this block so far (point order)
     for (int rep = 0; rep < kPtsPerThread; rep++) {
@@ -3362,7 +3377,6 @@ __global__ __launch_bounds__(kBlock) void k_hshare_ik(HsParams P) {
         // the solve forms the reference's measurement-space gain from them
         const bool eff = row[14] != 0.0;
         const unsigned long long bal = __ballot(eff);
-        const int lane = tid & 63;
         if (lane == 0) wcnt[tid >> 6] = (uint32_t)__popcll(bal);
         __syncthreads();
         uint32_t pos = bcnt + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
@@ -3376,21 +3390,36 @@ __global__ __launch_bounds__(kBlock) void k_hshare_ik(HsParams P) {
             for (int k = 0; k < 13; k++) dst[k] = row[k];
         }
         bcnt += tot;
-        if (tid < kIkUsed) {  // rows in point order
-            for (int r = 0; r < kBlock; r++) {
-                const double* q = rows + r * kIkRow;
+        // (the rows were written before the __syncthreads above)
+        const double* wrows = rows + (wv * 64) * kIkRow;
+        for (int r = 0; r < 64; r++) {
+            const double* q = wrows + r * kIkRow;
+            comp_add(acc1, acc1_c, q[a1] * q[b1]);
+            if (o2 < kIkUsed) {
                 double v;
-                if (tid < 78) v = q[oa] * q[ob];
-                else if (tid < 90) v = q[tid - 78] * q[12];
-                else v = q[tid == 90 ? 13 : 14];
-                comp_add(acc, acc_c, v);
+                if (o2 < 78) v = q[a2] * q[b2];
+                else if (o2 < 90) v = q[o2 - 78] * q[12];
+                else v = q[o2 == 90 ? 13 : 14];
+                comp_add(acc2, acc2_c, v);
             }
         }
         __syncthreads();
     }
+    wpart[wv][0][o1] = acc1;
+    wpart[wv][1][o1] = acc1_c;
+    if (o2 < kIkUsed) {
+        wpart[wv][0][o2] = acc2;
+        wpart[wv][1][o2] = acc2_c;
+    }
+    __syncthreads();
     if (tid < kIkUsed) {
-        job.partial[(size_t)blockIdx.x * kIkCols + tid] = acc;
-        job.partial[(size_t)blockIdx.x * kIkCols + kIkCompOff + tid] = acc_c;
+        double sc = 0.0, cc = 0.0;
+        for (int w = 0; w < kBlock / 64; w++) {
+            comp_add(sc, cc, wpart[w][0][tid]);
+            cc += wpart[w][1][tid];
+        }
+        job.partial[(size_t)blockIdx.x * kIkCols + tid] = sc;
+        job.partial[(size_t)blockIdx.x * kIkCols + kIkCompOff + tid] = cc;
     }
     if (tid == 0) job.ikcnt[blockIdx.x] = bcnt < (uint32_t)kIkFewRows ? bcnt : (uint32_t)kIkFewRows + 1u;
 }
@@ -3411,6 +3440,7 @@ __global__ __launch_bounds__(64 * kIkSolveWaves) void k_solve_ik(HsParams P) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (P.replay_count && blockIdx.x == 0 && threadIdx.x == 0) *P.replay_count = 0u;
     if (slot->ctrl.stop) return;  // block-uniform
+    SOLVE_MARK(0);
     for (int c = lane; c < kIkUsed; c += 64) {
         double sc = 0.0, cc = 0.0;
         const double* src = job.partial + c;
@@ -3433,6 +3463,7 @@ __global__ __launch_bounds__(64 * kIkSolveWaves) void k_solve_ik(HsParams P) {
         wsum[wave][1][c] = cc;
     }
     __syncthreads();
+    SOLVE_MARK(1);
     if (wave > 0) return;
     for (int c = lane; c < kIkCols; c += 64) {
         double sc = 0.0, cc = 0.0;
@@ -3458,6 +3489,7 @@ __global__ __launch_bounds__(64 * kIkSolveWaves) void k_solve_ik(HsParams P) {
         }
     }
     WAVE_SYNC();
+    SOLVE_MARK(2);
     ik_solve(slot, job, S, lane, P.lpc);
 }
 
@@ -3604,6 +3636,14 @@ extern "C" int livo_debug_eval_stats(unsigned long long* out) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_eval_stats), sizeof(g_eval_stats)) != hipSuccess) return LIVO_E_HIP;
     static const unsigned long long zero[24] = {};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_eval_stats), zero, sizeof(zero)) == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+#endif
+
+#ifdef LIVO_SOLVE_PROF
+// k_solve_ik phase marks of the last launch, [block][mark] (the profiling build only)
+extern "C" int livo_debug_solve_prof(unsigned long long* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return LIVO_E_HIP;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_solve_prof), sizeof(g_solve_prof)) == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 #endif
 

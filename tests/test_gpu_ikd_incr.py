@@ -190,17 +190,16 @@ def test_iekf_search_records_on_updated_map(built, monkeypatch, mode):
     """The fused IEKF search on the incremental map: with the runs of the base
     point set (deleted base points marked, points added since in the delta
     grid), with a rebase of the runs at every change (LIVO_DYN_REBASE tiny),
-    and with the cell walk (LIVO_DYN_RUNS=0).  One evaluation (max_iteration
+    and with the cell walk (the default; the runs are LIVO_DYN_RUNS=1).  One evaluation (max_iteration
     0: one search at the initial state) after each change: every point's
     neighbour record (indices and squared distances, in order) equals the
     oracle's k-NN of the world points on the updated map, bit for bit."""
     import livo_amd
     import oracle
     from livo_amd import synth
+    monkeypatch.setenv("LIVO_DYN_RUNS", "0" if mode == "cell_walk" else "1")  # (the runs are opt-in)
     if mode == "rebase_every_change":
         monkeypatch.setenv("LIVO_DYN_REBASE", "1e-9")
-    if mode == "cell_walk":
-        monkeypatch.setenv("LIVO_DYN_RUNS", "0")
     m = synth.make_map(200_000)
     dm = oracle.DynMap(m)
     rng = np.random.default_rng(77)
@@ -234,6 +233,7 @@ def test_odometry_with_rebases(built, monkeypatch):
     import livo_amd
     import oracle
     from livo_amd import synth
+    monkeypatch.setenv("LIVO_DYN_RUNS", "1")
     monkeypatch.setenv("LIVO_DYN_REBASE", "1e-9")
     m = synth.make_map(100_000)
     dm = oracle.DynMap(m)
