@@ -38,6 +38,7 @@ struct ScanBuf {
     uint8_t* pstate = nullptr;  // N: plane state (0: not fitted since the neighbours changed)
     double* ikrows = nullptr;   // IKFoM few-point rows (nblk x kIkFewRows x 13)
     uint32_t* ikcnt = nullptr;  // per block
+    double* ikprep = nullptr;   // IKFoM per-evaluation prep (kIkPrep doubles)
     bool searched = false;      // a search has filled the neighbour cache
     int64_t cap = 0;            // points the buffers were sized for (>= n; reused after a release)
 };
@@ -61,7 +62,7 @@ static void dev_free(T*& p) {
 
 static void free_scan_buf(ScanBuf& s) {
     dev_free(s.pts); dev_free(s.nn); dev_free(s.partial); dev_free(s.d_perm); dev_free(s.d_iperm);
-    dev_free(s.plane); dev_free(s.pstate); dev_free(s.ikrows); dev_free(s.ikcnt);
+    dev_free(s.plane); dev_free(s.pstate); dev_free(s.ikrows); dev_free(s.ikcnt); dev_free(s.ikprep);
 }
 
 }  // namespace
@@ -170,6 +171,10 @@ struct livo_ctx {
     // extra streams for the groups of a batch (overlap of latency-bound kernels)
     hipStream_t xstream[kMaxGroups - 1] = {};
     hipEvent_t xjoin[kMaxGroups - 1] = {};
+    // IKFoM batches: per group a stream for k_ik_prep beside the search and
+    // plane pass, and its fork / done events
+    hipStream_t ikst[kMaxGroups] = {};
+    hipEvent_t ikev[kMaxGroups][2] = {};
     // stream groups per batch (LIVO_STREAM_GROUPS; 0: 1 for a fused evaluation
     // of <= 1.2M points, 2 otherwise).  MI355X, 8 x 100k scans: unfused 1 / 2 / 4 groups 8884 / 9503 /
     // 9145 updates/s; fused 12020 / 11883 / 11777 (profiles/r02_ab_groups.txt)
@@ -516,6 +521,7 @@ static void fill_job(HsJob& j, ScanBuf& s, IekfSlot* slot) {
     j.pstate = s.pstate;
     j.ikrows = s.ikrows;
     j.ikcnt = s.ikcnt;
+    j.ikprep = s.ikprep;
     j.slot = slot;
     j.n = (int32_t)s.n;
     j.nblk = s.nblk;
@@ -1525,6 +1531,14 @@ int livo_ctx_destroy(livo_ctx* c) {
         (void)hipEventDestroy(c->b_end[0]);
         (void)hipEventDestroy(c->b_end[1]);
     }
+    for (int k = 0; k < kMaxGroups; k++) {
+        if (c->ikst[k]) {
+            (void)hipStreamSynchronize(c->ikst[k]);
+            (void)hipStreamDestroy(c->ikst[k]);
+        }
+        for (hipEvent_t e : c->ikev[k])
+            if (e) (void)hipEventDestroy(e);
+    }
     for (int k = 0; k < kMaxGroups - 1; k++) {
         if (c->xstream[k]) (void)hipStreamSynchronize(c->xstream[k]);
         if (c->xjoin[k]) (void)hipEventDestroy(c->xjoin[k]);
@@ -2024,6 +2038,7 @@ static int alloc_scan_buf(livo_ctx* c, ScanBuf& s, int64_t N) {
         rc |= dev_alloc(&s.pstate, (size_t)cap);
         rc |= dev_alloc(&s.ikrows, (size_t)cblk * kIkFewRows * 13);
         rc |= dev_alloc(&s.ikcnt, (size_t)cblk);
+        if (!s.ikprep) rc |= dev_alloc(&s.ikprep, (size_t)kIkPrep);
         if (rc) {
             free_scan_buf(s);
             return LIVO_E_OOM;
@@ -2350,6 +2365,12 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
     if (set_device(c)) return LIVO_E_HIP;
     int rc = lane_streams(c, L);
     if (rc) return rc;
+    if (!lm && !c->ikst[0])
+        for (int k = 0; k < kMaxGroups; k++) {
+            if (hipStreamCreateWithFlags(&c->ikst[k], hipStreamNonBlocking) != hipSuccess) return LIVO_E_HIP;
+            for (hipEvent_t& e : c->ikev[k])
+                if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return LIVO_E_HIP;
+        }
     rc = lm ? ensure_lm(B, n) : ensure_slots(c, n);
     if (rc) return rc;
     // Slots and jobs: the IKFoM model uses whole slots (c->h_slots / d_slots);
@@ -2466,7 +2487,7 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
         kp[gi].replay_list = c->d_replay_list + g[gi].off;
         // the iVox overflow pass of each group has its own scratch slices (groups run concurrently)
         if (kp[gi].iv.scratch) kp[gi].iv.scratch += (int64_t)gi * c->iv.big_threads * c->iv.big_slice;
-        hp[gi].solve = 1;  // the last plane-pass block of each scan runs its solve
+        hp[gi].solve = lm ? 1 : 0;  // the last plane-pass block of each scan runs its solve (IKFoM: k_solve_ik below)
         hp[gi].replay_count = c->d_replay_count + gi;
     }
     for (int e = 0; e < evals; e++) {
@@ -2483,12 +2504,26 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
             if (full && (e > 0 || gi > 0)) HIP_TRY(hipEventRecord(c->ev[gi][3 * e], st));
             // leaf-map search; rematch passes are bounded by the previous neighbours
             // (the group's replay count was zeroed before the batch / by the last k_solve)
+            if (!lm) {
+                // IKFoM: the measurement-free part of the solve (k_ik_prep) on the group's
+                // side stream once the last solve is done, beside this search and plane pass
+                HIP_TRY(hipEventRecord(c->ikev[gi][0], st));
+                HIP_TRY(hipStreamWaitEvent(c->ikst[gi], c->ikev[gi][0], 0));
+                rc = launch_ik_prep(hp[gi], g[gi].count, c->ikst[gi]);
+                if (rc) return rc;
+                HIP_TRY(hipEventRecord(c->ikev[gi][1], c->ikst[gi]));
+            }
             rc = backend_knn(c, kp[gi], g[gi].count, g[gi].max_n, e > 0, st);
             if (rc) return rc;
             if ((prof && e == 0) || full) HIP_TRY(hipEventRecord(c->ev[gi][3 * e + 1], st));
             rc = model == kModelIkfom ? launch_hshare_ik(hp[gi], g[gi].count, g[gi].max_nblk, e == 0, st)
                                       : launch_hshare(hp[gi], g[gi].count, g[gi].max_nblk, e == 0, st);
             if (rc) return rc;
+            if (!lm) {
+                HIP_TRY(hipStreamWaitEvent(st, c->ikev[gi][1], 0));
+                rc = launch_solve_ik(hp[gi], g[gi].count, st);
+                if (rc) return rc;
+            }
         }
     }
     for (int gi = 0; gi < ngroups; gi++)

@@ -3009,12 +3009,13 @@ struct IkSolveLds {
 };
 constexpr int kIkRow = 15;  // 12 row + h + |pd2| + keep
 
-// One wave: esekfom.hpp:1638-1921 from the reduced sums in S.sum.
-__device__ void ik_solve(IekfSlot* slot, const HsJob& job, IkSolveLds& S, const int lane, const double R) {
-    IkBlock& K = slot->ik;
-    const IekfCtrl ctrl0 = slot->ctrl;
-    const int e = ctrl0.n_evals;
-    const int it = ctrl0.iter_count;  // i of the reference loop (starts at -1)
+// One wave, the part of esekfom.hpp:1638-1787 that does not depend on this
+// evaluation's measurements: dx = x_ boxminus x_propagated, P_ = P_propagated
+// with the SO3 / S2 corrections of dx_new and P_ (:1638-1697), and (P_ / R)^-1
+// of the information-form gain (:1775-1777).  k_ik_prep runs it on its own
+// stream beside the evaluation's search and plane pass; k_solve_ik loads it.
+__device__ void ik_prep(const IekfSlot* slot, IkSolveLds& S, const int lane, const double R) {
+    const IkBlock& K = slot->ik;
     constexpr int N = kIkDim;
     if (lane == 0) {
         double dx[N];
@@ -3062,6 +3063,29 @@ __device__ void ik_solve(IekfSlot* slot, const HsJob& job, IkSolveLds& S, const 
         WAVE_SYNC();
     }
     SOLVE_MARK(4);
+    {
+        double A[N];
+        for (int j = 0; j < N; j++) A[j] = lane < N ? S.P[lane * N + j] / R : 0.0;
+        wave_lu_to_lds<N>(A, lane, S.LU, S.piv);
+        WAVE_SYNC();
+        if (lane < N) {
+            double y[N];
+            lds_lu_column<N>(S.LU, S.piv, lane, y);
+            for (int i = 0; i < N; i++) S.Pinv[i * N + lane] = y[i];
+        }
+        WAVE_SYNC();
+    }
+    SOLVE_MARK(5);
+}
+
+// One wave: esekfom.hpp:1701-1921 from the reduced sums in S.sum and the
+// evaluation's prep (ik_prep: S.dx, S.dxn, S.P, S.Pinv = (P_ / R)^-1).
+__device__ void ik_solve(IekfSlot* slot, const HsJob& job, IkSolveLds& S, const int lane, const double R) {
+    IkBlock& K = slot->ik;
+    const IekfCtrl ctrl0 = slot->ctrl;
+    const int e = ctrl0.n_evals;
+    const int it = ctrl0.iter_count;  // i of the reference loop (starts at -1)
+    constexpr int N = kIkDim;
     auto hth = [&](int r, int c) {
         const int a = r < c ? r : c, bb = r < c ? c : r;
         return S.sum[a * 12 - (a * (a - 1)) / 2 + (bb - a)];
@@ -3123,16 +3147,6 @@ __device__ void ik_solve(IekfSlot* slot, const HsJob& job, IkSolveLds& S, const 
     // gain, information form (:1775-1787): P_temp = (P_/R)^-1 + HTH, P_inv = P_temp^-1
     {
         double A[N];
-        for (int j = 0; j < N; j++) A[j] = lane < N ? S.P[lane * N + j] / R : 0.0;
-        wave_lu_to_lds<N>(A, lane, S.LU, S.piv);
-        WAVE_SYNC();
-        if (lane < N) {
-            double y[N];
-            lds_lu_column<N>(S.LU, S.piv, lane, y);
-            for (int i = 0; i < N; i++) S.Pinv[i * N + lane] = y[i];
-        }
-        WAVE_SYNC();
-        SOLVE_MARK(5);
         for (int t = lane; t < 144; t += 64) {
             const int r = t / 12, c = t % 12;
             const int a = r < c ? r : c, bb = r < c ? c : r;
@@ -3490,7 +3504,40 @@ __global__ __launch_bounds__(64 * kIkSolveWaves) void k_solve_ik(HsParams P) {
     }
     WAVE_SYNC();
     SOLVE_MARK(2);
+    {  // the evaluation's prep (k_ik_prep, stream-ordered before this launch)
+        const double* src = job.ikprep;
+        for (int t = lane; t < kIkDim * kIkDim; t += 64) {
+            S.P[t] = src[t];
+            S.Pinv[t] = src[kIkDim * kIkDim + t];
+        }
+        if (lane < kIkDim) {
+            S.dx[lane] = src[2 * kIkDim * kIkDim + lane];
+            S.dxn[lane] = src[2 * kIkDim * kIkDim + kIkDim + lane];
+        }
+    }
+    WAVE_SYNC();
     ik_solve(slot, job, S, lane, P.lpc);
+}
+
+// One wave per scan: ik_prep of the scan's current estimate into job.ikprep.
+// Launched on its own stream once the previous evaluation's solve is done, it
+// runs beside this evaluation's search and plane pass (k_solve_ik waits on it).
+__global__ __launch_bounds__(64) void k_ik_prep(HsParams P) {
+    __shared__ IkSolveLds S;
+    const HsJob job = P.jobs[blockIdx.x];
+    const IekfSlot* slot = job.slot;
+    const int lane = threadIdx.x;
+    if (slot->ctrl.stop) return;  // block-uniform
+    ik_prep(slot, S, lane, P.lpc);
+    double* dst = job.ikprep;
+    for (int t = lane; t < kIkDim * kIkDim; t += 64) {
+        dst[t] = S.P[t];
+        dst[kIkDim * kIkDim + t] = S.Pinv[t];
+    }
+    if (lane < kIkDim) {
+        dst[2 * kIkDim * kIkDim + lane] = S.dx[lane];
+        dst[2 * kIkDim * kIkDim + kIkDim + lane] = S.dxn[lane];
+    }
 }
 
 __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
@@ -3700,6 +3747,18 @@ int launch_hshare_ik(const HsParams& p, int n_jobs, int max_nblk, bool first, vo
         hipLaunchKernelGGL(k_hshare_ik<false>, grid, block, 0, (hipStream_t)stream, p);
     if (hipGetLastError() != hipSuccess) return LIVO_E_HIP;
     if (!p.solve) return LIVO_OK;
+    const int rc = launch_ik_prep(p, n_jobs, stream);
+    return rc ? rc : launch_solve_ik(p, n_jobs, stream);
+}
+
+int launch_ik_prep(const HsParams& p, int n_jobs, void* stream) {
+    if (n_jobs <= 0) return LIVO_OK;
+    hipLaunchKernelGGL(k_ik_prep, dim3(n_jobs), dim3(64), 0, (hipStream_t)stream, p);
+    return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+
+int launch_solve_ik(const HsParams& p, int n_jobs, void* stream) {
+    if (n_jobs <= 0) return LIVO_OK;
     hipLaunchKernelGGL(k_solve_ik, dim3(n_jobs), dim3(64 * kIkSolveWaves), 0, (hipStream_t)stream, p);
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
