@@ -253,6 +253,7 @@ struct livo_ctx {
     bool lane_serial = false;
     bool lane_zc = true;            // submitted batches: staging copies by kernel over host-mapped memory (LIVO_LANE_ZC)
     bool sync_zc = false;           // synchronous batches too (LIVO_SYNC_ZC)
+    bool slot_wb = true;            // fused batches: the stopping solve writes the slot back (LIVO_SLOT_WB)
     int last_lane = -1;             // lane of the batch enqueued last
     unsigned long long last_replays = 0;  // profiled batches: the replay counter read back
     IekfSlot* h_slots = nullptr;  // pinned
@@ -522,6 +523,7 @@ static void fill_job(HsJob& j, ScanBuf& s, IekfSlot* slot) {
     j.ikrows = s.ikrows;
     j.ikcnt = s.ikcnt;
     j.ikprep = s.ikprep;
+    j.host_slot = nullptr;
     j.slot = slot;
     j.n = (int32_t)s.n;
     j.nblk = s.nblk;
@@ -1461,6 +1463,7 @@ int livo_ctx_create(int device, const livo_params* p, livo_ctx** out) {
     if (const char* env = std::getenv("LIVO_LANE_SERIAL")) c->lane_serial = std::atoi(env) != 0;
     if (const char* env = std::getenv("LIVO_LANE_ZC")) c->lane_zc = std::atoi(env) != 0;
     if (const char* env = std::getenv("LIVO_SYNC_ZC")) c->sync_zc = std::atoi(env) != 0;
+    if (const char* env = std::getenv("LIVO_SLOT_WB")) c->slot_wb = std::atoi(env) != 0;
     if (const char* env = std::getenv("LIVO_XCD_CHUNK")) c->xcd_chunk = std::max(0, std::atoi(env));  // tuning knob
     if (const char* env = std::getenv("LIVO_GRID_PPC")) {  // tuning knob
         const float v = (float)std::atof(env);
@@ -2386,6 +2389,9 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
     auto hslot = [&](int32_t b) -> IekfSlot& { return *reinterpret_cast<IekfSlot*>(hbase + (size_t)b * stride); };
     auto dslot = [&](int32_t b) { return reinterpret_cast<IekfSlot*>(dbase + (size_t)b * stride); };
     const int max_iter = c->params.max_iterations;
+    // fused batches: the solve that stops a scan writes its slot into the
+    // host-mapped staging copy itself (LIVO_SLOT_WB=0: copies after the batch)
+    const bool wb = fused && lm && B.h_lm_dev && c->slot_wb;
     int64_t total_n = 0;
     for (int32_t b = 0; b < n; b++) {
         ScanBuf* s = get_scan(c, ids[b]);
@@ -2395,6 +2401,7 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
             init_slot(hslot(b), states[b], priors ? priors[b] : states[b], max_iter, kSlotLmBytes);
         }
         fill_job(hjobs[b], *s, dslot(b));
+        if (wb) hjobs[b].host_slot = reinterpret_cast<uint4*>(B.h_lm_dev + (size_t)b * stride);
         total_n += s->n;
     }
     rc = ensure_replay(c, total_n);
@@ -2531,7 +2538,9 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
     // each group copies its own slots back on its own stream (no cross-stream
     // join before the copy); the host then waits for every group's stream
     for (int gi = 0; gi < ngroups; gi++) {
-        if (kcopy) {
+        if (wb) {
+            // (written by the stopping solves)
+        } else if (kcopy) {
             rc = launch_copy_words(dslot(g[gi].first), B.h_lm_dev + (size_t)g[gi].first * stride, stride * g[gi].count,
                                    g[gi].st);
             if (rc) return rc;

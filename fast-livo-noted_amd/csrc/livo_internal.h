@@ -272,6 +272,8 @@ struct HsJob {
     double* ikrows;       // IKFoM: nblk x kIkFewRows x 13 effective rows (h_x row, h) per block
     uint32_t* ikcnt;      // IKFoM: nblk: effective rows of the block (capped at kIkFewRows + 1)
     double* ikprep;       // IKFoM: kIkPrep doubles: the evaluation's corrected P_, (P_ / R)^-1, dx, dx_new (k_ik_prep)
+    uint4* host_slot;     // fused batches: the slot's host-mapped staging copy, written by the solve that
+                          // stops the scan (nullptr: the batch copies the slots back itself)
     int32_t n;
     int32_t nblk;
 };

@@ -2674,6 +2674,16 @@ __device__ __forceinline__ void hshare_reduce_solve(const HsParams& P, const HsJ
     if (!P.solve) return;  // livo_h_share: the sums only
     WAVE_SYNC();
     solve_scan(slot, L, tid);
+    if (job.host_slot) {
+        // the solve that stops the scan writes its slot straight into the host's
+        // staging copy (no copy back after the batch's last evaluation)
+        __threadfence();
+        WAVE_SYNC();
+        if (slot->ctrl.stop) {
+            const uint4* src = reinterpret_cast<const uint4*>(slot);
+            for (int w = tid; w < (int)((kSlotLmBytes + 15) / 16); w += 64) job.host_slot[w] = src[w];
+        }
+    }
 }
 
 template <bool FIRST>
