@@ -191,6 +191,7 @@ def test_ivox_lru_eviction_runs(ivctx):
     ivctx.ivox_add_points(b)
     iv.add_points(b)
     passes = ivctx.ivox_info()["add_passes"] - before
+    print(f"add_passes {passes}")
     gx, gi, gk = ivctx.ivox_dump()
     rx, ri, rg, rk = iv.dump()
     assert np.array_equal(gi, ri)
