@@ -25,6 +25,7 @@ MAX_EVALS, TL_BLOCKS = 16, 4096  # LIVO_MAX_EVALS, kTlBlocks
 
 def main():
     config5 = "--config5" in sys.argv
+    seed0 = int(sys.argv[sys.argv.index("--seed0") + 1]) if "--seed0" in sys.argv else 0  # first scan seed (config 2)
     m = synth.cached_map(10_000_000 if config5 else 1_000_000)
     with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=4) as ctx:
         ctx.map_build(m)
@@ -35,8 +36,8 @@ def main():
                 sids.append(ctx.scan_preprocess(raw, poses, Re, pe, leaf_size=synth.CONFIG5_LEAF)[0])
             st0 = [synth.make_state(1000 + s) for s in range(8)]
         else:
-            sids = [ctx.scan_upload(synth.make_scan(100_000, s)[0]) for s in range(8)]
-            st0 = [synth.make_state(s) for s in range(8)]
+            sids = [ctx.scan_upload(synth.make_scan(100_000, seed0 + s)[0]) for s in range(8)]
+            st0 = [synth.make_state(seed0 + s) for s in range(8)]
         L = ctx._L
         L.livo_debug_eval_timeline.argtypes = [C.c_void_p, C.c_int64]
         buf = np.zeros((MAX_EVALS, TL_BLOCKS, 2), np.uint64)
@@ -63,6 +64,10 @@ def main():
               f"{np.median(dur) / 1e3:.1f} mean {dur.mean() / 1e3:.1f} p90 {np.percentile(dur, 90) / 1e3:.1f} "
               f"max {dur.max() / 1e3:.1f} kcyc  in flight {dur.sum() / span:.0f}  tail after 90% of blocks "
               f"{(span - p90_end) / span:.2f} of the span  last start {(st.max() - t0) / span:.2f}")
+        if "--top" in sys.argv:  # the longest blocks: launch index, start and duration
+            idx = np.nonzero(ok)[0]
+            for k in np.argsort(-dur)[:8]:
+                print(f"    block {idx[k]}: start {(st[k] - t0) / 1e3:.1f} dur {dur[k] / 1e3:.1f} kcyc")
 
 
 if __name__ == "__main__":
