@@ -206,7 +206,13 @@ struct livo_ctx {
     int32_t vlog2 = 0;
     // ball runs (static map only): anchor cells of edge bh, runs of radius brmax
     bool bruns = true;                 // LIVO_BRUNS=0: the cell runs only
-    float br_ha = 2.0f, br_r = 3.2f;   // bh = br_ha r5, brmax = sqrt(3)/2 bh + br_r r5 (LIVO_BR_HA / LIVO_BR_R)
+    // bh = br_ha r5, brmax = sqrt(3)/2 bh + br_r r5 (LIVO_BR_HA / LIVO_BR_R).  R = 6
+    // (round 4; 3.2 before): on distinct scans the queries a ball of 3.2 r5 left
+    // uncertified (off the surfaces by the prior's pose error) certify in their
+    // ball run instead of the cell run and walk: pooled 21.4k vs 18.5k updates/s,
+    // first evaluation 0.157 vs 0.231 ms; R = 8 / 10 / 13 no better
+    // (profiles/r04_ab_ball_radius.txt)
+    float br_ha = 2.0f, br_r = 6.0f;
     GridSlot* bslots = nullptr;
     RunWord* bpts = nullptr;
     int32_t blog2 = 0;

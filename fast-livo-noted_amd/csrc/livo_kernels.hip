@@ -3458,33 +3458,37 @@ __global__ __launch_bounds__(kBlock) void k_hshare_ik(HsParams P) {
 constexpr int kIkSolveWaves = 8;
 __global__ __launch_bounds__(64 * kIkSolveWaves) void k_solve_ik(HsParams P) {
     __shared__ IkSolveLds S;
-    __shared__ double wsum[kIkSolveWaves][2][kIkUsed];
+    constexpr int kG = (64 * kIkSolveWaves) / kIkUsed;  // threads per column (5)
+    __shared__ double wsum[kG][2][kIkUsed];
     const HsJob job = P.jobs[blockIdx.x];
     IekfSlot* slot = job.slot;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (P.replay_count && blockIdx.x == 0 && threadIdx.x == 0) *P.replay_count = 0u;
     if (slot->ctrl.stop) return;  // block-uniform
     SOLVE_MARK(0);
-    for (int c = lane; c < kIkUsed; c += 64) {
+    // thread t < kG * 92: column t % 92 over blocks g, g + kG, ... (g = t / 92),
+    // 10 blocks' loads in flight, so a 98-block scan is two rounds of loads
+    if ((int)threadIdx.x < kG * kIkUsed) {
+        const int c = threadIdx.x % kIkUsed, g = threadIdx.x / kIkUsed;
         double sc = 0.0, cc = 0.0;
         const double* src = job.partial + c;
-        for (int b = wave; b < job.nblk; b += 8 * kIkSolveWaves) {
-            double v[8], w[8];
+        for (int b = g; b < job.nblk; b += 10 * kG) {
+            double v[10], w[10];
 #pragma unroll
-            for (int k = 0; k < 8; k++) {
-                const int bb = b + k * kIkSolveWaves;
+            for (int k = 0; k < 10; k++) {
+                const int bb = b + k * kG;
                 const bool in = bb < job.nblk;
                 v[k] = in ? src[(size_t)bb * kIkCols] : 0.0;
                 w[k] = in ? src[(size_t)bb * kIkCols + kIkCompOff] : 0.0;
             }
 #pragma unroll
-            for (int k = 0; k < 8; k++) {
+            for (int k = 0; k < 10; k++) {
                 comp_add(sc, cc, v[k]);
                 cc += w[k];
             }
         }
-        wsum[wave][0][c] = sc;
-        wsum[wave][1][c] = cc;
+        wsum[g][0][c] = sc;
+        wsum[g][1][c] = cc;
     }
     __syncthreads();
     SOLVE_MARK(1);
@@ -3492,9 +3496,9 @@ __global__ __launch_bounds__(64 * kIkSolveWaves) void k_solve_ik(HsParams P) {
     for (int c = lane; c < kIkCols; c += 64) {
         double sc = 0.0, cc = 0.0;
         if (c < kIkUsed)
-            for (int w = 0; w < kIkSolveWaves; w++) {
-                comp_add(sc, cc, wsum[w][0][c]);
-                cc += wsum[w][1][c];
+            for (int g = 0; g < kG; g++) {
+                comp_add(sc, cc, wsum[g][0][c]);
+                cc += wsum[g][1][c];
             }
         S.sum[c] = sc + cc;
     }
