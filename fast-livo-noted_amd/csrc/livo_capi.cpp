@@ -2457,14 +2457,13 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
         hipStream_t st;
     };
     Group g[kMaxGroups];
-    // default: two groups (8 x 100k: 1 / 2 / 3 / 4 groups 15463 / 16566 /
-    // 15602 / 16365 updates/s, profiles/r03_ab_groups.txt), four beyond 1.2M
-    // points (8 x 200k on the 10M map: 4437 vs 3960 with two): one group's
+    // default: four groups, one per hardware queue (round 4, 8 x 100k distinct
+    // scans, pipelined: 1 / 2 / 3 / 4 groups 18675 / 21170 / 22350 / 22984
+    // updates/s; 6 / 8 share the box's 4 queues and lose, profiles/r04_ab_groups.txt;
+    // 8 x 200k on the 10M map: 4437 vs 3960 with two): one group's
     // latency-bound evaluations (no search: launch, reduction, solve) and its
     // replay tail overlap the other groups' searches
-    int64_t batch_pts = 0;
-    for (int32_t b = 0; b < n; b++) batch_pts += get_scan(c, ids[b])->n;
-    const int auto_groups = batch_pts > 1200000 ? 4 : 2;
+    const int auto_groups = 4;
     const int ngroups = std::max(1, std::min<int>(c->groups > 0 ? c->groups : auto_groups, n));
     int64_t off = 0;
     for (int gi = 0; gi < ngroups; gi++) {

@@ -42,7 +42,10 @@ constexpr int kKnnBlock = LIVO_KNN_BLOCK;   // threads per block of the k-NN pas
 constexpr int kPtsPerThread = LIVO_PTS_PER_THREAD;  // points per thread of the plane-fit pass
 constexpr int kRedCols = 32;                // doubles per block partial (29 used)
 constexpr int kRedUsed = 29;                // 21 HTH upper-tri + 6 HTL + residual sum + count
-constexpr int kMaxGroups = 4;               // stream groups of a batched IEKF update
+#ifndef LIVO_MAX_GROUPS
+#define LIVO_MAX_GROUPS 4
+#endif
+constexpr int kMaxGroups = LIVO_MAX_GROUPS;               // stream groups of a batched IEKF update
 
 // ---------------------------------------------------------------------------
 // Device map: the ikd-Tree built exactly as KD_TREE::Build (median of the
