@@ -116,10 +116,10 @@ def launch_ranks(a) -> int:
 
 def stream_groups(batch_points: int = 800_000) -> int:
     """Stream groups of a batched update (LIVO_STREAM_GROUPS; livo_capi.cpp's default:
-    2, or 4 beyond 1.2M points)."""
+    4 since round 4)."""
     if os.environ.get("LIVO_STREAM_GROUPS"):
         return int(os.environ["LIVO_STREAM_GROUPS"])
-    return 4 if batch_points > 1_200_000 else 2
+    return 4
 
 
 def host_threads() -> int:
