@@ -2462,8 +2462,9 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
     // updates/s; 6 / 8 share the box's 4 queues and lose, profiles/r04_ab_groups.txt;
     // 8 x 200k on the 10M map: 4437 vs 3960 with two): one group's
     // latency-bound evaluations (no search: launch, reduction, solve) and its
-    // replay tail overlap the other groups' searches
-    const int auto_groups = 4;
+    // replay tail overlap the other groups' searches.  The unfused paths (IKFoM,
+    // iVox) keep two: IKFoM 4,114 with four vs 5,177 updates/s with two
+    const int auto_groups = fused ? 4 : 2;
     const int ngroups = std::max(1, std::min<int>(c->groups > 0 ? c->groups : auto_groups, n));
     int64_t off = 0;
     for (int gi = 0; gi < ngroups; gi++) {
