@@ -418,6 +418,31 @@ def test_batch_stream_groups(built, map100k, groups, monkeypatch):
 
 
 @pytest.mark.gpu
+def test_slot_writeback_equals_copy(built, map100k, monkeypatch):
+    """The stopping solve's slot write into the host staging copy (default) and the
+    copy after the batch (LIVO_SLOT_WB=0) return the same states and stats, synchronous
+    and submitted, an empty scan included."""
+    import livo_amd
+    synth = _synth()
+    out = {}
+    for wb in ("1", "0"):
+        monkeypatch.setenv("LIVO_SLOT_WB", wb)
+        with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=4) as ctx:
+            ctx.map_build(map100k)
+            scans = [synth.make_scan(2000 + 500 * s, s)[0] for s in range(6)] + [np.zeros((0, 3), np.float32)]
+            sids = [ctx.scan_upload(sc) for sc in scans]
+            states = [synth.make_state(s) for s in range(7)]
+            b, st = ctx.iekf_update_batch(sids, states)
+            t = ctx.iekf_update_batch_submit(sids[:3], states[:3])
+            b2, st2 = ctx.iekf_update_batch_wait(t, 3)
+            out[wb] = (b, st, b2, st2)
+    for x, y in zip(out["1"], out["0"]):
+        for u, v in zip(x, y):
+            for k in u:
+                assert np.asarray(u[k]).tobytes() == np.asarray(v[k]).tobytes(), k  # (bitwise: NaN stats of the empty scan)
+
+
+@pytest.mark.gpu
 def test_profiling_levels(ctx100k):
     """Profiling level 1 times only the batch's first search, level 2 every stage; neither
     changes the results."""
