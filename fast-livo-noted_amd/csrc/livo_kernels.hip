@@ -3344,23 +3344,40 @@ __global__ __launch_bounds__(kBlock) void k_hshare_ik(HsParams P) {
             float wx, wy, wz;
             ik_world_point(X, pb.x, pb.y, pb.z, wx, wy, wz);
             const float4* rec = reinterpret_cast<const float4*>(job.nn + i);
-            float nx[kNN], ny[kNN], nz[kNN];
-            float d4 = 0.0f;
-#pragma unroll
-            for (int k = 0; k < kNN; k++) {
-                const float4 v = rec[k];
-                nx[k] = v.x; ny[k] = v.y; nz[k] = v.z;
-                if (k == kNN - 1) d4 = v.w;
-            }
             int* flagp = reinterpret_cast<int*>(job.nn + i) + 26;  // NNRec::flag
             const int cnt = reinterpret_cast<const int4*>(job.nn + i)[6].y;
             const int flag = *flagp;
-            const bool sel = search ? ((cnt == kNN) && !(d4 > P.max_sqd)) : !(flag & kIkDrop);
+            // Without a search a point is processed only if the last evaluation
+            // kept it, and that evaluation fitted its plane from the same five
+            // neighbours: the plane cache (pstate 2) holds that fit, so the
+            // neighbours are not read and esti_plane not rerun.  A search (or a
+            // point not fitted since one, pstate 0) fits and caches it.
+#ifndef LIVO_IK_PLANE_CACHE
+#define LIVO_IK_PLANE_CACHE 1
+#endif
+            const uint8_t ps = (search || !LIVO_IK_PLANE_CACHE) ? (uint8_t)0 : job.pstate[i];
+            const bool sel = search ? ((cnt == kNN) && !(rec[kNN - 1].w > P.max_sqd)) : !(flag & kIkDrop);
             bool fin = false;
             float pa[4] = {0.0f, 0.0f, 0.0f, 0.0f};
             float pd2 = 0.0f;
+            bool planed = false;
             if (sel && cnt >= kNN) {
-                if (esti_plane(nx, ny, nz, P.plane_thr, pa)) {
+                if (ps == 2) {
+                    const float4 c4 = reinterpret_cast<const float4*>(job.plane)[i];
+                    pa[0] = c4.x; pa[1] = c4.y; pa[2] = c4.z; pa[3] = c4.w;
+                    planed = true;
+                } else if (ps == 0) {
+                    float nx[kNN], ny[kNN], nz[kNN];
+#pragma unroll
+                    for (int k = 0; k < kNN; k++) {
+                        const float4 v = rec[k];
+                        nx[k] = v.x; ny[k] = v.y; nz[k] = v.z;
+                    }
+                    planed = esti_plane(nx, ny, nz, P.plane_thr, pa);
+                    if (planed) reinterpret_cast<float4*>(job.plane)[i] = make_float4(pa[0], pa[1], pa[2], pa[3]);
+                    job.pstate[i] = planed ? 2 : 1;
+                }
+                if (planed) {
                     pd2 = ((pa[0] * wx + pa[1] * wy) + pa[2] * wz) + pa[3];
                     const double bx = pb.x, by = pb.y, bz = pb.z;
                     const double bn = sqrt((bx * bx + by * by) + bz * bz);
