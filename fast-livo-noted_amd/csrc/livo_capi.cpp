@@ -171,10 +171,6 @@ struct livo_ctx {
     // extra streams for the groups of a batch (overlap of latency-bound kernels)
     hipStream_t xstream[kMaxGroups - 1] = {};
     hipEvent_t xjoin[kMaxGroups - 1] = {};
-    // IKFoM batches: per group a stream for k_ik_prep beside the search and
-    // plane pass, and its fork / done events
-    hipStream_t ikst[kMaxGroups] = {};
-    hipEvent_t ikev[kMaxGroups][2] = {};
     // stream groups per batch (LIVO_STREAM_GROUPS; 0: 1 for a fused evaluation
     // of <= 1.2M points, 2 otherwise).  MI355X, 8 x 100k scans: unfused 1 / 2 / 4 groups 8884 / 9503 /
     // 9145 updates/s; fused 12020 / 11883 / 11777 (profiles/r02_ab_groups.txt)
@@ -1540,14 +1536,6 @@ int livo_ctx_destroy(livo_ctx* c) {
         (void)hipEventDestroy(c->b_end[0]);
         (void)hipEventDestroy(c->b_end[1]);
     }
-    for (int k = 0; k < kMaxGroups; k++) {
-        if (c->ikst[k]) {
-            (void)hipStreamSynchronize(c->ikst[k]);
-            (void)hipStreamDestroy(c->ikst[k]);
-        }
-        for (hipEvent_t e : c->ikev[k])
-            if (e) (void)hipEventDestroy(e);
-    }
     for (int k = 0; k < kMaxGroups - 1; k++) {
         if (c->xstream[k]) (void)hipStreamSynchronize(c->xstream[k]);
         if (c->xjoin[k]) (void)hipEventDestroy(c->xjoin[k]);
@@ -2374,12 +2362,6 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
     if (set_device(c)) return LIVO_E_HIP;
     int rc = lane_streams(c, L);
     if (rc) return rc;
-    if (!lm && !c->ikst[0])
-        for (int k = 0; k < kMaxGroups; k++) {
-            if (hipStreamCreateWithFlags(&c->ikst[k], hipStreamNonBlocking) != hipSuccess) return LIVO_E_HIP;
-            for (hipEvent_t& e : c->ikev[k])
-                if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return LIVO_E_HIP;
-        }
     rc = lm ? ensure_lm(B, n) : ensure_slots(c, n);
     if (rc) return rc;
     // Slots and jobs: the IKFoM model uses whole slots (c->h_slots / d_slots);
@@ -2462,9 +2444,9 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
     // updates/s; 6 / 8 share the box's 4 queues and lose, profiles/r04_ab_groups.txt;
     // 8 x 200k on the 10M map: 4437 vs 3960 with two): one group's
     // latency-bound evaluations (no search: launch, reduction, solve) and its
-    // replay tail overlap the other groups' searches.  The unfused paths (IKFoM,
-    // iVox) keep two: IKFoM 4,114 with four vs 5,177 updates/s with two
-    const int auto_groups = fused ? 4 : 2;
+    // replay tail overlap the other groups' searches.  IKFoM four too (5.40k vs
+    // 5.13k with two); the iVox path two (1,520 vs 1,513 with four)
+    const int auto_groups = (fused || model == kModelIkfom) ? 4 : 2;
     const int ngroups = std::max(1, std::min<int>(c->groups > 0 ? c->groups : auto_groups, n));
     int64_t off = 0;
     for (int gi = 0; gi < ngroups; gi++) {
@@ -2517,15 +2499,6 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
             if (full && (e > 0 || gi > 0)) HIP_TRY(hipEventRecord(c->ev[gi][3 * e], st));
             // leaf-map search; rematch passes are bounded by the previous neighbours
             // (the group's replay count was zeroed before the batch / by the last k_solve)
-            if (!lm) {
-                // IKFoM: the measurement-free part of the solve (k_ik_prep) on the group's
-                // side stream once the last solve is done, beside this search and plane pass
-                HIP_TRY(hipEventRecord(c->ikev[gi][0], st));
-                HIP_TRY(hipStreamWaitEvent(c->ikst[gi], c->ikev[gi][0], 0));
-                rc = launch_ik_prep(hp[gi], g[gi].count, c->ikst[gi]);
-                if (rc) return rc;
-                HIP_TRY(hipEventRecord(c->ikev[gi][1], c->ikst[gi]));
-            }
             rc = backend_knn(c, kp[gi], g[gi].count, g[gi].max_n, e > 0, st);
             if (rc) return rc;
             if ((prof && e == 0) || full) HIP_TRY(hipEventRecord(c->ev[gi][3 * e + 1], st));
@@ -2533,8 +2506,11 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
                                       : launch_hshare(hp[gi], g[gi].count, g[gi].max_nblk, e == 0, st);
             if (rc) return rc;
             if (!lm) {
-                HIP_TRY(hipStreamWaitEvent(st, c->ikev[gi][1], 0));
-                rc = launch_solve_ik(hp[gi], g[gi].count, st);
+                // IKFoM: the measurement-free part of the solve (k_ik_prep), then the
+                // gain (k_solve_ik); k_ik_prep on a side stream beside the search and
+                // plane pass measured no better (5.1k vs 5.2k updates/s, r04_ab_groups.txt)
+                rc = launch_ik_prep(hp[gi], g[gi].count, st);
+                if (!rc) rc = launch_solve_ik(hp[gi], g[gi].count, st);
                 if (rc) return rc;
             }
         }
