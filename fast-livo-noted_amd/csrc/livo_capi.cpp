@@ -173,9 +173,9 @@ struct livo_ctx {
     // extra streams for the groups of a batch (overlap of latency-bound kernels)
     hipStream_t xstream[kMaxGroups - 1] = {};
     hipEvent_t xjoin[kMaxGroups - 1] = {};
-    // stream groups per batch (LIVO_STREAM_GROUPS; 0: 1 for a fused evaluation
-    // of <= 1.2M points, 2 otherwise).  MI355X, 8 x 100k scans: unfused 1 / 2 / 4 groups 8884 / 9503 /
-    // 9145 updates/s; fused 12020 / 11883 / 11777 (profiles/r02_ab_groups.txt)
+    // stream groups per batch (LIVO_STREAM_GROUPS; 0: the default of
+    // batch_enqueue, four for the fused and IKFoM paths, two for iVox,
+    // profiles/r04_ab_groups.txt)
     int groups = 0;
     int leaf_size = kLeafSize;         // leaf-map points per leaf (LIVO_LEAF_SIZE)
     hipEvent_t fork = nullptr;
