@@ -140,8 +140,10 @@ struct DynDev {
     int64_t d_n = 0, dslot_cap = 0, dpts_cap = 0;
     int64_t rebases = 0;
     double rebase_frac = 0.125;      // LIVO_DYN_REBASE
-    float min_gh = 0.f;              // the cell-walk grid's smallest edge: box_cell x the Add_Points box
+    float min_gh = 0.f;              // the cell-walk grid's edge range: [box_cell, box_cell_max] x the Add_Points box
+    float max_gh = 0.f;
     float box_cell = 1.2f;           // LIVO_DYN_BOX_CELL
+    float box_cell_max = 2.0f;       // LIVO_DYN_BOX_CELL_MAX (0: no upper bound)
 };
 
 // One batch's staging and streams.  LaserMapping batches: slots packed at
@@ -1225,6 +1227,10 @@ static int dyn_activate(livo_ctx* c) {
     d.active = true;
     d.runs = false;
     d.d_n = 0;
+    if (const char* env = std::getenv("LIVO_DYN_BOX_CELL_MAX")) {  // tuning knob (0: off)
+        const double v = std::atof(env);
+        if (v >= 0.0 && v < 100.0) d.box_cell_max = (float)v;
+    }
     if (const char* env = std::getenv("LIVO_DYN_BOX_CELL")) {  // tuning knob (0: off)
         const double v = std::atof(env);
         if (v >= 0.0 && v < 100.0) d.box_cell = (float)v;
@@ -1253,9 +1259,10 @@ static int dyn_activate(livo_ctx* c) {
 // build_grid_map: cells in key order, a cell's points in id order).
 static int dyn_rebuild(livo_ctx* c) {
     DynDev& d = c->dyn;
-    if (!d.runs && c->gh < d.min_gh) {
+    if (!d.runs && (c->gh < d.min_gh || (d.max_gh > 0.f && c->gh > d.max_gh))) {
         const float lo = (float)(2.0 * (double)d.cmax / (double)(kGridBias - 2));
-        c->gh = std::max(d.min_gh, lo * 1.01f);
+        const float h = c->gh < d.min_gh ? d.min_gh : std::max(d.max_gh, d.min_gh);
+        c->gh = std::max(h, lo * 1.01f);
     }
     int rc = dyn_sort_scratch(c, std::max<int64_t>(d.n_ids, 1));
     if (rc) return rc;
@@ -1305,12 +1312,17 @@ static int dyn_add(livo_ctx* c, int64_t n, float ds, bool downsample, livo_map_a
     DynDev& d = c->dyn;
     // Add_Points' downsampling leaves one point per box of edge ds where the
     // scans pass: the cell walk's grid (rebuilt after this change) takes cells
-    // of at least box_cell * ds, so a walk through those thinned regions probes
-    // a few cells, not a cube of near-empty ones sized for the built map's
-    // density (IEKF 0.58 vs 0.78 ms per scan on the thinned 1M map with 0.6 m
-    // cells; maps grown from scans already have larger cells,
-    // profiles/r04_ab_dyn_cell.txt).  The runs, when kept, index the built grid.
-    if (downsample && ds > 0.f && !d.runs) d.min_gh = std::max(d.min_gh, d.box_cell * ds);
+    // of [box_cell, box_cell_max] * ds = [0.6, 1.0] m for 0.5 m boxes, so a walk
+    // through thinned regions probes a few cells, not a cube of near-empty ones
+    // sized for a dense built map (IEKF 0.58 vs 0.78 ms per scan on the thinned
+    // 1M map), and a map built from one sparse scan does not keep cells sized
+    // for its first few thousand points (0.245 vs 0.272 ms, Add_Points 0.48 vs
+    // 0.62 ms; profiles/r04_ab_dyn_box_cell.txt).  The runs, when kept, index
+    // the built grid.
+    if (downsample && ds > 0.f && !d.runs) {
+        d.min_gh = std::max(d.min_gh, d.box_cell * ds);
+        if (d.box_cell_max > 0.f) d.max_gh = std::max(d.max_gh, d.box_cell_max * ds);
+    }
     livo_map_add_stats st{};
     if (n > 0) {
         if (d.n_ids + n > kMaxMapPoints || n > (int64_t)0x7FFFFFFF) return LIVO_E_RANGE;
@@ -1894,7 +1906,7 @@ int livo_map_build(livo_ctx* c, const float* xyz, int64_t M, int64_t stride_byte
     c->leaf_bytes = c->grid_bytes = 0;
     c->has_map = false;
     c->dyn.active = false;  // a new static map (the incremental buffers are kept for reuse)
-    c->dyn.min_gh = 0.f;
+    c->dyn.min_gh = c->dyn.max_gh = 0.f;
     c->dyn.runs = false;
     c->dyn.d_n = 0;
     c->dyn.n_ids = c->dyn.n_alive = 0;
