@@ -168,7 +168,10 @@ void free_grid_map(HostGridMap* m);
 // ---------------------------------------------------------------------------
 constexpr int kIvBias = 1 << 20;            // key bias (21 bits per axis)
 constexpr int kIvMaxKey = kIvBias - 64;     // |cell| limit of stored points
-constexpr int kIvCap = 128;                 // private candidates per query (k_ivox_knn); beyond: overflow pass
+#ifndef LIVO_IV_CAP
+#define LIVO_IV_CAP 128
+#endif
+constexpr int kIvCap = LIVO_IV_CAP;                 // private candidates per query (k_ivox_knn); beyond: overflow pass
 constexpr int kIvMaxNearby = 27;
 
 struct IvoxParams {
