@@ -778,8 +778,12 @@ def main():
         # Add_Points with the 0.5 m box downsampling, so the map is the room at
         # one point per box.  Mapping scans (pool scans after the first batch,
         # at their true poses) build it up before the timed odometry passes.
-        map_seeds = pool_seeds[a.batch:a.batch + 32]
-        map_scans = pool_scans[a.batch:a.batch + 32]
+        map_seeds = list(pool_seeds[a.batch:a.batch + 32])
+        map_scans = list(pool_scans[a.batch:a.batch + 32])
+        if len(map_seeds) < 32:  # a pool of fewer than batch + 32 scans: the rest made here (in-process: the GPU is up)
+            extra = [pool_seeds[-1] + 1 + j for j in range(32 - len(map_seeds))]
+            map_seeds += extra
+            map_scans += gen_scans(a.scan_points, extra, 1)
         R0, p0, _ = synth.true_pose(map_seeds[0])
         w0 = (map_scans[0].astype(np.float64) @ synth.R_LI.T + synth.T_LI) @ R0.T + p0
         _, first = np.unique(np.floor(w0 / 0.5).astype(np.int64), axis=0, return_index=True)

@@ -144,8 +144,20 @@ __device__ __forceinline__ void mat3_mul(const double* A, const double* B, doubl
             C[i * 3 + j] = (A[i * 3 + 0] * B[0 * 3 + j] + A[i * 3 + 1] * B[1 * 3 + j]) + A[i * 3 + 2] * B[2 * 3 + j];
 }
 
+// The head of livo_state (everything but cov): a staged copy in LDS.
+struct StateHead {
+    double rot[9];
+    double pos[3];
+    double vel[3];
+    double bias_g[3];
+    double bias_a[3];
+    double gravity[3];
+};
+
 // StatesGroup a - b (common_lib.h:576-587): Log(b.rot^T a.rot), then differences.
-__device__ __forceinline__ void state_minus_d(const livo_state& a, const livo_state& b, double* v) {
+// S: livo_state or its StateHead.
+template <class S>
+__device__ __forceinline__ void state_minus_d(const S& a, const S& b, double* v) {
     double bt[9], ra[9], rd[9], v3[3];
 #pragma unroll
     for (int r = 0; r < 3; r++)
@@ -168,7 +180,8 @@ __device__ __forceinline__ void state_minus_d(const livo_state& a, const livo_st
 }
 
 // StatesGroup += (common_lib.h:565-574): rot * Exp(d0..2), the rest added.
-__device__ __forceinline__ void state_boxplus_d(livo_state& st, const double* sol) {
+template <class S>
+__device__ __forceinline__ void state_boxplus_d(S& st, const double* sol) {
     double E[9], Rn[9];
     so3_exp(sol[0], sol[1], sol[2], E);
     mat3_mul(st.rot, E, Rn);

@@ -201,6 +201,7 @@ struct livo_ctx {
     // 18.3k vs 17.1k / 17.1k vs 16.4k updates/s against 0, one range per XCD, whose
     // most expensive scan's XCD was the straggler; profiles/r04_ab_block_order.txt)
     int xcd_chunk = 8;
+    int ns_k = 4;                      // evaluations without a search: chunks per block (LIVO_NS_K)
     GridSlot* vslots = nullptr;        // vertex runs (static map only)
     RunWord* vpts = nullptr;           // run entries (LIVO_IDX_RUNS: grid positions; else x, y, z, map index bits)
     int32_t vlog2 = 0;
@@ -474,6 +475,7 @@ static KnnParams make_knn_params(livo_ctx* c) {
     // keeps points with cr_rho2 <= brmax^2 in float: a relative 1e-5 below covers its rounding)
     kp.bcert2 = c->brmax * c->brmax * (1.0f - 1e-5f);
     kp.xcd_chunk = c->xcd_chunk;
+    kp.ns_k = c->ns_k;
     kp.identity = 0;
     kp.iv = ivox_params(c);
     kp.canon = c->dyn.active ? 1 : 0;
@@ -870,7 +872,12 @@ static int ivox_add_part(livo_ctx* c, int64_t off, int64_t n, int64_t* done) {
                 if (rc) return rc;
                 HIP_TRY(hipMemcpyAsync(ctr, v.ctr, sizeof(ctr), hipMemcpyDeviceToHost, c->stream));
                 HIP_TRY(hipStreamSynchronize(c->stream));
-                if ((ctr[0] & 2ull) || E + (int64_t)ctr[1] - (C - 1) != evs) return LIVO_E_HIP;  // (the scan's invariant)
+                if ((ctr[0] & 2ull) || E + (int64_t)ctr[1] - (C - 1) != evs) {  // (the scan's invariant)
+                    // undo the prefix's uncommitted slots, so the table stays clean for the next AddPoints
+                    rc = launch_ivox_rollback(P, c->stream);
+                    if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = LIVO_E_HIP;
+                    return rc ? rc : LIVO_E_HIP;
+                }
                 consumed = pend;
                 ev = evs;
                 conflict = false;
@@ -1497,6 +1504,7 @@ int livo_ctx_create(int device, const livo_params* p, livo_ctx** out) {
     if (const char* env = std::getenv("LIVO_SYNC_ZC")) c->sync_zc = std::atoi(env) != 0;
     if (const char* env = std::getenv("LIVO_SLOT_WB")) c->slot_wb = std::atoi(env) != 0;
     if (const char* env = std::getenv("LIVO_XCD_CHUNK")) c->xcd_chunk = std::max(0, std::atoi(env));  // tuning knob
+    if (const char* env = std::getenv("LIVO_NS_K")) c->ns_k = std::max(1, std::atoi(env));  // tuning knob
     if (const char* env = std::getenv("LIVO_GRID_PPC")) {  // tuning knob
         const float v = (float)std::atof(env);
         if (v > 0.f) c->grid_ppc = v;

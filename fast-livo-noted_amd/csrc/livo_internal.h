@@ -321,6 +321,7 @@ struct KnnParams {
     int32_t identity;       // 1: pts are world points already (livo_knn)
     int32_t nb;             // blocks per scan (set by the launcher)
     int32_t xcd_chunk;      // k_iekf_eval block order: XCD-interleaved chunks of this many blocks (0: one range per XCD)
+    int32_t ns_k;           // k_iekf_eval without a search: 256-point chunks per block (1: one)
     int32_t ldepth;         // leaf map depth D
     const LeafNode* lnodes; // leaf map internal records
     const float* lpts;      // leaf map points, 4 floats each (x, y, z, index bits)

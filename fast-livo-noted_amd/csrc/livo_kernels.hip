@@ -2205,10 +2205,27 @@ __device__ unsigned long long g_solve_prof[256][16];
 #else
 #define SOLVE_MARK(k) do { } while (0)
 #endif
-// LDS of one scan's solve.
-struct SolveLds {
+#ifdef LIVO_EVAL_PROF  // solve_scan's phases summed per evaluation kind (tools/eval_prof.py)
+__device__ unsigned long long g_solve_ph[3][16];
+#define SPH_MARK(k)                                                                                     \
+    do {                                                                                               \
+        if (pk >= 0 && lane == 0) {                                                                    \
+            const unsigned long long now_ = __builtin_amdgcn_s_memtime();                             \
+            atomicAdd(&g_solve_ph[pk][(k)], now_ - sph_t);                                             \
+            sph_t = now_;                                                                              \
+        }                                                                                              \
+    } while (0)
+#else
+#define SPH_MARK(k) do { } while (0)
+#endif
+// LDS of one scan's solve.  The slot fields it reads are staged here by the
+// calling block (solve_stage) in one round trip, so the solve itself reads no
+// global memory and its stores go out behind it.
+struct alignas(16) SolveLds {
     double sum[kRedCols];
     double P[kDim * kDim];      // state.cov
+    StateHead st;               // state (rot, pos, vel, biases, gravity)
+    StateHead pr;               // prior (state_propagat)
     double C[36];               // H_T_H(0:6, 0:6)
     double M[36];               // I6 + C P66
     double LU[36];
@@ -2219,24 +2236,78 @@ struct SolveLds {
     double vec[kDim];
     double sol[kDim];
     int piv[6];
+    alignas(16) IekfCtrl ctrl;
+    int knn_passes;             // stats.knn_passes so far
 };
+constexpr int kStHead = (int)(sizeof(StateHead) / sizeof(double));  // 24
+static_assert(sizeof(StateHead) == 24 * sizeof(double) && offsetof(livo_state, cov) == sizeof(StateHead),
+              "StateHead is the head of livo_state");
 
-// One wave (lanes 0..63 of the calling block, the other waves idle), from the
-// reduced h_share sums in L.sum.  Only this wave touches L, so LDS hand-offs
-// between lanes need a wave-level fence, not a block barrier.
-__device__ __forceinline__ void solve_scan(IekfSlot* slot, SolveLds& L, const int lane) {
+__device__ __forceinline__ double ld_sc1(const double* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int ld_sc1(const int* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Stage the solve's inputs (cov, state and prior heads, control, knn_passes)
+// into L: thread t of nt, two loads in flight per thread before any LDS store.
+// sc1 loads: the slot may have been written by another CU of this launch.
+__device__ __forceinline__ void solve_stage(const IekfSlot* slot, SolveLds& L, int t, int nt) {
+    constexpr int nP = kDim * kDim, nD = nP + 2 * kStHead;  // doubles: cov, state head, prior head
+    auto src = [&](int k) -> const double* {
+        return k < nP ? slot->state.cov + k
+                      : (k < nP + kStHead ? slot->state.rot + (k - nP) : slot->prior.rot + (k - nP - kStHead));
+    };
+    auto dst = [&](int k) -> double* {
+        return k < nP ? L.P + k : (k < nP + kStHead ? L.st.rot + (k - nP) : L.pr.rot + (k - nP - kStHead));
+    };
+    for (int k0 = t; k0 < nD; k0 += 2 * nt) {
+        const int k1 = k0 + nt;
+        const double v0 = ld_sc1(src(k0));
+        const double v1 = k1 < nD ? ld_sc1(src(k1)) : 0.0;
+        *dst(k0) = v0;
+        if (k1 < nD) *dst(k1) = v1;
+    }
+    if (t == nt - 1) {
+        const int4* c = reinterpret_cast<const int4*>(&slot->ctrl);
+        const int4 c0 = c[0], c1 = c[1];
+        const int kp = slot->stats.knn_passes;
+        int4* d = reinterpret_cast<int4*>(&L.ctrl);
+        d[0] = c0;
+        d[1] = c1;
+        L.knn_passes = kp;
+    }
+}
+static_assert(sizeof(IekfCtrl) == 8 * sizeof(int) && alignof(IekfSlot) >= 16 && offsetof(IekfSlot, ctrl) % 16 == 0,
+              "IekfCtrl is two aligned int4");
+
+// One wave (lanes 0..63 of the calling block), from the reduced h_share sums
+// in L.sum and the staged inputs.  vec = state_propagat - state is computed by
+// lane 0 first (SPLIT_VEC = false) or, beside M and its LU, by another wave of
+// the block that then meets this wave at one block barrier (SPLIT_VEC = true).
+// Only this wave touches L otherwise, so LDS hand-offs between its lanes need
+// a wave-level fence, not a block barrier.  Returns EKF_stop_flg (uniform).
+template <bool SPLIT_VEC = false>
+__device__ __forceinline__ int solve_scan(IekfSlot* slot, SolveLds& L, const int lane, int pk = -1) {
+#ifdef LIVO_EVAL_PROF
+    unsigned long long sph_t = __builtin_amdgcn_s_memtime();
+#else
+    (void)pk;
+#endif
     const double* const s_sum = L.sum;
-    double* const s_P = L.P;
-    for (int t = lane; t < kDim * kDim; t += 64) s_P[t] = slot->state.cov[t];
+    const double* const s_P = L.P;
+    if (!SPLIT_VEC && lane == 0) state_minus_d(L.pr, L.st, L.vec);  // vec = state_propagat - state
     if (lane < 36) {
         const int r = lane / 6, c = lane % 6;
         const int a = r < c ? r : c, b = r < c ? c : r;
         L.C[lane] = s_sum[a * 6 - (a * (a - 1)) / 2 + (b - a)];  // upper-tri packed index
     }
-    const IekfCtrl ctrl0 = slot->ctrl;
+    const IekfCtrl ctrl0 = L.ctrl;
     const int e = ctrl0.n_evals;
     WAVE_SYNC();
     SOLVE_MARK(2);
+    SPH_MARK(0);
     // M = I6 + C P66
     if (lane < 36) {
         const int r = lane / 6, c = lane % 6;
@@ -2245,9 +2316,8 @@ __device__ __forceinline__ void solve_scan(IekfSlot* slot, SolveLds& L, const in
         for (int k = 1; k < 6; k++) m = m + L.C[r * 6 + k] * s_P[k * kDim + c];
         L.M[lane] = (r == c ? 1.0 : 0.0) + m;
     }
-    // vec = state_propagat - state
-    if (lane == 0) state_minus_d(slot->prior, slot->state, L.vec);
     WAVE_SYNC();
+    SPH_MARK(1);
     {
         double A[6];
 #pragma unroll
@@ -2255,12 +2325,14 @@ __device__ __forceinline__ void solve_scan(IekfSlot* slot, SolveLds& L, const in
         wave_lu_to_lds<6>(A, lane, L.LU, L.piv);
     }
     WAVE_SYNC();
+    SPH_MARK(2);
     if (lane < 6) {
         double y[6];
         lds_lu_column<6>(L.LU, L.piv, lane, y);
 #pragma unroll
         for (int i = 0; i < 6; i++) L.Minv[i * 6 + lane] = y[i];
     }
+    if (SPLIT_VEC) __syncthreads();  // L.vec from the other wave (it waits here too)
     if (lane < 6) {
         double wv = s_sum[21 + lane];
 #pragma unroll
@@ -2269,6 +2341,7 @@ __device__ __forceinline__ void solve_scan(IekfSlot* slot, SolveLds& L, const in
     }
     WAVE_SYNC();
     SOLVE_MARK(4);
+    SPH_MARK(3);
     // K1(:, 0:6) = P(:, 0:6) M^-1
     for (int t = lane; t < kDim * 6; t += 64) {
         const int r = t / 6, c = t % 6;
@@ -2278,6 +2351,7 @@ __device__ __forceinline__ void solve_scan(IekfSlot* slot, SolveLds& L, const in
         L.K6[t] = k6;
     }
     WAVE_SYNC();
+    SPH_MARK(4);
     // G(:, 0:6) = K1(:, 0:6) C ;  solution = K1(:, 0:6) w + vec
     for (int t = lane; t < kDim * 6; t += 64) {
         const int r = t / 6, c = t % 6;
@@ -2293,16 +2367,17 @@ __device__ __forceinline__ void solve_scan(IekfSlot* slot, SolveLds& L, const in
         L.sol[lane] = a + L.vec[lane];
     }
     WAVE_SYNC();
-
+    SPH_MARK(5);
     SOLVE_MARK(7);
-    // 8. boxplus, convergence, rematch control (laser_mapping.cpp:204-237), lane 0
-    int stop_now = 0;
+    // 8. boxplus, convergence, rematch control (laser_mapping.cpp:204-237), lane 0 on
+    // the staged state; the stores below go out behind the solve (nothing waits for them)
+    int stop_now = 0, converged_i = 0;
     if (lane == 0) {
+        IekfCtrl ctrl = ctrl0;
         double sol[kDim];
 #pragma unroll
         for (int k = 0; k < kDim; k++) sol[k] = L.sol[k];
-        IekfCtrl ctrl = ctrl0;
-        state_boxplus_d(slot->state, sol);
+        state_boxplus_d(L.st, sol);
         const double rn = sqrt((sol[0] * sol[0] + sol[1] * sol[1]) + sol[2] * sol[2]);
         const double tn = sqrt((sol[3] * sol[3] + sol[4] * sol[4]) + sol[5] * sol[5]);
         const bool converged = (rn * 180 / (3.14159265358) < 0.01) && (tn * 100 < 0.015);
@@ -2313,19 +2388,8 @@ __device__ __forceinline__ void solve_scan(IekfSlot* slot, SolveLds& L, const in
             ctrl.rematch_num++;
         }
         const bool stop = (ctrl.rematch_num >= 2 || (ctrl.iter_count == ctrl.max_iter - 1));
-        livo_iter_stats& S = slot->stats;
-        if (e < LIVO_MAX_EVALS) {
-            S.effct_feat_num[e] = (int64_t)s_sum[28];
-            S.res_mean[e] = s_sum[27] / s_sum[28];
-#pragma unroll
-            for (int k = 0; k < kDim; k++) S.solution[e][k] = sol[k];
-            slot->eval_search[e] = searched;
-        }
-        S.iterations = e + 1;
-        S.knn_passes += searched ? 1 : 0;
-        S.converged = converged ? 1 : 0;
-        S.rematch_num = ctrl.rematch_num;
-        ctrl.converged = converged ? 1 : 0;
+        converged_i = converged ? 1 : 0;
+        ctrl.converged = converged_i;
         ctrl.last_search = searched;
         ctrl.search_en = next_search ? 1 : 0;
         ctrl.iter_count++;
@@ -2333,10 +2397,33 @@ __device__ __forceinline__ void solve_scan(IekfSlot* slot, SolveLds& L, const in
         // the loop condition iterCount < NUM_MAX_ITERATIONS (:178) also ends it
         ctrl.stop = (stop || ctrl.iter_count >= ctrl.max_iter || ctrl.n_evals >= LIVO_MAX_EVALS) ? 1 : 0;
         stop_now = stop ? 1 : 0;
-        slot->ctrl = ctrl;
+        L.ctrl = ctrl;
     }
     stop_now = __builtin_amdgcn_readfirstlane(stop_now);
+    WAVE_SYNC();
     SOLVE_MARK(8);
+    SPH_MARK(6);
+    // stores: state head, statistics, control
+    if (lane < kStHead) slot->state.rot[lane] = L.st.rot[lane];
+    livo_iter_stats& S = slot->stats;
+    if (e < LIVO_MAX_EVALS) {
+        if (lane < kDim) S.solution[e][lane] = L.sol[lane];
+        if (lane == 0) {
+            S.effct_feat_num[e] = (int64_t)s_sum[28];
+            S.res_mean[e] = s_sum[27] / s_sum[28];
+            slot->eval_search[e] = ctrl0.search_en;
+        }
+    }
+    if (lane == 0) {
+        S.iterations = e + 1;
+        S.knn_passes = L.knn_passes + (ctrl0.search_en ? 1 : 0);
+        S.converged = L.ctrl.converged;
+        S.rematch_num = L.ctrl.rematch_num;
+    }
+    if (lane < 2) {  // the control block as two 16-B stores
+        const int4 c = reinterpret_cast<const int4*>(&L.ctrl)[lane];
+        reinterpret_cast<int4*>(&slot->ctrl)[lane] = c;
+    }
     // 9. covariance update state.cov = (I - G) * state.cov (:224-227) = P - G(:,0:6) P(0:6,:)
     if (stop_now) {
         for (int t = lane; t < kDim * kDim; t += 64) {
@@ -2348,6 +2435,12 @@ __device__ __forceinline__ void solve_scan(IekfSlot* slot, SolveLds& L, const in
         }
     }
     SOLVE_MARK(9);
+#ifdef LIVO_EVAL_PROF
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    SPH_MARK(7);
+    (void)converged_i;
+    return stop_now;
 }
 
 // ===================================================== per-point pass =====
@@ -2583,11 +2676,33 @@ __device__ __forceinline__ void hs_row_sums_bfly(const Col& col, HsReduceLds& R,
     if (base + 1 < NU) R.red[(tid >> 4) * kRedCols + base + 1] = x[1];
 }
 
-template <int NT, int NU = kRedUsed, class Col>
-__device__ __forceinline__ void hshare_reduce_solve(const HsParams& P, const HsJob& job, IekfSlot* slot,
-                                                    const Col& col, int nblk, unsigned blk, HsReduceLds& R,
-                                                    SolveLds& L) {
-    static_assert(NU == kRedUsed || NU == kRedUsed + 2, "h_share sums (+ search counts)");
+#ifdef LIVO_EVAL_PROF  // the reduction's phases (tools/eval_prof.py; compiled out of the product)
+// [kind][k]: 0 blocks, 1 butterfly + partial store + ticket (every block), 2 last block: the
+// partials' reduction, 3 solve, 4 host slot write, 5 last blocks
+__device__ unsigned long long g_tail_prof[3][8];
+#define TAIL_MARK(k, t)                                                                                 \
+    do {                                                                                               \
+        if (pk >= 0 && threadIdx.x == 0) {                                                             \
+            const unsigned long long now_ = __builtin_amdgcn_s_memtime();                             \
+            atomicAdd(&g_tail_prof[pk][(k)], now_ - (t));                                              \
+            (t) = now_;                                                                                \
+        }                                                                                              \
+    } while (0)
+#else
+#define TAIL_MARK(k, t) do { } while (0)
+#endif
+#ifndef LIVO_SOLVE_PRIO
+#define LIVO_SOLVE_PRIO 1
+#endif
+#ifndef LIVO_RED_INFLIGHT
+#define LIVO_RED_INFLIGHT 32
+#endif
+constexpr int kRedInFlight = LIVO_RED_INFLIGHT;  // partial loads in flight per thread of the last block
+// The block partial of one 256-point chunk (blk): the row butterflies into R.red,
+// then wave 0's fixed pairwise tree over the rows, stored write-through (sc1).
+// Ends with wave 0's stores issued; a caller that reuses R.red must barrier first.
+template <int NT, int NU, class Col>
+__device__ __forceinline__ void hs_block_partial(const HsJob& job, const Col& col, unsigned blk, HsReduceLds& R) {
     const int tid = threadIdx.x;
     constexpr int NR = NT / 16;  // 16-lane rows of the block
     static_assert(NR <= kRedRows, "HsReduceLds row partials");
@@ -2596,56 +2711,89 @@ __device__ __forceinline__ void hshare_reduce_solve(const HsParams& P, const HsJ
     // search 0.107 vs 0.116 ms per step: profiles/r03_ab_bfly.txt)
     hs_row_sums_bfly<NU>(col, R, tid, std::make_integer_sequence<int, 32>{});
     __syncthreads();
-    // Wave 0 stores the block partial write-through (sc1) and, once the store
-    // has drained, takes the scan's ticket; the last block of the scan then
+    if (tid < NU) {
+        double r[NRM];
+#pragma unroll
+        for (int w = 0; w < NRM; w++) r[w] = w < NR ? R.red[w * kRedCols + tid] : 0.0;
+#pragma unroll
+        for (int h = NRM / 2; h >= 1; h >>= 1)  // fixed pairwise tree
+#pragma unroll
+            for (int w = 0; w < h; w++) r[w] = r[w] + r[w + h];
+        const double v = r[0];
+        __hip_atomic_store(job.partial + (size_t)blk * kRedCols + tid, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// Block partials of a scan's h_share sums -> the last block of the scan
+// reduces every partial in a fixed order and (P.solve) its wave 0 runs the
+// scan's solve.  nblk = partials (256-point chunks) of the scan in this launch;
+// this block has stored `count` of them (hs_block_partial) before the call.
+template <int NT, int NU = kRedUsed>
+__device__ __forceinline__ void hs_ticket_tail(const HsParams& P, const HsJob& job, IekfSlot* slot, int nblk,
+                                               unsigned count, HsReduceLds& R, SolveLds& L, int pk = -1) {
+    static_assert(NU == kRedUsed || NU == kRedUsed + 2, "h_share sums (+ search counts)");
+    const int tid = threadIdx.x;
+#ifdef LIVO_EVAL_PROF
+    unsigned long long tp = __builtin_amdgcn_s_memtime();
+    if (pk >= 0 && tid == 0) atomicAdd(&g_tail_prof[pk][0], 1ull);
+#else
+    (void)pk;
+#endif
+    // Wave 0 stored the block partials write-through (sc1) and, once the stores
+    // have drained, takes the scan's ticket; the last block of the scan then
     // reduces every partial with sc1 loads in a fixed order and its wave 0 runs
     // the scan's solve (MI355X_MICROARCH.md §Workgroup dispatch: sc1 hand-off,
     // no L2 write-back fence).  One launch less per evaluation than a separate
     // solve kernel.
     if (tid < 64) {
-        if (tid < NU) {
-            double r[NRM];
-#pragma unroll
-            for (int w = 0; w < NRM; w++) r[w] = w < NR ? R.red[w * kRedCols + tid] : 0.0;
-#pragma unroll
-            for (int h = NRM / 2; h >= 1; h >>= 1)  // fixed pairwise tree
-#pragma unroll
-                for (int w = 0; w < h; w++) r[w] = r[w] + r[w + h];
-            const double v = r[0];
-            __hip_atomic_store(job.partial + (size_t)blk * kRedCols + tid, v, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (tid == 0)
-            R.last = __hip_atomic_fetch_add(&slot->hs_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                     (unsigned)nblk - 1u;
+            R.last = __hip_atomic_fetch_add(&slot->hs_ticket, count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                     (unsigned)nblk - count;
     }
     __syncthreads();
+    TAIL_MARK(1, tp);
     if (!R.last) return;
+#if LIVO_SOLVE_PRIO
+    // the scan's serial tail (reduction, solve) ahead of the other waves on its SIMDs
+    __builtin_amdgcn_s_setprio(3);
+#endif
+#ifdef LIVO_EVAL_PROF
+    if (pk >= 0 && tid == 0) atomicAdd(&g_tail_prof[pk][5], 1ull);
+#endif
+    const bool solve = P.solve != 0;  // (kernel parameter: uniform)
+    // the solve's inputs go out first, in the same round trip as the partials
+    if (solve) solve_stage(slot, L, tid, NT);
     {
-        // thread (g, c) sums blocks g, g+G, ... of column c, 16 loads in flight (G = NT / 32 groups)
+        // thread (g, c) sums blocks g, g+G, ... of column c in that order, kRedInFlight
+        // loads in flight (G = NT / 32 groups)
         constexpr int G = NT / 32;
         const int c = tid & 31, g = tid >> 5;
-        double acc16 = 0.0;
+        double acc = 0.0;
         if (c < NU) {
             double* src = job.partial + c;
-            for (int b0 = g; b0 < nblk; b0 += 16 * G) {
-                double v[16];
+            for (int b0 = g; b0 < nblk; b0 += kRedInFlight * G) {
+                double v[kRedInFlight];
 #pragma unroll
-                for (int k = 0; k < 16; k++) {
+                for (int k = 0; k < kRedInFlight; k++) {
                     const int b = b0 + G * k;
-                    v[k] = b < nblk ? __hip_atomic_load(src + (size_t)b * kRedCols, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT)
-                                    : 0.0;
+                    v[k] = b < nblk ? ld_sc1(src + (size_t)b * kRedCols) : 0.0;
                 }
 #pragma unroll
-                for (int k = 0; k < 16; k++) acc16 += v[k];
+                for (int k = 0; k < kRedInFlight; k++) acc += v[k];
             }
         }
-        R.fin[g * kRedCols + c] = acc16;
+        R.fin[g * kRedCols + c] = acc;
     }
-    __syncthreads();
-    if (tid >= 64) return;  // the solve is one wave's work
+    __syncthreads();  // the block partials' sums and the staged inputs
+    if (tid >= 64) {
+        // vec = state_propagat - state beside wave 0's M and LU; then the one barrier
+        // solve_scan<true> waits at before it uses vec
+        if (solve && tid == 64) state_minus_d(L.pr, L.st, L.vec);
+        if (solve) __syncthreads();
+        return;
+    }
+    TAIL_MARK(2, tp);
     if (tid < kRedCols) {
         double v = 0.0;
         if (tid < NU) {
@@ -2661,9 +2809,10 @@ __device__ __forceinline__ void hshare_reduce_solve(const HsParams& P, const HsJ
         }
         if (NU > kRedUsed && tid >= kRedUsed) {
             if (tid < NU && v > 0.0) {
-                int e = slot->ctrl.n_evals;
+                int e = solve ? L.ctrl.n_evals : slot->ctrl.n_evals;
                 e = e < LIVO_MAX_EVALS ? e : LIVO_MAX_EVALS - 1;
-                (tid == kRedUsed ? slot->visits : slot->scanned)[e] += (unsigned long long)v;
+                // (no return value: the wave does not wait for it)
+                atomicAdd((tid == kRedUsed ? slot->visits : slot->scanned) + e, (unsigned long long)v);
             }
             v = 0.0;
         }
@@ -2671,19 +2820,35 @@ __device__ __forceinline__ void hshare_reduce_solve(const HsParams& P, const HsJ
         slot->red[tid] = v;
     }
     if (tid == 0) slot->hs_ticket = 0u;  // ready for the next pass
-    if (!P.solve) return;  // livo_h_share: the sums only
+    if (!solve) return;  // livo_h_share: the sums only
     WAVE_SYNC();
-    solve_scan(slot, L, tid);
-    if (job.host_slot) {
+    solve_scan<true>(slot, L, tid, pk);
+    TAIL_MARK(3, tp);
+    if (job.host_slot && L.ctrl.stop) {
         // the solve that stops the scan writes its slot straight into the host's
-        // staging copy (no copy back after the batch's last evaluation)
-        __threadfence();
-        WAVE_SYNC();
-        if (slot->ctrl.stop) {
-            const uint4* src = reinterpret_cast<const uint4*>(slot);
-            for (int w = tid; w < (int)((kSlotLmBytes + 15) / 16); w += 64) job.host_slot[w] = src[w];
+        // staging copy (no copy back after the batch's last evaluation): this wave's
+        // slot stores drained to L2, then read back past the L1 (sc1)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned long long* src = reinterpret_cast<const unsigned long long*>(slot);
+        for (int w = tid; w < (int)((kSlotLmBytes + 15) / 16); w += 64) {
+            const unsigned long long lo = __hip_atomic_load(src + 2 * w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long hi = __hip_atomic_load(src + 2 * w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            job.host_slot[w] = make_uint4((unsigned)lo, (unsigned)(lo >> 32), (unsigned)hi, (unsigned)(hi >> 32));
         }
     }
+#ifdef LIVO_EVAL_PROF
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    TAIL_MARK(4, tp);
+}
+
+// One chunk per block: its partial, then the ticket and the tail.
+template <int NT, int NU = kRedUsed, class Col>
+__device__ __forceinline__ void hshare_reduce_solve(const HsParams& P, const HsJob& job, IekfSlot* slot,
+                                                    const Col& col, int nblk, unsigned blk, HsReduceLds& R,
+                                                    SolveLds& L, int pk = -1) {
+    hs_block_partial<NT, NU>(job, col, blk, R);
+    hs_ticket_tail<NT, NU>(P, job, slot, nblk, 1u, R, L, pk);
 }
 
 template <bool FIRST>
@@ -2798,6 +2963,9 @@ __device__ unsigned long long g_eval_tl[LIVO_MAX_EVALS][kTlBlocks][2];
 #ifndef LIVO_EVAL_WAVES
 #define LIVO_EVAL_WAVES 4  // waves per SIMD the VGPR budget must allow (<= 128 VGPRs)
 #endif
+#ifndef LIVO_NS_K
+#define LIVO_NS_K 4  // most 256-point chunks per block in an evaluation without a search (KnnParams::ns_k)
+#endif
 template <bool FIRST>
 __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalParams E) {
     const KnnParams& P = E.k;
@@ -2827,6 +2995,49 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
     bool prefit = false;  // the plane of this evaluation fitted in the search branch
     if (slot->ctrl.stop) return;  // block-uniform
     const int search = FIRST ? 1 : slot->ctrl.search_en;
+#if LIVO_NS_K > 1
+    if (!FIRST && !search && P.ns_k > 1) {  // (ns_k: kernel parameter, uniform; search: block-uniform)
+        // An evaluation without a search: the group leader (its place in the block
+        // order a multiple of K = ns_k, or the scan's chunk 0) takes chunks bx .. cend-1
+        // of its scan, K consecutive 256-point chunks, the others exit at once: a
+        // quarter of the blocks to dispatch, their loads all issued up front.  Each
+        // chunk's partial is the one-chunk block's (same columns, same fixed tree),
+        // so the sums are bit for bit those of one chunk per block.
+        const int K = min(P.ns_k, LIVO_NS_K);
+        const unsigned r = (bjob * (unsigned)P.nb + bx) % (unsigned)K;
+        if (r != 0u && bx != 0u) return;  // block-uniform
+        const int nblk = max(1, (job.n + kEvalBlock - 1) / kEvalBlock);
+        const int cend = min(nblk, (int)bx + K - (int)r);
+        HsPointIn pin_k[LIVO_NS_K];
+        pin_k[0] = pin;
+#pragma unroll
+        for (int k = 1; k < LIVO_NS_K; k++) {
+            const int ii = ((int)bx + k) * kEvalBlock + threadIdx.x;
+            pin_k[k] = ((int)bx + k < cend && ii < job.n) ? hshare_load(job, ii, true) : HsPointIn{};
+        }
+        const double inv_r = E.h.inv_r;
+#pragma unroll
+        for (int k = 0; k < LIVO_NS_K; k++) {
+            const int c = (int)bx + k;
+            if (c < cend) {  // uniform
+                if (k > 0) __syncthreads();  // wave 0 has read the last chunk's rows
+                HsRow w;
+                hs_row_clear(w);
+                const int ii = c * kEvalBlock + threadIdx.x;
+                if (ii < job.n) hshare_point(E.h, job, slot->state, ii, 0, w, pin_k[k], false);
+                auto col = [&](auto jc) -> double {
+                    constexpr int j = decltype(jc)::value;
+                    if constexpr (j < kRedUsed) return hs_col<j>(w, inv_r);
+                    else return 0.0;  // (no search: no hash-slot / map-point counts)
+                };
+                hs_block_partial<kEvalBlock, kRedUsed + 2>(job, col, (unsigned)c, U.rs.R);
+            }
+        }
+        hs_ticket_tail<kEvalBlock, kRedUsed + 2>(E.h, job, slot, nblk, (unsigned)(cend - (int)bx), U.rs.R,
+                                                 U.rs.solve, -1);
+        return;
+    }
+#endif
 #ifdef LIVO_EVAL_PROF
     const int tl_e = min(slot->ctrl.n_evals, LIVO_MAX_EVALS - 1);
 #endif
@@ -2986,7 +3197,12 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
         else if constexpr (j == kRedUsed) return (double)n_slots;
         else return (double)n_pts;
     };
-    hshare_reduce_solve<kEvalBlock, kRedUsed + 2>(E.h, job, slot, col, nblk, bx, U.rs.R, U.rs.solve);
+#ifdef LIVO_EVAL_PROF
+    const int pk = FIRST ? 2 : (search ? 1 : 0);
+#else
+    const int pk = -1;
+#endif
+    hshare_reduce_solve<kEvalBlock, kRedUsed + 2>(E.h, job, slot, col, nblk, bx, U.rs.R, U.rs.solve, pk);
     EVAL_MARK(4);
 #ifdef LIVO_EVAL_PROF
     if (threadIdx.x == 0 && blockIdx.x < (unsigned)kTlBlocks) {
@@ -3551,8 +3767,8 @@ __global__ __launch_bounds__(64 * kIkSolveWaves) void k_solve_ik(HsParams P) {
 }
 
 // One wave per scan: ik_prep of the scan's current estimate into job.ikprep.
-// Launched on its own stream once the previous evaluation's solve is done, it
-// runs beside this evaluation's search and plane pass (k_solve_ik waits on it).
+// Launched in-line on the group's stream right before k_solve_ik (a side-stream
+// launch beside the search and plane pass measured no faster and was dropped).
 __global__ __launch_bounds__(64) void k_ik_prep(HsParams P) {
     __shared__ IkSolveLds S;
     const HsJob job = P.jobs[blockIdx.x];
@@ -3607,6 +3823,7 @@ __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
     }
     SOLVE_MARK(1);
     if (P.mode == 1) return;
+    solve_stage(slot, L, lane, 64);
     WAVE_SYNC();
     solve_scan(slot, L, lane);
 }
@@ -3663,6 +3880,7 @@ int launch_knn_grid(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, 
 #if LIVO_IDX_RUNS
     if (q.vslots && !q.canon && !q.dyn_runs) {  // the runs of a static map: their search pass
         q.nb = (int32_t)((max_n + kEvalBlock - 1) / kEvalBlock);
+        if ((int64_t)q.nb * n_jobs >= (1ll << 31)) return LIVO_E_RANGE;  // (the grid actually launched)
         const dim3 rgrid((unsigned)(q.nb * n_jobs)), rblock(kEvalBlock);
         if (seeded)
             hipLaunchKernelGGL(k_knn_runs<true>, rgrid, rblock, 0, (hipStream_t)stream, q);
@@ -3702,6 +3920,32 @@ extern "C" int livo_debug_eval_prof(unsigned long long* out) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_eval_prof), sizeof(g_eval_prof)) != hipSuccess) return LIVO_E_HIP;
     static const unsigned long long zero[24] = {};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_eval_prof), zero, sizeof(zero)) == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+// s_memtime ticks per s_memrealtime tick (100 MHz): the phase marks' clock
+__global__ void k_clock_cal(unsigned long long* out, int iters) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    float x = (float)threadIdx.x;
+    for (int k = 0; k < iters; k++) x = x * 0.999f + 1.0f;
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) { out[0] = t1 - t0; out[1] = r1 - r0; out[2] = (unsigned long long)x; }
+}
+extern "C" int livo_debug_clock(double* mhz) {
+    unsigned long long* d = nullptr;
+    if (hipMalloc(&d, 32) != hipSuccess) return LIVO_E_HIP;
+    unsigned long long h[3] = {};
+    hipLaunchKernelGGL(k_clock_cal, dim3(1), dim3(64), 0, 0, d, 4 << 20);
+    const bool ok = hipMemcpy(h, d, 24, hipMemcpyDeviceToHost) == hipSuccess;
+    (void)hipFree(d);
+    if (!ok || h[1] == 0) return LIVO_E_HIP;
+    *mhz = 100.0 * (double)h[0] / (double)h[1];
+    return LIVO_OK;
+}
+extern "C" int livo_debug_tail_prof(unsigned long long* out) {  // [3][8] tail, then [3][16] solve phases; reset
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tail_prof), sizeof(g_tail_prof)) != hipSuccess) return LIVO_E_HIP;
+    if (hipMemcpyFromSymbol(out + 24, HIP_SYMBOL(g_solve_ph), sizeof(g_solve_ph)) != hipSuccess) return LIVO_E_HIP;
+    unsigned long long zero[3][16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_solve_ph), zero, sizeof(g_solve_ph)) != hipSuccess) return LIVO_E_HIP;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_tail_prof), zero, sizeof(g_tail_prof)) == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 extern "C" int livo_debug_amb_reason(unsigned long long* out) {
     if (hipDeviceSynchronize() != hipSuccess) return LIVO_E_HIP;

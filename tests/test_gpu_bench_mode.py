@@ -58,12 +58,15 @@ def test_golden_fixture(built):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("seed0", [0, 8, 176])
-def test_bench_headline_mode_parity(built, seed0):
+@pytest.mark.parametrize("seed0,groups", [(0, None), (8, None), (176, None), (0, 2)])
+def test_bench_headline_mode_parity(built, seed0, groups, monkeypatch):
     """8 x 100k scans, 1M map, one livo_iekf_update_batch in the default stream
-    grouping (two groups at 800k points: the bench's step): per scan, the oracle's iterations, k-NN passes,
+    grouping (four groups of two scans: the bench's step; groups=2: LIVO_STREAM_GROUPS=2,
+    two groups of four): per scan, the oracle's iterations, k-NN passes,
     effective points and per-evaluation state deltas.  seed0: the bench pool's
-    first batch (0), its second (8) and its last at the default 20 + 3 steps (176)."""
+    first batch (0), its second (8) and a late one (176)."""
+    if groups is not None:
+        monkeypatch.setenv("LIVO_STREAM_GROUPS", str(groups))  # (read at context creation)
     import livo_amd
     import oracle
     from livo_amd import synth

@@ -34,10 +34,22 @@ def main():
         L.livo_debug_eval_prof.argtypes = [C.c_void_p]
         buf = (C.c_ulonglong * 24)()
         ctx.iekf_update_batch(sids, st0)
+        ctx.set_profiling(2)
+        ctx.iekf_update_batch(sids, st0)
+        t = ctx.last_timings()
+        print("per-evaluation windows (ms, events, max over groups):", [round(x, 4) for x in t["eval_ms"]])
+        ctx.set_profiling(0)
         L.livo_debug_eval_stats.argtypes = [C.c_void_p]
         sbuf = (C.c_ulonglong * 24)()
         L.livo_debug_amb_reason.argtypes = [C.c_void_p]
         abuf = (C.c_ulonglong * 8)()
+        mhz = C.c_double(0.0)
+        L.livo_debug_clock.argtypes = [C.c_void_p]
+        if L.livo_debug_clock(C.byref(mhz)) == 0:
+            print(f"s_memtime clock: {mhz.value:.0f} MHz (vs s_memrealtime)")
+        L.livo_debug_tail_prof.argtypes = [C.c_void_p]
+        tbuf = (C.c_ulonglong * 72)()
+        L.livo_debug_tail_prof(tbuf)
         L.livo_debug_eval_prof(buf)  # reset after the warm-up
         L.livo_debug_eval_stats(sbuf)
         L.livo_debug_amb_reason(abuf)
@@ -47,6 +59,18 @@ def main():
         assert L.livo_debug_eval_prof(buf) == 0
         assert L.livo_debug_eval_stats(sbuf) == 0
         assert L.livo_debug_amb_reason(abuf) == 0
+        assert L.livo_debug_tail_prof(tbuf) == 0
+        # the reduction's tail (thread 0 s_memtime cycles): every block's butterfly + partial store +
+        # ticket; the scan's last block: the partials' reduction, the solve, the host slot write
+        for s, name in ((2, "first-search evals"), (1, "rematch evals"), (0, "no-search evals")):
+            r = tbuf[8 * s: 8 * s + 8]
+            nb, nl = max(r[0], 1), max(r[5], 1)
+            print(f"{name} tail: blocks {r[0]}  bfly+ticket {r[1] / nb / 1e3:.2f} kcyc/block  last blocks {r[5]}: "
+                  f"reduce {r[2] / nl / 1e3:.2f}  solve {r[3] / nl / 1e3:.2f}  slot write {r[4] / nl / 1e3:.2f} kcyc")
+            ph = tbuf[24 + 16 * s: 24 + 16 * s + 8]
+            names = ("P+C", "M+vec", "LU", "Minv+w", "K6", "G6+sol", "boxplus+ctrl", "cov")
+            print(f"    solve phases (kcyc per last block): " +
+                  "  ".join(f"{n} {v / nl / 1e3:.2f}" for n, v in zip(names, ph)))
         print(f"flagged queries per batch: uncertified {abuf[0] / steps:.2f}  C1 near-tie {abuf[1] / steps:.2f}  "
               f"C1 exact tie {abuf[4] / steps:.2f}  C2 gap {abuf[2] / steps:.2f}  C2 equal x {abuf[3] / steps:.2f}")
         for s, name in ((2, "first-search evals"), (1, "rematch evals")):
