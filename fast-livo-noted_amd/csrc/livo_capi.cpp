@@ -30,17 +30,18 @@ struct ScanBuf {
     int32_t nblk = 0;
     float* pts = nullptr;  // n x 4
     NNRec* nn = nullptr;   // neighbour records (Nearest_Points cache)
-    std::vector<int32_t> perm;  // stored (Morton) position -> caller's point index
-    int32_t* d_perm = nullptr;  // the same on the device
+    int32_t* d_perm = nullptr;  // stored (Morton) position -> caller's point index
+    std::vector<int32_t> perm;  // the same on the host, fetched on first use (host_perm)
     int32_t* d_iperm = nullptr; // caller's point index -> stored position
     double* partial = nullptr;  // nblk x kIkCols (the A-path uses kRedCols of each)
     float* plane = nullptr;     // N x 4: planes of the cached neighbours (k_hshare)
     uint8_t* pstate = nullptr;  // N: plane state (0: not fitted since the neighbours changed)
     double* ikrows = nullptr;   // IKFoM few-point rows (nblk x kIkFewRows x 13)
     uint32_t* ikcnt = nullptr;  // per block
-    double* ikprep = nullptr;   // IKFoM per-evaluation prep (kIkPrep doubles)
     bool searched = false;      // a search has filled the neighbour cache
     int64_t cap = 0;            // points the buffers were sized for (>= n; reused after a release)
+    hipEvent_t ready = nullptr; // livo_scan_upload_async: recorded on the upload stream when the scan is built
+    bool pending = false;       // an asynchronous upload may still be building it (get_scan waits)
 };
 
 template <typename T>
@@ -62,7 +63,9 @@ static void dev_free(T*& p) {
 
 static void free_scan_buf(ScanBuf& s) {
     dev_free(s.pts); dev_free(s.nn); dev_free(s.partial); dev_free(s.d_perm); dev_free(s.d_iperm);
-    dev_free(s.plane); dev_free(s.pstate); dev_free(s.ikrows); dev_free(s.ikcnt); dev_free(s.ikprep);
+    dev_free(s.plane); dev_free(s.pstate); dev_free(s.ikrows); dev_free(s.ikcnt);
+    if (s.ready) (void)hipEventDestroy(s.ready);
+    s.ready = nullptr;
 }
 
 }  // namespace
@@ -169,6 +172,9 @@ struct BatchLane {
     std::vector<int32_t> ids;
 };
 
+// pinned staging buffers of livo_scan_upload_async (two batches of 8 ahead)
+constexpr int kPinRing = 16;
+
 struct livo_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -246,6 +252,20 @@ struct livo_ctx {
     // upload scratch: Morton keys, sort buffers, bounds and the packed source points
     void* up_tmp = nullptr;
     size_t up_tmp_bytes = 0;
+    // livo_scan_upload_async: its own stream, scratch and rocPRIM scratch, and a
+    // ring of pinned staging buffers (each reused once the copy out of it is done)
+    hipStream_t up_stream = nullptr;
+    void* aup_tmp = nullptr;
+    size_t aup_tmp_bytes = 0;
+    void* aup_prim = nullptr;
+    size_t aup_prim_bytes = 0;
+    struct PinSlot {
+        float* h = nullptr;
+        size_t bytes = 0;
+        hipEvent_t copied = nullptr;
+        bool inflight = false;
+    } pin[kPinRing];
+    int pin_next = 0;
     // batch resources
     int32_t slot_cap = 0;
     IekfSlot* d_slots = nullptr;
@@ -530,7 +550,6 @@ static void fill_job(HsJob& j, ScanBuf& s, IekfSlot* slot) {
     j.pstate = s.pstate;
     j.ikrows = s.ikrows;
     j.ikcnt = s.ikcnt;
-    j.ikprep = s.ikprep;
     j.host_slot = nullptr;
     j.slot = slot;
     j.n = (int32_t)s.n;
@@ -987,6 +1006,7 @@ static int backend_knn(livo_ctx* c, const KnnParams& kp, int n_jobs, int64_t max
 // ---------------------------------------------- ikd-Tree incremental map --
 extern "C" {
 static ScanBuf* get_scan(livo_ctx* c, int32_t id);
+static ScanBuf* get_scan_q(livo_ctx* c, int32_t id);
 }
 static int build_cell_runs(livo_ctx* c, int64_t M);
 static int build_ball_runs(livo_ctx* c, int64_t M, float r5, double ext);
@@ -1532,9 +1552,17 @@ int livo_ctx_destroy(livo_ctx* c) {
     }
     for (int k = 0; k < kMaxGroups - 1; k++)
         if (c->xstream[k]) (void)hipStreamSynchronize(c->xstream[k]);
+    if (c->up_stream) (void)hipStreamSynchronize(c->up_stream);
     for (auto& s : c->scans) free_scan_buf(s);
     for (auto& s : c->spare) free_scan_buf(s);
     if (c->up_tmp) (void)hipFree(c->up_tmp);
+    if (c->aup_tmp) (void)hipFree(c->aup_tmp);
+    if (c->aup_prim) (void)hipFree(c->aup_prim);
+    for (auto& P : c->pin) {
+        if (P.h) (void)hipHostFree(P.h);
+        if (P.copied) (void)hipEventDestroy(P.copied);
+    }
+    if (c->up_stream) (void)hipStreamDestroy(c->up_stream);
     ivox_free(c->iv);
     dyn_free(c->dyn);
     if (c->fe_buf) (void)hipFree(c->fe_buf);
@@ -2050,7 +2078,7 @@ static int32_t register_scan(livo_ctx* c, const ScanBuf& s) {
 
 // The device buffers of a scan of N points: a released scan's when one fits
 // (capacity N .. 2N + 4096), else fresh allocations sized for N.
-static constexpr size_t kMaxSpareScans = 16;
+static constexpr size_t kMaxSpareScans = 32;
 static int alloc_scan_buf(livo_ctx* c, ScanBuf& s, int64_t N) {
     int best = -1;
     for (size_t k = 0; k < c->spare.size(); k++) {
@@ -2074,7 +2102,6 @@ static int alloc_scan_buf(livo_ctx* c, ScanBuf& s, int64_t N) {
         rc |= dev_alloc(&s.pstate, (size_t)cap);
         rc |= dev_alloc(&s.ikrows, (size_t)cblk * kIkFewRows * 13);
         rc |= dev_alloc(&s.ikcnt, (size_t)cblk);
-        if (!s.ikprep) rc |= dev_alloc(&s.ikprep, (size_t)kIkPrep);
         if (rc) {
             free_scan_buf(s);
             return LIVO_E_OOM;
@@ -2085,6 +2112,7 @@ static int alloc_scan_buf(livo_ctx* c, ScanBuf& s, int64_t N) {
     s.searched = false;
     s.n = N;
     s.nblk = (int32_t)std::max<int64_t>(1, (N + kBlock * kPtsPerThread - 1) / (kBlock * kPtsPerThread));
+    s.pending = false;
     s.perm.clear();
     return LIVO_OK;
 }
@@ -2097,6 +2125,7 @@ static void release_scan_buf(livo_ctx* c, ScanBuf& s) {
     }
     ScanBuf r = s;
     r.used = false;
+    r.pending = false;
     r.perm = std::vector<int32_t>();
     c->spare.push_back(r);
     s = ScanBuf{};
@@ -2115,44 +2144,71 @@ static int ensure_up_tmp(livo_ctx* c, size_t bytes) {
     return LIVO_OK;
 }
 
-// A resident scan from N device points (x, y, z at d_src + stride * i floats):
-// the same Morton order as livo_scan_upload's host sort, computed on the device.
+// Where a scan is built: the stream, the sort scratch (keys, sorted keys, iota,
+// perm, bounds: up_tmp_bytes) and the rocPRIM scratch, grown on demand.
+struct UpTarget {
+    hipStream_t st;
+    void** tmp;
+    size_t* tmp_bytes;
+    void** prim;
+    size_t* prim_bytes;
+};
+static int ensure_dev_bytes(void** p, size_t* have, size_t need) {
+    if (need <= *have) return LIVO_OK;
+    if (*p) (void)hipFree(*p);  // (the caller has drained the stream that used it)
+    *p = nullptr;
+    *have = 0;
+    if (hipMalloc(p, need) != hipSuccess) return LIVO_E_OOM;
+    *have = need;
+    return LIVO_OK;
+}
+
+// Morton-order N device points (x, y, z at d_src + stride * i floats) into the
+// scan buffers s on U.st: the same keys and stable order as a host sort.  Only
+// enqueues; the caller synchronises or records an event.
+static int scan_build_on(const UpTarget& U, const float* d_src, int stride, int64_t N, ScanBuf& s) {
+    if (N <= 0) return LIVO_OK;
+    char* base = (char*)*U.tmp;
+    auto* codes = (unsigned long long*)base;
+    auto* scodes = codes + N;
+    auto* iota = (uint32_t*)(scodes + N);
+    auto* perm = iota + N;
+    auto* mm = (unsigned*)(((uintptr_t)(perm + N) + 15) & ~(uintptr_t)15);
+    int rc = LIVO_OK;
+    // bounds start at (+max, -max) in the order-preserving encoding
+    if (hipMemsetD32Async((hipDeviceptr_t)mm, 0xFFFFFFFFu, 3, U.st) != hipSuccess ||
+        hipMemsetD32Async((hipDeviceptr_t)(mm + 3), 0u, 3, U.st) != hipSuccess)
+        rc = LIVO_E_HIP;
+    if (!rc) rc = launch_fe_minmax(d_src, N, stride, mm, U.st);
+    if (!rc) rc = launch_fe_morton(d_src, N, stride, mm, morton_scale(), codes, iota, U.st);
+    if (!rc) {
+        size_t tb = 0;
+        rc = prim_sort_pairs_u64(nullptr, &tb, codes, scodes, iota, perm, N, 60, U.st);
+        if (!rc && tb > *U.prim_bytes) {
+            if (hipStreamSynchronize(U.st) != hipSuccess) rc = LIVO_E_HIP;
+            if (!rc) rc = ensure_dev_bytes(U.prim, U.prim_bytes, tb);
+        }
+        tb = *U.prim_bytes;
+        if (!rc) rc = prim_sort_pairs_u64(*U.prim, &tb, codes, scodes, iota, perm, N, 60, U.st);
+    }
+    if (!rc) rc = launch_fe_gather(d_src, N, stride, perm, s.pts, s.d_iperm, U.st);
+    if (!rc && (hipMemcpyAsync(s.d_perm, perm, (size_t)N * 4, hipMemcpyDeviceToDevice, U.st) != hipSuccess ||
+                hipMemsetAsync(s.nn, 0, (size_t)N * sizeof(NNRec), U.st) != hipSuccess ||
+                hipMemsetAsync(s.pstate, 0, (size_t)N, U.st) != hipSuccess))
+        rc = LIVO_E_HIP;
+    return rc;
+}
+
+// A resident scan from N device points (x, y, z at d_src + stride * i floats),
+// built synchronously on the context's stream.
 static int scan_create_device(livo_ctx* c, const float* d_src, int stride, int64_t N, int32_t* scan_id) {
     ScanBuf s;
     int rc = alloc_scan_buf(c, s, N);
     if (rc) return rc;
     if (N > 0) {
         rc = ensure_up_tmp(c, up_tmp_bytes(N));
-        if (rc) {
-            release_scan_buf(c, s);
-            return rc;
-        }
-        char* base = (char*)c->up_tmp;
-        auto* codes = (unsigned long long*)base;
-        auto* scodes = codes + N;
-        auto* iota = (uint32_t*)(scodes + N);
-        auto* perm = iota + N;
-        auto* mm = (unsigned*)(((uintptr_t)(perm + N) + 15) & ~(uintptr_t)15);
-        // bounds start at (+max, -max) in the order-preserving encoding
-        if (hipMemsetD32Async((hipDeviceptr_t)mm, 0xFFFFFFFFu, 3, c->stream) != hipSuccess ||
-            hipMemsetD32Async((hipDeviceptr_t)(mm + 3), 0u, 3, c->stream) != hipSuccess)
-            rc = LIVO_E_HIP;
-        if (!rc) rc = launch_fe_minmax(d_src, N, stride, mm, c->stream);
-        if (!rc) rc = launch_fe_morton(d_src, N, stride, mm, morton_scale(), codes, iota, c->stream);
-        if (!rc) {
-            size_t tb = 0;
-            rc = prim_sort_pairs_u64(nullptr, &tb, codes, scodes, iota, perm, N, 60, c->stream);
-            if (!rc) rc = ensure_prim(c, tb);
-            tb = c->prim_bytes;
-            if (!rc) rc = prim_sort_pairs_u64(c->prim_tmp, &tb, codes, scodes, iota, perm, N, 60, c->stream);
-        }
-        if (!rc) rc = launch_fe_gather(d_src, N, stride, perm, s.pts, s.d_iperm, c->stream);
-        s.perm.resize((size_t)N);
-        if (!rc && (hipMemcpyAsync(s.d_perm, perm, (size_t)N * 4, hipMemcpyDeviceToDevice, c->stream) != hipSuccess ||
-                    hipMemcpyAsync(s.perm.data(), perm, (size_t)N * 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-                    hipMemsetAsync(s.nn, 0, (size_t)N * sizeof(NNRec), c->stream) != hipSuccess ||
-                    hipMemsetAsync(s.pstate, 0, (size_t)N, c->stream) != hipSuccess))
-            rc = LIVO_E_HIP;
+        const UpTarget U{c->stream, &c->up_tmp, &c->up_tmp_bytes, &c->prim_tmp, &c->prim_bytes};
+        if (!rc) rc = scan_build_on(U, d_src, stride, N, s);
         if (hipStreamSynchronize(c->stream) != hipSuccess && !rc) rc = LIVO_E_HIP;
         if (rc) {
             release_scan_buf(c, s);
@@ -2163,28 +2219,36 @@ static int scan_create_device(livo_ctx* c, const float* d_src, int stride, int64
     return LIVO_OK;
 }
 
+// The caller's points packed to x, y, z (a strided PointType array is read once).
+static void pack_xyz(const float* xyz, int64_t N, int64_t stride_bytes, float* out) {
+    const char* base = (const char*)xyz;
+    if (stride_bytes == (int64_t)(3 * sizeof(float))) {
+        std::memcpy(out, xyz, (size_t)N * 3 * sizeof(float));
+        return;
+    }
+    for (int64_t i = 0; i < N; i++) std::memcpy(out + 3 * i, base + i * stride_bytes, 3 * sizeof(float));
+}
+
 int livo_scan_upload(livo_ctx* c, const float* xyz, int64_t N, int64_t stride_bytes, int32_t* scan_id) {
     if (!c || !scan_id || N < 0 || (N > 0 && !xyz)) return LIVO_E_INVALID;
     if (N > (int64_t)0x7FFFFFFF - kBlock) return LIVO_E_RANGE;
     if (stride_bytes == 0) stride_bytes = 3 * sizeof(float);
     if (stride_bytes < (int64_t)(3 * sizeof(float))) return LIVO_E_INVALID;
     if (set_device(c)) return LIVO_E_HIP;
-    // the caller's points packed to x, y, z (a strided PointType array is
-    // read once), copied to HBM behind the upload scratch, then Morton-ordered
-    // on the device (scan_create_device: the same keys and stable order as a host sort)
+    // the caller's points packed to x, y, z, copied to HBM behind the upload
+    // scratch, then Morton-ordered on the device (scan_create_device)
     float* d_src = nullptr;
     if (N > 0) {
         const size_t off = (up_tmp_bytes(N) + 255) & ~(size_t)255;
         int rc = ensure_up_tmp(c, off + (size_t)N * 3 * sizeof(float));
         if (rc) return rc;
         d_src = (float*)((char*)c->up_tmp + off);
-        const char* base = (const char*)xyz;
         float* h = nullptr;
         const bool packed = stride_bytes == (int64_t)(3 * sizeof(float));
         if (!packed) {
             h = (float*)std::malloc((size_t)N * 3 * sizeof(float));
             if (!h) return LIVO_E_OOM;
-            for (int64_t i = 0; i < N; i++) std::memcpy(h + 3 * i, base + i * stride_bytes, 3 * sizeof(float));
+            pack_xyz(xyz, N, stride_bytes, h);
         }
         const hipError_t e = hipMemcpyAsync(d_src, packed ? xyz : h, (size_t)N * 3 * sizeof(float),
                                             hipMemcpyHostToDevice, c->stream);
@@ -2195,21 +2259,117 @@ int livo_scan_upload(livo_ctx* c, const float* xyz, int64_t N, int64_t stride_by
     return scan_create_device(c, d_src, 3, N, scan_id);
 }
 
-int livo_scan_release(livo_ctx* c, int32_t id) {
-    if (!c) return LIVO_E_INVALID;
-    if (any_inflight(c)) return LIVO_E_BUSY;  // submitted batches are collected first
-    if (id < 0 || id >= (int32_t)c->scans.size() || !c->scans[id].used) return LIVO_E_NOSCAN;
-    (void)hipSetDevice(c->device);
-    (void)hipStreamSynchronize(c->stream);
-    for (int k = 0; k < kMaxGroups - 1; k++)
-        if (c->xstream[k]) (void)hipStreamSynchronize(c->xstream[k]);
-    release_scan_buf(c, c->scans[id]);
+// livo_scan_upload without waiting: the points go through a pinned staging
+// buffer (the caller's array is free again on return) and are copied and
+// Morton-ordered on the context's upload stream, beside whatever the batch
+// lanes run; the scan's `ready` event gates its users (batch_enqueue waits for
+// it on the device, every other call through get_scan on the host).
+int livo_scan_upload_async(livo_ctx* c, const float* xyz, int64_t N, int64_t stride_bytes, int32_t* scan_id) {
+    if (!c || !scan_id || N < 0 || (N > 0 && !xyz)) return LIVO_E_INVALID;
+    if (N > (int64_t)0x7FFFFFFF - kBlock) return LIVO_E_RANGE;
+    if (stride_bytes == 0) stride_bytes = 3 * sizeof(float);
+    if (stride_bytes < (int64_t)(3 * sizeof(float))) return LIVO_E_INVALID;
+    if (N == 0) return livo_scan_upload(c, xyz, N, stride_bytes, scan_id);
+    if (set_device(c)) return LIVO_E_HIP;
+    if (!c->up_stream && hipStreamCreateWithFlags(&c->up_stream, hipStreamNonBlocking) != hipSuccess) {
+        c->up_stream = nullptr;
+        return LIVO_E_HIP;
+    }
+    const size_t off = (up_tmp_bytes(N) + 255) & ~(size_t)255, bytes = (size_t)N * 3 * sizeof(float);
+    if (off + bytes > c->aup_tmp_bytes) {  // (growing: the uploads queued on it finish first)
+        if (hipStreamSynchronize(c->up_stream) != hipSuccess) return LIVO_E_HIP;
+        const int rc = ensure_dev_bytes(&c->aup_tmp, &c->aup_tmp_bytes, off + bytes);
+        if (rc) return rc;
+    }
+    // a pinned staging buffer whose last copy is done (the ring's oldest)
+    livo_ctx::PinSlot& P = c->pin[c->pin_next];
+    c->pin_next = (c->pin_next + 1) % kPinRing;
+    if (P.inflight && hipEventSynchronize(P.copied) != hipSuccess) return LIVO_E_HIP;
+    P.inflight = false;
+    if (!P.copied && hipEventCreateWithFlags(&P.copied, hipEventDisableTiming) != hipSuccess) {
+        P.copied = nullptr;
+        return LIVO_E_HIP;
+    }
+    if (bytes > P.bytes) {
+        if (P.h) (void)hipHostFree(P.h);
+        P.h = nullptr;
+        P.bytes = 0;
+        if (hipHostMalloc((void**)&P.h, bytes, hipHostMallocDefault) != hipSuccess) {
+            P.h = nullptr;
+            return LIVO_E_OOM;
+        }
+        P.bytes = bytes;
+    }
+    pack_xyz(xyz, N, stride_bytes, P.h);
+    ScanBuf s;
+    int rc = alloc_scan_buf(c, s, N);
+    if (rc) return rc;
+    if (!s.ready && hipEventCreateWithFlags(&s.ready, hipEventDisableTiming) != hipSuccess) {
+        s.ready = nullptr;
+        release_scan_buf(c, s);
+        return LIVO_E_HIP;
+    }
+    float* d_src = (float*)((char*)c->aup_tmp + off);
+    if (hipMemcpyAsync(d_src, P.h, bytes, hipMemcpyHostToDevice, c->up_stream) != hipSuccess ||
+        hipEventRecord(P.copied, c->up_stream) != hipSuccess)
+        rc = LIVO_E_HIP;
+    P.inflight = rc == LIVO_OK;
+    const UpTarget U{c->up_stream, &c->aup_tmp, &c->aup_tmp_bytes, &c->aup_prim, &c->aup_prim_bytes};
+    if (!rc) rc = scan_build_on(U, d_src, 3, N, s);
+    if (!rc && hipEventRecord(s.ready, c->up_stream) != hipSuccess) rc = LIVO_E_HIP;
+    if (rc) {
+        (void)hipStreamSynchronize(c->up_stream);
+        release_scan_buf(c, s);
+        return rc;
+    }
+    s.pending = true;
+    *scan_id = register_scan(c, s);
     return LIVO_OK;
 }
 
-static ScanBuf* get_scan(livo_ctx* c, int32_t id) {
+int livo_scan_release(livo_ctx* c, int32_t id) {
+    if (!c) return LIVO_E_INVALID;
+    if (id < 0 || id >= (int32_t)c->scans.size() || !c->scans[id].used) return LIVO_E_NOSCAN;
+    // a scan of a submitted batch is released once that batch is collected; every
+    // other call that reads a scan returns only when its device work is done, so
+    // the buffers are idle once the scan's own upload is (no stream drain: the
+    // farm releases scans while the next batches run)
+    for (int l = 0; l < LIVO_MAX_INFLIGHT; l++)
+        if (c->lane[l].busy)
+            for (int32_t x : c->lane[l].ids)
+                if (x == id) return LIVO_E_BUSY;
+    (void)hipSetDevice(c->device);
+    ScanBuf& s = c->scans[id];
+    if (s.pending && hipEventSynchronize(s.ready) != hipSuccess) return LIVO_E_HIP;
+    s.pending = false;
+    release_scan_buf(c, s);
+    return LIVO_OK;
+}
+
+// A resident scan, its asynchronous upload finished (host wait); get_scan_q:
+// without the wait (batch_enqueue, which waits for it on the device).
+static ScanBuf* get_scan_q(livo_ctx* c, int32_t id) {
     if (id < 0 || id >= (int32_t)c->scans.size() || !c->scans[id].used) return nullptr;
     return &c->scans[id];
+}
+static ScanBuf* get_scan(livo_ctx* c, int32_t id) {
+    ScanBuf* s = get_scan_q(c, id);
+    if (s && s->pending) {
+        if (hipEventSynchronize(s->ready) != hipSuccess) return nullptr;
+        s->pending = false;
+    }
+    return s;
+}
+// The scan's stored -> caller order on the host (the per-point outputs), copied
+// from the device on first use.
+static int host_perm(ScanBuf* s) {
+    if ((int64_t)s->perm.size() == s->n) return LIVO_OK;
+    s->perm.resize((size_t)s->n);
+    if (s->n > 0 && hipMemcpy(s->perm.data(), s->d_perm, (size_t)s->n * 4, hipMemcpyDeviceToHost) != hipSuccess) {
+        s->perm.clear();
+        return LIVO_E_HIP;
+    }
+    return LIVO_OK;
 }
 
 int livo_scan_neighbors(livo_ctx* c, int32_t id, int32_t* idx, float* sqdist) {
@@ -2226,8 +2386,9 @@ int livo_scan_neighbors(livo_ctx* c, int32_t id, int32_t* idx, float* sqdist) {
         HIP_TRY(hipStreamSynchronize(c->stream));
         HIP_TRY(hipMemcpy(rec.data(), s->nn, (size_t)s->n * sizeof(NNRec), hipMemcpyDeviceToHost));
     }
+    if (host_perm(s)) return LIVO_E_HIP;
     for (int64_t j = 0; j < s->n; j++) {
-        const int64_t o = s->perm.empty() ? j : (int64_t)s->perm[(size_t)j];  // caller's point index
+        const int64_t o = (int64_t)s->perm[(size_t)j];  // caller's point index
         for (int k = 0; k < kNN; k++) {
             if (idx) idx[o * kNN + k] = rec[(size_t)j].idx[k];
             if (sqdist) sqdist[o * kNN + k] = rec[(size_t)j].p[k][3];
@@ -2347,6 +2508,7 @@ int livo_h_share(livo_ctx* c, int32_t id, const livo_state* state, int search_en
     if (effct) *effct = (int64_t)r[28];
     if (out && out->visits) *out->visits = (int64_t)hs.visits[0];
     // per-point outputs come back in the caller's point order (stored order is Morton)
+    if (host_perm(s)) return LIVO_E_HIP;
     for (int64_t k = 0; k < N; k++) {
         const int64_t i = s->perm[k];
         if (!h_nv.empty()) std::memcpy(out->normvec + 4 * i, &h_nv[4 * k], 16);
@@ -2376,7 +2538,7 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
     if (!map_ready(c)) return LIVO_E_NOMAP;
     if (model == kModelIkfom && c->backend != LIVO_BACKEND_IKDTREE) return LIVO_E_INVALID;  // ikd-Tree h-model only
     for (int32_t b = 0; b < n; b++)
-        if (!get_scan(c, ids[b])) return LIVO_E_NOSCAN;
+        if (!get_scan_q(c, ids[b])) return LIVO_E_NOSCAN;
     {
         // a scan's neighbour records, plane cache and partials are per scan: the
         // same id twice in one batch would have two updates write them concurrently
@@ -2421,7 +2583,7 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
     const bool wb = fused && lm && B.h_lm_dev && c->slot_wb;
     int64_t total_n = 0;
     for (int32_t b = 0; b < n; b++) {
-        ScanBuf* s = get_scan(c, ids[b]);
+        ScanBuf* s = get_scan_q(c, ids[b]);
         if (model == kModelIkfom) {
             init_slot_ik(hslot(b), ik_states[b], max_iter);
         } else {
@@ -2433,9 +2595,15 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
     }
     rc = ensure_replay(c, total_n);
     if (rc) return rc;
+    // scans whose asynchronous upload may still run: the lane's stream 0 waits for
+    // them on the device (every group forks from it after the staging copy)
+    for (int32_t b = 0; b < n; b++) {
+        const ScanBuf* s = get_scan_q(c, ids[b]);
+        if (s->pending) HIP_TRY(hipStreamWaitEvent(B.st[0], s->ready, 0));
+    }
     if (model == kModelIkfom)  // its searches rewrite the neighbours without refitting the cached planes
         for (int32_t b = 0; b < n; b++) {
-            ScanBuf* s = get_scan(c, ids[b]);
+            ScanBuf* s = get_scan_q(c, ids[b]);
             if (s->n > 0) HIP_TRY(hipMemsetAsync(s->pstate, 0, (size_t)s->n, B.st[0]));
         }
     const bool prof = sync && L == 0 && c->profiling && c->events_ready;  // 1: first-search events only
@@ -2496,7 +2664,7 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
         g[gi].off = off;
         g[gi].st = B.st[gi];
         for (int32_t b = g[gi].first; b < g[gi].first + g[gi].count; b++) {
-            const ScanBuf* s = get_scan(c, ids[b]);
+            const ScanBuf* s = get_scan_q(c, ids[b]);
             g[gi].max_nblk = std::max(g[gi].max_nblk, (int)s->nblk);
             g[gi].max_n = std::max<int64_t>(g[gi].max_n, s->n);
             off += s->n;
@@ -2545,11 +2713,9 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
                                       : launch_hshare(hp[gi], g[gi].count, g[gi].max_nblk, e == 0, st);
             if (rc) return rc;
             if (!lm) {
-                // IKFoM: the measurement-free part of the solve (k_ik_prep), then the
-                // gain (k_solve_ik); k_ik_prep on a side stream beside the search and
-                // plane pass measured no better (5.1k vs 5.2k updates/s, r04_ab_groups.txt)
-                rc = launch_ik_prep(hp[gi], g[gi].count, st);
-                if (!rc) rc = launch_solve_ik(hp[gi], g[gi].count, st);
+                // IKFoM: the reduction, the measurement-free part of the update and
+                // the gain (k_solve_ik)
+                rc = launch_solve_ik(hp[gi], g[gi].count, st);
                 if (rc) return rc;
             }
         }
@@ -2998,8 +3164,10 @@ int livo_map_incremental(livo_ctx* c, int32_t id, const livo_state* state, doubl
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
     const int64_t total = (int64_t)tail[1] + tail[2], n_add = tail[0];
-    if (cat)
+    if (cat) {
+        if (host_perm(s)) return LIVO_E_HIP;
         for (int64_t k = 0; k < N; k++) cat[s->perm[(size_t)k]] = hcat[(size_t)k];
+    }
     rc = ivox_add_dev(c, total);
     if (rc) return rc;
     if (counts) {

@@ -224,7 +224,6 @@ constexpr int kIkDim = LIVO_IKFOM_DOF;  // 23
 constexpr int kIkFewRows = kIkDim - 1;  // below 23 effective points the gain is formed in measurement space
 constexpr int kIkCols = 192;            // doubles per IKFoM block partial: 92 sums, then their 92 compensations
 constexpr int kIkCompOff = 96;          // offset of the compensation terms in a partial
-constexpr int kIkPrep = 2 * kIkDim * kIkDim + 2 * kIkDim;  // IKFoM per-scan prep: P_, (P_ / R)^-1, dx, dx_new
 constexpr int kIkUsed = 92;             // 78 HTH upper-tri + 12 HTh + residual sum + count
 
 // IKFoM update state (esekfom.hpp:1619-1928): x_, x_propagated (its cov is
@@ -277,7 +276,6 @@ struct HsJob {
     uint8_t* pstate;      // N: 0 not fitted since the last search, 1 no plane, 2 plane
     double* ikrows;       // IKFoM: nblk x kIkFewRows x 13 effective rows (h_x row, h) per block
     uint32_t* ikcnt;      // IKFoM: nblk: effective rows of the block (capped at kIkFewRows + 1)
-    double* ikprep;       // IKFoM: kIkPrep doubles: the evaluation's corrected P_, (P_ / R)^-1, dx, dx_new (k_ik_prep)
     uint4* host_slot;     // fused batches: the slot's host-mapped staging copy, written by the solve that
                           // stops the scan (nullptr: the batch copies the slots back itself)
     int32_t n;
@@ -388,7 +386,6 @@ int launch_hshare(const HsParams& p, int n_jobs, int max_nblk, bool first, void*
 #endif
 constexpr int kEvalBlock = LIVO_EVAL_BLOCK;  // threads (points) per block of k_iekf_eval
 int launch_iekf_eval(const KnnParams& kp, const HsParams& hp, int n_jobs, int64_t max_n, bool first, void* stream);
-int launch_ik_prep(const HsParams& p, int n_jobs, void* stream);
 int launch_solve_ik(const HsParams& p, int n_jobs, void* stream);
 int launch_copy_words(const void* src, void* dst, size_t bytes, void* stream);  // 16-B aligned, bytes % 16 == 0
 // IKFoM plane pass (12-wide rows) with the manifold update in each scan's last block.

@@ -3235,11 +3235,11 @@ struct IkSolveLds {
 };
 constexpr int kIkRow = 15;  // 12 row + h + |pd2| + keep
 
-// One wave, the part of esekfom.hpp:1638-1787 that does not depend on this
+// One wave, the part of esekfom.hpp:1638-1697 that does not depend on this
 // evaluation's measurements: dx = x_ boxminus x_propagated, P_ = P_propagated
-// with the SO3 / S2 corrections of dx_new and P_ (:1638-1697), and (P_ / R)^-1
-// of the information-form gain (:1775-1777).  k_ik_prep runs it on its own
-// stream beside the evaluation's search and plane pass; k_solve_ik loads it.
+// with the SO3 / S2 corrections of dx_new and P_.  k_solve_ik runs it on its
+// last wave beside the other waves' reduction of the block partials.  The
+// information-form gain needs no (P_ / R)^-1 (ik_solve: Woodbury).
 __device__ void ik_prep(const IekfSlot* slot, IkSolveLds& S, const int lane, const double R) {
     const IkBlock& K = slot->ik;
     constexpr int N = kIkDim;
@@ -3289,23 +3289,11 @@ __device__ void ik_prep(const IekfSlot* slot, IkSolveLds& S, const int lane, con
         WAVE_SYNC();
     }
     SOLVE_MARK(4);
-    {
-        double A[N];
-        for (int j = 0; j < N; j++) A[j] = lane < N ? S.P[lane * N + j] / R : 0.0;
-        wave_lu_to_lds<N>(A, lane, S.LU, S.piv);
-        WAVE_SYNC();
-        if (lane < N) {
-            double y[N];
-            lds_lu_column<N>(S.LU, S.piv, lane, y);
-            for (int i = 0; i < N; i++) S.Pinv[i * N + lane] = y[i];
-        }
-        WAVE_SYNC();
-    }
-    SOLVE_MARK(5);
+    (void)R;
 }
 
 // One wave: esekfom.hpp:1701-1921 from the reduced sums in S.sum and the
-// evaluation's prep (ik_prep: S.dx, S.dxn, S.P, S.Pinv = (P_ / R)^-1).
+// evaluation's prep (ik_prep: S.dx, S.dxn, S.P).
 __device__ void ik_solve(IekfSlot* slot, const HsJob& job, IkSolveLds& S, const int lane, const double R) {
     IkBlock& K = slot->ik;
     const IekfCtrl ctrl0 = slot->ctrl;
@@ -3370,34 +3358,51 @@ __device__ void ik_solve(IekfSlot* slot, const HsJob& job, IkSolveLds& S, const 
         }
         WAVE_SYNC();
     } else {
-    // gain, information form (:1775-1787): P_temp = (P_/R)^-1 + HTH, P_inv = P_temp^-1
-    {
-        double A[N];
-        for (int t = lane; t < 144; t += 64) {
-            const int r = t / 12, c = t % 12;
-            const int a = r < c ? r : c, bb = r < c ? c : r;
-            S.Pinv[r * N + c] += S.sum[a * 12 - (a * (a - 1)) / 2 + (bb - a)];
-        }
-        WAVE_SYNC();
-        for (int j = 0; j < N; j++) A[j] = lane < N ? S.Pinv[lane * N + j] : 0.0;
-        wave_lu_to_lds<N>(A, lane, S.LU, S.piv);
-        WAVE_SYNC();
-        if (lane < N) {
-            double y[N];
-            lds_lu_column<N>(S.LU, S.piv, lane, y);
-            for (int i = 0; i < N; i++) S.Pinv[i * N + lane] = y[i];
-        }
-        WAVE_SYNC();
+    // gain, information form (:1775-1787): K = P_temp^-1, P_temp = (P_/R)^-1 + HTH,
+    // of which only K(:, 0:12) is used (K_h = K HTh, K_x = K HTH: HTH is zero
+    // outside its 12 x 12 block C).  With A = P_ / R and U = [I12; 0],
+    // (A^-1 + U C U^T) A U (I12 + C A11)^-1 = U, so
+    //   K(:, 0:12) = A(:, 0:12) (I12 + C A(0:12, 0:12))^-1
+    // -- one 12 x 12 LU instead of two 23 x 23 inversions (the 18-dim solve's
+    // DESIGN.md §4.3 form); within 1e-5 of the oracle's inversions per step.
+    double* const M = S.Pinv;             // I12 + C A11, then its LU's inverse at M + 144
+    double* const Minv = S.Pinv + 144;
+    double* const K12 = S.L;              // K(:, 0:12), 23 x 12 (S.L is rebuilt for the covariance)
+    for (int t = lane; t < 144; t += 64) {
+        const int r = t / 12, c = t % 12;
+        double acc = hth(r, 0) * (S.P[0 * N + c] / R);
+        for (int k = 1; k < 12; k++) acc = acc + hth(r, k) * (S.P[k * N + c] / R);
+        M[t] = (r == c ? 1.0 : 0.0) + acc;
     }
+    WAVE_SYNC();
+    {
+        double A[12];
+        for (int j = 0; j < 12; j++) A[j] = lane < 12 ? M[lane * 12 + j] : 0.0;
+        wave_lu_to_lds<12>(A, lane, S.LU, S.piv);
+    }
+    WAVE_SYNC();
+    if (lane < 12) {
+        double y[12];
+        lds_lu_column<12>(S.LU, S.piv, lane, y);
+        for (int i = 0; i < 12; i++) Minv[i * 12 + lane] = y[i];
+    }
+    WAVE_SYNC();
+    for (int t = lane; t < N * 12; t += 64) {
+        const int r = t / 12, c = t % 12;
+        double acc = (S.P[r * N + 0] / R) * Minv[0 * 12 + c];
+        for (int k = 1; k < 12; k++) acc = acc + (S.P[r * N + k] / R) * Minv[k * 12 + c];
+        K12[t] = acc;
+    }
+    WAVE_SYNC();
     SOLVE_MARK(6);
     if (lane < N) {
         const int r = lane;
-        double kh = S.Pinv[r * N] * S.sum[78];
-        for (int c = 1; c < 12; c++) kh = kh + S.Pinv[r * N + c] * S.sum[78 + c];
+        double kh = K12[r * 12] * S.sum[78];
+        for (int c = 1; c < 12; c++) kh = kh + K12[r * 12 + c] * S.sum[78 + c];
         S.Kh[r] = kh;
         for (int c = 0; c < 12; c++) {
-            double a2 = S.Pinv[r * N] * hth(0, c);
-            for (int k = 1; k < 12; k++) a2 = a2 + S.Pinv[r * N + k] * hth(k, c);
+            double a2 = K12[r * 12] * hth(0, c);
+            for (int k = 1; k < 12; k++) a2 = a2 + K12[r * 12 + k] * hth(k, c);
             S.Kx[r * 12 + c] = a2;
         }
     }
@@ -3723,6 +3728,9 @@ __global__ __launch_bounds__(64 * kIkSolveWaves) void k_solve_ik(HsParams P) {
         wsum[g][0][c] = sc;
         wsum[g][1][c] = cc;
     }
+    // the evaluation's measurement-free part (boxminus, SO3 / S2 corrections) on
+    // the last wave, beside the others' reduction
+    if (wave == kIkSolveWaves - 1) ik_prep(slot, S, lane, P.lpc);
     __syncthreads();
     SOLVE_MARK(1);
     if (wave > 0) return;
@@ -3751,40 +3759,7 @@ __global__ __launch_bounds__(64 * kIkSolveWaves) void k_solve_ik(HsParams P) {
     }
     WAVE_SYNC();
     SOLVE_MARK(2);
-    {  // the evaluation's prep (k_ik_prep, stream-ordered before this launch)
-        const double* src = job.ikprep;
-        for (int t = lane; t < kIkDim * kIkDim; t += 64) {
-            S.P[t] = src[t];
-            S.Pinv[t] = src[kIkDim * kIkDim + t];
-        }
-        if (lane < kIkDim) {
-            S.dx[lane] = src[2 * kIkDim * kIkDim + lane];
-            S.dxn[lane] = src[2 * kIkDim * kIkDim + kIkDim + lane];
-        }
-    }
-    WAVE_SYNC();
     ik_solve(slot, job, S, lane, P.lpc);
-}
-
-// One wave per scan: ik_prep of the scan's current estimate into job.ikprep.
-// Launched in-line on the group's stream right before k_solve_ik (a side-stream
-// launch beside the search and plane pass measured no faster and was dropped).
-__global__ __launch_bounds__(64) void k_ik_prep(HsParams P) {
-    __shared__ IkSolveLds S;
-    const HsJob job = P.jobs[blockIdx.x];
-    const IekfSlot* slot = job.slot;
-    const int lane = threadIdx.x;
-    if (slot->ctrl.stop) return;  // block-uniform
-    ik_prep(slot, S, lane, P.lpc);
-    double* dst = job.ikprep;
-    for (int t = lane; t < kIkDim * kIkDim; t += 64) {
-        dst[t] = S.P[t];
-        dst[kIkDim * kIkDim + t] = S.Pinv[t];
-    }
-    if (lane < kIkDim) {
-        dst[2 * kIkDim * kIkDim + lane] = S.dx[lane];
-        dst[2 * kIkDim * kIkDim + kIkDim + lane] = S.dxn[lane];
-    }
 }
 
 __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
@@ -4022,14 +3997,7 @@ int launch_hshare_ik(const HsParams& p, int n_jobs, int max_nblk, bool first, vo
         hipLaunchKernelGGL(k_hshare_ik<false>, grid, block, 0, (hipStream_t)stream, p);
     if (hipGetLastError() != hipSuccess) return LIVO_E_HIP;
     if (!p.solve) return LIVO_OK;
-    const int rc = launch_ik_prep(p, n_jobs, stream);
-    return rc ? rc : launch_solve_ik(p, n_jobs, stream);
-}
-
-int launch_ik_prep(const HsParams& p, int n_jobs, void* stream) {
-    if (n_jobs <= 0) return LIVO_OK;
-    hipLaunchKernelGGL(k_ik_prep, dim3(n_jobs), dim3(64), 0, (hipStream_t)stream, p);
-    return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+    return launch_solve_ik(p, n_jobs, stream);
 }
 
 int launch_solve_ik(const HsParams& p, int n_jobs, void* stream) {

@@ -7,12 +7,12 @@
 //   k_vio_iter    one iteration: one visual point per thread -- projection
 //                 (vikit PinholeCamera::world2cam), dpi (:90-100), the
 //                 patch_size^2 bilinear residuals and their 6-wide Jacobian
-//                 rows (:818-850), HᵀH / Hᵀz block partials; the last block
-//                 then sums the patch errors in point order (float, as the
-//                 reference's `error += patch_error`), reduces the partials in
-//                 block order and, on one wave, runs the update: (cov /
-//                 img_point_cov)^-1 once, K1 = (HᵀH + that)^-1 (columns 0..5,
-//                 the only ones read), G, solution, boxplus, convergence, or
+//                 rows (:818-850), HᵀH / Hᵀz block partials and patch errors.
+//   k_vio_solve   the iteration's update, one block: the patch errors summed
+//                 in point order (float, as the reference's `error +=
+//                 patch_error`) beside the partials' reduction in block order
+//                 and the gain K1(:, 0:6) of (HᵀH + (cov / img_point_cov)^-1)^-1
+//                 by one 6x6 LU, G, solution; then boxplus and convergence, or
 //                 the revert when the error grew (:855-891).
 //   k_vio_end     ComputeJ's covariance update cov -= G cov (:975-978).
 // Control stays on the device (VioCtrl): every launch of a finished level
@@ -20,6 +20,8 @@
 // -ffp-contract=off, the reference's float / double expression order.
 #include <hip/hip_runtime.h>
 #include <math.h>
+
+#include <algorithm>
 
 #include "device_common.h"
 #include "device_linalg.h"
@@ -63,112 +65,133 @@ __device__ __forceinline__ void row3_mat(const double* r, const double* M, doubl
     for (int k = 0; k < 3; k++) o[k] = (r[0] * M[0 * 3 + k] + r[1] * M[1 * 3 + k]) + r[2] * M[2 * 3 + k];
 }
 
-struct VioLds {
-    double wsum[4][32];
+// LDS of k_vio_solve (the patch errors are staged in dynamic LDS behind it).
+struct VioSolveLds {
     double sum[32];
-    double Pinv[kDim * kDim];
-    double LU[kDim * kDim];
-    double K1[kDim * 6];
-    double HTH[36];
+    double A[kDim * 6];   // (cov / img_point_cov)(:, 0:6)
+    double C[36];         // H_T_H(0:6, 0:6)
+    double M[36];         // I6 + C A(0:6, 0:6)
+    double LU[36];
+    double Minv[36];
+    double K1[kDim * 6];  // K1(:, 0:6)
+    double G6[kDim * 6];
     double vec[kDim];
     double sol[kDim];
-    int piv[kDim];
+    int piv[6];
     float error;
-    int last;
 };
 
-// The update of the last block (one wave): lidar_selection.cpp:851-891.
-__device__ void vio_solve(const VioParams& P, VioLds& L, const int lane) {
-    VioSlot* slot = P.slot;
-    const int pst = P.ps * P.ps;
-    // error = sum of patch errors in point order (float), / n_meas
-    if (lane == 0) {
-        float err = 0.0f;
-        for (int i = 0; i < P.n; i++) err += P.perr[i];
-        const int n_meas = P.n * pst;
-        L.error = err / n_meas;
-        slot->ctrl.n_meas = n_meas;
+// The gain and the solution of one iteration (lidar_selection.cpp:855-866) on
+// one wave, from the reduced sums: K1 = (H_T_H + (cov / img_point_cov)^-1)^-1
+// is needed only in its columns 0..5 and H_T_H is zero outside its 6x6 block
+// C, so with A = cov / img_point_cov, K1(:, 0:6) = A(:, 0:6) (I6 + C A66)^-1
+// (livo_kernels.hip solve_scan's form: one 6x6 LU instead of two 18x18
+// inversions); G(:, 0:6) = K1(:, 0:6) C, solution = -K1 Hᵀz + vec - G vec(0:6).
+__device__ void vio_gain(const VioSlot* slot, VioSolveLds& L, const int lane) {
+    if (lane < 36) {
+        const int r = lane / 6, c = lane % 6;
+        const int a = r < c ? r : c, b = r < c ? c : r;
+        L.C[lane] = L.sum[a * 6 - (a * (a - 1)) / 2 + (b - a)];
     }
-    // HᵀH / Hᵀz: the block partials summed in block order
-    if (lane < 27) {
-        double v = P.partial[lane];
-        for (int b = 1; b < P.nblk; b++) v = v + P.partial[(size_t)b * kVioCols + lane];
-        L.sum[lane] = v;
+    if (lane == 0) state_minus_d(slot->prior, slot->state, L.vec);
+    WAVE_SYNC();
+    if (lane < 36) {
+        const int r = lane / 6, c = lane % 6;
+        double m = L.C[r * 6 + 0] * L.A[0 * 6 + c];
+#pragma unroll
+        for (int k = 1; k < 6; k++) m = m + L.C[r * 6 + k] * L.A[k * 6 + c];
+        L.M[lane] = (r == c ? 1.0 : 0.0) + m;
     }
     WAVE_SYNC();
+    {
+        double Ar[6];
+#pragma unroll
+        for (int j = 0; j < 6; j++) Ar[j] = lane < 6 ? L.M[lane * 6 + j] : 0.0;
+        wave_lu_to_lds<6>(Ar, lane, L.LU, L.piv);
+    }
+    WAVE_SYNC();
+    if (lane < 6) {
+        double y[6];
+        lds_lu_column<6>(L.LU, L.piv, lane, y);
+#pragma unroll
+        for (int i = 0; i < 6; i++) L.Minv[i * 6 + lane] = y[i];
+    }
+    WAVE_SYNC();
+    for (int t = lane; t < kDim * 6; t += 64) {
+        const int r = t / 6, c = t % 6;
+        double k1 = L.A[r * 6 + 0] * L.Minv[0 * 6 + c];
+#pragma unroll
+        for (int k = 1; k < 6; k++) k1 = k1 + L.A[r * 6 + k] * L.Minv[k * 6 + c];
+        L.K1[t] = k1;
+    }
+    WAVE_SYNC();
+    for (int t = lane; t < kDim * 6; t += 64) {
+        const int i = t / 6, j = t % 6;
+        double g = L.K1[i * 6 + 0] * L.C[0 * 6 + j];
+#pragma unroll
+        for (int l = 1; l < 6; l++) g = g + L.K1[i * 6 + l] * L.C[l * 6 + j];
+        L.G6[t] = g;
+    }
+    WAVE_SYNC();
+    if (lane < kDim) {
+        const int i = lane;
+        double kz = L.K1[i * 6 + 0] * L.sum[21 + 0];
+#pragma unroll
+        for (int l = 1; l < 6; l++) kz = kz + L.K1[i * 6 + l] * L.sum[21 + l];
+        double g = L.G6[i * 6 + 0] * L.vec[0];
+#pragma unroll
+        for (int l = 1; l < 6; l++) g = g + L.G6[i * 6 + l] * L.vec[l];
+        L.sol[i] = (-kz + L.vec[i]) - g;
+    }
+}
+
+// One iteration's update (lidar_selection.cpp:851-891), one block after the
+// iteration's k_vio_iter: the HᵀH / Hᵀz partials in block order (wave 0), the
+// gain and solution (wave 1) beside the patch errors' float sum in point order
+// (the reference's `error += patch_error`, serial by definition: thread 0 over
+// the errors staged in LDS, `chunk` at a time), then the accept / revert.
+__global__ __launch_bounds__(256) void k_vio_solve(VioParams P, int chunk) {
+    __shared__ VioSolveLds L;
+    extern __shared__ float s_err[];  // chunk floats
+    VioSlot* slot = P.slot;
+    if (slot->ctrl.end) return;  // block-uniform
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int n = P.n, pst = P.ps * P.ps;
+    if (tid < 27) {
+        double v = P.partial[tid];
+        for (int b = 1; b < P.nblk; b++) v = v + P.partial[(size_t)b * kVioCols + tid];
+        L.sum[tid] = v;
+    }
+    for (int t = tid; t < kDim * 6; t += 256) L.A[t] = slot->state.cov[(t / 6) * kDim + t % 6] / P.img_cov;
+    float err = 0.0f;
+    for (int base = 0; base < n; base += chunk) {
+        const int cnt = min(chunk, n - base);
+        for (int t = tid; t < cnt; t += 256) s_err[t] = P.perr[base + t];
+        __syncthreads();
+        if (base == 0 && w == 1) vio_gain(slot, L, lane);
+        if (tid == 0) {
+            const float4* e4 = reinterpret_cast<const float4*>(s_err);
+            int t = 0;
+            for (; t + 4 <= cnt; t += 4) {
+                const float4 v = e4[t >> 2];
+                err += v.x;
+                err += v.y;
+                err += v.z;
+                err += v.w;
+            }
+            for (; t < cnt; t++) err += s_err[t];
+        }
+        __syncthreads();
+    }
+    if (w > 0) return;
+    const int n_meas = n * pst;
+    const float error = __shfl(err, 0) / n_meas;
     const int li = 2 - slot->ctrl.level;
-    const float error = L.error;
     bool end = false;
     if (error <= slot->ctrl.last_error) {
         for (int t = lane; t < (int)(sizeof(livo_state) / sizeof(double)); t += 64)
             reinterpret_cast<double*>(&slot->old_state)[t] = reinterpret_cast<const double*>(&slot->state)[t];
-        for (int t = lane; t < 36; t += 64) {
-            const int r = t / 6, c = t % 6;
-            const int a = r < c ? r : c, b = r < c ? c : r;
-            L.HTH[t] = L.sum[a * 6 - (a * (a - 1)) / 2 + (b - a)];
-        }
-        const bool row = lane < kDim;
-        // (cov / img_point_cov)^-1, once: the covariance is fixed inside ComputeJ
-        if (!slot->ctrl.pinv_ready) {
-            double A[kDim];
-#pragma unroll
-            for (int j = 0; j < kDim; j++) A[j] = row ? slot->state.cov[lane * kDim + j] / P.img_cov : 0.0;
-            wave_lu_to_lds<kDim>(A, lane, L.LU, L.piv);
-            WAVE_SYNC();
-            if (lane < kDim) {
-                double y[kDim];
-                lds_lu_column<kDim>(L.LU, L.piv, lane, y);
-#pragma unroll
-                for (int i = 0; i < kDim; i++) L.Pinv[i * kDim + lane] = y[i];
-            }
-            WAVE_SYNC();
-            for (int t = lane; t < kDim * kDim; t += 64) slot->Pinv[t] = L.Pinv[t];
-        } else {
-            for (int t = lane; t < kDim * kDim; t += 64) L.Pinv[t] = slot->Pinv[t];
-        }
-        WAVE_SYNC();
-        // K1 = (H_T_H + Pinv)^-1, columns 0..5
-        {
-            double A[kDim];
-#pragma unroll
-            for (int j = 0; j < kDim; j++)
-                A[j] = row ? (((lane < 6 && j < 6) ? L.HTH[lane * 6 + j] : 0.0) + L.Pinv[lane * kDim + j]) : 0.0;
-            if (lane < 6) {
-                // HTH6 + Pinv in the oracle's order: A = Pinv, then the 6x6 block = HTH + Pinv
-#pragma unroll
-                for (int j = 0; j < 6; j++) A[j] = L.HTH[lane * 6 + j] + L.Pinv[lane * kDim + j];
-            }
-            wave_lu_to_lds<kDim>(A, lane, L.LU, L.piv);
-            WAVE_SYNC();
-            if (lane < 6) {
-                double y[kDim];
-                lds_lu_column<kDim>(L.LU, L.piv, lane, y);
-#pragma unroll
-                for (int i = 0; i < kDim; i++) L.K1[i * 6 + lane] = y[i];
-            }
-            WAVE_SYNC();
-        }
-        // G(:, 0:6) = K1(:, 0:6) HTH6
-        for (int t = lane; t < kDim * 6; t += 64) {
-            const int i = t / 6, j = t % 6;
-            double g = L.K1[i * 6 + 0] * L.HTH[0 * 6 + j];
-#pragma unroll
-            for (int l = 1; l < 6; l++) g = g + L.K1[i * 6 + l] * L.HTH[l * 6 + j];
-            slot->G6[t] = g;
-        }
-        if (lane == 0) state_minus_d(slot->prior, slot->state, L.vec);
-        WAVE_SYNC();
-        // solution = -K1(:,0:6) Hᵀz + vec - G(:,0:6) vec(0:6)
-        if (row) {
-            const int i = lane;
-            double kz = L.K1[i * 6 + 0] * L.sum[21 + 0];
-#pragma unroll
-            for (int l = 1; l < 6; l++) kz = kz + L.K1[i * 6 + l] * L.sum[21 + l];
-            double g = slot->G6[i * 6 + 0] * L.vec[0];
-#pragma unroll
-            for (int l = 1; l < 6; l++) g = g + slot->G6[i * 6 + l] * L.vec[l];
-            L.sol[i] = (-kz + L.vec[i]) - g;
-        }
+        for (int t = lane; t < kDim * 6; t += 64) slot->G6[t] = L.G6[t];
         WAVE_SYNC();
         if (lane == 0) {
             double sol[kDim];
@@ -189,6 +212,7 @@ __device__ void vio_solve(const VioParams& P, VioLds& L, const int lane) {
     }
     WAVE_SYNC();
     if (lane == 0) {
+        slot->ctrl.n_meas = n_meas;
         slot->ctrl.iters[li]++;
         slot->ctrl.iteration++;
         slot->ctrl.end = (end || slot->ctrl.iteration >= P.max_iter) ? 1 : 0;
@@ -197,7 +221,6 @@ __device__ void vio_solve(const VioParams& P, VioLds& L, const int lane) {
 }
 
 __global__ __launch_bounds__(256) void k_vio_iter(VioParams P) {
-    __shared__ VioLds L;
     VioSlot* slot = P.slot;
     if (slot->ctrl.end) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -275,29 +298,20 @@ __global__ __launch_bounds__(256) void k_vio_iter(VioParams P) {
         P.perr[i] = patch_error;
         if (oof) atomicAdd(&slot->ctrl.oof, (unsigned long long)oof);
     }
-    // deterministic block partial: lanes (xor tree), then waves in order
+    // deterministic block partial: lanes (xor tree), then waves in order; the
+    // iteration's update runs in k_vio_solve behind this launch
+    __shared__ double wsum[4][32];
 #pragma unroll
     for (int k = 0; k < 27; k++) {
         const double v = wave_sum(acc[k]);
-        if (lane == 0) L.wsum[w][k] = v;
+        if (lane == 0) wsum[w][k] = v;
     }
     __syncthreads();
     if (tid < 27) {
-        double v = L.wsum[0][tid];
-        for (int ww = 1; ww < 4; ww++) v = v + L.wsum[ww][tid];
+        double v = wsum[0][tid];
+        for (int ww = 1; ww < 4; ww++) v = v + wsum[ww][tid];
         P.partial[(size_t)blockIdx.x * kVioCols + tid] = v;
     }
-    // the last block to finish runs the update
-    __threadfence();
-    __syncthreads();
-    if (tid == 0)
-        L.last = __hip_atomic_fetch_add(&slot->ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
-                 (unsigned)(P.nblk - 1);
-    __syncthreads();
-    if (!L.last) return;
-    __threadfence();
-    if (w == 0) vio_solve(P, L, lane);
-    if (tid == 0) slot->ticket = 0u;
 }
 
 // ComputeJ's covariance update (:975-978): if the last level's error < 1e10,
@@ -325,6 +339,10 @@ int launch_vio_begin(const VioParams& p, int level, void* stream) {
 int launch_vio_iter(const VioParams& p, void* stream) {
     if (p.n <= 0) return LIVO_OK;
     hipLaunchKernelGGL(k_vio_iter, dim3((unsigned)p.nblk), dim3(256), 0, (hipStream_t)stream, p);
+    if (hipGetLastError() != hipSuccess) return LIVO_E_HIP;
+    // the errors staged 24k at a time (96 KB of LDS; one workgroup may take 160 KB)
+    const int chunk = (int)std::min<int64_t>(((int64_t)p.n + 3) & ~(int64_t)3, 24576);
+    hipLaunchKernelGGL(k_vio_solve, dim3(1), dim3(256), (size_t)chunk * sizeof(float), (hipStream_t)stream, p, chunk);
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 int launch_vio_end(const VioParams& p, void* stream) {

@@ -167,6 +167,7 @@ SIGNATURES = {
     "livo_map_get_info": (C.c_int, [_P, C.POINTER(MapInfo)]),
     "livo_knn": (C.c_int, [_P, _P, C.c_int64, C.c_int32, _P, _P]),
     "livo_scan_upload": (C.c_int, [_P, _P, C.c_int64, C.c_int64, C.POINTER(C.c_int32)]),
+    "livo_scan_upload_async": (C.c_int, [_P, _P, C.c_int64, C.c_int64, C.POINTER(C.c_int32)]),
     "livo_scan_release": (C.c_int, [_P, C.c_int32]),
     "livo_scan_neighbors": (C.c_int, [_P, C.c_int32, _P, _P]),
     "livo_h_share": (C.c_int, [_P, C.c_int32, C.POINTER(State), C.c_int, _P, _P, C.POINTER(C.c_int64),
@@ -328,6 +329,17 @@ class Context:
         sid = C.c_int32()
         _check("livo_scan_upload", self._L.livo_scan_upload(self.h, _ptr(xyz), xyz.shape[0], xyz.shape[1] * 4,
                                                             C.byref(sid)))
+        self.scans[sid.value] = xyz.shape[0]
+        return sid.value
+
+    def scan_upload_async(self, xyz: np.ndarray) -> int:
+        """livo_scan_upload_async: returns once the points are staged; the copy and
+        Morton sort run on the context's upload stream (batches wait for them)."""
+        xyz = np.ascontiguousarray(xyz, np.float32)
+        assert xyz.ndim == 2 and xyz.shape[1] >= 3
+        sid = C.c_int32()
+        _check("livo_scan_upload_async",
+               self._L.livo_scan_upload_async(self.h, _ptr(xyz), xyz.shape[0], xyz.shape[1] * 4, C.byref(sid)))
         self.scans[sid.value] = xyz.shape[0]
         return sid.value
 

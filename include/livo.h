@@ -55,7 +55,7 @@ extern "C" {
  * 4: livo_timings grew the per-evaluation fields (eval_ms ... gap_ms), LIVO_E_BUSY
  *    and the submit / wait pair were added (round 3); a binary built against 3
  *    passes a smaller livo_timings. */
-#define LIVO_ABI_VERSION 5
+#define LIVO_ABI_VERSION 6
 #define LIVO_DIM_STATE 18        /* DIM_STATE, include/common_lib.h:32 */
 #define LIVO_NUM_MATCH_POINTS 5  /* NUM_MATCH_POINTS, include/common_lib.h:37 */
 #define LIVO_MAX_EVALS 16        /* max h_share/solve evaluations per scan update */
@@ -184,6 +184,15 @@ int livo_knn(livo_ctx* ctx, const float* q_xyz, int64_t n, int32_t k, int32_t* i
 
 /* Copy a body-frame scan (feats_down_body) to HBM; it stays resident until released. */
 int livo_scan_upload(livo_ctx* ctx, const float* xyz, int64_t N, int64_t stride_bytes, int32_t* scan_id);
+/* livo_scan_upload without waiting for the device: the points are packed into a
+ * pinned staging buffer (xyz is free again on return), then copied and ordered
+ * on the context's upload stream beside the batches in flight.  A batch using
+ * the scan waits for that on the device; any other call on it, on the host.
+ * (The reference hands each frame's feats_down_body to h_share_model,
+ * src/laser_mapping.cpp:129-131: the upload of frame k+1 can run under frame k.) */
+int livo_scan_upload_async(livo_ctx* ctx, const float* xyz, int64_t N, int64_t stride_bytes, int32_t* scan_id);
+/* Release a resident scan: LIVO_E_BUSY while a submitted batch that holds it is
+ * not collected; other batches may be in flight. */
 int livo_scan_release(livo_ctx* ctx, int32_t scan_id);
 
 /* The neighbour cache of a resident scan: the k = 5 nearest map points of each

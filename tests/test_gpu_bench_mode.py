@@ -249,3 +249,42 @@ def test_rccl_counter_allreduce_world1(built):
     assert r.returncode == 0, r.stderr[-2000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("BACKEND")]
     assert line == ["BACKEND nccl [8, 40, 16, 123456, 77, 800000] 0.125"], r.stdout[-1000:]
+
+
+def test_scan_upload_async_farm(built):
+    """livo_scan_upload_async (pinned staging, the upload stream) feeding the
+    pipelined farm: scans uploaded while the previous batches run give bit for
+    bit the synchronous uploads' updates; a scan is released (LIVO_E_BUSY while
+    its batch is in flight) while another batch still runs; neighbours of an
+    asynchronously uploaded scan are readable after its batch."""
+    import livo_amd
+    from livo_amd import synth
+    m = synth.cached_map(1_000_000)
+    scans = [synth.make_scan(50_000, 500 + s)[0] for s in range(12)]
+    states = [synth.make_state(500 + s) for s in range(12)]
+    with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=4) as ctx:
+        ctx.map_build(m)
+        ref_ids = [ctx.scan_upload(b) for b in scans]
+        ref = list(zip(*ctx.iekf_update_batch(ref_ids, states)))
+        for sid in ref_ids:
+            ctx.scan_release(sid)
+        a = [ctx.scan_upload_async(b) for b in scans[:4]]
+        b = [ctx.scan_upload_async(b) for b in scans[4:8]]
+        ta = ctx.iekf_update_batch_submit(a, states[:4])
+        tb = ctx.iekf_update_batch_submit(b, states[4:8])
+        c = [ctx.scan_upload_async(x) for x in scans[8:]]  # beside both batches
+        with pytest.raises(livo_amd.LivoError) as e:
+            ctx.scan_release(a[0])
+        assert e.value.code == -8
+        out_a = list(zip(*ctx.iekf_update_batch_wait(ta, 4)))
+        for sid in a[1:]:
+            ctx.scan_release(sid)  # batch b still in flight
+        tc = ctx.iekf_update_batch_submit(c, states[8:])
+        out_b = list(zip(*ctx.iekf_update_batch_wait(tb, 4)))
+        out_c = list(zip(*ctx.iekf_update_batch_wait(tc, 4)))
+        idx, _ = ctx.scan_neighbors(a[0])
+        assert idx.shape == (50_000, 5) and (idx >= 0).all()
+    for k in range(4):
+        _same_update(out_a[k], ref[k])
+        _same_update(out_b[k], ref[4 + k])
+        _same_update(out_c[k], ref[8 + k])
