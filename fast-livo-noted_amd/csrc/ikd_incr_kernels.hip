@@ -643,6 +643,7 @@ __global__ void k_cr_fill(const float4* __restrict__ gpts, const uint32_t* __res
 struct BrGeo {
     float org[3];
     float h, inv, rmax, rmax2;
+    int x0, x1;  // anchors with x index in [x0, x1) only (a chunk of the build)
 };
 template <class F>
 __device__ __forceinline__ void br_anchors(const BrGeo& G, const float4 p, F&& f) {
@@ -653,6 +654,8 @@ __device__ __forceinline__ void br_anchors(const BrGeo& G, const float4 p, F&& f
         lo[k] = (int)floorf((q[k] - G.org[k] - G.rmax) * G.inv) - 1;
         hi[k] = (int)floorf((q[k] - G.org[k] + G.rmax) * G.inv) + 1;
     }
+    lo[0] = max(lo[0], G.x0);
+    hi[0] = min(hi[0], G.x1 - 1);
     for (int z = lo[2]; z <= hi[2]; z++)
         for (int y = lo[1]; y <= hi[1]; y++)
             for (int x = lo[0]; x <= hi[0]; x++) {
@@ -857,17 +860,49 @@ int launch_cr_fill(const float* gpts, const uint32_t* e2, const unsigned long lo
     DYN_LAUNCH(k_cr_fill, n + 8, reinterpret_cast<const float4*>(gpts), e2, skeys, n,
                reinterpret_cast<float4*>(vpts), heads);
 }
-static BrGeo br_geo(const float org[3], float h, float rmax) {
-    return BrGeo{{org[0], org[1], org[2]}, h, 1.0f / h, rmax, rmax * rmax};
+static BrGeo br_geo(const float org[3], float h, float rmax, int x0, int x1) {
+    return BrGeo{{org[0], org[1], org[2]}, h, 1.0f / h, rmax, rmax * rmax, x0, x1};
 }
 int launch_br_count(const float* gpts, int64_t n, const float org[3], float h, float rmax, uint32_t* cnt,
-                    unsigned long long* total, void* stream) {
-    DYN_LAUNCH(k_br_count, n, reinterpret_cast<const float4*>(gpts), n, br_geo(org, h, rmax), cnt, total);
+                    unsigned long long* total, void* stream, int x0, int x1) {
+    DYN_LAUNCH(k_br_count, n, reinterpret_cast<const float4*>(gpts), n, br_geo(org, h, rmax, x0, x1), cnt, total);
 }
 int launch_br_emit(const float* gpts, int64_t n, const float org[3], float h, float rmax, const uint32_t* off,
-                   uint32_t* rho_bits, unsigned long long* keys, uint32_t* pt, uint32_t* iota, void* stream) {
-    DYN_LAUNCH(k_br_emit, n, reinterpret_cast<const float4*>(gpts), n, br_geo(org, h, rmax), off, rho_bits, keys, pt,
-               iota);
+                   uint32_t* rho_bits, unsigned long long* keys, uint32_t* pt, uint32_t* iota, void* stream, int x0,
+                   int x1) {
+    DYN_LAUNCH(k_br_emit, n, reinterpret_cast<const float4*>(gpts), n, br_geo(org, h, rmax, x0, x1), off, rho_bits,
+               keys, pt, iota);
+}
+// One chunk's runs as {key, start >> 2, count} records (the chunk's placed runs
+// start at word base + pstart[r], a multiple of 4), for k_trip_slots.
+__global__ void k_run_trip(const unsigned long long* __restrict__ skeys, const uint32_t* __restrict__ starts,
+                           const uint32_t* __restrict__ pstart, int64_t nruns, unsigned long long base,
+                           GridSlot* trip) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nruns) return;
+    const uint32_t s0 = starts[r], s1 = starts[r + 1];
+    GridSlot g;
+    g.key = skeys[s0];
+    g.start = (uint32_t)((base + pstart[r]) >> 2);
+    g.count = s1 - s0;
+    trip[r] = g;
+}
+__global__ void k_trip_slots(const GridSlot* __restrict__ trip, int64_t nruns, GridSlot* slots, int log2) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nruns) return;
+    const GridSlot g = trip[r];
+    const uint64_t mask = (1ull << log2) - 1ull;
+    uint64_t sl = (uint64_t)((g.key * 0x9E3779B97F4A7C15ull) >> (64 - log2));
+    while (atomicCAS(&slots[sl].key, kGridEmpty, g.key) != kGridEmpty) sl = (sl + 1) & mask;
+    slots[sl].start = g.start;
+    slots[sl].count = g.count;
+}
+int launch_run_trip(const unsigned long long* skeys, const uint32_t* starts, const uint32_t* pstart, int64_t nruns,
+                    unsigned long long base, GridSlot* trip, void* stream) {
+    DYN_LAUNCH(k_run_trip, nruns, skeys, starts, pstart, nruns, base, trip);
+}
+int launch_trip_slots(const GridSlot* trip, int64_t nruns, GridSlot* slots, int log2, void* stream) {
+    DYN_LAUNCH(k_trip_slots, nruns, trip, nruns, slots, log2);
 }
 int launch_br_gather_keys(const unsigned long long* keys, const uint32_t* e1, int64_t n, unsigned long long* out,
                           void* stream) {

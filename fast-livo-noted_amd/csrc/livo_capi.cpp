@@ -225,6 +225,7 @@ struct livo_ctx {
     int32_t blog2 = 0;
     float bh = 0.f, brmax = 0.f, br5 = 0.f;
     int64_t bentries = 0;
+    int32_t bchunks = 0;               // anchor chunks of the ball runs' build
     GridSlot* gslots = nullptr;        // cell grid
     float* gpts = nullptr;
     float gorg[3] = {0.f, 0.f, 0.f};
@@ -1784,6 +1785,219 @@ static int build_cell_runs(livo_ctx* c, int64_t M) {
 #endif
 }
 
+#if LIVO_IDX_RUNS
+// The index ball runs, built in chunks of anchors (their x index in [x0, x1)),
+// each chunk at most `cap` entries (LIVO_BR_CHUNK, default 2^29: ~26 GB of sort
+// scratch), so the 32-bit sort indices and offsets of one chunk never wrap
+// however many entries the map has (config 5's 10M map with 6 r5 balls passes
+// 2^31).  A chunk is counted, placed behind the runs of the chunks before it in
+// one run array (every run starts on a 4-word boundary), and its runs recorded
+// as {key, start / 4, count}; the hash table then takes every record, so a slot's
+// start addresses 2^34 words.  The runs' contents and order are those of the
+// one-pass build.
+static int build_ball_runs_idx(livo_ctx* c, int64_t M, float r5, float bh, float brmax, double ext) {
+    int64_t cap = (int64_t)1 << 29;
+    if (const char* env = std::getenv("LIVO_BR_CHUNK")) cap = std::max<int64_t>(1 << 16, std::atoll(env));
+    cap = std::min<int64_t>(cap, ((int64_t)1 << 31) - 64);
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    uint32_t* cnt = nullptr;
+    uint32_t* off = nullptr;
+    unsigned long long* tot = nullptr;
+    if (dev_alloc(&cnt, (size_t)M) || dev_alloc(&off, (size_t)M) || dev_alloc(&tot, 1)) {
+        dev_free(cnt);
+        dev_free(off);
+        dev_free(tot);
+        return LIVO_E_OOM;
+    }
+    // entries of the anchors with x index in [x0, x1) (a count pass over the map)
+    auto count = [&](int x0, int x1, unsigned long long* n_out) -> int {
+        int rc = hipMemsetAsync(tot, 0, 8, c->stream) == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+        if (!rc) rc = launch_br_count(c->gpts, M, c->gorg, bh, brmax, cnt, tot, c->stream, x0, x1);
+        if (!rc && hipMemcpyAsync(n_out, tot, 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess) rc = LIVO_E_HIP;
+        if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = LIVO_E_HIP;
+        return rc;
+    };
+    // the anchors' x range: the map spans [gorg, gorg + ext] on every axis (the
+    // grid's origin is its minimum corner), a point's anchors lie within brmax
+    const int xlo = (int)std::floor(-(double)brmax / (double)bh) - 2;
+    const int xhi = (int)std::floor((ext + (double)brmax) / (double)bh) + 3;  // exclusive
+    struct Chunk {
+        int x0, x1;
+        int64_t n;
+    };
+    std::vector<Chunk> chunks, todo{{xlo, xhi, -1}};
+    int64_t total_entries = 0, max_n = 0;
+    int rc = LIVO_OK;
+    while (!todo.empty() && !rc) {  // bisect the x range until every chunk fits
+        Chunk ch = todo.back();
+        todo.pop_back();
+        unsigned long long n64 = 0;
+        rc = count(ch.x0, ch.x1, &n64);
+        if (rc) break;
+        if ((int64_t)n64 > cap && ch.x1 - ch.x0 > 1) {
+            const int mid = ch.x0 + (ch.x1 - ch.x0) / 2;
+            todo.push_back({mid, ch.x1, -1});
+            todo.push_back({ch.x0, mid, -1});
+            continue;
+        }
+        if ((int64_t)n64 > cap) rc = LIVO_E_RANGE;  // one anchor column beyond the cap
+        if (n64 == 0) continue;
+        ch.n = (int64_t)n64;
+        chunks.push_back(ch);
+        total_entries += ch.n;
+        max_n = std::max(max_n, ch.n);
+    }
+    dev_free(tot);
+    if (rc || total_entries == 0) {
+        dev_free(cnt);
+        dev_free(off);
+        return rc;
+    }
+    // the run array: the entries plus the padding of every run to 4 words (grown if short)
+    int64_t words_cap = total_entries + total_entries / 8 + 4096 + kRunPad;
+    if (dev_alloc(&c->bpts, (size_t)words_cap) ||
+        hipMemsetAsync(c->bpts, 0, (size_t)words_cap * sizeof(RunWord), c->stream) != hipSuccess) {
+        dev_free(cnt);
+        dev_free(off);
+        dev_free(c->bpts);
+        return LIVO_E_OOM;
+    }
+    const int64_t n = max_n;
+    const size_t b4 = al((size_t)n * 4), b8 = al((size_t)n * 8);
+    char* scr = nullptr;
+    if (hipMalloc((void**)&scr, 7 * b4 + 3 * b8 + 2 * al(((size_t)n + 1) * 4) + 256) != hipSuccess) {
+        dev_free(cnt);
+        dev_free(off);
+        dev_free(c->bpts);
+        return LIVO_E_OOM;
+    }
+    char* p = scr;
+    uint32_t* rho = (uint32_t*)p; p += b4;
+    uint32_t* iota = (uint32_t*)p; p += b4;
+    uint32_t* srho = (uint32_t*)p; p += b4;
+    uint32_t* e1 = (uint32_t*)p; p += b4;
+    uint32_t* e2 = (uint32_t*)p; p += b4;
+    uint32_t* pt = (uint32_t*)p; p += b4;
+    uint32_t* heads = (uint32_t*)p; p += b4;
+    unsigned long long* keys = (unsigned long long*)p; p += b8;
+    unsigned long long* key1 = (unsigned long long*)p; p += b8;
+    unsigned long long* skeys = (unsigned long long*)p; p += b8;
+    uint32_t* starts = (uint32_t*)p; p += al(((size_t)n + 1) * 4);
+    uint32_t* plen = (uint32_t*)p; p += al(((size_t)n + 1) * 4);
+    unsigned long long* nruns_dev = (unsigned long long*)p;
+    uint32_t* runid = rho;    // (rho is dead after the first sort)
+    uint32_t* pstart = srho;  // (srho too)
+    GridSlot* trip = nullptr;
+    int64_t trip_cap = 0, runs_total = 0, base = 0;
+    for (const Chunk& ch : chunks) {
+        const int64_t nc = ch.n;
+        rc = launch_br_count(c->gpts, M, c->gorg, bh, brmax, cnt, nruns_dev, c->stream, ch.x0, ch.x1);
+        if (!rc) rc = ivox_scan(c, cnt, off, M);
+        if (!rc) rc = launch_br_emit(c->gpts, M, c->gorg, bh, brmax, off, rho, keys, pt, iota, c->stream, ch.x0, ch.x1);
+        if (!rc) {
+            size_t tb = 0;
+            rc = prim_sort_pairs_u32(nullptr, &tb, rho, srho, iota, e1, nc, 32, c->stream);
+            if (!rc) rc = ensure_prim(c, tb);
+            tb = c->prim_bytes;
+            if (!rc) rc = prim_sort_pairs_u32(c->prim_tmp, &tb, rho, srho, iota, e1, nc, 32, c->stream);
+        }
+        if (!rc) rc = launch_br_gather_keys(keys, e1, nc, key1, c->stream);
+        if (!rc) rc = sort_u64(c, key1, skeys, e1, e2, nc);
+        // runs: heads, starts, lengths padded to 4 and their scan
+        if (!rc) rc = launch_run_heads(skeys, nc, heads, c->stream);
+        if (!rc) rc = ivox_scan(c, heads, runid, nc);
+        if (!rc && hipMemsetAsync(nruns_dev, 0, 8, c->stream) != hipSuccess) rc = LIVO_E_HIP;
+        if (!rc) rc = launch_dyn_runs(heads, runid, nc, starts, nruns_dev, c->stream);
+        unsigned long long runs = 0;
+        if (!rc && hipMemcpyAsync(&runs, nruns_dev, 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess) rc = LIVO_E_HIP;
+        if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = LIVO_E_HIP;
+        if (rc) break;
+        if (runs == 0) continue;
+        rc = launch_run_plen(starts, (int64_t)runs, plen, c->stream);
+        if (!rc) rc = ivox_scan(c, plen, pstart, (int64_t)runs);
+        uint32_t tail[2] = {0u, 0u};
+        if (!rc && (hipMemcpyAsync(&tail[0], pstart + runs - 1, 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+                    hipMemcpyAsync(&tail[1], plen + runs - 1, 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+                    hipStreamSynchronize(c->stream) != hipSuccess))
+            rc = LIVO_E_HIP;
+        if (rc) break;
+        const int64_t words = (int64_t)tail[0] + tail[1];
+        if (words < nc || words >= (int64_t)0xFFFFFFFFll) {
+            rc = LIVO_E_RANGE;
+            break;
+        }
+        if (base + words + kRunPad > words_cap) {  // more padding than reserved: grow the run array
+            const int64_t ncap = (base + words + kRunPad) + (base + words) / 8;
+            RunWord* nb = nullptr;
+            if (dev_alloc(&nb, (size_t)ncap)) {
+                rc = LIVO_E_OOM;
+                break;
+            }
+            if (hipMemsetAsync(nb, 0, (size_t)ncap * sizeof(RunWord), c->stream) != hipSuccess ||
+                hipMemcpyAsync(nb, c->bpts, (size_t)base * sizeof(RunWord), hipMemcpyDeviceToDevice, c->stream) !=
+                    hipSuccess ||
+                hipStreamSynchronize(c->stream) != hipSuccess)
+                rc = LIVO_E_HIP;
+            dev_free(c->bpts);
+            c->bpts = nb;
+            words_cap = ncap;
+            if (rc) break;
+        }
+        if (runs_total + (int64_t)runs > trip_cap) {  // the run records (grown by doubling)
+            const int64_t ncap = std::max<int64_t>(2 * trip_cap, runs_total + (int64_t)runs + 4096);
+            GridSlot* nt = nullptr;
+            if (dev_alloc(&nt, (size_t)ncap)) {
+                rc = LIVO_E_OOM;
+                break;
+            }
+            if (runs_total > 0 &&
+                (hipMemcpyAsync(nt, trip, (size_t)runs_total * sizeof(GridSlot), hipMemcpyDeviceToDevice,
+                                c->stream) != hipSuccess ||
+                 hipStreamSynchronize(c->stream) != hipSuccess))
+                rc = LIVO_E_HIP;
+            dev_free(trip);
+            trip = nt;
+            trip_cap = ncap;
+            if (rc) break;
+        }
+        rc = launch_run_place(e2, pt, heads, runid, starts, pstart, nc, c->bpts + base, c->stream);
+        if (!rc) rc = launch_run_trip(skeys, starts, pstart, (int64_t)runs, (unsigned long long)base,
+                                      trip + runs_total, c->stream);
+        if (rc) break;
+        base += words;
+        runs_total += (int64_t)runs;
+    }
+    if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = LIVO_E_HIP;
+    (void)hipFree(scr);
+    dev_free(cnt);
+    dev_free(off);
+    if (!rc && (base >> 2) >= ((int64_t)1 << 32)) rc = LIVO_E_RANGE;  // start / 4 in 32 bits
+    int log2 = 4;
+    while (((int64_t)1 << log2) < 4 * runs_total) log2++;
+    if (!rc && runs_total > 0) {
+        const int64_t table = (int64_t)1 << log2;
+        if (dev_alloc(&c->bslots, (size_t)table)) rc = LIVO_E_OOM;
+        if (!rc) rc = launch_ivox_clear(c->bslots, table, c->stream);
+        if (!rc) rc = launch_trip_slots(trip, runs_total, c->bslots, log2, c->stream);
+        if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = LIVO_E_HIP;
+    }
+    dev_free(trip);
+    if (rc || runs_total == 0) {
+        dev_free(c->bslots);
+        dev_free(c->bpts);
+        return rc;
+    }
+    c->blog2 = log2;
+    c->bh = bh;
+    c->brmax = brmax;
+    c->br5 = r5;
+    c->bentries = total_entries;
+    c->bchunks = (int32_t)chunks.size();
+    c->grid_bytes += (int64_t)(((int64_t)1 << log2) * sizeof(GridSlot) + words_cap * sizeof(RunWord));
+    return LIVO_OK;
+}
+#endif
+
 // The ball runs of the static map (livo_internal.h KnnParams::bslots), built on
 // the device: every grid point emits one entry per anchor cell (edge bh) whose
 // centre lies within brmax (k_br_count, a scan, k_br_emit); a stable radix sort
@@ -1802,6 +2016,9 @@ static int build_ball_runs(livo_ctx* c, int64_t M, float r5, double ext) {
     // ball radius) spans that many anchors keeps the cell runs only, rather
     // than letting keys alias into a run not sorted about its own anchor
     if ((ext + 2.0 * (double)brmax) / (double)bh + 4.0 >= (double)(kGridBias - 8)) return LIVO_OK;
+#if LIVO_IDX_RUNS
+    return build_ball_runs_idx(c, M, r5, bh, brmax, ext);
+#endif
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     uint32_t* cnt = nullptr;
     uint32_t* off = nullptr;
@@ -1871,6 +2088,7 @@ static int build_ball_runs(livo_ctx* c, int64_t M, float r5, double ext) {
     c->brmax = brmax;
     c->br5 = r5;
     c->bentries = n;
+    c->bchunks = 1;
     c->grid_bytes += (int64_t)(((int64_t)1 << c->blog2) * sizeof(GridSlot) + words * sizeof(RunWord));
     return LIVO_OK;
 #else
@@ -1899,6 +2117,7 @@ static int build_ball_runs(livo_ctx* c, int64_t M, float r5, double ext) {
     c->brmax = brmax;
     c->br5 = r5;
     c->bentries = n;
+    c->bchunks = 1;
     c->grid_bytes += (int64_t)(table * sizeof(GridSlot) + (size_t)(n + kRunPad) * 16);
     return LIVO_OK;
 #endif
@@ -2010,7 +2229,8 @@ int livo_map_get_info(livo_ctx* c, livo_map_info* out) {
     if (!c->has_map) return LIVO_E_NOMAP;
     out->num_points = c->map_points;
     out->depth = c->map_depth;
-    out->reserved = 0;
+    out->ball_chunks = c->bslots ? c->bchunks : 0;
+    out->ball_entries = c->bslots ? c->bentries : 0;
     out->num_slots = c->map_slots;
     out->device_bytes = (c->map_slots + 1) * (int64_t)sizeof(MapNode) + c->leaf_bytes + c->grid_bytes +
                         c->dyn.cap * 17;

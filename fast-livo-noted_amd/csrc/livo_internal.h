@@ -613,9 +613,14 @@ int launch_dyn_delete_boxes(const float* all, uint8_t* alive, int64_t n_ids, con
 // (x, y, z, map index bits) and the run heads.
 // ball runs (k_br_*, ikd_incr_kernels.hip)
 int launch_br_count(const float* gpts, int64_t n, const float org[3], float h, float rmax, uint32_t* cnt,
-                    unsigned long long* total, void* stream);
+                    unsigned long long* total, void* stream, int x0 = -(1 << 30), int x1 = 1 << 30);
 int launch_br_emit(const float* gpts, int64_t n, const float org[3], float h, float rmax, const uint32_t* off,
-                   uint32_t* rho_bits, unsigned long long* keys, uint32_t* pt, uint32_t* iota, void* stream);
+                   uint32_t* rho_bits, unsigned long long* keys, uint32_t* pt, uint32_t* iota, void* stream,
+                   int x0 = -(1 << 30), int x1 = 1 << 30);
+// ball runs built in chunks of anchors: each chunk's runs as {key, start >> 2, count}, then the table
+int launch_run_trip(const unsigned long long* skeys, const uint32_t* starts, const uint32_t* pstart, int64_t nruns,
+                    unsigned long long base, GridSlot* trip, void* stream);
+int launch_trip_slots(const GridSlot* trip, int64_t nruns, GridSlot* slots, int log2, void* stream);
 int launch_br_gather_keys(const unsigned long long* keys, const uint32_t* e1, int64_t n, unsigned long long* out,
                           void* stream);
 int launch_br_fill(const float* gpts, const uint32_t* pt, const uint32_t* e2, const unsigned long long* skeys,

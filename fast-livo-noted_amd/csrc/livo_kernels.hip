@@ -1638,7 +1638,12 @@ __device__ __forceinline__ bool brun_search(LeafQuery& q, const KnnParams& P, bo
         visits++;
     }
     if (g.key != key) return false;
-    const uint32_t lo = g.start, cnt = g.count;
+#if LIVO_IDX_RUNS
+    const size_t lo = (size_t)g.start << 2;  // (ball-run starts are stored / 4: 2^34 words addressable)
+#else
+    const uint32_t lo = g.start;
+#endif
+    const uint32_t cnt = g.count;
     const float cx = cell_centre(P.gorg[0], P.bh, a[0]), cy = cell_centre(P.gorg[1], P.bh, a[1]);
     const float cz = cell_centre(P.gorg[2], P.bh, a[2]);
     const float dqv = __builtin_amdgcn_sqrtf(centre_d2(cx, cy, cz, q.qx, q.qy, q.qz)) * (1.0f + 1e-6f);

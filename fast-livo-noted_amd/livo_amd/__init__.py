@@ -62,8 +62,8 @@ class IterStats(C.Structure):
 
 
 class MapInfo(C.Structure):
-    _fields_ = [("num_points", C.c_int64), ("depth", C.c_int32), ("reserved", C.c_int32),
-                ("num_slots", C.c_int64), ("device_bytes", C.c_int64)]
+    _fields_ = [("num_points", C.c_int64), ("depth", C.c_int32), ("ball_chunks", C.c_int32),
+                ("num_slots", C.c_int64), ("device_bytes", C.c_int64), ("ball_entries", C.c_int64)]
 
 
 class PointOut(C.Structure):
@@ -312,7 +312,7 @@ class Context:
         mi = MapInfo()
         _check("livo_map_get_info", self._L.livo_map_get_info(self.h, C.byref(mi)))
         return {"num_points": mi.num_points, "depth": mi.depth, "num_slots": mi.num_slots,
-                "device_bytes": mi.device_bytes}
+                "device_bytes": mi.device_bytes, "ball_chunks": mi.ball_chunks, "ball_entries": mi.ball_entries}
 
     def knn(self, q: np.ndarray, k: int = 5):
         q = np.ascontiguousarray(q, np.float32).reshape(-1, 3)

@@ -111,9 +111,10 @@ typedef struct livo_iter_stats {
 typedef struct livo_map_info {
     int64_t num_points;   /* M                                                    */
     int32_t depth;        /* tree levels                                          */
-    int32_t reserved;
+    int32_t ball_chunks;  /* anchor chunks the ball runs were built in (0: none)  */
     int64_t num_slots;    /* heap-ordered node slots (2^depth - 1)                */
     int64_t device_bytes; /* HBM bytes held by the map                            */
+    int64_t ball_entries; /* entries of the ball runs (0: the cell runs only)     */
 } livo_map_info;
 
 /* Optional per-point outputs of livo_h_share (any pointer may be NULL). */

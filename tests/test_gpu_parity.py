@@ -574,3 +574,35 @@ def test_exact_ties_resolved_in_kernel(built, kind, monkeypatch):
     np.testing.assert_array_equal(d_g, d_r)
     np.testing.assert_array_equal(idx_g, idx_r)
     assert replays <= 0.01 * len(q), replays
+
+
+def test_ball_runs_chunked_build(built, monkeypatch):
+    """The ball runs built in anchor chunks (LIVO_BR_CHUNK forces ~8 of them on
+    the 1M map) hold the runs of the one-pass build: same entry count, and a
+    batch of scans on either map gives bit for bit the same updates (a run
+    read at its chunk's place must equal the same run of the one-pass array)."""
+    import livo_amd
+    synth = _synth()
+    m = synth.cached_map(1_000_000)
+    scans = [synth.make_scan(50_000, 700 + s)[0] for s in range(4)]
+    states = [synth.make_state(700 + s) for s in range(4)]
+    res = {}
+    for chunk in (None, 1 << 23):
+        if chunk is None:
+            monkeypatch.delenv("LIVO_BR_CHUNK", raising=False)
+        else:
+            monkeypatch.setenv("LIVO_BR_CHUNK", str(chunk))
+        with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=4) as ctx:
+            ctx.map_build(m)
+            info = ctx.map_info()
+            sids = [ctx.scan_upload(b) for b in scans]
+            res[chunk] = (info, ctx.iekf_update_batch(sids, states))
+    i0, i1 = res[None][0], res[1 << 23][0]
+    assert i0["ball_chunks"] == 1 and i1["ball_chunks"] >= 4, (i0, i1)
+    assert i0["ball_entries"] == i1["ball_entries"] > 0
+    for k in range(4):
+        a = (res[None][1][0][k], res[None][1][1][k])
+        b = (res[1 << 23][1][0][k], res[1 << 23][1][1][k])
+        for f in ("rot", "pos", "cov"):
+            assert np.array_equal(np.asarray(a[0][f]), np.asarray(b[0][f])), (k, f)
+        assert np.array_equal(np.asarray(a[1]["solution"]), np.asarray(b[1]["solution"])), k
