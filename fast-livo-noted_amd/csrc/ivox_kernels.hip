@@ -500,28 +500,172 @@ __global__ __launch_bounds__(64 * kWaves) void k_ivox_knn_wave(KnnParams P) {
     }
 }
 
+// ------------------------------------------------------- team search ----
+// One query per 16-lane team (4 per wave, 16 per 256-thread block), the list
+// in LDS (kIvTeamCap SelElems = 1 KB per team): the team probes the nearby
+// grids (a lane each) and loads each grid's points together (16 at a time);
+// the in-range ones are appended to the list in push order (ivox3d_node.hpp:
+// 154-164), and the team's lane 0 runs every std::nth_element exactly as the
+// per-thread search does (stl_select.h) on the LDS list.  No private
+// candidate array (k_ivox_knn's lives in scratch: ~1 KB a thread), and 16x
+// fewer lanes per query than the wave search.  A query whose list would
+// outgrow the capacity goes to the global-memory pass (k_ivox_knn_big).
+constexpr int kIvTeam = 16;
+constexpr int kIvTeamCap = 128;
+__device__ __forceinline__ uint32_t team_bits(unsigned long long m, int lane) {
+    return (uint32_t)(m >> (lane & 48)) & 0xFFFFu;
+}
+template <bool LATER>
+__global__ __launch_bounds__(256) void k_ivox_knn_team(KnnParams P) {
+    __shared__ SelElem lst[256 / kIvTeam][kIvTeamCap];
+    const int lane = threadIdx.x & 63, tl = threadIdx.x & (kIvTeam - 1), team = threadIdx.x / kIvTeam;
+    SelElem* L = lst[team];
+    unsigned bjob, bx;
+    xcd_block(P.nb, bjob, bx);
+    const HsJob job = P.jobs[bjob];
+    const IekfSlot* slot = job.slot;
+    if (P.force >= 0) {
+        if (!P.force) return;
+    } else {
+        if (slot->ctrl.stop) return;  // block-uniform
+        if (LATER && !slot->ctrl.search_en) return;
+    }
+    const int i = (int)bx * (256 / kIvTeam) + team;
+    if (i >= job.n) return;  // team-uniform
+    const IvoxParams& V = P.iv;
+    const float4 b = reinterpret_cast<const float4*>(job.pts)[i];
+    float qx, qy, qz;
+    iv_world(P, slot, b, qx, qy, qz);
+    int kx, ky, kz;
+    const float qlim = (float)(kIvMaxKey + 8);
+    if (!iv_cell(qx, V.inv_res, qlim, kx) || !iv_cell(qy, V.inv_res, qlim, ky) || !iv_cell(qz, V.inv_res, qlim, kz))
+        return;  // no grid within reach: nothing found, the cache stays
+    // the nearby grids' runs: grid t on lane t % 16 (two per lane for t >= 16)
+    uint2 r0 = make_uint2(0u, 0u), r1 = make_uint2(0u, 0u);
+    if (tl < V.nearby)
+        r0 = iv_lookup(V.slots, V.log2, iv_key(kx + c_nearby[tl][0], ky + c_nearby[tl][1], kz + c_nearby[tl][2]));
+    if (tl + kIvTeam < V.nearby) {
+        const int t = tl + kIvTeam;
+        r1 = iv_lookup(V.slots, V.log2, iv_key(kx + c_nearby[t][0], ky + c_nearby[t][1], kz + c_nearby[t][2]));
+    }
+    const float4* __restrict__ pts = reinterpret_cast<const float4*>(V.pts);
+    const int K = V.max_num;
+    const int tb = lane & 48;  // the team's first lane in the wave
+    int n = 0;
+    bool ok = true;
+#pragma unroll 1
+    for (int t = 0; t < V.nearby; t++) {
+        const int src = tb + (t & (kIvTeam - 1));
+        const uint32_t st = (uint32_t)__shfl((int)(t < kIvTeam ? r0.x : r1.x), src, 64);
+        const uint32_t c = (uint32_t)__shfl((int)(t < kIvTeam ? r0.y : r1.y), src, 64);
+        if (c == 0u) continue;  // team-uniform
+        const int old = n;
+#pragma unroll 1
+        for (uint32_t k0 = 0; k0 < c; k0 += kIvTeam) {
+            const uint32_t k = k0 + (uint32_t)tl;
+            bool in = false;
+            float d = 0.f;
+            if (k < c) {
+                const float4 v = pts[st + k];
+                const float dx = v.x - qx, dy = v.y - qy, dz = v.z - qz;
+                d = dx * dx + (dy * dy + dz * dz);  // distance2, ivox3d_node.hpp:12-16
+                in = (double)d < V.range2;
+            }
+            const uint32_t m = team_bits(__ballot(in), lane);
+            if (n + __popc(m) > kIvTeamCap) {
+                ok = false;
+                break;
+            }
+            if (in) L[n + __popc(m & ((1u << tl) - 1u))] = SelElem{d, st + k};
+            n += __popc(m);
+        }
+        if (!ok) break;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        // KNNPointByCondition (ivox3d_node.hpp:179-183) on the grid's segment
+        if (n - old > K) {
+            if (tl == 0) sel_nth_element(L, old, old + K - 1, n);
+            n = old + K;
+        }
+    }
+    if (!ok) {  // a list beyond the team's capacity: the exact global-memory pass
+        if (tl == 0) {
+            const unsigned r = atomicAdd(P.replay_count, 1u);
+            P.replay_list[r] = ((unsigned long long)bjob << 32) | (unsigned)i;
+        }
+        return;
+    }
+    if (n == 0) return;  // no candidate: the reference returns false, the cache stays
+    if (tl == 0) {
+        if (n > K) {  // ivox3d.h:173-177
+            sel_nth_element(L, 0, K - 1, n);
+        }
+        sel_nth_element(L, 0, 0, n > K ? K : n);  // ivox3d.h:178
+    }
+    n = n > K ? K : n;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // the record: lanes 0..4 of the team the points, lane 0 the indices
+    NNRec* out = job.nn + i;
+    SelElem e = tl < n ? L[tl] : SelElem{INFINITY, 0u};
+    float4 pv = make_float4(0.f, 0.f, 0.f, INFINITY);
+    int32_t pidx = -1, node = -1;
+    if (tl < n) {
+        const float4 p = pts[e.id];
+        pv = make_float4(p.x, p.y, p.z, e.d);
+        pidx = __float_as_int(p.w);
+        node = (int32_t)e.id;
+    }
+    if (tl < kNN) reinterpret_cast<float4*>(out)[tl] = pv;
+    int32_t ix[kNN], nd[kNN];
+#pragma unroll
+    for (int k = 0; k < kNN; k++) {
+        ix[k] = __shfl(pidx, tb + k, 64);
+        nd[k] = __shfl(node, tb + k, 64);
+    }
+    if (tl == 0) {
+        int4* oi = reinterpret_cast<int4*>(out) + 5;
+        oi[0] = make_int4(ix[0], ix[1], ix[2], ix[3]);
+        oi[1] = make_int4(ix[4], n, 0, nd[0]);
+        oi[2] = make_int4(nd[1], nd[2], nd[3], nd[4]);
+    }
+}
+
 // Kernel choice per launch: the wave-cooperative search has ~20x less latency
-// per query (small scans: the IEKF of one downsampled frame), the
-// one-query-per-thread search (private candidate array) more throughput when
-// hundreds of thousands of queries are in flight (scan farms).
-// LIVO_IVOX_KIND=thread|wave forces one; LIVO_IVOX_WAVE_MAX sets the switch
+// per query (small scans: the IEKF of one downsampled frame), the team search
+// (16 lanes a query, list in LDS) more throughput when hundreds of thousands
+// of queries are in flight (scan farms); the one-query-per-thread search
+// (private candidate array, in scratch) is kept as a reference.
+// LIVO_IVOX_KIND=thread|wave|team forces one; LIVO_IVOX_WAVE_MAX sets the switch
 // point (queries per launch, default 131072).
 static int ivox_kind(int64_t queries) {
     const char* e = std::getenv("LIVO_IVOX_KIND");  // read per launch (tests switch it)
-    const int forced = !e ? -1 : (std::strcmp(e, "thread") == 0 ? 0 : (std::strcmp(e, "wave") == 0 ? 1 : -1));
+    const int forced = !e ? -1
+                          : (std::strcmp(e, "thread") == 0 ? 0
+                                                           : (std::strcmp(e, "wave") == 0 ? 1
+                                                                                          : (std::strcmp(e, "team") == 0 ? 2 : -1)));
     static const int64_t wave_max = [] {
         const char* e = std::getenv("LIVO_IVOX_WAVE_MAX");
         return e ? (int64_t)std::atoll(e) : (int64_t)131072;
     }();
     if (forced >= 0) return forced;
-    return queries <= wave_max ? 1 : 0;
+    return queries <= wave_max ? 1 : 2;
 }
 
 int launch_ivox_knn(const KnnParams& p, int n_jobs, int64_t max_n, bool later, int64_t overflow_threads,
                     void* stream) {
     if (n_jobs <= 0 || max_n <= 0) return LIVO_OK;
     KnnParams q = p;
-    if (ivox_kind((int64_t)n_jobs * max_n) == 0) {
+    const int kind = ivox_kind((int64_t)n_jobs * max_n);
+    if (kind == 2) {
+        q.nb = (int32_t)((max_n + (256 / kIvTeam) - 1) / (256 / kIvTeam));
+        if ((int64_t)q.nb * n_jobs >= (1ll << 31)) return LIVO_E_RANGE;
+        const dim3 grid((unsigned)(q.nb * n_jobs)), block(256);
+        if (later)
+            hipLaunchKernelGGL((k_ivox_knn_team<true>), grid, block, 0, (hipStream_t)stream, q);
+        else
+            hipLaunchKernelGGL((k_ivox_knn_team<false>), grid, block, 0, (hipStream_t)stream, q);
+    } else if (kind == 0) {
         q.nb = (int32_t)((max_n + kKnnBlock - 1) / kKnnBlock);
         if ((int64_t)q.nb * n_jobs >= (1ll << 31)) return LIVO_E_RANGE;
         const dim3 grid((unsigned)(q.nb * n_jobs)), block(kKnnBlock);

@@ -210,7 +210,11 @@ def load(path: str = LIB_PATH):
         if not os.path.exists(path):
             raise ImportError(f"HIP library not built: {path} (run __graft_entry__.build())")
         L = C.CDLL(path)
+        # an A/B variant of an older build (LIVO_LIB) may lack entry points added since
+        old_ok = os.path.abspath(path) != os.path.abspath(os.path.join(PKG_ROOT, "lib", "liblivo_hip.so"))
         for name, (res, args) in SIGNATURES.items():
+            if old_ok and not hasattr(L, name):
+                continue
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args

@@ -402,10 +402,10 @@ def test_wave_nth_matches_libstdcxx(built):
     assert " 0 mismatches" in r.stdout
 
 
-@pytest.mark.parametrize("kind", ["wave", "thread"])
+@pytest.mark.parametrize("kind", ["wave", "thread", "team"])
 def test_ivox_kernel_kinds_agree(ivctx, kind, monkeypatch):
-    """Both search kernels (chosen per launch by size; LIVO_IVOX_KIND forces
-    one) give the oracle's answer, in batch IEKF updates too."""
+    """Every search kernel (wave or team chosen per launch by size; LIVO_IVOX_KIND
+    forces one) gives the oracle's answer, in batch IEKF updates too."""
     import oracle
     synth = _synth()
     monkeypatch.setenv("LIVO_IVOX_KIND", kind)
