@@ -44,47 +44,62 @@ __device__ __forceinline__ double bcast(double v, int lane) {
 
 // PartialPivLU as the oracle (inverse18): first maximum |a_ik| over i >= k,
 // f = a_ik / a_kk, a_ij -= f * a_kj.  Row `lane` of the matrix is A; on return
-// LU (row-major 18x18) and the row permutation are in LDS.
+// LU (row-major N x N, rows in the swapped order) and the row permutation are
+// in LDS.  Rows never move between lanes: each lane keeps its row and its
+// position `pos` in the swapped order (a swap of rows k and p exchanges the two
+// lanes' positions), the pivot is a wave max-reduction of (|a_k|, -pos) over
+// the lanes at positions >= k (DPP within 16 lanes, one swizzle across), which
+// is the sequential scan's first maximum, and the pivot row -- final once
+// chosen -- is written to its place in s_LU, from where the lanes below read
+// it.  Every a_ij sees the same operations in the same order as with the rows
+// swapped in registers, so the factors are bit for bit those.
+__device__ __forceinline__ void lu_pick(double& v, int& pos, double ov, int op) {
+    // larger |a| wins; equal |a|: the smaller position (the scan's first maximum)
+    const bool take = ov > v || (ov == v && op < pos);
+    v = take ? ov : v;
+    pos = take ? op : pos;
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
 template <int N>
 __device__ __forceinline__ void wave_lu_to_lds(double (&A)[N], int lane, double* s_LU, int* s_piv) {
-    int piv = lane;
+    static_assert(N <= 32, "rows on lanes 0..31");
+    int pos = lane;
 #pragma unroll
     for (int k = 0; k < N; k++) {
-        // pivot: the first maximum of |a_ik| over i >= k, scanned in row order
-        // on wave-uniform copies of column k (v_readlane, no LDS round trips)
-        int p = k;
-        double best = fabs(bcast(A[k], k));
+        // pivot: the first maximum of |a_ik| over positions i >= k (NaN never
+        // replaces the running maximum: a NaN at position k keeps k, elsewhere it
+        // is skipped)
+        const bool live = lane < N && pos >= k;
+        const bool nan_at_k = __ballot(lane < N && pos == k && A[k] != A[k]) != 0ull;
+        double v = live && !(fabs(A[k]) != fabs(A[k])) ? fabs(A[k]) : -1.0;
+        int pp = live ? pos : 0x7fffffff;
+        lu_pick(v, pp, dpp_f64<0xB1>(v), dpp_i32<0xB1>(pp));   // quad_perm [1,0,3,2]
+        lu_pick(v, pp, dpp_f64<0x4E>(v), dpp_i32<0x4E>(pp));   // quad_perm [2,3,0,1]
+        lu_pick(v, pp, dpp_f64<0x141>(v), dpp_i32<0x141>(pp)); // row_half_mirror
+        lu_pick(v, pp, dpp_f64<0x140>(v), dpp_i32<0x140>(pp)); // row_mirror
+        lu_pick(v, pp, __shfl_xor(v, 16, 64), __shfl_xor(pp, 16, 64));
+        int p = __builtin_amdgcn_readfirstlane(pp);
+        if (nan_at_k) p = k;  // (a NaN at position k: the scan keeps k)
+        // swap positions k and p (wave-uniform), then the row now at k is the pivot
+        if (p != k) pos = pos == k ? p : (pos == p ? k : pos);
+        if (lane < N && pos == k) {
 #pragma unroll
-        for (int i = k + 1; i < N; i++) {
-            const double v = fabs(bcast(A[k], i));
-            if (v > best) {
-                best = v;
-                p = i;
-            }
+            for (int j = 0; j < N; j++) s_LU[k * N + j] = A[j];
+            s_piv[k] = lane;
         }
-        if (p != k) {  // wave-uniform: swap rows k and p, one element at a time
-            const int pk = __builtin_amdgcn_readlane(piv, k), pp = __builtin_amdgcn_readlane(piv, p);
-#pragma unroll
-            for (int j = 0; j < N; j++) {
-                const double ak = bcast(A[j], k), ap = bcast(A[j], p);
-                A[j] = lane == k ? ap : (lane == p ? ak : A[j]);
-            }
-            piv = lane == k ? pp : (lane == p ? pk : piv);
-        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // f = a_ik / a_kk, a_ij -= f * a_kj (rows below k)
-        const double f = A[k] / bcast(A[k], k);
-        const bool below = lane > k && lane < N;
-        if (below) A[k] = f;
+        if (lane < N && pos > k) {
+            const double f = A[k] / s_LU[k * N + k];
+            A[k] = f;
 #pragma unroll
-        for (int j = k + 1; j < N; j++) {
-            const double rkj = bcast(A[j], k);
-            if (below) A[j] = A[j] - f * rkj;
+            for (int j = k + 1; j < N; j++) A[j] = A[j] - f * s_LU[k * N + j];
         }
-    }
-    if (lane < N) {
-#pragma unroll
-        for (int j = 0; j < N; j++) s_LU[lane * N + j] = A[j];
-        s_piv[lane] = piv;
     }
 }
 

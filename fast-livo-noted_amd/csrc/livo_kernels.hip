@@ -3240,11 +3240,11 @@ struct IkSolveLds {
 };
 constexpr int kIkRow = 15;  // 12 row + h + |pd2| + keep
 
-// One wave, the part of esekfom.hpp:1638-1697 that does not depend on this
+// One wave, the part of esekfom.hpp:1638-1787 that does not depend on this
 // evaluation's measurements: dx = x_ boxminus x_propagated, P_ = P_propagated
-// with the SO3 / S2 corrections of dx_new and P_.  k_solve_ik runs it on its
-// last wave beside the other waves' reduction of the block partials.  The
-// information-form gain needs no (P_ / R)^-1 (ik_solve: Woodbury).
+// with the SO3 / S2 corrections of dx_new and P_ (:1638-1697), and (P_ / R)^-1
+// of the information-form gain (:1775-1777).  k_solve_ik runs it on its last
+// wave beside the other waves' reduction of the block partials.
 __device__ void ik_prep(const IekfSlot* slot, IkSolveLds& S, const int lane, const double R) {
     const IkBlock& K = slot->ik;
     constexpr int N = kIkDim;
@@ -3257,6 +3257,7 @@ __device__ void ik_prep(const IekfSlot* slot, IkSolveLds& S, const int lane, con
     WAVE_SYNC();
     SOLVE_MARK(3);
     // SO3 (idx 3, 6) and S2 (idx 21) corrections of dx_new and P_ (:1659-1697)
+#pragma unroll
     for (int b = 0; b < 3; b++) {
         const int idx = b == 0 ? 3 : (b == 1 ? 6 : 21), d = b == 2 ? 2 : 3;
         if (lane == 0) {
@@ -3294,11 +3295,23 @@ __device__ void ik_prep(const IekfSlot* slot, IkSolveLds& S, const int lane, con
         WAVE_SYNC();
     }
     SOLVE_MARK(4);
-    (void)R;
+    {
+        double A[N];
+        for (int j = 0; j < N; j++) A[j] = lane < N ? S.P[lane * N + j] / R : 0.0;
+        wave_lu_to_lds<N>(A, lane, S.LU, S.piv);
+        WAVE_SYNC();
+        if (lane < N) {
+            double y[N];
+            lds_lu_column<N>(S.LU, S.piv, lane, y);
+            for (int i = 0; i < N; i++) S.Pinv[i * N + lane] = y[i];
+        }
+        WAVE_SYNC();
+    }
+    SOLVE_MARK(5);
 }
 
 // One wave: esekfom.hpp:1701-1921 from the reduced sums in S.sum and the
-// evaluation's prep (ik_prep: S.dx, S.dxn, S.P).
+// evaluation's prep (ik_prep: S.dx, S.dxn, S.P, S.Pinv = (P_ / R)^-1).
 __device__ void ik_solve(IekfSlot* slot, const HsJob& job, IkSolveLds& S, const int lane, const double R) {
     IkBlock& K = slot->ik;
     const IekfCtrl ctrl0 = slot->ctrl;
@@ -3363,51 +3376,38 @@ __device__ void ik_solve(IekfSlot* slot, const HsJob& job, IkSolveLds& S, const 
         }
         WAVE_SYNC();
     } else {
-    // gain, information form (:1775-1787): K = P_temp^-1, P_temp = (P_/R)^-1 + HTH,
-    // of which only K(:, 0:12) is used (K_h = K HTh, K_x = K HTH: HTH is zero
-    // outside its 12 x 12 block C).  With A = P_ / R and U = [I12; 0],
-    // (A^-1 + U C U^T) A U (I12 + C A11)^-1 = U, so
-    //   K(:, 0:12) = A(:, 0:12) (I12 + C A(0:12, 0:12))^-1
-    // -- one 12 x 12 LU instead of two 23 x 23 inversions (the 18-dim solve's
-    // DESIGN.md §4.3 form); within 1e-5 of the oracle's inversions per step.
-    double* const M = S.Pinv;             // I12 + C A11, then its LU's inverse at M + 144
-    double* const Minv = S.Pinv + 144;
-    double* const K12 = S.L;              // K(:, 0:12), 23 x 12 (S.L is rebuilt for the covariance)
-    for (int t = lane; t < 144; t += 64) {
-        const int r = t / 12, c = t % 12;
-        double acc = hth(r, 0) * (S.P[0 * N + c] / R);
-        for (int k = 1; k < 12; k++) acc = acc + hth(r, k) * (S.P[k * N + c] / R);
-        M[t] = (r == c ? 1.0 : 0.0) + acc;
-    }
-    WAVE_SYNC();
+    // gain, information form (:1775-1787): P_temp = (P_/R)^-1 + HTH, P_inv = P_temp^-1.
+    // (The Woodbury form K(:, 0:12) = A(:, 0:12) (I12 + C A11)^-1 with A = P_ / R
+    // needs one 12x12 LU instead of two 23x23 inversions, but at converged steps
+    // dx = K_h + (K_x - I) dx_new cancels ~1e5-fold and shows its different
+    // rounding at 4e-5 of |dx| against the reference's inversions: kept exact.)
     {
-        double A[12];
-        for (int j = 0; j < 12; j++) A[j] = lane < 12 ? M[lane * 12 + j] : 0.0;
-        wave_lu_to_lds<12>(A, lane, S.LU, S.piv);
+        double A[N];
+        for (int t = lane; t < 144; t += 64) {
+            const int r = t / 12, c = t % 12;
+            const int a = r < c ? r : c, bb = r < c ? c : r;
+            S.Pinv[r * N + c] += S.sum[a * 12 - (a * (a - 1)) / 2 + (bb - a)];
+        }
+        WAVE_SYNC();
+        for (int j = 0; j < N; j++) A[j] = lane < N ? S.Pinv[lane * N + j] : 0.0;
+        wave_lu_to_lds<N>(A, lane, S.LU, S.piv);
+        WAVE_SYNC();
+        if (lane < N) {
+            double y[N];
+            lds_lu_column<N>(S.LU, S.piv, lane, y);
+            for (int i = 0; i < N; i++) S.Pinv[i * N + lane] = y[i];
+        }
+        WAVE_SYNC();
     }
-    WAVE_SYNC();
-    if (lane < 12) {
-        double y[12];
-        lds_lu_column<12>(S.LU, S.piv, lane, y);
-        for (int i = 0; i < 12; i++) Minv[i * 12 + lane] = y[i];
-    }
-    WAVE_SYNC();
-    for (int t = lane; t < N * 12; t += 64) {
-        const int r = t / 12, c = t % 12;
-        double acc = (S.P[r * N + 0] / R) * Minv[0 * 12 + c];
-        for (int k = 1; k < 12; k++) acc = acc + (S.P[r * N + k] / R) * Minv[k * 12 + c];
-        K12[t] = acc;
-    }
-    WAVE_SYNC();
     SOLVE_MARK(6);
     if (lane < N) {
         const int r = lane;
-        double kh = K12[r * 12] * S.sum[78];
-        for (int c = 1; c < 12; c++) kh = kh + K12[r * 12 + c] * S.sum[78 + c];
+        double kh = S.Pinv[r * N] * S.sum[78];
+        for (int c = 1; c < 12; c++) kh = kh + S.Pinv[r * N + c] * S.sum[78 + c];
         S.Kh[r] = kh;
         for (int c = 0; c < 12; c++) {
-            double a2 = K12[r * 12] * hth(0, c);
-            for (int k = 1; k < 12; k++) a2 = a2 + K12[r * 12 + k] * hth(k, c);
+            double a2 = S.Pinv[r * N] * hth(0, c);
+            for (int k = 1; k < 12; k++) a2 = a2 + S.Pinv[r * N + k] * hth(k, c);
             S.Kx[r * 12 + c] = a2;
         }
     }
@@ -3464,6 +3464,7 @@ __device__ void ik_solve(IekfSlot* slot, const HsJob& job, IkSolveLds& S, const 
     // covariance (:1838-1921): L_ = P_ with the corrections at dx_, P_ = L_ - K_x(:,0:12) P_(0:12,:)
     for (int t = lane; t < N * N; t += 64) S.L[t] = S.P[t];
     WAVE_SYNC();
+#pragma unroll
     for (int b = 0; b < 3; b++) {
         const int idx = b == 0 ? 3 : (b == 1 ? 6 : 21), d = b == 2 ? 2 : 3;
         if (lane == 0) {
