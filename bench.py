@@ -377,7 +377,8 @@ def main():
     # from host arrays (four distinct batches of the pool, cycled) through
     # livo_scan_upload_async two batches ahead of their submit, overlapping the
     # batches in flight, and are released once collected; untimed for value.
-    n_up = min(4, len(pool_scans) // a.batch)
+    # (an A/B build from before livo_scan_upload_async skips this leg)
+    n_up = min(4, len(pool_scans) // a.batch) if hasattr(ctx._L, "livo_scan_upload_async") else 0
     up_sets = [(pool_scans[b * a.batch:(b + 1) * a.batch], batches[b][1]) for b in range(n_up)]
 
     def pipeline_upload(nsteps, counters=None):

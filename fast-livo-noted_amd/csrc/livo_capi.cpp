@@ -207,7 +207,10 @@ struct livo_ctx {
     // 18.3k vs 17.1k / 17.1k vs 16.4k updates/s against 0, one range per XCD, whose
     // most expensive scan's XCD was the straggler; profiles/r04_ab_block_order.txt)
     int xcd_chunk = 8;
-    int ns_k = 4;                      // evaluations without a search: chunks per block (LIVO_NS_K)
+    // evaluations without a search: 256-point chunks per block (LIVO_NS_K).  1: four
+    // measured slower (pooled 21.8k vs 24.5k updates/s, eval_nosearch 0.187 vs 0.161 ms per
+    // step, profiles/r05_ab_ns_k.txt): fewer blocks each with a serial chain of chunks
+    int ns_k = 1;
     GridSlot* vslots = nullptr;        // vertex runs (static map only)
     RunWord* vpts = nullptr;           // run entries (LIVO_IDX_RUNS: grid positions; else x, y, z, map index bits)
     int32_t vlog2 = 0;
@@ -3843,6 +3846,7 @@ int livo_sync(livo_ctx* c) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     for (const BatchLane& B : c->lane)  // submitted batches run on their lanes' streams
         for (int k = 0; k < kMaxGroups && B.st[k]; k++) HIP_TRY(hipStreamSynchronize(B.st[k]));
+    if (c->up_stream) HIP_TRY(hipStreamSynchronize(c->up_stream));  // asynchronous uploads
     return LIVO_OK;
 }
 
