@@ -76,11 +76,12 @@ __device__ __forceinline__ void wave_lu_to_lds(double (&A)[N], int lane, double*
         const bool nan_at_k = __ballot(lane < N && pos == k && A[k] != A[k]) != 0ull;
         double v = live && !(fabs(A[k]) != fabs(A[k])) ? fabs(A[k]) : -1.0;
         int pp = live ? pos : 0x7fffffff;
-        lu_pick(v, pp, dpp_f64<0xB1>(v), dpp_i32<0xB1>(pp));   // quad_perm [1,0,3,2]
-        lu_pick(v, pp, dpp_f64<0x4E>(v), dpp_i32<0x4E>(pp));   // quad_perm [2,3,0,1]
-        lu_pick(v, pp, dpp_f64<0x141>(v), dpp_i32<0x141>(pp)); // row_half_mirror
-        lu_pick(v, pp, dpp_f64<0x140>(v), dpp_i32<0x140>(pp)); // row_mirror
-        lu_pick(v, pp, __shfl_xor(v, 16, 64), __shfl_xor(pp, 16, 64));
+        // (only the steps the rows' lanes need: lanes 0..N-1)
+        lu_pick(v, pp, dpp_f64<0xB1>(v), dpp_i32<0xB1>(pp));                      // quad_perm [1,0,3,2]
+        if (N > 2) lu_pick(v, pp, dpp_f64<0x4E>(v), dpp_i32<0x4E>(pp));           // quad_perm [2,3,0,1]
+        if (N > 4) lu_pick(v, pp, dpp_f64<0x141>(v), dpp_i32<0x141>(pp));         // row_half_mirror
+        if (N > 8) lu_pick(v, pp, dpp_f64<0x140>(v), dpp_i32<0x140>(pp));         // row_mirror
+        if (N > 16) lu_pick(v, pp, __shfl_xor(v, 16, 64), __shfl_xor(pp, 16, 64));
         int p = __builtin_amdgcn_readfirstlane(pp);
         if (nan_at_k) p = k;  // (a NaN at position k: the scan keeps k)
         // swap positions k and p (wave-uniform), then the row now at k is the pivot

@@ -34,6 +34,10 @@
 #include "device_common.h"
 #include "device_linalg.h"
 
+#if defined(LIVO_EVAL_PROF) && !defined(LIVO_TAIL_PROF)
+#define LIVO_TAIL_PROF  // the tail / solve phase marks alone: no per-block atomics (tools/tail_prof.py)
+#endif
+
 namespace livo {
 
 // ========================================================= IKFoM path =====
@@ -2210,7 +2214,7 @@ __device__ unsigned long long g_solve_prof[256][16];
 #else
 #define SOLVE_MARK(k) do { } while (0)
 #endif
-#ifdef LIVO_EVAL_PROF  // solve_scan's phases summed per evaluation kind (tools/eval_prof.py)
+#ifdef LIVO_TAIL_PROF  // solve_scan's phases summed per evaluation kind (tools/eval_prof.py)
 __device__ unsigned long long g_solve_ph[3][16];
 #define SPH_MARK(k)                                                                                     \
     do {                                                                                               \
@@ -2295,7 +2299,7 @@ static_assert(sizeof(IekfCtrl) == 8 * sizeof(int) && alignof(IekfSlot) >= 16 && 
 // a wave-level fence, not a block barrier.  Returns EKF_stop_flg (uniform).
 template <bool SPLIT_VEC = false>
 __device__ __forceinline__ int solve_scan(IekfSlot* slot, SolveLds& L, const int lane, int pk = -1) {
-#ifdef LIVO_EVAL_PROF
+#ifdef LIVO_TAIL_PROF
     unsigned long long sph_t = __builtin_amdgcn_s_memtime();
 #else
     (void)pk;
@@ -2440,7 +2444,7 @@ __device__ __forceinline__ int solve_scan(IekfSlot* slot, SolveLds& L, const int
         }
     }
     SOLVE_MARK(9);
-#ifdef LIVO_EVAL_PROF
+#ifdef LIVO_TAIL_PROF
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
     SPH_MARK(7);
@@ -2681,7 +2685,7 @@ __device__ __forceinline__ void hs_row_sums_bfly(const Col& col, HsReduceLds& R,
     if (base + 1 < NU) R.red[(tid >> 4) * kRedCols + base + 1] = x[1];
 }
 
-#ifdef LIVO_EVAL_PROF  // the reduction's phases (tools/eval_prof.py; compiled out of the product)
+#ifdef LIVO_TAIL_PROF  // the reduction's phases (tools/eval_prof.py; compiled out of the product)
 // [kind][k]: 0 blocks, 1 butterfly + partial store + ticket (every block), 2 last block: the
 // partials' reduction, 3 solve, 4 host slot write, 5 last blocks
 __device__ unsigned long long g_tail_prof[3][8];
@@ -2703,6 +2707,17 @@ __device__ unsigned long long g_tail_prof[3][8];
 #define LIVO_RED_INFLIGHT 32
 #endif
 constexpr int kRedInFlight = LIVO_RED_INFLIGHT;  // partial loads in flight per thread of the last block
+// The scan's slot into the host-mapped staging copy, by threads t of nt: read
+// back past the L1 (sc1: this CU's other waves stored it, drained to L2).
+__device__ __forceinline__ void hs_host_slot(const HsJob& job, const IekfSlot* slot, int t, int nt) {
+    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(slot);
+    for (int w = t; w < (int)((kSlotLmBytes + 15) / 16); w += nt) {
+        const unsigned long long lo = __hip_atomic_load(src + 2 * w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long hi = __hip_atomic_load(src + 2 * w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        job.host_slot[w] = make_uint4((unsigned)lo, (unsigned)(lo >> 32), (unsigned)hi, (unsigned)(hi >> 32));
+    }
+}
+
 // The block partial of one 256-point chunk (blk): the row butterflies into R.red,
 // then wave 0's fixed pairwise tree over the rows, stored write-through (sc1).
 // Ends with wave 0's stores issued; a caller that reuses R.red must barrier first.
@@ -2738,7 +2753,7 @@ __device__ __forceinline__ void hs_ticket_tail(const HsParams& P, const HsJob& j
                                                unsigned count, HsReduceLds& R, SolveLds& L, int pk = -1) {
     static_assert(NU == kRedUsed || NU == kRedUsed + 2, "h_share sums (+ search counts)");
     const int tid = threadIdx.x;
-#ifdef LIVO_EVAL_PROF
+#ifdef LIVO_TAIL_PROF
     unsigned long long tp = __builtin_amdgcn_s_memtime();
     if (pk >= 0 && tid == 0) atomicAdd(&g_tail_prof[pk][0], 1ull);
 #else
@@ -2763,7 +2778,7 @@ __device__ __forceinline__ void hs_ticket_tail(const HsParams& P, const HsJob& j
     // the scan's serial tail (reduction, solve) ahead of the other waves on its SIMDs
     __builtin_amdgcn_s_setprio(3);
 #endif
-#ifdef LIVO_EVAL_PROF
+#ifdef LIVO_TAIL_PROF
     if (pk >= 0 && tid == 0) atomicAdd(&g_tail_prof[pk][5], 1ull);
 #endif
     const bool solve = P.solve != 0;  // (kernel parameter: uniform)
@@ -2791,11 +2806,16 @@ __device__ __forceinline__ void hs_ticket_tail(const HsParams& P, const HsJob& j
         R.fin[g * kRedCols + c] = acc;
     }
     __syncthreads();  // the block partials' sums and the staged inputs
+    const bool wb = solve && job.host_slot != nullptr;  // (uniform) the stopping solve writes the host's slot
     if (tid >= 64) {
         // vec = state_propagat - state beside wave 0's M and LU; then the one barrier
         // solve_scan<true> waits at before it uses vec
         if (solve && tid == 64) state_minus_d(L.pr, L.st, L.vec);
         if (solve) __syncthreads();
+        if (wb) {
+            __syncthreads();  // wave 0's solve and its slot stores are done
+            if (L.ctrl.stop) hs_host_slot(job, slot, tid, NT);
+        }
         return;
     }
     TAIL_MARK(2, tp);
@@ -2829,19 +2849,15 @@ __device__ __forceinline__ void hs_ticket_tail(const HsParams& P, const HsJob& j
     WAVE_SYNC();
     solve_scan<true>(slot, L, tid, pk);
     TAIL_MARK(3, tp);
-    if (job.host_slot && L.ctrl.stop) {
+    if (wb) {
         // the solve that stops the scan writes its slot straight into the host's
-        // staging copy (no copy back after the batch's last evaluation): this wave's
-        // slot stores drained to L2, then read back past the L1 (sc1)
+        // staging copy (no copy back after the batch's last evaluation), the
+        // whole block sharing it: wave 0's slot stores drained to L2 first
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned long long* src = reinterpret_cast<const unsigned long long*>(slot);
-        for (int w = tid; w < (int)((kSlotLmBytes + 15) / 16); w += 64) {
-            const unsigned long long lo = __hip_atomic_load(src + 2 * w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const unsigned long long hi = __hip_atomic_load(src + 2 * w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            job.host_slot[w] = make_uint4((unsigned)lo, (unsigned)(lo >> 32), (unsigned)hi, (unsigned)(hi >> 32));
-        }
+        __syncthreads();
+        if (L.ctrl.stop) hs_host_slot(job, slot, tid, NT);
     }
-#ifdef LIVO_EVAL_PROF
+#ifdef LIVO_TAIL_PROF
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
     TAIL_MARK(4, tp);
@@ -3202,7 +3218,7 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
         else if constexpr (j == kRedUsed) return (double)n_slots;
         else return (double)n_pts;
     };
-#ifdef LIVO_EVAL_PROF
+#ifdef LIVO_TAIL_PROF
     const int pk = FIRST ? 2 : (search ? 1 : 0);
 #else
     const int pk = -1;
@@ -3887,21 +3903,7 @@ int launch_knn_grid(const KnnParams& p, int n_jobs, int64_t max_n, bool seeded, 
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 
-// per-phase profile of k_iekf_eval (LIVO_EVAL_PROF builds only): out[24], reset after reading
-#ifdef LIVO_EVAL_PROF
-// Profiling builds only (not part of livo.h): per-phase block cycles of the
-// fused evaluation since the last call (tools/eval_prof.py).
-extern "C" int livo_debug_eval_timeline(unsigned long long* out, int64_t bytes) {  // LIVO_MAX_EVALS x kTlBlocks x 2
-    if (bytes != (int64_t)sizeof(g_eval_tl)) return LIVO_E_INVALID;
-    if (hipDeviceSynchronize() != hipSuccess) return LIVO_E_HIP;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_eval_tl), sizeof(g_eval_tl)) == hipSuccess ? LIVO_OK : LIVO_E_HIP;
-}
-extern "C" int livo_debug_eval_prof(unsigned long long* out) {
-    if (hipDeviceSynchronize() != hipSuccess) return LIVO_E_HIP;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_eval_prof), sizeof(g_eval_prof)) != hipSuccess) return LIVO_E_HIP;
-    static const unsigned long long zero[24] = {};
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_eval_prof), zero, sizeof(zero)) == hipSuccess ? LIVO_OK : LIVO_E_HIP;
-}
+#ifdef LIVO_TAIL_PROF
 // s_memtime ticks per s_memrealtime tick (100 MHz): the phase marks' clock
 __global__ void k_clock_cal(unsigned long long* out, int iters) {
     const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
@@ -3927,6 +3929,23 @@ extern "C" int livo_debug_tail_prof(unsigned long long* out) {  // [3][8] tail, 
     unsigned long long zero[3][16] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_solve_ph), zero, sizeof(g_solve_ph)) != hipSuccess) return LIVO_E_HIP;
     return hipMemcpyToSymbol(HIP_SYMBOL(g_tail_prof), zero, sizeof(g_tail_prof)) == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+#endif
+
+// per-phase profile of k_iekf_eval (LIVO_EVAL_PROF builds only): out[24], reset after reading
+#ifdef LIVO_EVAL_PROF
+// Profiling builds only (not part of livo.h): per-phase block cycles of the
+// fused evaluation since the last call (tools/eval_prof.py).
+extern "C" int livo_debug_eval_timeline(unsigned long long* out, int64_t bytes) {  // LIVO_MAX_EVALS x kTlBlocks x 2
+    if (bytes != (int64_t)sizeof(g_eval_tl)) return LIVO_E_INVALID;
+    if (hipDeviceSynchronize() != hipSuccess) return LIVO_E_HIP;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_eval_tl), sizeof(g_eval_tl)) == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+extern "C" int livo_debug_eval_prof(unsigned long long* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return LIVO_E_HIP;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_eval_prof), sizeof(g_eval_prof)) != hipSuccess) return LIVO_E_HIP;
+    static const unsigned long long zero[24] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_eval_prof), zero, sizeof(zero)) == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 extern "C" int livo_debug_amb_reason(unsigned long long* out) {
     if (hipDeviceSynchronize() != hipSuccess) return LIVO_E_HIP;

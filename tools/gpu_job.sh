@@ -10,6 +10,7 @@
 #   c5ab=SPEC,SPEC..      config-5 leg per variant (tools/c5_ab.sh)
 #   kt[=ARGS]             rocprofv3 --kernel-trace --stats over bench.py ARGS
 #                         (default: the headline leg, 20 steps)
+#   ktpy=SCRIPT ARGS      rocprofv3 --kernel-trace --stats over python3 SCRIPT ARGS (repo-relative script)
 #   pmc_eval              PMC passes over the first evaluation (tools/pmc_eval.sh)
 #   pmc_c5                PMC passes over the config-5 batch (tools/pmc_c5.sh)
 #   py=SCRIPT ARGS        python SCRIPT ARGS (any lab/probe script), 200 s limit
@@ -46,6 +47,9 @@ for step in "$@"; do
       a=${arg:-"--legs headline --steps 20 --warmup 3 --cpu-seconds 0 --pmc off"}
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
           -d "$OUT/kt$n" -o kt -- python3 "$R/bench.py" $a) > "$log" 2>&1 || { tail -30 "$log"; exit 1; } ;;
+    ktpy)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+          -d "$OUT/kt$n" -o kt -- python3 $(echo "$arg" | sed "s|^|$R/|")) > "$log" 2>&1 || { tail -30 "$log"; exit 1; } ;;
     pmc_eval)
       bash tools/pmc_eval.sh "$OUT/pmc$n" > "$log" 2>&1 || { tail -30 "$log"; exit 1; } ;;
     pmc_c5)
