@@ -211,6 +211,11 @@ struct livo_ctx {
     // measured slower (pooled 21.8k vs 24.5k updates/s, eval_nosearch 0.187 vs 0.161 ms per
     // step, profiles/r05_ab_ns_k.txt): fewer blocks each with a serial chain of chunks
     int ns_k = 1;
+    // the evaluations without a search in one persistent launch per run of them
+    // (k_iekf_ns: F, P, E, P per group instead of one launch per evaluation);
+    // LIVO_PERSIST=0 / LIVO_NS_TEAM (workers per scan)
+    int persist = 0;  // measured slower at every team size: profiles/r05_ab_persist.txt
+    int ns_team = 48;
     GridSlot* vslots = nullptr;        // vertex runs (static map only)
     RunWord* vpts = nullptr;           // run entries (LIVO_IDX_RUNS: grid positions; else x, y, z, map index bits)
     int32_t vlog2 = 0;
@@ -368,7 +373,11 @@ constexpr size_t kLmStride = (kSlotLmBytes + 255) & ~(size_t)255;
 static_assert(kLmStride % alignof(HsJob) == 0 && kLmStride % alignof(IekfSlot) == 0, "packed slot alignment");
 static_assert(kLmStride % 16 == 0, "kernel staging copies move 16-B words");
 // bytes of a batch's packed staging area, rounded up to whole 16-B words
-static size_t lm_bytes(int32_t n) { return ((size_t)n * (kLmStride + sizeof(HsJob)) + 15) & ~(size_t)15; }
+// Then the persistent evaluations' team counters (two launches per group),
+// zeroed in the host copy so the staging copy clears them too.
+constexpr int kTeamCtrs = 2 * kMaxGroups;
+static size_t lm_team_off(int32_t n) { return ((size_t)n * (kLmStride + sizeof(HsJob)) + 15) & ~(size_t)15; }
+static size_t lm_bytes(int32_t n) { return (lm_team_off(n) + sizeof(unsigned) * kTeamCtrs + 15) & ~(size_t)15; }
 static int ensure_lm(BatchLane& B, int32_t n) {
     const size_t need = lm_bytes(n);
     if (need <= B.lm_cap) return LIVO_OK;
@@ -1529,6 +1538,8 @@ int livo_ctx_create(int device, const livo_params* p, livo_ctx** out) {
     if (const char* env = std::getenv("LIVO_SLOT_WB")) c->slot_wb = std::atoi(env) != 0;
     if (const char* env = std::getenv("LIVO_XCD_CHUNK")) c->xcd_chunk = std::max(0, std::atoi(env));  // tuning knob
     if (const char* env = std::getenv("LIVO_NS_K")) c->ns_k = std::max(1, std::atoi(env));  // tuning knob
+    if (const char* env = std::getenv("LIVO_PERSIST")) c->persist = std::atoi(env) != 0;
+    if (const char* env = std::getenv("LIVO_NS_TEAM")) c->ns_team = std::max(1, std::atoi(env));
     if (const char* env = std::getenv("LIVO_GRID_PPC")) {  // tuning knob
         const float v = (float)std::atof(env);
         if (v > 0.f) c->grid_ppc = v;
@@ -2847,11 +2858,17 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
     // kernel copies for batches queued behind another on shared streams (a DMA
     // copy there waits on an engine hand-off); LIVO_LANE_ZC=0: DMA copies always
     const bool kcopy = lm && B.h_lm_dev && (sync ? c->sync_zc : c->lane_zc);
+    const bool persist = fused && lm && c->persist && !full && max_iter + 1 >= 2;
+    unsigned* dteam = nullptr;
+    if (persist) {  // (before the staging copy below: it clears the device counters)
+        std::memset(B.h_lm + lm_team_off(n), 0, sizeof(unsigned) * kTeamCtrs);
+        dteam = reinterpret_cast<unsigned*>(B.d_lm + lm_team_off(n));
+    }
     if (lm && kcopy) {
         rc = launch_copy_words(B.h_lm_dev, B.d_lm, lm_bytes(n), B.st[0]);
         if (rc) return rc;
     } else if (lm) {
-        HIP_TRY(hipMemcpyAsync(B.d_lm, B.h_lm, (size_t)n * (kLmStride + sizeof(HsJob)), hipMemcpyHostToDevice,
+        HIP_TRY(hipMemcpyAsync(B.d_lm, B.h_lm, lm_bytes(n), hipMemcpyHostToDevice,
                                B.st[0]));
     } else {
         HIP_TRY(hipMemcpyAsync(c->d_slots, c->h_slots, sizeof(IekfSlot) * n, hipMemcpyHostToDevice, c->stream));
@@ -2915,12 +2932,22 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
         hp[gi].solve = lm ? 1 : 0;  // the last plane-pass block of each scan runs its solve (IKFoM: k_solve_ik below)
         hp[gi].replay_count = c->d_replay_count + gi;
     }
-    for (int e = 0; e < evals; e++) {
+    // Persistent: the first evaluation (search), then the run of evaluations without
+    // one (k_iekf_ns), the one search a rematch asks for (k_iekf_eval: the solve
+    // sets nearest_search_en at most once more, :226-233, the second rematch stops
+    // the scan) and the run after it: F, P, E, P whatever the convergence.  A
+    // launch whose scans all stopped exits at once.
+    const int launches = persist ? 4 : evals;
+    for (int e = 0; e < launches; e++) {
         for (int gi = 0; gi < ngroups && fused; gi++) {
             hipStream_t st = g[gi].st;
             // full: ev[gi][e] before evaluation e, ev[gi][evals] after the last
             if (full && (e > 0 || gi > 0)) HIP_TRY(hipEventRecord(c->ev[gi][e], st));
-            rc = launch_iekf_eval(kp[gi], hp[gi], g[gi].count, g[gi].max_n, e == 0, st);
+            if (persist && (e & 1))
+                rc = launch_iekf_ns(kp[gi], hp[gi], g[gi].count, ns_team_size(g[gi].max_n, c->ns_team),
+                                    dteam + 2 * gi + (e >> 1), st);
+            else
+                rc = launch_iekf_eval(kp[gi], hp[gi], g[gi].count, g[gi].max_n, e == 0, st);
             if (rc) return rc;
             if (prof && !full && e == 0) HIP_TRY(hipEventRecord(c->ev[gi][1], st));
         }

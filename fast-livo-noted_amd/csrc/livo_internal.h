@@ -250,7 +250,8 @@ struct alignas(16) IekfSlot {
     int32_t eval_search[LIVO_MAX_EVALS];
     unsigned hs_ticket;         // k_hshare blocks done in the current pass (the last one reduces)
     int32_t model;              // SlotModel
-    unsigned pad_[2];
+    unsigned gen;               // k_iekf_ns: evaluations published by its solves (the teams poll it)
+    unsigned pad_;
     IkBlock ik;                 // model == kModelIkfom (last: the LaserMapping model copies only the part before it)
 };
 constexpr size_t kSlotLmBytes = offsetof(IekfSlot, ik);  // bytes of a slot the LaserMapping model reads / writes
@@ -386,6 +387,12 @@ int launch_hshare(const HsParams& p, int n_jobs, int max_nblk, bool first, void*
 #endif
 constexpr int kEvalBlock = LIVO_EVAL_BLOCK;  // threads (points) per block of k_iekf_eval
 int launch_iekf_eval(const KnnParams& kp, const HsParams& hp, int n_jobs, int64_t max_n, bool first, void* stream);
+// The evaluations without a search of a group in one persistent launch (k_iekf_ns):
+// team_ctr zeroed before it; LIVO_E_RANGE when the scans are too large for it.
+// k_iekf_ns: the evaluations without a search, persistent (team of T workers + a
+// solver per scan; team_ctr zeroed before the launch).  T from ns_team_size.
+int ns_team_size(int64_t max_n, int team);
+int launch_iekf_ns(const KnnParams& kp, const HsParams& hp, int n_jobs, int T, unsigned* team_ctr, void* stream);
 int launch_solve_ik(const HsParams& p, int n_jobs, void* stream);
 int launch_copy_words(const void* src, void* dst, size_t bytes, void* stream);  // 16-B aligned, bytes % 16 == 0
 // IKFoM plane pass (12-wide rows) with the manifold update in each scan's last block.

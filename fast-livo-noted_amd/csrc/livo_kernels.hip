@@ -2258,6 +2258,15 @@ __device__ __forceinline__ double ld_sc1(const double* p) {
 __device__ __forceinline__ int ld_sc1(const int* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ unsigned long long ld_sc1(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Write-through (sc1) stores of the slot's fields: the persistent evaluation
+// loop (k_iekf_ns) reads them from other CUs inside one launch.
+template <class T>
+__device__ __forceinline__ void st_sc1(T* p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // Stage the solve's inputs (cov, state and prior heads, control, knn_passes)
 // into L: thread t of nt, two loads in flight per thread before any LDS store.
@@ -2279,12 +2288,14 @@ __device__ __forceinline__ void solve_stage(const IekfSlot* slot, SolveLds& L, i
         if (k1 < nD) *dst(k1) = v1;
     }
     if (t == nt - 1) {
-        const int4* c = reinterpret_cast<const int4*>(&slot->ctrl);
-        const int4 c0 = c[0], c1 = c[1];
-        const int kp = slot->stats.knn_passes;
-        int4* d = reinterpret_cast<int4*>(&L.ctrl);
+        const unsigned long long* c = reinterpret_cast<const unsigned long long*>(&slot->ctrl);
+        const unsigned long long c0 = ld_sc1(c), c1 = ld_sc1(c + 1), c2 = ld_sc1(c + 2), c3 = ld_sc1(c + 3);
+        const int kp = ld_sc1(&slot->stats.knn_passes);
+        unsigned long long* d = reinterpret_cast<unsigned long long*>(&L.ctrl);
         d[0] = c0;
         d[1] = c1;
+        d[2] = c2;
+        d[3] = c3;
         L.knn_passes = kp;
     }
 }
@@ -2412,8 +2423,9 @@ __device__ __forceinline__ int solve_scan(IekfSlot* slot, SolveLds& L, const int
     WAVE_SYNC();
     SOLVE_MARK(8);
     SPH_MARK(6);
-    // stores: state head, statistics, control
-    if (lane < kStHead) slot->state.rot[lane] = L.st.rot[lane];
+    // stores: state head, statistics, control (the state and control write-through:
+    // k_iekf_ns's teams read them inside the launch)
+    if (lane < kStHead) st_sc1(slot->state.rot + lane, L.st.rot[lane]);
     livo_iter_stats& S = slot->stats;
     if (e < LIVO_MAX_EVALS) {
         if (lane < kDim) S.solution[e][lane] = L.sol[lane];
@@ -2425,13 +2437,13 @@ __device__ __forceinline__ int solve_scan(IekfSlot* slot, SolveLds& L, const int
     }
     if (lane == 0) {
         S.iterations = e + 1;
-        S.knn_passes = L.knn_passes + (ctrl0.search_en ? 1 : 0);
+        st_sc1(&S.knn_passes, L.knn_passes + (ctrl0.search_en ? 1 : 0));
         S.converged = L.ctrl.converged;
         S.rematch_num = L.ctrl.rematch_num;
     }
-    if (lane < 2) {  // the control block as two 16-B stores
-        const int4 c = reinterpret_cast<const int4*>(&L.ctrl)[lane];
-        reinterpret_cast<int4*>(&slot->ctrl)[lane] = c;
+    if (lane < 4) {  // the control block as four 8-B stores
+        const unsigned long long c = reinterpret_cast<const unsigned long long*>(&L.ctrl)[lane];
+        st_sc1(reinterpret_cast<unsigned long long*>(&slot->ctrl) + lane, c);
     }
     // 9. covariance update state.cov = (I - G) * state.cov (:224-227) = P - G(:,0:6) P(0:6,:)
     if (stop_now) {
@@ -2440,7 +2452,7 @@ __device__ __forceinline__ int solve_scan(IekfSlot* slot, SolveLds& L, const int
             double gp = L.G6[i * 6 + 0] * s_P[0 * kDim + j];
 #pragma unroll
             for (int l = 1; l < 6; l++) gp = gp + L.G6[i * 6 + l] * s_P[l * kDim + j];
-            slot->state.cov[t] = s_P[t] - gp;
+            st_sc1(slot->state.cov + t, s_P[t] - gp);
         }
     }
     SOLVE_MARK(9);
@@ -2552,8 +2564,11 @@ __device__ __forceinline__ uint8_t fit_plane(const HsParams& P, const HsJob& job
     return ps;
 }
 
-__device__ __forceinline__ void hshare_point(const HsParams& P, const HsJob& job, const livo_state& S, int i,
-                                             int search, HsRow& w, const HsPointIn& in, bool prefit = false) {
+// St: livo_state or a staged StateHead (only rot and pos are read).  A plane
+// fitted here (plane state 0) also updates `in`, the caller's copy of the cache.
+template <class St, bool NOFIT = false>
+__device__ __forceinline__ void hshare_point(const HsParams& P, const HsJob& job, const St& S, int i,
+                                             int search, HsRow& w, HsPointIn& in, bool prefit = false) {
             const float4 pb = in.pb;
             const double* R = S.rot;
             float wx, wy, wz;
@@ -2572,7 +2587,7 @@ __device__ __forceinline__ void hshare_point(const HsParams& P, const HsJob& job
             // prefit: the fused search already fitted this evaluation's plane
             // from its neighbours in registers (in.ps / in.plane, fit_plane)
             uint8_t ps = (search && !prefit) ? 0 : in.ps;
-            if (ps == 0 && !prefit) {
+            if (!NOFIT && ps == 0 && !prefit) {  // (NOFIT: the caller fitted every plane state 0 beforehand)
                 const float4* rec = reinterpret_cast<const float4*>(job.nn + i);
                 float4 nb[kNN];
     #pragma unroll
@@ -2582,6 +2597,8 @@ __device__ __forceinline__ void hshare_point(const HsParams& P, const HsJob& job
                 ps = fit_plane(P, job, i, search, nb, cnt, pl);
                 plane_ok = ps == 2;
                 pa[0] = pl.x; pa[1] = pl.y; pa[2] = pl.z; pa[3] = pl.w;
+                in.ps = ps;
+                in.plane = pl;
             } else if (ps == 2) {
                 const float4 v = in.plane;
                 pa[0] = v.x; pa[1] = v.y; pa[2] = v.z; pa[3] = v.w;
@@ -2744,6 +2761,14 @@ __device__ __forceinline__ void hs_block_partial(const HsJob& job, const Col& co
     }
 }
 
+template <int NT, int NU>
+__device__ __forceinline__ void hs_scan_tail(const HsParams& P, const HsJob& job, IekfSlot* slot, int nblk,
+                                             HsReduceLds& R, SolveLds& L, int pk
+#ifdef LIVO_TAIL_PROF
+                                             , unsigned long long tp
+#endif
+);
+
 // Block partials of a scan's h_share sums -> the last block of the scan
 // reduces every partial in a fixed order and (P.solve) its wave 0 runs the
 // scan's solve.  nblk = partials (256-point chunks) of the scan in this launch;
@@ -2774,6 +2799,23 @@ __device__ __forceinline__ void hs_ticket_tail(const HsParams& P, const HsJob& j
     __syncthreads();
     TAIL_MARK(1, tp);
     if (!R.last) return;
+#ifdef LIVO_TAIL_PROF
+    hs_scan_tail<NT, NU>(P, job, slot, nblk, R, L, pk, tp);
+#else
+    hs_scan_tail<NT, NU>(P, job, slot, nblk, R, L, pk);
+#endif
+}
+
+// The scan's tail once every partial of it is stored: the fixed-order reduction,
+// then (P.solve) wave 0's solve and the host slot copy of a stopping solve.
+template <int NT, int NU>
+__device__ __forceinline__ void hs_scan_tail(const HsParams& P, const HsJob& job, IekfSlot* slot, int nblk,
+                                             HsReduceLds& R, SolveLds& L, int pk
+#ifdef LIVO_TAIL_PROF
+                                             , unsigned long long tp
+#endif
+) {
+    const int tid = threadIdx.x;
 #if LIVO_SOLVE_PRIO
     // the scan's serial tail (reduction, solve) ahead of the other waves on its SIMDs
     __builtin_amdgcn_s_setprio(3);
@@ -2844,7 +2886,7 @@ __device__ __forceinline__ void hs_ticket_tail(const HsParams& P, const HsJob& j
         L.sum[tid] = v;
         slot->red[tid] = v;
     }
-    if (tid == 0) slot->hs_ticket = 0u;  // ready for the next pass
+    if (tid == 0) st_sc1(&slot->hs_ticket, 0u);  // ready for the next pass (atomics see it)
     if (!solve) return;  // livo_h_share: the sums only
     WAVE_SYNC();
     solve_scan<true>(slot, L, tid, pk);
@@ -2897,7 +2939,8 @@ __global__ __launch_bounds__(kBlock) void k_hshare(HsParams P) {
         if (i < job.n) {
             HsRow w;
             hs_row_clear(w);
-            hshare_point(P, job, S, i, search, w, hshare_load(job, i, !search));
+            HsPointIn in = hshare_load(job, i, !search);
+            hshare_point(P, job, S, i, search, w, in);
             hs_accumulate(acc, w, P.inv_r);
         }
     }
@@ -3231,6 +3274,215 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
         g_eval_tl[tl_e][blockIdx.x][1] = __builtin_amdgcn_s_memtime();
     }
 #endif
+}
+
+// ============================================ persistent evaluations =====
+// k_iekf_ns<K>: the evaluations WITHOUT a search of a group's scans in one
+// launch (laser_mapping.cpp:178-237 with nearest_search_en false: the plane of
+// the last search reused, residual gates, Jacobian, HᵀH / HᵀL, solve), as
+// many as the scans' control allows: a scan leaves the loop when its solve
+// stops it or asks for a search (k_iekf_eval does that evaluation).
+//
+// Each scan gets a team of T blocks (formed by arrival: block ticket t -> scan
+// t / T, rank t % T, so a team is always the first blocks to become resident
+// and no team waits on one that cannot start).  Rank r keeps the body points and
+// plane caches of chunks r, r + T, ... (K at most) in registers for the whole
+// loop, sums their rows per thread, and stores ONE block partial per
+// evaluation; the scan's last block (ticket) reduces the team's T partials and
+// solves (hs_ticket_tail, the same tail as k_iekf_eval), its state and control
+// stores write-through, then publishes the evaluation count (slot->gen, sc1).
+// The other blocks poll that word (one lane, s_sleep), read the new state and
+// control with sc1 loads and go on.  No launch boundary, no re-dispatch, no
+// reload of the points between evaluations, and T partials instead of one per
+// chunk.  Every spin is bounded (g_ns_timeouts counts a give-up).
+#ifndef LIVO_NS_ACC
+#define LIVO_NS_ACC 0
+#endif
+#ifndef LIVO_NS_WAVES
+#define LIVO_NS_WAVES 4  // waves per SIMD k_iekf_ns's VGPR budget allows
+#endif
+constexpr int kNsTeamMax = 64;
+constexpr unsigned kNsMaxSpins = 1u << 22;
+__device__ unsigned long long g_ns_timeouts;
+struct NsState {
+    double rot[9];
+    double pos[3];
+};
+struct NsLds {
+    HsReduceLds R;
+    SolveLds solve;
+    NsState st;
+    unsigned ticket;
+    int stop, search, abort;
+};
+__device__ __forceinline__ unsigned ld_sc1_u32(const unsigned* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Wait (thread 0, bounded) until the scan's word *w reaches `target`; 1 = gave up.
+__device__ __forceinline__ int ns_wait(const unsigned* w, unsigned target) {
+    unsigned spins = 0;
+    while (ld_sc1_u32(w) < target) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > kNsMaxSpins) {
+            atomicAdd(&g_ns_timeouts, 1ull);
+            return 1;
+        }
+    }
+    return 0;
+}
+
+__global__ __launch_bounds__(kEvalBlock, LIVO_NS_WAVES) void k_iekf_ns(EvalParams E, unsigned* team_ctr, int T) {
+    __shared__ NsLds L;
+    const int tid = threadIdx.x;
+    if (tid == 0) L.ticket = atomicAdd(team_ctr, 1u);
+    __syncthreads();
+    const unsigned tk = __builtin_amdgcn_readfirstlane(L.ticket);  // (uniform: the job in scalar registers)
+    const unsigned bjob = tk / (unsigned)(T + 1), r = tk % (unsigned)(T + 1);
+    // the job in scalar registers: the ticket atomic above rules out scalar loads
+    // (a store may precede them), so each word is loaded and made uniform
+    HsJob job;
+    {
+        static_assert(sizeof(HsJob) % 4 == 0, "HsJob words");
+        const unsigned* src = reinterpret_cast<const unsigned*>(E.k.jobs + bjob);
+        unsigned* dst = reinterpret_cast<unsigned*>(&job);
+#pragma unroll
+        for (int w = 0; w < (int)(sizeof(HsJob) / 4); w++) dst[w] = __builtin_amdgcn_readfirstlane(src[w]);
+    }
+    IekfSlot* slot = job.slot;
+    const int nblk = max(1, (job.n + kEvalBlock - 1) / kEvalBlock);
+    const int Ts = min(T, nblk);  // the scan's workers (its partials)
+    if ((int)r >= Ts && (int)r != T) return;  // a scan smaller than the team: a block with no chunk
+    // control and state at entry (stored before this launch)
+    if (slot->ctrl.stop || slot->ctrl.search_en) return;  // block-uniform
+    unsigned target = (unsigned)slot->ctrl.n_evals;
+#if LIVO_NS_ACC
+    const unsigned nparts = (unsigned)Ts;  // the solver's: one partial per worker
+#else
+    const unsigned nparts = (unsigned)nblk;  // one per chunk
+#endif
+    if ((int)r == T) {
+        // the scan's solver: waits for the workers' Ts partials, reduces them in a
+        // fixed order and solves (hs_scan_tail, k_iekf_eval's tail), then publishes
+        // the evaluation (slot->gen) once its state and control stores have drained
+#pragma unroll 1
+        for (int it = 0; it < LIVO_MAX_EVALS; it++) {
+            if (tid == 0) L.abort = ns_wait(&slot->hs_ticket, (unsigned)nparts);
+            __syncthreads();
+            if (L.abort) return;
+#ifdef LIVO_TAIL_PROF
+            hs_scan_tail<kEvalBlock, kRedUsed + 2>(E.h, job, slot, (int)nparts, L.R, L.solve, -1, 0ull);
+#else
+            hs_scan_tail<kEvalBlock, kRedUsed + 2>(E.h, job, slot, (int)nparts, L.R, L.solve, -1);
+#endif
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            target++;
+            if (tid == 0) {
+                st_sc1(&slot->gen, target);
+                L.stop = ld_sc1(&slot->ctrl.stop);
+                L.search = ld_sc1(&slot->ctrl.search_en);
+            }
+            __syncthreads();
+            if (L.stop || L.search) return;
+        }
+        return;
+    }
+    // a worker: chunks r, r + T, ... (nk of them)
+    const int nk = (nblk - (int)r + T - 1) / T;
+    // the planes a search left unfitted (a point beyond the sqdist gate: plane state 0)
+    // are fitted now, as the first evaluation without a search would: the loop below
+    // then reads every plane from the cache
+#pragma unroll 1
+    for (int k = 0; k < nk; k++) {
+        const int i = ((int)r + T * k) * kEvalBlock + tid;
+        if (i < job.n && job.pstate[i] == 0) {
+            const float4* rec = reinterpret_cast<const float4*>(job.nn + i);
+            float4 nb[kNN];
+#pragma unroll
+            for (int q = 0; q < kNN; q++) nb[q] = rec[q];
+            float4 pl;
+            (void)fit_plane(E.h, job, i, 0, nb, reinterpret_cast<const int4*>(job.nn + i)[6].y, pl);
+        }
+    }
+    if (tid < 12) (tid < 9 ? L.st.rot[tid] : L.st.pos[tid - 9]) = slot->state.rot[tid];  // (rot, pos contiguous)
+    __syncthreads();
+    const double inv_r = E.h.inv_r;
+#pragma unroll 1
+    for (int it = 0; it < LIVO_MAX_EVALS; it++) {
+#if LIVO_NS_ACC
+        // (variant) per-thread sums over the block's chunks, ONE partial per worker:
+        // not the summation order of the launch per evaluation
+        double acc[kRedUsed];
+#pragma unroll
+        for (int j = 0; j < kRedUsed; j++) acc[j] = 0.0;
+        {
+            int i = (int)r * kEvalBlock + tid;
+            HsPointIn nxt = i < job.n ? hshare_load(job, i, true) : HsPointIn{};
+#pragma unroll 1
+            for (int k = 0; k < nk; k++) {
+                HsPointIn in = nxt;
+                const int inext = i + T * kEvalBlock;
+                if (k + 1 < nk && inext < job.n) nxt = hshare_load(job, inext, true);
+                if (i < job.n) {
+                    HsRow w;
+                    hs_row_clear(w);
+                    hshare_point<NsState, true>(E.h, job, L.st, i, 0, w, in);
+                    hs_accumulate(acc, w, inv_r);
+                }
+                i = inext;
+            }
+        }
+        auto col = [&](auto jc) -> double {
+            constexpr int j = decltype(jc)::value;
+            if constexpr (j < kRedUsed) return acc[j];
+            else return 0.0;
+        };
+        hs_block_partial<kEvalBlock, kRedUsed + 2>(job, col, r, L.R);
+        const unsigned nparts = 1u;
+#else
+        const unsigned nparts = (unsigned)nk;
+        // one partial per chunk, each the one-chunk block's of k_iekf_eval (same rows,
+        // same fixed tree): the scan's sums are bit for bit those of the launch per
+        // evaluation.  The next chunk's points load while this one's rows reduce.
+        int i = (int)r * kEvalBlock + tid;
+        HsPointIn nxt = i < job.n ? hshare_load(job, i, true) : HsPointIn{};
+#pragma unroll 1
+        for (int k = 0; k < nk; k++) {
+            const int c = (int)r + T * k;
+            HsPointIn in = nxt;
+            const int inext = i + T * kEvalBlock;
+            if (k + 1 < nk && inext < job.n) nxt = hshare_load(job, inext, true);
+            HsRow w;
+            hs_row_clear(w);
+            if (i < job.n) hshare_point<NsState, true>(E.h, job, L.st, i, 0, w, in);
+            auto col = [&](auto jc) -> double {
+                constexpr int j = decltype(jc)::value;
+                if constexpr (j < kRedUsed) return hs_col<j>(w, inv_r);
+                else return 0.0;  // (no search: no hash-slot / map-point counts)
+            };
+            if (k > 0) __syncthreads();  // wave 0 has read the last chunk's rows
+            hs_block_partial<kEvalBlock, kRedUsed + 2>(job, col, (unsigned)c, L.R);
+            i = inext;
+        }
+#endif
+        target++;
+        if (tid < 64) {  // the partials have drained: count them
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (tid == 0) {
+                __hip_atomic_fetch_add(&slot->hs_ticket, nparts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                L.abort = ns_wait(&slot->gen, target);
+                if (!L.abort) {
+                    L.stop = ld_sc1(&slot->ctrl.stop);
+                    L.search = ld_sc1(&slot->ctrl.search_en);
+                }
+            }
+        }
+        __syncthreads();
+        if (L.abort) return;
+        if (tid < 12) (tid < 9 ? L.st.rot[tid] : L.st.pos[tid - 9]) = ld_sc1(slot->state.rot + tid);
+        __syncthreads();
+        if (L.stop || L.search) return;
+    }
 }
 
 // Per-point persistent selection of the IKFoM h-model: point_selected_surf is a
@@ -4001,6 +4253,27 @@ int launch_iekf_eval(const KnnParams& kp, const HsParams& hp, int n_jobs, int64_
     else
         hipLaunchKernelGGL(k_iekf_eval<false>, grid, block, 0, (hipStream_t)stream, E);
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+
+// k_iekf_ns for a group: T blocks per scan, K chunks per block at most (8 or
+// 12); LIVO_E_RANGE when the scans are too large for that (the caller then
+// runs the evaluations one launch each).  team_ctr: zeroed before the launch.
+int ns_team_size(int64_t max_n, int team) {
+    const int64_t nblk = std::max<int64_t>(1, (max_n + kEvalBlock - 1) / kEvalBlock);
+    return (int)std::min<int64_t>(std::max(1, std::min(team, kNsTeamMax)), nblk);
+}
+int launch_iekf_ns(const KnnParams& kp, const HsParams& hp, int n_jobs, int T, unsigned* team_ctr, void* stream) {
+    if (n_jobs <= 0 || T <= 0 || T > kNsTeamMax) return n_jobs <= 0 ? LIVO_OK : LIVO_E_RANGE;
+    EvalParams E;
+    E.k = kp;
+    E.h = hp;
+    const dim3 grid((unsigned)((T + 1) * n_jobs)), block(kEvalBlock);  // T workers + a solver per scan
+    hipLaunchKernelGGL(k_iekf_ns, grid, block, 0, (hipStream_t)stream, E, team_ctr, T);
+    return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+extern "C" int livo_debug_ns_timeouts(unsigned long long* out) {  // k_iekf_ns spins given up
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ns_timeouts), sizeof(unsigned long long)) == hipSuccess ? LIVO_OK
+                                                                                                        : LIVO_E_HIP;
 }
 
 int launch_hshare(const HsParams& p, int n_jobs, int max_nblk, bool first, void* stream) {

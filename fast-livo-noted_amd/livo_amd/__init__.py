@@ -168,6 +168,7 @@ SIGNATURES = {
     "livo_knn": (C.c_int, [_P, _P, C.c_int64, C.c_int32, _P, _P]),
     "livo_scan_upload": (C.c_int, [_P, _P, C.c_int64, C.c_int64, C.POINTER(C.c_int32)]),
     "livo_scan_upload_async": (C.c_int, [_P, _P, C.c_int64, C.c_int64, C.POINTER(C.c_int32)]),
+    "livo_debug_ns_timeouts": (C.c_int, [C.POINTER(C.c_ulonglong)]),
     "livo_scan_release": (C.c_int, [_P, C.c_int32]),
     "livo_scan_neighbors": (C.c_int, [_P, C.c_int32, _P, _P]),
     "livo_h_share": (C.c_int, [_P, C.c_int32, C.POINTER(State), C.c_int, _P, _P, C.POINTER(C.c_int64),

@@ -288,3 +288,51 @@ def test_scan_upload_async_farm(built):
         _same_update(out_a[k], ref[k])
         _same_update(out_b[k], ref[4 + k])
         _same_update(out_c[k], ref[8 + k])
+
+
+def _ns_timeouts():
+    import ctypes
+    import livo_amd
+    out = ctypes.c_ulonglong(0)
+    assert livo_amd.load().livo_debug_ns_timeouts(ctypes.byref(out)) == 0
+    return out.value
+
+
+@pytest.mark.parametrize("team,max_iter,sizes", [
+    ("16", 4, [100_000] * 8),
+    ("1", 4, [100_000, 3_000, 257, 1, 100_000, 65_537, 256, 20_000]),
+    ("64", 2, [100_000, 50_000, 3_000, 1_000, 100_000, 7, 512, 99_999]),
+    ("16", 1, [100_000] * 4),
+])
+def test_persistent_evaluations_bitwise(built, monkeypatch, team, max_iter, sizes):
+    """The evaluations without a search in one persistent launch per run of them
+    (k_iekf_ns: F, P, E, P per group) give bit for bit the states and statistics
+    of one k_iekf_eval launch per evaluation (LIVO_PERSIST=0), synchronous and
+    pipelined, for ragged scans (1 .. 100k points, teams larger than a scan) and
+    team sizes 1 / 16 / 64; no spin gives up (g_ns_timeouts stays 0)."""
+    import livo_amd
+    from livo_amd import synth
+    m = synth.cached_map(1_000_000)
+    scans = [synth.make_scan(n, 300 + s)[0] for s, n in enumerate(sizes)]
+    states = [synth.make_state(300 + s) for s in range(len(sizes))]
+    t0 = _ns_timeouts()
+    res = {}
+    for persist in ("0", "1"):
+        monkeypatch.setenv("LIVO_PERSIST", persist)  # (read at context creation)
+        monkeypatch.setenv("LIVO_NS_TEAM", team)
+        with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=max_iter) as ctx:
+            ctx.map_build(m)
+            sids = [ctx.scan_upload(b) for b in scans]
+            sync = ctx.iekf_update_batch(sids, states)
+            h = len(sids) // 2
+            ta = ctx.iekf_update_batch_submit(sids[:h], states[:h])
+            tb = ctx.iekf_update_batch_submit(sids[h:], states[h:])
+            pa = ctx.iekf_update_batch_wait(ta, h)
+            pb = ctx.iekf_update_batch_wait(tb, len(sids) - h)
+        res[persist] = (sync, (pa[0] + pb[0], pa[1] + pb[1]))
+    assert _ns_timeouts() == t0
+    for mode in range(2):
+        for s in range(len(sizes)):
+            for persist in ("0", "1"):
+                _same_update((res[persist][mode][0][s], res[persist][mode][1][s]),
+                             (res["0"][0][0][s], res["0"][0][1][s]))
