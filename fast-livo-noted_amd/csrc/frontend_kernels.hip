@@ -255,6 +255,90 @@ __global__ void k_fe_gather(const float* __restrict__ pts, int64_t n, int stride
     iperm[j] = (int32_t)k;
 }
 
+// ---- a batch of scans built in one pass (livo_scan_upload_batch_async) ----
+// Every scan's points lie packed (x, y, z) in one device array at seg.off[b];
+// blockIdx.y = the scan; its bounds at minmax[6b..6b+5] (mins, then the maxes
+// inverted, all initialised to 0xFFFFFFFF).  Per scan the same bounds, keys and stable order as
+// k_fe_minmax / k_fe_morton / k_fe_gather on that scan alone: the key carries
+// the scan in its top bits, so one stable sort of the batch orders each scan's
+// points as its own sort would (ties by input position in both).
+__global__ __launch_bounds__(256) void k_fe_minmax_seg(const float* __restrict__ pts, FeSegs S, unsigned* minmax) {
+    const int b = blockIdx.y;
+    const float* p = pts + 3 * S.off[b];
+    const int64_t n = S.n[b];
+    __shared__ unsigned red[4][6];
+    unsigned mn[3] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu}, mx[3] = {0u, 0u, 0u};
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const unsigned o = f2o(p[3 * i + k]);
+            mn[k] = min(mn[k], o);
+            mx[k] = max(mx[k], o);
+        }
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            mn[k] = min(mn[k], (unsigned)__shfl_xor((int)mn[k], off, 64));
+            mx[k] = max(mx[k], (unsigned)__shfl_xor((int)mx[k], off, 64));
+        }
+    const int wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            red[wave][k] = mn[k];
+            red[wave][3 + k] = mx[k];
+        }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        const int k = threadIdx.x;
+        unsigned v = red[0][k];
+        for (int w = 1; w < (int)(blockDim.x >> 6); w++) v = k < 3 ? min(v, red[w][k]) : max(v, red[w][k]);
+        atomicMin(minmax + 6 * b + k, k < 3 ? v : ~v);  // (maxes stored inverted: one 0xFF.. initialisation)
+    }
+}
+
+__global__ void k_fe_morton_seg(const float* __restrict__ pts, FeSegs S, const unsigned* minmax, float scale,
+                                unsigned long long* codes, uint32_t* iota) {
+    const int b = blockIdx.y;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= S.n[b]) return;
+    const int64_t g = S.off[b] + i;
+    unsigned long long code = (unsigned long long)b << 60;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const unsigned o = minmax[6 * b + a];
+        const float lo = __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
+        float f = (pts[3 * g + a] - lo) * scale;
+        if (!(f >= 0.0f)) f = 0.0f;
+        const uint32_t q = (uint32_t)fminf(f, 1048575.0f);
+#pragma unroll
+        for (int c = 0; c < 20; c++) code |= (unsigned long long)((q >> c) & 1u) << (3 * c + a);
+    }
+    codes[g] = code;
+    iota[g] = (uint32_t)g;
+}
+
+// scan b in stored order: pts4[k] = its point perm[k]; iperm[perm[k]] = k; the
+// stored position -> input index map (ScanBuf::d_perm) and cleared neighbour
+// records / plane states
+__global__ void k_fe_gather_seg(const float* __restrict__ pts, FeSegs S, const uint32_t* __restrict__ sorted) {
+    const int b = blockIdx.y;
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= S.n[b]) return;
+    const int64_t o = S.off[b];
+    const uint32_t jg = sorted[o + k];
+    const int32_t j = (int32_t)(jg - (uint32_t)o);
+    reinterpret_cast<float4*>(S.pts4[b])[k] =
+        make_float4(pts[3 * (int64_t)jg], pts[3 * (int64_t)jg + 1], pts[3 * (int64_t)jg + 2], 0.f);
+    S.iperm[b][j] = (int32_t)k;
+    S.perm[b][k] = j;
+    float4* rec = reinterpret_cast<float4*>(S.nn[b]) + 8 * k;  // (128-B NNRec)
+#pragma unroll
+    for (int w = 0; w < 8; w++) rec[w] = make_float4(0.f, 0.f, 0.f, 0.f);
+    S.pstate[b][k] = 0;
+}
+
 // RGBpointBodyToWorld (laser_mapping.cpp:647-660) over laserCloudFullRes
 // (:258-265): p_w = rot (R_LI p_b + t_LI) + pos in double, stored as float;
 // intensity copied (column 3 of a 5-float source, 0 for a 4-float scan),
@@ -331,6 +415,22 @@ int launch_fe_morton(const float* pts, int64_t n, int stride, const unsigned* mi
 int launch_fe_gather(const float* pts, int64_t n, int stride, const uint32_t* perm, float* pts4, int32_t* iperm,
                      void* stream) {
     FE_LAUNCH(k_fe_gather, n, pts, n, stride, perm, pts4, iperm);
+}
+int launch_fe_build_seg(const float* pts, const FeSegs& S, int n_scans, int64_t max_n, unsigned* minmax, float scale,
+                        unsigned long long* codes, uint32_t* iota, void* stream) {
+    if (n_scans <= 0 || n_scans > kFeSegMax || max_n <= 0) return n_scans == 0 ? LIVO_OK : LIVO_E_RANGE;
+    const unsigned bx = (unsigned)((max_n + 255) / 256);
+    const dim3 mm((unsigned)std::min<int64_t>(kMinmaxBlocks, bx), (unsigned)n_scans), g(bx, (unsigned)n_scans);
+    hipLaunchKernelGGL(k_fe_minmax_seg, mm, dim3(256), 0, (hipStream_t)stream, pts, S, minmax);
+    hipLaunchKernelGGL(k_fe_morton_seg, g, dim3(256), 0, (hipStream_t)stream, pts, S, minmax, scale, codes, iota);
+    return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+int launch_fe_gather_seg(const float* pts, const FeSegs& S, int n_scans, int64_t max_n, const uint32_t* sorted,
+                         void* stream) {
+    if (n_scans <= 0 || n_scans > kFeSegMax || max_n <= 0) return n_scans == 0 ? LIVO_OK : LIVO_E_RANGE;
+    hipLaunchKernelGGL(k_fe_gather_seg, dim3((unsigned)((max_n + 255) / 256), (unsigned)n_scans), dim3(256), 0,
+                       (hipStream_t)stream, pts, S, sorted);
+    return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 int launch_to_world(const float* src, int64_t n, int stride, const int32_t* perm, const WorldParams& W, float* out5,
                     void* stream) {

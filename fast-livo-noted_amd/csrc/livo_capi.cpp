@@ -2561,6 +2561,182 @@ int livo_scan_upload_async(livo_ctx* c, const float* xyz, int64_t N, int64_t str
     return LIVO_OK;
 }
 
+// True if p lies in page-locked host memory (livo_host_register, hipHostMalloc):
+// the copy engine reads it directly.
+static bool host_pinned(const void* p) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+int livo_host_register(livo_ctx* c, void* p, size_t bytes) {
+    if (!c || !p || bytes == 0) return LIVO_E_INVALID;
+    if (set_device(c)) return LIVO_E_HIP;
+    return hipHostRegister(p, bytes, hipHostRegisterDefault) == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+int livo_host_unregister(livo_ctx* c, void* p) {
+    if (!c || !p) return LIVO_E_INVALID;
+    if (set_device(c)) return LIVO_E_HIP;
+    if (hipDeviceSynchronize() != hipSuccess) return LIVO_E_HIP;  // (no copy may still read it)
+    return hipHostUnregister(p) == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+
+// livo_scan_upload_async for a batch of scans in one pass: one staging copy
+// (or, from page-locked caller memory, one DMA per scan and no host copy), then
+// one bounds pass, one key pass, ONE stable sort of the whole batch (the scan
+// in the key's top bits) and one gather that also clears the neighbour
+// records, kFeSegMax scans at a time, on the upload stream.  Each scan is
+// stored exactly as livo_scan_upload stores it.
+int livo_scan_upload_batch_async(livo_ctx* c, const float* const* xyz, const int64_t* N, int32_t n,
+                                 int64_t stride_bytes, int32_t* scan_ids) {
+    if (!c || !xyz || !N || !scan_ids || n < 0) return LIVO_E_INVALID;
+    if (stride_bytes == 0) stride_bytes = 3 * sizeof(float);
+    if (stride_bytes < (int64_t)(3 * sizeof(float))) return LIVO_E_INVALID;
+    for (int32_t b = 0; b < n; b++) {
+        if (N[b] < 0 || (N[b] > 0 && !xyz[b])) return LIVO_E_INVALID;
+        if (N[b] > (int64_t)0x7FFFFFFF - kBlock) return LIVO_E_RANGE;
+    }
+    if (set_device(c)) return LIVO_E_HIP;
+    if (!c->up_stream && hipStreamCreateWithFlags(&c->up_stream, hipStreamNonBlocking) != hipSuccess) {
+        c->up_stream = nullptr;
+        return LIVO_E_HIP;
+    }
+    for (int32_t b0 = 0; b0 < n; b0 += kFeSegMax) {
+        const int32_t m = std::min<int32_t>(kFeSegMax, n - b0);
+        int64_t tot = 0, max_n = 0;
+        for (int32_t b = 0; b < m; b++) {
+            tot += N[b0 + b];
+            max_n = std::max(max_n, N[b0 + b]);
+        }
+        if (tot == 0) {  // (empty scans only)
+            for (int32_t b = 0; b < m; b++) {
+                const int rc = livo_scan_upload(c, xyz[b0 + b], 0, stride_bytes, scan_ids + b0 + b);
+                if (rc) return rc;
+            }
+            continue;
+        }
+        if (tot > (int64_t)0xFFFFFFFF - kBlock) return LIVO_E_RANGE;  // (32-bit positions in the batch sort)
+        // scratch: [keys | sorted keys | iota | sorted iota | bounds (6 per scan)] then the packed points
+        const size_t kb = (size_t)tot * 8, vb = (size_t)tot * 4;
+        const size_t mm_off = 2 * kb + 2 * vb;
+        const size_t off = (mm_off + 6 * sizeof(unsigned) * kFeSegMax + 255) & ~(size_t)255;
+        const size_t bytes = (size_t)tot * 3 * sizeof(float);
+        if (off + bytes > c->aup_tmp_bytes) {  // (growing: the uploads queued on it finish first)
+            if (hipStreamSynchronize(c->up_stream) != hipSuccess) return LIVO_E_HIP;
+            const int rc = ensure_dev_bytes(&c->aup_tmp, &c->aup_tmp_bytes, off + bytes);
+            if (rc) return rc;
+        }
+        char* base = (char*)c->aup_tmp;
+        auto* codes = (unsigned long long*)base;
+        auto* scodes = (unsigned long long*)(base + kb);
+        auto* iota = (uint32_t*)(base + 2 * kb);
+        auto* sorted = (uint32_t*)(base + 2 * kb + vb);
+        auto* mm = (unsigned*)(base + mm_off);
+        float* d_src = (float*)(base + off);
+        // the points: straight from page-locked caller memory, else through a
+        // pinned staging buffer of the ring (the caller's arrays are free on return)
+        bool direct = stride_bytes == (int64_t)(3 * sizeof(float));
+        for (int32_t b = 0; b < m && direct; b++)
+            if (N[b0 + b] > 0 && !host_pinned(xyz[b0 + b])) direct = false;
+        int rc = LIVO_OK;
+        livo_ctx::PinSlot* P = nullptr;
+        if (!direct) {
+            P = &c->pin[c->pin_next];
+            c->pin_next = (c->pin_next + 1) % kPinRing;
+            if (P->inflight && hipEventSynchronize(P->copied) != hipSuccess) return LIVO_E_HIP;
+            P->inflight = false;
+            if (bytes > P->bytes) {
+                if (P->h) (void)hipHostFree(P->h);
+                P->h = nullptr;
+                P->bytes = 0;
+                if (hipHostMalloc((void**)&P->h, bytes, hipHostMallocDefault) != hipSuccess) {
+                    P->h = nullptr;
+                    return LIVO_E_OOM;
+                }
+                P->bytes = bytes;
+            }
+            if (!P->copied && hipEventCreateWithFlags(&P->copied, hipEventDisableTiming) != hipSuccess) {
+                P->copied = nullptr;
+                return LIVO_E_HIP;
+            }
+            int64_t o = 0;
+            for (int32_t b = 0; b < m; b++) {
+                if (N[b0 + b] > 0) pack_xyz(xyz[b0 + b], N[b0 + b], stride_bytes, P->h + 3 * o);
+                o += N[b0 + b];
+            }
+            if (hipMemcpyAsync(d_src, P->h, bytes, hipMemcpyHostToDevice, c->up_stream) != hipSuccess ||
+                hipEventRecord(P->copied, c->up_stream) != hipSuccess)
+                return LIVO_E_HIP;
+            P->inflight = true;
+        } else {
+            int64_t o = 0;
+            for (int32_t b = 0; b < m; b++) {
+                if (N[b0 + b] > 0 &&
+                    hipMemcpyAsync(d_src + 3 * o, xyz[b0 + b], (size_t)N[b0 + b] * 3 * sizeof(float),
+                                   hipMemcpyHostToDevice, c->up_stream) != hipSuccess)
+                    return LIVO_E_HIP;
+                o += N[b0 + b];
+            }
+        }
+        // the scans' buffers
+        ScanBuf sb[kFeSegMax];
+        FeSegs S{};
+        int64_t o = 0;
+        for (int32_t b = 0; b < m && !rc; b++) {
+            rc = alloc_scan_buf(c, sb[b], N[b0 + b]);
+            if (!rc && !sb[b].ready && hipEventCreateWithFlags(&sb[b].ready, hipEventDisableTiming) != hipSuccess) {
+                sb[b].ready = nullptr;
+                rc = LIVO_E_HIP;
+            }
+            S.off[b] = o;
+            S.n[b] = N[b0 + b];
+            S.pts4[b] = sb[b].pts;
+            S.iperm[b] = sb[b].d_iperm;
+            S.perm[b] = sb[b].d_perm;
+            S.nn[b] = sb[b].nn;
+            S.pstate[b] = sb[b].pstate;
+            o += N[b0 + b];
+        }
+        // bounds start at +max (mins) and ~(-max) (maxes, stored inverted) in the order-preserving encoding
+        if (!rc && (hipMemsetD32Async((hipDeviceptr_t)mm, 0xFFFFFFFFu, 6 * kFeSegMax, c->up_stream) != hipSuccess))
+            rc = LIVO_E_HIP;
+        if (!rc) rc = launch_fe_build_seg(d_src, S, m, max_n, mm, morton_scale(), codes, iota, c->up_stream);
+        if (!rc) {
+            size_t tb = 0;
+            rc = prim_sort_pairs_u64(nullptr, &tb, codes, scodes, iota, sorted, tot, 64, c->up_stream);
+            if (!rc && tb > c->aup_prim_bytes) {
+                if (hipStreamSynchronize(c->up_stream) != hipSuccess) rc = LIVO_E_HIP;
+                if (!rc) rc = ensure_dev_bytes(&c->aup_prim, &c->aup_prim_bytes, tb);
+            }
+            tb = c->aup_prim_bytes;
+            if (!rc) rc = prim_sort_pairs_u64(c->aup_prim, &tb, codes, scodes, iota, sorted, tot, 64, c->up_stream);
+        }
+        if (!rc) rc = launch_fe_gather_seg(d_src, S, m, max_n, sorted, c->up_stream);
+        for (int32_t b = 0; b < m && !rc; b++)
+            if (hipEventRecord(sb[b].ready, c->up_stream) != hipSuccess) rc = LIVO_E_HIP;
+        if (rc) {
+            (void)hipStreamSynchronize(c->up_stream);
+            for (int32_t b = 0; b < m; b++)
+                if (sb[b].used) release_scan_buf(c, sb[b]);
+            return rc;
+        }
+        for (int32_t b = 0; b < m; b++) {
+            if (N[b0 + b] == 0) {  // (an empty scan has nothing to build)
+                release_scan_buf(c, sb[b]);
+                rc = livo_scan_upload(c, xyz[b0 + b], 0, stride_bytes, scan_ids + b0 + b);
+                if (rc) return rc;
+                continue;
+            }
+            sb[b].pending = true;
+            scan_ids[b0 + b] = register_scan(c, sb[b]);
+        }
+    }
+    return LIVO_OK;
+}
+
 int livo_scan_release(livo_ctx* c, int32_t id) {
     if (!c) return LIVO_E_INVALID;
     if (id < 0 || id >= (int32_t)c->scans.size() || !c->scans[id].used) return LIVO_E_NOSCAN;

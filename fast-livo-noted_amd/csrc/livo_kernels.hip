@@ -40,6 +40,20 @@
 
 namespace livo {
 
+// Global addressing for the sc1 accessors' pointers (struct fields copied from
+// the job tables arrive generic): a generic (flat) access also counts against
+// the 4-bit LDS counter, so at most 15 are in flight per wave where global
+// loads keep up to 63.  Atomic accesses only: a plain load through a global,
+// block-uniform pointer may become a scalar load, which does not see other
+// CUs' stores within a launch.
+template <class T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T* gptr(const T* p) {
+    return (const __attribute__((address_space(1))) T*)p;
+}
+template <class T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* gptr(T* p) {
+    return (__attribute__((address_space(1))) T*)p;
+}
 // ========================================================= IKFoM path =====
 // The IKFoM formulation: state_ikfom (use-ikfom.hpp:12-21),
 // the legacy h-model (origin_laserMapping.cpp:916-1048) and
@@ -2252,20 +2266,22 @@ constexpr int kStHead = (int)(sizeof(StateHead) / sizeof(double));  // 24
 static_assert(sizeof(StateHead) == 24 * sizeof(double) && offsetof(livo_state, cov) == sizeof(StateHead),
               "StateHead is the head of livo_state");
 
+// sc1 (agent-coherent) loads and write-through stores of slot / partial words
+// (global addressing: gptr, top of the file).
 __device__ __forceinline__ double ld_sc1(const double* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_load(gptr(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ int ld_sc1(const int* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_load(gptr(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ unsigned long long ld_sc1(const unsigned long long* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_load(gptr(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // Write-through (sc1) stores of the slot's fields: the persistent evaluation
 // loop (k_iekf_ns) reads them from other CUs inside one launch.
 template <class T>
 __device__ __forceinline__ void st_sc1(T* p, T v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(gptr(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Stage the solve's inputs (cov, state and prior heads, control, knn_passes)
@@ -2729,8 +2745,8 @@ constexpr int kRedInFlight = LIVO_RED_INFLIGHT;  // partial loads in flight per 
 __device__ __forceinline__ void hs_host_slot(const HsJob& job, const IekfSlot* slot, int t, int nt) {
     const unsigned long long* src = reinterpret_cast<const unsigned long long*>(slot);
     for (int w = t; w < (int)((kSlotLmBytes + 15) / 16); w += nt) {
-        const unsigned long long lo = __hip_atomic_load(src + 2 * w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long hi = __hip_atomic_load(src + 2 * w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long lo = __hip_atomic_load(gptr(src + 2 * w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long hi = __hip_atomic_load(gptr(src + 2 * w + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         job.host_slot[w] = make_uint4((unsigned)lo, (unsigned)(lo >> 32), (unsigned)hi, (unsigned)(hi >> 32));
     }
 }
@@ -2757,7 +2773,7 @@ __device__ __forceinline__ void hs_block_partial(const HsJob& job, const Col& co
 #pragma unroll
             for (int w = 0; w < h; w++) r[w] = r[w] + r[w + h];
         const double v = r[0];
-        __hip_atomic_store(job.partial + (size_t)blk * kRedCols + tid, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(gptr(job.partial + (size_t)blk * kRedCols + tid), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -2793,7 +2809,7 @@ __device__ __forceinline__ void hs_ticket_tail(const HsParams& P, const HsJob& j
     if (tid < 64) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (tid == 0)
-            R.last = __hip_atomic_fetch_add(&slot->hs_ticket, count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            R.last = __hip_atomic_fetch_add(gptr(&slot->hs_ticket), count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                      (unsigned)nblk - count;
     }
     __syncthreads();
@@ -3316,7 +3332,7 @@ struct NsLds {
     int stop, search, abort;
 };
 __device__ __forceinline__ unsigned ld_sc1_u32(const unsigned* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_load(gptr(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // Wait (thread 0, bounded) until the scan's word *w reaches `target`; 1 = gave up.
 __device__ __forceinline__ int ns_wait(const unsigned* w, unsigned target) {
@@ -3469,7 +3485,7 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_NS_WAVES) void k_iekf_ns(EvalParam
         if (tid < 64) {  // the partials have drained: count them
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (tid == 0) {
-                __hip_atomic_fetch_add(&slot->hs_ticket, nparts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_add(gptr(&slot->hs_ticket), nparts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 L.abort = ns_wait(&slot->gen, target);
                 if (!L.abort) {
                     L.stop = ld_sc1(&slot->ctrl.stop);

@@ -169,6 +169,9 @@ SIGNATURES = {
     "livo_scan_upload": (C.c_int, [_P, _P, C.c_int64, C.c_int64, C.POINTER(C.c_int32)]),
     "livo_scan_upload_async": (C.c_int, [_P, _P, C.c_int64, C.c_int64, C.POINTER(C.c_int32)]),
     "livo_debug_ns_timeouts": (C.c_int, [C.POINTER(C.c_ulonglong)]),
+    "livo_scan_upload_batch_async": (C.c_int, [_P, _P, _P, C.c_int32, C.c_int64, _P]),
+    "livo_host_register": (C.c_int, [_P, _P, C.c_size_t]),
+    "livo_host_unregister": (C.c_int, [_P, _P]),
     "livo_scan_release": (C.c_int, [_P, C.c_int32]),
     "livo_scan_neighbors": (C.c_int, [_P, C.c_int32, _P, _P]),
     "livo_h_share": (C.c_int, [_P, C.c_int32, C.POINTER(State), C.c_int, _P, _P, C.POINTER(C.c_int64),
@@ -347,6 +350,33 @@ class Context:
                self._L.livo_scan_upload_async(self.h, _ptr(xyz), xyz.shape[0], xyz.shape[1] * 4, C.byref(sid)))
         self.scans[sid.value] = xyz.shape[0]
         return sid.value
+
+    def scan_upload_batch_async(self, scans) -> list:
+        """livo_scan_upload_batch_async: a list of (N_b, w) float32 arrays (one width w
+        >= 3 for all) in one pass; returns their scan ids.  Arrays in page-locked
+        memory (host_register) with w = 3 are read by the copy engine directly and
+        must stay unchanged until a batch using the scans returns."""
+        arrs = [np.ascontiguousarray(x, np.float32) for x in scans]
+        n = len(arrs)
+        w = arrs[0].shape[1] if n else 3
+        assert all(a.ndim == 2 and a.shape[1] == w for a in arrs) and w >= 3
+        ptrs = (C.c_void_p * max(n, 1))(*[a.ctypes.data for a in arrs])
+        ns = (C.c_int64 * max(n, 1))(*[a.shape[0] for a in arrs])
+        ids = (C.c_int32 * max(n, 1))()
+        _check("livo_scan_upload_batch_async",
+               self._L.livo_scan_upload_batch_async(self.h, ptrs, ns, n, w * 4, ids))
+        for b in range(n):
+            self.scans[ids[b]] = arrs[b].shape[0]
+        self._keep = arrs  # (the arrays the device may still read from)
+        return [ids[b] for b in range(n)]
+
+    def host_register(self, arr: np.ndarray):
+        """Page-lock a C-contiguous array's memory (livo_host_register)."""
+        assert arr.flags["C_CONTIGUOUS"] and arr.nbytes > 0
+        _check("livo_host_register", self._L.livo_host_register(self.h, arr.ctypes.data, arr.nbytes))
+
+    def host_unregister(self, arr: np.ndarray):
+        _check("livo_host_unregister", self._L.livo_host_unregister(self.h, arr.ctypes.data))
 
     def scan_release(self, sid: int):
         _check("livo_scan_release", self._L.livo_scan_release(self.h, sid))

@@ -45,6 +45,7 @@
 #ifndef LIVO_H
 #define LIVO_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -192,6 +193,19 @@ int livo_scan_upload(livo_ctx* ctx, const float* xyz, int64_t N, int64_t stride_
  * (The reference hands each frame's feats_down_body to h_share_model,
  * src/laser_mapping.cpp:129-131: the upload of frame k+1 can run under frame k.) */
 int livo_scan_upload_async(livo_ctx* ctx, const float* xyz, int64_t N, int64_t stride_bytes, int32_t* scan_id);
+/* livo_scan_upload_async for n scans in one pass (xyz[b]: N[b] points at
+ * stride_bytes, scan_ids[b] out): one staging copy, then one bounds pass, one
+ * key pass, one stable sort of the whole batch and one gather on the upload
+ * stream; each scan is stored exactly as livo_scan_upload stores it.  From
+ * page-locked memory (livo_host_register) with stride 12 the copy engine reads
+ * the caller's arrays directly (no host copy): keep them unchanged until a batch
+ * that uses the scans returns (or livo_sync); otherwise they are free on return. */
+int livo_scan_upload_batch_async(livo_ctx* ctx, const float* const* xyz, const int64_t* N, int32_t n,
+                                 int64_t stride_bytes, int32_t* scan_ids);
+/* Page-lock (hipHostRegister) / release a caller's host buffer, e.g. the point
+ * arrays a scan farm uploads from; unregister waits for the device first. */
+int livo_host_register(livo_ctx* ctx, void* p, size_t bytes);
+int livo_host_unregister(livo_ctx* ctx, void* p);
 /* Release a resident scan: LIVO_E_BUSY while a submitted batch that holds it is
  * not collected; other batches may be in flight. */
 int livo_scan_release(livo_ctx* ctx, int32_t scan_id);

@@ -336,3 +336,45 @@ def test_persistent_evaluations_bitwise(built, monkeypatch, team, max_iter, size
             for persist in ("0", "1"):
                 _same_update((res[persist][mode][0][s], res[persist][mode][1][s]),
                              (res["0"][0][0][s], res["0"][0][1][s]))
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_scan_upload_batch_async(built, pinned):
+    """livo_scan_upload_batch_async (one copy, bounds, keys, one stable sort of the
+    batch, one gather; 16 scans per pass): 18 ragged scans (an empty one, a
+    single point, 1..60k points, two passes) are stored exactly as
+    livo_scan_upload stores them -- bit for bit the same updates and neighbour
+    records -- from ordinary arrays (pinned staging) and from page-locked ones
+    (livo_host_register: the copy engine reads them directly)."""
+    import livo_amd
+    from livo_amd import synth
+    m = synth.cached_map(1_000_000)
+    sizes = [60_000, 1, 40_000, 0, 257, 30_000, 5, 12_345] + [20_000 + 1000 * s for s in range(10)]
+    scans = [np.ascontiguousarray(synth.make_scan(n, 700 + s)[0][:, :3], np.float32) if n > 0
+             else np.zeros((0, 3), np.float32) for s, n in enumerate(sizes)]
+    states = [synth.make_state(700 + s) for s in range(len(sizes))]
+    live = [s for s, n in enumerate(sizes) if n > 0]
+    with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=4) as ctx:
+        ctx.map_build(m)
+        ref_ids = [ctx.scan_upload(scans[s]) for s in live]
+        ref = list(zip(*ctx.iekf_update_batch(ref_ids, [states[s] for s in live])))
+        ref_nn = [ctx.scan_neighbors(sid) for sid in ref_ids]
+        for sid in ref_ids:
+            ctx.scan_release(sid)
+        if pinned:
+            for x in scans:
+                if x.nbytes:
+                    ctx.host_register(x)
+        ids = ctx.scan_upload_batch_async(scans)
+        assert len(ids) == len(sizes) and len(set(ids)) == len(ids)
+        got = list(zip(*ctx.iekf_update_batch([ids[s] for s in live], [states[s] for s in live])))
+        got_nn = [ctx.scan_neighbors(ids[s]) for s in live]
+        for sid in ids:
+            ctx.scan_release(sid)
+        if pinned:
+            for x in scans:
+                if x.nbytes:
+                    ctx.host_unregister(x)
+    for k in range(len(live)):
+        _same_update(got[k], ref[k])
+        assert np.array_equal(got_nn[k][0], ref_nn[k][0]) and np.array_equal(got_nn[k][1], ref_nn[k][1])
