@@ -11,6 +11,7 @@
 #   kt[=ARGS]             rocprofv3 --kernel-trace --stats over bench.py ARGS
 #                         (default: the headline leg, 20 steps)
 #   ktpy=SCRIPT ARGS      rocprofv3 --kernel-trace --stats over python3 SCRIPT ARGS (repo-relative script)
+#   ktcp=SCRIPT ARGS      the same with --memory-copy-trace (copy durations)
 #   pmc_eval              PMC passes over the first evaluation (tools/pmc_eval.sh)
 #   pmc_c5                PMC passes over the config-5 batch (tools/pmc_c5.sh)
 #   py=SCRIPT ARGS        python SCRIPT ARGS (any lab/probe script), 200 s limit
@@ -50,6 +51,9 @@ for step in "$@"; do
     ktpy)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
           -d "$OUT/kt$n" -o kt -- python3 $(echo "$arg" | sed "s|^|$R/|")) > "$log" 2>&1 || { tail -30 "$log"; exit 1; } ;;
+    ktcp)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats \
+          --output-format csv -d "$OUT/kt$n" -o kt -- python3 $(echo "$arg" | sed "s|^|$R/|")) > "$log" 2>&1 || { tail -30 "$log"; exit 1; } ;;
     pmc_eval)
       bash tools/pmc_eval.sh "$OUT/pmc$n" > "$log" 2>&1 || { tail -30 "$log"; exit 1; } ;;
     pmc_c5)
