@@ -158,8 +158,19 @@ __global__ __launch_bounds__(256) void k_vio_solve(VioParams P, int chunk) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int n = P.n, pst = P.ps * P.ps;
     if (tid < 27) {
+        // the block partials in order (the same additions as a serial loop), 16
+        // loads in flight: one dependent load per block took ~1 us each (~80 us
+        // per solve at 20k points)
+        constexpr int kF = 16;
         double v = P.partial[tid];
-        for (int b = 1; b < P.nblk; b++) v = v + P.partial[(size_t)b * kVioCols + tid];
+        for (int b0 = 1; b0 < P.nblk; b0 += kF) {
+            double x[kF];
+#pragma unroll
+            for (int k = 0; k < kF; k++) x[k] = b0 + k < P.nblk ? P.partial[(size_t)(b0 + k) * kVioCols + tid] : 0.0;
+#pragma unroll
+            for (int k = 0; k < kF; k++)
+                if (b0 + k < P.nblk) v = v + x[k];
+        }
         L.sum[tid] = v;
     }
     for (int t = tid; t < kDim * 6; t += 256) L.A[t] = slot->state.cov[(t / 6) * kDim + t % 6] / P.img_cov;
@@ -170,8 +181,22 @@ __global__ __launch_bounds__(256) void k_vio_solve(VioParams P, int chunk) {
         __syncthreads();
         if (base == 0 && w == 1) vio_gain(slot, L, lane);
         if (tid == 0) {
+            // error += patch_error in point order (lidar_selection.cpp:849): one
+            // dependent chain, its LDS reads 8 float4 ahead of the adds
             const float4* e4 = reinterpret_cast<const float4*>(s_err);
             int t = 0;
+            for (; t + 32 <= cnt; t += 32) {
+                float4 v[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++) v[k] = e4[(t >> 2) + k];
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    err += v[k].x;
+                    err += v[k].y;
+                    err += v[k].z;
+                    err += v[k].w;
+                }
+            }
             for (; t + 4 <= cnt; t += 4) {
                 const float4 v = e4[t >> 2];
                 err += v.x;
