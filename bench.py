@@ -508,6 +508,9 @@ def main():
                 "limiter": ("dependent-load latency: the priced roofline is HBM (bound), but the measured limiter is the "
                             "chain hash probe -> run chunks per query (L2/MALL hits), not bytes (frac_fabric_traffic)"),
                 "reference_equivalent_GBps": round(ref_equiv, 1),
+                "reference_equivalent_note": ("not a roofline (it exceeds the HBM peak): the bytes the reference's "
+                                              "ikd-Tree search would read per query (visits_per_query_ref x 64 B + "
+                                              "52 B) over this launch's time, a work-equivalence figure only"),
                 "visits_per_query_ref": round(vq_ref, 3)}
         if pmc:
             roof["pmc"] = {k: v for k, v in pmc.items() if k != "hbm_bytes_per_launch"}

@@ -226,6 +226,17 @@ def load(path: str = LIB_PATH):
     return _lib
 
 
+def page_aligned_copy(a: np.ndarray) -> np.ndarray:
+    """A C-contiguous copy of `a` whose data starts on a 4 KiB page (for
+    livo_host_register: the copy engine then reads whole pages of it)."""
+    a = np.ascontiguousarray(a)
+    raw = np.empty(a.nbytes + 4096, np.uint8)
+    off = (-raw.ctypes.data) % 4096
+    out = raw[off:off + a.nbytes].view(a.dtype).reshape(a.shape)
+    out[...] = a
+    return out
+
+
 def _check(fn, rc):
     if rc != LIVO_OK:
         raise LivoError(fn, rc)

@@ -17,9 +17,13 @@ from livo_amd import synth  # noqa: E402
 
 
 def main():
-    steps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    steps = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 20
     m = synth.cached_map(1_000_000)
+    align = "--unaligned" not in sys.argv
     scans = [np.ascontiguousarray(synth.make_scan(100_000, s)[0][:, :3], np.float32) for s in range(32)]
+    if align:
+        scans = [livo_amd.page_aligned_copy(x) for x in scans]
+    print("page-aligned arrays" if align else "arrays as numpy allocates them")
     states = [synth.make_state(s) for s in range(32)]
     with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=4) as ctx:
         ctx.map_build(m)
