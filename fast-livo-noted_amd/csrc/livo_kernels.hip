@@ -850,9 +850,13 @@ __device__ __forceinline__ float4 cand_point(const float4* __restrict__ lpts, co
 __device__ unsigned long long g_amb_reason[8];
 #endif
 template <bool RUNS = false>
+// stage: the wave's LDS record buffer (64 x 8 float4, part k of lane l's record at
+// l * 8 + ((k + l) & 7): 8 distinct 16-B slots per row, so the lanes' writes spread
+// over the banks); nullptr: the record goes straight to job.nn.
 __device__ __forceinline__ bool lq_finish(LeafQuery& q, const KnnParams& P, const HsJob& job, unsigned bjob,
                                           int i, const float4* __restrict__ lpts, bool overrun, bool enqueue = true,
-                                          const float4* __restrict__ vpts = nullptr, float4* nbr = nullptr) {
+                                          const float4* __restrict__ vpts = nullptr, float4* nbr = nullptr,
+                                          float4* stage = nullptr) {
     const int cnt = (int)min<int64_t>(P.lM, (int64_t)kNN);
     float4 a[kNN];
 #pragma unroll
@@ -904,6 +908,11 @@ __device__ __forceinline__ bool lq_finish(LeafQuery& q, const KnnParams& P, cons
     }
     // neighbour record: points, distances, original indices; node[] = leaf-map slots
     float4* o4 = reinterpret_cast<float4*>(job.nn + i);
+    const int sl = threadIdx.x & 63;
+    auto put = [&](int k, float4 v) {
+        if (stage) stage[sl * 8 + ((k + sl) & 7)] = v;
+        else o4[k] = v;
+    };
     int32_t idx[kNN];
 #pragma unroll
     for (int k = 0; k < kNN; k++) {
@@ -913,14 +922,16 @@ __device__ __forceinline__ bool lq_finish(LeafQuery& q, const KnnParams& P, cons
             v = make_float4(a[k].x, a[k].y, a[k].z, q.d[k]);
             idx[k] = (int32_t)__float_as_uint(a[k].w);
         }
-        o4[k] = v;
+        put(k, v);
         if (nbr) nbr[k] = v;  // (x, y, z, sqdist) as the record holds them
     }
     const int flag = amb ? 4 : (tie ? 16 : 0);
-    int4* oi = reinterpret_cast<int4*>(job.nn + i) + 5;
-    oi[0] = make_int4(idx[0], idx[1], idx[2], idx[3]);
-    oi[1] = make_int4(idx[4], cnt, flag, (int)q.nd[0]);
-    oi[2] = make_int4((int)q.nd[1], (int)q.nd[2], (int)q.nd[3], (int)q.nd[4]);
+    auto i4 = [](int x, int y, int z, int w) {
+        return make_float4(__int_as_float(x), __int_as_float(y), __int_as_float(z), __int_as_float(w));
+    };
+    put(5, i4(idx[0], idx[1], idx[2], idx[3]));
+    put(6, i4(idx[4], cnt, flag, (int)q.nd[0]));
+    put(7, i4((int)q.nd[1], (int)q.nd[2], (int)q.nd[3], (int)q.nd[4]));
     if (amb && enqueue) flag_for_replay(P, bjob, i);
     return amb;
 }
@@ -3060,6 +3071,7 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
             HsReduceLds R;
             SolveLds solve;  // the scan's last block solves after its search is done
         } rs;
+        float4 nnstage[kEvalBlock / 64][64 * 8];  // each wave's 64 neighbour records (the run searches)
     } U;
     unsigned bjob, bx;
     // the same block order in every evaluation: the plane caches stay in the L2 that wrote them
@@ -3217,12 +3229,13 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
                 float4 nb[kNN];
                 // candidates: grid positions (index runs, the cell walk), or run positions (float4 runs);
                 // on the incremental map positions in its base set rpts, or kRunPos | delta positions
+                float4* stage = U.nnstage[threadIdx.x >> 6];
                 if (dyn)
                     amb = lq_finish<true>(q, P, job, bjob, i, reinterpret_cast<const float4*>(walked ? P.gpts : P.rpts),
-                                          !certified, false, reinterpret_cast<const float4*>(P.dpts), nb);
+                                          !certified, false, reinterpret_cast<const float4*>(P.dpts), nb, stage);
                 else
                     amb = lq_finish<!LIVO_IDX_RUNS>(q, P, job, bjob, i, reinterpret_cast<const float4*>(P.gpts),
-                                                    !certified, false, walked ? nullptr : runs, nb);
+                                                    !certified, false, walked ? nullptr : runs, nb, stage);
                 // the plane from the neighbours in registers (18643 vs 18011 updates/s
                 // re-reading the record just written, profiles/r03_ab_prefit_seed.txt)
                 if (!amb && (!P.canon || dyn)) {  // (a replayed query's plane is fitted from its record below)
@@ -3231,6 +3244,24 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
                     pin.plane = pl;
                     prefit = true;
                 }
+            }
+            {
+                // the wave's 64 records leave as one coalesced 8-KB run (the AoS
+                // record stores put each lane's 16 B in its own 128-B line: 64
+                // lines per store instruction, 8 instructions per wave)
+                const int lane = threadIdx.x & 63;
+                const float4* st = U.nnstage[threadIdx.x >> 6];
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_wave_barrier();
+                const int base = i - lane;
+                float4* dst = reinterpret_cast<float4*>(job.nn + base);
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const int u = j * 64 + lane, rec = u >> 3;
+                    if (base + rec < job.n) dst[u] = st[rec * 8 + (((u & 7) + rec) & 7)];
+                }
+                // a flagged query's replay (same wave) reads its record back
+                if (__ballot(amb)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
             EVAL_MARK(6);
         } else {
