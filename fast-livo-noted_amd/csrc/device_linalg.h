@@ -124,6 +124,43 @@ __device__ __forceinline__ void lds_lu_column(const double* s_LU, const int* s_p
     }
 }
 
+// The same column solve with the factors read from the lanes that hold them:
+// after wave_lu_to_lds every lane's A is its row of the LU (row at position i
+// on lane piv[i]), so L / U entries come by v_readlane from registers instead
+// of as LDS broadcasts (no LDS round trip on the dependent chain).  The same
+// operations in the same order: bit for bit lds_lu_column.  Every lane < N of
+// the wave must hold its row (the caller keeps A from wave_lu_to_lds).
+template <int N>
+__device__ __forceinline__ void reg_lu_column(const double (&A)[N], const int* s_piv, int c, double (&y)[N]) {
+    int pv[N];
+#pragma unroll
+    for (int i = 0; i < N; i++) pv[i] = __builtin_amdgcn_readfirstlane(s_piv[i]);
+    // (scheduling barriers every 4 terms: the readlanes stay with their chain,
+    // not hoisted ahead into more scalar registers than the kernel has)
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        double sacc = (pv[i] == c) ? 1.0 : 0.0;
+#pragma unroll
+        for (int j = 0; j < i; j++) {
+            sacc = sacc - bcast(A[j], pv[i]) * y[j];
+            if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+        }
+        y[i] = sacc;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int i = N - 1; i >= 0; i--) {
+        double sacc = y[i];
+#pragma unroll
+        for (int j = i + 1; j < N; j++) {
+            sacc = sacc - bcast(A[j], pv[i]) * y[j];
+            if (((j - i) & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+        }
+        y[i] = sacc / bcast(A[i], pv[i]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 #define WAVE_SYNC() do { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); __builtin_amdgcn_wave_barrier(); } while (0)
 
 // SO3 Exp / Log (so3_math.h:55-81) and 3x3 products, sums in index order.

@@ -2332,7 +2332,23 @@ static int32_t register_scan(livo_ctx* c, const ScanBuf& s) {
 
 // The device buffers of a scan of N points: a released scan's when one fits
 // (capacity N .. 2N + 4096), else fresh allocations sized for N.
-static constexpr size_t kMaxSpareScans = 32;
+// Released scan buffers are kept for reuse up to a byte budget (LIVO_SPARE_MB,
+// default 8192): a hipFree synchronises the whole device, so freeing one while
+// a farm's batches and uploads are in flight stalled the pipeline (a 12.9 ms
+// upload call; the farm with uploads at 5.4k instead of 12.4k updates/s).
+static size_t scan_buf_bytes(int64_t cap) {
+    const int64_t cblk = std::max<int64_t>(1, (cap + kBlock * kPtsPerThread - 1) / (kBlock * kPtsPerThread));
+    return (size_t)cap * (16 + sizeof(NNRec) + 4 + 4 + 16 + 1) + partial_doubles(cap) * 8 +
+           (size_t)cblk * (kIkFewRows * 13 * 8 + 4);
+}
+static size_t spare_budget() {
+    static const size_t b = [] {
+        const char* e = std::getenv("LIVO_SPARE_MB");
+        const long long mb = e ? std::atoll(e) : 8192;
+        return (size_t)std::max(0LL, mb) << 20;
+    }();
+    return b;
+}
 static int alloc_scan_buf(livo_ctx* c, ScanBuf& s, int64_t N) {
     int best = -1;
     for (size_t k = 0; k < c->spare.size(); k++) {
@@ -2373,7 +2389,10 @@ static int alloc_scan_buf(livo_ctx* c, ScanBuf& s, int64_t N) {
 
 // Back to the spare list (the caller has synchronised the context's streams).
 static void release_scan_buf(livo_ctx* c, ScanBuf& s) {
-    if (c->spare.size() >= kMaxSpareScans) {
+    size_t kept = scan_buf_bytes(s.cap);
+    for (const ScanBuf& x : c->spare) kept += scan_buf_bytes(x.cap);
+    while (!c->spare.empty() && kept > spare_budget()) {  // the oldest go first
+        kept -= scan_buf_bytes(c->spare.front().cap);
         free_scan_buf(c->spare.front());
         c->spare.erase(c->spare.begin());
     }

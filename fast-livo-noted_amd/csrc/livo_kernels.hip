@@ -2235,7 +2235,7 @@ __device__ __forceinline__ bool esti_plane(const float (&px)[5], const float (&p
 // state delta 1e-5, covariance 1e-9).
 #ifdef LIVO_SOLVE_PROF  // phase timestamps for tools/solve_lab (compiled out of the product)
 __device__ unsigned long long g_solve_prof[256][16];
-#define SOLVE_MARK(k) do { if (threadIdx.x == 0) g_solve_prof[blockIdx.x][k] = __builtin_amdgcn_s_memtime(); } while (0)
+#define SOLVE_MARK(k) do { if ((threadIdx.x & 63) == 0) g_solve_prof[blockIdx.x][k] = __builtin_amdgcn_s_memtime(); } while (0)
 #else
 #define SOLVE_MARK(k) do { } while (0)
 #endif
@@ -2365,19 +2365,19 @@ __device__ __forceinline__ int solve_scan(IekfSlot* slot, SolveLds& L, const int
     }
     WAVE_SYNC();
     SPH_MARK(1);
-    {
-        double A[6];
+    double A6[6];
 #pragma unroll
-        for (int j = 0; j < 6; j++) A[j] = lane < 6 ? L.M[lane * 6 + j] : 0.0;
-        wave_lu_to_lds<6>(A, lane, L.LU, L.piv);
-    }
+    for (int j = 0; j < 6; j++) A6[j] = lane < 6 ? L.M[lane * 6 + j] : 0.0;
+    wave_lu_to_lds<6>(A6, lane, L.LU, L.piv);
     WAVE_SYNC();
     SPH_MARK(2);
-    if (lane < 6) {
+    {
         double y[6];
-        lds_lu_column<6>(L.LU, L.piv, lane, y);
+        reg_lu_column<6>(A6, L.piv, lane, y);  // (readlanes: every lane runs it)
+        if (lane < 6) {
 #pragma unroll
-        for (int i = 0; i < 6; i++) L.Minv[i * 6 + lane] = y[i];
+            for (int i = 0; i < 6; i++) L.Minv[i * 6 + lane] = y[i];
+        }
     }
     if (SPLIT_VEC) __syncthreads();  // L.vec from the other wave (it waits here too)
     if (lane < 6) {

@@ -103,18 +103,18 @@ __device__ void vio_gain(const VioSlot* slot, VioSolveLds& L, const int lane) {
         L.M[lane] = (r == c ? 1.0 : 0.0) + m;
     }
     WAVE_SYNC();
-    {
-        double Ar[6];
+    double Ar[6];
 #pragma unroll
-        for (int j = 0; j < 6; j++) Ar[j] = lane < 6 ? L.M[lane * 6 + j] : 0.0;
-        wave_lu_to_lds<6>(Ar, lane, L.LU, L.piv);
-    }
+    for (int j = 0; j < 6; j++) Ar[j] = lane < 6 ? L.M[lane * 6 + j] : 0.0;
+    wave_lu_to_lds<6>(Ar, lane, L.LU, L.piv);
     WAVE_SYNC();
-    if (lane < 6) {
+    {
         double y[6];
-        lds_lu_column<6>(L.LU, L.piv, lane, y);
+        reg_lu_column<6>(Ar, L.piv, lane, y);  // (readlanes: every lane runs it)
+        if (lane < 6) {
 #pragma unroll
-        for (int i = 0; i < 6; i++) L.Minv[i * 6 + lane] = y[i];
+            for (int i = 0; i < 6; i++) L.Minv[i * 6 + lane] = y[i];
+        }
     }
     WAVE_SYNC();
     for (int t = lane; t < kDim * 6; t += 64) {

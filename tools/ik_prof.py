@@ -2,8 +2,9 @@
 
 Build the profiling variant first:  python tools/ab_build.py ikprof -DLIVO_SOLVE_PROF
 then on the GPU box:  LIVO_LIB=fast-livo-noted_amd/lib/variants/ikprof.so python tools/ik_prof.py
-Marks (thread 0, s_memtime): 0 start, 1 partials merged per wave, 2 waves merged,
-3 boxminus + P copy, 4 SO3/S2 corrections, 5 (P/R)^-1, 6 P_temp^-1, 7 K_h/K_x,
+Marks (lane 0 of the wave that passes them, s_memtime): 0 start, 1 partials merged
+per wave, 2 waves merged; on the last wave beside them (ik_prep) 3 boxminus + P copy,
+4 SO3/S2 corrections, 5 (P/R)^-1; then 6 P_temp^-1, 7 K_h/K_x,
 8 dx_, boxplus and control, 9 covariance (stopping evaluations only).
 Development tool, not the product.
 """
@@ -32,8 +33,11 @@ def main():
             for b in range(8):
                 r = buf[16 * b: 16 * b + 16]
                 marks = [r[k] for k in range(10)]
-                d = [marks[k] - marks[k - 1] if marks[k] >= marks[k - 1] and marks[k - 1] else -1 for k in range(1, 10)]
-                print(f"rep {rep} block {b}: total {marks[8] - marks[0] if marks[8] > marks[0] else -1}  deltas {d}")
+                if not marks[0] or marks[0] == 2**64 - 1:
+                    continue
+                off = {k: marks[k] - marks[0] for k in range(1, 10) if marks[k] and marks[k] >= marks[0]
+                       and marks[k] - marks[0] < 10**7}
+                print(f"rep {rep} block {b}: cycles from mark 0: {off}")
 
 
 if __name__ == "__main__":
