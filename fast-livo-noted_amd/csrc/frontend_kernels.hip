@@ -224,23 +224,36 @@ __global__ void k_fe_centroid(FrontParams F, int64_t n_vox) {
     }
 }
 
-// livo_scan_upload's Morton key (0.25 m cells by default, 20 bits per axis)
-__global__ void k_fe_morton(const float* __restrict__ pts, int64_t n, int stride, const unsigned* minmax,
-                            float scale, unsigned long long* codes, uint32_t* iota) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    unsigned long long code = 0;
+// livo_scan_upload's Morton key: 9 bits per axis (27 bits) over the scan's
+// bounding box, cells of 1/scale m (0.25 m by default) or, for a box wider than
+// 512 cells, the box's widest extent / 512 (every scan keeps 512 cells per axis
+// at most, so one 32-bit radix sort orders it; 20 bits per axis and a 64-bit
+// sort took twice the passes).  lo / hi: the order-preserving encodings.
+__device__ __forceinline__ float fe_decode(unsigned o) { return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o); }
+__device__ __forceinline__ float fe_key_scale(const unsigned* lo, const unsigned* hi, float scale) {
+    float ext = 0.0f;
+#pragma unroll
+    for (int a = 0; a < 3; a++) ext = fmaxf(ext, fe_decode(hi[a]) - fe_decode(lo[a]));
+    return (ext * scale > 511.0f) ? 511.0f / ext : scale;
+}
+__device__ __forceinline__ uint32_t fe_key(const float* p, const unsigned* lo, float s) {
+    uint32_t code = 0;
 #pragma unroll
     for (int a = 0; a < 3; a++) {
-        const unsigned o = minmax[a];
-        const float lo = __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
-        float f = (pts[stride * i + a] - lo) * scale;
+        float f = (p[a] - fe_decode(lo[a])) * s;
         if (!(f >= 0.0f)) f = 0.0f;
-        const uint32_t q = (uint32_t)fminf(f, 1048575.0f);
+        const uint32_t q = (uint32_t)fminf(f, 511.0f);
 #pragma unroll
-        for (int b = 0; b < 20; b++) code |= (unsigned long long)((q >> b) & 1u) << (3 * b + a);
+        for (int b = 0; b < 9; b++) code |= ((q >> b) & 1u) << (3 * b + a);
     }
-    codes[i] = code;
+    return code;
+}
+__global__ void k_fe_morton(const float* __restrict__ pts, int64_t n, int stride, const unsigned* minmax,
+                            float scale, uint32_t* codes, uint32_t* iota) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float s = fe_key_scale(minmax, minmax + 3, scale);
+    codes[i] = fe_key(pts + stride * i, minmax, s);
     iota[i] = (uint32_t)i;
 }
 
@@ -299,23 +312,15 @@ __global__ __launch_bounds__(256) void k_fe_minmax_seg(const float* __restrict__
 }
 
 __global__ void k_fe_morton_seg(const float* __restrict__ pts, FeSegs S, const unsigned* minmax, float scale,
-                                unsigned long long* codes, uint32_t* iota) {
+                                uint32_t* codes, uint32_t* iota) {
     const int b = blockIdx.y;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= S.n[b]) return;
     const int64_t g = S.off[b] + i;
-    unsigned long long code = (unsigned long long)b << 60;
-#pragma unroll
-    for (int a = 0; a < 3; a++) {
-        const unsigned o = minmax[6 * b + a];
-        const float lo = __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
-        float f = (pts[3 * g + a] - lo) * scale;
-        if (!(f >= 0.0f)) f = 0.0f;
-        const uint32_t q = (uint32_t)fminf(f, 1048575.0f);
-#pragma unroll
-        for (int c = 0; c < 20; c++) code |= (unsigned long long)((q >> c) & 1u) << (3 * c + a);
-    }
-    codes[g] = code;
+    const unsigned* lo = minmax + 6 * b;
+    const unsigned hi[3] = {~lo[3], ~lo[4], ~lo[5]};  // (the maxes are stored inverted)
+    const float s = fe_key_scale(lo, hi, scale);
+    codes[g] = ((uint32_t)b << 27) | fe_key(pts + 3 * g, lo, s);
     iota[g] = (uint32_t)g;
 }
 
@@ -409,7 +414,7 @@ int launch_fe_centroid(const FrontParams& F, int64_t n_vox, void* stream) {
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 int launch_fe_morton(const float* pts, int64_t n, int stride, const unsigned* minmax, float scale,
-                     unsigned long long* codes, uint32_t* iota, void* stream) {
+                     uint32_t* codes, uint32_t* iota, void* stream) {
     FE_LAUNCH(k_fe_morton, n, pts, n, stride, minmax, scale, codes, iota);
 }
 int launch_fe_gather(const float* pts, int64_t n, int stride, const uint32_t* perm, float* pts4, int32_t* iperm,
@@ -417,7 +422,7 @@ int launch_fe_gather(const float* pts, int64_t n, int stride, const uint32_t* pe
     FE_LAUNCH(k_fe_gather, n, pts, n, stride, perm, pts4, iperm);
 }
 int launch_fe_build_seg(const float* pts, const FeSegs& S, int n_scans, int64_t max_n, unsigned* minmax, float scale,
-                        unsigned long long* codes, uint32_t* iota, void* stream) {
+                        uint32_t* codes, uint32_t* iota, void* stream) {
     if (n_scans <= 0 || n_scans > kFeSegMax || max_n <= 0) return n_scans == 0 ? LIVO_OK : LIVO_E_RANGE;
     const unsigned bx = (unsigned)((max_n + 255) / 256);
     const dim3 mm((unsigned)std::min<int64_t>(kMinmaxBlocks, bx), (unsigned)n_scans), g(bx, (unsigned)n_scans);

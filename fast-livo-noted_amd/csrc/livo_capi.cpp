@@ -2406,7 +2406,7 @@ static void release_scan_buf(livo_ctx* c, ScanBuf& s) {
 
 // Upload scratch of N points: [keys | sorted keys | iota | perm | bounds], then
 // (livo_scan_upload) the packed source points.
-static size_t up_tmp_bytes(int64_t N) { return (size_t)N * (8 + 8 + 4 + 4) + 256; }
+static size_t up_tmp_bytes(int64_t N) { return (size_t)N * (4 + 4 + 4 + 4) + 256; }
 static int ensure_up_tmp(livo_ctx* c, size_t bytes) {
     if (bytes <= c->up_tmp_bytes) return LIVO_OK;
     if (c->up_tmp) (void)hipFree(c->up_tmp);  // (synchronous: no upload is in flight)
@@ -2442,9 +2442,9 @@ static int ensure_dev_bytes(void** p, size_t* have, size_t need) {
 static int scan_build_on(const UpTarget& U, const float* d_src, int stride, int64_t N, ScanBuf& s) {
     if (N <= 0) return LIVO_OK;
     char* base = (char*)*U.tmp;
-    auto* codes = (unsigned long long*)base;
+    auto* codes = (uint32_t*)base;
     auto* scodes = codes + N;
-    auto* iota = (uint32_t*)(scodes + N);
+    auto* iota = scodes + N;
     auto* perm = iota + N;
     auto* mm = (unsigned*)(((uintptr_t)(perm + N) + 15) & ~(uintptr_t)15);
     int rc = LIVO_OK;
@@ -2456,13 +2456,13 @@ static int scan_build_on(const UpTarget& U, const float* d_src, int stride, int6
     if (!rc) rc = launch_fe_morton(d_src, N, stride, mm, morton_scale(), codes, iota, U.st);
     if (!rc) {
         size_t tb = 0;
-        rc = prim_sort_pairs_u64(nullptr, &tb, codes, scodes, iota, perm, N, 60, U.st);
+        rc = prim_sort_pairs_u32(nullptr, &tb, codes, scodes, iota, perm, N, 27, U.st);
         if (!rc && tb > *U.prim_bytes) {
             if (hipStreamSynchronize(U.st) != hipSuccess) rc = LIVO_E_HIP;
             if (!rc) rc = ensure_dev_bytes(U.prim, U.prim_bytes, tb);
         }
         tb = *U.prim_bytes;
-        if (!rc) rc = prim_sort_pairs_u64(*U.prim, &tb, codes, scodes, iota, perm, N, 60, U.st);
+        if (!rc) rc = prim_sort_pairs_u32(*U.prim, &tb, codes, scodes, iota, perm, N, 27, U.st);
     }
     if (!rc) rc = launch_fe_gather(d_src, N, stride, perm, s.pts, s.d_iperm, U.st);
     if (!rc && (hipMemcpyAsync(s.d_perm, perm, (size_t)N * 4, hipMemcpyDeviceToDevice, U.st) != hipSuccess ||
@@ -2614,7 +2614,11 @@ static bool host_pinned(const void* p) {
 int livo_host_register(livo_ctx* c, void* p, size_t bytes) {
     if (!c || !p || bytes == 0) return LIVO_E_INVALID;
     if (set_device(c)) return LIVO_E_HIP;
-    return hipHostRegister(p, bytes, hipHostRegisterDefault) == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+    // mapped + portable: the copy engine addresses the pages directly from any
+    // stream (hipHostRegisterDefault alone left some processes copying at ~6 GB/s,
+    // 1.5 ms of host time per 8 x 100k batch)
+    return hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable) == hipSuccess ? LIVO_OK
+                                                                                                    : LIVO_E_HIP;
 }
 int livo_host_unregister(livo_ctx* c, void* p) {
     if (!c || !p) return LIVO_E_INVALID;
@@ -2676,7 +2680,7 @@ int livo_scan_upload_batch_async(livo_ctx* c, const float* const* xyz, const int
         if (tot > (int64_t)0xFFFFFFFF - kBlock) return LIVO_E_RANGE;  // (32-bit positions in the batch sort)
         // build scratch (up_stream): [keys | sorted keys | iota | sorted iota | bounds (6 per scan)];
         // the packed points in the staging buffer of this pass (cp_stream copies into it)
-        const size_t kb = (size_t)tot * 8, vb = (size_t)tot * 4;
+        const size_t kb = (size_t)tot * 4, vb = (size_t)tot * 4;
         const size_t mm_off = 2 * kb + 2 * vb;
         const size_t tmp_need = mm_off + 6 * sizeof(unsigned) * kFeSegMax;
         const size_t bytes = (size_t)tot * 3 * sizeof(float);
@@ -2690,8 +2694,8 @@ int livo_scan_upload_batch_async(livo_ctx* c, const float* const* xyz, const int
             if (rc) return rc;
         }
         char* base = (char*)c->aup_tmp;
-        auto* codes = (unsigned long long*)base;
-        auto* scodes = (unsigned long long*)(base + kb);
+        auto* codes = (uint32_t*)base;
+        auto* scodes = (uint32_t*)(base + kb);
         auto* iota = (uint32_t*)(base + 2 * kb);
         auto* sorted = (uint32_t*)(base + 2 * kb + vb);
         auto* mm = (unsigned*)(base + mm_off);
@@ -2769,6 +2773,7 @@ int livo_scan_upload_batch_async(livo_ctx* c, const float* const* xyz, const int
                     return LIVO_E_HIP;
                 o += N[b0 + b];
             }
+            t_d = trace ? now_us() : 0.0;  // (the copies' host time)
         }
         if (hipEventRecord(c->bsrc_copied[sl], c->cp_stream) != hipSuccess ||
             hipStreamWaitEvent(c->up_stream, c->bsrc_copied[sl], 0) != hipSuccess)
@@ -2796,15 +2801,17 @@ int livo_scan_upload_batch_async(livo_ctx* c, const float* const* xyz, const int
         if (!rc && (hipMemsetD32Async((hipDeviceptr_t)mm, 0xFFFFFFFFu, 6 * kFeSegMax, c->up_stream) != hipSuccess))
             rc = LIVO_E_HIP;
         if (!rc) rc = launch_fe_build_seg(d_src, S, m, max_n, mm, morton_scale(), codes, iota, c->up_stream);
+        int key_bits = 27;  // + the scan index's bits
+        while ((1 << (key_bits - 27)) < m) key_bits++;
         if (!rc) {
             size_t tb = 0;
-            rc = prim_sort_pairs_u64(nullptr, &tb, codes, scodes, iota, sorted, tot, 64, c->up_stream);
+            rc = prim_sort_pairs_u32(nullptr, &tb, codes, scodes, iota, sorted, tot, key_bits, c->up_stream);
             if (!rc && tb > c->aup_prim_bytes) {
                 if (hipStreamSynchronize(c->up_stream) != hipSuccess) rc = LIVO_E_HIP;
                 if (!rc) rc = ensure_dev_bytes(&c->aup_prim, &c->aup_prim_bytes, tb);
             }
             tb = c->aup_prim_bytes;
-            if (!rc) rc = prim_sort_pairs_u64(c->aup_prim, &tb, codes, scodes, iota, sorted, tot, 64, c->up_stream);
+            if (!rc) rc = prim_sort_pairs_u32(c->aup_prim, &tb, codes, scodes, iota, sorted, tot, key_bits, c->up_stream);
         }
         if (!rc) rc = launch_fe_gather_seg(d_src, S, m, max_n, sorted, c->up_stream);
         if (!rc && hipEventRecord(c->bsrc_free[sl], c->up_stream) != hipSuccess) rc = LIVO_E_HIP;
@@ -2819,7 +2826,7 @@ int livo_scan_upload_batch_async(livo_ctx* c, const float* const* xyz, const int
             return rc;
         }
         if (trace)
-            std::fprintf(stderr, "[upload] %d scans %s: pinned check %.1f us, ring wait %.1f, pack %.1f, enqueue %.1f\n",
+            std::fprintf(stderr, "[upload] %d scans %s: pinned check %.1f us, ring wait %.1f, pack / copies %.1f, build %.1f\n",
                          (int)m, direct ? "direct" : "staged", t_b - t_a, t_c - t_b, t_d - t_c, now_us() - t_d);
         for (int32_t b = 0; b < m; b++) {
             if (N[b0 + b] == 0) {  // (an empty scan has nothing to build)

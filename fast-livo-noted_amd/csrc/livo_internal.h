@@ -486,9 +486,9 @@ int launch_fe_runs(const FrontParams& F, void* stream);
 int launch_fe_starts(const FrontParams& F, void* stream);
 int launch_fe_centroid(const FrontParams& F, int64_t n_vox, void* stream);
 int launch_fe_morton(const float* pts, int64_t n, int stride, const unsigned* minmax, float scale,
-                     unsigned long long* codes, uint32_t* iota, void* stream);
+                     uint32_t* codes, uint32_t* iota, void* stream);
 // A batch of at most kFeSegMax scans built in one pass (kernel argument table).
-constexpr int kFeSegMax = 16;  // (the scan index rides in the sort key's top 4 bits)
+constexpr int kFeSegMax = 16;  // (the scan index rides in the 32-bit sort key's bits 27..30)
 struct FeSegs {
     int64_t off[kFeSegMax];  // first point of scan b in the packed batch
     int64_t n[kFeSegMax];
@@ -499,7 +499,7 @@ struct FeSegs {
     uint8_t* pstate[kFeSegMax];
 };
 int launch_fe_build_seg(const float* pts, const FeSegs& S, int n_scans, int64_t max_n, unsigned* minmax, float scale,
-                        unsigned long long* codes, uint32_t* iota, void* stream);
+                        uint32_t* codes, uint32_t* iota, void* stream);
 int launch_fe_gather_seg(const float* pts, const FeSegs& S, int n_scans, int64_t max_n, const uint32_t* sorted,
                          void* stream);
 int launch_fe_gather(const float* pts, int64_t n, int stride, const uint32_t* perm, float* pts4, int32_t* iperm,
