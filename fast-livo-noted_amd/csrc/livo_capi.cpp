@@ -160,6 +160,12 @@ struct BatchLane {
     char* d_lm = nullptr;
     char* h_lm_dev = nullptr;  // h_lm's device address (host-mapped), for the kernel copies
     size_t lm_cap = 0;
+    // IKFoM batches: whole slots (their IKFoM block included) then the jobs,
+    // host pinned and device, per lane so two IKFoM batches can be in flight
+    char* h_ik = nullptr;
+    char* d_ik = nullptr;
+    char* h_ik_dev = nullptr;  // h_ik's device address (host-mapped), for the kernel copies
+    size_t ik_cap = 0;
     hipStream_t st[kMaxGroups] = {};
     hipEvent_t fork = nullptr;
     hipEvent_t done[kMaxGroups] = {};  // each group's last operation (its slot copy back)
@@ -417,6 +423,34 @@ static int ensure_lm(BatchLane& B, int32_t n) {
     return LIVO_OK;
 }
 
+static int ensure_ik(BatchLane& B, int32_t n) {
+    const size_t need = (size_t)n * (sizeof(IekfSlot) + sizeof(HsJob));
+    if (need <= B.ik_cap) return LIVO_OK;
+    const size_t cap = std::max(need, (size_t)8 * (sizeof(IekfSlot) + sizeof(HsJob)));
+    dev_free(B.d_ik);
+    if (B.h_ik) (void)hipHostFree(B.h_ik);
+    B.h_ik = nullptr;
+    B.ik_cap = 0;
+    if (hipMalloc((void**)&B.d_ik, cap) != hipSuccess) {
+        B.d_ik = nullptr;
+        return LIVO_E_OOM;
+    }
+    // mapped + coherent: a submitted batch's staging copies are kernels (as the
+    // LaserMapping lanes'); DMA copies behind another lane's kernels held the
+    // submitting host 2-3 ms per batch
+    if (hipHostMalloc((void**)&B.h_ik, cap, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+        B.h_ik = nullptr;
+        return LIVO_E_OOM;
+    }
+    B.h_ik_dev = nullptr;
+    if (hipHostGetDevicePointer((void**)&B.h_ik_dev, B.h_ik, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        B.h_ik_dev = nullptr;  // DMA copies then
+    }
+    B.ik_cap = cap;
+    return LIVO_OK;
+}
+
 // A lane's group streams: lane 0 the context's, the others their own.
 static int lane_streams(livo_ctx* c, int L) {
     BatchLane& B = c->lane[L];
@@ -458,16 +492,19 @@ static bool params_valid(const livo_params* p) {
            p->flags == 0;
 }
 
+// Replay counters and lists per lane (LIVO_MAX_INFLIGHT slices: lane L's
+// counters at L * kMaxGroups, its list at L * replay_cap), so two unfused
+// batches in flight (IKFoM) keep theirs apart.
 static int ensure_replay(livo_ctx* c, int64_t total) {
-    if (!c->d_replay_count && dev_alloc(&c->d_replay_count, kMaxGroups)) return LIVO_E_OOM;
+    if (!c->d_replay_count && dev_alloc(&c->d_replay_count, (size_t)kMaxGroups * LIVO_MAX_INFLIGHT)) return LIVO_E_OOM;
     if (!c->d_replay_total) {
         if (dev_alloc(&c->d_replay_total, 1)) return LIVO_E_OOM;
         HIP_TRY(hipMemset(c->d_replay_total, 0, sizeof(unsigned long long)));
     }
     if (total <= c->replay_cap) return LIVO_OK;
-    dev_free(c->d_replay_list);
+    dev_free(c->d_replay_list);  // (hipFree waits for the device: no batch is still using it)
     c->replay_cap = 0;
-    if (dev_alloc(&c->d_replay_list, (size_t)total)) return LIVO_E_OOM;
+    if (dev_alloc(&c->d_replay_list, (size_t)total * LIVO_MAX_INFLIGHT)) return LIVO_E_OOM;
     c->replay_cap = total;
     return LIVO_OK;
 }
@@ -1626,6 +1663,8 @@ int livo_ctx_destroy(livo_ctx* c) {
             for (int k = 0; k < kMaxGroups; k++)
                 if (B.st[k]) (void)hipStreamDestroy(B.st[k]);
         if (B.owned_fork && B.fork) (void)hipEventDestroy(B.fork);
+        dev_free(B.d_ik);
+        if (B.h_ik) (void)hipHostFree(B.h_ik);
         for (hipEvent_t e : B.done)
             if (e) (void)hipEventDestroy(e);
     }
@@ -3067,18 +3106,18 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
                     if (std::binary_search(sorted.begin(), sorted.end(), id)) return LIVO_E_INVALID;
     }
     const bool lm = model != kModelIkfom;
-    // the IKFoM model stages in the context's whole slots: synchronous batches on lane 0 only
-    if (!lm && (L != 0 || !sync)) return LIVO_E_INVALID;
     // the fused evaluation: search + replay + plane pass + solve in one launch
     const bool fused = c->fused && model == kModelLaserMapping && c->backend == LIVO_BACKEND_IKDTREE &&
                        c->knn_kind == 2;
-    // the unfused passes' replay lists are per context: synchronous batches only
-    // (checked before any device work, so a refused submit leaves nothing queued)
-    if (!fused && (L != 0 || !sync)) return LIVO_E_INVALID;
+    // the unfused LaserMapping passes (iVox: per-context search scratch) run as
+    // synchronous batches only; IKFoM batches keep their staging and replay
+    // lists per lane (checked before any device work, so a refused submit
+    // leaves nothing queued)
+    if (!fused && lm && (L != 0 || !sync)) return LIVO_E_INVALID;
     if (set_device(c)) return LIVO_E_HIP;
     int rc = lane_streams(c, L);
     if (rc) return rc;
-    rc = lm ? ensure_lm(B, n) : ensure_slots(c, n);
+    rc = lm ? ensure_lm(B, n) : ensure_ik(B, n);
     if (rc) return rc;
     // Slots and jobs: the IKFoM model uses whole slots (c->h_slots / d_slots);
     // the LaserMapping model only the part before the IKFoM block, packed at
@@ -3086,10 +3125,10 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
     // copy each way.  (A packed slot is addressed as an IekfSlot whose IKFoM
     // block lies outside the buffer; the LaserMapping kernels never touch it.)
     const size_t stride = lm ? kLmStride : sizeof(IekfSlot);
-    char* const hbase = lm ? B.h_lm : reinterpret_cast<char*>(c->h_slots);
-    char* const dbase = lm ? B.d_lm : reinterpret_cast<char*>(c->d_slots);
-    HsJob* const hjobs = lm ? reinterpret_cast<HsJob*>(B.h_lm + (size_t)n * kLmStride) : c->h_jobs;
-    HsJob* const djobs = lm ? reinterpret_cast<HsJob*>(B.d_lm + (size_t)n * kLmStride) : c->d_jobs;
+    char* const hbase = lm ? B.h_lm : B.h_ik;
+    char* const dbase = lm ? B.d_lm : B.d_ik;
+    HsJob* const hjobs = reinterpret_cast<HsJob*>(hbase + (size_t)n * stride);
+    HsJob* const djobs = reinterpret_cast<HsJob*>(dbase + (size_t)n * stride);
     auto hslot = [&](int32_t b) -> IekfSlot& { return *reinterpret_cast<IekfSlot*>(hbase + (size_t)b * stride); };
     auto dslot = [&](int32_t b) { return reinterpret_cast<IekfSlot*>(dbase + (size_t)b * stride); };
     const int max_iter = c->params.max_iterations;
@@ -3138,7 +3177,9 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
     c->last_lane = L;
     // kernel copies for batches queued behind another on shared streams (a DMA
     // copy there waits on an engine hand-off); LIVO_LANE_ZC=0: DMA copies always
-    const bool kcopy = lm && B.h_lm_dev && (sync ? c->sync_zc : c->lane_zc);
+    const bool kcopy = (lm ? B.h_lm_dev != nullptr : B.h_ik_dev != nullptr) && (sync ? c->sync_zc : c->lane_zc);
+    const size_t ik_bytes = (size_t)n * (sizeof(IekfSlot) + sizeof(HsJob));
+    static_assert((sizeof(IekfSlot) + sizeof(HsJob)) % 16 == 0 && sizeof(IekfSlot) % 16 == 0, "16-B word copies");
     const bool persist = fused && lm && c->persist && !full && max_iter + 1 >= 2;
     unsigned* dteam = nullptr;
     if (persist) {  // (before the staging copy below: it clears the device counters)
@@ -3151,9 +3192,11 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
     } else if (lm) {
         HIP_TRY(hipMemcpyAsync(B.d_lm, B.h_lm, lm_bytes(n), hipMemcpyHostToDevice,
                                B.st[0]));
+    } else if (kcopy) {
+        rc = launch_copy_words(B.h_ik_dev, B.d_ik, ik_bytes, B.st[0]);
+        if (rc) return rc;
     } else {
-        HIP_TRY(hipMemcpyAsync(c->d_slots, c->h_slots, sizeof(IekfSlot) * n, hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(hipMemcpyAsync(c->d_jobs, c->h_jobs, sizeof(HsJob) * n, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(B.d_ik, B.h_ik, ik_bytes, hipMemcpyHostToDevice, B.st[0]));
     }
 
     // The batch in groups on separate streams: the latency-bound kernels of
@@ -3191,7 +3234,9 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
             off += s->n;
         }
     }
-    if (!fused) HIP_TRY(hipMemsetAsync(c->d_replay_count, 0, sizeof(unsigned) * kMaxGroups, c->stream));
+    unsigned* const rcount = c->d_replay_count + (size_t)L * kMaxGroups;  // this lane's
+    unsigned long long* const rlist = c->d_replay_list + (size_t)L * c->replay_cap;
+    if (!fused) HIP_TRY(hipMemsetAsync(rcount, 0, sizeof(unsigned) * kMaxGroups, B.st[0]));
     // profiling: the batch's first search starts at ev[0][0], before the fork
     if (prof) HIP_TRY(hipEventRecord(c->ev[0][0], c->stream));
     if (ngroups > 1) {
@@ -3206,12 +3251,12 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
         hp[gi].jobs = djobs + g[gi].first;
         kp[gi] = make_knn_params(c);
         kp[gi].jobs = djobs + g[gi].first;
-        kp[gi].replay_count = c->d_replay_count + gi;
-        kp[gi].replay_list = c->d_replay_list + g[gi].off;
+        kp[gi].replay_count = rcount + gi;
+        kp[gi].replay_list = rlist + g[gi].off;
         // the iVox overflow pass of each group has its own scratch slices (groups run concurrently)
         if (kp[gi].iv.scratch) kp[gi].iv.scratch += (int64_t)gi * c->iv.big_threads * c->iv.big_slice;
         hp[gi].solve = lm ? 1 : 0;  // the last plane-pass block of each scan runs its solve (IKFoM: k_solve_ik below)
-        hp[gi].replay_count = c->d_replay_count + gi;
+        hp[gi].replay_count = rcount + gi;
     }
     // Persistent: the first evaluation (search), then the run of evaluations without
     // one (k_iekf_ns), the one search a rematch asks for (k_iekf_eval: the solve
@@ -3259,8 +3304,8 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
         if (wb) {
             // (written by the stopping solves)
         } else if (kcopy) {
-            rc = launch_copy_words(dslot(g[gi].first), B.h_lm_dev + (size_t)g[gi].first * stride, stride * g[gi].count,
-                                   g[gi].st);
+            rc = launch_copy_words(dslot(g[gi].first), (lm ? B.h_lm_dev : B.h_ik_dev) + (size_t)g[gi].first * stride,
+                                   stride * g[gi].count, g[gi].st);
             if (rc) return rc;
         } else {
             HIP_TRY(hipMemcpyAsync(&hslot(g[gi].first), dslot(g[gi].first), stride * g[gi].count,
@@ -3304,7 +3349,7 @@ static int batch_collect(livo_ctx* c, int L, livo_state* states, livo_iter_stats
     const int ngroups = B.ngroups;
     const bool lm = model != kModelIkfom;
     const size_t stride = lm ? kLmStride : sizeof(IekfSlot);
-    char* const hbase = lm ? B.h_lm : reinterpret_cast<char*>(c->h_slots);
+    char* const hbase = lm ? B.h_lm : B.h_ik;
     auto hslot = [&](int32_t b) -> IekfSlot& { return *reinterpret_cast<IekfSlot*>(hbase + (size_t)b * stride); };
     const bool fused = c->fused && model == kModelLaserMapping && c->backend == LIVO_BACKEND_IKDTREE &&
                        c->knn_kind == 2;
@@ -3417,14 +3462,14 @@ int livo_iekf_update_batch(livo_ctx* c, int32_t n, const int32_t* ids, livo_stat
     return batch_update(c, n, ids, kModelLaserMapping, states, priors, stats, nullptr, nullptr);
 }
 
-int livo_iekf_update_batch_submit(livo_ctx* c, int32_t n, const int32_t* ids, const livo_state* states,
-                                  const livo_state* priors, int32_t* ticket) {
+static int batch_submit(livo_ctx* c, int32_t n, const int32_t* ids, int model, const livo_state* states,
+                        const livo_state* priors, const livo_ikfom_state* ik_states, int32_t* ticket) {
     if (!c || !ticket) return LIVO_E_INVALID;
     int L = -1;
     for (int l = 0; l < LIVO_MAX_INFLIGHT && L < 0; l++)
         if (!c->lane[l].busy) L = l;
     if (L < 0) return LIVO_E_BUSY;
-    int rc = batch_enqueue(c, L, n, ids, kModelLaserMapping, states, priors, nullptr, false);
+    int rc = batch_enqueue(c, L, n, ids, model, states, priors, ik_states, false);
     if (rc) {
         BatchLane& B = c->lane[L];
         for (int k = 0; k < kMaxGroups && B.st[k]; k++) (void)hipStreamSynchronize(B.st[k]);
@@ -3440,19 +3485,38 @@ int livo_iekf_update_batch_submit(livo_ctx* c, int32_t n, const int32_t* ids, co
     return LIVO_OK;
 }
 
-int livo_iekf_update_batch_wait(livo_ctx* c, int32_t ticket, livo_state* states, livo_iter_stats* stats) {
+int livo_iekf_update_batch_submit(livo_ctx* c, int32_t n, const int32_t* ids, const livo_state* states,
+                                  const livo_state* priors, int32_t* ticket) {
+    return batch_submit(c, n, ids, kModelLaserMapping, states, priors, nullptr, ticket);
+}
+
+static int batch_wait(livo_ctx* c, int32_t ticket, int model, livo_state* states, livo_iter_stats* stats,
+                      livo_ikfom_state* ik_states, livo_ikfom_stats* ik_stats) {
     if (!c || ticket < 0) return LIVO_E_INVALID;
     const int L = ticket % LIVO_MAX_INFLIGHT;
     BatchLane& B = c->lane[L];
     if (!B.busy || B.ticket != ticket) return LIVO_E_INVALID;
-    if (B.n > 0 && !states) return LIVO_E_INVALID;
+    if (B.n > 0 && (B.model != model || (model == kModelIkfom ? !ik_states : !states))) return LIVO_E_INVALID;
     if (set_device(c)) return LIVO_E_HIP;
     B.ticket = -1;
     if (B.n == 0) {
         B.busy = false;
         return LIVO_OK;
     }
-    return batch_collect(c, L, states, stats, nullptr, nullptr, false);
+    return batch_collect(c, L, states, stats, ik_states, ik_stats, false);
+}
+
+int livo_iekf_update_batch_wait(livo_ctx* c, int32_t ticket, livo_state* states, livo_iter_stats* stats) {
+    return batch_wait(c, ticket, kModelLaserMapping, states, stats, nullptr, nullptr);
+}
+
+int livo_ikfom_update_batch_submit(livo_ctx* c, int32_t n, const int32_t* ids, const livo_ikfom_state* states,
+                                   int32_t* ticket) {
+    return batch_submit(c, n, ids, kModelIkfom, nullptr, nullptr, states, ticket);
+}
+
+int livo_ikfom_update_batch_wait(livo_ctx* c, int32_t ticket, livo_ikfom_state* states, livo_ikfom_stats* stats) {
+    return batch_wait(c, ticket, kModelIkfom, nullptr, nullptr, states, stats);
 }
 
 int livo_iekf_update(livo_ctx* c, int32_t id, livo_state* state, const livo_state* prior, livo_iter_stats* stats) {

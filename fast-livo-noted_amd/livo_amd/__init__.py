@@ -182,6 +182,8 @@ SIGNATURES = {
     "livo_iekf_update_batch_wait": (C.c_int, [_P, C.c_int32, _P, _P]),
     "livo_ikfom_update": (C.c_int, [_P, C.c_int32, C.POINTER(IkfomState), C.POINTER(IkfomStats)]),
     "livo_ikfom_update_batch": (C.c_int, [_P, C.c_int32, _P, _P, _P]),
+    "livo_ikfom_update_batch_submit": (C.c_int, [_P, C.c_int32, _P, _P, C.POINTER(C.c_int32)]),
+    "livo_ikfom_update_batch_wait": (C.c_int, [_P, C.c_int32, _P, _P]),
     "livo_ctx_set_backend": (C.c_int, [_P, C.c_int]),
     "livo_ivox_params_default": (C.c_int, [C.POINTER(IvoxParams)]),
     "livo_ivox_init": (C.c_int, [_P, C.POINTER(IvoxParams)]),
@@ -537,6 +539,30 @@ class Context:
         if raw:
             return sts, stats
         return [ikfom_from_c(s) for s in sts], [ikfom_stats_from_c(s) for s in stats]
+
+    def ikfom_update_batch_submit(self, sids, states, raw: bool = False) -> int:
+        """livo_ikfom_update_batch_submit: enqueue, return the ticket."""
+        n = len(sids)
+        ids = (C.c_int32 * max(n, 1))(*sids)
+        sts = states if raw else (IkfomState * max(n, 1))(*[ikfom_to_c(s) for s in states])
+        t = C.c_int32()
+        _check("livo_ikfom_update_batch_submit",
+               self._L.livo_ikfom_update_batch_submit(self.h, n, C.cast(ids, C.c_void_p), C.cast(sts, C.c_void_p),
+                                                      C.byref(t)))
+        return t.value
+
+    def ikfom_update_batch_wait(self, ticket: int, n: int, out=None, stats=None):
+        """livo_ikfom_update_batch_wait; with out / stats (ctypes arrays) the raw arrays."""
+        raw = out is not None
+        if out is None:
+            out = (IkfomState * max(n, 1))()
+            stats = (IkfomStats * max(n, 1))()
+        _check("livo_ikfom_update_batch_wait",
+               self._L.livo_ikfom_update_batch_wait(self.h, ticket, C.cast(out, C.c_void_p),
+                                                    C.cast(stats, C.c_void_p) if stats is not None else None))
+        if raw:
+            return out, stats
+        return [ikfom_from_c(out[b]) for b in range(n)], [ikfom_stats_from_c(stats[b]) for b in range(n)]
 
     # ----------------------------------------------------------- iVox ----
     def set_backend(self, backend: int):

@@ -297,6 +297,12 @@ typedef struct livo_ikfom_stats {
 int livo_ikfom_update_batch(livo_ctx* ctx, int32_t n, const int32_t* scan_ids, livo_ikfom_state* states,
                             livo_ikfom_stats* stats);
 int livo_ikfom_update(livo_ctx* ctx, int32_t scan_id, livo_ikfom_state* state, livo_ikfom_stats* stats);
+/* The IKFoM batch split into enqueue and collect, as livo_iekf_update_batch_submit
+ * / _wait (the same LIVO_MAX_INFLIGHT lanes and tickets; a ticket is collected
+ * with the wait of its own model). */
+int livo_ikfom_update_batch_submit(livo_ctx* ctx, int32_t n, const int32_t* scan_ids, const livo_ikfom_state* states,
+                                   int32_t* ticket);
+int livo_ikfom_update_batch_wait(livo_ctx* ctx, int32_t ticket, livo_ikfom_state* states, livo_ikfom_stats* stats);
 
 /* ------------------------------------------------------------------------
  * iVox backend: faster_lio::IVox<3, DEFAULT, PointType>

@@ -133,3 +133,35 @@ def test_ikfom_full_size_1M(built):
         g, gs = c.ikfom_update(sid, st0)
     r, rs = tree.ikfom_update(body, st0, max_iter=4, threads=8)
     _compare(g, gs, r, rs, st0)
+
+
+def test_ikfom_submit_wait_pipelined(ctx):
+    """livo_ikfom_update_batch_submit / _wait: two IKFoM batches in flight (their
+    slots, jobs and replay lists per lane) give bit for bit the synchronous
+    batches' states and statistics; a third submit while both lanes are busy is
+    LIVO_E_BUSY; a LaserMapping wait on an IKFoM ticket is LIVO_E_INVALID."""
+    import livo_amd
+    from livo_amd import synth
+    scans = [synth.make_scan(4000 + 211 * s, s + 40)[0] for s in range(10)]
+    states = [synth.make_ikfom_state(s + 40) for s in range(10)]
+    sids = [ctx.scan_upload(b) for b in scans]
+    try:
+        ref_a = ctx.ikfom_update_batch(sids[:5], states[:5])
+        ref_b = ctx.ikfom_update_batch(sids[5:], states[5:])
+        ta = ctx.ikfom_update_batch_submit(sids[:5], states[:5])
+        tb = ctx.ikfom_update_batch_submit(sids[5:], states[5:])
+        with pytest.raises(livo_amd.LivoError) as e:
+            ctx.ikfom_update_batch_submit(sids[:1], states[:1])
+        assert e.value.code == -8  # LIVO_E_BUSY
+        with pytest.raises(livo_amd.LivoError):
+            ctx.iekf_update_batch_wait(ta, 5)
+        got_b = ctx.ikfom_update_batch_wait(tb, 5)  # out of order
+        got_a = ctx.ikfom_update_batch_wait(ta, 5)
+        for got, ref in ((got_a, ref_a), (got_b, ref_b)):
+            for i in range(5):
+                assert all(np.array_equal(got[0][i][k], ref[0][i][k]) for k in ref[0][i])
+                assert got[1][i]["iterations"] == ref[1][i]["iterations"]
+                assert np.array_equal(got[1][i]["dx"], ref[1][i]["dx"])
+    finally:
+        for sid in sids:
+            ctx.scan_release(sid)
