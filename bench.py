@@ -420,7 +420,6 @@ def main():
     upload_counters = upload_counters_pg = farm.Counters()
     elapsed_up = elapsed_up_pg = 0.0
     if n_up >= 1:
-        upload_counters_pg, elapsed_up_pg = upload_leg()
         for x, _ in up_sets:
             for arr in x:
                 ctx.host_register(arr)
@@ -428,6 +427,7 @@ def main():
         for x, _ in up_sets:
             for arr in x:
                 ctx.host_unregister(arr)
+        upload_counters_pg, elapsed_up_pg = upload_leg()
 
     # The same steps one synchronous batch at a time (the host waits for each
     # batch before the next is queued), untimed for the headline and reported

@@ -421,6 +421,42 @@ int launch_fe_gather(const float* pts, int64_t n, int stride, const uint32_t* pe
                      void* stream) {
     FE_LAUNCH(k_fe_gather, n, pts, n, stride, perm, pts4, iperm);
 }
+// Scan b's 3 n floats from its mapped host array: 16-B reads when the source is
+// 16-B aligned (then 12 n / 16 words and a tail), else 4-B reads; blockIdx.y = b.
+__global__ __launch_bounds__(256) void k_fe_copy_seg(FeSrc S, float* __restrict__ dst) {
+    const int b = blockIdx.y;
+    const float* src = S.src[b];
+    float* d = dst + 3 * S.off[b];
+    const int64_t nf = 3 * S.n[b];
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if ((((uintptr_t)src | (uintptr_t)d) & 15u) == 0u) {
+        const int64_t nw = nf >> 2;
+        const float4* s4 = reinterpret_cast<const float4*>(src);
+        float4* d4 = reinterpret_cast<float4*>(d);
+        // 4 reads in flight per thread: the PCIe round trip, not the CU count, sets the rate
+        int64_t w = t;
+        for (; w + 3 * stride < nw; w += 4 * stride) {
+            float4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) v[u] = s4[w + u * stride];
+#pragma unroll
+            for (int u = 0; u < 4; u++) d4[w + u * stride] = v[u];
+        }
+        for (; w < nw; w += stride) d4[w] = s4[w];
+        for (int64_t k = 4 * nw + t; k < nf; k += stride) d[k] = src[k];
+    } else {
+        for (int64_t k = t; k < nf; k += stride) d[k] = src[k];
+    }
+}
+int launch_fe_copy_seg(const FeSrc& S, int n_scans, int64_t max_n, float* dst, void* stream) {
+    if (n_scans <= 0 || n_scans > kFeSegMax || max_n <= 0) return n_scans == 0 ? LIVO_OK : LIVO_E_RANGE;
+    // 16 blocks a scan (4 x 16 B in flight per thread, ~256 KB per batch in flight):
+    // enough outstanding reads for the link without holding the CUs the batches run on
+    const unsigned bx = (unsigned)std::min<int64_t>(16, (3 * max_n / 4 + 255) / 256);
+    hipLaunchKernelGGL(k_fe_copy_seg, dim3(bx, (unsigned)n_scans), dim3(256), 0, (hipStream_t)stream, S, dst);
+    return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
 int launch_fe_build_seg(const float* pts, const FeSegs& S, int n_scans, int64_t max_n, unsigned* minmax, float scale,
                         uint32_t* codes, uint32_t* iota, void* stream) {
     if (n_scans <= 0 || n_scans > kFeSegMax || max_n <= 0) return n_scans == 0 ? LIVO_OK : LIVO_E_RANGE;

@@ -2804,13 +2804,43 @@ int livo_scan_upload_batch_async(livo_ctx* c, const float* const* xyz, const int
                 return LIVO_E_HIP;
             P->inflight = true;
         } else {
+            // page-locked caller arrays: one kernel reads them through their mapped
+            // device addresses (no DMA command per scan: a hipMemcpyAsync of one
+            // held the host 13-16 ms now and then inside a running farm);
+            // LIVO_UPLOAD_DMA=1 or an unmapped array: DMA copies
+            static const bool use_dma = [] {
+                const char* e = std::getenv("LIVO_UPLOAD_DMA");
+                return e && std::atoi(e) != 0;
+            }();
+            FeSrc F{};
+            bool mapped = !use_dma;
             int64_t o = 0;
             for (int32_t b = 0; b < m; b++) {
-                if (N[b0 + b] > 0 &&
-                    hipMemcpyAsync(d_src + 3 * o, xyz[b0 + b], (size_t)N[b0 + b] * 3 * sizeof(float),
-                                   hipMemcpyHostToDevice, c->cp_stream) != hipSuccess)
-                    return LIVO_E_HIP;
+                F.off[b] = o;
+                F.n[b] = N[b0 + b];
+                F.src[b] = nullptr;
+                if (mapped && N[b0 + b] > 0) {
+                    void* dp = nullptr;
+                    if (hipHostGetDevicePointer(&dp, const_cast<float*>(xyz[b0 + b]), 0) != hipSuccess || !dp) {
+                        (void)hipGetLastError();
+                        mapped = false;
+                    }
+                    F.src[b] = (const float*)dp;
+                }
                 o += N[b0 + b];
+            }
+            if (mapped) {
+                const int r2 = launch_fe_copy_seg(F, m, max_n, d_src, c->cp_stream);
+                if (r2) return r2;
+            } else {
+                o = 0;
+                for (int32_t b = 0; b < m; b++) {
+                    if (N[b0 + b] > 0 &&
+                        hipMemcpyAsync(d_src + 3 * o, xyz[b0 + b], (size_t)N[b0 + b] * 3 * sizeof(float),
+                                       hipMemcpyHostToDevice, c->cp_stream) != hipSuccess)
+                        return LIVO_E_HIP;
+                    o += N[b0 + b];
+                }
             }
             t_d = trace ? now_us() : 0.0;  // (the copies' host time)
         }

@@ -498,6 +498,14 @@ struct FeSegs {
     void* nn[kFeSegMax];
     uint8_t* pstate[kFeSegMax];
 };
+// A batch's points copied by a kernel from host-mapped (page-locked) caller
+// arrays into the packed device staging (dst + 3 * off[b]).
+struct FeSrc {
+    const float* src[kFeSegMax];  // device addresses of the mapped host arrays
+    int64_t off[kFeSegMax];
+    int64_t n[kFeSegMax];
+};
+int launch_fe_copy_seg(const FeSrc& S, int n_scans, int64_t max_n, float* dst, void* stream);
 int launch_fe_build_seg(const float* pts, const FeSegs& S, int n_scans, int64_t max_n, unsigned* minmax, float scale,
                         uint32_t* codes, uint32_t* iota, void* stream);
 int launch_fe_gather_seg(const float* pts, const FeSegs& S, int n_scans, int64_t max_n, const uint32_t* sorted,
