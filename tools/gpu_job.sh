@@ -7,6 +7,7 @@
 #   smoke                 __graft_entry__.smoke()
 #   bench[=ARGS]          python bench.py ARGS  (default: the full default line)
 #   ab=R=SPEC,SPEC..      pooled-headline A/B in R rounds (tools/ab_pool.sh spec syntax)
+#   abs=R=SPEC;SPEC..     the same with ';' between specs (a spec may set several VAR=VAL,VAR=VAL)
 #   c5ab=SPEC,SPEC..      config-5 leg per variant (tools/c5_ab.sh)
 #   kt[=ARGS]             rocprofv3 --kernel-trace --stats over bench.py ARGS
 #                         (default: the headline leg, 20 steps)
@@ -40,6 +41,10 @@ for step in "$@"; do
       tail -1 "$log" ;;
     ab)
       rounds=${arg%%=*}; specs=$(echo "${arg#*=}" | tr ',' ' ')
+      (cd "$R" && bash tools/ab_pool.sh "$rounds" $specs) > "$log" 2>&1 || { tail -30 "$log"; exit 1; }
+      python tools/ab_summary.py gpurun_out >> "$log" 2>&1; tail -20 "$log" ;;
+    abs)  # as ab, specs separated by ';' so a spec can carry several VAR=VAL (comma-separated)
+      rounds=${arg%%=*}; specs=$(echo "${arg#*=}" | tr ';' ' ')
       (cd "$R" && bash tools/ab_pool.sh "$rounds" $specs) > "$log" 2>&1 || { tail -30 "$log"; exit 1; }
       python tools/ab_summary.py gpurun_out >> "$log" 2>&1; tail -20 "$log" ;;
     c5ab)
