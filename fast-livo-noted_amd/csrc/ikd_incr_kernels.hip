@@ -15,7 +15,7 @@
 //                 face (neighbouring float boxes overlap or leave a gap) marks
 //                 the boxes it touches dirty
 //   (stable radix sort by box key: a box's points in input order)
-//   k_add_group   one thread per box: its stored points from the cell grid,
+//   k_add_box     one wave per box: its stored points from the cell grid,
 //                 then the box's whole sequence of new points.  Boxes are
 //                 independent, except dirty boxes and boxes holding a stored
 //                 point that lies in two boxes: those are deferred
@@ -176,7 +176,7 @@ __global__ void k_add_heads(DynAddParams P) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= P.n) return;
     P.heads[k] = (k == 0 || P.skeys[k] != P.skeys[k - 1]) ? 1u : 0u;
-    // the points in box order: k_add_group then walks a box's sequence with contiguous loads
+    // the points in box order: k_add_box then walks a box's sequence with contiguous loads
     const uint32_t i = P.svals[k];
     const float4 p = reinterpret_cast<const float4*>(P.W)[i];
     reinterpret_cast<float4*>(P.Ws)[k] = make_float4(p.x, p.y, p.z, __uint_as_float(i));
@@ -193,9 +193,48 @@ __global__ void k_add_starts(DynAddParams P) {
     }
 }
 
-// A box's stored points (Search_by_range): count, the first nearest in id
-// order, whether another one ties with it at a different position; `defer`
-// if the box is dirty or holds a point that also lies in a neighbouring box.
+// A box's stored points (Search_by_range), one wave per box: the lanes take
+// the grid cells the box overlaps (one hash probe each), then the cells'
+// points spread over the lanes (a point's cell by a binary search of the
+// cells' exclusive counts in LDS).  `f(q, lane)` per stored point.
+struct WaveCells {
+    uint32_t exc[64], start[64];
+};
+template <class F>
+__device__ __forceinline__ void wave_box_points(const DynAddParams& P, const int (&l)[3], const int (&h)[3], int lane,
+                                                WaveCells& W, F&& f) {
+    const int ex = h[0] - l[0] + 1, ey = h[1] - l[1] + 1, ez = h[2] - l[2] + 1;
+    const int ncell = (ex > 0 && ey > 0 && ez > 0) ? ex * ey * ez : 0;
+    const float4* __restrict__ gp = reinterpret_cast<const float4*>(P.gpts);
+    for (int c0 = 0; c0 < ncell; c0 += 64) {  // wave-uniform
+        const int c = c0 + lane;
+        uint2 r = make_uint2(0u, 0u);
+        if (c < ncell) r = cell_run(P.gslots, P.glog2, l[0] + c % ex, l[1] + (c / ex) % ey, l[2] + c / (ex * ey));
+        uint32_t inc = r.y;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t v = __shfl_up(inc, off, 64);
+            if (lane >= off) inc += v;
+        }
+        const uint32_t total = __shfl(inc, 63, 64);
+        W.exc[lane] = inc - r.y;
+        W.start[lane] = r.x;
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t t = lane; t < total; t += 64) {
+            int j = 0;  // the last cell whose exclusive count is <= t (it holds point t)
+#pragma unroll
+            for (int step = 32; step >= 1; step >>= 1)
+                if (W.exc[j + step] <= t) j += step;
+            f(gp[W.start[j] + (t - W.exc[j])]);
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+// A box's stored points: count, the first nearest in id order, whether points
+// of two different positions share the nearest distance (the reference's tie,
+// decided by its tree order); `defer` if the box is dirty or holds a point that
+// also lies in a neighbouring box.  The lanes' partial results merge in any
+// order to the same (uniform) result.
 struct BoxStore {
     int cnt;
     float bd, bx, by, bz;
@@ -203,105 +242,50 @@ struct BoxStore {
     bool tie, defer;
     int l[3], h[3];
 };
-__device__ __forceinline__ void box_store(const DynAddParams& P, unsigned long long key, const DBox& b, BoxStore& S) {
+__device__ __forceinline__ void store_merge(BoxStore& S, float d, uint32_t id, float x, float y, float z, bool tie) {
+    if (d < S.bd) {
+        S.bd = d; S.bid = id; S.bx = x; S.by = y; S.bz = z; S.tie = tie;
+    } else if (d == S.bd) {
+        S.tie = S.tie || tie || x != S.bx || y != S.by || z != S.bz;
+        if (id < S.bid) { S.bid = id; S.bx = x; S.by = y; S.bz = z; }
+    }
+}
+__device__ __forceinline__ void wave_box_store(const DynAddParams& P, unsigned long long key, const DBox& b, int lane,
+                                               WaveCells& W, BoxStore& S) {
     S.cnt = 0; S.bd = INFINITY; S.bx = S.by = S.bz = 0.f; S.bid = 0xFFFFFFFFu; S.tie = false;
     S.l[0] = S.l[1] = S.l[2] = 0; S.h[0] = S.h[1] = S.h[2] = -1;
     const unsigned long long nd = P.ctr[kDynDirty];
     bool defer = nd > (unsigned long long)P.dirty_cap;
-    for (unsigned long long d = 0; d < nd && d < (unsigned long long)P.dirty_cap && !defer; d++)
-        defer = P.dirty[d] == key;
+    if (!defer) {
+        bool hit = false;
+        for (unsigned long long d = lane; d < nd; d += 64) hit = hit || P.dirty[d] == key;
+        defer = __ballot(hit) != 0ull;
+    }
     if (!defer && !box_cells(P, b, S.l, S.h)) defer = true;
-    const float4* __restrict__ gp = reinterpret_cast<const float4*>(P.gpts);
-    for (int z = S.l[2]; z <= S.h[2] && !defer; z++)
-        for (int y = S.l[1]; y <= S.h[1] && !defer; y++)
-            for (int x = S.l[0]; x <= S.h[0] && !defer; x++) {
-                const uint2 r = cell_run(P.gslots, P.glog2, x, y, z);
-                for (uint32_t k = r.x; k < r.x + r.y; k++) {
-                    const float4 q = gp[k];
-                    if (!in_dbox(b, q.x, q.y, q.z)) continue;
-                    if (in_two(key, P.ds, q.x, q.y, q.z)) {
-                        defer = true;
-                        break;
-                    }
-                    S.cnt++;
-                    const float d = mid_dist(b, q.x, q.y, q.z);
-                    const uint32_t id = __float_as_uint(q.w);
-                    if (d < S.bd) {
-                        S.bd = d; S.bid = id; S.bx = q.x; S.by = q.y; S.bz = q.z;
-                        S.tie = false;
-                    } else if (d == S.bd) {
-                        if (q.x != S.bx || q.y != S.by || q.z != S.bz) S.tie = true;
-                        if (id < S.bid) { S.bid = id; S.bx = q.x; S.by = q.y; S.bz = q.z; }
-                    }
-                }
-            }
-    S.defer = defer;
-}
-// Delete_by_range of the box; a stored winner is deleted and added again (it stays).
-__device__ __forceinline__ unsigned long long box_delete(const DynAddParams& P, const DBox& b, const BoxStore& S,
-                                                         bool newer) {
-    unsigned long long deleted = 0;
-    if (!(S.cnt > 0 && (newer || S.cnt > 1))) return 0;
-    const float4* __restrict__ gp = reinterpret_cast<const float4*>(P.gpts);
-    for (int z = S.l[2]; z <= S.h[2]; z++)
-        for (int y = S.l[1]; y <= S.h[1]; y++)
-            for (int x = S.l[0]; x <= S.h[0]; x++) {
-                const uint2 r = cell_run(P.gslots, P.glog2, x, y, z);
-                for (uint32_t k = r.x; k < r.x + r.y; k++) {
-                    const float4 q = gp[k];
-                    if (!in_dbox(b, q.x, q.y, q.z)) continue;
-                    const uint32_t id = __float_as_uint(q.w);
-                    if (!newer && id == S.bid) continue;
-                    P.alive[id] = 0;
-                    deleted++;
-                }
-            }
-    return deleted;
-}
-constexpr uint32_t kBigRun = 96;  // boxes with more new points: one wave each (k_add_group_big)
-
-// One box per thread: its stored points, then its new points in input order.
-__global__ __launch_bounds__(256) void k_add_group(DynAddParams P) {
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= (int64_t)P.ctr[kDynRuns]) return;
-    const uint32_t s0 = P.starts[g], s1 = P.starts[g + 1];
-    if (s1 - s0 > kBigRun) return;
-    const unsigned long long key = P.skeys[s0];
-    const DBox b = dbox(key, P.ds);
-    BoxStore S;
-    box_store(P, key, b, S);
-    if (S.defer) {
-        for (uint32_t k = s0; k < s1; k++) P.defer[P.svals[k]] = 1u;
+    if (defer) {
+        S.defer = true;
         return;
     }
-    const float4* __restrict__ Ws = reinterpret_cast<const float4*>(P.Ws);
-    // the box's new points in input order (:390-437); after the first, the box holds one point
-    float4 p = Ws[s0];
-    uint32_t win = __float_as_uint(p.w);
-    float dc = mid_dist(b, p.x, p.y, p.z);
-    bool newer = !(S.cnt > 0 && S.bd < dc);
-    float wx = p.x, wy = p.y, wz = p.z;
-    if (!newer) { dc = S.bd; wx = S.bx; wy = S.by; wz = S.bz; }
-    unsigned long long events = 0, amb = 0;
-    if (S.cnt > 1 && !newer && S.tie) amb = 1;
-    if (S.cnt > 1 || newer || same_pt(p.x, p.y, p.z, wx, wy, wz)) events++;
-    for (uint32_t k = s0 + 1; k < s1; k++) {
-        p = Ws[k];
-        const uint32_t i = __float_as_uint(p.w);
-        const float d = mid_dist(b, p.x, p.y, p.z);
-        if (d <= dc) {  // the stored point replaces it only if strictly nearer
-            newer = true; win = i; dc = d; wx = p.x; wy = p.y; wz = p.z;
-            events++;
-        } else if (same_pt(p.x, p.y, p.z, wx, wy, wz)) {
-            events++;
-        }
+    bool two = false;
+    wave_box_points(P, S.l, S.h, lane, W, [&](const float4 q) {
+        if (!in_dbox(b, q.x, q.y, q.z)) return;
+        if (in_two(key, P.ds, q.x, q.y, q.z)) two = true;
+        S.cnt++;
+        store_merge(S, mid_dist(b, q.x, q.y, q.z), __float_as_uint(q.w), q.x, q.y, q.z, false);
+    });
+    S.defer = __ballot(two) != 0ull;
+    if (S.defer) return;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        S.cnt += __shfl_xor(S.cnt, off, 64);
+        const float d = __shfl_xor(S.bd, off, 64);
+        const uint32_t id = __shfl_xor(S.bid, off, 64);
+        const float x = __shfl_xor(S.bx, off, 64), y = __shfl_xor(S.by, off, 64), z = __shfl_xor(S.bz, off, 64);
+        const bool t = __shfl_xor((int)S.tie, off, 64) != 0;
+        store_merge(S, d, id, x, y, z, t);
     }
-    if (newer) P.keep[win] = 1u;
-    const unsigned long long deleted = box_delete(P, b, S, newer);
-    if (events) atomicAdd(P.ctr + kDynEvents, events);
-    if (deleted) atomicAdd(P.ctr + kDynDeleted, deleted);
-    if (amb) atomicAdd(P.ctr + kDynAmbig, amb);
 }
+constexpr int kBoxWaves = 4;  // k_add_box: waves per block
 
 // The running winner as a scan: (distance, position) with the smaller distance,
 // the later position on ties ("d <= dc" lets the later point win).
@@ -309,41 +293,39 @@ __device__ __forceinline__ void win_combine(float& d, int& k, float d2, int k2) 
     if (d2 < d || (d2 == d && k2 > k)) { d = d2; k = k2; }
 }
 
-// One wave per box with more than kBigRun new points (boxes near the sensor):
-// lane 0 takes the stored points, then the sequence of new points is a
-// prefix scan of the running winner, 64 points per step.
-__global__ __launch_bounds__(64) void k_add_group_big(DynAddParams P) {
-    const int lane = threadIdx.x;
+// One wave per box (Add_Points' loop body for the box's points, :390-437):
+// the stored points (wave_box_store), then the box's new points in input
+// order as a prefix scan of the running winner, 64 points per step (after the
+// first point the box holds one point), then Delete_by_range of the box with
+// the lanes over its stored points (a stored winner is deleted and added
+// again: it stays).
+__global__ __launch_bounds__(64 * kBoxWaves) void k_add_box(DynAddParams P) {
+    __shared__ WaveCells cells[kBoxWaves];
+    const int lane = threadIdx.x & 63;
+    WaveCells& W = cells[threadIdx.x >> 6];
+    if (P.ctr[kDynError]) return;  // k_add_prep refused the batch: nothing changes
     const int64_t runs = (int64_t)P.ctr[kDynRuns];
     const float4* __restrict__ Ws = reinterpret_cast<const float4*>(P.Ws);
-    for (int64_t g = blockIdx.x; g < runs; g += gridDim.x) {
+    for (int64_t g = (int64_t)blockIdx.x * kBoxWaves + (threadIdx.x >> 6); g < runs;
+         g += (int64_t)gridDim.x * kBoxWaves) {
         const uint32_t s0 = P.starts[g], s1 = P.starts[g + 1];
-        if (s1 - s0 <= kBigRun) continue;  // wave-uniform
         const unsigned long long key = P.skeys[s0];
         const DBox b = dbox(key, P.ds);
         BoxStore S;
-        if (lane == 0) box_store(P, key, b, S);
-        const int defer = __shfl(lane == 0 ? (int)S.defer : 0, 0, 64);
-        if (defer) {
+        wave_box_store(P, key, b, lane, W, S);
+        if (S.defer) {
             for (uint32_t k = s0 + lane; k < s1; k += 64) P.defer[P.svals[k]] = 1u;
             continue;
         }
-        // the first new point against the stored ones (lane 0), broadcast as the carry
-        float cd = 0.f;   // running winner: distance, position (-1: the stored point), coordinates
-        int ck = 0;
-        float cx = 0.f, cy = 0.f, cz = 0.f;
-        unsigned long long events = 0, amb = 0;
-        if (lane == 0) {
-            const float4 p = Ws[s0];
-            cd = mid_dist(b, p.x, p.y, p.z);
-            ck = (int)s0;
-            cx = p.x; cy = p.y; cz = p.z;
-            if (S.cnt > 0 && S.bd < cd) { cd = S.bd; ck = -1; cx = S.bx; cy = S.by; cz = S.bz; }
-            if (S.cnt > 1 && ck < 0 && S.tie) amb = 1;
-            if (S.cnt > 1 || ck >= 0 || same_pt(p.x, p.y, p.z, cx, cy, cz)) events = 1;
-        }
-        cd = __shfl(cd, 0, 64); ck = __shfl(ck, 0, 64);
-        cx = __shfl(cx, 0, 64); cy = __shfl(cy, 0, 64); cz = __shfl(cz, 0, 64);
+        // the first new point against the stored ones, the carry of the scan
+        const float4 p0 = Ws[s0];
+        float cd = mid_dist(b, p0.x, p0.y, p0.z);  // running winner: distance, position (-1: the stored point)
+        int ck = (int)s0;
+        float cx = p0.x, cy = p0.y, cz = p0.z;
+        if (S.cnt > 0 && S.bd < cd) { cd = S.bd; ck = -1; cx = S.bx; cy = S.by; cz = S.bz; }
+        const unsigned long long amb = (S.cnt > 1 && ck < 0 && S.tie) ? 1ull : 0ull;
+        unsigned long long events = 0;
+        if (lane == 0 && (S.cnt > 1 || ck >= 0 || same_pt(p0.x, p0.y, p0.z, cx, cy, cz))) events = 1;
         for (uint32_t k0 = s0 + 1; k0 < s1; k0 += 64) {
             const uint32_t k = k0 + lane;
             const bool valid = k < s1;
@@ -377,9 +359,7 @@ __global__ __launch_bounds__(64) void k_add_group_big(DynAddParams P) {
                 const float4 w = Ws[pkk];
                 qx = w.x; qy = w.y; qz = w.z;
             }
-            unsigned long long ev = 0;
-            if (valid) ev = (d <= pd || same_pt(p.x, p.y, p.z, qx, qy, qz)) ? 1ull : 0ull;
-            events += ev;
+            if (valid && (d <= pd || same_pt(p.x, p.y, p.z, qx, qy, qz))) events++;
             // new carry: the inclusive winner of the last valid lane against the carry
             const int last = (int)min<uint32_t>(63u, s1 - 1 - k0);
             const float ld = __shfl(sd, last, 64);
@@ -390,13 +370,24 @@ __global__ __launch_bounds__(64) void k_add_group_big(DynAddParams P) {
                 cx = w.x; cy = w.y; cz = w.z;
             }
         }
-        // wave sums
+        const bool newer = ck >= 0;
+        if (newer && lane == 0) P.keep[__float_as_uint(Ws[ck].w)] = 1u;
+        unsigned long long deleted = 0;
+        if (S.cnt > 0 && (newer || S.cnt > 1)) {
+            wave_box_points(P, S.l, S.h, lane, W, [&](const float4 q) {
+                if (!in_dbox(b, q.x, q.y, q.z)) return;
+                const uint32_t id = __float_as_uint(q.w);
+                if (!newer && id == S.bid) return;
+                P.alive[id] = 0;
+                deleted++;
+            });
+        }
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) events += __shfl_xor(events, off, 64);
+        for (int off = 32; off >= 1; off >>= 1) {
+            events += __shfl_xor(events, off, 64);
+            deleted += __shfl_xor(deleted, off, 64);
+        }
         if (lane == 0) {
-            const bool newer = ck >= 0;
-            if (newer) P.keep[__float_as_uint(Ws[ck].w)] = 1u;
-            const unsigned long long deleted = box_delete(P, b, S, newer);
             if (events) atomicAdd(P.ctr + kDynEvents, events);
             if (deleted) atomicAdd(P.ctr + kDynDeleted, deleted);
             if (amb) atomicAdd(P.ctr + kDynAmbig, amb);
@@ -413,7 +404,7 @@ __global__ void k_add_dlist(DynAddParams P) {
 
 // The deferred points in input order on one thread: exactly Add_Points' loop.
 __global__ void k_add_seq(DynAddParams P) {
-    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    if (blockIdx.x != 0 || threadIdx.x != 0 || P.ctr[kDynError]) return;
     const uint32_t D = (uint32_t)P.ctr[kDynDeferred];
     const float4* __restrict__ gp = reinterpret_cast<const float4*>(P.gpts);
     const float4* __restrict__ W = reinterpret_cast<const float4*>(P.W);
@@ -495,9 +486,12 @@ __global__ void k_add_seq(DynAddParams P) {
 }
 
 __global__ void k_add_append(const float4* __restrict__ W, const uint32_t* __restrict__ keep,
-                             const uint32_t* __restrict__ apos, int64_t n, int64_t base, float4* all, uint8_t* alive) {
+                             const uint32_t* __restrict__ apos, int64_t n, int64_t base, float4* all, uint8_t* alive,
+                             unsigned long long* ctr) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || !keep[i]) return;
+    if (i >= n || ctr[kDynError]) return;  // a refused batch changes nothing
+    if (i == n - 1) ctr[kDynAdded] = (unsigned long long)apos[i] + keep[i];
+    if (!keep[i]) return;
     const float4 p = W[i];
     const uint32_t id = (uint32_t)(base + (int64_t)apos[i]);
     all[id] = make_float4(p.x, p.y, p.z, __uint_as_float(id));
@@ -804,11 +798,9 @@ int launch_add_heads(const DynAddParams& p, void* stream) { DYN_LAUNCH(k_add_hea
 int launch_add_starts(const DynAddParams& p, void* stream) { DYN_LAUNCH(k_add_starts, p.n, p); }
 int launch_add_group(const DynAddParams& p, void* stream) {
     if (p.n <= 0) return LIVO_OK;
-    hipLaunchKernelGGL(k_add_group, grid_for(p.n), dim3(256), 0, (hipStream_t)stream, p);
-    if (hipGetLastError() != hipSuccess) return LIVO_E_HIP;
-    const int64_t w = p.n / (kBigRun + 1) + 1;
-    const unsigned waves = (unsigned)(w < 4096 ? w : 4096);
-    hipLaunchKernelGGL(k_add_group_big, dim3(waves), dim3(64), 0, (hipStream_t)stream, p);
+    const int64_t blocks = (p.n + kBoxWaves - 1) / kBoxWaves;  // runs <= n: a wave per box, at most 16k waves
+    hipLaunchKernelGGL(k_add_box, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(64 * kBoxWaves), 0,
+                       (hipStream_t)stream, p);
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 int launch_add_dlist(const DynAddParams& p, void* stream) { DYN_LAUNCH(k_add_dlist, p.n, p); }
@@ -817,9 +809,9 @@ int launch_add_seq(const DynAddParams& p, void* stream) {
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 int launch_add_append(const float* W, const uint32_t* keep, const uint32_t* apos, int64_t n, int64_t base, float* all,
-                      uint8_t* alive, void* stream) {
+                      uint8_t* alive, unsigned long long* ctr, void* stream) {
     DYN_LAUNCH(k_add_append, n, reinterpret_cast<const float4*>(W), keep, apos, n, base, reinterpret_cast<float4*>(all),
-               alive);
+               alive, ctr);
 }
 int launch_dyn_seed(const float* gpts, int64_t M, float* all, uint8_t* alive, void* stream) {
     DYN_LAUNCH(k_dyn_seed, M, reinterpret_cast<const float4*>(gpts), M, reinterpret_cast<float4*>(all), alive);

@@ -1430,12 +1430,11 @@ static int dyn_add(livo_ctx* c, int64_t n, float ds, bool downsample, livo_map_a
         P.heads = d.heads; P.runid = d.runid; P.starts = d.starts;
         P.defer = d.defer; P.dpos = d.dpos; P.dlist = d.dlist; P.keep = d.keep; P.seq = d.seq;
         P.dirty = d.dirty; P.dirty_cap = kDynDirtyCap; P.ctr = d.ctr;
+        // k_add_prep refuses an out-of-range batch (ctr[kDynError] bit 0): the
+        // passes that change the map (k_add_box, k_add_seq, k_add_append) then
+        // do nothing, so the one read-back at the end decides
         rc = launch_add_prep(P, c->stream);
         if (rc) return rc;
-        unsigned long long h[kDynCtrN];
-        HIP_TRY(hipMemcpyAsync(h, d.ctr, sizeof(h), hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        if (h[kDynError]) return LIVO_E_RANGE;  // nothing changed
         if (downsample) {
             rc = sort_u64(c, d.keys, d.skeys, d.iota, d.svals, n);
             if (!rc) rc = launch_add_heads(P, c->stream);
@@ -1447,18 +1446,16 @@ static int dyn_add(livo_ctx* c, int64_t n, float ds, bool downsample, livo_map_a
             if (!rc) rc = launch_add_seq(P, c->stream);
         }
         if (!rc) rc = ivox_scan(c, d.keep, d.apos, n);
+        if (!rc) rc = launch_add_append(d.W, d.keep, d.apos, n, d.n_ids, d.all, d.alive, d.ctr, c->stream);
         if (rc) return rc;
-        uint32_t tail[2];
-        HIP_TRY(hipMemcpyAsync(&tail[0], d.apos + n - 1, 4, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipMemcpyAsync(&tail[1], d.keep + n - 1, 4, hipMemcpyDeviceToHost, c->stream));
+        unsigned long long h[kDynCtrN];
         HIP_TRY(hipMemcpyAsync(h, d.ctr, sizeof(h), hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
+        if (h[kDynError] & 1ull) return LIVO_E_RANGE;  // nothing changed
         // k_add_prep checked the range of every box the later passes read, so
         // the group / sequential passes cannot fail once the map is modified
         if (h[kDynError]) return LIVO_E_HIP;
-        const int64_t added = (int64_t)tail[0] + tail[1];
-        rc = launch_add_append(d.W, d.keep, d.apos, n, d.n_ids, d.all, d.alive, c->stream);
-        if (rc) return rc;
+        const int64_t added = (int64_t)h[kDynAdded];
         st.events = (int64_t)h[kDynEvents];
         st.deleted = (int64_t)h[kDynDeleted];
         st.ambiguous = (int64_t)h[kDynAmbig];

@@ -577,7 +577,7 @@ int launch_vio_end(const VioParams& p, void* stream);
 // KD_TREE::Add_Points / Delete_Point_Boxes on the map's point set, then the
 // cell grid rebuilt from the surviving points.  Counters in DynAddParams::ctr:
 enum { kDynEvents = 0, kDynDeleted = 1, kDynAmbig = 2, kDynDeferred = 3, kDynError = 4, kDynDirty = 5,
-       kDynAbsMax = 6, kDynRuns = 7, kDynTomb = 8, kDynAliveCnt = 9, kDynCtrN = 10 };
+       kDynAbsMax = 6, kDynRuns = 7, kDynTomb = 8, kDynAliveCnt = 9, kDynAdded = 10, kDynCtrN = 11 };
 constexpr uint32_t kDynDirtyCap = 4096;  // dirty boxes listed; beyond, every point takes the sequential pass
 struct DynAddParams {
     const float* W;             // n points to add (x, y, z, -), PointToAdd order
@@ -624,7 +624,7 @@ int launch_add_group(const DynAddParams& p, void* stream);
 int launch_add_dlist(const DynAddParams& p, void* stream);
 int launch_add_seq(const DynAddParams& p, void* stream);
 int launch_add_append(const float* W, const uint32_t* keep, const uint32_t* apos, int64_t n, int64_t base, float* all,
-                      uint8_t* alive, void* stream);
+                      uint8_t* alive, unsigned long long* ctr, void* stream);
 int launch_dyn_seed(const float* gpts, int64_t M, float* all, uint8_t* alive, void* stream);
 int launch_dyn_world(const DynWorldParams& p, void* stream);
 int launch_dyn_cellkeys(const float* all, const uint8_t* alive, int64_t n_ids, const float* org, float inv,
