@@ -517,7 +517,20 @@ __global__ void k_dyn_world(DynWorldParams P) {
     reinterpret_cast<float4*>(P.W)[P.perm[k]] = make_float4(wx, wy, wz, 0.f);
 }
 
-// Cell key of every alive point (k_knn_grid's cell_of: floor((p - org) * inv) in float).
+// Cell key of a point (k_knn_grid's cell_of: floor((p - org) * inv) in float);
+// `bad` if outside the grid's key range (clamped).
+__device__ __forceinline__ unsigned long long cell_key_of(const float4 p, float ox, float oy, float oz, float inv,
+                                                          bool& bad) {
+    const float lim = (float)(kGridBias - 8);
+    float c[3] = {floorf((p.x - ox) * inv), floorf((p.y - oy) * inv), floorf((p.z - oz) * inv)};
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        if (!(fabsf(c[a]) < lim)) bad = true;
+        c[a] = fminf(fmaxf(c[a], -lim), lim);
+    }
+    return pack_key((int)c[0], (int)c[1], (int)c[2]);
+}
+// Cell key of every alive point.
 __global__ void k_dyn_cellkeys(const float4* __restrict__ all, const uint8_t* __restrict__ alive, int64_t n_ids,
                                float ox, float oy, float oz, float inv, unsigned long long* keys, uint32_t* vals,
                                unsigned long long* ctr) {
@@ -528,15 +541,65 @@ __global__ void k_dyn_cellkeys(const float4* __restrict__ all, const uint8_t* __
         keys[id] = ~0ull;
         return;
     }
-    const float4 p = all[id];
-    const float lim = (float)(kGridBias - 8);
-    float c[3] = {floorf((p.x - ox) * inv), floorf((p.y - oy) * inv), floorf((p.z - oz) * inv)};
-#pragma unroll
-    for (int a = 0; a < 3; a++) {
-        if (!(fabsf(c[a]) < lim)) atomicOr(ctr + kDynError, 4ull);
-        c[a] = fminf(fmaxf(c[a], -lim), lim);
+    bool bad = false;
+    keys[id] = cell_key_of(all[id], ox, oy, oz, inv, bad);
+    if (bad) atomicOr(ctr + kDynError, 4ull);
+}
+
+// ---- the grid merged instead of re-sorted (dyn_rebuild's incremental path) ----
+// flags[i] = the old grid's point i is still alive (i < na_old), flags[na_old] = 0.
+__global__ void k_dyn_flags(const float4* __restrict__ gpts, int64_t na_old, const uint8_t* __restrict__ alive,
+                            uint32_t* flags) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > na_old) return;
+    flags[i] = i < na_old ? (uint32_t)alive[__float_as_uint(gpts[i].w)] : 0u;
+}
+// The merged grid in (cell key, id) order: the old grid's survivors keep their
+// order and go before the new points of the same cell (their ids are smaller);
+// the new points come sorted by (key, id).  A survivor's position = survivors
+// before it + new keys below its key; a new point's = new points before it +
+// survivors with key <= its key (a binary search of the old grid, keys from the
+// points as k_dyn_cellkeys computes them).
+__global__ void k_dyn_merge(DynMergeParams P) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    float4* out = reinterpret_cast<float4*>(P.out);
+    const float4* __restrict__ gp = reinterpret_cast<const float4*>(P.gpts);
+    bool bad = false;
+    if (t < P.na_old) {
+        const float4 q = gp[t];
+        if (!P.alive[__float_as_uint(q.w)]) return;
+        const unsigned long long key = cell_key_of(q, P.org[0], P.org[1], P.org[2], P.inv, bad);
+        int64_t lo = 0, hi = P.m;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (P.nkeys[mid] < key) lo = mid + 1; else hi = mid;
+        }
+        const int64_t pos = (int64_t)P.rank[t] + lo;
+        if (pos >= P.na) {
+            atomicOr(P.ctr + kDynError, 16ull);
+            return;
+        }
+        out[pos] = q;
+        P.okeys[pos] = key;
+    } else if (t < P.na_old + P.m) {
+        const int64_t j = t - P.na_old;
+        const unsigned long long key = P.nkeys[j];
+        if (key == ~0ull) return;  // (a dead new id sorts last)
+        int64_t lo = 0, hi = P.na_old;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (cell_key_of(gp[mid], P.org[0], P.org[1], P.org[2], P.inv, bad) <= key) lo = mid + 1; else hi = mid;
+        }
+        const int64_t pos = j + (int64_t)P.rank[lo];
+        if (pos >= P.na) {
+            atomicOr(P.ctr + kDynError, 16ull);
+            return;
+        }
+        out[pos] = reinterpret_cast<const float4*>(P.all)[P.g0 + P.nidx[j]];
+        P.okeys[pos] = key;
+    } else if (t < P.na_old + P.m + 3) {  // chunk padding of k_knn_grid
+        out[P.na + (t - P.na_old - P.m)] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    keys[id] = pack_key((int)c[0], (int)c[1], (int)c[2]);
 }
 
 __global__ void k_dyn_gather(const unsigned long long* __restrict__ skeys, const uint32_t* __restrict__ sids,
@@ -563,9 +626,20 @@ __global__ void k_dyn_runs(const uint32_t* __restrict__ heads, const uint32_t* _
     }
 }
 
+// `dcells` (optional): the count on the device, `cells` then the bound the table
+// was sized for (a count above it inserts nothing and sets ctr bit 8).
 __global__ void k_dyn_slots(const unsigned long long* __restrict__ skeys, const uint32_t* __restrict__ starts,
-                            int64_t cells, GridSlot* slots, int log2) {
+                            int64_t cells, GridSlot* slots, int log2, const unsigned long long* dcells,
+                            unsigned long long* err) {
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (dcells) {
+        const int64_t nc = (int64_t)*dcells;
+        if (nc > cells) {
+            if (g == 0) atomicOr(err, 8ull);
+            return;
+        }
+        cells = nc;
+    }
     if (g >= cells) return;
     const uint32_t s0 = starts[g], s1 = starts[g + 1];
     const unsigned long long key = skeys[s0];
@@ -832,9 +906,13 @@ int launch_dyn_runs(const uint32_t* heads, const uint32_t* runid, int64_t na, ui
     DYN_LAUNCH(k_dyn_runs, na, heads, runid, na, starts, nruns);
 }
 int launch_dyn_slots(const unsigned long long* skeys, const uint32_t* starts, int64_t cells, GridSlot* slots, int log2,
-                     void* stream) {
-    DYN_LAUNCH(k_dyn_slots, cells, skeys, starts, cells, slots, log2);
+                     void* stream, const unsigned long long* dcells, unsigned long long* err) {
+    DYN_LAUNCH(k_dyn_slots, cells, skeys, starts, cells, slots, log2, dcells, err);
 }
+int launch_dyn_flags(const float* gpts, int64_t na_old, const uint8_t* alive, uint32_t* flags, void* stream) {
+    DYN_LAUNCH(k_dyn_flags, na_old + 1, reinterpret_cast<const float4*>(gpts), na_old, alive, flags);
+}
+int launch_dyn_merge(const DynMergeParams& p, void* stream) { DYN_LAUNCH(k_dyn_merge, p.na_old + p.m + 3, p); }
 int launch_cr_rho(const float* gpts, int64_t n, const float org[3], float h, uint32_t* rho_bits, uint32_t* iota,
                   void* stream) {
     const CrGeo G{{org[0], org[1], org[2]}, h, 1.0f / h};

@@ -149,6 +149,15 @@ struct DynDev {
     float max_gh = 0.f;
     float box_cell = 1.2f;           // LIVO_DYN_BOX_CELL
     float box_cell_max = 2.0f;       // LIVO_DYN_BOX_CELL_MAX (0: no upper bound)
+    // The grid rebuild merges instead of re-sorting (dyn_rebuild_merge): the
+    // grid holds every alive id below grid_ids in (key, id) order on cells of
+    // edge grid_gh (-1: unknown, the next rebuild sorts), `cells` of them.
+    float* gpts_alt = nullptr;       // the merge's output, swapped with ctx->gpts
+    int64_t gpts_alt_cap = 0;
+    int64_t grid_ids = -1, cells = -1;
+    float grid_gh = 0.f;
+    bool merge = true;               // LIVO_DYN_MERGE=0: always sort
+    int64_t rebuilds_sorted = 0, rebuilds_merged = 0;
 };
 
 // One batch's staging and streams.  LaserMapping batches: slots packed at
@@ -1085,7 +1094,7 @@ static void dyn_free(DynDev& d) {
     dev_free(d.defer); dev_free(d.dpos); dev_free(d.dlist); dev_free(d.keep); dev_free(d.apos);
     dev_free(d.boxes); dev_free(d.dirty); dev_free(d.ctr);
     dev_free(d.rpts); dev_free(d.rpos); dev_free(d.dslots); dev_free(d.dpts);
-    dev_free(d.dvslots); dev_free(d.dvidx);
+    dev_free(d.dvslots); dev_free(d.dvidx); dev_free(d.gpts_alt);
     d = DynDev{};
 }
 
@@ -1317,6 +1326,8 @@ static int dyn_activate(livo_ctx* c) {
     d.active = true;
     d.runs = false;
     d.d_n = 0;
+    d.grid_ids = -1;  // (the build's grid: the first rebuild sorts)
+    if (const char* env = std::getenv("LIVO_DYN_MERGE")) d.merge = std::atoi(env) != 0;
     if (const char* env = std::getenv("LIVO_DYN_BOX_CELL_MAX")) {  // tuning knob (0: off)
         const double v = std::atof(env);
         if (v >= 0.0 && v < 100.0) d.box_cell_max = (float)v;
@@ -1345,6 +1356,9 @@ static int dyn_activate(livo_ctx* c) {
     return LIVO_OK;
 }
 
+constexpr int kMergeRetry = -1000;  // dyn_rebuild_merge: the counts disagree, sort instead
+static int dyn_rebuild_merge(livo_ctx* c);
+
 // The cell grid of k_knn_grid rebuilt from the alive points (same layout as
 // build_grid_map: cells in key order, a cell's points in id order).
 static int dyn_rebuild(livo_ctx* c) {
@@ -1353,6 +1367,11 @@ static int dyn_rebuild(livo_ctx* c) {
         const float lo = (float)(2.0 * (double)d.cmax / (double)(kGridBias - 2));
         const float h = c->gh < d.min_gh ? d.min_gh : std::max(d.max_gh, d.min_gh);
         c->gh = std::max(h, lo * 1.01f);
+    }
+    if (d.merge && d.grid_ids >= 0 && d.cells >= 0 && d.grid_gh == c->gh && d.grid_ids <= d.n_ids) {
+        const int rc = dyn_rebuild_merge(c);
+        if (rc != kMergeRetry) return rc;
+        (void)hipGetLastError();  // (the merge found an inconsistency: sort instead)
     }
     int rc = dyn_sort_scratch(c, std::max<int64_t>(d.n_ids, 1));
     if (rc) return rc;
@@ -1394,6 +1413,82 @@ static int dyn_rebuild(livo_ctx* c) {
     c->geps = (float)(32.0 * std::ldexp(1.0, -24) * (double)d.cmax + 1e-7);
     c->grid_bytes = table * (int64_t)sizeof(GridSlot) + d.gpts_cap * 16;
     for (auto& s : c->scans) s.searched = false;  // cached neighbours refer to the old map
+    d.grid_ids = d.n_ids;
+    d.grid_gh = c->gh;
+    d.cells = cells;
+    d.rebuilds_sorted++;
+    return dyn_runs_update(c);
+}
+
+// The grid after a change without sorting the map again: the ids added since
+// the last rebuild (a few hundred per scan) are keyed and sorted, the old
+// grid's survivors are ranked by a scan, and k_dyn_merge places both (the
+// same (key, id) order a sort gives, so the same grid bit for bit).  The hash
+// table is sized for the old cell count + the new points (a bound: each new
+// point opens at most one cell), so nothing is read back before it is filled;
+// one read-back at the end.  kMergeRetry: inconsistent counts (the caller
+// sorts instead).
+static int dyn_rebuild_merge(livo_ctx* c) {
+    DynDev& d = c->dyn;
+    const int64_t na_old = c->map_points, na = d.n_alive, g0 = d.grid_ids, m = d.n_ids - g0;
+    int rc = dyn_sort_scratch(c, std::max<int64_t>(std::max<int64_t>(na_old, na), m) + 1);
+    if (rc) return rc;
+    if (d.gpts_alt_cap < na + 3) {
+        const int64_t cap = (na + 3) + ((na + 3) >> 2);
+        dev_free(d.gpts_alt);
+        d.gpts_alt_cap = 0;
+        if (dev_alloc(&d.gpts_alt, (size_t)cap * 4)) return LIVO_E_OOM;
+        d.gpts_alt_cap = cap;
+    }
+    const float inv = 1.0f / c->gh;
+    HIP_TRY(hipMemsetAsync(d.ctr, 0, kDynCtrN * sizeof(unsigned long long), c->stream));
+    if (m > 0) {
+        rc = launch_dyn_cellkeys(d.all + 4 * g0, d.alive + g0, m, c->gorg, inv, d.keys, d.iota, d.ctr, c->stream);
+        if (!rc) rc = sort_u64(c, d.keys, d.skeys, d.iota, d.svals, m);
+    }
+    if (!rc) rc = launch_dyn_flags(c->gpts, na_old, d.alive, d.heads, c->stream);
+    if (!rc) rc = ivox_scan(c, d.heads, d.runid, na_old + 1);
+    if (rc) return rc;
+    DynMergeParams P{};
+    P.gpts = c->gpts; P.na_old = na_old; P.rank = d.runid; P.alive = d.alive;
+    P.nkeys = d.skeys; P.nidx = d.svals; P.m = m; P.g0 = g0; P.all = d.all;
+    P.out = d.gpts_alt; P.okeys = d.keys; P.na = na;
+    std::memcpy(P.org, c->gorg, sizeof(P.org));
+    P.inv = inv; P.ctr = d.ctr;
+    rc = launch_dyn_merge(P, c->stream);
+    if (!rc && na > 0) rc = launch_run_heads(d.keys, na, d.heads, c->stream);
+    if (!rc && na > 0) rc = ivox_scan(c, d.heads, d.runid, na);
+    if (!rc && na > 0) rc = launch_dyn_runs(d.heads, d.runid, na, d.starts, d.ctr + kDynRuns, c->stream);
+    if (rc) return rc;
+    const int64_t bound = std::max<int64_t>(std::min<int64_t>(na, d.cells + m), 1);
+    int log2 = 4;
+    while (((int64_t)1 << log2) < 4 * bound) log2++;  // load factor <= 1/4, as build_grid_map
+    const int64_t table = (int64_t)1 << log2;
+    if (d.gslot_cap < table) {
+        dev_free(c->gslots);
+        d.gslot_cap = 0;
+        if (dev_alloc(&c->gslots, (size_t)table)) return LIVO_E_OOM;
+        d.gslot_cap = table;
+    }
+    rc = launch_ivox_clear(c->gslots, table, c->stream);
+    if (!rc && na > 0) rc = launch_dyn_slots(d.keys, d.starts, bound, c->gslots, log2, c->stream, d.ctr + kDynRuns,
+                                             d.ctr + kDynError);
+    if (rc) return rc;
+    unsigned long long h[kDynCtrN];
+    HIP_TRY(hipMemcpyAsync(h, d.ctr, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (h[kDynError] & (8ull | 16ull)) return kMergeRetry;  // (c->gpts untouched: the sort rebuilds from it)
+    if (h[kDynError]) return LIVO_E_RANGE;
+    std::swap(c->gpts, d.gpts_alt);
+    std::swap(d.gpts_cap, d.gpts_alt_cap);
+    c->glog2 = log2;
+    c->map_points = na;
+    c->geps = (float)(32.0 * std::ldexp(1.0, -24) * (double)d.cmax + 1e-7);
+    c->grid_bytes = table * (int64_t)sizeof(GridSlot) + d.gpts_cap * 16;
+    for (auto& s : c->scans) s.searched = false;  // cached neighbours refer to the old map
+    d.grid_ids = d.n_ids;
+    d.cells = (int64_t)h[kDynRuns];
+    d.rebuilds_merged++;
     return dyn_runs_update(c);
 }
 
@@ -4251,3 +4346,10 @@ int livo_sync(livo_ctx* c) {
 }
 
 }  // extern "C"
+
+extern "C" int livo_debug_map_rebuilds(livo_ctx* c, int64_t out[2]) {
+    if (!c || !out) return LIVO_E_INVALID;
+    out[0] = c->dyn.rebuilds_sorted;
+    out[1] = c->dyn.rebuilds_merged;
+    return LIVO_OK;
+}

@@ -633,8 +633,28 @@ int launch_dyn_gather(const unsigned long long* skeys, const uint32_t* sids, int
                       uint32_t* heads, void* stream);
 int launch_dyn_runs(const uint32_t* heads, const uint32_t* runid, int64_t na, uint32_t* starts,
                     unsigned long long* nruns, void* stream);
+// dcells (optional): the cell count on the device, `cells` the bound the table was sized for
 int launch_dyn_slots(const unsigned long long* skeys, const uint32_t* starts, int64_t cells, GridSlot* slots, int log2,
-                     void* stream);
+                     void* stream, const unsigned long long* dcells = nullptr, unsigned long long* err = nullptr);
+// The incremental path of the grid rebuild (k_dyn_merge, ikd_incr_kernels.hip).
+struct DynMergeParams {
+    const float* gpts;                 // the old grid, na_old points (x, y, z, id bits) in (key, id) order
+    int64_t na_old;
+    const uint32_t* rank;              // na_old + 1: exclusive scan of its survivors
+    const uint8_t* alive;
+    const unsigned long long* nkeys;   // m: the new ids' cell keys, sorted (dead: ~0)
+    const uint32_t* nidx;              // m: their index from g0
+    int64_t m, g0;
+    const float* all;
+    float* out;                        // na + 3: the merged grid
+    unsigned long long* okeys;         // na: its cell keys
+    int64_t na;
+    float org[3];
+    float inv;
+    unsigned long long* ctr;
+};
+int launch_dyn_flags(const float* gpts, int64_t na_old, const uint8_t* alive, uint32_t* flags, void* stream);
+int launch_dyn_merge(const DynMergeParams& p, void* stream);
 int launch_dyn_delete_boxes(const float* all, uint8_t* alive, int64_t n_ids, const float* boxes, int64_t nb,
                             unsigned long long* cnt, void* stream);
 

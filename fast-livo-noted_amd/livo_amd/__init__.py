@@ -169,6 +169,7 @@ SIGNATURES = {
     "livo_scan_upload": (C.c_int, [_P, _P, C.c_int64, C.c_int64, C.POINTER(C.c_int32)]),
     "livo_scan_upload_async": (C.c_int, [_P, _P, C.c_int64, C.c_int64, C.POINTER(C.c_int32)]),
     "livo_debug_ns_timeouts": (C.c_int, [C.POINTER(C.c_ulonglong)]),
+    "livo_debug_map_rebuilds": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64)]),
     "livo_scan_upload_batch_async": (C.c_int, [_P, _P, _P, C.c_int32, C.c_int64, _P]),
     "livo_host_register": (C.c_int, [_P, _P, C.c_size_t]),
     "livo_host_unregister": (C.c_int, [_P, _P]),
@@ -328,6 +329,12 @@ class Context:
         xyz = np.ascontiguousarray(xyz, np.float32)
         assert xyz.ndim == 2 and xyz.shape[1] >= 3
         _check("livo_map_build", self._L.livo_map_build(self.h, _ptr(xyz), xyz.shape[0], xyz.shape[1] * 4))
+
+    def map_rebuilds(self) -> tuple:
+        """(grid rebuilds by sorting every id, by merging the added ids) of the incremental map."""
+        out = (C.c_int64 * 2)()
+        _check("livo_debug_map_rebuilds", self._L.livo_debug_map_rebuilds(self.h, out))
+        return int(out[0]), int(out[1])
 
     def map_info(self) -> dict:
         mi = MapInfo()

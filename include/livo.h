@@ -504,6 +504,9 @@ int livo_sync(livo_ctx* ctx);
 /* Diagnostics: the persistent evaluation loop's bounded spins that gave up
  * (LIVO_PERSIST=1; device-wide since the library loaded; 0 on a healthy run). */
 int livo_debug_ns_timeouts(unsigned long long* out);
+/* Diagnostics: the incremental map's grid rebuilds since the context was made,
+ * out[0] by a sort of every id, out[1] by merging the added ids into the grid. */
+int livo_debug_map_rebuilds(livo_ctx* ctx, int64_t out[2]);
 
 #ifdef __cplusplus
 }

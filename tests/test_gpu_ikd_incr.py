@@ -253,3 +253,50 @@ def test_odometry_with_rebases(built, monkeypatch):
                       dm.map_incremental(body, gs, t_LI=synth.T_LI, filter_size_map=0.3))
             _same_map(ctx, dm)
             ctx.scan_release(sid)
+
+
+def test_grid_merge_equals_sort(built, monkeypatch):
+    """The grid rebuild after a change merges the added ids into the old grid
+    (dyn_rebuild_merge) instead of sorting every id: over adds, a no-downsample
+    add, box deletions and map_incremental, the map, its k-NN and the IEKF's
+    neighbour records equal those with LIVO_DYN_MERGE=0 (a sort at every
+    change) bit for bit, and the merge path ran."""
+    import livo_amd
+    from livo_amd import synth
+    m = synth.make_map(100_000)
+    rng = np.random.default_rng(12)
+    q = rng.uniform([-32, -22, -2], [32, 22, 3], (4000, 3)).astype(f32)
+    out = {}
+    for merge in ("1", "0"):
+        monkeypatch.setenv("LIVO_DYN_MERGE", merge)
+        rec = []
+        with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=0) as ctx:
+            ctx.map_build(m)
+            for k in range(5):
+                body, _, _ = synth.make_scan(20_000, 70 + k)
+                st = synth.make_state(70 + k)
+                if k == 3:
+                    sid = ctx.scan_upload(body)
+                    rec.append(ctx.map_incremental(sid, st, filter_size_map=0.5)[1])
+                    ctx.scan_release(sid)
+                else:
+                    rec.append(ctx.map_add_points(_world(body, st), 0.5, downsample=k != 2))
+                if k == 1:
+                    boxes = np.array([[-5, -5, -2, 0, 0, 3], [10, 10, -2, 12, 12, 3]], f32)
+                    rec.append(ctx.map_delete_boxes(boxes))
+                rec.append(ctx.map_dump())
+                rec.append(ctx.knn(q))
+                sid = ctx.scan_upload(synth.make_scan(15_000, 80 + k)[0])
+                ctx.iekf_update(sid, synth.make_state(80 + k))
+                rec.append(ctx.scan_neighbors(sid))
+                ctx.scan_release(sid)
+            out[merge] = (rec, ctx.map_rebuilds())
+    (a, ra), (b, rb) = out["1"], out["0"]
+    assert ra[1] >= 4 and rb[1] == 0, (ra, rb)
+    assert len(a) == len(b)
+    for x, y in zip(a, b):
+        if isinstance(x, tuple):
+            for u, v in zip(x, y):
+                assert np.array_equal(np.asarray(u).view(np.uint8), np.asarray(v).view(np.uint8))
+        else:
+            assert x == y
