@@ -15,7 +15,7 @@
 //                 face (neighbouring float boxes overlap or leave a gap) marks
 //                 the boxes it touches dirty
 //   (stable radix sort by box key: a box's points in input order)
-//   k_add_box     one wave per box: its stored points from the cell grid,
+//   k_add_box     a group of lanes per box: its stored points from the cell grid,
 //                 then the box's whole sequence of new points.  Boxes are
 //                 independent, except dirty boxes and boxes holding a stored
 //                 point that lies in two boxes: those are deferred
@@ -112,21 +112,58 @@ __device__ __forceinline__ bool box_cells(const DynAddParams& P, const DBox& b, 
 }
 
 // ------------------------------------------------------------ Add_Points ----
+__device__ __forceinline__ uint32_t dirty_slot(unsigned long long key, uint32_t cap) {
+    return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 40) & (cap - 1u);
+}
+// Box `key` into the dirty set (count in ctr[kDynDirty]; a full probe marks overflow).
+__device__ __forceinline__ void dirty_insert(const DynAddParams& P, unsigned long long key) {
+    uint32_t sl = dirty_slot(key, P.dirty_cap);
+    for (uint32_t probe = 0; probe < P.dirty_cap; probe++) {
+        const unsigned long long prev = atomicCAS(P.dirty + sl, 0ull, key);
+        if (prev == 0ull) {
+            atomicAdd(P.ctr + kDynDirty, 1ull);
+            return;
+        }
+        if (prev == key) return;
+        sl = (sl + 1u) & (P.dirty_cap - 1u);
+    }
+    atomicAdd(P.ctr + kDynDirty, (unsigned long long)P.dirty_cap);
+}
+// Whether box `key` is dirty (every box is, once the set is past half full).
+__device__ __forceinline__ bool dirty_has(const DynAddParams& P, unsigned long long key) {
+    if (P.ctr[kDynDirty] > (unsigned long long)(P.dirty_cap / 2)) return true;
+    uint32_t sl = dirty_slot(key, P.dirty_cap);
+    for (uint32_t probe = 0; probe < P.dirty_cap; probe++) {
+        const unsigned long long v = P.dirty[sl];
+        if (v == key) return true;
+        if (v == 0ull) return false;
+        sl = (sl + 1u) & (P.dirty_cap - 1u);
+    }
+    return true;
+}
+
 __global__ void k_add_prep(DynAddParams P) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P.n) return;
-    const float4 p = reinterpret_cast<const float4*>(P.W)[i];
+    float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < P.n) p = reinterpret_cast<const float4*>(P.W)[i];
     const float v[3] = {p.x, p.y, p.z};
     const float am = fmaxf(fmaxf(fabsf(p.x), fabsf(p.y)), fabsf(p.z));
     bool ok = am <= 1e30f;  // false for NaN / inf
     // the point's cell of the map grid must be addressable (k_knn_grid's key range)
 #pragma unroll
     for (int a = 0; a < 3; a++) ok = ok && fabsf(floorf((v[a] - P.gorg[a]) * P.ginv)) < (float)(kGridBias - 8);
+    {  // the batch's largest |coordinate|: one atomic per wave
+        uint32_t m = (i < P.n && ok) ? __float_as_uint(am) : 0u;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
+        if ((threadIdx.x & 63) == 0 && m) atomicMax(P.ctr + kDynAbsMax, (unsigned long long)m);
+    }
+    if (i >= P.n) return;
     P.iota[i] = (uint32_t)i;
     P.keep[i] = P.downsample ? 0u : 1u;  // without downsampling every point is added (:438-454)
     P.defer[i] = 0u;
-    if (ok) atomicMax(P.ctr + kDynAbsMax, (unsigned long long)__float_as_uint(am));
     P.keys[i] = 0ull;
+    if (P.keys32) P.keys32[i] = 0u;
     if (!P.downsample) {
         if (!ok) atomicOr(P.ctr + kDynError, 1ull);
         return;
@@ -158,34 +195,54 @@ __global__ void k_add_prep(DynAddParams P) {
         }
     }
     P.keys[i] = k;
+    if (P.keys32) P.keys32[i] = (uint32_t)(j[0] & 1023) | ((uint32_t)(j[1] & 1023) << 10) | ((uint32_t)(j[2] & 1023) << 20);
     if (clean) return;
     // processed in box k, lying inside the boxes of `mem`: all of them go to the sequential pass
-    auto mark = [&](unsigned long long key) {
-        const unsigned long long s = atomicAdd(P.ctr + kDynDirty, 1ull);
-        if (s < (unsigned long long)P.dirty_cap) P.dirty[s] = key;
-    };
-    mark(k);
+    dirty_insert(P, k);
     for (int o0 = 0; o0 < 3; o0++)
         for (int o1 = 0; o1 < 3; o1++)
             for (int o2 = 0; o2 < 3; o2++)
                 if (mem[0][o0] && mem[1][o1] && mem[2][o2] && !(o0 == 1 && o1 == 1 && o2 == 1))
-                    mark(pack_key(j[0] + o0 - 1, j[1] + o1 - 1, j[2] + o2 - 1));
+                    dirty_insert(P, pack_key(j[0] + o0 - 1, j[1] + o1 - 1, j[2] + o2 - 1));
 }
 
+// Runs of equal box keys in sorted order.  With the wrapped 30-bit keys two
+// boxes 1024 boxes apart on every axis they differ on would share a run: such a
+// pair is adjacent somewhere in the run, is found here, and the batch is redone
+// with the 64-bit keys (ctr bit 32; the passes that change the map skip it).
 __global__ void k_add_heads(DynAddParams P) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= P.n) return;
-    P.heads[k] = (k == 0 || P.skeys[k] != P.skeys[k - 1]) ? 1u : 0u;
-    // the points in box order: k_add_box then walks a box's sequence with contiguous loads
     const uint32_t i = P.svals[k];
+    if (P.skeys32) {
+        const unsigned long long key = P.keys[i];
+        const bool head = k == 0 || P.skeys32[k] != P.skeys32[k - 1];
+        if (!head && P.keys[P.svals[k - 1]] != key) atomicOr(P.ctr + kDynError, 32ull);
+        P.heads[k] = head ? 1u : 0u;
+        P.skeys_w[k] = key;
+    } else {
+        P.heads[k] = (k == 0 || P.skeys[k] != P.skeys[k - 1]) ? 1u : 0u;
+    }
+    // the points in box order: k_add_box then walks a box's sequence with contiguous loads
     const float4 p = reinterpret_cast<const float4*>(P.W)[i];
     reinterpret_cast<float4*>(P.Ws)[k] = make_float4(p.x, p.y, p.z, __uint_as_float(i));
 }
 
+constexpr int kBoxWaves = 4;       // k_add_box: waves per block
+constexpr uint32_t kBoxSmall = 64;  // boxes with at most this many new points: 16-lane groups
+constexpr int kBigBlocks = 64;      // k_add_box's first blocks: a wave per crowded box
+
 __global__ void k_add_starts(DynAddParams P) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= P.n) return;
-    if (P.heads[k]) P.starts[P.runid[k]] = (uint32_t)k;
+    if (P.heads[k]) {
+        const uint32_t r = P.runid[k];
+        P.starts[r] = (uint32_t)k;
+        // a crowded box (more than kBoxSmall new points) for k_add_box's waves: position
+        // k + kBoxSmall still in this run (runid = heads before: r + 1 inside the run)
+        const int64_t e = k + kBoxSmall;
+        if (e < P.n && !P.heads[e] && P.runid[e] == r + 1u) P.bigs[atomicAdd(P.ctr + kDynBig, 1ull)] = r;
+    }
     if (k == P.n - 1) {
         const uint32_t runs = P.runid[k] + P.heads[k];
         P.starts[runs] = (uint32_t)P.n;
@@ -193,37 +250,45 @@ __global__ void k_add_starts(DynAddParams P) {
     }
 }
 
-// A box's stored points (Search_by_range), one wave per box: the lanes take
-// the grid cells the box overlaps (one hash probe each), then the cells'
-// points spread over the lanes (a point's cell by a binary search of the
-// cells' exclusive counts in LDS).  `f(q, lane)` per stored point.
-struct WaveCells {
-    uint32_t exc[64], start[64];
+// A box's stored points (Search_by_range) by a group of G lanes (16: most
+// boxes hold a few stored points and new points; 64: the crowded boxes): the
+// lanes take the grid cells the box overlaps (one hash probe each), then the
+// cells' points spread over the lanes (a point's cell by a binary search of the
+// cells' exclusive counts in LDS).  `f(q)` per stored point.
+template <int G>
+struct GroupCells {
+    uint32_t exc[G], start[G];
 };
-template <class F>
-__device__ __forceinline__ void wave_box_points(const DynAddParams& P, const int (&l)[3], const int (&h)[3], int lane,
-                                                WaveCells& W, F&& f) {
+template <int G>
+__device__ __forceinline__ bool group_any(bool x) {
+    const unsigned long long b = __ballot(x);
+    if constexpr (G == 64) return b != 0ull;
+    else return ((b >> ((threadIdx.x & 63) & ~(G - 1))) & ((1ull << G) - 1ull)) != 0ull;
+}
+template <int G, class F>
+__device__ __forceinline__ void group_box_points(const DynAddParams& P, const int (&l)[3], const int (&h)[3], int gl,
+                                                 GroupCells<G>& W, F&& f) {
     const int ex = h[0] - l[0] + 1, ey = h[1] - l[1] + 1, ez = h[2] - l[2] + 1;
     const int ncell = (ex > 0 && ey > 0 && ez > 0) ? ex * ey * ez : 0;
     const float4* __restrict__ gp = reinterpret_cast<const float4*>(P.gpts);
-    for (int c0 = 0; c0 < ncell; c0 += 64) {  // wave-uniform
-        const int c = c0 + lane;
+    for (int c0 = 0; c0 < ncell; c0 += G) {  // group-uniform
+        const int c = c0 + gl;
         uint2 r = make_uint2(0u, 0u);
         if (c < ncell) r = cell_run(P.gslots, P.glog2, l[0] + c % ex, l[1] + (c / ex) % ey, l[2] + c / (ex * ey));
         uint32_t inc = r.y;
 #pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t v = __shfl_up(inc, off, 64);
-            if (lane >= off) inc += v;
+        for (int off = 1; off < G; off <<= 1) {
+            const uint32_t v = __shfl_up(inc, off, G);
+            if (gl >= off) inc += v;
         }
-        const uint32_t total = __shfl(inc, 63, 64);
-        W.exc[lane] = inc - r.y;
-        W.start[lane] = r.x;
+        const uint32_t total = __shfl(inc, G - 1, G);
+        W.exc[gl] = inc - r.y;
+        W.start[gl] = r.x;
         __builtin_amdgcn_wave_barrier();
-        for (uint32_t t = lane; t < total; t += 64) {
+        for (uint32_t t = gl; t < total; t += G) {
             int j = 0;  // the last cell whose exclusive count is <= t (it holds point t)
 #pragma unroll
-            for (int step = 32; step >= 1; step >>= 1)
+            for (int step = G / 2; step >= 1; step >>= 1)
                 if (W.exc[j + step] <= t) j += step;
             f(gp[W.start[j] + (t - W.exc[j])]);
         }
@@ -234,7 +299,7 @@ __device__ __forceinline__ void wave_box_points(const DynAddParams& P, const int
 // of two different positions share the nearest distance (the reference's tie,
 // decided by its tree order); `defer` if the box is dirty or holds a point that
 // also lies in a neighbouring box.  The lanes' partial results merge in any
-// order to the same (uniform) result.
+// order to the same (group-uniform) result.
 struct BoxStore {
     int cnt;
     float bd, bx, by, bz;
@@ -250,150 +315,200 @@ __device__ __forceinline__ void store_merge(BoxStore& S, float d, uint32_t id, f
         if (id < S.bid) { S.bid = id; S.bx = x; S.by = y; S.bz = z; }
     }
 }
-__device__ __forceinline__ void wave_box_store(const DynAddParams& P, unsigned long long key, const DBox& b, int lane,
-                                               WaveCells& W, BoxStore& S) {
+template <int G>
+__device__ __forceinline__ void group_box_store(const DynAddParams& P, unsigned long long key, const DBox& b, int gl,
+                                                GroupCells<G>& W, BoxStore& S) {
     S.cnt = 0; S.bd = INFINITY; S.bx = S.by = S.bz = 0.f; S.bid = 0xFFFFFFFFu; S.tie = false;
     S.l[0] = S.l[1] = S.l[2] = 0; S.h[0] = S.h[1] = S.h[2] = -1;
-    const unsigned long long nd = P.ctr[kDynDirty];
-    bool defer = nd > (unsigned long long)P.dirty_cap;
-    if (!defer) {
-        bool hit = false;
-        for (unsigned long long d = lane; d < nd; d += 64) hit = hit || P.dirty[d] == key;
-        defer = __ballot(hit) != 0ull;
-    }
+    bool defer = dirty_has(P, key);
     if (!defer && !box_cells(P, b, S.l, S.h)) defer = true;
     if (defer) {
         S.defer = true;
         return;
     }
     bool two = false;
-    wave_box_points(P, S.l, S.h, lane, W, [&](const float4 q) {
+    group_box_points<G>(P, S.l, S.h, gl, W, [&](const float4 q) {
         if (!in_dbox(b, q.x, q.y, q.z)) return;
         if (in_two(key, P.ds, q.x, q.y, q.z)) two = true;
         S.cnt++;
         store_merge(S, mid_dist(b, q.x, q.y, q.z), __float_as_uint(q.w), q.x, q.y, q.z, false);
     });
-    S.defer = __ballot(two) != 0ull;
+    S.defer = group_any<G>(two);
     if (S.defer) return;
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        S.cnt += __shfl_xor(S.cnt, off, 64);
-        const float d = __shfl_xor(S.bd, off, 64);
-        const uint32_t id = __shfl_xor(S.bid, off, 64);
-        const float x = __shfl_xor(S.bx, off, 64), y = __shfl_xor(S.by, off, 64), z = __shfl_xor(S.bz, off, 64);
-        const bool t = __shfl_xor((int)S.tie, off, 64) != 0;
+    for (int off = G / 2; off >= 1; off >>= 1) {
+        S.cnt += __shfl_xor(S.cnt, off, G);
+        const float d = __shfl_xor(S.bd, off, G);
+        const uint32_t id = __shfl_xor(S.bid, off, G);
+        const float x = __shfl_xor(S.bx, off, G), y = __shfl_xor(S.by, off, G), z = __shfl_xor(S.bz, off, G);
+        const bool t = __shfl_xor((int)S.tie, off, G) != 0;
         store_merge(S, d, id, x, y, z, t);
     }
 }
-constexpr int kBoxWaves = 4;  // k_add_box: waves per block
 
-// The running winner as a scan: (distance, position) with the smaller distance,
-// the later position on ties ("d <= dc" lets the later point win).
-__device__ __forceinline__ void win_combine(float& d, int& k, float d2, int k2) {
-    if (d2 < d || (d2 == d && k2 > k)) { d = d2; k = k2; }
-}
+// The running winner of a box's new points is a scan: (distance, position) with
+// the smaller distance, the later position on ties ("d <= dc" lets the later
+// point win), the winner's coordinates carried along.
 
-// One wave per box (Add_Points' loop body for the box's points, :390-437):
-// the stored points (wave_box_store), then the box's new points in input
-// order as a prefix scan of the running winner, 64 points per step (after the
-// first point the box holds one point), then Delete_by_range of the box with
-// the lanes over its stored points (a stored winner is deleted and added
+// Add_Points' loop body for the box's points (:390-437) by one group of G
+// lanes: the stored points (group_box_store), then the box's new points in
+// input order as a prefix scan of the running winner, G points per step (after
+// the first point the box holds one point), then Delete_by_range of the box
+// with the lanes over its stored points (a stored winner is deleted and added
 // again: it stays).
-__global__ __launch_bounds__(64 * kBoxWaves) void k_add_box(DynAddParams P) {
-    __shared__ WaveCells cells[kBoxWaves];
-    const int lane = threadIdx.x & 63;
-    WaveCells& W = cells[threadIdx.x >> 6];
-    if (P.ctr[kDynError]) return;  // k_add_prep refused the batch: nothing changes
-    const int64_t runs = (int64_t)P.ctr[kDynRuns];
+template <int G>
+__device__ __forceinline__ void add_box(const DynAddParams& P, int64_t g, int gl, GroupCells<G>& W) {
     const float4* __restrict__ Ws = reinterpret_cast<const float4*>(P.Ws);
-    for (int64_t g = (int64_t)blockIdx.x * kBoxWaves + (threadIdx.x >> 6); g < runs;
-         g += (int64_t)gridDim.x * kBoxWaves) {
-        const uint32_t s0 = P.starts[g], s1 = P.starts[g + 1];
-        const unsigned long long key = P.skeys[s0];
-        const DBox b = dbox(key, P.ds);
-        BoxStore S;
-        wave_box_store(P, key, b, lane, W, S);
-        if (S.defer) {
-            for (uint32_t k = s0 + lane; k < s1; k += 64) P.defer[P.svals[k]] = 1u;
-            continue;
+    const uint32_t s0 = P.starts[g], s1 = P.starts[g + 1];
+    const unsigned long long key = P.skeys[s0];
+    const DBox b = dbox(key, P.ds);
+    BoxStore S;
+    group_box_store<G>(P, key, b, gl, W, S);
+    if (S.defer) {
+        for (uint32_t k = s0 + gl; k < s1; k += G) P.defer[P.svals[k]] = 1u;
+        return;
+    }
+    // the first new point against the stored ones, the carry of the scan
+    const float4 p0 = Ws[s0];
+    float cd = mid_dist(b, p0.x, p0.y, p0.z);  // running winner: distance, position (-1: the stored point)
+    int ck = (int)s0;
+    float cx = p0.x, cy = p0.y, cz = p0.z;
+    if (S.cnt > 0 && S.bd < cd) { cd = S.bd; ck = -1; cx = S.bx; cy = S.by; cz = S.bz; }
+    const unsigned long long amb = (S.cnt > 1 && ck < 0 && S.tie) ? 1ull : 0ull;
+    unsigned long long events = 0;
+    if (gl == 0 && (S.cnt > 1 || ck >= 0 || same_pt(p0.x, p0.y, p0.z, cx, cy, cz))) events = 1;
+    if constexpr (G == 64) {
+        // a crowded box (up to thousands of new points): each lane a segment of
+        // consecutive points -- its winner, a scan of the segments' winners, then
+        // the segment replayed from the winner before it to count the events
+        const uint32_t cnt = s1 - (s0 + 1), L = (cnt + 63u) / 64u;
+        const uint32_t a0 = min(s1, s0 + 1 + (uint32_t)gl * L), a1 = min(s1, a0 + L);
+        float sd = INFINITY, sx = 0.f, sy = 0.f, sz = 0.f;
+        int sk = -2;
+        for (uint32_t k = a0; k < a1; k++) {
+            const float4 p = Ws[k];
+            const float d = mid_dist(b, p.x, p.y, p.z);
+            if (d <= sd) { sd = d; sk = (int)k; sx = p.x; sy = p.y; sz = p.z; }
         }
-        // the first new point against the stored ones, the carry of the scan
-        const float4 p0 = Ws[s0];
-        float cd = mid_dist(b, p0.x, p0.y, p0.z);  // running winner: distance, position (-1: the stored point)
-        int ck = (int)s0;
-        float cx = p0.x, cy = p0.y, cz = p0.z;
-        if (S.cnt > 0 && S.bd < cd) { cd = S.bd; ck = -1; cx = S.bx; cy = S.by; cz = S.bz; }
-        const unsigned long long amb = (S.cnt > 1 && ck < 0 && S.tie) ? 1ull : 0ull;
-        unsigned long long events = 0;
-        if (lane == 0 && (S.cnt > 1 || ck >= 0 || same_pt(p0.x, p0.y, p0.z, cx, cy, cz))) events = 1;
-        for (uint32_t k0 = s0 + 1; k0 < s1; k0 += 64) {
-            const uint32_t k = k0 + lane;
-            const bool valid = k < s1;
-            float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-            float d = INFINITY;
-            int pk = -2;  // loses every comparison
-            if (valid) {
-                p = Ws[k];
-                d = mid_dist(b, p.x, p.y, p.z);
-                pk = (int)k;
-            }
-            // inclusive scan of the running winner over lanes 0..lane
-            float sd = d;
-            int sk = pk;
 #pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const float od = __shfl_up(sd, off, 64);
-                const int okk = __shfl_up(sk, off, 64);
-                if (lane >= off) win_combine(sd, sk, od, okk);
-            }
-            // the winner before this point: the carry (every earlier point), then the
-            // chunk's exclusive prefix -- later on equal distance, so the chunk wins ties
-            float pd = cd;
-            int pkk = ck;
+        for (int off = 1; off < 64; off <<= 1) {  // inclusive: the later segment wins ties
+            const float od = __shfl_up(sd, off, 64);
+            const int okk = __shfl_up(sk, off, 64);
+            const float ox = __shfl_up(sx, off, 64), oy = __shfl_up(sy, off, 64), oz = __shfl_up(sz, off, 64);
+            if (gl >= off && !(sd <= od)) { sd = od; sk = okk; sx = ox; sy = oy; sz = oz; }
+        }
+        float rd = cd, rx = cx, ry = cy, rz = cz;  // the winner before the segment
+        {
             const float xd = __shfl_up(sd, 1, 64);
-            const int xk = __shfl_up(sk, 1, 64);
-            if (lane > 0) win_combine(pd, pkk, xd, xk);
-            // the previous winner's coordinates
-            float qx = cx, qy = cy, qz = cz;
-            if (pkk >= 0 && pkk != ck) {
-                const float4 w = Ws[pkk];
-                qx = w.x; qy = w.y; qz = w.z;
-            }
-            if (valid && (d <= pd || same_pt(p.x, p.y, p.z, qx, qy, qz))) events++;
-            // new carry: the inclusive winner of the last valid lane against the carry
-            const int last = (int)min<uint32_t>(63u, s1 - 1 - k0);
-            const float ld = __shfl(sd, last, 64);
-            const int lk = __shfl(sk, last, 64);
-            if (ld < cd || (ld == cd && lk > ck)) {
-                cd = ld; ck = lk;
-                const float4 w = Ws[lk];
-                cx = w.x; cy = w.y; cz = w.z;
+            const float xx = __shfl_up(sx, 1, 64), xy = __shfl_up(sy, 1, 64), xz = __shfl_up(sz, 1, 64);
+            if (gl > 0 && xd <= rd) { rd = xd; rx = xx; ry = xy; rz = xz; }
+        }
+        for (uint32_t k = a0; k < a1; k++) {
+            const float4 p = Ws[k];
+            const float d = mid_dist(b, p.x, p.y, p.z);
+            if (d <= rd) {
+                events++;
+                rd = d; rx = p.x; ry = p.y; rz = p.z;
+            } else if (same_pt(p.x, p.y, p.z, rx, ry, rz)) {
+                events++;
             }
         }
-        const bool newer = ck >= 0;
-        if (newer && lane == 0) P.keep[__float_as_uint(Ws[ck].w)] = 1u;
-        unsigned long long deleted = 0;
-        if (S.cnt > 0 && (newer || S.cnt > 1)) {
-            wave_box_points(P, S.l, S.h, lane, W, [&](const float4 q) {
-                if (!in_dbox(b, q.x, q.y, q.z)) return;
-                const uint32_t id = __float_as_uint(q.w);
-                if (!newer && id == S.bid) return;
-                P.alive[id] = 0;
-                deleted++;
-            });
+        const float ld = __shfl(sd, 63, 64);
+        const int lk = __shfl(sk, 63, 64);
+        const float lx = __shfl(sx, 63, 64), ly = __shfl(sy, 63, 64), lz = __shfl(sz, 63, 64);
+        if (lk >= 0 && ld <= cd) { cd = ld; ck = lk; cx = lx; cy = ly; cz = lz; }
+    } else
+    for (uint32_t k0 = s0 + 1; k0 < s1; k0 += G) {
+        const uint32_t k = k0 + gl;
+        const bool valid = k < s1;
+        float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+        float d = INFINITY;
+        int pk = -2;  // loses every comparison
+        if (valid) {
+            p = Ws[k];
+            d = mid_dist(b, p.x, p.y, p.z);
+            pk = (int)k;
         }
+        // inclusive scan of the running winner over lanes 0..gl, its coordinates carried along
+        float sd = d, sx = p.x, sy = p.y, sz = p.z;
+        int sk = pk;
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            events += __shfl_xor(events, off, 64);
-            deleted += __shfl_xor(deleted, off, 64);
+        for (int off = 1; off < G; off <<= 1) {
+            const float od = __shfl_up(sd, off, G);
+            const int okk = __shfl_up(sk, off, G);
+            const float ox = __shfl_up(sx, off, G), oy = __shfl_up(sy, off, G), oz = __shfl_up(sz, off, G);
+            if (gl >= off && (od < sd || (od == sd && okk > sk))) {
+                sd = od; sk = okk; sx = ox; sy = oy; sz = oz;
+            }
         }
-        if (lane == 0) {
-            if (events) atomicAdd(P.ctr + kDynEvents, events);
-            if (deleted) atomicAdd(P.ctr + kDynDeleted, deleted);
-            if (amb) atomicAdd(P.ctr + kDynAmbig, amb);
+        // the winner before this point: the carry (every earlier point), then the
+        // chunk's exclusive prefix -- later on equal distance, so the chunk wins ties
+        float pd = cd, qx = cx, qy = cy, qz = cz;
+        int pkk = ck;
+        {
+            const float xd = __shfl_up(sd, 1, G);
+            const int xk = __shfl_up(sk, 1, G);
+            const float xx = __shfl_up(sx, 1, G), xy = __shfl_up(sy, 1, G), xz = __shfl_up(sz, 1, G);
+            if (gl > 0 && (xd < pd || (xd == pd && xk > pkk))) {
+                pd = xd; pkk = xk; qx = xx; qy = xy; qz = xz;
+            }
+        }
+        if (valid && (d <= pd || same_pt(p.x, p.y, p.z, qx, qy, qz))) events++;
+        // new carry: the inclusive winner of the last valid lane against the carry
+        const int last = (int)min<uint32_t>((uint32_t)(G - 1), s1 - 1 - k0);
+        const float ld = __shfl(sd, last, G);
+        const int lk = __shfl(sk, last, G);
+        const float lx = __shfl(sx, last, G), ly = __shfl(sy, last, G), lz = __shfl(sz, last, G);
+        if (ld < cd || (ld == cd && lk > ck)) {
+            cd = ld; ck = lk; cx = lx; cy = ly; cz = lz;
         }
     }
+    const bool newer = ck >= 0;
+    if (newer && gl == 0) P.keep[__float_as_uint(Ws[ck].w)] = 1u;
+    unsigned long long deleted = 0;
+    if (S.cnt > 0 && (newer || S.cnt > 1)) {
+        group_box_points<G>(P, S.l, S.h, gl, W, [&](const float4 q) {
+            if (!in_dbox(b, q.x, q.y, q.z)) return;
+            const uint32_t id = __float_as_uint(q.w);
+            if (!newer && id == S.bid) return;
+            P.alive[id] = 0;
+            deleted++;
+        });
+    }
+#pragma unroll
+    for (int off = G / 2; off >= 1; off >>= 1) {
+        events += __shfl_xor(events, off, G);
+        deleted += __shfl_xor(deleted, off, G);
+    }
+    if (gl == 0) {
+        if (events) atomicAdd(P.ctr + kDynEvents, events);
+        if (deleted) atomicAdd(P.ctr + kDynDeleted, deleted);
+        if (amb) atomicAdd(P.ctr + kDynAmbig, amb);
+    }
 }
+// One launch: the first kBigBlocks blocks take the crowded boxes (listed by
+// k_add_starts), a wave each; the others the rest, a 16-lane group each.
+__global__ __launch_bounds__(64 * kBoxWaves) void k_add_box(DynAddParams P) {
+    constexpr int G = 16, kGroups = 64 * kBoxWaves / G;
+    __shared__ GroupCells<G> cells[kGroups];
+    if (P.ctr[kDynError]) return;  // k_add_prep refused the batch: nothing changes
+    if (blockIdx.x < kBigBlocks) {
+        GroupCells<64>& W = reinterpret_cast<GroupCells<64>*>(cells)[threadIdx.x >> 6];
+        const int64_t nb = (int64_t)P.ctr[kDynBig];
+        for (int64_t b = (int64_t)blockIdx.x * kBoxWaves + (threadIdx.x >> 6); b < nb; b += kBigBlocks * kBoxWaves)
+            add_box<64>(P, P.bigs[b], threadIdx.x & 63, W);
+        return;
+    }
+    const int gl = threadIdx.x & (G - 1);
+    GroupCells<G>& W = cells[threadIdx.x / G];
+    const int64_t runs = (int64_t)P.ctr[kDynRuns];
+    for (int64_t g = (int64_t)(blockIdx.x - kBigBlocks) * kGroups + threadIdx.x / G; g < runs;
+         g += (int64_t)(gridDim.x - kBigBlocks) * kGroups) {
+        if (P.starts[g + 1] - P.starts[g] > kBoxSmall) continue;  // (group-uniform) a crowded box
+        add_box<G>(P, g, gl, W);
+    }
+}
+static_assert(sizeof(GroupCells<64>) * kBoxWaves <= sizeof(GroupCells<16>) * (64 * kBoxWaves / 16), "LDS");
 
 __global__ void k_add_dlist(DynAddParams P) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -547,6 +662,38 @@ __global__ void k_dyn_cellkeys(const float4* __restrict__ all, const uint8_t* __
 }
 
 // ---- the grid merged instead of re-sorted (dyn_rebuild's incremental path) ----
+// The new ids' cell keys sorted by (key, index), m <= kNewSortMax: every
+// workgroup keys all of them into LDS, then 8 lanes count one key's rank, each
+// over an eighth of the keys (broadcast reads), summed by shuffles.
+constexpr int kNewSortSplit = 8;
+__global__ __launch_bounds__(256) void k_dyn_newsort(const float4* __restrict__ all, const uint8_t* __restrict__ alive,
+                                                     int64_t m, float ox, float oy, float oz, float inv,
+                                                     unsigned long long* skeys, uint32_t* svals,
+                                                     unsigned long long* ctr) {
+    __shared__ unsigned long long K[kNewSortMax];
+    const int mm = (int)m;
+    bool bad = false;
+    for (int i = threadIdx.x; i < mm; i += blockDim.x)
+        K[i] = alive[i] ? cell_key_of(all[i], ox, oy, oz, inv, bad) : ~0ull;
+    if (bad && blockIdx.x == 0) atomicOr(ctr + kDynError, 4ull);
+    __syncthreads();
+    const int i = (blockIdx.x * blockDim.x + threadIdx.x) / kNewSortSplit;  // (the 8 lanes of i: one wave)
+    const int q = threadIdx.x % kNewSortSplit;
+    const int ii = i < mm ? i : mm - 1;
+    const unsigned long long key = K[ii];
+    const int per = (mm + kNewSortSplit - 1) / kNewSortSplit, j1 = min(mm, (q + 1) * per);
+    int r = 0;
+    for (int j = q * per; j < j1; j++) {
+        const unsigned long long kj = K[j];
+        r += (int)(kj < key) | ((int)(kj == key) & (int)(j < ii));
+    }
+#pragma unroll
+    for (int off = 1; off < kNewSortSplit; off <<= 1) r += __shfl_xor(r, off, kNewSortSplit);
+    if (q == 0 && i < mm) {
+        skeys[r] = key;
+        svals[r] = (uint32_t)i;
+    }
+}
 // flags[i] = the old grid's point i is still alive (i < na_old), flags[na_old] = 0.
 __global__ void k_dyn_flags(const float4* __restrict__ gpts, int64_t na_old, const uint8_t* __restrict__ alive,
                             uint32_t* flags) {
@@ -872,9 +1019,10 @@ int launch_add_heads(const DynAddParams& p, void* stream) { DYN_LAUNCH(k_add_hea
 int launch_add_starts(const DynAddParams& p, void* stream) { DYN_LAUNCH(k_add_starts, p.n, p); }
 int launch_add_group(const DynAddParams& p, void* stream) {
     if (p.n <= 0) return LIVO_OK;
-    const int64_t blocks = (p.n + kBoxWaves - 1) / kBoxWaves;  // runs <= n: a wave per box, at most 16k waves
-    hipLaunchKernelGGL(k_add_box, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(64 * kBoxWaves), 0,
-                       (hipStream_t)stream, p);
+    const int64_t per_block = 64 * kBoxWaves / 16;  // runs <= n: a 16-lane group per box, at most 64k groups
+    const int64_t blocks = (p.n + per_block - 1) / per_block;
+    hipLaunchKernelGGL(k_add_box, dim3((unsigned)(kBigBlocks + (blocks < 4096 ? blocks : 4096))), dim3(64 * kBoxWaves),
+                       0, (hipStream_t)stream, p);
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 int launch_add_dlist(const DynAddParams& p, void* stream) { DYN_LAUNCH(k_add_dlist, p.n, p); }
@@ -911,6 +1059,15 @@ int launch_dyn_slots(const unsigned long long* skeys, const uint32_t* starts, in
 }
 int launch_dyn_flags(const float* gpts, int64_t na_old, const uint8_t* alive, uint32_t* flags, void* stream) {
     DYN_LAUNCH(k_dyn_flags, na_old + 1, reinterpret_cast<const float4*>(gpts), na_old, alive, flags);
+}
+int launch_dyn_newsort(const float* all, const uint8_t* alive, int64_t m, const float* org, float inv,
+                       unsigned long long* skeys, uint32_t* svals, unsigned long long* ctr, void* stream) {
+    if (m <= 0) return LIVO_OK;
+    if (m > kNewSortMax) return LIVO_E_RANGE;
+    hipLaunchKernelGGL(k_dyn_newsort, dim3((unsigned)((m * kNewSortSplit + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const float4*>(all),
+                       alive, m, org[0], org[1], org[2], inv, skeys, svals, ctr);
+    return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 int launch_dyn_merge(const DynMergeParams& p, void* stream) { DYN_LAUNCH(k_dyn_merge, p.na_old + p.m + 3, p); }
 int launch_cr_rho(const float* gpts, int64_t n, const float org[3], float h, uint32_t* rho_bits, uint32_t* iota,

@@ -158,6 +158,7 @@ struct DynDev {
     float grid_gh = 0.f;
     bool merge = true;               // LIVO_DYN_MERGE=0: always sort
     int64_t rebuilds_sorted = 0, rebuilds_merged = 0;
+    int64_t wide_redos = 0;          // Add_Points batches redone with 64-bit box keys
 };
 
 // One batch's staging and streams.  LaserMapping batches: slots packed at
@@ -1092,7 +1093,7 @@ static void dyn_free(DynDev& d) {
     dev_free(d.heads); dev_free(d.runid); dev_free(d.starts);
     dev_free(d.W); dev_free(d.seq); dev_free(d.Ws);
     dev_free(d.defer); dev_free(d.dpos); dev_free(d.dlist); dev_free(d.keep); dev_free(d.apos);
-    dev_free(d.boxes); dev_free(d.dirty); dev_free(d.ctr);
+    dev_free(d.boxes); dev_free(d.ctr);  // (d.dirty lives in d.ctr's allocation)
     dev_free(d.rpts); dev_free(d.rpos); dev_free(d.dslots); dev_free(d.dpts);
     dev_free(d.dvslots); dev_free(d.dvidx); dev_free(d.gpts_alt);
     d = DynDev{};
@@ -1153,6 +1154,15 @@ static int dyn_add_scratch(livo_ctx* c, int64_t n) {
     return LIVO_OK;
 }
 
+static int sort_u32(livo_ctx* c, const uint32_t* kin, uint32_t* kout, const uint32_t* vin, uint32_t* vout, int64_t n,
+                    int bits) {
+    size_t tb = 0;
+    int rc = prim_sort_pairs_u32(nullptr, &tb, kin, kout, vin, vout, n, bits, c->stream);
+    if (!rc) rc = ensure_prim(c, tb);
+    tb = c->prim_bytes;
+    if (!rc) rc = prim_sort_pairs_u32(c->prim_tmp, &tb, kin, kout, vin, vout, n, bits, c->stream);
+    return rc;
+}
 static int sort_u64(livo_ctx* c, const unsigned long long* kin, unsigned long long* kout, const uint32_t* vin,
                     uint32_t* vout, int64_t n) {
     size_t tb = 0;
@@ -1307,7 +1317,10 @@ static int dyn_activate(livo_ctx* c) {
     if (d.active) return LIVO_OK;
     if (!c->has_map) return LIVO_E_NOMAP;
     if (c->knn_kind == 0) return LIVO_E_INVALID;  // kept on the cell grid (not LIVO_KNN_KIND=leaf)
-    if (!d.ctr && (dev_alloc(&d.ctr, kDynCtrN) || dev_alloc(&d.dirty, kDynDirtyCap))) return LIVO_E_OOM;
+    if (!d.ctr) {
+        if (dev_alloc(&d.ctr, kDynCtrPad + kDynDirtyCap)) return LIVO_E_OOM;
+        d.dirty = d.ctr + kDynCtrPad;  // (one allocation: dyn_add clears both with one memset)
+    }
     const int64_t M = c->map_points;
     d.n_ids = d.n_alive = 0;
     int rc = dyn_grow(c, M + 1);
@@ -1442,7 +1455,9 @@ static int dyn_rebuild_merge(livo_ctx* c) {
     }
     const float inv = 1.0f / c->gh;
     HIP_TRY(hipMemsetAsync(d.ctr, 0, kDynCtrN * sizeof(unsigned long long), c->stream));
-    if (m > 0) {
+    if (m > 0 && m <= kNewSortMax) {  // (a scan's few hundred winners: one workgroup)
+        rc = launch_dyn_newsort(d.all + 4 * g0, d.alive + g0, m, c->gorg, inv, d.skeys, d.svals, d.ctr, c->stream);
+    } else if (m > 0) {
         rc = launch_dyn_cellkeys(d.all + 4 * g0, d.alive + g0, m, c->gorg, inv, d.keys, d.iota, d.ctr, c->stream);
         if (!rc) rc = sort_u64(c, d.keys, d.skeys, d.iota, d.svals, m);
     }
@@ -1514,39 +1529,55 @@ static int dyn_add(livo_ctx* c, int64_t n, float ds, bool downsample, livo_map_a
         int rc = dyn_grow(c, d.n_ids + n);
         if (!rc) rc = dyn_sort_scratch(c, n + 1);
         if (rc) return rc;
-        HIP_TRY(hipMemsetAsync(d.ctr, 0, kDynCtrN * sizeof(unsigned long long), c->stream));
-        DynAddParams P{};
-        P.W = d.W; P.n = n; P.ds = ds; P.downsample = downsample ? 1 : 0;
-        P.gslots = c->gslots; P.gpts = c->gpts; P.glog2 = c->glog2;
-        std::memcpy(P.gorg, c->gorg, sizeof(P.gorg));
-        P.gh = c->gh; P.ginv = 1.0f / c->gh; P.geps = c->geps;
-        P.base = d.n_ids; P.alive = d.alive;
-        P.keys = d.keys; P.iota = d.iota; P.skeys = d.skeys; P.svals = d.svals; P.Ws = d.Ws;
-        P.heads = d.heads; P.runid = d.runid; P.starts = d.starts;
-        P.defer = d.defer; P.dpos = d.dpos; P.dlist = d.dlist; P.keep = d.keep; P.seq = d.seq;
-        P.dirty = d.dirty; P.dirty_cap = kDynDirtyCap; P.ctr = d.ctr;
-        // k_add_prep refuses an out-of-range batch (ctr[kDynError] bit 0): the
-        // passes that change the map (k_add_box, k_add_seq, k_add_append) then
-        // do nothing, so the one read-back at the end decides
-        rc = launch_add_prep(P, c->stream);
-        if (rc) return rc;
-        if (downsample) {
-            rc = sort_u64(c, d.keys, d.skeys, d.iota, d.svals, n);
-            if (!rc) rc = launch_add_heads(P, c->stream);
-            if (!rc) rc = ivox_scan(c, d.heads, d.runid, n);
-            if (!rc) rc = launch_add_starts(P, c->stream);
-            if (!rc) rc = launch_add_group(P, c->stream);
-            if (!rc) rc = ivox_scan(c, d.defer, d.dpos, n);
-            if (!rc) rc = launch_add_dlist(P, c->stream);
-            if (!rc) rc = launch_add_seq(P, c->stream);
-        }
-        if (!rc) rc = ivox_scan(c, d.keep, d.apos, n);
-        if (!rc) rc = launch_add_append(d.W, d.keep, d.apos, n, d.n_ids, d.all, d.alive, d.ctr, c->stream);
-        if (rc) return rc;
+        // The box keys sort as 30-bit keys (10 bits per axis, wrapped): k_add_heads
+        // finds two boxes sharing a wrapped key and the batch is redone with the
+        // 64-bit keys (ctr bit 32: nothing changed).  LIVO_DYN_WIDE_KEYS=1: always 64-bit.
+        static const bool wide_env = [] {
+            const char* e = std::getenv("LIVO_DYN_WIDE_KEYS");
+            return e && std::atoi(e) == 1;
+        }();
         unsigned long long h[kDynCtrN];
-        HIP_TRY(hipMemcpyAsync(h, d.ctr, sizeof(h), hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        if (h[kDynError] & 1ull) return LIVO_E_RANGE;  // nothing changed
+        for (bool wide = wide_env;; wide = true) {
+            HIP_TRY(hipMemsetAsync(d.ctr, 0, (kDynCtrPad + kDynDirtyCap) * sizeof(unsigned long long), c->stream));
+            DynAddParams P{};
+            P.W = d.W; P.n = n; P.ds = ds; P.downsample = downsample ? 1 : 0;
+            P.gslots = c->gslots; P.gpts = c->gpts; P.glog2 = c->glog2;
+            std::memcpy(P.gorg, c->gorg, sizeof(P.gorg));
+            P.gh = c->gh; P.ginv = 1.0f / c->gh; P.geps = c->geps;
+            P.base = d.n_ids; P.alive = d.alive;
+            P.keys = d.keys; P.iota = d.iota; P.skeys = d.skeys; P.svals = d.svals; P.Ws = d.Ws;
+            P.heads = d.heads; P.runid = d.runid; P.starts = d.starts;
+            P.defer = d.defer; P.dpos = d.dpos; P.dlist = d.dlist; P.keep = d.keep; P.seq = d.seq;
+            P.dirty = d.dirty; P.dirty_cap = kDynDirtyCap; P.ctr = d.ctr;
+            P.bigs = d.dlist;  // (dlist is free from the sort until k_add_dlist)
+            if (downsample && !wide) {  // (dlist / dpos are free until k_add_box)
+                P.keys32 = d.dlist; P.skeys32 = d.dpos; P.skeys_w = d.skeys;
+            }
+            // k_add_prep refuses an out-of-range batch (ctr[kDynError] bit 0): the
+            // passes that change the map (k_add_box, k_add_seq, k_add_append) then
+            // do nothing, so the one read-back at the end decides
+            rc = launch_add_prep(P, c->stream);
+            if (rc) return rc;
+            if (downsample) {
+                if (P.keys32) rc = sort_u32(c, P.keys32, P.skeys32, d.iota, d.svals, n, 30);
+                else rc = sort_u64(c, d.keys, d.skeys, d.iota, d.svals, n);
+                if (!rc) rc = launch_add_heads(P, c->stream);
+                if (!rc) rc = ivox_scan(c, d.heads, d.runid, n);
+                if (!rc) rc = launch_add_starts(P, c->stream);
+                if (!rc) rc = launch_add_group(P, c->stream);
+                if (!rc) rc = ivox_scan(c, d.defer, d.dpos, n);
+                if (!rc) rc = launch_add_dlist(P, c->stream);
+                if (!rc) rc = launch_add_seq(P, c->stream);
+            }
+            if (!rc) rc = ivox_scan(c, d.keep, d.apos, n);
+            if (!rc) rc = launch_add_append(d.W, d.keep, d.apos, n, d.n_ids, d.all, d.alive, d.ctr, c->stream);
+            if (rc) return rc;
+            HIP_TRY(hipMemcpyAsync(h, d.ctr, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            if (h[kDynError] & 1ull) return LIVO_E_RANGE;  // nothing changed
+            if (!(h[kDynError] & 32ull) || wide) break;
+            d.wide_redos++;
+        }
         // k_add_prep checked the range of every box the later passes read, so
         // the group / sequential passes cannot fail once the map is modified
         if (h[kDynError]) return LIVO_E_HIP;
@@ -4347,9 +4378,10 @@ int livo_sync(livo_ctx* c) {
 
 }  // extern "C"
 
-extern "C" int livo_debug_map_rebuilds(livo_ctx* c, int64_t out[2]) {
+extern "C" int livo_debug_map_rebuilds(livo_ctx* c, int64_t out[3]) {
     if (!c || !out) return LIVO_E_INVALID;
     out[0] = c->dyn.rebuilds_sorted;
     out[1] = c->dyn.rebuilds_merged;
+    out[2] = c->dyn.wide_redos;
     return LIVO_OK;
 }

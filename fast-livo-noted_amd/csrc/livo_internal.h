@@ -577,8 +577,10 @@ int launch_vio_end(const VioParams& p, void* stream);
 // KD_TREE::Add_Points / Delete_Point_Boxes on the map's point set, then the
 // cell grid rebuilt from the surviving points.  Counters in DynAddParams::ctr:
 enum { kDynEvents = 0, kDynDeleted = 1, kDynAmbig = 2, kDynDeferred = 3, kDynError = 4, kDynDirty = 5,
-       kDynAbsMax = 6, kDynRuns = 7, kDynTomb = 8, kDynAliveCnt = 9, kDynAdded = 10, kDynCtrN = 11 };
-constexpr uint32_t kDynDirtyCap = 4096;  // dirty boxes listed; beyond, every point takes the sequential pass
+       kDynAbsMax = 6, kDynRuns = 7, kDynTomb = 8, kDynAliveCnt = 9, kDynAdded = 10, kDynBig = 11, kDynCtrN = 12 };
+constexpr uint32_t kDynDirtyCap = 4096;  // dirty-box set slots; past half full every point takes the sequential pass
+constexpr int kDynCtrPad = 16;           // ctr, then the dirty-box set (one allocation, one clear)
+static_assert(kDynCtrN <= kDynCtrPad, "ctr overlaps the dirty-box set");
 struct DynAddParams {
     const float* W;             // n points to add (x, y, z, -), PointToAdd order
     int64_t n;
@@ -604,9 +606,13 @@ struct DynAddParams {
     uint32_t* dlist;            // deferred points, input order
     uint32_t* keep;             // n, by point: left in the map by this call
     float* seq;                 // sequential pass: its kept points (4 floats each)
-    unsigned long long* dirty;  // dirty box keys
+    unsigned long long* dirty;  // dirty box keys: an open-addressing set of dirty_cap slots (0: empty)
     uint32_t dirty_cap;
     unsigned long long* ctr;    // kDynCtrN counters
+    uint32_t* keys32;           // n: the box key wrapped to 10 bits per axis (null: sort the 64-bit keys)
+    uint32_t* skeys32;          // n: sorted
+    unsigned long long* skeys_w;  // = skeys (k_add_heads writes the 64-bit keys in sorted order)
+    uint32_t* bigs;             // the crowded boxes (runs), listed by k_add_starts (count: ctr[kDynBig])
 };
 struct DynWorldParams {
     const float* pts;           // scan body points (stored order, 4 floats each)
@@ -654,6 +660,9 @@ struct DynMergeParams {
     unsigned long long* ctr;
 };
 int launch_dyn_flags(const float* gpts, int64_t na_old, const uint8_t* alive, uint32_t* flags, void* stream);
+constexpr int kNewSortMax = 2048;  // k_dyn_newsort: new ids keyed and sorted in one workgroup
+int launch_dyn_newsort(const float* all, const uint8_t* alive, int64_t m, const float* org, float inv,
+                       unsigned long long* skeys, uint32_t* svals, unsigned long long* ctr, void* stream);
 int launch_dyn_merge(const DynMergeParams& p, void* stream);
 int launch_dyn_delete_boxes(const float* all, uint8_t* alive, int64_t n_ids, const float* boxes, int64_t nb,
                             unsigned long long* cnt, void* stream);

@@ -331,10 +331,11 @@ class Context:
         _check("livo_map_build", self._L.livo_map_build(self.h, _ptr(xyz), xyz.shape[0], xyz.shape[1] * 4))
 
     def map_rebuilds(self) -> tuple:
-        """(grid rebuilds by sorting every id, by merging the added ids) of the incremental map."""
-        out = (C.c_int64 * 2)()
+        """(grid rebuilds by sorting every id, by merging the added ids, Add_Points batches
+        redone with 64-bit box keys) of the incremental map."""
+        out = (C.c_int64 * 3)()
         _check("livo_debug_map_rebuilds", self._L.livo_debug_map_rebuilds(self.h, out))
-        return int(out[0]), int(out[1])
+        return int(out[0]), int(out[1]), int(out[2])
 
     def map_info(self) -> dict:
         mi = MapInfo()

@@ -293,6 +293,7 @@ def test_grid_merge_equals_sort(built, monkeypatch):
             out[merge] = (rec, ctx.map_rebuilds())
     (a, ra), (b, rb) = out["1"], out["0"]
     assert ra[1] >= 4 and rb[1] == 0, (ra, rb)
+    assert ra[2] == rb[2] == 0
     assert len(a) == len(b)
     for x, y in zip(a, b):
         if isinstance(x, tuple):
@@ -300,3 +301,24 @@ def test_grid_merge_equals_sort(built, monkeypatch):
                 assert np.array_equal(np.asarray(u).view(np.uint8), np.asarray(v).view(np.uint8))
         else:
             assert x == y
+
+
+def test_add_points_wrapped_box_key_clash(ictx):
+    """The box keys sort as 30-bit keys (10 bits per axis, wrapped): boxes 1024
+    boxes apart share a wrapped key, the batch is redone with the 64-bit keys,
+    and the result equals the oracle's."""
+    rng = np.random.default_rng(21)
+    ds = 0.05
+    m = rng.uniform(0, 2, (400, 3)).astype(f32)
+    dm = _pair(ictx, m)
+    base = rng.uniform(0, 2, (300, 3))
+    W = np.concatenate([base, base[:40] + [1024 * ds, 0, 0], base[40:80] + [1024 * ds, 1024 * ds, 1024 * ds]])
+    W = W[rng.permutation(len(W))].astype(f32)
+    r0 = ictx.map_rebuilds()[2]
+    _same_add(ictx.map_add_points(W, ds), dm.add_points(W, ds))
+    _same_map(ictx, dm)
+    assert ictx.map_rebuilds()[2] == r0 + 1
+    W2 = rng.uniform(0, 2, (300, 3)).astype(f32)  # no clash: no redo
+    _same_add(ictx.map_add_points(W2, ds), dm.add_points(W2, ds))
+    _same_map(ictx, dm)
+    assert ictx.map_rebuilds()[2] == r0 + 1
