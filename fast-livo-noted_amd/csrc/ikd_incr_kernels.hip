@@ -19,9 +19,9 @@
 //                 then the box's whole sequence of new points.  Boxes are
 //                 independent, except dirty boxes and boxes holding a stored
 //                 point that lies in two boxes: those are deferred
-//   k_add_seq     one thread: the deferred points in input order, with the
-//                 reference's sequential rule
-//   k_add_append  kept points appended with the next ids (input order)
+//   k_add_finish  one workgroup: the deferred points in input order on one
+//                 thread with the reference's sequential rule, then the kept
+//                 points appended with the next ids (input order)
 //   k_dyn_*       the cell grid of k_knn_grid rebuilt from the surviving
 //                 points (keys -> radix sort -> runs -> hash), and
 //                 Delete_Point_Boxes (:501-521)
@@ -152,11 +152,16 @@ __global__ void k_add_prep(DynAddParams P) {
     // the point's cell of the map grid must be addressable (k_knn_grid's key range)
 #pragma unroll
     for (int a = 0; a < 3; a++) ok = ok && fabsf(floorf((v[a] - P.gorg[a]) * P.ginv)) < (float)(kGridBias - 8);
-    {  // the batch's largest |coordinate|: one atomic per wave
+    {  // the batch's largest |coordinate|: one global atomic per block (one address: they serialise)
+        __shared__ uint32_t bmax;
+        if (threadIdx.x == 0) bmax = 0u;
+        __syncthreads();
         uint32_t m = (i < P.n && ok) ? __float_as_uint(am) : 0u;
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
-        if ((threadIdx.x & 63) == 0 && m) atomicMax(P.ctr + kDynAbsMax, (unsigned long long)m);
+        if ((threadIdx.x & 63) == 0 && m) atomicMax(&bmax, m);
+        __syncthreads();
+        if (threadIdx.x == 0 && bmax) atomicMax(P.ctr + kDynAbsMax, (unsigned long long)bmax);
     }
     if (i >= P.n) return;
     P.iota[i] = (uint32_t)i;
@@ -364,8 +369,15 @@ __device__ __forceinline__ void add_box(const DynAddParams& P, int64_t g, int gl
     const DBox b = dbox(key, P.ds);
     BoxStore S;
     group_box_store<G>(P, key, b, gl, W, S);
-    if (S.defer) {
-        for (uint32_t k = s0 + gl; k < s1; k += G) P.defer[P.svals[k]] = 1u;
+    if (S.defer) {  // flagged, and listed (unordered) for k_add_finish
+        unsigned long long at = 0;
+        if (gl == 0) at = atomicAdd(P.ctr + kDynDeferred, (unsigned long long)(s1 - s0));
+        at = __shfl(at, 0, G);
+        for (uint32_t k = s0 + gl; k < s1; k += G) {
+            const uint32_t i = P.svals[k];
+            P.defer[i] = 1u;
+            P.dlist_u[at + (k - s0)] = i;
+        }
         return;
     }
     // the first new point against the stored ones, the carry of the scan
@@ -385,6 +397,7 @@ __device__ __forceinline__ void add_box(const DynAddParams& P, int64_t g, int gl
         const uint32_t a0 = min(s1, s0 + 1 + (uint32_t)gl * L), a1 = min(s1, a0 + L);
         float sd = INFINITY, sx = 0.f, sy = 0.f, sz = 0.f;
         int sk = -2;
+#pragma unroll 4
         for (uint32_t k = a0; k < a1; k++) {
             const float4 p = Ws[k];
             const float d = mid_dist(b, p.x, p.y, p.z);
@@ -403,6 +416,7 @@ __device__ __forceinline__ void add_box(const DynAddParams& P, int64_t g, int gl
             const float xx = __shfl_up(sx, 1, 64), xy = __shfl_up(sy, 1, 64), xz = __shfl_up(sz, 1, 64);
             if (gl > 0 && xd <= rd) { rd = xd; rx = xx; ry = xy; rz = xz; }
         }
+#pragma unroll 4
         for (uint32_t k = a0; k < a1; k++) {
             const float4 p = Ws[k];
             const float d = mid_dist(b, p.x, p.y, p.z);
@@ -464,7 +478,11 @@ __device__ __forceinline__ void add_box(const DynAddParams& P, int64_t g, int gl
         }
     }
     const bool newer = ck >= 0;
-    if (newer && gl == 0) P.keep[__float_as_uint(Ws[ck].w)] = 1u;
+    if (newer && gl == 0) {
+        const uint32_t win = __float_as_uint(Ws[ck].w);
+        P.keep[win] = 1u;
+        P.klist[atomicAdd(P.ctr + kDynKept, 1ull)] = win;
+    }
     unsigned long long deleted = 0;
     if (S.cnt > 0 && (newer || S.cnt > 1)) {
         group_box_points<G>(P, S.l, S.h, gl, W, [&](const float4 q) {
@@ -510,24 +528,16 @@ __global__ __launch_bounds__(64 * kBoxWaves) void k_add_box(DynAddParams P) {
 }
 static_assert(sizeof(GroupCells<64>) * kBoxWaves <= sizeof(GroupCells<16>) * (64 * kBoxWaves / 16), "LDS");
 
-__global__ void k_add_dlist(DynAddParams P) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P.n) return;
-    if (P.defer[i]) P.dlist[P.dpos[i]] = (uint32_t)i;
-    if (i == P.n - 1) P.ctr[kDynDeferred] = P.dpos[i] + P.defer[i];
-}
-
 // The deferred points in input order on one thread: exactly Add_Points' loop.
-__global__ void k_add_seq(DynAddParams P) {
-    if (blockIdx.x != 0 || threadIdx.x != 0 || P.ctr[kDynError]) return;
-    const uint32_t D = (uint32_t)P.ctr[kDynDeferred];
+// Returns the count of this pass's kept points (seq[0, ns), w = ~0 once deleted).
+__device__ uint32_t add_seq(const DynAddParams& P, const uint32_t* list, uint32_t D) {
     const float4* __restrict__ gp = reinterpret_cast<const float4*>(P.gpts);
     const float4* __restrict__ W = reinterpret_cast<const float4*>(P.W);
     float4* seq = reinterpret_cast<float4*>(P.seq);  // this pass's kept points (x, y, z, input index)
     uint32_t ns = 0;
     unsigned long long events = 0, deleted = 0, amb = 0;
     for (uint32_t t = 0; t < D; t++) {
-        const uint32_t i = P.dlist[t];
+        const uint32_t i = list[t];
         const float4 p = W[i];
         const DBox b = dbox(P.keys[i], P.ds);
         int l[3] = {0, 0, 0}, h[3] = {-1, -1, -1};
@@ -598,19 +608,115 @@ __global__ void k_add_seq(DynAddParams P) {
     if (events) atomicAdd(P.ctr + kDynEvents, events);
     if (deleted) atomicAdd(P.ctr + kDynDeleted, deleted);
     if (amb) atomicAdd(P.ctr + kDynAmbig, amb);
+    return ns;
 }
 
-__global__ void k_add_append(const float4* __restrict__ W, const uint32_t* __restrict__ keep,
-                             const uint32_t* __restrict__ apos, int64_t n, int64_t base, float4* all, uint8_t* alive,
-                             unsigned long long* ctr) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || ctr[kDynError]) return;  // a refused batch changes nothing
-    if (i == n - 1) ctr[kDynAdded] = (unsigned long long)apos[i] + keep[i];
-    if (!keep[i]) return;
-    const float4 p = W[i];
-    const uint32_t id = (uint32_t)(base + (int64_t)apos[i]);
-    all[id] = make_float4(p.x, p.y, p.z, __uint_as_float(id));
-    alive[id] = 1;
+constexpr int kFinishThreads = 1024;
+constexpr uint32_t kFinishList = 2048;  // lists up to this long are ordered by rank counts in LDS
+// The positions i < n with flags[i] != 0 in input order: emit(i, rank); one
+// workgroup, four flags per thread per step.  Returns the count.
+template <class F>
+__device__ uint32_t block_compact(const uint32_t* __restrict__ flags, int64_t n, F&& emit) {
+    __shared__ uint32_t wsum[kFinishThreads / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t carry = 0;
+    for (int64_t c0 = 0; c0 < n; c0 += 4 * kFinishThreads) {
+        const int64_t i0 = c0 + 4 * (int64_t)threadIdx.x;
+        uint32_t f[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) f[u] = (i0 + u < n && flags[i0 + u]) ? 1u : 0u;
+        const uint32_t mine = f[0] + f[1] + f[2] + f[3];
+        uint32_t inc = mine;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t v = __shfl_up(inc, off, 64);
+            if (lane >= off) inc += v;
+        }
+        if (lane == 63) wsum[wave] = inc;
+        __syncthreads();
+        uint32_t woff = 0, tot = 0;
+        for (int w = 0; w < kFinishThreads / 64; w++) {
+            const uint32_t v = wsum[w];
+            woff += w < wave ? v : 0u;
+            tot += v;
+        }
+        uint32_t r = carry + woff + inc - mine;
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (f[u]) emit(i0 + u, r++);
+        carry += tot;
+        __syncthreads();
+    }
+    return carry;
+}
+// The input indices in `src` (m distinct values) in increasing order into dst (LDS ranks).
+__device__ __forceinline__ void block_rank_sort(const uint32_t* src, uint32_t m, uint32_t* dst) {
+    for (uint32_t t = threadIdx.x; t < m; t += kFinishThreads) {
+        const uint32_t v = src[t];
+        uint32_t r = 0;
+        for (uint32_t j = 0; j < m; j++) r += src[j] < v ? 1u : 0u;
+        dst[r] = v;
+    }
+}
+
+// After k_add_box, one workgroup: the deferred points in input order (ranked
+// in LDS, or compacted from the flags past kFinishList), Add_Points' loop over
+// them on one thread (add_seq), then the kept points in input order get the
+// next ids (k_add_box's box winners + the loop's), their coordinates and
+// alive flags; ctr[kDynAdded] the count.  Without downsampling every point is
+// kept in input order.
+__global__ __launch_bounds__(kFinishThreads) void k_add_finish(DynAddParams P, float4* all, uint8_t* alive) {
+    __shared__ uint32_t A[kFinishList], B[kFinishList];
+    __shared__ uint32_t ns_s, nk_s;
+    if (P.ctr[kDynError]) return;  // a refused batch changes nothing (block-uniform)
+    const float4* __restrict__ W = reinterpret_cast<const float4*>(P.W);
+    auto put = [&](uint32_t i, uint32_t r) {
+        const uint32_t id = (uint32_t)(P.base + (int64_t)r);
+        const float4 p = W[i];
+        all[id] = make_float4(p.x, p.y, p.z, __uint_as_float(id));
+        alive[id] = 1;
+    };
+    if (!P.downsample) {
+        for (int64_t i = threadIdx.x; i < P.n; i += kFinishThreads) put((uint32_t)i, (uint32_t)i);
+        if (threadIdx.x == 0) P.ctr[kDynAdded] = (unsigned long long)P.n;
+        return;
+    }
+    // the deferred points in input order
+    const uint32_t D = (uint32_t)P.ctr[kDynDeferred];
+    const uint32_t* list = B;
+    if (D <= kFinishList) {
+        for (uint32_t t = threadIdx.x; t < D; t += kFinishThreads) A[t] = P.dlist_u[t];
+        __syncthreads();
+        block_rank_sort(A, D, B);
+    } else {
+        block_compact(P.defer, P.n, [&](int64_t i, uint32_t r) { P.dlist[r] = (uint32_t)i; });
+        list = P.dlist;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) ns_s = D ? add_seq(P, list, D) : 0u;
+    __syncthreads();
+    // the kept points in input order: the box winners, then the loop's survivors
+    const uint32_t nb = (uint32_t)P.ctr[kDynKept], ns = ns_s;
+    if (threadIdx.x == 0) nk_s = nb;
+    __syncthreads();
+    const float4* seq = reinterpret_cast<const float4*>(P.seq);
+    bool fits = nb + ns <= kFinishList;
+    if (fits) {
+        for (uint32_t t = threadIdx.x; t < nb; t += kFinishThreads) A[t] = P.klist[t];
+        for (uint32_t t = threadIdx.x; t < ns; t += kFinishThreads) {
+            const uint32_t qi = __float_as_uint(seq[t].w);
+            if (qi != 0xFFFFFFFFu) A[atomicAdd(&nk_s, 1u)] = qi;
+        }
+        __syncthreads();
+        const uint32_t K = nk_s;
+        block_rank_sort(A, K, B);
+        __syncthreads();
+        for (uint32_t t = threadIdx.x; t < K; t += kFinishThreads) put(B[t], t);
+        if (threadIdx.x == 0) P.ctr[kDynAdded] = K;
+    } else {
+        const uint32_t K = block_compact(P.keep, P.n, [&](int64_t i, uint32_t r) { put((uint32_t)i, r); });
+        if (threadIdx.x == 0) P.ctr[kDynAdded] = K;
+    }
 }
 
 // ------------------------------------------------------ grid rebuild ------
@@ -659,6 +765,181 @@ __global__ void k_dyn_cellkeys(const float4* __restrict__ all, const uint8_t* __
     bool bad = false;
     keys[id] = cell_key_of(all[id], ox, oy, oz, inv, bad);
     if (bad) atomicOr(ctr + kDynError, 4ull);
+}
+
+// ---- one-launch exclusive scan (decoupled look-back) with fused input / output ----
+// Tiles of kScanTile values; a tile takes its number from a ticket counter
+// (tiles are claimed in the order they run, so a tile only waits on tiles
+// that are running or done), publishes its aggregate, looks back over the
+// tiles before it (64 at a time, one wave) for their aggregates up to the
+// nearest published prefix, then publishes its own prefix.  Status words:
+// value (bits 0-31), flag (32-33: 1 aggregate, 2 prefix), the call's epoch
+// (34-63), so the status array is never cleared.  A look-back that waits
+// ~seconds gives up and sets ctr bit 64 (the caller fails the call).
+constexpr int kScanThreads = 256, kScanItems = 8, kScanTile = kScanThreads * kScanItems;
+template <class T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* gptr_i(T* p) {
+    return (__attribute__((address_space(1))) T*)p;
+}
+struct ScanState {
+    unsigned long long* ticket;  // tickets issued so far (device)
+    unsigned long long base;     // the tickets issued before this call
+    unsigned long long* status;  // per tile
+    unsigned long long epoch;    // this call's (30 bits)
+    unsigned long long* err;     // ctr + kDynError
+};
+__device__ __forceinline__ unsigned long long scan_word(unsigned long long epoch, unsigned flag, uint32_t v) {
+    return (epoch << 34) | ((unsigned long long)flag << 32) | v;
+}
+template <int ITEMS = kScanItems, class In, class Out>
+__device__ __forceinline__ void block_scan_lookback(int64_t n, const ScanState& S, In&& in, Out&& out) {
+    __shared__ uint32_t wsum[kScanThreads / 64];
+    __shared__ uint32_t s_tile, s_prefix;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (threadIdx.x == 0) {
+        const unsigned long long t = atomicAdd(S.ticket, 1ull) - S.base;
+        s_tile = t < gridDim.x ? (uint32_t)t : 0xFFFFFFFFu;
+        if (t >= gridDim.x) atomicOr(S.err, 64ull);  // (tickets out of step: never expected)
+    }
+    __syncthreads();
+    if (s_tile == 0xFFFFFFFFu) return;
+    const int64_t tile = s_tile;
+    const int64_t i0 = tile * (kScanThreads * ITEMS) + (int64_t)threadIdx.x * ITEMS;
+    uint32_t v[ITEMS], mine = 0;
+#pragma unroll
+    for (int u = 0; u < ITEMS; u++) {
+        v[u] = i0 + u < n ? in(i0 + u) : 0u;
+        mine += v[u];
+    }
+    uint32_t inc = mine;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += t;
+    }
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    uint32_t woff = 0, agg = 0;
+#pragma unroll
+    for (int w = 0; w < kScanThreads / 64; w++) {
+        woff += w < wave ? wsum[w] : 0u;
+        agg += wsum[w];
+    }
+    if (wave == 0) {
+        auto* st = gptr_i(S.status);
+        if (tile == 0) {
+            if (lane == 0) {
+                __hip_atomic_store(st, scan_word(S.epoch, 2, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                s_prefix = 0u;
+            }
+        } else {
+            if (lane == 0)
+                __hip_atomic_store(st + tile, scan_word(S.epoch, 1, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            uint32_t prefix = 0;
+            int64_t hi = tile - 1;  // look at tiles hi, hi-1, ... (lane j: hi - j)
+            int spins = 0;
+            for (;;) {
+                const int64_t t = hi - lane;
+                unsigned long long w = scan_word(S.epoch, 2, 0);  // (before tile 0: a zero prefix)
+                if (t >= 0) w = __hip_atomic_load(st + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const bool ready = (w >> 34) == S.epoch && ((w >> 32) & 3ull) != 0;
+                if (__ballot(!ready)) {  // some tile of the window has not published: wait
+                    if (++spins > (1 << 22)) {
+                        if (lane == 0) atomicOr(S.err, 64ull);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                const unsigned long long pref = __ballot(((w >> 32) & 3ull) == 2);
+                const int stop = pref ? __builtin_ctzll(pref) : 64;  // the nearest tile with a prefix
+                uint32_t x = lane <= stop ? (uint32_t)w : 0u;
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off, 64);
+                prefix += x;
+                if (pref) break;
+                hi -= 64;
+                spins = 0;
+            }
+            if (lane == 0) {
+                __hip_atomic_store(st + tile, scan_word(S.epoch, 2, prefix + agg), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                s_prefix = prefix;
+            }
+        }
+    }
+    __syncthreads();
+    uint32_t r = s_prefix + woff + inc - mine;
+#pragma unroll
+    for (int u = 0; u < ITEMS; u++) {
+        if (i0 + u < n) out(i0 + u, r, v[u]);
+        r += v[u];
+    }
+}
+// rank[i] = survivors of the old grid before i (i <= na_old; flag = alive[id of gpts[i]]).
+__global__ __launch_bounds__(kScanThreads) void k_scan_flags(const float4* __restrict__ gpts, int64_t na_old,
+                                                             const uint8_t* __restrict__ alive, uint32_t* rank,
+                                                             ScanState S) {
+    block_scan_lookback(
+        na_old + 1, S,
+        [&](int64_t i) { return i < na_old ? (uint32_t)alive[__float_as_uint(gpts[i].w)] : 0u; },
+        [&](int64_t i, uint32_t r, uint32_t) { rank[i] = r; });
+}
+// Runs of equal keys: starts[run] = first position, starts[runs] = n, *nruns = runs.
+__global__ __launch_bounds__(kScanThreads) void k_scan_runs(const unsigned long long* __restrict__ keys, int64_t n,
+                                                            uint32_t* starts, unsigned long long* nruns, ScanState S) {
+    block_scan_lookback(
+        n, S, [&](int64_t i) { return (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u; },
+        [&](int64_t i, uint32_t r, uint32_t h) {
+            if (h) starts[r] = (uint32_t)i;
+            if (i == n - 1) {
+                starts[r + h] = (uint32_t)n;
+                *nruns = r + h;
+            }
+        });
+}
+// runid[k] = heads before k (Add_Points' box runs).
+__global__ __launch_bounds__(kScanThreads) void k_scan_u32(const uint32_t* __restrict__ in, int64_t n, uint32_t* out,
+                                                           ScanState S) {
+    block_scan_lookback(n, S, [&](int64_t i) { return in[i]; }, [&](int64_t i, uint32_t r, uint32_t) { out[i] = r; });
+}
+
+// Add_Points' box runs in one launch: the sorted points' run heads in (with the
+// points in box order into Ws, the 64-bit keys, the wrapped-key clash check of
+// k_add_heads), starts[run] / the run count / the crowded-box list out (a run
+// is crowded when the key kBoxSmall positions on is still its own).
+constexpr int kBoxScanItems = 2;  // (the input gathers a point per item: fewer in sequence per thread)
+__global__ __launch_bounds__(kScanThreads) void k_scan_boxes(DynAddParams P, ScanState S) {
+    const float4* __restrict__ W = reinterpret_cast<const float4*>(P.W);
+    block_scan_lookback<kBoxScanItems>(
+        P.n, S,
+        [&](int64_t k) {
+            const uint32_t i = P.svals[k];
+            bool head;
+            if (P.skeys32) {
+                const unsigned long long key = P.keys[i];
+                head = k == 0 || P.skeys32[k] != P.skeys32[k - 1];
+                if (!head && P.keys[P.svals[k - 1]] != key) atomicOr(P.ctr + kDynError, 32ull);
+                P.skeys_w[k] = key;
+            } else {
+                head = k == 0 || P.skeys[k] != P.skeys[k - 1];
+            }
+            const float4 p = W[i];
+            reinterpret_cast<float4*>(P.Ws)[k] = make_float4(p.x, p.y, p.z, __uint_as_float(i));
+            return head ? 1u : 0u;
+        },
+        [&](int64_t k, uint32_t r, uint32_t h) {
+            if (h) {
+                P.starts[r] = (uint32_t)k;
+                const int64_t e = k + kBoxSmall;
+                if (e < P.n && (P.skeys32 ? P.skeys32[e] == P.skeys32[k] : P.skeys[e] == P.skeys[k]))
+                    P.bigs[atomicAdd(P.ctr + kDynBig, 1ull)] = r;
+            }
+            if (k == P.n - 1) {
+                P.starts[r + h] = (uint32_t)P.n;
+                P.ctr[kDynRuns] = r + h;
+            }
+        });
 }
 
 // ---- the grid merged instead of re-sorted (dyn_rebuild's incremental path) ----
@@ -1025,15 +1306,11 @@ int launch_add_group(const DynAddParams& p, void* stream) {
                        0, (hipStream_t)stream, p);
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
-int launch_add_dlist(const DynAddParams& p, void* stream) { DYN_LAUNCH(k_add_dlist, p.n, p); }
-int launch_add_seq(const DynAddParams& p, void* stream) {
-    hipLaunchKernelGGL(k_add_seq, dim3(1), dim3(64), 0, (hipStream_t)stream, p);
+int launch_add_finish(const DynAddParams& p, float* all, uint8_t* alive, void* stream) {
+    if (p.n <= 0) return LIVO_OK;
+    hipLaunchKernelGGL(k_add_finish, dim3(1), dim3(kFinishThreads), 0, (hipStream_t)stream, p,
+                       reinterpret_cast<float4*>(all), alive);
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
-}
-int launch_add_append(const float* W, const uint32_t* keep, const uint32_t* apos, int64_t n, int64_t base, float* all,
-                      uint8_t* alive, unsigned long long* ctr, void* stream) {
-    DYN_LAUNCH(k_add_append, n, reinterpret_cast<const float4*>(W), keep, apos, n, base, reinterpret_cast<float4*>(all),
-               alive, ctr);
 }
 int launch_dyn_seed(const float* gpts, int64_t M, float* all, uint8_t* alive, void* stream) {
     DYN_LAUNCH(k_dyn_seed, M, reinterpret_cast<const float4*>(gpts), M, reinterpret_cast<float4*>(all), alive);
@@ -1068,6 +1345,55 @@ int launch_dyn_newsort(const float* all, const uint8_t* alive, int64_t m, const 
                        reinterpret_cast<const float4*>(all),
                        alive, m, org[0], org[1], org[2], inv, skeys, svals, ctr);
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+static ScanState scan_state(const ScanCtx& sc, int64_t tiles) {
+    ScanState S;
+    S.ticket = sc.ticket;
+    S.base = sc.issued;
+    S.status = sc.status;
+    S.epoch = sc.epoch & ((1ull << 30) - 1ull);
+    S.err = sc.err;
+    return S;
+}
+static int scan_launch_check(ScanCtx& sc, int64_t tiles) {
+    if (hipGetLastError() != hipSuccess) return LIVO_E_HIP;  // (no tickets taken)
+    sc.issued += (unsigned long long)tiles;
+    sc.epoch++;
+    return LIVO_OK;
+}
+int scan_tiles(int64_t n) { return (int)((n + kScanThreads * kBoxScanItems - 1) / (kScanThreads * kBoxScanItems)); }
+int launch_scan_flags(ScanCtx& sc, const float* gpts, int64_t na_old, const uint8_t* alive, uint32_t* rank,
+                      void* stream) {
+    const int64_t tiles = (na_old + 1 + kScanTile - 1) / kScanTile;
+    if (tiles > sc.status_cap) return LIVO_E_RANGE;
+    hipLaunchKernelGGL(k_scan_flags, dim3((unsigned)tiles), dim3(kScanThreads), 0, (hipStream_t)stream,
+                       reinterpret_cast<const float4*>(gpts), na_old, alive, rank, scan_state(sc, tiles));
+    return scan_launch_check(sc, tiles);
+}
+int launch_scan_runs(ScanCtx& sc, const unsigned long long* keys, int64_t n, uint32_t* starts,
+                     unsigned long long* nruns, void* stream) {
+    if (n <= 0) return LIVO_OK;
+    const int64_t tiles = (n + kScanTile - 1) / kScanTile;
+    if (tiles > sc.status_cap) return LIVO_E_RANGE;
+    hipLaunchKernelGGL(k_scan_runs, dim3((unsigned)tiles), dim3(kScanThreads), 0, (hipStream_t)stream, keys, n, starts,
+                       nruns, scan_state(sc, tiles));
+    return scan_launch_check(sc, tiles);
+}
+int launch_scan_boxes(ScanCtx& sc, const DynAddParams& p, void* stream) {
+    if (p.n <= 0) return LIVO_OK;
+    const int64_t tile = kScanThreads * kBoxScanItems, tiles = (p.n + tile - 1) / tile;
+    if (tiles > sc.status_cap) return LIVO_E_RANGE;
+    hipLaunchKernelGGL(k_scan_boxes, dim3((unsigned)tiles), dim3(kScanThreads), 0, (hipStream_t)stream, p,
+                       scan_state(sc, tiles));
+    return scan_launch_check(sc, tiles);
+}
+int launch_scan_u32(ScanCtx& sc, const uint32_t* in, int64_t n, uint32_t* out, void* stream) {
+    if (n <= 0) return LIVO_OK;
+    const int64_t tiles = (n + kScanTile - 1) / kScanTile;
+    if (tiles > sc.status_cap) return LIVO_E_RANGE;
+    hipLaunchKernelGGL(k_scan_u32, dim3((unsigned)tiles), dim3(kScanThreads), 0, (hipStream_t)stream, in, n, out,
+                       scan_state(sc, tiles));
+    return scan_launch_check(sc, tiles);
 }
 int launch_dyn_merge(const DynMergeParams& p, void* stream) { DYN_LAUNCH(k_dyn_merge, p.na_old + p.m + 3, p); }
 int launch_cr_rho(const float* gpts, int64_t n, const float org[3], float h, uint32_t* rho_bits, uint32_t* iota,

@@ -159,6 +159,7 @@ struct DynDev {
     bool merge = true;               // LIVO_DYN_MERGE=0: always sort
     int64_t rebuilds_sorted = 0, rebuilds_merged = 0;
     int64_t wide_redos = 0;          // Add_Points batches redone with 64-bit box keys
+    ScanCtx scan;                    // the one-launch scans' ticket and status words
 };
 
 // One batch's staging and streams.  LaserMapping batches: slots packed at
@@ -1096,6 +1097,7 @@ static void dyn_free(DynDev& d) {
     dev_free(d.boxes); dev_free(d.ctr);  // (d.dirty lives in d.ctr's allocation)
     dev_free(d.rpts); dev_free(d.rpos); dev_free(d.dslots); dev_free(d.dpts);
     dev_free(d.dvslots); dev_free(d.dvidx); dev_free(d.gpts_alt);
+    dev_free(d.scan.ticket); dev_free(d.scan.status);
     d = DynDev{};
 }
 
@@ -1154,6 +1156,27 @@ static int dyn_add_scratch(livo_ctx* c, int64_t n) {
     return LIVO_OK;
 }
 
+// The one-launch scans' state for up to n values (status words cleared once;
+// every call tags its own with a new epoch).
+static int dyn_scan_ready(livo_ctx* c, int64_t n) {
+    ScanCtx& sc = c->dyn.scan;
+    sc.err = c->dyn.ctr + kDynError;
+    if (!sc.ticket) {
+        if (dev_alloc(&sc.ticket, 1)) return LIVO_E_OOM;
+        HIP_TRY(hipMemsetAsync(sc.ticket, 0, 8, c->stream));
+        sc.issued = 0;
+    }
+    const int64_t tiles = scan_tiles(n + 1) + 1;
+    if (sc.status_cap < tiles) {
+        const int64_t cap = tiles + (tiles >> 1) + 64;
+        dev_free(sc.status);
+        sc.status_cap = 0;
+        if (dev_alloc(&sc.status, (size_t)cap)) return LIVO_E_OOM;
+        HIP_TRY(hipMemsetAsync(sc.status, 0, (size_t)cap * 8, c->stream));
+        sc.status_cap = cap;
+    }
+    return LIVO_OK;
+}
 static int sort_u32(livo_ctx* c, const uint32_t* kin, uint32_t* kout, const uint32_t* vin, uint32_t* vout, int64_t n,
                     int bits) {
     size_t tb = 0;
@@ -1461,8 +1484,8 @@ static int dyn_rebuild_merge(livo_ctx* c) {
         rc = launch_dyn_cellkeys(d.all + 4 * g0, d.alive + g0, m, c->gorg, inv, d.keys, d.iota, d.ctr, c->stream);
         if (!rc) rc = sort_u64(c, d.keys, d.skeys, d.iota, d.svals, m);
     }
-    if (!rc) rc = launch_dyn_flags(c->gpts, na_old, d.alive, d.heads, c->stream);
-    if (!rc) rc = ivox_scan(c, d.heads, d.runid, na_old + 1);
+    if (!rc) rc = dyn_scan_ready(c, std::max(na_old, na) + 1);
+    if (!rc) rc = launch_scan_flags(d.scan, c->gpts, na_old, d.alive, d.runid, c->stream);
     if (rc) return rc;
     DynMergeParams P{};
     P.gpts = c->gpts; P.na_old = na_old; P.rank = d.runid; P.alive = d.alive;
@@ -1471,9 +1494,7 @@ static int dyn_rebuild_merge(livo_ctx* c) {
     std::memcpy(P.org, c->gorg, sizeof(P.org));
     P.inv = inv; P.ctr = d.ctr;
     rc = launch_dyn_merge(P, c->stream);
-    if (!rc && na > 0) rc = launch_run_heads(d.keys, na, d.heads, c->stream);
-    if (!rc && na > 0) rc = ivox_scan(c, d.heads, d.runid, na);
-    if (!rc && na > 0) rc = launch_dyn_runs(d.heads, d.runid, na, d.starts, d.ctr + kDynRuns, c->stream);
+    if (!rc && na > 0) rc = launch_scan_runs(d.scan, d.keys, na, d.starts, d.ctr + kDynRuns, c->stream);
     if (rc) return rc;
     const int64_t bound = std::max<int64_t>(std::min<int64_t>(na, d.cells + m), 1);
     int log2 = 4;
@@ -1492,6 +1513,7 @@ static int dyn_rebuild_merge(livo_ctx* c) {
     unsigned long long h[kDynCtrN];
     HIP_TRY(hipMemcpyAsync(h, d.ctr, sizeof(h), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    if (h[kDynError] & 64ull) return LIVO_E_HIP;  // a scan's look-back gave up
     if (h[kDynError] & (8ull | 16ull)) return kMergeRetry;  // (c->gpts untouched: the sort rebuilds from it)
     if (h[kDynError]) return LIVO_E_RANGE;
     std::swap(c->gpts, d.gpts_alt);
@@ -1549,7 +1571,8 @@ static int dyn_add(livo_ctx* c, int64_t n, float ds, bool downsample, livo_map_a
             P.heads = d.heads; P.runid = d.runid; P.starts = d.starts;
             P.defer = d.defer; P.dpos = d.dpos; P.dlist = d.dlist; P.keep = d.keep; P.seq = d.seq;
             P.dirty = d.dirty; P.dirty_cap = kDynDirtyCap; P.ctr = d.ctr;
-            P.bigs = d.dlist;  // (dlist is free from the sort until k_add_dlist)
+            P.bigs = d.dlist;  // (dlist is free from the sort until k_add_finish)
+            P.dlist_u = d.dpos; P.klist = d.apos;  // (dpos: free once k_add_heads has read the sorted keys)
             if (downsample && !wide) {  // (dlist / dpos are free until k_add_box)
                 P.keys32 = d.dlist; P.skeys32 = d.dpos; P.skeys_w = d.skeys;
             }
@@ -1561,20 +1584,16 @@ static int dyn_add(livo_ctx* c, int64_t n, float ds, bool downsample, livo_map_a
             if (downsample) {
                 if (P.keys32) rc = sort_u32(c, P.keys32, P.skeys32, d.iota, d.svals, n, 30);
                 else rc = sort_u64(c, d.keys, d.skeys, d.iota, d.svals, n);
-                if (!rc) rc = launch_add_heads(P, c->stream);
-                if (!rc) rc = ivox_scan(c, d.heads, d.runid, n);
-                if (!rc) rc = launch_add_starts(P, c->stream);
+                if (!rc) rc = dyn_scan_ready(c, n);
+                if (!rc) rc = launch_scan_boxes(d.scan, P, c->stream);
                 if (!rc) rc = launch_add_group(P, c->stream);
-                if (!rc) rc = ivox_scan(c, d.defer, d.dpos, n);
-                if (!rc) rc = launch_add_dlist(P, c->stream);
-                if (!rc) rc = launch_add_seq(P, c->stream);
             }
-            if (!rc) rc = ivox_scan(c, d.keep, d.apos, n);
-            if (!rc) rc = launch_add_append(d.W, d.keep, d.apos, n, d.n_ids, d.all, d.alive, d.ctr, c->stream);
+            if (!rc) rc = launch_add_finish(P, d.all, d.alive, c->stream);
             if (rc) return rc;
             HIP_TRY(hipMemcpyAsync(h, d.ctr, sizeof(h), hipMemcpyDeviceToHost, c->stream));
             HIP_TRY(hipStreamSynchronize(c->stream));
             if (h[kDynError] & 1ull) return LIVO_E_RANGE;  // nothing changed
+            if (h[kDynError] & 64ull) return LIVO_E_HIP;   // a scan's look-back gave up (nothing changed)
             if (!(h[kDynError] & 32ull) || wide) break;
             d.wide_redos++;
         }

@@ -577,7 +577,7 @@ int launch_vio_end(const VioParams& p, void* stream);
 // KD_TREE::Add_Points / Delete_Point_Boxes on the map's point set, then the
 // cell grid rebuilt from the surviving points.  Counters in DynAddParams::ctr:
 enum { kDynEvents = 0, kDynDeleted = 1, kDynAmbig = 2, kDynDeferred = 3, kDynError = 4, kDynDirty = 5,
-       kDynAbsMax = 6, kDynRuns = 7, kDynTomb = 8, kDynAliveCnt = 9, kDynAdded = 10, kDynBig = 11, kDynCtrN = 12 };
+       kDynAbsMax = 6, kDynRuns = 7, kDynTomb = 8, kDynAliveCnt = 9, kDynAdded = 10, kDynBig = 11, kDynKept = 12, kDynCtrN = 13 };
 constexpr uint32_t kDynDirtyCap = 4096;  // dirty-box set slots; past half full every point takes the sequential pass
 constexpr int kDynCtrPad = 16;           // ctr, then the dirty-box set (one allocation, one clear)
 static_assert(kDynCtrN <= kDynCtrPad, "ctr overlaps the dirty-box set");
@@ -613,6 +613,8 @@ struct DynAddParams {
     uint32_t* skeys32;          // n: sorted
     unsigned long long* skeys_w;  // = skeys (k_add_heads writes the 64-bit keys in sorted order)
     uint32_t* bigs;             // the crowded boxes (runs), listed by k_add_starts (count: ctr[kDynBig])
+    uint32_t* dlist_u;          // the deferred points, unordered (k_add_box; count ctr[kDynDeferred])
+    uint32_t* klist;            // the box winners, unordered (k_add_box; count ctr[kDynKept])
 };
 struct DynWorldParams {
     const float* pts;           // scan body points (stored order, 4 floats each)
@@ -627,10 +629,7 @@ int launch_add_prep(const DynAddParams& p, void* stream);
 int launch_add_heads(const DynAddParams& p, void* stream);
 int launch_add_starts(const DynAddParams& p, void* stream);
 int launch_add_group(const DynAddParams& p, void* stream);
-int launch_add_dlist(const DynAddParams& p, void* stream);
-int launch_add_seq(const DynAddParams& p, void* stream);
-int launch_add_append(const float* W, const uint32_t* keep, const uint32_t* apos, int64_t n, int64_t base, float* all,
-                      uint8_t* alive, unsigned long long* ctr, void* stream);
+int launch_add_finish(const DynAddParams& p, float* all, uint8_t* alive, void* stream);
 int launch_dyn_seed(const float* gpts, int64_t M, float* all, uint8_t* alive, void* stream);
 int launch_dyn_world(const DynWorldParams& p, void* stream);
 int launch_dyn_cellkeys(const float* all, const uint8_t* alive, int64_t n_ids, const float* org, float inv,
@@ -660,6 +659,26 @@ struct DynMergeParams {
     unsigned long long* ctr;
 };
 int launch_dyn_flags(const float* gpts, int64_t na_old, const uint8_t* alive, uint32_t* flags, void* stream);
+// One-launch exclusive scans (decoupled look-back, ikd_incr_kernels.hip): the
+// context's ticket counter and status words (never cleared: each call tags
+// its words with a new epoch).
+struct ScanCtx {
+    unsigned long long* ticket = nullptr;  // device: tickets issued
+    unsigned long long* status = nullptr;  // device: status_cap words
+    int64_t status_cap = 0;
+    unsigned long long issued = 0, epoch = 1;
+    unsigned long long* err = nullptr;     // where a look-back that gives up sets bit 64
+};
+int scan_tiles(int64_t n);
+// rank[i] = old-grid survivors before i, i <= na_old (k_dyn_flags + a scan)
+int launch_scan_flags(ScanCtx& sc, const float* gpts, int64_t na_old, const uint8_t* alive, uint32_t* rank,
+                      void* stream);
+// runs of equal keys -> starts, *nruns (k_run_heads + a scan + k_dyn_runs)
+int launch_scan_runs(ScanCtx& sc, const unsigned long long* keys, int64_t n, uint32_t* starts,
+                     unsigned long long* nruns, void* stream);
+int launch_scan_u32(ScanCtx& sc, const uint32_t* in, int64_t n, uint32_t* out, void* stream);
+// Add_Points' box runs: k_add_heads + a scan + k_add_starts in one launch
+int launch_scan_boxes(ScanCtx& sc, const DynAddParams& p, void* stream);
 constexpr int kNewSortMax = 2048;  // k_dyn_newsort: new ids keyed and sorted in one workgroup
 int launch_dyn_newsort(const float* all, const uint8_t* alive, int64_t m, const float* org, float inv,
                        unsigned long long* skeys, uint32_t* svals, unsigned long long* ctr, void* stream);
