@@ -211,49 +211,9 @@ __global__ void k_add_prep(DynAddParams P) {
                     dirty_insert(P, pack_key(j[0] + o0 - 1, j[1] + o1 - 1, j[2] + o2 - 1));
 }
 
-// Runs of equal box keys in sorted order.  With the wrapped 30-bit keys two
-// boxes 1024 boxes apart on every axis they differ on would share a run: such a
-// pair is adjacent somewhere in the run, is found here, and the batch is redone
-// with the 64-bit keys (ctr bit 32; the passes that change the map skip it).
-__global__ void k_add_heads(DynAddParams P) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= P.n) return;
-    const uint32_t i = P.svals[k];
-    if (P.skeys32) {
-        const unsigned long long key = P.keys[i];
-        const bool head = k == 0 || P.skeys32[k] != P.skeys32[k - 1];
-        if (!head && P.keys[P.svals[k - 1]] != key) atomicOr(P.ctr + kDynError, 32ull);
-        P.heads[k] = head ? 1u : 0u;
-        P.skeys_w[k] = key;
-    } else {
-        P.heads[k] = (k == 0 || P.skeys[k] != P.skeys[k - 1]) ? 1u : 0u;
-    }
-    // the points in box order: k_add_box then walks a box's sequence with contiguous loads
-    const float4 p = reinterpret_cast<const float4*>(P.W)[i];
-    reinterpret_cast<float4*>(P.Ws)[k] = make_float4(p.x, p.y, p.z, __uint_as_float(i));
-}
-
 constexpr int kBoxWaves = 4;       // k_add_box: waves per block
 constexpr uint32_t kBoxSmall = 64;  // boxes with at most this many new points: 16-lane groups
 constexpr int kBigBlocks = 64;      // k_add_box's first blocks: a wave per crowded box
-
-__global__ void k_add_starts(DynAddParams P) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= P.n) return;
-    if (P.heads[k]) {
-        const uint32_t r = P.runid[k];
-        P.starts[r] = (uint32_t)k;
-        // a crowded box (more than kBoxSmall new points) for k_add_box's waves: position
-        // k + kBoxSmall still in this run (runid = heads before: r + 1 inside the run)
-        const int64_t e = k + kBoxSmall;
-        if (e < P.n && !P.heads[e] && P.runid[e] == r + 1u) P.bigs[atomicAdd(P.ctr + kDynBig, 1ull)] = r;
-    }
-    if (k == P.n - 1) {
-        const uint32_t runs = P.runid[k] + P.heads[k];
-        P.starts[runs] = (uint32_t)P.n;
-        P.ctr[kDynRuns] = runs;
-    }
-}
 
 // A box's stored points (Search_by_range) by a group of G lanes (16: most
 // boxes hold a few stored points and new points; 64: the crowded boxes): the
@@ -505,7 +465,7 @@ __device__ __forceinline__ void add_box(const DynAddParams& P, int64_t g, int gl
     }
 }
 // One launch: the first kBigBlocks blocks take the crowded boxes (listed by
-// k_add_starts), a wave each; the others the rest, a 16-lane group each.
+// k_scan_boxes), a wave each; the others the rest, a 16-lane group each.
 __global__ __launch_bounds__(64 * kBoxWaves) void k_add_box(DynAddParams P) {
     constexpr int G = 16, kGroups = 64 * kBoxWaves / G;
     __shared__ GroupCells<G> cells[kGroups];
@@ -898,15 +858,10 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_runs(const unsigned long 
             }
         });
 }
-// runid[k] = heads before k (Add_Points' box runs).
-__global__ __launch_bounds__(kScanThreads) void k_scan_u32(const uint32_t* __restrict__ in, int64_t n, uint32_t* out,
-                                                           ScanState S) {
-    block_scan_lookback(n, S, [&](int64_t i) { return in[i]; }, [&](int64_t i, uint32_t r, uint32_t) { out[i] = r; });
-}
 
 // Add_Points' box runs in one launch: the sorted points' run heads in (with the
 // points in box order into Ws, the 64-bit keys, the wrapped-key clash check of
-// k_add_heads), starts[run] / the run count / the crowded-box list out (a run
+// the old k_add_heads), starts[run] / the run count / the crowded-box list out (a run
 // is crowded when the key kBoxSmall positions on is still its own).
 constexpr int kBoxScanItems = 2;  // (the input gathers a point per item: fewer in sequence per thread)
 __global__ __launch_bounds__(kScanThreads) void k_scan_boxes(DynAddParams P, ScanState S) {
@@ -974,13 +929,6 @@ __global__ __launch_bounds__(256) void k_dyn_newsort(const float4* __restrict__ 
         skeys[r] = key;
         svals[r] = (uint32_t)i;
     }
-}
-// flags[i] = the old grid's point i is still alive (i < na_old), flags[na_old] = 0.
-__global__ void k_dyn_flags(const float4* __restrict__ gpts, int64_t na_old, const uint8_t* __restrict__ alive,
-                            uint32_t* flags) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i > na_old) return;
-    flags[i] = i < na_old ? (uint32_t)alive[__float_as_uint(gpts[i].w)] : 0u;
 }
 // The merged grid in (cell key, id) order: the old grid's survivors keep their
 // order and go before the new points of the same cell (their ids are smaller);
@@ -1296,8 +1244,6 @@ static inline dim3 grid_for(int64_t n) { return dim3((unsigned)((n + 255) / 256)
     } while (0)
 
 int launch_add_prep(const DynAddParams& p, void* stream) { DYN_LAUNCH(k_add_prep, p.n, p); }
-int launch_add_heads(const DynAddParams& p, void* stream) { DYN_LAUNCH(k_add_heads, p.n, p); }
-int launch_add_starts(const DynAddParams& p, void* stream) { DYN_LAUNCH(k_add_starts, p.n, p); }
 int launch_add_group(const DynAddParams& p, void* stream) {
     if (p.n <= 0) return LIVO_OK;
     const int64_t per_block = 64 * kBoxWaves / 16;  // runs <= n: a 16-lane group per box, at most 64k groups
@@ -1333,9 +1279,6 @@ int launch_dyn_runs(const uint32_t* heads, const uint32_t* runid, int64_t na, ui
 int launch_dyn_slots(const unsigned long long* skeys, const uint32_t* starts, int64_t cells, GridSlot* slots, int log2,
                      void* stream, const unsigned long long* dcells, unsigned long long* err) {
     DYN_LAUNCH(k_dyn_slots, cells, skeys, starts, cells, slots, log2, dcells, err);
-}
-int launch_dyn_flags(const float* gpts, int64_t na_old, const uint8_t* alive, uint32_t* flags, void* stream) {
-    DYN_LAUNCH(k_dyn_flags, na_old + 1, reinterpret_cast<const float4*>(gpts), na_old, alive, flags);
 }
 int launch_dyn_newsort(const float* all, const uint8_t* alive, int64_t m, const float* org, float inv,
                        unsigned long long* skeys, uint32_t* svals, unsigned long long* ctr, void* stream) {
@@ -1384,14 +1327,6 @@ int launch_scan_boxes(ScanCtx& sc, const DynAddParams& p, void* stream) {
     const int64_t tile = kScanThreads * kBoxScanItems, tiles = (p.n + tile - 1) / tile;
     if (tiles > sc.status_cap) return LIVO_E_RANGE;
     hipLaunchKernelGGL(k_scan_boxes, dim3((unsigned)tiles), dim3(kScanThreads), 0, (hipStream_t)stream, p,
-                       scan_state(sc, tiles));
-    return scan_launch_check(sc, tiles);
-}
-int launch_scan_u32(ScanCtx& sc, const uint32_t* in, int64_t n, uint32_t* out, void* stream) {
-    if (n <= 0) return LIVO_OK;
-    const int64_t tiles = (n + kScanTile - 1) / kScanTile;
-    if (tiles > sc.status_cap) return LIVO_E_RANGE;
-    hipLaunchKernelGGL(k_scan_u32, dim3((unsigned)tiles), dim3(kScanThreads), 0, (hipStream_t)stream, in, n, out,
                        scan_state(sc, tiles));
     return scan_launch_check(sc, tiles);
 }

@@ -1551,7 +1551,7 @@ static int dyn_add(livo_ctx* c, int64_t n, float ds, bool downsample, livo_map_a
         int rc = dyn_grow(c, d.n_ids + n);
         if (!rc) rc = dyn_sort_scratch(c, n + 1);
         if (rc) return rc;
-        // The box keys sort as 30-bit keys (10 bits per axis, wrapped): k_add_heads
+        // The box keys sort as 30-bit keys (10 bits per axis, wrapped): k_scan_boxes
         // finds two boxes sharing a wrapped key and the batch is redone with the
         // 64-bit keys (ctr bit 32: nothing changed).  LIVO_DYN_WIDE_KEYS=1: always 64-bit.
         static const bool wide_env = [] {
@@ -1572,7 +1572,7 @@ static int dyn_add(livo_ctx* c, int64_t n, float ds, bool downsample, livo_map_a
             P.defer = d.defer; P.dpos = d.dpos; P.dlist = d.dlist; P.keep = d.keep; P.seq = d.seq;
             P.dirty = d.dirty; P.dirty_cap = kDynDirtyCap; P.ctr = d.ctr;
             P.bigs = d.dlist;  // (dlist is free from the sort until k_add_finish)
-            P.dlist_u = d.dpos; P.klist = d.apos;  // (dpos: free once k_add_heads has read the sorted keys)
+            P.dlist_u = d.dpos; P.klist = d.apos;  // (dpos: free once k_scan_boxes has read the sorted keys)
             if (downsample && !wide) {  // (dlist / dpos are free until k_add_box)
                 P.keys32 = d.dlist; P.skeys32 = d.dpos; P.skeys_w = d.skeys;
             }

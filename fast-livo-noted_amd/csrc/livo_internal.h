@@ -611,8 +611,8 @@ struct DynAddParams {
     unsigned long long* ctr;    // kDynCtrN counters
     uint32_t* keys32;           // n: the box key wrapped to 10 bits per axis (null: sort the 64-bit keys)
     uint32_t* skeys32;          // n: sorted
-    unsigned long long* skeys_w;  // = skeys (k_add_heads writes the 64-bit keys in sorted order)
-    uint32_t* bigs;             // the crowded boxes (runs), listed by k_add_starts (count: ctr[kDynBig])
+    unsigned long long* skeys_w;  // = skeys (k_scan_boxes writes the 64-bit keys in sorted order)
+    uint32_t* bigs;             // the crowded boxes (runs), listed by k_scan_boxes (count: ctr[kDynBig])
     uint32_t* dlist_u;          // the deferred points, unordered (k_add_box; count ctr[kDynDeferred])
     uint32_t* klist;            // the box winners, unordered (k_add_box; count ctr[kDynKept])
 };
@@ -626,8 +626,6 @@ struct DynWorldParams {
     float* W;                   // n world points in caller order (feats_down_world)
 };
 int launch_add_prep(const DynAddParams& p, void* stream);
-int launch_add_heads(const DynAddParams& p, void* stream);
-int launch_add_starts(const DynAddParams& p, void* stream);
 int launch_add_group(const DynAddParams& p, void* stream);
 int launch_add_finish(const DynAddParams& p, float* all, uint8_t* alive, void* stream);
 int launch_dyn_seed(const float* gpts, int64_t M, float* all, uint8_t* alive, void* stream);
@@ -658,7 +656,6 @@ struct DynMergeParams {
     float inv;
     unsigned long long* ctr;
 };
-int launch_dyn_flags(const float* gpts, int64_t na_old, const uint8_t* alive, uint32_t* flags, void* stream);
 // One-launch exclusive scans (decoupled look-back, ikd_incr_kernels.hip): the
 // context's ticket counter and status words (never cleared: each call tags
 // its words with a new epoch).
@@ -670,14 +667,13 @@ struct ScanCtx {
     unsigned long long* err = nullptr;     // where a look-back that gives up sets bit 64
 };
 int scan_tiles(int64_t n);
-// rank[i] = old-grid survivors before i, i <= na_old (k_dyn_flags + a scan)
+// rank[i] = old-grid survivors before i, i <= na_old (the flags read in the scan)
 int launch_scan_flags(ScanCtx& sc, const float* gpts, int64_t na_old, const uint8_t* alive, uint32_t* rank,
                       void* stream);
 // runs of equal keys -> starts, *nruns (k_run_heads + a scan + k_dyn_runs)
 int launch_scan_runs(ScanCtx& sc, const unsigned long long* keys, int64_t n, uint32_t* starts,
                      unsigned long long* nruns, void* stream);
-int launch_scan_u32(ScanCtx& sc, const uint32_t* in, int64_t n, uint32_t* out, void* stream);
-// Add_Points' box runs: k_add_heads + a scan + k_add_starts in one launch
+// Add_Points' box runs: heads, a scan and starts in one launch
 int launch_scan_boxes(ScanCtx& sc, const DynAddParams& p, void* stream);
 constexpr int kNewSortMax = 2048;  // k_dyn_newsort: new ids keyed and sorted in one workgroup
 int launch_dyn_newsort(const float* all, const uint8_t* alive, int64_t m, const float* org, float inv,
