@@ -322,3 +322,24 @@ def test_add_points_wrapped_box_key_clash(ictx):
     _same_add(ictx.map_add_points(W2, ds), dm.add_points(W2, ds))
     _same_map(ictx, dm)
     assert ictx.map_rebuilds()[2] == r0 + 1
+
+
+def test_add_points_large_multi_tile(built):
+    """Scans of 60k points into a 400k-point map: the one-launch scans span more
+    than one 64-tile look-back window (k_scan_boxes ~118 tiles, the merged
+    rebuild's survivor ranks ~196), the crowded boxes take whole waves and the
+    kept list passes the LDS ranking's 2,048 (the in-order compaction): counts
+    and the map bit for bit the oracle's after every call, the merge path ran."""
+    import livo_amd
+    import oracle
+    from livo_amd import synth
+    m = synth.make_map(400_000)
+    dm = oracle.DynMap(m)
+    with livo_amd.Context(0, t_LI=synth.T_LI, max_iterations=4) as ctx:
+        ctx.map_build(m)
+        for k in range(3):
+            body, _, _ = synth.make_scan(60_000, 90 + k)
+            W = _world(body, synth.make_state(90 + k))
+            _same_add(ctx.map_add_points(W, 0.5), dm.add_points(W, 0.5))
+            _same_map(ctx, dm)
+        assert ctx.map_rebuilds()[1] >= 2
