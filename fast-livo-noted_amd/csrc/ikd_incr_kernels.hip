@@ -847,7 +847,9 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_flags(const float4* __res
 }
 // Runs of equal keys: starts[run] = first position, starts[runs] = n, *nruns = runs.
 __global__ __launch_bounds__(kScanThreads) void k_scan_runs(const unsigned long long* __restrict__ keys, int64_t n,
-                                                            uint32_t* starts, unsigned long long* nruns, ScanState S) {
+                                                            uint32_t* starts, unsigned long long* nruns, ScanState S,
+                                                            const unsigned long long* dn) {
+    if (dn) n = (int64_t)*dn;  // the count on the device (n: the bound the tiles were sized for)
     block_scan_lookback(
         n, S, [&](int64_t i) { return (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u; },
         [&](int64_t i, uint32_t r, uint32_t h) {
@@ -905,8 +907,18 @@ constexpr int kNewSortSplit = 8;
 __global__ __launch_bounds__(256) void k_dyn_newsort(const float4* __restrict__ all, const uint8_t* __restrict__ alive,
                                                      int64_t m, float ox, float oy, float oz, float inv,
                                                      unsigned long long* skeys, uint32_t* svals,
-                                                     unsigned long long* ctr) {
+                                                     unsigned long long* ctr, const unsigned long long* dm,
+                                                     unsigned long long* rerr) {
     __shared__ unsigned long long K[kNewSortMax];
+    if (dm) {  // the count on the device (Add_Points' kept points), m the grid's bound
+        const unsigned long long md = *dm;
+        if (md > (unsigned long long)kNewSortMax) {  // too many for one workgroup: the caller sorts instead
+            if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(rerr, 1ull);
+            return;
+        }
+        if ((int64_t)blockIdx.x * (256 / kNewSortSplit) >= (int64_t)md) return;
+        m = (int64_t)md;
+    }
     const int mm = (int)m;
     bool bad = false;
     for (int i = threadIdx.x; i < mm; i += blockDim.x)
@@ -941,6 +953,16 @@ __global__ void k_dyn_merge(DynMergeParams P) {
     float4* out = reinterpret_cast<float4*>(P.out);
     const float4* __restrict__ gp = reinterpret_cast<const float4*>(P.gpts);
     bool bad = false;
+    const int64_t m_grid = P.m;  // threads for the new points (the bound when the count is on the device)
+    if (P.dm) {  // the counts on the device: m = Add_Points' kept points, na = survivors + m
+        P.m = (int64_t)*P.dm;
+        P.na = (int64_t)P.rank[P.na_old] + P.m;
+        if (t == 0) *P.dna = (unsigned long long)P.na;
+        if (P.m > m_grid) {
+            if (t == 0) atomicOr(P.ctr + kDynError, 16ull);
+            return;
+        }
+    }
     if (t < P.na_old) {
         const float4 q = gp[t];
         if (!P.alive[__float_as_uint(q.w)]) return;
@@ -957,8 +979,9 @@ __global__ void k_dyn_merge(DynMergeParams P) {
         }
         out[pos] = q;
         P.okeys[pos] = key;
-    } else if (t < P.na_old + P.m) {
+    } else if (t < P.na_old + m_grid) {
         const int64_t j = t - P.na_old;
+        if (j >= P.m) return;
         const unsigned long long key = P.nkeys[j];
         if (key == ~0ull) return;  // (a dead new id sorts last)
         int64_t lo = 0, hi = P.na_old;
@@ -973,8 +996,8 @@ __global__ void k_dyn_merge(DynMergeParams P) {
         }
         out[pos] = reinterpret_cast<const float4*>(P.all)[P.g0 + P.nidx[j]];
         P.okeys[pos] = key;
-    } else if (t < P.na_old + P.m + 3) {  // chunk padding of k_knn_grid
-        out[P.na + (t - P.na_old - P.m)] = make_float4(0.f, 0.f, 0.f, 0.f);
+    } else if (t < P.na_old + m_grid + 3) {  // chunk padding of k_knn_grid
+        out[P.na + (t - P.na_old - m_grid)] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
 }
 
@@ -1281,12 +1304,16 @@ int launch_dyn_slots(const unsigned long long* skeys, const uint32_t* starts, in
     DYN_LAUNCH(k_dyn_slots, cells, skeys, starts, cells, slots, log2, dcells, err);
 }
 int launch_dyn_newsort(const float* all, const uint8_t* alive, int64_t m, const float* org, float inv,
-                       unsigned long long* skeys, uint32_t* svals, unsigned long long* ctr, void* stream) {
+                       unsigned long long* skeys, uint32_t* svals, unsigned long long* ctr, void* stream,
+                       const unsigned long long* dm, unsigned long long* rerr) {
     if (m <= 0) return LIVO_OK;
-    if (m > kNewSortMax) return LIVO_E_RANGE;
+    if (m > kNewSortMax) {
+        if (!dm) return LIVO_E_RANGE;
+        m = kNewSortMax;  // (a device count above it is flagged in rerr)
+    }
     hipLaunchKernelGGL(k_dyn_newsort, dim3((unsigned)((m * kNewSortSplit + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                       reinterpret_cast<const float4*>(all),
-                       alive, m, org[0], org[1], org[2], inv, skeys, svals, ctr);
+                       reinterpret_cast<const float4*>(all), alive, m, org[0], org[1], org[2], inv, skeys, svals, ctr,
+                       dm, rerr);
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 static ScanState scan_state(const ScanCtx& sc, int64_t tiles) {
@@ -1314,12 +1341,12 @@ int launch_scan_flags(ScanCtx& sc, const float* gpts, int64_t na_old, const uint
     return scan_launch_check(sc, tiles);
 }
 int launch_scan_runs(ScanCtx& sc, const unsigned long long* keys, int64_t n, uint32_t* starts,
-                     unsigned long long* nruns, void* stream) {
+                     unsigned long long* nruns, void* stream, const unsigned long long* dn) {
     if (n <= 0) return LIVO_OK;
     const int64_t tiles = (n + kScanTile - 1) / kScanTile;
     if (tiles > sc.status_cap) return LIVO_E_RANGE;
     hipLaunchKernelGGL(k_scan_runs, dim3((unsigned)tiles), dim3(kScanThreads), 0, (hipStream_t)stream, keys, n, starts,
-                       nruns, scan_state(sc, tiles));
+                       nruns, scan_state(sc, tiles), dn);
     return scan_launch_check(sc, tiles);
 }
 int launch_scan_boxes(ScanCtx& sc, const DynAddParams& p, void* stream) {

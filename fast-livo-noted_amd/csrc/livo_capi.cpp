@@ -159,6 +159,7 @@ struct DynDev {
     bool merge = true;               // LIVO_DYN_MERGE=0: always sort
     int64_t rebuilds_sorted = 0, rebuilds_merged = 0;
     int64_t wide_redos = 0;          // Add_Points batches redone with 64-bit box keys
+    int64_t rebuilds_fused = 0;      // merged rebuilds run in Add_Points' pass (one read-back)
     ScanCtx scan;                    // the one-launch scans' ticket and status words
 };
 
@@ -1435,10 +1436,11 @@ static int dyn_rebuild(livo_ctx* c) {
     int log2 = 4;
     while (((int64_t)1 << log2) < 4 * cells) log2++;  // load factor <= 1/4, as build_grid_map
     const int64_t table = (int64_t)1 << log2;
-    if (d.gslot_cap < table) {
+    if (d.gslot_cap < table) {  // (twice: headroom for Add_Points' fused rebuild)
         dev_free(c->gslots);
-        if (dev_alloc(&c->gslots, (size_t)table)) return LIVO_E_OOM;
-        d.gslot_cap = table;
+        d.gslot_cap = 0;
+        if (dev_alloc(&c->gslots, (size_t)(2 * table))) return LIVO_E_OOM;
+        d.gslot_cap = 2 * table;
     }
     rc = launch_ivox_clear(c->gslots, table, c->stream);
     if (!rc) rc = launch_dyn_slots(d.skeys, d.starts, cells, c->gslots, log2, c->stream);
@@ -1500,11 +1502,11 @@ static int dyn_rebuild_merge(livo_ctx* c) {
     int log2 = 4;
     while (((int64_t)1 << log2) < 4 * bound) log2++;  // load factor <= 1/4, as build_grid_map
     const int64_t table = (int64_t)1 << log2;
-    if (d.gslot_cap < table) {
+    if (d.gslot_cap < table) {  // (twice: the fused pass's bound, + kNewSortMax, fits the next calls)
         dev_free(c->gslots);
         d.gslot_cap = 0;
-        if (dev_alloc(&c->gslots, (size_t)table)) return LIVO_E_OOM;
-        d.gslot_cap = table;
+        if (dev_alloc(&c->gslots, (size_t)(2 * table))) return LIVO_E_OOM;
+        d.gslot_cap = 2 * table;
     }
     rc = launch_ivox_clear(c->gslots, table, c->stream);
     if (!rc && na > 0) rc = launch_dyn_slots(d.keys, d.starts, bound, c->gslots, log2, c->stream, d.ctr + kDynRuns,
@@ -1551,6 +1553,33 @@ static int dyn_add(livo_ctx* c, int64_t n, float ds, bool downsample, livo_map_a
         int rc = dyn_grow(c, d.n_ids + n);
         if (!rc) rc = dyn_sort_scratch(c, n + 1);
         if (rc) return rc;
+        // The merged grid rebuild runs in the same stream pass with the counts on
+        // the device (one read-back for both), when the grid covers every id, its
+        // cell edge stays, and the kept points fit k_dyn_newsort's workgroup (else,
+        // or on any flag, dyn_rebuild runs after the read-back as before).
+        const bool gh_stays = !(c->gh < d.min_gh || (d.max_gh > 0.f && c->gh > d.max_gh));
+        bool fused = downsample && d.merge && !d.runs && d.grid_ids == d.n_ids && d.cells >= 0 &&
+                     d.grid_gh == c->gh && gh_stays;
+        const int64_t na_old = c->map_points, g0 = d.n_ids, m_ub = std::min<int64_t>(n, kNewSortMax);
+        const int64_t na_ub = na_old + m_ub, cell_bound = std::max<int64_t>(std::min(na_ub, d.cells + m_ub), 1);
+        int log2 = 4;
+        while (((int64_t)1 << log2) < 4 * cell_bound) log2++;  // load factor <= 1/4, as build_grid_map
+        const int64_t table = (int64_t)1 << log2;
+        if (fused) {
+            rc = dyn_sort_scratch(c, std::max(n, na_ub) + 1);
+            if (!rc) rc = dyn_scan_ready(c, std::max(n, na_ub) + 1);
+            if (!rc && d.gpts_alt_cap < na_ub + 3) {
+                const int64_t cap = (na_ub + 3) + ((na_ub + 3) >> 2);
+                dev_free(d.gpts_alt);
+                d.gpts_alt_cap = 0;
+                if (dev_alloc(&d.gpts_alt, (size_t)cap * 4)) rc = LIVO_E_OOM;
+                else d.gpts_alt_cap = cap;
+            }
+            if (rc) return rc;
+            // the add reads the current table: a table that must grow takes the
+            // separate rebuild this time (which leaves headroom for the next)
+            if (d.gslot_cap < table) fused = false;
+        }
         // The box keys sort as 30-bit keys (10 bits per axis, wrapped): k_scan_boxes
         // finds two boxes sharing a wrapped key and the batch is redone with the
         // 64-bit keys (ctr bit 32: nothing changed).  LIVO_DYN_WIDE_KEYS=1: always 64-bit.
@@ -1589,9 +1618,35 @@ static int dyn_add(livo_ctx* c, int64_t n, float ds, bool downsample, livo_map_a
                 if (!rc) rc = launch_add_group(P, c->stream);
             }
             if (!rc) rc = launch_add_finish(P, d.all, d.alive, c->stream);
+            if (!rc && fused) {  // the merged rebuild on the device counts (kDynR*: its flags, runs, size)
+                unsigned long long* rctr = d.ctr + (kDynRErr - kDynError);  // (rctr + kDynError = ctr + kDynRErr)
+                const float inv = 1.0f / c->gh;
+                rc = launch_dyn_newsort(d.all + 4 * g0, d.alive + g0, m_ub, c->gorg, inv, d.skeys, d.svals, rctr,
+                                        c->stream, d.ctr + kDynAdded, d.ctr + kDynRErr);
+                if (!rc) rc = launch_scan_flags(d.scan, c->gpts, na_old, d.alive, d.runid, c->stream);
+                DynMergeParams M{};
+                M.gpts = c->gpts; M.na_old = na_old; M.rank = d.runid; M.alive = d.alive;
+                M.nkeys = d.skeys; M.nidx = d.svals; M.m = m_ub; M.g0 = g0; M.all = d.all;
+                M.out = d.gpts_alt; M.okeys = d.keys; M.na = na_ub;
+                std::memcpy(M.org, c->gorg, sizeof(M.org));
+                M.inv = inv; M.ctr = rctr;
+                M.dm = d.ctr + kDynAdded; M.dna = d.ctr + kDynRNa;
+                if (!rc) rc = launch_dyn_merge(M, c->stream);
+                if (!rc) rc = launch_scan_runs(d.scan, d.keys, na_ub, d.starts, d.ctr + kDynRRuns, c->stream,
+                                               d.ctr + kDynRNa);
+                if (!rc) rc = launch_ivox_clear(c->gslots, table, c->stream);
+                if (!rc) rc = launch_dyn_slots(d.keys, d.starts, cell_bound, c->gslots, log2, c->stream,
+                                               d.ctr + kDynRRuns, d.ctr + kDynRErr);
+            }
             if (rc) return rc;
             HIP_TRY(hipMemcpyAsync(h, d.ctr, sizeof(h), hipMemcpyDeviceToHost, c->stream));
             HIP_TRY(hipStreamSynchronize(c->stream));
+            if (fused && (h[kDynError] & (1ull | 64ull))) {
+                // the fused pass refilled the table from an unchanged point set, sized
+                // for its bound: rebuild it as the grid's own before returning
+                const int rrc = dyn_rebuild(c);
+                if (rrc) return rrc;
+            }
             if (h[kDynError] & 1ull) return LIVO_E_RANGE;  // nothing changed
             if (h[kDynError] & 64ull) return LIVO_E_HIP;   // a scan's look-back gave up (nothing changed)
             if (!(h[kDynError] & 32ull) || wide) break;
@@ -1599,7 +1654,10 @@ static int dyn_add(livo_ctx* c, int64_t n, float ds, bool downsample, livo_map_a
         }
         // k_add_prep checked the range of every box the later passes read, so
         // the group / sequential passes cannot fail once the map is modified
-        if (h[kDynError]) return LIVO_E_HIP;
+        if (h[kDynError]) {
+            if (fused) (void)dyn_rebuild(c);
+            return LIVO_E_HIP;
+        }
         const int64_t added = (int64_t)h[kDynAdded];
         st.events = (int64_t)h[kDynEvents];
         st.deleted = (int64_t)h[kDynDeleted];
@@ -1612,7 +1670,22 @@ static int dyn_add(livo_ctx* c, int64_t n, float ds, bool downsample, livo_map_a
         float amf;
         std::memcpy(&amf, &am, 4);
         d.cmax = std::max(d.cmax, amf);
-        rc = dyn_rebuild(c);
+        if (fused && h[kDynRErr] == 0 && (int64_t)h[kDynRNa] == d.n_alive && d.n_ids - g0 <= m_ub) {
+            std::swap(c->gpts, d.gpts_alt);
+            std::swap(d.gpts_cap, d.gpts_alt_cap);
+            c->glog2 = log2;
+            c->map_points = d.n_alive;
+            c->geps = (float)(32.0 * std::ldexp(1.0, -24) * (double)d.cmax + 1e-7);
+            c->grid_bytes = table * (int64_t)sizeof(GridSlot) + d.gpts_cap * 16;
+            for (auto& sc : c->scans) sc.searched = false;  // cached neighbours refer to the old map
+            d.grid_ids = d.n_ids;
+            d.cells = (int64_t)h[kDynRRuns];
+            d.rebuilds_merged++;
+            d.rebuilds_fused++;
+            rc = dyn_runs_update(c);
+        } else {
+            rc = dyn_rebuild(c);  // (c->gpts untouched by the fused pass)
+        }
         if (rc) return rc;
     }
     st.map_points = d.n_alive;
@@ -4397,10 +4470,11 @@ int livo_sync(livo_ctx* c) {
 
 }  // extern "C"
 
-extern "C" int livo_debug_map_rebuilds(livo_ctx* c, int64_t out[3]) {
+extern "C" int livo_debug_map_rebuilds(livo_ctx* c, int64_t out[4]) {
     if (!c || !out) return LIVO_E_INVALID;
     out[0] = c->dyn.rebuilds_sorted;
     out[1] = c->dyn.rebuilds_merged;
     out[2] = c->dyn.wide_redos;
+    out[3] = c->dyn.rebuilds_fused;
     return LIVO_OK;
 }

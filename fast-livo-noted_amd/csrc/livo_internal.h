@@ -577,7 +577,8 @@ int launch_vio_end(const VioParams& p, void* stream);
 // KD_TREE::Add_Points / Delete_Point_Boxes on the map's point set, then the
 // cell grid rebuilt from the surviving points.  Counters in DynAddParams::ctr:
 enum { kDynEvents = 0, kDynDeleted = 1, kDynAmbig = 2, kDynDeferred = 3, kDynError = 4, kDynDirty = 5,
-       kDynAbsMax = 6, kDynRuns = 7, kDynTomb = 8, kDynAliveCnt = 9, kDynAdded = 10, kDynBig = 11, kDynKept = 12, kDynCtrN = 13 };
+       kDynAbsMax = 6, kDynRuns = 7, kDynTomb = 8, kDynAliveCnt = 9, kDynAdded = 10, kDynBig = 11, kDynKept = 12,
+       kDynRErr = 13, kDynRRuns = 14, kDynRNa = 15, kDynCtrN = 16 };  // 13-15: the merged rebuild run with Add_Points
 constexpr uint32_t kDynDirtyCap = 4096;  // dirty-box set slots; past half full every point takes the sequential pass
 constexpr int kDynCtrPad = 16;           // ctr, then the dirty-box set (one allocation, one clear)
 static_assert(kDynCtrN <= kDynCtrPad, "ctr overlaps the dirty-box set");
@@ -655,6 +656,8 @@ struct DynMergeParams {
     float org[3];
     float inv;
     unsigned long long* ctr;
+    const unsigned long long* dm = nullptr;  // optional: m on the device (m above: the bound); na follows
+    unsigned long long* dna = nullptr;       // with dm: na written here
 };
 // One-launch exclusive scans (decoupled look-back, ikd_incr_kernels.hip): the
 // context's ticket counter and status words (never cleared: each call tags
@@ -672,12 +675,13 @@ int launch_scan_flags(ScanCtx& sc, const float* gpts, int64_t na_old, const uint
                       void* stream);
 // runs of equal keys -> starts, *nruns (k_run_heads + a scan + k_dyn_runs)
 int launch_scan_runs(ScanCtx& sc, const unsigned long long* keys, int64_t n, uint32_t* starts,
-                     unsigned long long* nruns, void* stream);
+                     unsigned long long* nruns, void* stream, const unsigned long long* dn = nullptr);
 // Add_Points' box runs: heads, a scan and starts in one launch
 int launch_scan_boxes(ScanCtx& sc, const DynAddParams& p, void* stream);
 constexpr int kNewSortMax = 2048;  // k_dyn_newsort: new ids keyed and sorted in one workgroup
 int launch_dyn_newsort(const float* all, const uint8_t* alive, int64_t m, const float* org, float inv,
-                       unsigned long long* skeys, uint32_t* svals, unsigned long long* ctr, void* stream);
+                       unsigned long long* skeys, uint32_t* svals, unsigned long long* ctr, void* stream,
+                       const unsigned long long* dm = nullptr, unsigned long long* rerr = nullptr);
 int launch_dyn_merge(const DynMergeParams& p, void* stream);
 int launch_dyn_delete_boxes(const float* all, uint8_t* alive, int64_t n_ids, const float* boxes, int64_t nb,
                             unsigned long long* cnt, void* stream);

@@ -332,10 +332,10 @@ class Context:
 
     def map_rebuilds(self) -> tuple:
         """(grid rebuilds by sorting every id, by merging the added ids, Add_Points batches
-        redone with 64-bit box keys) of the incremental map."""
-        out = (C.c_int64 * 3)()
+        redone with 64-bit box keys, merged rebuilds run inside Add_Points' pass) of the incremental map."""
+        out = (C.c_int64 * 4)()
         _check("livo_debug_map_rebuilds", self._L.livo_debug_map_rebuilds(self.h, out))
-        return int(out[0]), int(out[1]), int(out[2])
+        return int(out[0]), int(out[1]), int(out[2]), int(out[3])
 
     def map_info(self) -> dict:
         mi = MapInfo()

@@ -506,8 +506,9 @@ int livo_sync(livo_ctx* ctx);
 int livo_debug_ns_timeouts(unsigned long long* out);
 /* Diagnostics: the incremental map's grid rebuilds since the context was made,
  * out[0] by a sort of every id, out[1] by merging the added ids into the grid;
- * out[2] the Add_Points batches redone with 64-bit box keys (a wrapped-key clash). */
-int livo_debug_map_rebuilds(livo_ctx* ctx, int64_t out[3]);
+ * out[2] the Add_Points batches redone with 64-bit box keys (a wrapped-key clash),
+ * out[3] the merged rebuilds run inside Add_Points' pass (counted in out[1] too). */
+int livo_debug_map_rebuilds(livo_ctx* ctx, int64_t out[4]);
 
 #ifdef __cplusplus
 }
