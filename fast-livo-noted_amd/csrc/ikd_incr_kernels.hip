@@ -143,9 +143,21 @@ __device__ __forceinline__ bool dirty_has(const DynAddParams& P, unsigned long l
 }
 
 __global__ void k_add_prep(DynAddParams P) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t i = g;
     float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (i < P.n) p = reinterpret_cast<const float4*>(P.W)[i];
+    if (g < P.n) {
+        if (P.wpts) {  // map_incremental: the stored point g is caller point perm[g], to the world frame
+            const float4 b = reinterpret_cast<const float4*>(P.wpts)[g];
+            float wx, wy, wz;
+            world_point(P.wrot, P.wpos, P.R_LI, P.t_LI, b.x, b.y, b.z, wx, wy, wz);
+            i = P.wperm[g];
+            p = make_float4(wx, wy, wz, 0.f);
+            reinterpret_cast<float4*>(const_cast<float*>(P.W))[i] = p;
+        } else {
+            p = reinterpret_cast<const float4*>(P.W)[i];
+        }
+    }
     const float v[3] = {p.x, p.y, p.z};
     const float am = fmaxf(fmaxf(fabsf(p.x), fabsf(p.y)), fabsf(p.z));
     bool ok = am <= 1e30f;  // false for NaN / inf
@@ -156,14 +168,14 @@ __global__ void k_add_prep(DynAddParams P) {
         __shared__ uint32_t bmax;
         if (threadIdx.x == 0) bmax = 0u;
         __syncthreads();
-        uint32_t m = (i < P.n && ok) ? __float_as_uint(am) : 0u;
+        uint32_t m = (g < P.n && ok) ? __float_as_uint(am) : 0u;
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
         if ((threadIdx.x & 63) == 0 && m) atomicMax(&bmax, m);
         __syncthreads();
         if (threadIdx.x == 0 && bmax) atomicMax(P.ctr + kDynAbsMax, (unsigned long long)bmax);
     }
-    if (i >= P.n) return;
+    if (g >= P.n) return;
     P.iota[i] = (uint32_t)i;
     P.keep[i] = P.downsample ? 0u : 1u;  // without downsampling every point is added (:438-454)
     P.defer[i] = 0u;
@@ -689,14 +701,6 @@ __global__ void k_dyn_seed(const float4* __restrict__ gpts, int64_t M, float4* a
     alive[id] = 1;
 }
 
-__global__ void k_dyn_world(DynWorldParams P) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= P.n) return;
-    const float4 b = reinterpret_cast<const float4*>(P.pts)[k];
-    float wx, wy, wz;
-    world_point(P.slot->state.rot, P.slot->state.pos, P.R_LI, P.t_LI, b.x, b.y, b.z, wx, wy, wz);
-    reinterpret_cast<float4*>(P.W)[P.perm[k]] = make_float4(wx, wy, wz, 0.f);
-}
 
 // Cell key of a point (k_knn_grid's cell_of: floor((p - org) * inv) in float);
 // `bad` if outside the grid's key range (clamped).
@@ -839,7 +843,10 @@ __device__ __forceinline__ void block_scan_lookback(int64_t n, const ScanState& 
 // rank[i] = survivors of the old grid before i (i <= na_old; flag = alive[id of gpts[i]]).
 __global__ __launch_bounds__(kScanThreads) void k_scan_flags(const float4* __restrict__ gpts, int64_t na_old,
                                                              const uint8_t* __restrict__ alive, uint32_t* rank,
-                                                             ScanState S) {
+                                                             ScanState S, GridSlot* clr, int64_t clr_n) {
+    // (optional: the hash table the rebuild fills next, cleared here -- k_iv_clear's work)
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < clr_n; t += (int64_t)gridDim.x * blockDim.x)
+        clr[t] = GridSlot{kGridEmpty, 0u, 0u};
     block_scan_lookback(
         na_old + 1, S,
         [&](int64_t i) { return i < na_old ? (uint32_t)alive[__float_as_uint(gpts[i].w)] : 0u; },
@@ -1284,7 +1291,6 @@ int launch_add_finish(const DynAddParams& p, float* all, uint8_t* alive, void* s
 int launch_dyn_seed(const float* gpts, int64_t M, float* all, uint8_t* alive, void* stream) {
     DYN_LAUNCH(k_dyn_seed, M, reinterpret_cast<const float4*>(gpts), M, reinterpret_cast<float4*>(all), alive);
 }
-int launch_dyn_world(const DynWorldParams& p, void* stream) { DYN_LAUNCH(k_dyn_world, p.n, p); }
 int launch_dyn_cellkeys(const float* all, const uint8_t* alive, int64_t n_ids, const float* org, float inv,
                         unsigned long long* keys, uint32_t* vals, unsigned long long* ctr, void* stream) {
     DYN_LAUNCH(k_dyn_cellkeys, n_ids, reinterpret_cast<const float4*>(all), alive, n_ids, org[0], org[1], org[2], inv,
@@ -1333,11 +1339,12 @@ static int scan_launch_check(ScanCtx& sc, int64_t tiles) {
 }
 int scan_tiles(int64_t n) { return (int)((n + kScanThreads * kBoxScanItems - 1) / (kScanThreads * kBoxScanItems)); }
 int launch_scan_flags(ScanCtx& sc, const float* gpts, int64_t na_old, const uint8_t* alive, uint32_t* rank,
-                      void* stream) {
+                      void* stream, GridSlot* clr, int64_t clr_n) {
     const int64_t tiles = (na_old + 1 + kScanTile - 1) / kScanTile;
     if (tiles > sc.status_cap) return LIVO_E_RANGE;
     hipLaunchKernelGGL(k_scan_flags, dim3((unsigned)tiles), dim3(kScanThreads), 0, (hipStream_t)stream,
-                       reinterpret_cast<const float4*>(gpts), na_old, alive, rank, scan_state(sc, tiles));
+                       reinterpret_cast<const float4*>(gpts), na_old, alive, rank, scan_state(sc, tiles), clr,
+                       clr ? clr_n : (int64_t)0);
     return scan_launch_check(sc, tiles);
 }
 int launch_scan_runs(ScanCtx& sc, const unsigned long long* keys, int64_t n, uint32_t* starts,

@@ -1532,7 +1532,14 @@ static int dyn_rebuild_merge(livo_ctx* c) {
 }
 
 // Add_Points of the n points in d.W (filled by the caller).
-static int dyn_add(livo_ctx* c, int64_t n, float ds, bool downsample, livo_map_add_stats* out) {
+// world: map_incremental's scan and state (k_add_prep transforms the points into d.W), or null (d.W filled)
+struct DynWorldIn {
+    const float* pts;
+    const int32_t* perm;
+    const livo_state* state;
+};
+static int dyn_add(livo_ctx* c, int64_t n, float ds, bool downsample, livo_map_add_stats* out,
+                   const DynWorldIn* world = nullptr) {
     DynDev& d = c->dyn;
     // Add_Points' downsampling leaves one point per box of edge ds where the
     // scans pass: the cell walk's grid (rebuilt after this change) takes cells
@@ -1600,6 +1607,13 @@ static int dyn_add(livo_ctx* c, int64_t n, float ds, bool downsample, livo_map_a
             P.heads = d.heads; P.runid = d.runid; P.starts = d.starts;
             P.defer = d.defer; P.dpos = d.dpos; P.dlist = d.dlist; P.keep = d.keep; P.seq = d.seq;
             P.dirty = d.dirty; P.dirty_cap = kDynDirtyCap; P.ctr = d.ctr;
+            if (world) {
+                P.wpts = world->pts; P.wperm = world->perm;
+                std::memcpy(P.wrot, world->state->rot, sizeof(P.wrot));
+                std::memcpy(P.wpos, world->state->pos, sizeof(P.wpos));
+                std::memcpy(P.R_LI, c->params.R_LI, sizeof(P.R_LI));
+                std::memcpy(P.t_LI, c->params.t_LI, sizeof(P.t_LI));
+            }
             P.bigs = d.dlist;  // (dlist is free from the sort until k_add_finish)
             P.dlist_u = d.dpos; P.klist = d.apos;  // (dpos: free once k_scan_boxes has read the sorted keys)
             if (downsample && !wide) {  // (dlist / dpos are free until k_add_box)
@@ -1623,7 +1637,7 @@ static int dyn_add(livo_ctx* c, int64_t n, float ds, bool downsample, livo_map_a
                 const float inv = 1.0f / c->gh;
                 rc = launch_dyn_newsort(d.all + 4 * g0, d.alive + g0, m_ub, c->gorg, inv, d.skeys, d.svals, rctr,
                                         c->stream, d.ctr + kDynAdded, d.ctr + kDynRErr);
-                if (!rc) rc = launch_scan_flags(d.scan, c->gpts, na_old, d.alive, d.runid, c->stream);
+                if (!rc) rc = launch_scan_flags(d.scan, c->gpts, na_old, d.alive, d.runid, c->stream, c->gslots, table);
                 DynMergeParams M{};
                 M.gpts = c->gpts; M.na_old = na_old; M.rank = d.runid; M.alive = d.alive;
                 M.nkeys = d.skeys; M.nidx = d.svals; M.m = m_ub; M.g0 = g0; M.all = d.all;
@@ -1634,7 +1648,6 @@ static int dyn_add(livo_ctx* c, int64_t n, float ds, bool downsample, livo_map_a
                 if (!rc) rc = launch_dyn_merge(M, c->stream);
                 if (!rc) rc = launch_scan_runs(d.scan, d.keys, na_ub, d.starts, d.ctr + kDynRRuns, c->stream,
                                                d.ctr + kDynRNa);
-                if (!rc) rc = launch_ivox_clear(c->gslots, table, c->stream);
                 if (!rc) rc = launch_dyn_slots(d.keys, d.starts, cell_bound, c->gslots, log2, c->stream,
                                                d.ctr + kDynRRuns, d.ctr + kDynRErr);
             }
@@ -1707,20 +1720,11 @@ static int map_incremental_ikd(livo_ctx* c, int32_t id, const livo_state* state,
     if (counts) counts[0] = counts[1] = 0;
     int rc = dyn_activate(c);
     if (!rc) rc = dyn_add_scratch(c, std::max<int64_t>(N, 1));
-    if (!rc) rc = ensure_slots(c, 1);
     if (rc) return rc;
-    if (N > 0) {
-        init_slot(c->h_slots[0], *state, *state, c->params.max_iterations);
-        HIP_TRY(hipMemcpyAsync(c->d_slots, c->h_slots, sizeof(IekfSlot), hipMemcpyHostToDevice, c->stream));
-        DynWorldParams wp{};
-        wp.pts = s->pts; wp.perm = s->d_perm; wp.n = N; wp.slot = c->d_slots; wp.W = c->dyn.W;
-        std::memcpy(wp.R_LI, c->params.R_LI, sizeof(wp.R_LI));
-        std::memcpy(wp.t_LI, c->params.t_LI, sizeof(wp.t_LI));
-        rc = launch_dyn_world(wp, c->stream);
-        if (rc) return rc;
-    }
+    // (feats_down_world: k_add_prep takes the points to the world frame, the state in its arguments)
+    const DynWorldIn world{s->pts, s->d_perm, state};
     livo_map_add_stats st{};
-    rc = dyn_add(c, N, (float)fs, true, &st);
+    rc = dyn_add(c, N, (float)fs, true, &st, &world);
     if (rc) return rc;
     if (cat && N > 0) std::memset(cat, 1, (size_t)N);  // every point is handed to Add_Points
     if (counts) {

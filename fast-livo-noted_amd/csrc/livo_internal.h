@@ -616,21 +616,16 @@ struct DynAddParams {
     uint32_t* bigs;             // the crowded boxes (runs), listed by k_scan_boxes (count: ctr[kDynBig])
     uint32_t* dlist_u;          // the deferred points, unordered (k_add_box; count ctr[kDynDeferred])
     uint32_t* klist;            // the box winners, unordered (k_add_box; count ctr[kDynKept])
-};
-struct DynWorldParams {
-    const float* pts;           // scan body points (stored order, 4 floats each)
-    const int32_t* perm;        // stored position -> caller index
-    int64_t n;
-    const IekfSlot* slot;       // its state
-    double R_LI[9];
-    double t_LI[3];
-    float* W;                   // n world points in caller order (feats_down_world)
+    // map_incremental: k_add_prep first takes the scan's stored points to the
+    // world frame into W (pointBodyToWorld at rot / pos; null: W is filled)
+    const float* wpts;          // scan body points, stored order (4 floats each)
+    const int32_t* wperm;       // stored position -> caller index
+    double wrot[9], wpos[3], R_LI[9], t_LI[3];
 };
 int launch_add_prep(const DynAddParams& p, void* stream);
 int launch_add_group(const DynAddParams& p, void* stream);
 int launch_add_finish(const DynAddParams& p, float* all, uint8_t* alive, void* stream);
 int launch_dyn_seed(const float* gpts, int64_t M, float* all, uint8_t* alive, void* stream);
-int launch_dyn_world(const DynWorldParams& p, void* stream);
 int launch_dyn_cellkeys(const float* all, const uint8_t* alive, int64_t n_ids, const float* org, float inv,
                         unsigned long long* keys, uint32_t* vals, unsigned long long* ctr, void* stream);
 int launch_dyn_gather(const unsigned long long* skeys, const uint32_t* sids, int64_t na, const float* all, float* gpts,
@@ -672,7 +667,7 @@ struct ScanCtx {
 int scan_tiles(int64_t n);
 // rank[i] = old-grid survivors before i, i <= na_old (the flags read in the scan)
 int launch_scan_flags(ScanCtx& sc, const float* gpts, int64_t na_old, const uint8_t* alive, uint32_t* rank,
-                      void* stream);
+                      void* stream, GridSlot* clr = nullptr, int64_t clr_n = 0);
 // runs of equal keys -> starts, *nruns (k_run_heads + a scan + k_dyn_runs)
 int launch_scan_runs(ScanCtx& sc, const unsigned long long* keys, int64_t n, uint32_t* starts,
                      unsigned long long* nruns, void* stream, const unsigned long long* dn = nullptr);
