@@ -225,7 +225,7 @@ __global__ void k_add_prep(DynAddParams P) {
 
 constexpr int kBoxWaves = 4;       // k_add_box: waves per block
 constexpr uint32_t kBoxSmall = 64;  // boxes with at most this many new points: 16-lane groups
-constexpr int kBigBlocks = 64;      // k_add_box's first blocks: a wave per crowded box
+constexpr int kBigBlocks = 128;     // k_add_box's first blocks: a wave per crowded box
 
 // A box's stored points (Search_by_range) by a group of G lanes (16: most
 // boxes hold a few stored points and new points; 64: the crowded boxes): the
