@@ -908,9 +908,9 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_boxes(DynAddParams P, Sca
 
 // ---- the grid merged instead of re-sorted (dyn_rebuild's incremental path) ----
 // The new ids' cell keys sorted by (key, index), m <= kNewSortMax: every
-// workgroup keys all of them into LDS, then 8 lanes count one key's rank, each
-// over an eighth of the keys (broadcast reads), summed by shuffles.
-constexpr int kNewSortSplit = 8;
+// workgroup keys all of them into LDS, then kNewSortSplit lanes count one key's rank, each
+// over its share of the keys (broadcast reads), summed by shuffles.
+constexpr int kNewSortSplit = 16;
 __global__ __launch_bounds__(256) void k_dyn_newsort(const float4* __restrict__ all, const uint8_t* __restrict__ alive,
                                                      int64_t m, float ox, float oy, float oz, float inv,
                                                      unsigned long long* skeys, uint32_t* svals,
@@ -932,7 +932,7 @@ __global__ __launch_bounds__(256) void k_dyn_newsort(const float4* __restrict__ 
         K[i] = alive[i] ? cell_key_of(all[i], ox, oy, oz, inv, bad) : ~0ull;
     if (bad && blockIdx.x == 0) atomicOr(ctr + kDynError, 4ull);
     __syncthreads();
-    const int i = (blockIdx.x * blockDim.x + threadIdx.x) / kNewSortSplit;  // (the 8 lanes of i: one wave)
+    const int i = (blockIdx.x * blockDim.x + threadIdx.x) / kNewSortSplit;  // (the lanes of i: one wave)
     const int q = threadIdx.x % kNewSortSplit;
     const int ii = i < mm ? i : mm - 1;
     const unsigned long long key = K[ii];
