@@ -227,15 +227,6 @@ struct livo_ctx {
     // 18.3k vs 17.1k / 17.1k vs 16.4k updates/s against 0, one range per XCD, whose
     // most expensive scan's XCD was the straggler; profiles/r04_ab_block_order.txt)
     int xcd_chunk = 8;
-    // evaluations without a search: 256-point chunks per block (LIVO_NS_K).  1: four
-    // measured slower (pooled 21.8k vs 24.5k updates/s, eval_nosearch 0.187 vs 0.161 ms per
-    // step, profiles/r05_ab_ns_k.txt): fewer blocks each with a serial chain of chunks
-    int ns_k = 1;
-    // the evaluations without a search in one persistent launch per run of them
-    // (k_iekf_ns: F, P, E, P per group instead of one launch per evaluation);
-    // LIVO_PERSIST=0 / LIVO_NS_TEAM (workers per scan)
-    int persist = 0;  // measured slower at every team size: profiles/r05_ab_persist.txt
-    int ns_team = 48;
     GridSlot* vslots = nullptr;        // vertex runs (static map only)
     RunWord* vpts = nullptr;           // run entries (LIVO_IDX_RUNS: grid positions; else x, y, z, map index bits)
     int32_t vlog2 = 0;
@@ -404,11 +395,7 @@ constexpr size_t kLmStride = (kSlotLmBytes + 255) & ~(size_t)255;
 static_assert(kLmStride % alignof(HsJob) == 0 && kLmStride % alignof(IekfSlot) == 0, "packed slot alignment");
 static_assert(kLmStride % 16 == 0, "kernel staging copies move 16-B words");
 // bytes of a batch's packed staging area, rounded up to whole 16-B words
-// Then the persistent evaluations' team counters (two launches per group),
-// zeroed in the host copy so the staging copy clears them too.
-constexpr int kTeamCtrs = 2 * kMaxGroups;
-static size_t lm_team_off(int32_t n) { return ((size_t)n * (kLmStride + sizeof(HsJob)) + 15) & ~(size_t)15; }
-static size_t lm_bytes(int32_t n) { return (lm_team_off(n) + sizeof(unsigned) * kTeamCtrs + 15) & ~(size_t)15; }
+static size_t lm_bytes(int32_t n) { return ((size_t)n * (kLmStride + sizeof(HsJob)) + 15) & ~(size_t)15; }
 static int ensure_lm(BatchLane& B, int32_t n) {
     const size_t need = lm_bytes(n);
     if (need <= B.lm_cap) return LIVO_OK;
@@ -570,7 +557,6 @@ static KnnParams make_knn_params(livo_ctx* c) {
     // keeps points with cr_rho2 <= brmax^2 in float: a relative 1e-5 below covers its rounding)
     kp.bcert2 = c->brmax * c->brmax * (1.0f - 1e-5f);
     kp.xcd_chunk = c->xcd_chunk;
-    kp.ns_k = c->ns_k;
     kp.identity = 0;
     kp.iv = ivox_params(c);
     kp.canon = c->dyn.active ? 1 : 0;
@@ -643,8 +629,56 @@ static void init_slot_ik(IekfSlot& s, const livo_ikfom_state& st, int max_iter) 
     s.ctrl.max_iter = max_iter;
 }
 
+// The covariance factors of the device solve (IekfSlot::covL / covB): the
+// state covariance is fixed for the whole IEKF loop of a scan (it changes only
+// when the loop stops, laser_mapping.cpp:224-227), so the 6x6 Cholesky of its
+// pose block S = P(0:6, 0:6) = L L^T and B = P(:, 0:6) L^-T are formed once, on
+// the host, when the slot is staged.  cov_ok = 0 (the device then takes its
+// pivoted 6x6 LU path) unless P's first six rows and columns are symmetric and
+// S is numerically positive definite.
+static void cov_factor(IekfSlot& s) {
+    const double* P = s.state.cov;
+    constexpr int D = kDim;
+    s.cov_ok = 0;
+    double amax = 0.0;
+    for (int i = 0; i < D; i++)
+        for (int j = 0; j < 6; j++) {
+            const double a = P[i * D + j], b = P[j * D + i];
+            if (!std::isfinite(a) || !std::isfinite(b)) return;
+            amax = std::max(amax, std::fabs(a));
+        }
+    for (int i = 0; i < D; i++)
+        for (int j = 0; j < 6; j++)
+            if (std::fabs(P[i * D + j] - P[j * D + i]) > 1e-12 * amax) return;
+    double Lm[36] = {};
+    for (int j = 0; j < 6; j++) {
+        double d = P[j * D + j];
+        for (int k = 0; k < j; k++) d -= Lm[j * 6 + k] * Lm[j * 6 + k];
+        if (!(d > 1e-13 * P[j * D + j]) || !(d > 0.0)) return;  // not (numerically) positive definite
+        const double l = std::sqrt(d);
+        Lm[j * 6 + j] = l;
+        for (int i = j + 1; i < 6; i++) {
+            double v = P[i * D + j];
+            for (int k = 0; k < j; k++) v -= Lm[i * 6 + k] * Lm[j * 6 + k];
+            Lm[i * 6 + j] = v / l;
+        }
+    }
+    double Bm[(D - 6) * 6];
+    for (int r = 6; r < D; r++)  // B(r, :) L^T = P(r, 0:6): forward substitution
+        for (int j = 0; j < 6; j++) {
+            double v = P[r * D + j];
+            for (int k = 0; k < j; k++) v -= Bm[(r - 6) * 6 + k] * Lm[j * 6 + k];
+            Bm[(r - 6) * 6 + j] = v / Lm[j * 6 + j];
+        }
+    for (double v : Bm)
+        if (!std::isfinite(v)) return;
+    std::memcpy(s.covL, Lm, sizeof(Lm));
+    std::memcpy(s.covB, Bm, sizeof(Bm));
+    s.cov_ok = 1;
+}
+
 // bytes: how much of the slot to clear; the batched LaserMapping update uploads
-// and reads only its first kSlotLmBytes (8.8 of 20.9 KB), so it clears only those
+// and reads only its first kSlotLmBytes, so it clears only those
 static void init_slot(IekfSlot& s, const livo_state& st, const livo_state& prior, int max_iter,
                       size_t bytes = sizeof(IekfSlot)) {
     std::memset(&s, 0, bytes);
@@ -655,6 +689,7 @@ static void init_slot(IekfSlot& s, const livo_state& st, const livo_state& prior
     s.ctrl.iter_count = -1;
     s.ctrl.rematch_num = 0;
     s.ctrl.max_iter = max_iter;
+    cov_factor(s);
 }
 
 static int create_group_streams(livo_ctx* c) {
@@ -1654,9 +1689,10 @@ static int dyn_add(livo_ctx* c, int64_t n, float ds, bool downsample, livo_map_a
             if (rc) return rc;
             HIP_TRY(hipMemcpyAsync(h, d.ctr, sizeof(h), hipMemcpyDeviceToHost, c->stream));
             HIP_TRY(hipStreamSynchronize(c->stream));
-            if (fused && (h[kDynError] & (1ull | 64ull))) {
-                // the fused pass refilled the table from an unchanged point set, sized
-                // for its bound: rebuild it as the grid's own before returning
+            if (fused && (h[kDynError] & (1ull | 32ull | 64ull))) {
+                // the fused pass refilled the table from an unchanged point set, hashed
+                // with its bound's log2 (not c->glog2): rebuild it as the grid's own
+                // before returning or before the 64-bit-key redo reads it (bit 32)
                 const int rrc = dyn_rebuild(c);
                 if (rrc) return rrc;
             }
@@ -1806,9 +1842,6 @@ int livo_ctx_create(int device, const livo_params* p, livo_ctx** out) {
     if (const char* env = std::getenv("LIVO_SYNC_ZC")) c->sync_zc = std::atoi(env) != 0;
     if (const char* env = std::getenv("LIVO_SLOT_WB")) c->slot_wb = std::atoi(env) != 0;
     if (const char* env = std::getenv("LIVO_XCD_CHUNK")) c->xcd_chunk = std::max(0, std::atoi(env));  // tuning knob
-    if (const char* env = std::getenv("LIVO_NS_K")) c->ns_k = std::max(1, std::atoi(env));  // tuning knob
-    if (const char* env = std::getenv("LIVO_PERSIST")) c->persist = std::atoi(env) != 0;
-    if (const char* env = std::getenv("LIVO_NS_TEAM")) c->ns_team = std::max(1, std::atoi(env));
     if (const char* env = std::getenv("LIVO_GRID_PPC")) {  // tuning knob
         const float v = (float)std::atof(env);
         if (v > 0.f) c->grid_ppc = v;
@@ -3429,12 +3462,6 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
     const bool kcopy = (lm ? B.h_lm_dev != nullptr : B.h_ik_dev != nullptr) && (sync ? c->sync_zc : c->lane_zc);
     const size_t ik_bytes = (size_t)n * (sizeof(IekfSlot) + sizeof(HsJob));
     static_assert((sizeof(IekfSlot) + sizeof(HsJob)) % 16 == 0 && sizeof(IekfSlot) % 16 == 0, "16-B word copies");
-    const bool persist = fused && lm && c->persist && !full && max_iter + 1 >= 2;
-    unsigned* dteam = nullptr;
-    if (persist) {  // (before the staging copy below: it clears the device counters)
-        std::memset(B.h_lm + lm_team_off(n), 0, sizeof(unsigned) * kTeamCtrs);
-        dteam = reinterpret_cast<unsigned*>(B.d_lm + lm_team_off(n));
-    }
     if (lm && kcopy) {
         rc = launch_copy_words(B.h_lm_dev, B.d_lm, lm_bytes(n), B.st[0]);
         if (rc) return rc;
@@ -3507,22 +3534,13 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
         hp[gi].solve = lm ? 1 : 0;  // the last plane-pass block of each scan runs its solve (IKFoM: k_solve_ik below)
         hp[gi].replay_count = rcount + gi;
     }
-    // Persistent: the first evaluation (search), then the run of evaluations without
-    // one (k_iekf_ns), the one search a rematch asks for (k_iekf_eval: the solve
-    // sets nearest_search_en at most once more, :226-233, the second rematch stops
-    // the scan) and the run after it: F, P, E, P whatever the convergence.  A
-    // launch whose scans all stopped exits at once.
-    const int launches = persist ? 4 : evals;
-    for (int e = 0; e < launches; e++) {
+    // one launch per evaluation (a launch whose scans all stopped exits at once)
+    for (int e = 0; e < evals; e++) {
         for (int gi = 0; gi < ngroups && fused; gi++) {
             hipStream_t st = g[gi].st;
             // full: ev[gi][e] before evaluation e, ev[gi][evals] after the last
             if (full && (e > 0 || gi > 0)) HIP_TRY(hipEventRecord(c->ev[gi][e], st));
-            if (persist && (e & 1))
-                rc = launch_iekf_ns(kp[gi], hp[gi], g[gi].count, ns_team_size(g[gi].max_n, c->ns_team),
-                                    dteam + 2 * gi + (e >> 1), st);
-            else
-                rc = launch_iekf_eval(kp[gi], hp[gi], g[gi].count, g[gi].max_n, e == 0, st);
+            rc = launch_iekf_eval(kp[gi], hp[gi], g[gi].count, g[gi].max_n, e == 0, st);
             if (rc) return rc;
             if (prof && !full && e == 0) HIP_TRY(hipEventRecord(c->ev[gi][1], st));
         }

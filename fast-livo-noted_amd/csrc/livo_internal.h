@@ -42,6 +42,11 @@ constexpr int kKnnBlock = LIVO_KNN_BLOCK;   // threads per block of the k-NN pas
 constexpr int kPtsPerThread = LIVO_PTS_PER_THREAD;  // points per thread of the plane-fit pass
 constexpr int kRedCols = 32;                // doubles per block partial (29 used)
 constexpr int kRedUsed = 29;                // 21 HTH upper-tri + 6 HTL + residual sum + count
+#ifndef LIVO_RED_SHARDS
+#define LIVO_RED_SHARDS 8
+#endif
+constexpr int kRedShards = LIVO_RED_SHARDS;  // first-level shards of a scan's block partials (<= 32)
+static_assert(kRedShards >= 1 && kRedShards <= 32, "one shard row per column thread group of the tail");
 #ifndef LIVO_MAX_GROUPS
 #define LIVO_MAX_GROUPS 4
 #endif
@@ -239,7 +244,7 @@ struct alignas(16) IkBlock {
 enum SlotModel { kModelLaserMapping = 0, kModelIkfom = 1 };
 
 // Everything one scan update needs on the device (one per batch entry).
-struct alignas(16) IekfSlot {
+struct alignas(128) IekfSlot {
     livo_state state;     // in/out
     livo_state prior;     // state_propagat
     double red[kRedCols];       // last reduced h_share sums (for livo_h_share)
@@ -248,13 +253,26 @@ struct alignas(16) IekfSlot {
     unsigned long long visits[LIVO_MAX_EVALS];  // k-NN nodes visited (grid: hash slots probed) per evaluation
     unsigned long long scanned[LIVO_MAX_EVALS]; // grid k-NN: map points read per evaluation
     int32_t eval_search[LIVO_MAX_EVALS];
-    unsigned hs_ticket;         // k_hshare blocks done in the current pass (the last one reduces)
+    unsigned hs_ticket;         // reduction shards done in the current pass (the last one solves; IKFoM: blocks)
     int32_t model;              // SlotModel
-    unsigned gen;               // k_iekf_ns: evaluations published by its solves (the teams poll it)
-    unsigned pad_;
+    unsigned pad_[2];
+    // Factors of the state covariance, made by the host when it stages the slot
+    // (init_slot; the covariance changes only when the scan's loop stops):
+    // S = P(0:6, 0:6) = L L^T (Cholesky, row-major 6x6, zero above the diagonal)
+    // and B = P(:, 0:6) L^-T (rows 6..17; rows 0..5 are L).  The solve forms
+    // K1(:, 0:6) = B Q^-1 L^T with Q = I6 + L^T C L (SPD) -- see solve_scan.
+    // cov_ok 0: S is not numerically SPD or P is not symmetric (the 6x6 LU path).
+    double covL[36];
+    double covB[(kDim - 6) * 6];
+    int32_t cov_ok;
+    int32_t pad2_[3];
+    // two-level reduction of the block partials (hs_ticket_tail): one ticket per
+    // shard, each on a 128-B line of its own (device-scope atomics serialise per line)
+    alignas(128) unsigned sh_ticket[kRedShards * 32];
     IkBlock ik;                 // model == kModelIkfom (last: the LaserMapping model copies only the part before it)
 };
 constexpr size_t kSlotLmBytes = offsetof(IekfSlot, ik);  // bytes of a slot the LaserMapping model reads / writes
+constexpr size_t kSlotWbBytes = offsetof(IekfSlot, covL);  // what the host reads back (no factors, no tickets)
 
 // Nearest_Points[i] + pointSearchSqDis for one point: 128 B, written by the
 // k-NN pass, read by every plane-fit pass until the next search.
@@ -320,7 +338,6 @@ struct KnnParams {
     int32_t identity;       // 1: pts are world points already (livo_knn)
     int32_t nb;             // blocks per scan (set by the launcher)
     int32_t xcd_chunk;      // k_iekf_eval block order: XCD-interleaved chunks of this many blocks (0: one range per XCD)
-    int32_t ns_k;           // k_iekf_eval without a search: 256-point chunks per block (1: one)
     int32_t ldepth;         // leaf map depth D
     const LeafNode* lnodes; // leaf map internal records
     const float* lpts;      // leaf map points, 4 floats each (x, y, z, index bits)
@@ -387,12 +404,6 @@ int launch_hshare(const HsParams& p, int n_jobs, int max_nblk, bool first, void*
 #endif
 constexpr int kEvalBlock = LIVO_EVAL_BLOCK;  // threads (points) per block of k_iekf_eval
 int launch_iekf_eval(const KnnParams& kp, const HsParams& hp, int n_jobs, int64_t max_n, bool first, void* stream);
-// The evaluations without a search of a group in one persistent launch (k_iekf_ns):
-// team_ctr zeroed before it; LIVO_E_RANGE when the scans are too large for it.
-// k_iekf_ns: the evaluations without a search, persistent (team of T workers + a
-// solver per scan; team_ctr zeroed before the launch).  T from ns_team_size.
-int ns_team_size(int64_t max_n, int team);
-int launch_iekf_ns(const KnnParams& kp, const HsParams& hp, int n_jobs, int T, unsigned* team_ctr, void* stream);
 int launch_solve_ik(const HsParams& p, int n_jobs, void* stream);
 int launch_copy_words(const void* src, void* dst, size_t bytes, void* stream);  // 16-B aligned, bytes % 16 == 0
 // IKFoM plane pass (12-wide rows) with the manifold update in each scan's last block.

@@ -2269,10 +2269,24 @@ struct alignas(16) SolveLds {
     double w[6];                // HTL6 - C vec6
     double vec[kDim];
     double sol[kDim];
+    // the factored path (slot->cov_ok): S = L L^T and B = P(:, 0:6) L^-T staged
+    // from the slot (covL, covB contiguous, as in IekfSlot), Q = I6 + L^T C L
+    double covL[36];
+    double covB[(kDim - 6) * 6];
+    double T[36];               // C L
+    double Q[36];               // I6 + L^T C L
+    double F[28];               // LDL^T of Q: 21 packed lower entries (D on the diagonal), then 6 x 1/D
+    double u[6];                // L^T w
+    double Qi[36];              // Q^-1 (stopping solve)
+    double V[kDim * 6];         // B (I6 - Q^-1) (stopping solve)
     int piv[6];
     alignas(16) IekfCtrl ctrl;
     int knn_passes;             // stats.knn_passes so far
+    int cov_ok;                 // slot->cov_ok
 };
+static_assert(offsetof(SolveLds, covB) == offsetof(SolveLds, covL) + 36 * sizeof(double) &&
+                  offsetof(IekfSlot, covB) == offsetof(IekfSlot, covL) + 36 * sizeof(double),
+              "covL, covB contiguous in the slot and in LDS");
 constexpr int kStHead = (int)(sizeof(StateHead) / sizeof(double));  // 24
 static_assert(sizeof(StateHead) == 24 * sizeof(double) && offsetof(livo_state, cov) == sizeof(StateHead),
               "StateHead is the head of livo_state");
@@ -2288,8 +2302,12 @@ __device__ __forceinline__ int ld_sc1(const int* p) {
 __device__ __forceinline__ unsigned long long ld_sc1(const unsigned long long* p) {
     return __hip_atomic_load(gptr(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// Write-through (sc1) stores of the slot's fields: the persistent evaluation
-// loop (k_iekf_ns) reads them from other CUs inside one launch.
+// Write-through (sc1) stores of slot / partial words read by other CUs inside
+// one launch (the reduction's hand-offs).  INVARIANT: every in-launch read of a
+// word another workgroup stored goes through ld_sc1 (an agent-scope atomic load
+// of a global address): a plain or scalar load may be served by this CU's L1 or
+// by the scalar cache, which other CUs' stores do not refresh (round 5: job
+// pointers laundered into scalar loads faulted).
 template <class T>
 __device__ __forceinline__ void st_sc1(T* p, T v) {
     __hip_atomic_store(gptr(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2299,13 +2317,16 @@ __device__ __forceinline__ void st_sc1(T* p, T v) {
 // into L: thread t of nt, two loads in flight per thread before any LDS store.
 // sc1 loads: the slot may have been written by another CU of this launch.
 __device__ __forceinline__ void solve_stage(const IekfSlot* slot, SolveLds& L, int t, int nt) {
-    constexpr int nP = kDim * kDim, nD = nP + 2 * kStHead;  // doubles: cov, state head, prior head
+    // doubles: cov, state head, prior head, covariance factors (covL, covB)
+    constexpr int nP = kDim * kDim, nH = nP + 2 * kStHead, nD = nH + 36 + (kDim - 6) * 6;
     auto src = [&](int k) -> const double* {
         return k < nP ? slot->state.cov + k
-                      : (k < nP + kStHead ? slot->state.rot + (k - nP) : slot->prior.rot + (k - nP - kStHead));
+                      : (k < nP + kStHead ? slot->state.rot + (k - nP)
+                                          : (k < nH ? slot->prior.rot + (k - nP - kStHead) : slot->covL + (k - nH)));
     };
     auto dst = [&](int k) -> double* {
-        return k < nP ? L.P + k : (k < nP + kStHead ? L.st.rot + (k - nP) : L.pr.rot + (k - nP - kStHead));
+        return k < nP ? L.P + k
+                      : (k < nP + kStHead ? L.st.rot + (k - nP) : (k < nH ? L.pr.rot + (k - nP - kStHead) : L.covL + (k - nH)));
     };
     for (int k0 = t; k0 < nD; k0 += 2 * nt) {
         const int k1 = k0 + nt;
@@ -2318,12 +2339,14 @@ __device__ __forceinline__ void solve_stage(const IekfSlot* slot, SolveLds& L, i
         const unsigned long long* c = reinterpret_cast<const unsigned long long*>(&slot->ctrl);
         const unsigned long long c0 = ld_sc1(c), c1 = ld_sc1(c + 1), c2 = ld_sc1(c + 2), c3 = ld_sc1(c + 3);
         const int kp = ld_sc1(&slot->stats.knn_passes);
+        const int ok = ld_sc1(&slot->cov_ok);
         unsigned long long* d = reinterpret_cast<unsigned long long*>(&L.ctrl);
         d[0] = c0;
         d[1] = c1;
         d[2] = c2;
         d[3] = c3;
         L.knn_passes = kp;
+        L.cov_ok = ok;
     }
 }
 static_assert(sizeof(IekfCtrl) == 8 * sizeof(int) && alignof(IekfSlot) >= 16 && offsetof(IekfSlot, ctrl) % 16 == 0,
@@ -2355,78 +2378,206 @@ __device__ __forceinline__ int solve_scan(IekfSlot* slot, SolveLds& L, const int
     WAVE_SYNC();
     SOLVE_MARK(2);
     SPH_MARK(0);
-    // M = I6 + C P66
-    if (lane < 36) {
-        const int r = lane / 6, c = lane % 6;
-        double m = L.C[r * 6 + 0] * s_P[0 * kDim + c];
+    const bool fac = L.cov_ok != 0;  // (LDS: uniform)
+    if (fac) {
+        // The factored form (slot covL / covB, made by the host from the covariance):
+        // with S = P66 = L L^T, M = I6 + C S = L^-T Q L^T for Q = I6 + L^T C L, so
+        //   K1(:, 0:6) = P(:, 0:6) M^-1 = B Q^-1 L^T,  B = P(:, 0:6) L^-T,
+        //   solution = B Q^-1 (L^T w) + vec.
+        // Q is SPD with eigenvalues >= 1: an LDL^T without pivoting is stable, and
+        // every lane factors it in registers (the same values, no cross-lane steps):
+        // the pivoted 6x6 LU's argmax / row broadcasts are off the chain.
+        const double* const Lf = L.covL;
+#ifdef LIVO_TAIL_TWICE  // I-cache probe (tools/tail_prof.py): T and Q formed twice, the first pass timed into marks 8, 9
+#pragma unroll 1
+        for (int rep = 0; rep < 2; rep++) {
+#endif
+        // T = C L (lanes 0..35): T(r, c) = sum_{k >= c} C(r, k) L(k, c)
+        if (lane < 36) {
+            const int r = lane / 6, c = lane % 6;
+            double t = 0.0;
 #pragma unroll
-        for (int k = 1; k < 6; k++) m = m + L.C[r * 6 + k] * s_P[k * kDim + c];
-        L.M[lane] = (r == c ? 1.0 : 0.0) + m;
-    }
-    WAVE_SYNC();
-    SPH_MARK(1);
-    double A6[6];
-#pragma unroll
-    for (int j = 0; j < 6; j++) A6[j] = lane < 6 ? L.M[lane * 6 + j] : 0.0;
-    wave_lu_to_lds<6>(A6, lane, L.LU, L.piv);
-    WAVE_SYNC();
-    SPH_MARK(2);
-    {
-        double y[6];
-        reg_lu_column<6>(A6, L.piv, lane, y);  // (readlanes: every lane runs it)
-        if (lane < 6) {
-#pragma unroll
-            for (int i = 0; i < 6; i++) L.Minv[i * 6 + lane] = y[i];
+            for (int k = 0; k < 6; k++)
+                if (k >= c) t = t + L.C[r * 6 + k] * Lf[k * 6 + c];
+            L.T[lane] = t;
         }
-    }
-    if (SPLIT_VEC) __syncthreads();  // L.vec from the other wave (it waits here too)
-    if (lane < 6) {
-        double wv = s_sum[21 + lane];
+        WAVE_SYNC();
+#ifdef LIVO_TAIL_TWICE
+        SPH_MARK(rep == 0 ? 8 : 1);
+#else
+        SPH_MARK(1);
+#endif
+        // Q = I6 + L^T T (lanes 0..35): Q(r, c) = [r == c] + sum_{k >= r} L(k, r) T(k, c)
+        if (lane < 36) {
+            const int r = lane / 6, c = lane % 6;
+            double q = 0.0;
 #pragma unroll
-        for (int k = 0; k < 6; k++) wv = wv - L.C[lane * 6 + k] * L.vec[k];
-        L.w[lane] = wv;
-    }
-    WAVE_SYNC();
-    SOLVE_MARK(4);
-    SPH_MARK(3);
-    // K1(:, 0:6) = P(:, 0:6) M^-1
-    for (int t = lane; t < kDim * 6; t += 64) {
-        const int r = t / 6, c = t % 6;
-        double k6 = s_P[r * kDim + 0] * L.Minv[0 * 6 + c];
+            for (int k = 0; k < 6; k++)
+                if (k >= r) q = q + Lf[k * 6 + r] * L.T[k * 6 + c];
+            L.Q[lane] = (r == c ? 1.0 : 0.0) + q;
+        }
+        WAVE_SYNC();
+#ifdef LIVO_TAIL_TWICE
+        if (rep == 0) SPH_MARK(9);
+        }
+#endif
+        // LDL^T of Q in place (f: packed lower, D on the diagonal), every lane
+        double f[21], di[6];
 #pragma unroll
-        for (int k = 1; k < 6; k++) k6 = k6 + s_P[r * kDim + k] * L.Minv[k * 6 + c];
-        L.K6[t] = k6;
-    }
-    WAVE_SYNC();
-    SPH_MARK(4);
-    // G(:, 0:6) = K1(:, 0:6) C ;  solution = K1(:, 0:6) w + vec
-    for (int t = lane; t < kDim * 6; t += 64) {
-        const int r = t / 6, c = t % 6;
-        double g = L.K6[r * 6 + 0] * L.C[0 * 6 + c];
+        for (int i = 0; i < 6; i++)
 #pragma unroll
-        for (int k = 1; k < 6; k++) g = g + L.K6[r * 6 + k] * L.C[k * 6 + c];
-        L.G6[t] = g;
-    }
-    if (lane < kDim) {
-        double a = L.K6[lane * 6 + 0] * L.w[0];
+            for (int j = 0; j <= i; j++) f[i * (i + 1) / 2 + j] = 0.5 * (L.Q[i * 6 + j] + L.Q[j * 6 + i]);
 #pragma unroll
-        for (int k = 1; k < 6; k++) a = a + L.K6[lane * 6 + k] * L.w[k];
-        L.sol[lane] = a + L.vec[lane];
+        for (int j = 0; j < 6; j++) {
+            double wv[6];
+            double d = f[j * (j + 1) / 2 + j];
+#pragma unroll
+            for (int k = 0; k < j; k++) {
+                wv[k] = f[j * (j + 1) / 2 + k] * f[k * (k + 1) / 2 + k];  // L(j, k) D(k)
+                d = d - f[j * (j + 1) / 2 + k] * wv[k];
+            }
+            f[j * (j + 1) / 2 + j] = d;
+            di[j] = 1.0 / d;
+#pragma unroll
+            for (int i = j + 1; i < 6; i++) {
+                double v = f[i * (i + 1) / 2 + j];
+#pragma unroll
+                for (int k = 0; k < j; k++) v = v - f[i * (i + 1) / 2 + k] * wv[k];
+                f[i * (i + 1) / 2 + j] = v * di[j];
+            }
+        }
+        if (lane == 0) {  // for a stopping solve's Q^-1
+#pragma unroll
+            for (int k = 0; k < 21; k++) L.F[k] = f[k];
+#pragma unroll
+            for (int k = 0; k < 6; k++) L.F[21 + k] = di[k];
+        }
+        SPH_MARK(2);
+        if (SPLIT_VEC) __syncthreads();  // L.vec from the other wave (it waits here too)
+        // w = HTL6 - C vec6, u = L^T w (lanes 0..5)
+        if (lane < 6) {
+            double wv = s_sum[21 + lane];
+#pragma unroll
+            for (int k = 0; k < 6; k++) wv = wv - L.C[lane * 6 + k] * L.vec[k];
+            L.w[lane] = wv;
+        }
+        WAVE_SYNC();
+        if (lane < 6) {
+            double uu = 0.0;
+#pragma unroll
+            for (int k = 0; k < 6; k++)
+                if (k >= lane) uu = uu + Lf[k * 6 + lane] * L.w[k];
+            L.u[lane] = uu;
+        }
+        WAVE_SYNC();
+        SPH_MARK(3);
+        // y = Q^-1 u (every lane), solution = B y + vec (lanes 0..17)
+        double y[6];
+#pragma unroll
+        for (int i = 0; i < 6; i++) {
+            double z = L.u[i];
+#pragma unroll
+            for (int k = 0; k < i; k++) z = z - f[i * (i + 1) / 2 + k] * y[k];
+            y[i] = z;
+        }
+#pragma unroll
+        for (int i = 0; i < 6; i++) y[i] = y[i] * di[i];
+#pragma unroll
+        for (int i = 4; i >= 0; i--) {
+            double z = y[i];
+#pragma unroll
+            for (int k = i + 1; k < 6; k++) z = z - f[k * (k + 1) / 2 + i] * y[k];
+            y[i] = z;
+        }
+        SPH_MARK(4);
+        if (lane < kDim) {
+            const double* b = lane < 6 ? Lf + lane * 6 : L.covB + (lane - 6) * 6;
+            double a = b[0] * y[0];
+#pragma unroll
+            for (int k = 1; k < 6; k++) a = a + b[k] * y[k];
+            L.sol[lane] = a + L.vec[lane];
+        }
+        WAVE_SYNC();
+        SPH_MARK(5);
+    } else {
+        // M = I6 + C P66
+        if (lane < 36) {
+            const int r = lane / 6, c = lane % 6;
+            double m = L.C[r * 6 + 0] * s_P[0 * kDim + c];
+#pragma unroll
+            for (int k = 1; k < 6; k++) m = m + L.C[r * 6 + k] * s_P[k * kDim + c];
+            L.M[lane] = (r == c ? 1.0 : 0.0) + m;
+        }
+        WAVE_SYNC();
+        SPH_MARK(1);
+        double A6[6];
+#pragma unroll
+        for (int j = 0; j < 6; j++) A6[j] = lane < 6 ? L.M[lane * 6 + j] : 0.0;
+        wave_lu_to_lds<6>(A6, lane, L.LU, L.piv);
+        WAVE_SYNC();
+        SPH_MARK(2);
+        {
+            double y[6];
+            reg_lu_column<6>(A6, L.piv, lane, y);  // (readlanes: every lane runs it)
+            if (lane < 6) {
+#pragma unroll
+                for (int i = 0; i < 6; i++) L.Minv[i * 6 + lane] = y[i];
+            }
+        }
+        if (SPLIT_VEC) __syncthreads();  // L.vec from the other wave (it waits here too)
+        if (lane < 6) {
+            double wv = s_sum[21 + lane];
+#pragma unroll
+            for (int k = 0; k < 6; k++) wv = wv - L.C[lane * 6 + k] * L.vec[k];
+            L.w[lane] = wv;
+        }
+        WAVE_SYNC();
+        SOLVE_MARK(4);
+        SPH_MARK(3);
+        // K1(:, 0:6) = P(:, 0:6) M^-1
+        for (int t = lane; t < kDim * 6; t += 64) {
+            const int r = t / 6, c = t % 6;
+            double k6 = s_P[r * kDim + 0] * L.Minv[0 * 6 + c];
+#pragma unroll
+            for (int k = 1; k < 6; k++) k6 = k6 + s_P[r * kDim + k] * L.Minv[k * 6 + c];
+            L.K6[t] = k6;
+        }
+        WAVE_SYNC();
+        SPH_MARK(4);
+        // G(:, 0:6) = K1(:, 0:6) C ;  solution = K1(:, 0:6) w + vec
+        for (int t = lane; t < kDim * 6; t += 64) {
+            const int r = t / 6, c = t % 6;
+            double g = L.K6[r * 6 + 0] * L.C[0 * 6 + c];
+#pragma unroll
+            for (int k = 1; k < 6; k++) g = g + L.K6[r * 6 + k] * L.C[k * 6 + c];
+            L.G6[t] = g;
+        }
+        if (lane < kDim) {
+            double a = L.K6[lane * 6 + 0] * L.w[0];
+#pragma unroll
+            for (int k = 1; k < 6; k++) a = a + L.K6[lane * 6 + k] * L.w[k];
+            L.sol[lane] = a + L.vec[lane];
+        }
+        WAVE_SYNC();
+        SPH_MARK(5);
+        SOLVE_MARK(7);
     }
-    WAVE_SYNC();
-    SPH_MARK(5);
-    SOLVE_MARK(7);
-    // 8. boxplus, convergence, rematch control (laser_mapping.cpp:204-237), lane 0 on
-    // the staged state; the stores below go out behind the solve (nothing waits for them)
-    int stop_now = 0, converged_i = 0;
-    if (lane == 0) {
+    // 8. boxplus, convergence, rematch control (laser_mapping.cpp:204-237) on the
+    // staged state, the whole wave: every lane forms Exp(sol(0:3)) and the control
+    // from the same values (one SIMT pass of the sin / cos chain instead of lane 0
+    // alone walking the state), lanes 0..8 the new rotation, 9..23 the additive
+    // parts; the stores below go out behind the solve (nothing waits for them)
+    int stop_now = 0;
+    {
         IekfCtrl ctrl = ctrl0;
-        double sol[kDim];
+        const double v0 = L.sol[0], v1 = L.sol[1], v2 = L.sol[2];
+        const double t0 = L.sol[3], t1 = L.sol[4], t2 = L.sol[5];
+        double rot[9], E[9];
 #pragma unroll
-        for (int k = 0; k < kDim; k++) sol[k] = L.sol[k];
-        state_boxplus_d(L.st, sol);
-        const double rn = sqrt((sol[0] * sol[0] + sol[1] * sol[1]) + sol[2] * sol[2]);
-        const double tn = sqrt((sol[3] * sol[3] + sol[4] * sol[4]) + sol[5] * sol[5]);
+        for (int k = 0; k < 9; k++) rot[k] = L.st.rot[k];
+        so3_exp(v0, v1, v2, E);  // StatesGroup += (common_lib.h:565-574): rot * Exp(sol(0:3))
+        const double rn = sqrt((v0 * v0 + v1 * v1) + v2 * v2);
+        const double tn = sqrt((t0 * t0 + t1 * t1) + t2 * t2);
         const bool converged = (rn * 180 / (3.14159265358) < 0.01) && (tn * 100 < 0.015);
         const int searched = ctrl.search_en;
         bool next_search = false;
@@ -2435,8 +2586,7 @@ __device__ __forceinline__ int solve_scan(IekfSlot* slot, SolveLds& L, const int
             ctrl.rematch_num++;
         }
         const bool stop = (ctrl.rematch_num >= 2 || (ctrl.iter_count == ctrl.max_iter - 1));
-        converged_i = converged ? 1 : 0;
-        ctrl.converged = converged_i;
+        ctrl.converged = converged ? 1 : 0;
         ctrl.last_search = searched;
         ctrl.search_en = next_search ? 1 : 0;
         ctrl.iter_count++;
@@ -2444,14 +2594,26 @@ __device__ __forceinline__ int solve_scan(IekfSlot* slot, SolveLds& L, const int
         // the loop condition iterCount < NUM_MAX_ITERATIONS (:178) also ends it
         ctrl.stop = (stop || ctrl.iter_count >= ctrl.max_iter || ctrl.n_evals >= LIVO_MAX_EVALS) ? 1 : 0;
         stop_now = stop ? 1 : 0;
-        L.ctrl = ctrl;
+        if (lane < 9) {  // mat3_mul(rot, E) entry (r, c), sums in index order
+            const int r = lane / 3, c = lane % 3;
+            double a0 = 0.0, a1 = 0.0, a2 = 0.0, e0 = 0.0, e1 = 0.0, e2 = 0.0;
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                if (r == k) { a0 = rot[k * 3 + 0]; a1 = rot[k * 3 + 1]; a2 = rot[k * 3 + 2]; }
+                if (c == k) { e0 = E[0 * 3 + k]; e1 = E[1 * 3 + k]; e2 = E[2 * 3 + k]; }
+            }
+            L.st.rot[lane] = (a0 * e0 + a1 * e1) + a2 * e2;
+        } else if (lane < kStHead) {  // pos, vel, bias_g, bias_a, gravity += sol(3:18)
+            L.st.rot[lane] = L.st.rot[lane] + L.sol[lane - 6];
+        }
+        if (lane == 0) L.ctrl = ctrl;
     }
     stop_now = __builtin_amdgcn_readfirstlane(stop_now);
     WAVE_SYNC();
     SOLVE_MARK(8);
     SPH_MARK(6);
-    // stores: state head, statistics, control (the state and control write-through:
-    // k_iekf_ns's teams read them inside the launch)
+    // stores: state head, statistics, control (write-through: the stopping scan's
+    // host slot copy reads them back inside this launch)
     if (lane < kStHead) st_sc1(slot->state.rot + lane, L.st.rot[lane]);
     livo_iter_stats& S = slot->stats;
     if (e < LIVO_MAX_EVALS) {
@@ -2473,7 +2635,49 @@ __device__ __forceinline__ int solve_scan(IekfSlot* slot, SolveLds& L, const int
         st_sc1(reinterpret_cast<unsigned long long*>(&slot->ctrl) + lane, c);
     }
     // 9. covariance update state.cov = (I - G) * state.cov (:224-227) = P - G(:,0:6) P(0:6,:)
-    if (stop_now) {
+    if (stop_now && fac) {
+        // factored: G(:, 0:6) P(0:6, :) = B Q^-1 (L^T C L) B^T = B (I6 - Q^-1) B^T
+        if (lane < 6) {  // column `lane` of Q^-1 from the LDL^T factors
+            double x[6];
+#pragma unroll
+            for (int i = 0; i < 6; i++) {
+                double z = i == lane ? 1.0 : 0.0;
+#pragma unroll
+                for (int k = 0; k < i; k++) z = z - L.F[i * (i + 1) / 2 + k] * x[k];
+                x[i] = z;
+            }
+#pragma unroll
+            for (int i = 0; i < 6; i++) x[i] = x[i] * L.F[21 + i];
+#pragma unroll
+            for (int i = 4; i >= 0; i--) {
+                double z = x[i];
+#pragma unroll
+                for (int k = i + 1; k < 6; k++) z = z - L.F[k * (k + 1) / 2 + i] * x[k];
+                x[i] = z;
+            }
+#pragma unroll
+            for (int i = 0; i < 6; i++) L.Qi[i * 6 + lane] = x[i];
+        }
+        WAVE_SYNC();
+        auto brow = [&](int r) -> const double* { return r < 6 ? L.covL + r * 6 : L.covB + (r - 6) * 6; };
+        for (int t = lane; t < kDim * 6; t += 64) {  // V = B (I6 - Q^-1)
+            const int r = t / 6, c = t % 6;
+            const double* b = brow(r);
+            double v = b[0] * L.Qi[0 * 6 + c];
+#pragma unroll
+            for (int k = 1; k < 6; k++) v = v + b[k] * L.Qi[k * 6 + c];
+            L.V[t] = b[c] - v;
+        }
+        WAVE_SYNC();
+        for (int t = lane; t < kDim * kDim; t += 64) {  // cov = P - V B^T
+            const int i = t / kDim, j = t % kDim;
+            const double* b = brow(j);
+            double gp = L.V[i * 6 + 0] * b[0];
+#pragma unroll
+            for (int l = 1; l < 6; l++) gp = gp + L.V[i * 6 + l] * b[l];
+            st_sc1(slot->state.cov + t, s_P[t] - gp);
+        }
+    } else if (stop_now) {
         for (int t = lane; t < kDim * kDim; t += 64) {
             const int i = t / kDim, j = t % kDim;
             double gp = L.G6[i * 6 + 0] * s_P[0 * kDim + j];
@@ -2487,7 +2691,6 @@ __device__ __forceinline__ int solve_scan(IekfSlot* slot, SolveLds& L, const int
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
     SPH_MARK(7);
-    (void)converged_i;
     return stop_now;
 }
 
@@ -2682,7 +2885,7 @@ constexpr int kRedRows = kEvalBlock > 256 ? kEvalBlock / 16 : 16;  // 16-lane ro
 struct HsReduceLds {
     double red[kRedRows * kRedCols];      // one partial per 16-lane row
     double fin[kRedRows / 2 * kRedCols];  // the last block: one sum per 32-thread group
-    int last;
+    int last, last2;                      // this block completed its shard / the scan
 };
 // NU = kRedUsed + 2 (the fused evaluation): columns 29 / 30 carry the search's
 // hash-slot and map-point counts (integers, exact in double), reduced with the
@@ -2755,7 +2958,7 @@ constexpr int kRedInFlight = LIVO_RED_INFLIGHT;  // partial loads in flight per 
 // back past the L1 (sc1: this CU's other waves stored it, drained to L2).
 __device__ __forceinline__ void hs_host_slot(const HsJob& job, const IekfSlot* slot, int t, int nt) {
     const unsigned long long* src = reinterpret_cast<const unsigned long long*>(slot);
-    for (int w = t; w < (int)((kSlotLmBytes + 15) / 16); w += nt) {
+    for (int w = t; w < (int)((kSlotWbBytes + 15) / 16); w += nt) {
         const unsigned long long lo = __hip_atomic_load(gptr(src + 2 * w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long hi = __hip_atomic_load(gptr(src + 2 * w + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         job.host_slot[w] = make_uint4((unsigned)lo, (unsigned)(lo >> 32), (unsigned)hi, (unsigned)(hi >> 32));
@@ -2796,14 +2999,28 @@ __device__ __forceinline__ void hs_scan_tail(const HsParams& P, const HsJob& job
 #endif
 );
 
-// Block partials of a scan's h_share sums -> the last block of the scan
-// reduces every partial in a fixed order and (P.solve) its wave 0 runs the
-// scan's solve.  nblk = partials (256-point chunks) of the scan in this launch;
-// this block has stored `count` of them (hs_block_partial) before the call.
+// Block partials of a scan's h_share sums -> a two-level fixed-order reduction
+// -> (P.solve) the scan's solve.  nblk = partials (256-point chunks) of the scan
+// in this launch; this block has stored partial `blk` (hs_block_partial).
+//
+// Level 1: partial b belongs to shard b % K (K = min(kRedShards, nblk)); each
+// shard has a ticket of its own (a 128-B line of the slot), so ~nblk / K blocks
+// contend per counter instead of every block of the scan on one (a device-scope
+// atomic serialises per line: ~12 ns each, 391 arrivals ~4.7 us,
+// MI355X_MICROARCH.md fan-in).  The block that completes a shard sums its
+// partials (~nblk / K rows, all loads in flight at once: ~6 per thread) in a
+// fixed order into row s of the partial buffer.  Level 2: that block takes the
+// scan's ticket; the last of the K reduces rows 0..K-1 and solves (hs_scan_tail).
+// The scan's last block thus reads K rows instead of every partial (~97 KB at
+// 100k points), and the per-shard work runs on K CUs at once.  Every hand-off
+// is sc1 stores drained by s_waitcnt vmcnt(0) before an agent-scope atomic, and
+// sc1 loads after it (MI355X_MICROARCH.md, Workgroup dispatch: sc1 hand-off).
+// The sums' order depends only on nblk, not on arrival order: deterministic.
 template <int NT, int NU = kRedUsed>
 __device__ __forceinline__ void hs_ticket_tail(const HsParams& P, const HsJob& job, IekfSlot* slot, int nblk,
-                                               unsigned count, HsReduceLds& R, SolveLds& L, int pk = -1) {
+                                               unsigned blk, HsReduceLds& R, SolveLds& L, int pk = -1) {
     static_assert(NU == kRedUsed || NU == kRedUsed + 2, "h_share sums (+ search counts)");
+    static_assert(NT / 32 <= kRedRows / 2, "R.fin holds one row per 32-thread group");
     const int tid = threadIdx.x;
 #ifdef LIVO_TAIL_PROF
     unsigned long long tp = __builtin_amdgcn_s_memtime();
@@ -2811,25 +3028,68 @@ __device__ __forceinline__ void hs_ticket_tail(const HsParams& P, const HsJob& j
 #else
     (void)pk;
 #endif
-    // Wave 0 stored the block partials write-through (sc1) and, once the stores
-    // have drained, takes the scan's ticket; the last block of the scan then
-    // reduces every partial with sc1 loads in a fixed order and its wave 0 runs
-    // the scan's solve (MI355X_MICROARCH.md §Workgroup dispatch: sc1 hand-off,
-    // no L2 write-back fence).  One launch less per evaluation than a separate
-    // solve kernel.
+    const int K = nblk < kRedShards ? nblk : kRedShards;
+    const int sh = (int)(blk % (unsigned)K);
+    const int cnt = (nblk - sh + K - 1) / K;  // partials of shard sh: sh, sh + K, ...
+    unsigned* const sh_ticket = slot->sh_ticket + 32 * sh;
+    // wave 0 stored the partial write-through; once drained, the shard's ticket
     if (tid < 64) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (tid == 0)
-            R.last = __hip_atomic_fetch_add(gptr(&slot->hs_ticket), count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                     (unsigned)nblk - count;
+            R.last = __hip_atomic_fetch_add(gptr(sh_ticket), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                     (unsigned)cnt - 1u;
     }
     __syncthreads();
     TAIL_MARK(1, tp);
     if (!R.last) return;
+    if (cnt > 1) {
+        // thread (g, c) sums rows sh + K (g + G t), t = 0, 1, ... of column c in that
+        // order, every load in flight at once (G = NT / 32 groups)
+        constexpr int G = NT / 32;
+        constexpr int kMaxPer = 8;  // loads per thread per round (nblk <= 8 G K in one round)
+        const int c = tid & 31, g = tid >> 5;
+        double acc = 0.0;
+        if (c < NU) {
+            const double* src = job.partial + c;
+            for (int j0 = g; j0 < cnt; j0 += kMaxPer * G) {
+                double v[kMaxPer];
+#pragma unroll
+                for (int k = 0; k < kMaxPer; k++) {
+                    const int j = j0 + G * k;
+                    v[k] = j < cnt ? ld_sc1(src + (size_t)(sh + K * j) * kRedCols) : 0.0;
+                }
+#pragma unroll
+                for (int k = 0; k < kMaxPer; k++) acc += v[k];
+            }
+        }
+        R.fin[g * kRedCols + c] = acc;
+        __syncthreads();
+        if (tid < NU) {
+            constexpr int NG = G > 8 ? G : 8;
+            double f[NG];
+#pragma unroll
+            for (int q = 0; q < NG; q++) f[q] = q < G ? R.fin[q * kRedCols + tid] : 0.0;
+#pragma unroll
+            for (int h = NG / 2; h >= 1; h >>= 1)  // ((f0 + f1) + (f2 + f3)) + ...
+#pragma unroll
+                for (int q = 0; q < h; q++) f[q] = f[2 * q] + f[2 * q + 1];
+            st_sc1(job.partial + (size_t)sh * kRedCols + tid, f[0]);  // row sh: the shard's sum
+        }
+    }
+    // the shard's ticket ready for the next pass; the shard's row drained, the scan's ticket
+    if (tid < 64) {
+        if (tid == 0) st_sc1(sh_ticket, 0u);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (tid == 0)
+            R.last2 = __hip_atomic_fetch_add(gptr(&slot->hs_ticket), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                      (unsigned)K - 1u;
+    }
+    __syncthreads();
+    if (!R.last2) return;
 #ifdef LIVO_TAIL_PROF
-    hs_scan_tail<NT, NU>(P, job, slot, nblk, R, L, pk, tp);
+    hs_scan_tail<NT, NU>(P, job, slot, K, R, L, pk, tp);
 #else
-    hs_scan_tail<NT, NU>(P, job, slot, nblk, R, L, pk);
+    hs_scan_tail<NT, NU>(P, job, slot, K, R, L, pk);
 #endif
 }
 
@@ -2938,7 +3198,7 @@ __device__ __forceinline__ void hshare_reduce_solve(const HsParams& P, const HsJ
                                                     const Col& col, int nblk, unsigned blk, HsReduceLds& R,
                                                     SolveLds& L, int pk = -1) {
     hs_block_partial<NT, NU>(job, col, blk, R);
-    hs_ticket_tail<NT, NU>(P, job, slot, nblk, 1u, R, L, pk);
+    hs_ticket_tail<NT, NU>(P, job, slot, nblk, blk, R, L, pk);
 }
 
 template <bool FIRST>
@@ -3054,9 +3314,6 @@ __device__ unsigned long long g_eval_tl[LIVO_MAX_EVALS][kTlBlocks][2];
 #ifndef LIVO_EVAL_WAVES
 #define LIVO_EVAL_WAVES 4  // waves per SIMD the VGPR budget must allow (<= 128 VGPRs)
 #endif
-#ifndef LIVO_NS_K
-#define LIVO_NS_K 4  // most 256-point chunks per block in an evaluation without a search (KnnParams::ns_k)
-#endif
 template <bool FIRST>
 __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalParams E) {
     const KnnParams& P = E.k;
@@ -3087,49 +3344,6 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
     bool prefit = false;  // the plane of this evaluation fitted in the search branch
     if (slot->ctrl.stop) return;  // block-uniform
     const int search = FIRST ? 1 : slot->ctrl.search_en;
-#if LIVO_NS_K > 1
-    if (!FIRST && !search && P.ns_k > 1) {  // (ns_k: kernel parameter, uniform; search: block-uniform)
-        // An evaluation without a search: the group leader (its place in the block
-        // order a multiple of K = ns_k, or the scan's chunk 0) takes chunks bx .. cend-1
-        // of its scan, K consecutive 256-point chunks, the others exit at once: a
-        // quarter of the blocks to dispatch, their loads all issued up front.  Each
-        // chunk's partial is the one-chunk block's (same columns, same fixed tree),
-        // so the sums are bit for bit those of one chunk per block.
-        const int K = min(P.ns_k, LIVO_NS_K);
-        const unsigned r = (bjob * (unsigned)P.nb + bx) % (unsigned)K;
-        if (r != 0u && bx != 0u) return;  // block-uniform
-        const int nblk = max(1, (job.n + kEvalBlock - 1) / kEvalBlock);
-        const int cend = min(nblk, (int)bx + K - (int)r);
-        HsPointIn pin_k[LIVO_NS_K];
-        pin_k[0] = pin;
-#pragma unroll
-        for (int k = 1; k < LIVO_NS_K; k++) {
-            const int ii = ((int)bx + k) * kEvalBlock + threadIdx.x;
-            pin_k[k] = ((int)bx + k < cend && ii < job.n) ? hshare_load(job, ii, true) : HsPointIn{};
-        }
-        const double inv_r = E.h.inv_r;
-#pragma unroll
-        for (int k = 0; k < LIVO_NS_K; k++) {
-            const int c = (int)bx + k;
-            if (c < cend) {  // uniform
-                if (k > 0) __syncthreads();  // wave 0 has read the last chunk's rows
-                HsRow w;
-                hs_row_clear(w);
-                const int ii = c * kEvalBlock + threadIdx.x;
-                if (ii < job.n) hshare_point(E.h, job, slot->state, ii, 0, w, pin_k[k], false);
-                auto col = [&](auto jc) -> double {
-                    constexpr int j = decltype(jc)::value;
-                    if constexpr (j < kRedUsed) return hs_col<j>(w, inv_r);
-                    else return 0.0;  // (no search: no hash-slot / map-point counts)
-                };
-                hs_block_partial<kEvalBlock, kRedUsed + 2>(job, col, (unsigned)c, U.rs.R);
-            }
-        }
-        hs_ticket_tail<kEvalBlock, kRedUsed + 2>(E.h, job, slot, nblk, (unsigned)(cend - (int)bx), U.rs.R,
-                                                 U.rs.solve, -1);
-        return;
-    }
-#endif
 #ifdef LIVO_EVAL_PROF
     const int tl_e = min(slot->ctrl.n_evals, LIVO_MAX_EVALS - 1);
 #endif
@@ -3321,215 +3535,6 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
         g_eval_tl[tl_e][blockIdx.x][1] = __builtin_amdgcn_s_memtime();
     }
 #endif
-}
-
-// ============================================ persistent evaluations =====
-// k_iekf_ns<K>: the evaluations WITHOUT a search of a group's scans in one
-// launch (laser_mapping.cpp:178-237 with nearest_search_en false: the plane of
-// the last search reused, residual gates, Jacobian, HᵀH / HᵀL, solve), as
-// many as the scans' control allows: a scan leaves the loop when its solve
-// stops it or asks for a search (k_iekf_eval does that evaluation).
-//
-// Each scan gets a team of T blocks (formed by arrival: block ticket t -> scan
-// t / T, rank t % T, so a team is always the first blocks to become resident
-// and no team waits on one that cannot start).  Rank r keeps the body points and
-// plane caches of chunks r, r + T, ... (K at most) in registers for the whole
-// loop, sums their rows per thread, and stores ONE block partial per
-// evaluation; the scan's last block (ticket) reduces the team's T partials and
-// solves (hs_ticket_tail, the same tail as k_iekf_eval), its state and control
-// stores write-through, then publishes the evaluation count (slot->gen, sc1).
-// The other blocks poll that word (one lane, s_sleep), read the new state and
-// control with sc1 loads and go on.  No launch boundary, no re-dispatch, no
-// reload of the points between evaluations, and T partials instead of one per
-// chunk.  Every spin is bounded (g_ns_timeouts counts a give-up).
-#ifndef LIVO_NS_ACC
-#define LIVO_NS_ACC 0
-#endif
-#ifndef LIVO_NS_WAVES
-#define LIVO_NS_WAVES 4  // waves per SIMD k_iekf_ns's VGPR budget allows
-#endif
-constexpr int kNsTeamMax = 64;
-constexpr unsigned kNsMaxSpins = 1u << 22;
-__device__ unsigned long long g_ns_timeouts;
-struct NsState {
-    double rot[9];
-    double pos[3];
-};
-struct NsLds {
-    HsReduceLds R;
-    SolveLds solve;
-    NsState st;
-    unsigned ticket;
-    int stop, search, abort;
-};
-__device__ __forceinline__ unsigned ld_sc1_u32(const unsigned* p) {
-    return __hip_atomic_load(gptr(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// Wait (thread 0, bounded) until the scan's word *w reaches `target`; 1 = gave up.
-__device__ __forceinline__ int ns_wait(const unsigned* w, unsigned target) {
-    unsigned spins = 0;
-    while (ld_sc1_u32(w) < target) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > kNsMaxSpins) {
-            atomicAdd(&g_ns_timeouts, 1ull);
-            return 1;
-        }
-    }
-    return 0;
-}
-
-__global__ __launch_bounds__(kEvalBlock, LIVO_NS_WAVES) void k_iekf_ns(EvalParams E, unsigned* team_ctr, int T) {
-    __shared__ NsLds L;
-    const int tid = threadIdx.x;
-    if (tid == 0) L.ticket = atomicAdd(team_ctr, 1u);
-    __syncthreads();
-    const unsigned tk = __builtin_amdgcn_readfirstlane(L.ticket);  // (uniform: the job in scalar registers)
-    const unsigned bjob = tk / (unsigned)(T + 1), r = tk % (unsigned)(T + 1);
-    // the job in scalar registers: the ticket atomic above rules out scalar loads
-    // (a store may precede them), so each word is loaded and made uniform
-    HsJob job;
-    {
-        static_assert(sizeof(HsJob) % 4 == 0, "HsJob words");
-        const unsigned* src = reinterpret_cast<const unsigned*>(E.k.jobs + bjob);
-        unsigned* dst = reinterpret_cast<unsigned*>(&job);
-#pragma unroll
-        for (int w = 0; w < (int)(sizeof(HsJob) / 4); w++) dst[w] = __builtin_amdgcn_readfirstlane(src[w]);
-    }
-    IekfSlot* slot = job.slot;
-    const int nblk = max(1, (job.n + kEvalBlock - 1) / kEvalBlock);
-    const int Ts = min(T, nblk);  // the scan's workers (its partials)
-    if ((int)r >= Ts && (int)r != T) return;  // a scan smaller than the team: a block with no chunk
-    // control and state at entry (stored before this launch)
-    if (slot->ctrl.stop || slot->ctrl.search_en) return;  // block-uniform
-    unsigned target = (unsigned)slot->ctrl.n_evals;
-#if LIVO_NS_ACC
-    const unsigned nparts = (unsigned)Ts;  // the solver's: one partial per worker
-#else
-    const unsigned nparts = (unsigned)nblk;  // one per chunk
-#endif
-    if ((int)r == T) {
-        // the scan's solver: waits for the workers' Ts partials, reduces them in a
-        // fixed order and solves (hs_scan_tail, k_iekf_eval's tail), then publishes
-        // the evaluation (slot->gen) once its state and control stores have drained
-#pragma unroll 1
-        for (int it = 0; it < LIVO_MAX_EVALS; it++) {
-            if (tid == 0) L.abort = ns_wait(&slot->hs_ticket, (unsigned)nparts);
-            __syncthreads();
-            if (L.abort) return;
-#ifdef LIVO_TAIL_PROF
-            hs_scan_tail<kEvalBlock, kRedUsed + 2>(E.h, job, slot, (int)nparts, L.R, L.solve, -1, 0ull);
-#else
-            hs_scan_tail<kEvalBlock, kRedUsed + 2>(E.h, job, slot, (int)nparts, L.R, L.solve, -1);
-#endif
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            target++;
-            if (tid == 0) {
-                st_sc1(&slot->gen, target);
-                L.stop = ld_sc1(&slot->ctrl.stop);
-                L.search = ld_sc1(&slot->ctrl.search_en);
-            }
-            __syncthreads();
-            if (L.stop || L.search) return;
-        }
-        return;
-    }
-    // a worker: chunks r, r + T, ... (nk of them)
-    const int nk = (nblk - (int)r + T - 1) / T;
-    // the planes a search left unfitted (a point beyond the sqdist gate: plane state 0)
-    // are fitted now, as the first evaluation without a search would: the loop below
-    // then reads every plane from the cache
-#pragma unroll 1
-    for (int k = 0; k < nk; k++) {
-        const int i = ((int)r + T * k) * kEvalBlock + tid;
-        if (i < job.n && job.pstate[i] == 0) {
-            const float4* rec = reinterpret_cast<const float4*>(job.nn + i);
-            float4 nb[kNN];
-#pragma unroll
-            for (int q = 0; q < kNN; q++) nb[q] = rec[q];
-            float4 pl;
-            (void)fit_plane(E.h, job, i, 0, nb, reinterpret_cast<const int4*>(job.nn + i)[6].y, pl);
-        }
-    }
-    if (tid < 12) (tid < 9 ? L.st.rot[tid] : L.st.pos[tid - 9]) = slot->state.rot[tid];  // (rot, pos contiguous)
-    __syncthreads();
-    const double inv_r = E.h.inv_r;
-#pragma unroll 1
-    for (int it = 0; it < LIVO_MAX_EVALS; it++) {
-#if LIVO_NS_ACC
-        // (variant) per-thread sums over the block's chunks, ONE partial per worker:
-        // not the summation order of the launch per evaluation
-        double acc[kRedUsed];
-#pragma unroll
-        for (int j = 0; j < kRedUsed; j++) acc[j] = 0.0;
-        {
-            int i = (int)r * kEvalBlock + tid;
-            HsPointIn nxt = i < job.n ? hshare_load(job, i, true) : HsPointIn{};
-#pragma unroll 1
-            for (int k = 0; k < nk; k++) {
-                HsPointIn in = nxt;
-                const int inext = i + T * kEvalBlock;
-                if (k + 1 < nk && inext < job.n) nxt = hshare_load(job, inext, true);
-                if (i < job.n) {
-                    HsRow w;
-                    hs_row_clear(w);
-                    hshare_point<NsState, true>(E.h, job, L.st, i, 0, w, in);
-                    hs_accumulate(acc, w, inv_r);
-                }
-                i = inext;
-            }
-        }
-        auto col = [&](auto jc) -> double {
-            constexpr int j = decltype(jc)::value;
-            if constexpr (j < kRedUsed) return acc[j];
-            else return 0.0;
-        };
-        hs_block_partial<kEvalBlock, kRedUsed + 2>(job, col, r, L.R);
-        const unsigned nparts = 1u;
-#else
-        const unsigned nparts = (unsigned)nk;
-        // one partial per chunk, each the one-chunk block's of k_iekf_eval (same rows,
-        // same fixed tree): the scan's sums are bit for bit those of the launch per
-        // evaluation.  The next chunk's points load while this one's rows reduce.
-        int i = (int)r * kEvalBlock + tid;
-        HsPointIn nxt = i < job.n ? hshare_load(job, i, true) : HsPointIn{};
-#pragma unroll 1
-        for (int k = 0; k < nk; k++) {
-            const int c = (int)r + T * k;
-            HsPointIn in = nxt;
-            const int inext = i + T * kEvalBlock;
-            if (k + 1 < nk && inext < job.n) nxt = hshare_load(job, inext, true);
-            HsRow w;
-            hs_row_clear(w);
-            if (i < job.n) hshare_point<NsState, true>(E.h, job, L.st, i, 0, w, in);
-            auto col = [&](auto jc) -> double {
-                constexpr int j = decltype(jc)::value;
-                if constexpr (j < kRedUsed) return hs_col<j>(w, inv_r);
-                else return 0.0;  // (no search: no hash-slot / map-point counts)
-            };
-            if (k > 0) __syncthreads();  // wave 0 has read the last chunk's rows
-            hs_block_partial<kEvalBlock, kRedUsed + 2>(job, col, (unsigned)c, L.R);
-            i = inext;
-        }
-#endif
-        target++;
-        if (tid < 64) {  // the partials have drained: count them
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (tid == 0) {
-                __hip_atomic_fetch_add(gptr(&slot->hs_ticket), nparts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                L.abort = ns_wait(&slot->gen, target);
-                if (!L.abort) {
-                    L.stop = ld_sc1(&slot->ctrl.stop);
-                    L.search = ld_sc1(&slot->ctrl.search_en);
-                }
-            }
-        }
-        __syncthreads();
-        if (L.abort) return;
-        if (tid < 12) (tid < 9 ? L.st.rot[tid] : L.st.pos[tid - 9]) = ld_sc1(slot->state.rot + tid);
-        __syncthreads();
-        if (L.stop || L.search) return;
-    }
 }
 
 // Per-point persistent selection of the IKFoM h-model: point_selected_surf is a
@@ -4300,27 +4305,6 @@ int launch_iekf_eval(const KnnParams& kp, const HsParams& hp, int n_jobs, int64_
     else
         hipLaunchKernelGGL(k_iekf_eval<false>, grid, block, 0, (hipStream_t)stream, E);
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
-}
-
-// k_iekf_ns for a group: T blocks per scan, K chunks per block at most (8 or
-// 12); LIVO_E_RANGE when the scans are too large for that (the caller then
-// runs the evaluations one launch each).  team_ctr: zeroed before the launch.
-int ns_team_size(int64_t max_n, int team) {
-    const int64_t nblk = std::max<int64_t>(1, (max_n + kEvalBlock - 1) / kEvalBlock);
-    return (int)std::min<int64_t>(std::max(1, std::min(team, kNsTeamMax)), nblk);
-}
-int launch_iekf_ns(const KnnParams& kp, const HsParams& hp, int n_jobs, int T, unsigned* team_ctr, void* stream) {
-    if (n_jobs <= 0 || T <= 0 || T > kNsTeamMax) return n_jobs <= 0 ? LIVO_OK : LIVO_E_RANGE;
-    EvalParams E;
-    E.k = kp;
-    E.h = hp;
-    const dim3 grid((unsigned)((T + 1) * n_jobs)), block(kEvalBlock);  // T workers + a solver per scan
-    hipLaunchKernelGGL(k_iekf_ns, grid, block, 0, (hipStream_t)stream, E, team_ctr, T);
-    return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
-}
-extern "C" int livo_debug_ns_timeouts(unsigned long long* out) {  // k_iekf_ns spins given up
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ns_timeouts), sizeof(unsigned long long)) == hipSuccess ? LIVO_OK
-                                                                                                        : LIVO_E_HIP;
 }
 
 int launch_hshare(const HsParams& p, int n_jobs, int max_nblk, bool first, void* stream) {

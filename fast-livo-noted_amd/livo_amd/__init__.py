@@ -168,7 +168,6 @@ SIGNATURES = {
     "livo_knn": (C.c_int, [_P, _P, C.c_int64, C.c_int32, _P, _P]),
     "livo_scan_upload": (C.c_int, [_P, _P, C.c_int64, C.c_int64, C.POINTER(C.c_int32)]),
     "livo_scan_upload_async": (C.c_int, [_P, _P, C.c_int64, C.c_int64, C.POINTER(C.c_int32)]),
-    "livo_debug_ns_timeouts": (C.c_int, [C.POINTER(C.c_ulonglong)]),
     "livo_debug_map_rebuilds": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64)]),
     "livo_scan_upload_batch_async": (C.c_int, [_P, _P, _P, C.c_int32, C.c_int64, _P]),
     "livo_host_register": (C.c_int, [_P, _P, C.c_size_t]),

@@ -501,9 +501,6 @@ int livo_map_last_add_stats(livo_ctx* ctx, livo_map_add_stats* out);
 int livo_frame_to_world(livo_ctx* ctx, int32_t scan_id, const livo_state* state, livo_raw_point* out, int64_t cap,
                         int64_t* n);
 int livo_sync(livo_ctx* ctx);
-/* Diagnostics: the persistent evaluation loop's bounded spins that gave up
- * (LIVO_PERSIST=1; device-wide since the library loaded; 0 on a healthy run). */
-int livo_debug_ns_timeouts(unsigned long long* out);
 /* Diagnostics: the incremental map's grid rebuilds since the context was made,
  * out[0] by a sort of every id, out[1] by merging the added ids into the grid;
  * out[2] the Add_Points batches redone with 64-bit box keys (a wrapped-key clash),

@@ -324,6 +324,46 @@ def test_add_points_wrapped_box_key_clash(ictx):
     assert ictx.map_rebuilds()[2] == r0 + 1
 
 
+def test_add_points_wrapped_box_key_clash_fused(ictx):
+    """The same clash on a call that takes the fused pass (the map has changed
+    already, so the merged rebuild runs inside Add_Points' stream pass and
+    refills the table with its bound's size): the 64-bit-key redo must read the
+    grid's own table, so the map equals the oracle's, the redo ran and the
+    fused rebuild ran in it."""
+    rng = np.random.default_rng(22)
+    ds = 0.05
+    m = rng.uniform(0, 2, (400, 3)).astype(f32)
+    dm = _pair(ictx, m)
+    fused = False
+    for _ in range(4):  # no clash; until the merged rebuild runs inside Add_Points' pass
+        r0 = ictx.map_rebuilds()
+        W1 = rng.uniform(0, 2, (200, 3)).astype(f32)
+        _same_add(ictx.map_add_points(W1, ds), dm.add_points(W1, ds))
+        _same_map(ictx, dm)
+        if ictx.map_rebuilds()[3] == r0[3] + 1:
+            fused = True
+            break
+    assert fused
+    base = rng.uniform(0, 2, (120, 3))
+    W = np.concatenate([base, base[:40] + [1024 * ds, 0, 0], base[40:80] + [1024 * ds, 1024 * ds, 1024 * ds]])
+    W = W[rng.permutation(len(W))].astype(f32)
+    r0 = ictx.map_rebuilds()
+    _same_add(ictx.map_add_points(W, ds), dm.add_points(W, ds))
+    _same_map(ictx, dm)
+    r1 = ictx.map_rebuilds()
+    assert r1[2] == r0[2] + 1  # redone with the 64-bit keys
+    assert r1[3] == r0[3] + 1  # and the redo's merged rebuild ran in its pass
+    for _ in range(2):  # later adds read the grid's table after the redo
+        W3 = rng.uniform(0, 2, (150, 3)).astype(f32)
+        _same_add(ictx.map_add_points(W3, ds), dm.add_points(W3, ds))
+        _same_map(ictx, dm)
+    q = rng.uniform(0, 2, (500, 3)).astype(f32)
+    gi, gd = ictx.knn(q)
+    ri, rd = dm.knn(q)
+    assert np.array_equal(gi, ri)
+    assert np.array_equal(gd.view(np.uint32), rd.view(np.uint32))
+
+
 def test_add_points_large_multi_tile(built):
     """Scans of 60k points into a 400k-point map: the one-launch scans span more
     than one 64-tile look-back window (k_scan_boxes ~118 tiles, the merged

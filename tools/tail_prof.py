@@ -46,14 +46,18 @@ def main():
     n = min(len(w) for w in wins)
     print("per-evaluation windows (us, mean of 5 synchronous batches, max over groups):",
           [round(1e3 * sum(w[e] for w in wins) / len(wins), 1) for e in range(n)])
-    names = ("P+C", "M", "LU", "Minv+w", "K6", "G6+sol", "boxplus+ctrl", "stores+cov")
+    # factored path (cov_ok): C, T = C L, Q + LDL^T, w / u (incl. the wait for vec), y, sol; LU path: C, M, LU, ...
+    names = ("C", "T|M", "Q+LDL|LU", "w,u|Minv+w", "y|K6", "sol|G6+sol", "boxplus+ctrl", "stores+cov")
     for s, name in ((2, "first-search"), (1, "rematch"), (0, "no-search")):
         r = tbuf[8 * s: 8 * s + 8]
         nb, nl = max(r[0], 1), max(r[5], 1)
         print(f"{name:12s}: bfly+ticket {r[1] / nb * us:6.2f} us/block; last block ({r[5]}): partial reduction "
               f"{r[2] / nl * us:6.2f}  solve {r[3] / nl * us:6.2f}  slot write {r[4] / nl * us:6.2f} us")
-        ph = tbuf[24 + 16 * s: 24 + 16 * s + 8]
+        ph = tbuf[24 + 16 * s: 24 + 16 * s + 16]
         print("    solve: " + "  ".join(f"{k} {v / nl * us:.2f}" for k, v in zip(names, ph)) + " us")
+        if ph[8] or ph[9]:  # LIVO_TAIL_TWICE: the same T / Q code timed cold (first pass) and warm (second)
+            print(f"    I-cache probe: T cold {ph[8] / nl * us:.2f} warm {ph[1] / nl * us:.2f} us;  Q cold "
+                  f"{ph[9] / nl * us:.2f} us")
 
 
 if __name__ == "__main__":
