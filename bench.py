@@ -601,21 +601,28 @@ def main():
             ctx.iekf_update_batch([sids[j]], one, raw=True)
         sync()
         lat = (time.perf_counter() - t) / reps
+
+        def upload_pass():
+            for k in range(a.batch):
+                C.memmove(one, C.byref(init, k * C.sizeof(livo_amd.State)), C.sizeof(livo_amd.State))
+                sid = ctx.scan_upload(scans[k])
+                ctx.iekf_update_batch([sid], one, raw=True)
+                ctx.scan_release(sid)
+
+        upload_pass()  # warm: a frame loop reuses the released scan buffers after its first frame
         sync()
         t = time.perf_counter()
-        for k in range(a.batch):
-            C.memmove(one, C.byref(init, k * C.sizeof(livo_amd.State)), C.sizeof(livo_amd.State))
-            sid = ctx.scan_upload(scans[k])
-            ctx.iekf_update_batch([sid], one, raw=True)
-            ctx.scan_release(sid)
+        for _ in range(2):
+            upload_pass()
         sync()
-        lat_up = (time.perf_counter() - t) / a.batch
+        lat_up = (time.perf_counter() - t) / (2 * a.batch)
         if rank == 0:
             result["drop_in"] = {"ms_per_scan": round(lat * 1e3, 4), "updates_per_s": round(1.0 / lat, 2),
                                  "ms_per_scan_with_upload": round(lat_up * 1e3, 4),
                                  "note": "batch 1, sequential: livo_iekf_update on a resident scan; then "
                                          "livo_scan_upload (host points -> HBM, device Morton sort) + update + "
-                                         "release per scan, host-timed"}
+                                         "release per scan, host-timed over two passes after one warm pass (the "
+                                         "released buffers reused, as a frame loop does)"}
 
     # ---- config 5 (BASELINE configs[4]): 10M-point map, 200k-point scans at
     # filter_size_surf = 0.05: each scan is the device VoxelGrid (leaf 0.05,
@@ -764,21 +771,26 @@ def main():
         sync()
         iv_elapsed = time.perf_counter() - t
         iv_total = farm.Counters(scans=iv_steps * a.batch, evals=iv_evals)
-        # odometry: one scan after the other, each updated then merged into the map
-        odo_sids = [ctx.scan_upload(sc) for sc in scans]
-        sync()
-        t = time.perf_counter()
-        t_incr = 0.0
-        added = 0
-        for sid, s in zip(odo_sids, st0):
-            st, _ = ctx.iekf_update(sid, s)
-            t1 = time.perf_counter()
-            _, cnt = ctx.map_incremental(sid, st, filter_size_map=0.5)
-            t_incr += time.perf_counter() - t1
-            added += cnt["added"] + cnt["no_downsample"]
-        sync()
-        odo_elapsed = time.perf_counter() - t
-        for sid in odo_sids + iv_sids:
+        # odometry: one scan after the other, each updated then merged into the map;
+        # two passes over the scans (fresh scan buffers each), the second timed: the
+        # first warms the allocations and grows the map, as the ikd-Tree leg does
+        for rep in range(2):
+            odo_sids = [ctx.scan_upload(sc) for sc in scans]
+            sync()
+            t = time.perf_counter()
+            t_incr = 0.0
+            added = 0
+            for sid, s in zip(odo_sids, st0):
+                st, _ = ctx.iekf_update(sid, s)
+                t1 = time.perf_counter()
+                _, cnt = ctx.map_incremental(sid, st, filter_size_map=0.5)
+                t_incr += time.perf_counter() - t1
+                added += cnt["added"] + cnt["no_downsample"]
+            sync()
+            odo_elapsed = time.perf_counter() - t
+            for sid in odo_sids:
+                ctx.scan_release(sid)
+        for sid in iv_sids:
             ctx.scan_release(sid)
         # the whole per-frame pipeline on the device: raw
         # 100k-point frame -> UndistortPcl de-skew + VoxelGrid (filter_size_surf
@@ -822,7 +834,8 @@ def main():
                              "ms_per_scan": round(odo_elapsed / len(odo_sids) * 1e3, 3),
                              "map_incremental_ms_per_scan": round(t_incr / len(odo_sids) * 1e3, 3),
                              "points_added_per_scan": round(added / len(odo_sids), 1),
-                             "note": "sequential: livo_iekf_update + livo_map_incremental per scan (map grows)"},
+                             "note": "sequential: livo_iekf_update + livo_map_incremental per scan (map grows); "
+                                     "second pass over the scans timed (the first warms and grows the map)"},
                 "pipeline": {"frames_per_s": round(len(raws) / pipe_elapsed, 3),
                              "ms_per_frame": round(pipe_elapsed / len(raws) * 1e3, 3),
                              "preprocess_ms": round(t_pre / len(raws) * 1e3, 3),

@@ -205,19 +205,21 @@ __global__ __launch_bounds__(kKnnBlock) void k_ivox_knn(KnnParams P) {
     bool overflow;
     const int n = iv_query(P.iv, qx, qy, qz, a, kIvCap, overflow);
     if (overflow) {
-        const unsigned r = atomicAdd(P.replay_count, 1u);
-        P.replay_list[r] = ((unsigned long long)bjob << 32) | (unsigned)i;
+        const unsigned r = atomicAdd(P.replay_count2, 1u);
+        P.replay_list2[r] = ((unsigned long long)bjob << 32) | (unsigned)i;
         return;
     }
     if (n > 0) iv_write(job.nn + i, reinterpret_cast<const float4*>(P.iv.pts), a, n);
 }
 
+// The exact global-memory pass over the queries no other search could hold
+// (replay_list2): one query per thread, its candidates in a private slice.
 __global__ __launch_bounds__(64) void k_ivox_knn_big(KnnParams P) {
-    const unsigned cnt = *P.replay_count;
+    const unsigned cnt = *P.replay_count2;
     const unsigned tid = blockIdx.x * blockDim.x + threadIdx.x;
     SelElem* a = P.iv.scratch + (int64_t)tid * P.iv.slice;
     for (unsigned r = tid; r < cnt; r += gridDim.x * blockDim.x) {
-        const unsigned long long e = P.replay_list[r];
+        const unsigned long long e = P.replay_list2[r];
         const unsigned bjob = (unsigned)(e >> 32);
         const int i = (int)(e & 0xFFFFFFFFu);
         const HsJob job = P.jobs[bjob];
@@ -280,23 +282,12 @@ __device__ __forceinline__ void wave_write(NNRec* __restrict__ out, const float4
     }
 }
 
-template <bool LATER>
-__global__ __launch_bounds__(64 * kWaves) void k_ivox_knn_wave(KnnParams P) {
-    __shared__ WaveLds lds[kWaves];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    WaveLds& L = lds[w];
-    unsigned bjob, bx;
-    xcd_block(P.nb, bjob, bx);
-    const HsJob job = P.jobs[bjob];
-    const IekfSlot* slot = job.slot;
-    if (P.force >= 0) {
-        if (!P.force) return;
-    } else {
-        if (slot->ctrl.stop) return;
-        if (LATER && !slot->ctrl.search_en) return;
-    }
-    const int i = (int)bx * kWaves + w;
-    if (i >= job.n) return;
+// One query (point i of job) by the whole wave: the record written (or the
+// cache left as it is when no candidate is in range); true when it needs the
+// exact global-memory pass (a grid too large even for streaming, or an
+// introselect that exhausted its depth limit).
+__device__ __forceinline__ bool ivox_wave_query(const KnnParams& P, const HsJob& job, const IekfSlot* slot, int i,
+                                                WaveLds& L, int lane) {
     const IvoxParams& V = P.iv;
     const float4 b = reinterpret_cast<const float4*>(job.pts)[i];
     float qx, qy, qz;
@@ -304,7 +295,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_ivox_knn_wave(KnnParams P) {
     int kx, ky, kz;
     const float qlim = (float)(kIvMaxKey + 8);
     if (!iv_cell(qx, V.inv_res, qlim, kx) || !iv_cell(qy, V.inv_res, qlim, ky) || !iv_cell(qz, V.inv_res, qlim, kz))
-        return;  // no grid within reach: nothing found, the cache stays
+        return false;  // no grid within reach: nothing found, the cache stays
     // one nearby grid per lane
     uint2 run = make_uint2(0u, 0u);
     if (lane < V.nearby)
@@ -357,7 +348,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_ivox_knn_wave(KnnParams P) {
                 n = old + K;
             }
         }
-        if (ok && n == 0) return;  // no candidate: the cache stays
+        if (ok && n == 0) return false;  // no candidate: the cache stays
         if (ok && n > K) {
             ok = wave_nth(L, 0, K - 1, n, lane);
             n = K;
@@ -365,13 +356,9 @@ __global__ __launch_bounds__(64 * kWaves) void k_ivox_knn_wave(KnnParams P) {
         if (ok) ok = wave_nth(L, 0, 0, n, lane);
         if (ok) {
             wave_write(job.nn + i, pts, L, n, lane);
-            return;
+            return false;
         }
-        if (lane == 0) {  // a grid too large even for streaming, or a heap select
-            const unsigned r = atomicAdd(P.replay_count, 1u);
-            P.replay_list[r] = ((unsigned long long)bjob << 32) | (unsigned)i;
-        }
-        return;
+        return true;  // a grid too large even for streaming, or a heap select
     }
     if (lane <= kIvMaxNearby) L.m[lane] = 0u;
     // every raw point at once (raw index g = 64 r + lane, in grid order)
@@ -427,7 +414,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_ivox_knn_wave(KnnParams P) {
 #define IVDBG(tag, cnt)
 #endif
     IVDBG("staged", base);
-    if (base == 0) return;  // no candidate: the reference returns false, the cache stays
+    if (base == 0) return false;  // no candidate: the reference returns false, the cache stays
     // per grid: KNNPointByCondition's nth_element on its own run (ivox3d_node.hpp:179-183)
     const uint32_t mt = lane < V.nearby ? L.m[lane] : 0u;
     uint32_t s_incl = mt;
@@ -490,13 +477,57 @@ __global__ __launch_bounds__(64 * kWaves) void k_ivox_knn_wave(KnnParams P) {
         IVDBG("final", n);
         if (ok) {
             wave_write(job.nn + i, pts, L, n, lane);
-            return;
+            return false;
         }
     }
     // the depth limit ran out (libstdc++ would heap-select): the exact global-memory pass
-    if (lane == 0) {
-        const unsigned r = atomicAdd(P.replay_count, 1u);
-        P.replay_list[r] = ((unsigned long long)bjob << 32) | (unsigned)i;
+    return true;
+}
+
+template <bool LATER>
+__global__ __launch_bounds__(64 * kWaves) void k_ivox_knn_wave(KnnParams P) {
+    __shared__ WaveLds lds[kWaves];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    WaveLds& L = lds[w];
+    unsigned bjob, bx;
+    xcd_block(P.nb, bjob, bx);
+    const HsJob job = P.jobs[bjob];
+    const IekfSlot* slot = job.slot;
+    if (P.force >= 0) {
+        if (!P.force) return;
+    } else {
+        if (slot->ctrl.stop) return;
+        if (LATER && !slot->ctrl.search_en) return;
+    }
+    const int i = (int)bx * kWaves + w;
+    if (i >= job.n) return;
+    if (ivox_wave_query(P, job, slot, i, L, lane) && lane == 0) {
+        const unsigned r = atomicAdd(P.replay_count2, 1u);
+        P.replay_list2[r] = ((unsigned long long)bjob << 32) | (unsigned)i;
+    }
+}
+
+// The team search's overflow (replay_list: a list past kIvTeamCap entries), one
+// query per wave, grid-stride: a single 16-lane team cannot hold it, the wave's
+// LDS list (kWRaw raw points, streaming past that) can; what it cannot either
+// goes on to the global-memory pass.  (Before this pass every overflow query ran
+// on one thread of k_ivox_knn_big: ~0.6 ms per launch on a grown map, the long
+// pole of a single-scan iVox update.)
+__global__ __launch_bounds__(64 * kWaves) void k_ivox_knn_wave_list(KnnParams P) {
+    __shared__ WaveLds lds[kWaves];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    WaveLds& L = lds[w];
+    const unsigned cnt = *P.replay_count;
+    for (unsigned r = blockIdx.x * kWaves + w; r < cnt; r += gridDim.x * kWaves) {  // (wave-uniform)
+        const unsigned long long e = P.replay_list[r];
+        const unsigned bjob = (unsigned)(e >> 32);
+        const int i = (int)(e & 0xFFFFFFFFu);
+        const HsJob job = P.jobs[bjob];
+        if (ivox_wave_query(P, job, job.slot, i, L, lane) && lane == 0) {
+            const unsigned q = atomicAdd(P.replay_count2, 1u);
+            P.replay_list2[q] = e;
+        }
+        wave_sync();  // (L reused by the next entry)
     }
 }
 
@@ -511,7 +542,11 @@ __global__ __launch_bounds__(64 * kWaves) void k_ivox_knn_wave(KnnParams P) {
 // fewer lanes per query than the wave search.  A query whose list would
 // outgrow the capacity goes to the global-memory pass (k_ivox_knn_big).
 constexpr int kIvTeam = 16;
-constexpr int kIvTeamCap = 128;
+// list capacity per team: a query's list holds <= K survivors of every grid before
+// the current one plus all of the current grid's in-range points, so 18 x 5 + the
+// largest grid; 128 overflowed (to the wave pass) once map_incremental had grown
+// grids past ~38 points (32 KB of LDS per block: 5 blocks per CU)
+constexpr int kIvTeamCap = 256;
 __device__ __forceinline__ uint32_t team_bits(unsigned long long m, int lane) {
     return (uint32_t)(m >> (lane & 48)) & 0xFFFFu;
 }
@@ -631,24 +666,18 @@ __global__ __launch_bounds__(256) void k_ivox_knn_team(KnnParams P) {
     }
 }
 
-// Kernel choice per launch: the wave-cooperative search has ~20x less latency
-// per query (small scans: the IEKF of one downsampled frame), the team search
-// (16 lanes a query, list in LDS) more throughput when hundreds of thousands
-// of queries are in flight (scan farms); the one-query-per-thread search
-// (private candidate array, in scratch) is kept as a reference.
-// LIVO_IVOX_KIND=thread|wave|team forces one; LIVO_IVOX_WAVE_MAX sets the switch
-// point (queries per launch, default 131072).
-static int ivox_kind(int64_t queries) {
-    const char* e = std::getenv("LIVO_IVOX_KIND");  // read per launch (tests switch it)
-    const int forced = !e ? -1
-                          : (std::strcmp(e, "thread") == 0 ? 0
-                                                           : (std::strcmp(e, "wave") == 0 ? 1
-                                                                                          : (std::strcmp(e, "team") == 0 ? 2 : -1)));
+// Kernel choice per launch: the team search (16 lanes a query, list in LDS) by
+// default; the wave-cooperative search (a query per wave) for launches of at
+// most LIVO_IVOX_WAVE_MAX queries (default 0: never; a 100k-point scan alone
+// is throughput-bound too); the one-query-per-thread search (private candidate
+// array, in scratch) is kept as a reference.  IvoxParams::kind >= 0 (LIVO_IVOX_KIND
+// = thread | wave | team at livo_ivox_init) forces one.
+static int ivox_kind(const IvoxParams& V, int64_t queries) {
     static const int64_t wave_max = [] {
         const char* e = std::getenv("LIVO_IVOX_WAVE_MAX");
-        return e ? (int64_t)std::atoll(e) : (int64_t)131072;
+        return e ? (int64_t)std::atoll(e) : (int64_t)0;
     }();
-    if (forced >= 0) return forced;
+    if (V.kind >= 0) return V.kind;
     return queries <= wave_max ? 1 : 2;
 }
 
@@ -656,7 +685,7 @@ int launch_ivox_knn(const KnnParams& p, int n_jobs, int64_t max_n, bool later, i
                     void* stream) {
     if (n_jobs <= 0 || max_n <= 0) return LIVO_OK;
     KnnParams q = p;
-    const int kind = ivox_kind((int64_t)n_jobs * max_n);
+    const int kind = ivox_kind(p.iv, (int64_t)n_jobs * max_n);
     if (kind == 2) {
         q.nb = (int32_t)((max_n + (256 / kIvTeam) - 1) / (256 / kIvTeam));
         if ((int64_t)q.nb * n_jobs >= (1ll << 31)) return LIVO_E_RANGE;
@@ -683,6 +712,8 @@ int launch_ivox_knn(const KnnParams& p, int n_jobs, int64_t max_n, bool later, i
             hipLaunchKernelGGL((k_ivox_knn_wave<false>), grid, block, 0, (hipStream_t)stream, q);
     }
     if (hipGetLastError() != hipSuccess) return LIVO_E_HIP;
+    if (kind == 2)  // the team search's overflow, one query per wave
+        hipLaunchKernelGGL(k_ivox_knn_wave_list, dim3(256), dim3(64 * kWaves), 0, (hipStream_t)stream, q);
     const unsigned blocks = (unsigned)std::max<int64_t>(1, overflow_threads / 64);
     hipLaunchKernelGGL(k_ivox_knn_big, dim3(blocks), dim3(64), 0, (hipStream_t)stream, q);
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;

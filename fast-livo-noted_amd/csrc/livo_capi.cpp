@@ -75,6 +75,7 @@ static void free_scan_buf(ScanBuf& s) {
 // The device iVox map and its AddPoints / overflow-pass scratch.
 struct IvoxDev {
     bool ready = false;
+    int kind = -1;  // search kernel (IvoxParams::kind), LIVO_IVOX_KIND=thread|wave|team read by livo_ivox_init
     int64_t add_passes = 0;  // device passes AddPoints took (one per batch, more at LRU conflicts)
     livo_ivox_params prm{};
     float inv_res = 5.0f;
@@ -322,6 +323,10 @@ struct livo_ctx {
     unsigned long long* d_replay_total = nullptr;
     unsigned long long* d_replay_list = nullptr;
     int64_t replay_cap = 0;
+    // iVox: the wave pass's overflow for the global-memory pass (KnnParams::replay_list2);
+    // per group of lane 0 (the iVox batches are synchronous)
+    unsigned* d_replay_count2 = nullptr;
+    unsigned long long* d_replay_list2 = nullptr;
     // scratch for livo_knn / debug outputs
     void* scratch = nullptr;
     size_t scratch_bytes = 0;
@@ -500,10 +505,16 @@ static int ensure_replay(livo_ctx* c, int64_t total) {
         if (dev_alloc(&c->d_replay_total, 1)) return LIVO_E_OOM;
         HIP_TRY(hipMemset(c->d_replay_total, 0, sizeof(unsigned long long)));
     }
+    if (!c->d_replay_count2) {
+        if (dev_alloc(&c->d_replay_count2, (size_t)kMaxGroups)) return LIVO_E_OOM;
+        HIP_TRY(hipMemset(c->d_replay_count2, 0, sizeof(unsigned) * kMaxGroups));
+    }
     if (total <= c->replay_cap) return LIVO_OK;
     dev_free(c->d_replay_list);  // (hipFree waits for the device: no batch is still using it)
+    dev_free(c->d_replay_list2);
     c->replay_cap = 0;
     if (dev_alloc(&c->d_replay_list, (size_t)total * LIVO_MAX_INFLIGHT)) return LIVO_E_OOM;
+    if (dev_alloc(&c->d_replay_list2, (size_t)total)) return LIVO_E_OOM;
     c->replay_cap = total;
     return LIVO_OK;
 }
@@ -516,6 +527,8 @@ static KnnParams make_knn_params(livo_ctx* c) {
     kp.jobs = c->d_jobs;
     kp.replay_count = c->d_replay_count;
     kp.replay_list = c->d_replay_list;
+    kp.replay_count2 = c->d_replay_count2;
+    kp.replay_list2 = c->d_replay_list2;
     kp.replay_total = c->d_replay_total;
     std::memcpy(kp.R_LI, c->params.R_LI, sizeof(kp.R_LI));
     std::memcpy(kp.t_LI, c->params.t_LI, sizeof(kp.t_LI));
@@ -830,6 +843,7 @@ static IvoxParams ivox_params(livo_ctx* c) {
     P.log2 = v.log2;
     P.nearby = v.nearby;
     P.max_num = kNN;
+    P.kind = v.kind;
     P.range2 = 5.0 * 5.0;  // GetClosestPoint's default max_range (ivox3d.h:79), laser_mapping.cpp:520
     P.scratch = v.big;
     P.slice = v.big_slice;
@@ -1904,6 +1918,8 @@ int livo_ctx_destroy(livo_ctx* c) {
     dev_free(c->d_replay_count);
     dev_free(c->d_replay_total);
     dev_free(c->d_replay_list);
+    dev_free(c->d_replay_count2);
+    dev_free(c->d_replay_list2);
     dev_free(c->d_slots);
     dev_free(c->d_jobs);
     if (c->h_slots) (void)hipHostFree(c->h_slots);
@@ -2901,6 +2917,11 @@ static bool host_pinned(const void* p) {
     }
     return a.type == hipMemoryTypeHost;
 }
+// Both ends of [p, p + bytes) page-locked: a caller that registered a shorter
+// range than the array takes the staging path, not a device page fault.
+static bool host_pinned_range(const void* p, size_t bytes) {
+    return host_pinned(p) && (bytes <= 1 || host_pinned((const char*)p + bytes - 1));
+}
 
 int livo_host_register(livo_ctx* c, void* p, size_t bytes) {
     if (!c || !p || bytes == 0) return LIVO_E_INVALID;
@@ -2924,8 +2945,23 @@ int livo_host_unregister(livo_ctx* c, void* p) {
 // in the key's top bits) and one gather that also clears the neighbour
 // records, kFeSegMax scans at a time, on the upload stream.  Each scan is
 // stored exactly as livo_scan_upload stores it.
+static int upload_batch_chunks(livo_ctx* c, const float* const* xyz, const int64_t* N, int32_t n,
+                               int64_t stride_bytes, int32_t* scan_ids, int32_t* registered);
+
+// The scans are built in passes of kFeSegMax: a pass that fails releases the
+// scans the earlier passes of the same call registered, so a failed call leaves
+// no scan behind (scan_ids unspecified).
 int livo_scan_upload_batch_async(livo_ctx* c, const float* const* xyz, const int64_t* N, int32_t n,
                                  int64_t stride_bytes, int32_t* scan_ids) {
+    int32_t registered = 0;
+    const int rc = upload_batch_chunks(c, xyz, N, n, stride_bytes, scan_ids, &registered);
+    if (rc)
+        for (int32_t b = 0; b < registered; b++) (void)livo_scan_release(c, scan_ids[b]);
+    return rc;
+}
+
+static int upload_batch_chunks(livo_ctx* c, const float* const* xyz, const int64_t* N, int32_t n,
+                               int64_t stride_bytes, int32_t* scan_ids, int32_t* registered) {
     if (!c || !xyz || !N || !scan_ids || n < 0) return LIVO_E_INVALID;
     if (stride_bytes == 0) stride_bytes = 3 * sizeof(float);
     if (stride_bytes < (int64_t)(3 * sizeof(float))) return LIVO_E_INVALID;
@@ -2934,17 +2970,11 @@ int livo_scan_upload_batch_async(livo_ctx* c, const float* const* xyz, const int
         if (N[b] > (int64_t)0x7FFFFFFF - kBlock) return LIVO_E_RANGE;
     }
     if (set_device(c)) return LIVO_E_HIP;
-    if (!c->up_stream) {
-        // LIVO_UP_PRIO=1: the scan builds on a high-priority stream (its own hardware
-        // queue, ahead of the batches' kernels)
-        int lo = 0, hi = 0;
-        const char* pe = std::getenv("LIVO_UP_PRIO");
-        const bool prio = pe && std::atoi(pe) != 0 && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess;
-        if ((prio ? hipStreamCreateWithPriority(&c->up_stream, hipStreamNonBlocking, hi)
-                  : hipStreamCreateWithFlags(&c->up_stream, hipStreamNonBlocking)) != hipSuccess) {
-            c->up_stream = nullptr;
-            return LIVO_E_HIP;
-        }
+    // (the builds on a high-priority stream were slower: 3.8k vs 11.8k updates/s
+    // with uploads)
+    if (!c->up_stream && hipStreamCreateWithFlags(&c->up_stream, hipStreamNonBlocking) != hipSuccess) {
+        c->up_stream = nullptr;
+        return LIVO_E_HIP;
     }
     if (!c->cp_stream && hipStreamCreateWithFlags(&c->cp_stream, hipStreamNonBlocking) != hipSuccess) {
         c->cp_stream = nullptr;
@@ -2965,6 +2995,7 @@ int livo_scan_upload_batch_async(livo_ctx* c, const float* const* xyz, const int
             for (int32_t b = 0; b < m; b++) {
                 const int rc = livo_scan_upload(c, xyz[b0 + b], 0, stride_bytes, scan_ids + b0 + b);
                 if (rc) return rc;
+                *registered = b0 + b + 1;
             }
             continue;
         }
@@ -3002,7 +3033,7 @@ int livo_scan_upload_batch_async(livo_ctx* c, const float* const* xyz, const int
         const double t_a = trace ? now_us() : 0.0;
         bool direct = stride_bytes == (int64_t)(3 * sizeof(float));
         for (int32_t b = 0; b < m && direct; b++)
-            if (N[b0 + b] > 0 && !host_pinned(xyz[b0 + b])) direct = false;
+            if (N[b0 + b] > 0 && !host_pinned_range(xyz[b0 + b], (size_t)N[b0 + b] * 3 * sizeof(float))) direct = false;
         const double t_b = trace ? now_us() : 0.0;
         double t_c = t_b, t_d = t_b;
         int rc = LIVO_OK;
@@ -3058,14 +3089,10 @@ int livo_scan_upload_batch_async(livo_ctx* c, const float* const* xyz, const int
         } else {
             // page-locked caller arrays: one kernel reads them through their mapped
             // device addresses (no DMA command per scan: a hipMemcpyAsync of one
-            // held the host 13-16 ms now and then inside a running farm);
-            // LIVO_UPLOAD_DMA=1 or an unmapped array: DMA copies
-            static const bool use_dma = [] {
-                const char* e = std::getenv("LIVO_UPLOAD_DMA");
-                return e && std::atoi(e) != 0;
-            }();
+            // held the host 13-16 ms now and then inside a running farm); an
+            // array without a device mapping: DMA copies
             FeSrc F{};
-            bool mapped = !use_dma;
+            bool mapped = true;
             int64_t o = 0;
             for (int32_t b = 0; b < m; b++) {
                 F.off[b] = o;
@@ -3153,11 +3180,16 @@ int livo_scan_upload_batch_async(livo_ctx* c, const float* const* xyz, const int
             if (N[b0 + b] == 0) {  // (an empty scan has nothing to build)
                 release_scan_buf(c, sb[b]);
                 rc = livo_scan_upload(c, xyz[b0 + b], 0, stride_bytes, scan_ids + b0 + b);
-                if (rc) return rc;
+                if (rc) {
+                    for (int32_t q = b + 1; q < m; q++) release_scan_buf(c, sb[q]);  // (built, not registered)
+                    return rc;
+                }
+                *registered = b0 + b + 1;
                 continue;
             }
             sb[b].pending = true;
             scan_ids[b0 + b] = register_scan(c, sb[b]);
+            *registered = b0 + b + 1;
         }
     }
     return LIVO_OK;
@@ -3270,6 +3302,7 @@ int livo_h_share(livo_ctx* c, int32_t id, const livo_state* state, int search_en
         kp.force = 1;
         if (c->backend == LIVO_BACKEND_IVOX) {
             HIP_TRY(hipMemsetAsync(kp.replay_count, 0, sizeof(unsigned), c->stream));
+            HIP_TRY(hipMemsetAsync(kp.replay_count2, 0, sizeof(unsigned), c->stream));
             rc = backend_knn(c, kp, 1, N, false, c->stream);
         } else {
             rc = knn_pass(kp, 1, N, c->stream);
@@ -3431,49 +3464,6 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
     }
     rc = ensure_replay(c, total_n);
     if (rc) return rc;
-    // scans whose asynchronous upload may still run: the lane's stream 0 waits for
-    // them on the device (every group forks from it after the staging copy)
-    for (int32_t b = 0; b < n; b++) {
-        const ScanBuf* s = get_scan_q(c, ids[b]);
-        if (s->pending) HIP_TRY(hipStreamWaitEvent(B.st[0], s->ready, 0));
-    }
-    if (model == kModelIkfom)  // its searches rewrite the neighbours without refitting the cached planes
-        for (int32_t b = 0; b < n; b++) {
-            ScanBuf* s = get_scan_q(c, ids[b]);
-            if (s->n > 0) HIP_TRY(hipMemsetAsync(s->pstate, 0, (size_t)s->n, B.st[0]));
-        }
-    const bool prof = sync && L == 0 && c->profiling && c->events_ready;  // 1: first-search events only
-    const bool full = prof && c->profiling >= 2;         // 2: every evaluation, the batch span and the gap
-    if (full) {
-        HIP_TRY(hipEventRecord(c->b_start, c->stream));
-        // the replay count of this batch only (every batch's replays add to it)
-        HIP_TRY(hipMemsetAsync(c->d_replay_total, 0, 8, c->stream));
-    }
-    // queued behind another lane's batch on shared streams: with LIVO_LANE_SERIAL=1
-    // start only once all of its groups are done (default: as soon as stream 0 frees)
-    if (!c->lane_own_streams && c->lane_serial && c->last_lane >= 0 && c->last_lane != L &&
-        c->lane[c->last_lane].busy) {
-        const BatchLane& P = c->lane[c->last_lane];
-        for (int gi = 1; gi < P.ngroups; gi++) HIP_TRY(hipStreamWaitEvent(B.st[0], P.done[gi], 0));
-    }
-    c->last_lane = L;
-    // kernel copies for batches queued behind another on shared streams (a DMA
-    // copy there waits on an engine hand-off); LIVO_LANE_ZC=0: DMA copies always
-    const bool kcopy = (lm ? B.h_lm_dev != nullptr : B.h_ik_dev != nullptr) && (sync ? c->sync_zc : c->lane_zc);
-    const size_t ik_bytes = (size_t)n * (sizeof(IekfSlot) + sizeof(HsJob));
-    static_assert((sizeof(IekfSlot) + sizeof(HsJob)) % 16 == 0 && sizeof(IekfSlot) % 16 == 0, "16-B word copies");
-    if (lm && kcopy) {
-        rc = launch_copy_words(B.h_lm_dev, B.d_lm, lm_bytes(n), B.st[0]);
-        if (rc) return rc;
-    } else if (lm) {
-        HIP_TRY(hipMemcpyAsync(B.d_lm, B.h_lm, lm_bytes(n), hipMemcpyHostToDevice,
-                               B.st[0]));
-    } else if (kcopy) {
-        rc = launch_copy_words(B.h_ik_dev, B.d_ik, ik_bytes, B.st[0]);
-        if (rc) return rc;
-    } else {
-        HIP_TRY(hipMemcpyAsync(B.d_ik, B.h_ik, ik_bytes, hipMemcpyHostToDevice, B.st[0]));
-    }
 
     // The batch in groups on separate streams: the latency-bound kernels of
     // one group (18x18 solve, tie replay, launch gaps) overlap the
@@ -3510,14 +3500,55 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
             off += s->n;
         }
     }
+    const bool prof = sync && L == 0 && c->profiling && c->events_ready;  // 1: first-search events only
+    const bool full = prof && c->profiling >= 2;         // 2: every evaluation, the batch span and the gap
+    if (full) {
+        HIP_TRY(hipEventRecord(c->b_start, c->stream));
+        // the replay count of this batch only (every batch's replays add to it)
+        HIP_TRY(hipMemsetAsync(c->d_replay_total, 0, 8, c->stream));
+    }
+    // queued behind another lane's batch on shared streams: with LIVO_LANE_SERIAL=1
+    // start only once all of its groups are done (default: each group as soon as its
+    // own stream frees)
+    const BatchLane* prev = (!c->lane_own_streams && c->lane_serial && c->last_lane >= 0 && c->last_lane != L &&
+                             c->lane[c->last_lane].busy) ? &c->lane[c->last_lane] : nullptr;
+    c->last_lane = L;
+    // kernel copies for batches queued behind another on shared streams (a DMA
+    // copy there waits on an engine hand-off); LIVO_LANE_ZC=0: DMA copies always
+    const bool kcopy = (lm ? B.h_lm_dev != nullptr : B.h_ik_dev != nullptr) && (sync ? c->sync_zc : c->lane_zc);
+    static_assert(sizeof(HsJob) % 16 == 0 && sizeof(IekfSlot) % 16 == 0 && kLmStride % 16 == 0, "16-B word copies");
+    const char* const hsrc = lm ? (kcopy ? B.h_lm_dev : B.h_lm) : (kcopy ? B.h_ik_dev : B.h_ik);
+    const bool iv = c->backend == LIVO_BACKEND_IVOX && lm;  // (synchronous batches only: lane 0)
     unsigned* const rcount = c->d_replay_count + (size_t)L * kMaxGroups;  // this lane's
     unsigned long long* const rlist = c->d_replay_list + (size_t)L * c->replay_cap;
-    if (!fused) HIP_TRY(hipMemsetAsync(rcount, 0, sizeof(unsigned) * kMaxGroups, B.st[0]));
-    // profiling: the batch's first search starts at ev[0][0], before the fork
-    if (prof) HIP_TRY(hipEventRecord(c->ev[0][0], c->stream));
-    if (ngroups > 1) {
-        HIP_TRY(hipEventRecord(B.fork, B.st[0]));
-        for (int gi = 1; gi < ngroups; gi++) HIP_TRY(hipStreamWaitEvent(g[gi].st, B.fork, 0));
+    // Each group stages its own slots and jobs on its own stream and starts from
+    // there: no fork from stream 0, so a group waits only for its own scans'
+    // uploads and, in a pipelined farm, for its own stream's previous batch (a
+    // queued batch's group g no longer waits for the previous batch's group 0).
+    for (int gi = 0; gi < ngroups; gi++) {
+        const hipStream_t st = g[gi].st;
+        for (int32_t b = g[gi].first; b < g[gi].first + g[gi].count; b++) {
+            ScanBuf* s = get_scan_q(c, ids[b]);
+            // a scan whose asynchronous upload may still run: the group waits on the device
+            if (s->pending) HIP_TRY(hipStreamWaitEvent(st, s->ready, 0));
+            // IKFoM: its searches rewrite the neighbours without refitting the cached planes
+            if (model == kModelIkfom && s->n > 0) HIP_TRY(hipMemsetAsync(s->pstate, 0, (size_t)s->n, st));
+        }
+        if (prev)
+            for (int q = 0; q < prev->ngroups; q++) HIP_TRY(hipStreamWaitEvent(st, prev->done[q], 0));
+        const size_t s0 = (size_t)g[gi].first * stride, sb = (size_t)g[gi].count * stride;
+        const size_t j0 = (size_t)n * stride + (size_t)g[gi].first * sizeof(HsJob), jb = (size_t)g[gi].count * sizeof(HsJob);
+        if (kcopy) {
+            rc = launch_copy_ranges(hsrc, dbase, s0, sb, j0, jb, st);
+            if (rc) return rc;
+        } else {
+            HIP_TRY(hipMemcpyAsync(dbase + s0, hsrc + s0, sb, hipMemcpyHostToDevice, st));
+            HIP_TRY(hipMemcpyAsync(dbase + j0, hsrc + j0, jb, hipMemcpyHostToDevice, st));
+        }
+        if (!fused) HIP_TRY(hipMemsetAsync(rcount + gi, 0, sizeof(unsigned), st));
+        if (iv) HIP_TRY(hipMemsetAsync(c->d_replay_count2 + gi, 0, sizeof(unsigned), st));
+        // profiling: each group's first search starts at ev[gi][0]
+        if (prof) HIP_TRY(hipEventRecord(c->ev[gi][0], st));
     }
     const int evals = max_iter + 1;
     HsParams hp[kMaxGroups];
@@ -3529,24 +3560,27 @@ static int batch_enqueue(livo_ctx* c, int L, int32_t n, const int32_t* ids, int 
         kp[gi].jobs = djobs + g[gi].first;
         kp[gi].replay_count = rcount + gi;
         kp[gi].replay_list = rlist + g[gi].off;
+        kp[gi].replay_count2 = iv ? c->d_replay_count2 + gi : nullptr;
+        kp[gi].replay_list2 = iv ? c->d_replay_list2 + g[gi].off : nullptr;
         // the iVox overflow pass of each group has its own scratch slices (groups run concurrently)
         if (kp[gi].iv.scratch) kp[gi].iv.scratch += (int64_t)gi * c->iv.big_threads * c->iv.big_slice;
         hp[gi].solve = lm ? 1 : 0;  // the last plane-pass block of each scan runs its solve (IKFoM: k_solve_ik below)
         hp[gi].replay_count = rcount + gi;
+        hp[gi].replay_count2 = kp[gi].replay_count2;
     }
     // one launch per evaluation (a launch whose scans all stopped exits at once)
     for (int e = 0; e < evals; e++) {
         for (int gi = 0; gi < ngroups && fused; gi++) {
             hipStream_t st = g[gi].st;
             // full: ev[gi][e] before evaluation e, ev[gi][evals] after the last
-            if (full && (e > 0 || gi > 0)) HIP_TRY(hipEventRecord(c->ev[gi][e], st));
+            if (full && e > 0) HIP_TRY(hipEventRecord(c->ev[gi][e], st));
             rc = launch_iekf_eval(kp[gi], hp[gi], g[gi].count, g[gi].max_n, e == 0, st);
             if (rc) return rc;
             if (prof && !full && e == 0) HIP_TRY(hipEventRecord(c->ev[gi][1], st));
         }
         for (int gi = 0; gi < ngroups && !fused; gi++) {
             hipStream_t st = g[gi].st;
-            if (full && (e > 0 || gi > 0)) HIP_TRY(hipEventRecord(c->ev[gi][3 * e], st));
+            if (full && e > 0) HIP_TRY(hipEventRecord(c->ev[gi][3 * e], st));
             // leaf-map search; rematch passes are bounded by the previous neighbours
             // (the group's replay count was zeroed before the batch / by the last k_solve)
             rc = backend_knn(c, kp[gi], g[gi].count, g[gi].max_n, e > 0, st);
@@ -3645,25 +3679,31 @@ static int batch_collect(livo_ctx* c, int L, livo_state* states, livo_iter_stats
     }
     if (prof) {
         livo_timings t{};
-        // first search of the whole batch: wall time from its start on stream 0
-        // to the later of the two streams' ends (the halves run concurrently)
+        // first search of the whole batch: wall time from the earliest group's
+        // start to the latest group's end (the groups start on their own streams)
+        double lead = 0.0;  // how long before group 0 the earliest group started
         for (int gi = 0; gi < ngroups; gi++) {
-            float ms = 0.f;
+            float ms = 0.f, m0 = 0.f;
             (void)hipEventElapsedTime(&ms, c->ev[0][0], c->ev[gi][1]);
+            (void)hipEventElapsedTime(&m0, c->ev[0][0], c->ev[gi][0]);
             t.knn_ms = std::max(t.knn_ms, (double)ms);
+            lead = std::max(lead, -(double)m0);
         }
+        t.knn_ms += lead;
         t.knn_launches = 1;
         if (full && fused) {
             // every evaluation launch: max over the concurrent groups
-            t.knn_ms = 0.0;
             t.n_evals = std::min(evals, LIVO_MAX_EVALS);
             for (int e = 0; e < t.n_evals; e++) {
+                // the evaluation's window over the concurrent groups (e = 0: the same
+                // window as knn_ms above, from the earliest group's start)
                 double m = 0.0;
                 for (int gi = 0; gi < ngroups; gi++) {
                     float ms = 0.f;
-                    (void)hipEventElapsedTime(&ms, (e == 0 && gi == 0) ? c->ev[0][0] : c->ev[gi][e], c->ev[gi][e + 1]);
+                    (void)hipEventElapsedTime(&ms, e == 0 ? c->ev[0][0] : c->ev[gi][e], c->ev[gi][e + 1]);
                     m = std::max(m, (double)ms);
                 }
+                if (e == 0) m = t.knn_ms;
                 t.eval_ms[e] = m;
                 int searched = 0;
                 for (int32_t b = 0; b < n; b++) searched += hslot(b).eval_search[e] != 0;
@@ -3840,6 +3880,8 @@ int livo_ivox_init(livo_ctx* c, const livo_ivox_params* p) {
     v.prm = prm;
     v.inv_res = (float)(1.0 / (double)prm.resolution);  // options_.inv_resolution_ = 1.0 / resolution_
     v.nearby = nearby;
+    if (const char* e = std::getenv("LIVO_IVOX_KIND"))  // (A/B and tests: force one search kernel)
+        v.kind = std::strcmp(e, "thread") == 0 ? 0 : (std::strcmp(e, "wave") == 0 ? 1 : (std::strcmp(e, "team") == 0 ? 2 : -1));
     if (dev_alloc(&v.ctr, 5)) return LIVO_E_OOM;  // the counters of IvoxParams::ctr
     int rc = ivox_ensure_table(c, 1024);
     if (!rc) rc = ivox_ensure_big(c);
@@ -3906,6 +3948,7 @@ int livo_ivox_knn(livo_ctx* c, const float* q, int64_t n, int32_t max_num, doubl
     kp.iv.max_num = max_num;
     kp.iv.range2 = max_range * max_range;
     HIP_TRY(hipMemsetAsync(kp.replay_count, 0, sizeof(unsigned), c->stream));
+    HIP_TRY(hipMemsetAsync(kp.replay_count2, 0, sizeof(unsigned), c->stream));
     rc = launch_ivox_knn(kp, 1, n, false, c->iv.big_threads, c->stream);
     if (rc) return rc;
     std::vector<NNRec> hr((size_t)n);

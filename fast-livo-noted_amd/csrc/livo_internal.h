@@ -201,6 +201,7 @@ struct IvoxParams {
     int32_t log2;
     int32_t nearby;           // 1, 7, 19 or 27 nearby grids (NearbyType)
     int32_t max_num;          // GetClosestPoint max_num (<= 5)
+    int32_t kind;             // search kernel: -1 by batch size, 0 thread, 1 wave, 2 team (LIVO_IVOX_KIND at livo_ivox_init)
     double range2;            // max_range * max_range
     SelElem* scratch;         // overflow pass: one slice per thread
     int64_t slice;            // elements per slice
@@ -321,6 +322,7 @@ struct HsParams {
     double lpc;             // LASER_POINT_COV (the IKFoM gain divides P by it)
     int32_t solve;          // 1: the last block of a scan also runs its solve (IEKF loop)
     unsigned* replay_count; // zeroed once per launch (the group's k-NN replay count), may be null
+    unsigned* replay_count2;  // iVox: the wave pass's overflow count, zeroed with replay_count (may be null)
 };
 
 struct KnnParams {
@@ -328,6 +330,11 @@ struct KnnParams {
     const HsJob* jobs;
     unsigned* replay_count;            // queries flagged for the exact replay (zeroed per pass)
     unsigned long long* replay_list;   // (job << 32) | point
+    // iVox: queries the wave-cooperative search could not hold (a grid too large to
+    // stream, or a heap select), for the global-memory pass (k_ivox_knn_big); the
+    // team search's overflow (replay_list) goes to the wave pass first
+    unsigned* replay_count2;
+    unsigned long long* replay_list2;
     unsigned long long* replay_total;  // running count of replayed queries (diagnostics)
     double R_LI[9];
     double t_LI[3];
@@ -406,6 +413,8 @@ constexpr int kEvalBlock = LIVO_EVAL_BLOCK;  // threads (points) per block of k_
 int launch_iekf_eval(const KnnParams& kp, const HsParams& hp, int n_jobs, int64_t max_n, bool first, void* stream);
 int launch_solve_ik(const HsParams& p, int n_jobs, void* stream);
 int launch_copy_words(const void* src, void* dst, size_t bytes, void* stream);  // 16-B aligned, bytes % 16 == 0
+// bytes [o0, o0 + n0) and [o1, o1 + n1) of src to the same offsets of dst, one launch (16-B aligned)
+int launch_copy_ranges(const void* src, void* dst, size_t o0, size_t n0, size_t o1, size_t n1, void* stream);
 // IKFoM plane pass (12-wide rows) with the manifold update in each scan's last block.
 int launch_hshare_ik(const HsParams& p, int n_jobs, int max_nblk, bool first, void* stream);
 int launch_solve(const SolveParams& p, int n_jobs, void* stream);

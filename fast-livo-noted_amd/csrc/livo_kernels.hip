@@ -597,6 +597,20 @@ __device__ __forceinline__ void write_nnrec(NNRec* __restrict__ out, const MapNo
     oi[2] = make_int4((int)node[1], (int)node[2], (int)node[3], (int)node[4]);
 }
 
+// The state an evaluation transforms its points with, wherever it is held
+// (k_iekf_eval: in LDS, solved by the launch's own blocks).
+struct PoseRef {
+    const double* rot;
+    const double* pos;
+};
+__device__ __forceinline__ void query_point(const KnnParams& P, const PoseRef& S, const float4 b, float& qx, float& qy,
+                                            float& qz) {
+    if (P.identity) {
+        qx = b.x; qy = b.y; qz = b.z;
+    } else {
+        world_point(S.rot, S.pos, P.R_LI, P.t_LI, b.x, b.y, b.z, qx, qy, qz);
+    }
+}
 __device__ __forceinline__ void query_point(const KnnParams& P, const IekfSlot* slot, const float4 b, float& qx,
                                             float& qy, float& qz) {
     if (P.identity) {
@@ -759,8 +773,8 @@ struct LeafQuery {
     uint32_t nd[kNN];
 };
 
-template <bool SEEDED>
-__device__ __forceinline__ void lq_init(LeafQuery& q, const KnnParams& P, const IekfSlot* slot, const HsJob& job, int i,
+template <bool SEEDED, class Src>
+__device__ __forceinline__ void lq_init(LeafQuery& q, const KnnParams& P, const Src& slot, const HsJob& job, int i,
                                         bool valid) {
 #pragma unroll
     for (int k = 0; k < kNN; k++) { q.d[k] = INFINITY; q.nd[k] = 0u; }
@@ -1942,12 +1956,13 @@ constexpr int kCanonMaxCells = 1 << 15;
 __device__ __forceinline__ bool canon_less(float d1, float x1, uint32_t i1, float d2, float x2, uint32_t i2) {
     return d1 < d2 || (d1 == d2 && (x1 < x2 || (x1 == x2 && i1 < i2)));
 }
-__device__ __forceinline__ void canon_query(const KnnParams& P, const HsJob& job, int i) {
+template <class Src>
+__device__ __forceinline__ void canon_query(const KnnParams& P, const HsJob& job, int i, const Src& src) {
     const float4* __restrict__ gpts = reinterpret_cast<const float4*>(P.gpts);
     const uint64_t mask = (1ull << P.glog2) - 1ull;
     {
         float qx, qy, qz;
-        query_point(P, job.slot, reinterpret_cast<const float4*>(job.pts)[i], qx, qy, qz);
+        query_point(P, src, reinterpret_cast<const float4*>(job.pts)[i], qx, qy, qz);
         NNRec* rec = job.nn + i;
         const float T = rec->cnt == kNN ? rec->p[kNN - 1][3] : INFINITY;
         const int flag = rec->flag | 0x100;
@@ -2038,7 +2053,8 @@ __global__ __launch_bounds__(64) void k_knn_canon(KnnParams P) {
     if (blockIdx.x == 0 && threadIdx.x == 0 && n) atomicAdd(P.replay_total, (unsigned long long)n);
     for (unsigned t = blockIdx.x * 64 + threadIdx.x; t < n; t += gridDim.x * 64) {
         const unsigned long long e = P.replay_list[t];
-        canon_query(P, P.jobs[(unsigned)(e >> 32)], (int)(unsigned)(e & 0xffffffffu));
+        const HsJob& job = P.jobs[(unsigned)(e >> 32)];
+        canon_query(P, job, (int)(unsigned)(e & 0xffffffffu), job.slot);
     }
 }
 
@@ -3016,18 +3032,15 @@ __device__ __forceinline__ void hs_scan_tail(const HsParams& P, const HsJob& job
 // is sc1 stores drained by s_waitcnt vmcnt(0) before an agent-scope atomic, and
 // sc1 loads after it (MI355X_MICROARCH.md, Workgroup dispatch: sc1 hand-off).
 // The sums' order depends only on nblk, not on arrival order: deterministic.
+// Level 1 of the reduction: the shard ticket, and in the block that completes
+// the shard the sum of its partials into row sh (drained before return, the
+// shard's ticket reset).  Returns true in that block only (block-uniform).
 template <int NT, int NU = kRedUsed>
-__device__ __forceinline__ void hs_ticket_tail(const HsParams& P, const HsJob& job, IekfSlot* slot, int nblk,
-                                               unsigned blk, HsReduceLds& R, SolveLds& L, int pk = -1) {
+__device__ __forceinline__ bool hs_shard_level(const HsJob& job, IekfSlot* slot, int nblk, unsigned blk,
+                                               HsReduceLds& R) {
     static_assert(NU == kRedUsed || NU == kRedUsed + 2, "h_share sums (+ search counts)");
     static_assert(NT / 32 <= kRedRows / 2, "R.fin holds one row per 32-thread group");
     const int tid = threadIdx.x;
-#ifdef LIVO_TAIL_PROF
-    unsigned long long tp = __builtin_amdgcn_s_memtime();
-    if (pk >= 0 && tid == 0) atomicAdd(&g_tail_prof[pk][0], 1ull);
-#else
-    (void)pk;
-#endif
     const int K = nblk < kRedShards ? nblk : kRedShards;
     const int sh = (int)(blk % (unsigned)K);
     const int cnt = (nblk - sh + K - 1) / K;  // partials of shard sh: sh, sh + K, ...
@@ -3040,8 +3053,7 @@ __device__ __forceinline__ void hs_ticket_tail(const HsParams& P, const HsJob& j
                      (unsigned)cnt - 1u;
     }
     __syncthreads();
-    TAIL_MARK(1, tp);
-    if (!R.last) return;
+    if (!R.last) return false;
     if (cnt > 1) {
         // thread (g, c) sums rows sh + K (g + G t), t = 0, 1, ... of column c in that
         // order, every load in flight at once (G = NT / 32 groups)
@@ -3076,14 +3088,30 @@ __device__ __forceinline__ void hs_ticket_tail(const HsParams& P, const HsJob& j
             st_sc1(job.partial + (size_t)sh * kRedCols + tid, f[0]);  // row sh: the shard's sum
         }
     }
-    // the shard's ticket ready for the next pass; the shard's row drained, the scan's ticket
     if (tid < 64) {
-        if (tid == 0) st_sc1(sh_ticket, 0u);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (tid == 0)
-            R.last2 = __hip_atomic_fetch_add(gptr(&slot->hs_ticket), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                      (unsigned)K - 1u;
+        if (tid == 0) st_sc1(sh_ticket, 0u);  // ready for the next pass
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the shard's row drained
     }
+    return true;
+}
+
+template <int NT, int NU = kRedUsed>
+__device__ __forceinline__ void hs_ticket_tail(const HsParams& P, const HsJob& job, IekfSlot* slot, int nblk,
+                                               unsigned blk, HsReduceLds& R, SolveLds& L, int pk = -1) {
+    const int tid = threadIdx.x;
+#ifdef LIVO_TAIL_PROF
+    unsigned long long tp = __builtin_amdgcn_s_memtime();
+    if (pk >= 0 && tid == 0) atomicAdd(&g_tail_prof[pk][0], 1ull);
+#else
+    (void)pk;
+#endif
+    if (!hs_shard_level<NT, NU>(job, slot, nblk, blk, R)) return;
+    TAIL_MARK(1, tp);
+    const int K = nblk < kRedShards ? nblk : kRedShards;
+    // the shard's row drained: the scan's ticket
+    if (tid == 0)
+        R.last2 = __hip_atomic_fetch_add(gptr(&slot->hs_ticket), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                  (unsigned)K - 1u;
     __syncthreads();
     if (!R.last2) return;
 #ifdef LIVO_TAIL_PROF
@@ -3208,6 +3236,7 @@ __global__ __launch_bounds__(kBlock) void k_hshare(HsParams P) {
     const HsJob job = P.jobs[blockIdx.y];
     // the k-NN replay of this evaluation has run (stream order): reset its count
     if (P.replay_count && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *P.replay_count = 0u;
+    if (P.replay_count2 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *P.replay_count2 = 0u;
     if ((int)blockIdx.x >= job.nblk) return;
     IekfSlot* slot = job.slot;
     int search;
@@ -3261,7 +3290,8 @@ using BlockTile = TileLds<LIVO_EVAL_TILE_CELLS, LIVO_EVAL_TILE_PTS>;
 
 // The flagged queries of one wave (amb), each replayed by the whole wave
 // (knn_exact_wave) with `cache` (4 KB of LDS) as its subtree cache.
-__device__ __forceinline__ void replay_wave(const KnnParams& P, const HsJob& job, int i, bool amb, float4* cache) {
+__device__ __forceinline__ void replay_wave(const KnnParams& P, const HsJob& job, int i, bool amb, float4* cache,
+                                            const PoseRef& pose) {
     unsigned long long m = __ballot(amb);
     const int lane = (int)(threadIdx.x & 63u);
     while (m) {  // wave-uniform
@@ -3269,7 +3299,7 @@ __device__ __forceinline__ void replay_wave(const KnnParams& P, const HsJob& job
         m &= m - 1ull;
         const int il = __shfl(i, l);
         float qx, qy, qz;
-        query_point(P, job.slot, reinterpret_cast<const float4*>(job.pts)[il], qx, qy, qz);
+        query_point(P, pose, reinterpret_cast<const float4*>(job.pts)[il], qx, qy, qz);
         Cands c;
         knn_exact_wave(P.nodes, P.n_nodes, P.has_map, qx, qy, qz, cache, c);
         if (lane == l) {
@@ -3344,6 +3374,7 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
     bool prefit = false;  // the plane of this evaluation fitted in the search branch
     if (slot->ctrl.stop) return;  // block-uniform
     const int search = FIRST ? 1 : slot->ctrl.search_en;
+    const PoseRef pose{slot->state.rot, slot->state.pos};
 #ifdef LIVO_EVAL_PROF
     const int tl_e = min(slot->ctrl.n_evals, LIVO_MAX_EVALS - 1);
 #endif
@@ -3355,7 +3386,7 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
         // 18643 updates/s, profiles/r03_ab_prefit_seed.txt); the answer is the
         // same exact list either way
         LeafQuery q;
-        lq_init<false>(q, P, slot, job, i, valid);
+        lq_init<false>(q, P, pose, job, i, valid);
         int c0 = 0, c1 = 0, c2 = 0, s0 = 1, s1 = 1, s2 = 1;
         if (valid) grid_cell(P, q, c0, c1, c2, s0, s1, s2);
         unsigned visits = 0, npts = 0;
@@ -3376,7 +3407,7 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
             if (P.bslots) {  // (uniform) the ball runs first; the cell runs for a query they do not certify
                 certified = dyn ? brun_search<true>(q, P, valid, visits, npts) : brun_search<false>(q, P, valid, visits, npts);
                 if (certified) runs = reinterpret_cast<const float4*>(P.bpts);  // (float4 run entries only)
-                if (valid && !certified) lq_init<false>(q, P, slot, job, i, valid);
+                if (valid && !certified) lq_init<false>(q, P, pose, job, i, valid);
 #ifdef LIVO_EVAL_PROF
                 ball_ok = certified;
 #endif
@@ -3401,7 +3432,7 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
             // wave-parallel walk of one query's cells was slower)
             bool walked = false;
             if (dyn && valid && !certified) {  // the incremental map: the current grid's serial walk
-                lq_init<false>(q, P, slot, job, i, valid);
+                lq_init<false>(q, P, pose, job, i, valid);
                 TileView none;
                 certified = grid_search(q, P, c0, c1, c2, s0, s1, s2, none, visits, npts);
                 walked = true;
@@ -3472,6 +3503,9 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
 #pragma unroll
                 for (int j = 0; j < 8; j++) {
                     const int u = j * 64 + lane, rec = u >> 3;
+#ifdef LIVO_AB_REC_KNOCKOUT  // A/B only (wrong records): 64 of each record's 128 B stored, to price the writes
+                    if ((u & 7) >= 4) continue;
+#endif
                     if (base + rec < job.n) dst[u] = st[rec * 8 + (((u & 7) + rec) & 7)];
                 }
                 // a flagged query's replay (same wave) reads its record back
@@ -3495,14 +3529,14 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
         n_pts = npts;
         if (amb) atomicAdd(P.replay_total, 1ull);
         if (P.canon) {  // (kernel parameter: uniform) the incremental map's exact resolution
-            if (amb) canon_query(P, job, i);
+            if (amb) canon_query(P, job, i, pose);
             __syncthreads();  // the tile's LDS is reused by the solve
         } else if (__syncthreads_or(amb)) {  // block-uniform: some query of this block is flagged
             // the tile's LDS is free after the barrier: 4 KB per wave of subtree cache
             static_assert(sizeof(U) >= (size_t)(kEvalBlock / 64) * (4u << kReplayLevels) * sizeof(float4),
                           "replay caches do not fit the evaluation's LDS");
             float4* cache = reinterpret_cast<float4*>(&U) + (threadIdx.x >> 6) * (4u << kReplayLevels);
-            replay_wave(P, job, i, amb, cache);
+            replay_wave(P, job, i, amb, cache, pose);
             __syncthreads();  // the caches' LDS is reused by the solve
         }
         EVAL_MARK(2);
@@ -3511,7 +3545,7 @@ __global__ __launch_bounds__(kEvalBlock, LIVO_EVAL_WAVES) void k_iekf_eval(EvalP
     hs_row_clear(w);
     const int nblk = max(1, (job.n + kEvalBlock - 1) / kEvalBlock);
     if (valid) {
-        hshare_point(E.h, job, slot->state, i, search, w, pin, prefit);
+        hshare_point(E.h, job, pose, i, search, w, pin, prefit);
     }
     EVAL_MARK_SYNC(3);
     const double inv_r = E.h.inv_r;
@@ -4289,6 +4323,27 @@ int launch_copy_words(const void* src, void* dst, size_t bytes, void* stream) {
     const unsigned blocks = (unsigned)std::min<int64_t>((n16 + 255) / 256, 64);
     hipLaunchKernelGGL(k_copy_words, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
                        reinterpret_cast<const uint4*>(src), reinterpret_cast<uint4*>(dst), n16);
+    return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
+
+// Two ranges of 16-B words in one launch (a stream group's slots and its jobs).
+__global__ __launch_bounds__(256) void k_copy_ranges(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                     int64_t a0, int64_t n0, int64_t a1, int64_t n1) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n0 + n1; i += (int64_t)gridDim.x * 256) {
+        const int64_t w = i < n0 ? a0 + i : a1 + (i - n0);
+        dst[w] = src[w];
+    }
+}
+
+int launch_copy_ranges(const void* src, void* dst, size_t o0, size_t n0, size_t o1, size_t n1, void* stream) {
+    if (n0 + n1 == 0) return LIVO_OK;
+    if ((o0 | n0 | o1 | n1) % 16 || (reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) % 16)
+        return LIVO_E_INVALID;
+    const int64_t w0 = (int64_t)(n0 / 16), w1 = (int64_t)(n1 / 16);
+    const unsigned blocks = (unsigned)std::min<int64_t>((w0 + w1 + 255) / 256, 64);
+    hipLaunchKernelGGL(k_copy_ranges, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const uint4*>(src), reinterpret_cast<uint4*>(dst), (int64_t)(o0 / 16), w0,
+                       (int64_t)(o1 / 16), w1);
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 
