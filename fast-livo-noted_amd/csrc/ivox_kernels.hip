@@ -546,7 +546,10 @@ constexpr int kIvTeam = 16;
 // the current one plus all of the current grid's in-range points, so 18 x 5 + the
 // largest grid; 128 overflowed (to the wave pass) once map_incremental had grown
 // grids past ~38 points (32 KB of LDS per block: 5 blocks per CU)
-constexpr int kIvTeamCap = 256;
+#ifndef LIVO_IV_TEAM_CAP
+#define LIVO_IV_TEAM_CAP 128
+#endif
+constexpr int kIvTeamCap = LIVO_IV_TEAM_CAP;
 __device__ __forceinline__ uint32_t team_bits(unsigned long long m, int lane) {
     return (uint32_t)(m >> (lane & 48)) & 0xFFFFu;
 }
@@ -666,6 +669,9 @@ __global__ __launch_bounds__(256) void k_ivox_knn_team(KnnParams P) {
     }
 }
 
+#ifndef LIVO_IV_WLIST_BLOCKS
+#define LIVO_IV_WLIST_BLOCKS 4096
+#endif
 // Kernel choice per launch: the team search (16 lanes a query, list in LDS) by
 // default; the wave-cooperative search (a query per wave) for launches of at
 // most LIVO_IVOX_WAVE_MAX queries (default 0: never; a 100k-point scan alone
@@ -712,8 +718,8 @@ int launch_ivox_knn(const KnnParams& p, int n_jobs, int64_t max_n, bool later, i
             hipLaunchKernelGGL((k_ivox_knn_wave<false>), grid, block, 0, (hipStream_t)stream, q);
     }
     if (hipGetLastError() != hipSuccess) return LIVO_E_HIP;
-    if (kind == 2)  // the team search's overflow, one query per wave
-        hipLaunchKernelGGL(k_ivox_knn_wave_list, dim3(256), dim3(64 * kWaves), 0, (hipStream_t)stream, q);
+    if (kind == 2)  // the team search's overflow, one query per wave (grid-stride; blocks past the list exit)
+        hipLaunchKernelGGL(k_ivox_knn_wave_list, dim3(LIVO_IV_WLIST_BLOCKS), dim3(64 * kWaves), 0, (hipStream_t)stream, q);
     const unsigned blocks = (unsigned)std::max<int64_t>(1, overflow_threads / 64);
     hipLaunchKernelGGL(k_ivox_knn_big, dim3(blocks), dim3(64), 0, (hipStream_t)stream, q);
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
