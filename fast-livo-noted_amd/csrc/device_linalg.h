@@ -163,6 +163,36 @@ __device__ __forceinline__ void reg_lu_column(const double (&A)[N], const int* s
 
 #define WAVE_SYNC() do { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); __builtin_amdgcn_wave_barrier(); } while (0)
 
+// Short-argument sine / cosine and arccosine near 1 for the IEKF's rotation
+// increments (well under 0.5 rad, an arccosine argument near 1 for under 8
+// degrees): Taylor series in nested form, within a few ulp of the library's
+// (their next terms are below 1e-18 relative), and a fraction of its code.
+// The solve runs once per scan per evaluation on a CU that has not run it
+// recently, so its code is fetched cold (profiles/r06_tail_phases.txt): the
+// library's argument reduction is in the instruction stream only for the rare
+// large argument that takes it.
+__device__ __forceinline__ void sincos_short(double x, double& s, double& c) {
+    if (fabs(x) <= 0.5) {
+        const double x2 = x * x;
+        s = x * (1.0 - x2 / 6.0 * (1.0 - x2 / 20.0 * (1.0 - x2 / 42.0 * (1.0 - x2 / 72.0 *
+                 (1.0 - x2 / 110.0 * (1.0 - x2 / 156.0 * (1.0 - x2 / 210.0)))))));
+        c = 1.0 - x2 / 2.0 * (1.0 - x2 / 12.0 * (1.0 - x2 / 30.0 * (1.0 - x2 / 56.0 *
+                 (1.0 - x2 / 90.0 * (1.0 - x2 / 132.0 * (1.0 - x2 / 182.0 * (1.0 - x2 / 240.0)))))));
+    } else {
+        s = sin(x);
+        c = cos(x);
+    }
+}
+__device__ __forceinline__ double acos_near1(double x) {
+    if (x >= 0.99 && x <= 1.0) {  // acos(x) = 2 asin(y), y = sqrt((1 - x) / 2) <= 0.071
+        const double y = sqrt((1.0 - x) * 0.5), y2 = y * y;
+        const double a = y * (1.0 + y2 * (1.0 / 6.0 + y2 * (3.0 / 40.0 + y2 * (5.0 / 112.0 + y2 * (35.0 / 1152.0 +
+                         y2 * (63.0 / 2816.0 + y2 * (231.0 / 13312.0 + y2 * (143.0 / 10240.0))))))));
+        return 2.0 * a;
+    }
+    return acos(x);
+}
+
 // SO3 Exp / Log (so3_math.h:55-81) and 3x3 products, sums in index order.
 __device__ __forceinline__ void so3_exp(double v1, double v2, double v3, double* R) {
     const double norm = sqrt(v1 * v1 + v2 * v2 + v3 * v3);
@@ -170,7 +200,9 @@ __device__ __forceinline__ void so3_exp(double v1, double v2, double v3, double*
     if (norm > 0.00001) {
         const double r[3] = {v1 / norm, v2 / norm, v3 / norm};
         const double K[9] = {0.0, -r[2], r[1], r[2], 0.0, -r[0], -r[1], r[0], 0.0};
-        const double s = sin(norm), c1 = 1.0 - cos(norm);
+        double s, cn;
+        sincos_short(norm, s, cn);
+        const double c1 = 1.0 - cn;
         double cK[9];
         _Pragma("unroll") for (int i = 0; i < 9; i++) cK[i] = c1 * K[i];
         _Pragma("unroll") for (int i = 0; i < 3; i++)
@@ -182,12 +214,14 @@ __device__ __forceinline__ void so3_exp(double v1, double v2, double v3, double*
 }
 __device__ __forceinline__ void so3_log(const double* R, double* o) {
     const double tr = (R[0] + R[4]) + R[8];
-    const double theta = (tr > 3.0 - 1e-6) ? 0.0 : acos(0.5 * (tr - 1));
+    const double theta = (tr > 3.0 - 1e-6) ? 0.0 : acos_near1(0.5 * (tr - 1));
     const double K[3] = {R[7] - R[5], R[2] - R[6], R[3] - R[1]};
     if (fabs(theta) < 0.001) {
         _Pragma("unroll") for (int i = 0; i < 3; i++) o[i] = 0.5 * K[i];
     } else {
-        const double f = 0.5 * theta / sin(theta);
+        double st, ct;
+        sincos_short(theta, st, ct);
+        const double f = 0.5 * theta / st;
         _Pragma("unroll") for (int i = 0; i < 3; i++) o[i] = f * K[i];
     }
 }

@@ -212,6 +212,35 @@ __global__ __launch_bounds__(kKnnBlock) void k_ivox_knn(KnnParams P) {
     if (n > 0) iv_write(job.nn + i, reinterpret_cast<const float4*>(P.iv.pts), a, n);
 }
 
+// The queries no other search could hold (replay_list2: a grid of more points
+// than the wave search can stage, which map_incremental builds near the sensor),
+// one workgroup each: lane 0 runs the per-thread search on a list in LDS (the
+// slice: nearby x K + the largest grid), whose latency is a tenth of the
+// global-memory slice's.  Used when the slice fits in 64 KB of LDS.
+__global__ __launch_bounds__(64) void k_ivox_knn_big_lds(KnnParams P) {
+    extern __shared__ SelElem big_lst[];
+    const unsigned cnt = *P.replay_count2;
+    for (unsigned r = blockIdx.x; r < cnt; r += gridDim.x) {  // (block-uniform)
+        if (threadIdx.x == 0) {
+            const unsigned long long e = P.replay_list2[r];
+            const unsigned bjob = (unsigned)(e >> 32);
+            const int i = (int)(e & 0xFFFFFFFFu);
+            const HsJob job = P.jobs[bjob];
+            const float4 b = reinterpret_cast<const float4*>(job.pts)[i];
+            float qx, qy, qz;
+            iv_world(P, job.slot, b, qx, qy, qz);
+            bool overflow;
+            SelElem* a = big_lst;
+            const int n = iv_query(P.iv, qx, qy, qz, a, (int)P.iv.slice, overflow);
+            if (overflow) {
+                atomicOr(P.iv.ctr, 2ull);
+            } else if (n > 0) {
+                iv_write(job.nn + i, reinterpret_cast<const float4*>(P.iv.pts), a, n);
+            }
+        }
+    }
+}
+
 // The exact global-memory pass over the queries no other search could hold
 // (replay_list2): one query per thread, its candidates in a private slice.
 __global__ __launch_bounds__(64) void k_ivox_knn_big(KnnParams P) {
@@ -720,8 +749,13 @@ int launch_ivox_knn(const KnnParams& p, int n_jobs, int64_t max_n, bool later, i
     if (hipGetLastError() != hipSuccess) return LIVO_E_HIP;
     if (kind == 2)  // the team search's overflow, one query per wave (grid-stride; blocks past the list exit)
         hipLaunchKernelGGL(k_ivox_knn_wave_list, dim3(LIVO_IV_WLIST_BLOCKS), dim3(64 * kWaves), 0, (hipStream_t)stream, q);
-    const unsigned blocks = (unsigned)std::max<int64_t>(1, overflow_threads / 64);
-    hipLaunchKernelGGL(k_ivox_knn_big, dim3(blocks), dim3(64), 0, (hipStream_t)stream, q);
+    const size_t lds = (size_t)q.iv.slice * sizeof(SelElem);
+    if (lds <= 65536) {
+        hipLaunchKernelGGL(k_ivox_knn_big_lds, dim3(2048), dim3(64), lds, (hipStream_t)stream, q);
+    } else {
+        const unsigned blocks = (unsigned)std::max<int64_t>(1, overflow_threads / 64);
+        hipLaunchKernelGGL(k_ivox_knn_big, dim3(blocks), dim3(64), 0, (hipStream_t)stream, q);
+    }
     return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
 }
 
