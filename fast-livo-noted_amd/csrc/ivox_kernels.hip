@@ -214,30 +214,117 @@ __global__ __launch_bounds__(kKnnBlock) void k_ivox_knn(KnnParams P) {
 
 // The queries no other search could hold (replay_list2: a grid of more points
 // than the wave search can stage, which map_incremental builds near the sensor),
-// one workgroup each: lane 0 runs the per-thread search on a list in LDS (the
-// slice: nearby x K + the largest grid), whose latency is a tenth of the
-// global-memory slice's.  Used when the slice fits in 64 KB of LDS.
-__global__ __launch_bounds__(64) void k_ivox_knn_big_lds(KnnParams P) {
-    extern __shared__ SelElem big_lst[];
+// one wave each: the streaming form of the wave search (grid by grid, each
+// grid's in-range points staged after the survivors so far and cut to K by
+// KNNPointByCondition's nth_element, ivox3d_node.hpp:179-183), with the list and
+// the partition tables in LDS sized for the largest grid (nearby x K + that
+// grid) and the looped wave-parallel nth_element (wave_nth_big).  A selection
+// that exhausts introselect's depth limit (libstdc++ then heap-selects) redoes
+// the query with the per-thread search in the wave's global-memory slice.
+// Used when the list fits in 64 KB of LDS (12 B an entry).
+constexpr int kBigEntryBytes = 12;  // float + uint32 + two uint16 table entries
+__global__ __launch_bounds__(64) void k_ivox_knn_big_wave(KnnParams P) {
+    extern __shared__ uint32_t big_lds[];
+    const int lane = threadIdx.x;
+    const IvoxParams& V = P.iv;
+    const int cap = (int)V.slice;
+    const BigList L{reinterpret_cast<float*>(big_lds), big_lds + cap, reinterpret_cast<uint16_t*>(big_lds + 2 * cap),
+                    reinterpret_cast<uint16_t*>(big_lds + 2 * cap) + cap};
+    const float4* __restrict__ pts = reinterpret_cast<const float4*>(V.pts);
+    const int K = V.max_num;
     const unsigned cnt = *P.replay_count2;
-    for (unsigned r = blockIdx.x; r < cnt; r += gridDim.x) {  // (block-uniform)
-        if (threadIdx.x == 0) {
-            const unsigned long long e = P.replay_list2[r];
-            const unsigned bjob = (unsigned)(e >> 32);
-            const int i = (int)(e & 0xFFFFFFFFu);
-            const HsJob job = P.jobs[bjob];
-            const float4 b = reinterpret_cast<const float4*>(job.pts)[i];
-            float qx, qy, qz;
-            iv_world(P, job.slot, b, qx, qy, qz);
-            bool overflow;
-            SelElem* a = big_lst;
-            const int n = iv_query(P.iv, qx, qy, qz, a, (int)P.iv.slice, overflow);
-            if (overflow) {
-                atomicOr(P.iv.ctr, 2ull);
-            } else if (n > 0) {
-                iv_write(job.nn + i, reinterpret_cast<const float4*>(P.iv.pts), a, n);
+    for (unsigned r = blockIdx.x; r < cnt; r += gridDim.x) {  // (wave-uniform)
+        const unsigned long long e = P.replay_list2[r];
+        const unsigned bjob = (unsigned)(e >> 32);
+        const int i = (int)(e & 0xFFFFFFFFu);
+        const HsJob job = P.jobs[bjob];
+        const float4 b = reinterpret_cast<const float4*>(job.pts)[i];
+        float qx, qy, qz;
+        iv_world(P, job.slot, b, qx, qy, qz);
+        int kx, ky, kz;
+        const float qlim = (float)(kIvMaxKey + 8);
+        if (!iv_cell(qx, V.inv_res, qlim, kx) || !iv_cell(qy, V.inv_res, qlim, ky) || !iv_cell(qz, V.inv_res, qlim, kz))
+            continue;  // no grid within reach: the cache stays
+        uint2 run = make_uint2(0u, 0u);
+        if (lane < V.nearby)
+            run = iv_lookup(V.slots, V.log2, iv_key(kx + c_nearby[lane][0], ky + c_nearby[lane][1], kz + c_nearby[lane][2]));
+        int n = 0;
+        bool ok = true;
+#pragma unroll 1
+        for (int t = 0; t < V.nearby && ok; t++) {
+            const uint32_t c = __shfl(run.y, t, 64), st = __shfl(run.x, t, 64);
+            const int old = n;
+#pragma unroll 1
+            for (uint32_t k0 = 0; k0 < c && ok; k0 += 64) {
+                const uint32_t k = k0 + lane;
+                bool in = false;
+                float d = 0.f;
+                if (k < c) {
+                    const float4 v = pts[st + k];
+                    const float dx = v.x - qx, dy = v.y - qy, dz = v.z - qz;
+                    d = dx * dx + (dy * dy + dz * dz);  // distance2, ivox3d_node.hpp:12-16
+                    in = (double)d < V.range2;
+                }
+                const unsigned long long m = __ballot(in);
+                if (n + __popcll(m) > cap) {
+                    ok = false;  // (cannot happen: cap >= nearby x K + the largest grid)
+                } else {
+                    if (in) {
+                        const int pos = n + lanes_below(m, lane);
+                        L.d[pos] = d;
+                        L.id[pos] = st + k;
+                    }
+                    n += __popcll(m);
+                }
+            }
+            wave_sync();
+            if (ok && n - old > K) {
+                ok = wave_nth_big(L, old, old + K - 1, n, lane);
+                n = old + K;
             }
         }
+        if (ok && n == 0) continue;  // no candidate: the cache stays
+        if (ok && n > K) {  // ivox3d.h:173-177
+            ok = wave_nth_big(L, 0, K - 1, n, lane);
+            n = K;
+        }
+        if (ok) ok = wave_nth_big(L, 0, 0, n, lane);  // ivox3d.h:178
+        if (ok) {
+            // the record: lanes 0..4 the points, lane 0 the indices (as wave_write)
+            NNRec* out = job.nn + i;
+            const uint32_t myid = lane < n ? L.id[lane] : 0u;
+            const float myd = lane < n ? L.d[lane] : INFINITY;
+            int32_t pidx = -1;
+            if (lane < kNN) {
+                float4 v = make_float4(0.f, 0.f, 0.f, INFINITY);
+                if (lane < n) {
+                    const float4 pp = pts[myid];
+                    v = make_float4(pp.x, pp.y, pp.z, myd);
+                    pidx = __float_as_int(pp.w);
+                }
+                reinterpret_cast<float4*>(out)[lane] = v;
+            }
+            const int32_t node = lane < n ? (int32_t)myid : -1;
+            int32_t ix[kNN], nd[kNN];
+#pragma unroll
+            for (int q = 0; q < kNN; q++) {
+                ix[q] = __shfl(pidx, q, 64);
+                nd[q] = __shfl(node, q, 64);
+            }
+            if (lane == 0) {
+                int4* oi = reinterpret_cast<int4*>(out) + 5;
+                oi[0] = make_int4(ix[0], ix[1], ix[2], ix[3]);
+                oi[1] = make_int4(ix[4], n, 0, nd[0]);
+                oi[2] = make_int4(nd[1], nd[2], nd[3], nd[4]);
+            }
+        } else if (lane == 0) {  // the depth limit ran out: the exact per-thread search in global memory
+            SelElem* a = V.scratch + (int64_t)blockIdx.x * V.slice;
+            bool overflow;
+            const int nn = iv_query(V, qx, qy, qz, a, cap, overflow);
+            if (overflow) atomicOr(V.ctr, 2ull);
+            else if (nn > 0) iv_write(job.nn + i, pts, a, nn);
+        }
+        wave_sync();  // (the list is reused by the next query)
     }
 }
 
@@ -749,9 +836,12 @@ int launch_ivox_knn(const KnnParams& p, int n_jobs, int64_t max_n, bool later, i
     if (hipGetLastError() != hipSuccess) return LIVO_E_HIP;
     if (kind == 2)  // the team search's overflow, one query per wave (grid-stride; blocks past the list exit)
         hipLaunchKernelGGL(k_ivox_knn_wave_list, dim3(LIVO_IV_WLIST_BLOCKS), dim3(64 * kWaves), 0, (hipStream_t)stream, q);
-    const size_t lds = (size_t)q.iv.slice * sizeof(SelElem);
+    const size_t lds = (size_t)q.iv.slice * kBigEntryBytes;
+    // (the global slices of the depth-limit fallback: one per block, within the
+    // group's big_threads slices)
+    const unsigned wblocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, overflow_threads));
     if (lds <= 65536) {
-        hipLaunchKernelGGL(k_ivox_knn_big_lds, dim3(2048), dim3(64), lds, (hipStream_t)stream, q);
+        hipLaunchKernelGGL(k_ivox_knn_big_wave, dim3(wblocks), dim3(64), lds, (hipStream_t)stream, q);
     } else {
         const unsigned blocks = (unsigned)std::max<int64_t>(1, overflow_threads / 64);
         hipLaunchKernelGGL(k_ivox_knn_big, dim3(blocks), dim3(64), 0, (hipStream_t)stream, q);

@@ -162,4 +162,108 @@ __device__ __forceinline__ bool wave_nth(WaveLds& L, int first, int nth, int las
     return true;
 }
 
+// The same std::nth_element on a list of any length (< 65536) in LDS given as
+// separate arrays: the rounds of 64 positions are loops instead of register
+// arrays, and the swap pairs (Lo[k], Ro[k]), k < k*, are exchanged pair by pair
+// (the pairs are disjoint: Lo ascends, Ro descends and Lo[k] < Ro[k], so no
+// position is in two of them).  For the iVox queries whose grids are too large
+// for WaveLds (k_ivox_knn_big_wave).
+struct BigList {
+    float* d;
+    uint32_t* id;
+    uint16_t* lt;
+    uint16_t* rt;
+};
+__device__ __forceinline__ bool wave_nth_big(const BigList& L, int first, int nth, int last, int lane) {
+    if (first == last || nth == last) return true;
+    int depth = 2 * sel_lg(last - first);
+    while (last - first > 3) {
+        if (depth == 0) return false;
+        --depth;
+        const int mid = first + (last - first) / 2;
+        if (lane == 0) {  // __move_median_to_first(first, first + 1, mid, last - 1)
+            const float a = L.d[first + 1], b = L.d[mid], c = L.d[last - 1];
+            int pick;
+            if (a < b)
+                pick = (b < c) ? mid : ((a < c) ? last - 1 : first + 1);
+            else
+                pick = (a < c) ? first + 1 : ((b < c) ? last - 1 : mid);
+            const float td = L.d[first];
+            const uint32_t ti = L.id[first];
+            L.d[first] = L.d[pick];
+            L.id[first] = L.id[pick];
+            L.d[pick] = td;
+            L.id[pick] = ti;
+        }
+        wave_sync();
+        const float pv = L.d[first];
+        const int lo = first + 1;
+        const int nr = (last - lo + 63) >> 6;
+        int nL = 0, nR = 0;
+        for (int r = 0; r < nr; r++) {  // the Lo / Ro totals
+            const int p = lo + 64 * r + lane;
+            const bool valid = p < last;
+            const float v = valid ? L.d[p] : 0.f;
+            nL += __popcll(__ballot(valid && !(v < pv)));
+            nR += __popcll(__ballot(valid && !(pv < v)));
+        }
+        int kstar = 0, lb = 0, rb = 0;
+        for (int r = 0; r < nr; r++) {  // ranks in Lo / Ro, k* and the two tables
+            const int p = lo + 64 * r + lane;
+            const bool valid = p < last;
+            const float v = valid ? L.d[p] : 0.f;
+            const bool lf = valid && !(v < pv), rf = valid && !(pv < v);
+            const unsigned long long lm = __ballot(lf), rm = __ballot(rf);
+            const int lrank = lb + lanes_below(lm, lane);
+            const int rle = rb + lanes_below(rm, lane) + (rf ? 1 : 0);
+            const int rrank = nR - rle;
+            kstar += __popcll(__ballot(lf && rrank >= lrank + 1));
+            if (lf) L.lt[lrank] = (uint16_t)p;
+            if (rf) L.rt[rrank] = (uint16_t)p;
+            lb += __popcll(lm);
+            rb += __popcll(rm);
+        }
+        wave_sync();
+        const int cut = (kstar < nL) ? (kstar > 0 ? min((int)L.lt[kstar], (int)L.rt[kstar - 1]) : (int)L.lt[0])
+                                     : (int)L.rt[kstar - 1];
+        for (int k = lane; k < kstar; k += 64) {
+            const int a = L.lt[k], b = L.rt[k];
+            const float da = L.d[a], db = L.d[b];
+            const uint32_t ia = L.id[a], ib = L.id[b];
+            L.d[a] = db;
+            L.id[a] = ib;
+            L.d[b] = da;
+            L.id[b] = ia;
+        }
+        wave_sync();
+        if (cut <= nth)
+            first = cut;
+        else
+            last = cut;
+    }
+    if (lane == 0) {  // __insertion_sort(first, last), <= 3 elements
+        for (int i = first + 1; i < last; ++i) {
+            const float vd = L.d[i];
+            const uint32_t vi = L.id[i];
+            int hole = i;
+            if (vd < L.d[first]) {
+                for (; hole > first; --hole) {
+                    L.d[hole] = L.d[hole - 1];
+                    L.id[hole] = L.id[hole - 1];
+                }
+            } else {
+                while (vd < L.d[hole - 1]) {
+                    L.d[hole] = L.d[hole - 1];
+                    L.id[hole] = L.id[hole - 1];
+                    --hole;
+                }
+            }
+            L.d[hole] = vd;
+            L.id[hole] = vi;
+        }
+    }
+    wave_sync();
+    return true;
+}
+
 }  // namespace livo

@@ -36,6 +36,30 @@ __global__ void k_check(const Case* cases, const float* d_in, float* d_out, uint
     if (lane == 0) status[c] = ok ? 1 : 0;
 }
 
+// wave_nth_big (lists past WaveLds, k_ivox_knn_big_wave): one wave per case,
+// the list and its tables in dynamic LDS of kBigCap entries.
+constexpr int kBigCap = 4096;
+__global__ void k_check_big(const Case* cases, const float* d_in, float* d_out, uint32_t* id_out, int* status,
+                            int ncase) {
+    extern __shared__ uint32_t lds[];
+    const BigList L{reinterpret_cast<float*>(lds), lds + kBigCap, reinterpret_cast<uint16_t*>(lds + 2 * kBigCap),
+                    reinterpret_cast<uint16_t*>(lds + 2 * kBigCap) + kBigCap};
+    const int c = blockIdx.x, lane = threadIdx.x;
+    if (c >= ncase) return;
+    const Case k = cases[c];
+    for (int p = lane; p < k.n; p += 64) {
+        L.d[p] = d_in[(size_t)c * kBigCap + p];
+        L.id[p] = (uint32_t)p;
+    }
+    wave_sync();
+    const bool ok = wave_nth_big(L, k.first, k.nth, k.n, lane);
+    for (int p = lane; p < k.n; p += 64) {
+        d_out[(size_t)c * kBigCap + p] = L.d[p];
+        id_out[(size_t)c * kBigCap + p] = L.id[p];
+    }
+    if (lane == 0) status[c] = ok ? 1 : 0;
+}
+
 struct DP {
     float d;
     uint32_t id;
@@ -97,6 +121,60 @@ int main(int argc, char** argv) {
                 break;
             }
     }
-    std::printf("%d cases, %ld mismatches, %ld depth-limit fallbacks\n", ncase, bad, fallback);
-    return bad == 0 ? 0 : 1;
+    // wave_nth_big: cases of 1..kBigCap elements (ties, narrow and wide value ranges)
+    const int nbig = std::max(200, ncase / 10);
+    std::vector<Case> bcases(nbig);
+    std::vector<float> bin((size_t)nbig * kBigCap, 0.f);
+    for (int c = 0; c < nbig; c++) {
+        const int n = 1 + (int)(rng() % (c % 3 == 0 ? (unsigned)kBigCap : 2000u));
+        const int levels = 1 + (int)(rng() % 200u);
+        for (int p = 0; p < n; p++)
+            bin[(size_t)c * kBigCap + p] = (c % 2) ? (float)(rng() % (unsigned)levels) * 0.25f
+                                                   : std::ldexp((float)(rng() & 0xFFFFF), -20);
+        const int first = (c % 4 == 0 && n > 1) ? (int)(rng() % (unsigned)n) : 0;
+        const int nth = first + (int)(rng() % (unsigned)(n - first));
+        bcases[c] = Case{n, first, nth};
+    }
+    Case* bc;
+    float *bi, *bd;
+    uint32_t* bids;
+    int* bst;
+    hipMalloc(&bc, sizeof(Case) * nbig);
+    hipMalloc(&bi, bin.size() * 4);
+    hipMalloc(&bd, bin.size() * 4);
+    hipMalloc(&bids, bin.size() * 4);
+    hipMalloc(&bst, 4 * nbig);
+    hipMemcpy(bc, bcases.data(), sizeof(Case) * nbig, hipMemcpyHostToDevice);
+    hipMemcpy(bi, bin.data(), bin.size() * 4, hipMemcpyHostToDevice);
+    hipLaunchKernelGGL(k_check_big, dim3(nbig), dim3(64), kBigCap * 12, 0, bc, bi, bd, bids, bst, nbig);
+    if (hipDeviceSynchronize() != hipSuccess) {
+        std::printf("big kernel failed\n");
+        return 2;
+    }
+    std::vector<uint32_t> bout(bin.size());
+    std::vector<int> bs(nbig);
+    hipMemcpy(bout.data(), bids, bin.size() * 4, hipMemcpyDeviceToHost);
+    hipMemcpy(bs.data(), bst, 4 * nbig, hipMemcpyDeviceToHost);
+    long bbad = 0, bfall = 0;
+    for (int c = 0; c < nbig; c++) {
+        const Case k = bcases[c];
+        std::vector<DP> ref(k.n);
+        for (int p = 0; p < k.n; p++) ref[p] = DP{bin[(size_t)c * kBigCap + p], (uint32_t)p};
+        std::nth_element(ref.begin() + k.first, ref.begin() + k.nth, ref.begin() + k.n);
+        if (!bs[c]) {
+            bfall++;
+            continue;
+        }
+        for (int p = 0; p < k.n; p++)
+            if (bout[(size_t)c * kBigCap + p] != ref[p].id) {
+                if (bbad < 3) std::printf("big case %d n %d first %d nth %d: pos %d got %u want %u\n", c, k.n,
+                                          k.first, k.nth, p, bout[(size_t)c * kBigCap + p], ref[p].id);
+                bbad++;
+                break;
+            }
+    }
+    std::printf("wave_nth_big: %d cases of up to %d, %ld mismatched, %ld depth-limit fallbacks\n", nbig, kBigCap,
+                bbad, bfall);
+    std::printf("%d cases, %ld mismatches, %ld depth-limit fallbacks\n", ncase + nbig, bad + bbad, fallback + bfall);
+    return (bad + bbad) == 0 ? 0 : 1;
 }
