@@ -358,13 +358,9 @@ __global__ __launch_bounds__(64) void k_ivox_knn_big(KnnParams P) {
 // points loaded at once (<= kWRaw per query, 8 per lane), the in-range ones
 // staged in LDS in the reference's push order (grid by grid, insertion order),
 // and every std::nth_element of GetClosestPoint is run by the whole wave:
-// libstdc++'s unguarded Hoare partition computed in parallel.  With pv the
-// pivot value and, over the original values of [lo, last), Lo = the positions
-// with !(a < pv) ascending and Ro = those with !(pv < a) descending, the
-// sequential partition swaps Lo[k] <-> Ro[k] for every k < k* (the pairs with
-// Lo[k] < Ro[k]) and returns cut = min(Lo[k*], Ro[k*-1]).  Ranks come from
-// ballots, partners from two LDS tables.  The median-of-3 step and the final
-// insertion sort of <= 3 elements are done by lane 0 as written.  A query with
+// libstdc++'s unguarded Hoare partition computed in parallel (grp_nth,
+// wave_select.h: the swap pairs Lo[k] <-> Ro[k], k < k*, from two LDS tables of
+// ballot ranks; the final insertion sort of <= 3 elements on lane 0).  A query with
 // more than kWRaw raw points streams grid by grid instead (each grid truncated
 // right away, as the reference does); one whose grids are too large even for
 // that, or whose introselect exhausts its depth limit (libstdc++ then switches
@@ -669,11 +665,40 @@ constexpr int kIvTeamCap = LIVO_IV_TEAM_CAP;
 __device__ __forceinline__ uint32_t team_bits(unsigned long long m, int lane) {
     return (uint32_t)(m >> (lane & 48)) & 0xFFFFu;
 }
+// LIVO_IV_TEAM_NTH=1: the selections by the whole team (team_nth, wave_select.h);
+// 0: by the team's lane 0 (sel_nth_element), as round 6 first did.
+#ifndef LIVO_IV_TEAM_NTH
+#define LIVO_IV_TEAM_NTH 1
+#endif
+// segments shorter than this stay on lane 0 (sel_nth_element)
+#ifndef LIVO_IV_TEAM_NTH_MIN
+#define LIVO_IV_TEAM_NTH_MIN 0
+#endif
+static_assert(kIvTeam == kTeamLanes && kIvTeamCap <= 256, "team_nth runs on the search team, byte tables");
 template <bool LATER>
 __global__ __launch_bounds__(256) void k_ivox_knn_team(KnnParams P) {
     __shared__ SelElem lst[256 / kIvTeam][kIvTeamCap];
+#if LIVO_IV_TEAM_NTH
+    __shared__ uint8_t tabs[256 / kIvTeam][2][kIvTeamCap];
+#endif
     const int lane = threadIdx.x & 63, tl = threadIdx.x & (kIvTeam - 1), team = threadIdx.x / kIvTeam;
     SelElem* L = lst[team];
+#if LIVO_IV_TEAM_NTH
+    uint8_t* const lt = tabs[team][0];
+    uint8_t* const rt = tabs[team][1];
+#define IV_TEAM_NTH(f, k, l)                                      \
+    do {                                                          \
+        if ((l) - (f) >= LIVO_IV_TEAM_NTH_MIN)                    \
+            team_nth(L, lt, rt, f, k, l, tl, lane);               \
+        else if (tl == 0)                                         \
+            sel_nth_element(L, f, k, l);                          \
+    } while (0)
+#else
+#define IV_TEAM_NTH(f, k, l) \
+    do {                     \
+        if (tl == 0) sel_nth_element(L, f, k, l); \
+    } while (0)
+#endif
     unsigned bjob, bx;
     xcd_block(P.nb, bjob, bx);
     const HsJob job = P.jobs[bjob];
@@ -737,8 +762,8 @@ __global__ __launch_bounds__(256) void k_ivox_knn_team(KnnParams P) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         // KNNPointByCondition (ivox3d_node.hpp:179-183) on the grid's segment
-        if (n - old > K) {
-            if (tl == 0) sel_nth_element(L, old, old + K - 1, n);
+        if (n - old > K) {  // (team-uniform)
+            IV_TEAM_NTH(old, old + K - 1, n);
             n = old + K;
         }
     }
@@ -750,13 +775,10 @@ __global__ __launch_bounds__(256) void k_ivox_knn_team(KnnParams P) {
         return;
     }
     if (n == 0) return;  // no candidate: the reference returns false, the cache stays
-    if (tl == 0) {
-        if (n > K) {  // ivox3d.h:173-177
-            sel_nth_element(L, 0, K - 1, n);
-        }
-        sel_nth_element(L, 0, 0, n > K ? K : n);  // ivox3d.h:178
-    }
+    if (n > K) IV_TEAM_NTH(0, K - 1, n);  // ivox3d.h:173-177
     n = n > K ? K : n;
+    IV_TEAM_NTH(0, 0, n);  // ivox3d.h:178
+#undef IV_TEAM_NTH
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     // the record: lanes 0..4 of the team the points, lane 0 the indices

@@ -1,7 +1,7 @@
-// wave_select.h — std::nth_element run by a whole wavefront on an LDS list
-// (k_ivox_knn_wave, ivox_kernels.hip; checked element for element against
-// libstdc++ by tests/native/wave_nth_check.hip).  See ivox_kernels.hip for
-// the parallel formulation of libstdc++'s unguarded Hoare partition.
+// wave_select.h — std::nth_element run by a group of lanes (a 16-lane team or
+// a whole wavefront) on an LDS list (the iVox searches, ivox_kernels.hip;
+// checked element for element against libstdc++ by
+// tests/native/wave_nth_check.hip).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -26,6 +26,30 @@ struct WaveLds {
     uint32_t m[kIvMaxNearby + 1];  // in-range points per grid
 };
 
+// ---------------------------------------------------------------------------
+// std::nth_element(a + first, a + nth, a + last) run by a group of G lanes (a
+// 16-lane team or the whole wave) on a list in LDS, libstdc++'s introselect
+// round for round (stl_select.h restates it serially):
+//
+//   __move_median_to_first(first, first + 1, mid, last - 1), then
+//   __unguarded_partition(first + 1, last, pivot = *first).
+//
+// The serial partition swaps the k-th element from the left that is >= pivot
+// (Lo[k], by ascending position) with the k-th from the right that is <= pivot
+// (Ro[k], by descending position) for as long as Lo[k] < Ro[k], and returns the
+// position where the two scans cross.  Lo ascends and Ro descends, so the swaps
+// are the pairs k < k* with k* the count of k with Lo[k] < Ro[k], the pairs are
+// disjoint (no position is in two), and the cut is Lo[k*] when k* < |Lo| (or
+// Ro[k* - 1] before it), else Ro[k* - 1].  One pass over the round's positions
+// ranks both sets into LDS tables (lt: Lo ascending; rt: Ro by ascending
+// position, so Ro[k] = rt[nR - 1 - k]); the pairs are then swapped in parallel.
+// The median swap is folded in: the pass reads the element at `pick` as the one
+// from `first`, and lane 0 writes the swap after the pass's reads.  Returns
+// false when introselect's depth limit runs out (libstdc++ then heap-selects
+// [first, last) as left in first / last; the callers take that path).
+// Always inlined: an outlined call would reach LDS through flat pointers, whose
+// accesses are not ordered with the caller's ds_* ones.
+
 // Lanes exchange data through LDS: every access before this point has
 // completed before any after it is issued (workgroup-scope fences make the
 // compiler wait on the LDS counter; wavefront-scope ones are no-ops).
@@ -37,137 +61,124 @@ __device__ __forceinline__ void wave_sync() {
 __device__ __forceinline__ int lanes_below(unsigned long long mask, int lane) {
     return __popcll(mask & ((1ull << lane) - 1ull));
 }
-__device__ __forceinline__ void lds_swap(WaveLds& L, int i, int j) {
-    const float td = L.d[i];
-    const uint32_t ti = L.id[i];
-    L.d[i] = L.d[j];
-    L.id[i] = L.id[j];
-    L.d[j] = td;
-    L.id[j] = ti;
+
+// list accessors: SoA (separate key / id arrays) and AoS (SelElem)
+struct SoaList {
+    float* d;
+    uint32_t* id;
+    __device__ __forceinline__ float key(int p) const { return d[p]; }
+    __device__ __forceinline__ SelElem get(int p) const { return SelElem{d[p], id[p]}; }
+    __device__ __forceinline__ void put(int p, const SelElem& e) const {
+        d[p] = e.d;
+        id[p] = e.id;
+    }
+};
+struct AosList {
+    SelElem* a;
+    __device__ __forceinline__ float key(int p) const { return a[p].d; }
+    __device__ __forceinline__ SelElem get(int p) const { return a[p]; }
+    __device__ __forceinline__ void put(int p, const SelElem& e) const { a[p] = e; }
+};
+
+template <int G>
+__device__ __forceinline__ unsigned long long grp_mask(unsigned long long m, int lane) {
+    if constexpr (G == 64)
+        return m;
+    else
+        return (m >> (lane & (64 - G))) & ((1ull << G) - 1ull);
 }
 
-// std::nth_element(a + first, a + nth, a + last) on the wave's LDS list; false:
-// the depth limit ran out (heap select needed: the caller falls back).
-// Always inlined: an outlined call would reach the LDS list through flat
-// pointers, whose accesses are not ordered with the caller's ds_* ones.
-__device__ __forceinline__ bool wave_nth(WaveLds& L, int first, int nth, int last, int lane) {
+template <int G, class List, class Tab>
+__device__ __forceinline__ bool grp_nth(const List& L, Tab* lt, Tab* rt, int& first, int nth, int& last, int gl,
+                                        int lane) {
     if (first == last || nth == last) return true;
     int depth = 2 * sel_lg(last - first);
+    const unsigned long long below = (1ull << gl) - 1ull;
     while (last - first > 3) {
         if (depth == 0) return false;
         --depth;
         const int mid = first + (last - first) / 2;
-        if (lane == 0) {  // __move_median_to_first(first, first + 1, mid, last - 1)
-            const float a = L.d[first + 1], b = L.d[mid], c = L.d[last - 1];
-            int pick;
-            if (a < b)
-                pick = (b < c) ? mid : ((a < c) ? last - 1 : first + 1);
-            else
-                pick = (a < c) ? first + 1 : ((b < c) ? last - 1 : mid);
-            lds_swap(L, first, pick);
-        }
-        wave_sync();
-        const float pv = L.d[first];
-        const int lo = first + 1;
-        const int nr = (last - lo + 63) >> 6;  // rounds of 64 positions actually in range (uniform)
-        bool lf[kWRounds], rf[kWRounds];
-        unsigned long long lm[kWRounds], rm[kWRounds];
+        const SelElem e0 = L.get(first), ea = L.get(first + 1), eb = L.get(mid), ec = L.get(last - 1);
+        int pick;  // __move_median_to_first(first, first + 1, mid, last - 1)
+        SelElem pe;
+        if (ea.d < eb.d) {
+            if (eb.d < ec.d) { pick = mid; pe = eb; }
+            else if (ea.d < ec.d) { pick = last - 1; pe = ec; }
+            else { pick = first + 1; pe = ea; }
+        } else if (ea.d < ec.d) { pick = first + 1; pe = ea; }
+        else if (eb.d < ec.d) { pick = last - 1; pe = ec; }
+        else { pick = mid; pe = eb; }
+        const float pv = pe.d;
         int nL = 0, nR = 0;
-#pragma unroll
-        for (int r = 0; r < kWRounds; r++) {
-            lf[r] = rf[r] = false;
-            lm[r] = rm[r] = 0ull;
-            if (r < nr) {
-                const int p = lo + 64 * r + lane;
-                const bool valid = p < last;
-                const float v = valid ? L.d[p] : 0.f;
-                lf[r] = valid && !(v < pv);
-                rf[r] = valid && !(pv < v);
-                lm[r] = __ballot(lf[r]);
-                rm[r] = __ballot(rf[r]);
-                nL += __popcll(lm[r]);
-                nR += __popcll(rm[r]);
-            }
+#pragma unroll 1
+        for (int p0 = first + 1; p0 < last; p0 += G) {  // (group-uniform)
+            const int p = p0 + gl;
+            const bool valid = p < last;
+            const float lv = valid ? L.key(p) : 0.f;
+            const float v = p == pick ? e0.d : lv;
+            const bool lf = valid && !(v < pv), rf = valid && !(pv < v);
+            const unsigned long long lm = grp_mask<G>(__ballot(lf), lane), rm = grp_mask<G>(__ballot(rf), lane);
+            if (lf) lt[nL + __popcll(lm & below)] = (Tab)p;
+            if (rf) rt[nR + __popcll(rm & below)] = (Tab)p;
+            nL += __popcll(lm);
+            nR += __popcll(rm);
         }
-        int lrank[kWRounds], rrank[kWRounds];
-        bool ok[kWRounds];
-        int kstar = 0, lb = 0, rb = 0;
-#pragma unroll
-        for (int r = 0; r < kWRounds; r++) {
-            lrank[r] = lb + lanes_below(lm[r], lane);
-            const int rle = rb + lanes_below(rm[r], lane) + (rf[r] ? 1 : 0);  // rf positions <= p
-            rrank[r] = nR - rle;  // rf positions > p: the rank in Ro
-            ok[r] = lf[r] && (nR - rle) >= lrank[r] + 1;  // Lo[k] < Ro[k]
-            if (r < nr) kstar += __popcll(__ballot(ok[r]));
-            lb += __popcll(lm[r]);
-            rb += __popcll(rm[r]);
-        }
-#pragma unroll
-        for (int r = 0; r < kWRounds; r++) {
-            const int p = lo + 64 * r + lane;
-            if (lf[r]) L.lt[lrank[r]] = (uint16_t)p;
-            if (rf[r]) L.rt[rrank[r]] = (uint16_t)p;
+        if (gl == 0) {  // the median swap, after every read of the pass
+            L.put(first, pe);
+            L.put(pick, e0);
         }
         wave_sync();
-        float nd[kWRounds];
-        uint32_t nid[kWRounds];
-        bool sw[kWRounds];
-#pragma unroll
-        for (int r = 0; r < kWRounds; r++) {
-            sw[r] = (lf[r] && lrank[r] < kstar) || (rf[r] && rrank[r] < kstar);
-            int partner = 0;
-            if (lf[r] && lrank[r] < kstar) partner = L.rt[lrank[r]];
-            if (rf[r] && rrank[r] < kstar) partner = L.lt[rrank[r]];
-            nd[r] = sw[r] ? L.d[partner] : 0.f;
-            nid[r] = sw[r] ? L.id[partner] : 0u;
-        }
-        const int cut = (kstar < nL) ? (kstar > 0 ? min((int)L.lt[kstar], (int)L.rt[kstar - 1]) : (int)L.lt[0])
-                                     : (int)L.rt[kstar - 1];
-        wave_sync();
-#pragma unroll
-        for (int r = 0; r < kWRounds; r++)
-            if (sw[r]) {
-                const int p = lo + 64 * r + lane;
-                L.d[p] = nd[r];
-                L.id[p] = nid[r];
+        const int np = min(nL, nR);
+        int kstar = 0;
+#pragma unroll 1
+        for (int k0 = 0; k0 < np; k0 += G) {  // (group-uniform)
+            const int k = k0 + gl;
+            int a = 0, b = 0;
+            if (k < np) {
+                a = lt[k];
+                b = rt[nR - 1 - k];
             }
+            const bool sw = k < np && a < b;
+            kstar += __popcll(grp_mask<G>(__ballot(sw), lane));
+            if (sw) {
+                const SelElem xa = L.get(a), xb = L.get(b);
+                L.put(a, xb);
+                L.put(b, xa);
+            }
+        }
+        const int cut = (kstar < nL) ? (kstar > 0 ? min((int)lt[kstar], (int)rt[nR - kstar]) : (int)lt[0])
+                                     : (int)rt[nR - kstar];
         wave_sync();
         if (cut <= nth)
             first = cut;
         else
             last = cut;
     }
-    if (lane == 0) {  // __insertion_sort(first, last), <= 3 elements
+    if (gl == 0) {  // __insertion_sort(first, last), <= 3 elements
         for (int i = first + 1; i < last; ++i) {
-            const float vd = L.d[i];
-            const uint32_t vi = L.id[i];
+            const SelElem v = L.get(i);
             int hole = i;
-            if (vd < L.d[first]) {
-                for (; hole > first; --hole) {
-                    L.d[hole] = L.d[hole - 1];
-                    L.id[hole] = L.id[hole - 1];
-                }
+            if (v.d < L.key(first)) {
+                for (; hole > first; --hole) L.put(hole, L.get(hole - 1));
             } else {
-                while (vd < L.d[hole - 1]) {
-                    L.d[hole] = L.d[hole - 1];
-                    L.id[hole] = L.id[hole - 1];
+                while (v.d < L.key(hole - 1)) {
+                    L.put(hole, L.get(hole - 1));
                     --hole;
                 }
             }
-            L.d[hole] = vd;
-            L.id[hole] = vi;
+            L.put(hole, v);
         }
     }
     wave_sync();
     return true;
 }
 
-// The same std::nth_element on a list of any length (< 65536) in LDS given as
-// separate arrays: the rounds of 64 positions are loops instead of register
-// arrays, and the swap pairs (Lo[k], Ro[k]), k < k*, are exchanged pair by pair
-// (the pairs are disjoint: Lo ascends, Ro descends and Lo[k] < Ro[k], so no
-// position is in two of them).  For the iVox queries whose grids are too large
-// for WaveLds (k_ivox_knn_big_wave).
+// the wave's list of k_ivox_knn_wave / _wave_list (<= kWRaw entries)
+__device__ __forceinline__ bool wave_nth(WaveLds& L, int first, int nth, int last, int lane) {
+    return grp_nth<64>(SoaList{L.d, L.id}, L.lt, L.rt, first, nth, last, lane, lane);
+}
+
+// a list of any length (< 65536) in dynamic LDS (k_ivox_knn_big_wave)
 struct BigList {
     float* d;
     uint32_t* id;
@@ -175,95 +186,23 @@ struct BigList {
     uint16_t* rt;
 };
 __device__ __forceinline__ bool wave_nth_big(const BigList& L, int first, int nth, int last, int lane) {
-    if (first == last || nth == last) return true;
-    int depth = 2 * sel_lg(last - first);
-    while (last - first > 3) {
-        if (depth == 0) return false;
-        --depth;
-        const int mid = first + (last - first) / 2;
-        if (lane == 0) {  // __move_median_to_first(first, first + 1, mid, last - 1)
-            const float a = L.d[first + 1], b = L.d[mid], c = L.d[last - 1];
-            int pick;
-            if (a < b)
-                pick = (b < c) ? mid : ((a < c) ? last - 1 : first + 1);
-            else
-                pick = (a < c) ? first + 1 : ((b < c) ? last - 1 : mid);
-            const float td = L.d[first];
-            const uint32_t ti = L.id[first];
-            L.d[first] = L.d[pick];
-            L.id[first] = L.id[pick];
-            L.d[pick] = td;
-            L.id[pick] = ti;
+    return grp_nth<64>(SoaList{L.d, L.id}, L.lt, L.rt, first, nth, last, lane, lane);
+}
+
+// a 16-lane team's list of SelElems (k_ivox_knn_team: four queries a wave, <= 256
+// entries: byte tables); the teams of a wave run their rounds under their own
+// exec masks.  The depth limit's heap select runs on the team's lane 0, as the
+// serial restatement does (stl_select.h).
+constexpr int kTeamLanes = 16;
+__device__ __forceinline__ void team_nth(SelElem* L, uint8_t* lt, uint8_t* rt, int first, int nth, int last,
+                                         int tl, int lane) {
+    if (!grp_nth<kTeamLanes>(AosList{L}, lt, rt, first, nth, last, tl, lane)) {
+        if (tl == 0) {  // std::__heap_select + iter_swap (stl_algo.h __introselect)
+            sel_heap_select(L, first, nth + 1, last);
+            sel_swap(L, first, nth);
         }
         wave_sync();
-        const float pv = L.d[first];
-        const int lo = first + 1;
-        const int nr = (last - lo + 63) >> 6;
-        int nL = 0, nR = 0;
-        for (int r = 0; r < nr; r++) {  // the Lo / Ro totals
-            const int p = lo + 64 * r + lane;
-            const bool valid = p < last;
-            const float v = valid ? L.d[p] : 0.f;
-            nL += __popcll(__ballot(valid && !(v < pv)));
-            nR += __popcll(__ballot(valid && !(pv < v)));
-        }
-        int kstar = 0, lb = 0, rb = 0;
-        for (int r = 0; r < nr; r++) {  // ranks in Lo / Ro, k* and the two tables
-            const int p = lo + 64 * r + lane;
-            const bool valid = p < last;
-            const float v = valid ? L.d[p] : 0.f;
-            const bool lf = valid && !(v < pv), rf = valid && !(pv < v);
-            const unsigned long long lm = __ballot(lf), rm = __ballot(rf);
-            const int lrank = lb + lanes_below(lm, lane);
-            const int rle = rb + lanes_below(rm, lane) + (rf ? 1 : 0);
-            const int rrank = nR - rle;
-            kstar += __popcll(__ballot(lf && rrank >= lrank + 1));
-            if (lf) L.lt[lrank] = (uint16_t)p;
-            if (rf) L.rt[rrank] = (uint16_t)p;
-            lb += __popcll(lm);
-            rb += __popcll(rm);
-        }
-        wave_sync();
-        const int cut = (kstar < nL) ? (kstar > 0 ? min((int)L.lt[kstar], (int)L.rt[kstar - 1]) : (int)L.lt[0])
-                                     : (int)L.rt[kstar - 1];
-        for (int k = lane; k < kstar; k += 64) {
-            const int a = L.lt[k], b = L.rt[k];
-            const float da = L.d[a], db = L.d[b];
-            const uint32_t ia = L.id[a], ib = L.id[b];
-            L.d[a] = db;
-            L.id[a] = ib;
-            L.d[b] = da;
-            L.id[b] = ia;
-        }
-        wave_sync();
-        if (cut <= nth)
-            first = cut;
-        else
-            last = cut;
     }
-    if (lane == 0) {  // __insertion_sort(first, last), <= 3 elements
-        for (int i = first + 1; i < last; ++i) {
-            const float vd = L.d[i];
-            const uint32_t vi = L.id[i];
-            int hole = i;
-            if (vd < L.d[first]) {
-                for (; hole > first; --hole) {
-                    L.d[hole] = L.d[hole - 1];
-                    L.id[hole] = L.id[hole - 1];
-                }
-            } else {
-                while (vd < L.d[hole - 1]) {
-                    L.d[hole] = L.d[hole - 1];
-                    L.id[hole] = L.id[hole - 1];
-                    --hole;
-                }
-            }
-            L.d[hole] = vd;
-            L.id[hole] = vi;
-        }
-    }
-    wave_sync();
-    return true;
 }
 
 }  // namespace livo

@@ -60,6 +60,22 @@ __global__ void k_check_big(const Case* cases, const float* d_in, float* d_out, 
     if (lane == 0) status[c] = ok ? 1 : 0;
 }
 
+// team_nth (k_ivox_knn_team): four teams a wave, one case each, lists of up to 128
+constexpr int kTeamCap = 128;  // (k_ivox_knn_team's list capacity)
+__global__ void k_check_team(const Case* cases, const float* d_in, uint32_t* id_out, int ncase) {
+    __shared__ SelElem lst[4][kTeamCap];
+    __shared__ uint8_t tabs[4][2][kTeamCap];
+    const int lane = threadIdx.x, tl = lane & 15, team = lane >> 4;
+    const int c = blockIdx.x * 4 + team;
+    if (c >= ncase) return;  // (team-uniform)
+    const Case k = cases[c];
+    SelElem* L = lst[team];
+    for (int p = tl; p < k.n; p += 16) L[p] = SelElem{d_in[(size_t)c * kTeamCap + p], (uint32_t)p};
+    wave_sync();
+    team_nth(L, tabs[team][0], tabs[team][1], k.first, k.nth, k.n, tl, lane);
+    for (int p = tl; p < k.n; p += 16) id_out[(size_t)c * kTeamCap + p] = L[p].id;
+}
+
 struct DP {
     float d;
     uint32_t id;
@@ -175,6 +191,54 @@ int main(int argc, char** argv) {
     }
     std::printf("wave_nth_big: %d cases of up to %d, %ld mismatched, %ld depth-limit fallbacks\n", nbig, kBigCap,
                 bbad, bfall);
-    std::printf("%d cases, %ld mismatches, %ld depth-limit fallbacks\n", ncase + nbig, bad + bbad, fallback + bfall);
+    // team_nth: 1..128 elements, mostly the 6..40 of an iVox grid's segment; ties
+    // (few levels, incl. all equal: the heap-select path) and wide ranges
+    const int nteam = std::max(4000, ncase);
+    std::vector<Case> tcases(nteam);
+    std::vector<float> tin((size_t)nteam * kTeamCap, 0.f);
+    for (int c = 0; c < nteam; c++) {
+        const int n = 1 + (int)(rng() % (c % 3 == 0 ? (unsigned)kTeamCap : 40u));
+        const int levels = 1 + (int)(rng() % (c % 7 == 0 ? 2u : 30u));
+        for (int p = 0; p < n; p++)
+            tin[(size_t)c * kTeamCap + p] = (c % 2) ? (float)(rng() % (unsigned)levels) * 0.25f
+                                                    : std::ldexp((float)(rng() & 0xFFFFF), -20);
+        const int first = (c % 4 == 0 && n > 1) ? (int)(rng() % (unsigned)n) : 0;
+        const int nth = (c % 5 == 0) ? first + std::min(4, n - 1 - first)
+                                     : first + (int)(rng() % (unsigned)(n - first));
+        tcases[c] = Case{n, first, nth};
+    }
+    Case* tc;
+    float* ti;
+    uint32_t* tids;
+    hipMalloc(&tc, sizeof(Case) * nteam);
+    hipMalloc(&ti, tin.size() * 4);
+    hipMalloc(&tids, tin.size() * 4);
+    hipMemcpy(tc, tcases.data(), sizeof(Case) * nteam, hipMemcpyHostToDevice);
+    hipMemcpy(ti, tin.data(), tin.size() * 4, hipMemcpyHostToDevice);
+    hipLaunchKernelGGL(k_check_team, dim3((nteam + 3) / 4), dim3(64), 0, 0, tc, ti, tids, nteam);
+    if (hipDeviceSynchronize() != hipSuccess) {
+        std::printf("team kernel failed\n");
+        return 2;
+    }
+    std::vector<uint32_t> tout(tin.size());
+    hipMemcpy(tout.data(), tids, tin.size() * 4, hipMemcpyDeviceToHost);
+    long tbad = 0;
+    for (int c = 0; c < nteam; c++) {
+        const Case k = tcases[c];
+        std::vector<DP> ref(k.n);
+        for (int p = 0; p < k.n; p++) ref[p] = DP{tin[(size_t)c * kTeamCap + p], (uint32_t)p};
+        std::nth_element(ref.begin() + k.first, ref.begin() + k.nth, ref.begin() + k.n);
+        for (int p = 0; p < k.n; p++)
+            if (tout[(size_t)c * kTeamCap + p] != ref[p].id) {
+                if (tbad < 3) std::printf("team case %d n %d first %d nth %d: pos %d got %u want %u\n", c, k.n,
+                                          k.first, k.nth, p, tout[(size_t)c * kTeamCap + p], ref[p].id);
+                tbad++;
+                break;
+            }
+    }
+    std::printf("team_nth: %d cases of up to %d, %ld mismatched\n", nteam, kTeamCap, tbad);
+    bad += tbad;
+    std::printf("%d cases, %ld mismatches, %ld depth-limit fallbacks\n", ncase + nbig + nteam, bad + bbad,
+                fallback + bfall);
     return (bad + bbad) == 0 ? 0 : 1;
 }
