@@ -898,7 +898,10 @@ __global__ void k_iv_insert(IvoxParams P) {
         if (cur == kGridEmpty) {
             cur = atomicCAS(&P.slots[sl].key, kGridEmpty, key);
             if (cur == kGridEmpty) {
-                atomicAdd(P.ctr + 1, 1ull);
+                // new grids counted: one atomic per wave's group of creators (the
+                // lanes that leave the probe loop here together)
+                const unsigned long long made = __ballot(true);
+                if ((threadIdx.x & 63) == __ffsll((long long)made) - 1) atomicAdd(P.ctr + 1, (unsigned long long)__popcll(made));
                 break;
             }
         }
@@ -930,15 +933,33 @@ __global__ void k_iv_prepare(IvoxParams P) {
     P.tot[s] = P.evict[s] ? 0u : (P.slots[s].key != kGridEmpty ? P.slots[s].count : 0u) + P.addcnt[s];
 }
 
-// Old runs moved to their new start (one thread per grid).
+// Old runs moved to their new start: the wave's 64 slots in turn, each run
+// copied by the whole wave (coalesced; a grid of 1,000+ points next to the
+// sensor no longer copies on one thread).
 __global__ void k_iv_move(IvoxParams P) {
     const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= P.table) return;
-    const GridSlot g = P.slots[s];
-    if (g.key == kGridEmpty || g.count == 0u || P.evict[s]) return;
-    const float4* __restrict__ src = reinterpret_cast<const float4*>(P.pts) + g.start;
-    float4* __restrict__ dst = reinterpret_cast<float4*>(P.npts) + P.newstart[s];
-    for (uint32_t k = 0; k < g.count; k++) dst[k] = src[k];
+    const int lane = threadIdx.x & 63;
+    uint32_t st = 0u, cnt = 0u, dst = 0u;
+    bool act = false;
+    if (s < P.table) {
+        const GridSlot g = P.slots[s];
+        act = g.key != kGridEmpty && g.count != 0u && !P.evict[s];
+        if (act) {
+            st = g.start;
+            cnt = g.count;
+            dst = P.newstart[s];
+        }
+    }
+    const float4* __restrict__ src = reinterpret_cast<const float4*>(P.pts);
+    float4* __restrict__ out = reinterpret_cast<float4*>(P.npts);
+    unsigned long long m = __ballot(act);
+    while (m) {  // (wave-uniform)
+        const int l = __ffsll((long long)m) - 1;
+        m &= m - 1ull;
+        const uint32_t s0 = (uint32_t)__shfl((int)st, l, 64), c0 = (uint32_t)__shfl((int)cnt, l, 64),
+                       d0 = (uint32_t)__shfl((int)dst, l, 64);
+        for (uint32_t k = (uint32_t)lane; k < c0; k += 64) out[(size_t)d0 + k] = src[(size_t)s0 + k];
+    }
 }
 
 // New points appended to their grid's run in input order: the batch sorted by
@@ -956,10 +977,14 @@ __global__ void k_iv_place(IvoxParams P) {
         make_float4(p.x, p.y, p.z, __uint_as_float(id));
 }
 
-__global__ void k_iv_fix(IvoxParams P) {
-    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// Slots take their new run; the largest grid by a grid-stride pass of at most
+// kFixBlocks blocks and one atomic per block (an atomic or an agent-scope load
+// of the one counter per wave serialised on its line: ~88 us per 1M-slot table).
+constexpr int kFixBlocks = 1024;
+__global__ __launch_bounds__(256) void k_iv_fix(IvoxParams P) {
+    __shared__ unsigned wmax[4];
     unsigned cnt = 0;
-    if (s < P.table) {
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < P.table; s += (int64_t)gridDim.x * blockDim.x) {
         GridSlot g = P.slots[s];
         if (P.evict[s]) {
             P.addcnt[s] = 0u;  // (k_iv_drop empties the slot)
@@ -968,15 +993,17 @@ __global__ void k_iv_fix(IvoxParams P) {
             g.count += P.addcnt[s];
             P.slots[s] = g;
             P.addcnt[s] = 0u;
-            cnt = g.count;
+            cnt = max(cnt, g.count);
         }
     }
-    // the largest grid: one atomic per wave
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) cnt = max(cnt, (unsigned)__shfl_xor((int)cnt, off, 64));
-    if ((threadIdx.x & 63) == 0 && cnt &&
-        (unsigned long long)cnt > __hip_atomic_load(P.ctr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-        atomicMax(P.ctr + 2, (unsigned long long)cnt);
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned b = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+        if (b) atomicMax(P.ctr + 2, (unsigned long long)b);
+    }
 }
 
 __global__ void k_iv_rehash(const GridSlot* __restrict__ old_slots, const unsigned long long* __restrict__ old_t,
@@ -1096,7 +1123,12 @@ int launch_ivox_rollback(const IvoxParams& p, void* stream) { LAUNCH_CHECKED(k_i
 int launch_ivox_prepare(const IvoxParams& p, void* stream) { LAUNCH_CHECKED(k_iv_prepare, p.table, p); }
 int launch_ivox_move(const IvoxParams& p, void* stream) { LAUNCH_CHECKED(k_iv_move, p.table, p); }
 int launch_ivox_place(const IvoxParams& p, void* stream) { LAUNCH_CHECKED(k_iv_place, p.n_src, p); }
-int launch_ivox_fix(const IvoxParams& p, void* stream) { LAUNCH_CHECKED(k_iv_fix, p.table, p); }
+int launch_ivox_fix(const IvoxParams& p, void* stream) {
+    if (p.table <= 0) return LIVO_OK;
+    const unsigned blocks = (unsigned)std::min<int64_t>(kFixBlocks, (p.table + 255) / 256);
+    hipLaunchKernelGGL(k_iv_fix, dim3(blocks), dim3(256), 0, (hipStream_t)stream, p);
+    return hipGetLastError() == hipSuccess ? LIVO_OK : LIVO_E_HIP;
+}
 int launch_ivox_rehash(const GridSlot* old_slots, const unsigned long long* old_t, int64_t old_table, GridSlot* slots,
                        unsigned long long* tlast, int log2, void* stream) {
     LAUNCH_CHECKED(k_iv_rehash, old_table, old_slots, old_t, old_table, slots, tlast, log2);
