@@ -856,6 +856,11 @@ int launch_ivox_knn(const KnnParams& p, int n_jobs, int64_t max_n, bool later, i
             hipLaunchKernelGGL((k_ivox_knn_wave<false>), grid, block, 0, (hipStream_t)stream, q);
     }
     if (hipGetLastError() != hipSuccess) return LIVO_E_HIP;
+    // A list holds at most (nearby - 1) x K survivors + one grid's points <= slice - 8
+    // (slice: nearby x K + the largest grid + 8, grown with the map, never shrunk):
+    // when that fits the team's capacity no team search overflows, and the team
+    // search resolves its own depth-limit cases, so the overflow passes have no work.
+    if (kind == 2 && q.iv.slice - 8 <= kIvTeamCap) return LIVO_OK;
     if (kind == 2)  // the team search's overflow, one query per wave (grid-stride; blocks past the list exit)
         hipLaunchKernelGGL(k_ivox_knn_wave_list, dim3(LIVO_IV_WLIST_BLOCKS), dim3(64 * kWaves), 0, (hipStream_t)stream, q);
     const size_t lds = (size_t)q.iv.slice * kBigEntryBytes;
